@@ -1,0 +1,242 @@
+"""``POST /v1/chat/completions`` -- OpenAI-compatible, sync and SSE stream,
+served by the in-process engine of the selected GPU.
+
+Contract kept from the reference (core/internal/api/handlers.go:2087-2587):
+  * 10 MB body cap, ``messages`` required (400 ``messages_required``);
+  * empty ``model`` -> smart selection from headers ``X-Task-Type`` /
+    ``X-Accuracy`` / ``X-Max-Cost`` (response header ``X-Selected-Model``);
+  * model ids containing ``/`` are cloud models: proxied to OpenRouter only
+    when ``LMX_ALLOW_CLOUD=1`` (the hot path never falls back to the cloud);
+  * stream frames: ``data: {chat.completion.chunk}\\n\\n`` ... a final chunk
+    with empty delta and ``finish_reason``, then ``data: [DONE]\\n\\n``;
+  * non-stream: ``chat.completion`` with ``usage``.
+Defect fixed: ``max_tokens``, ``top_p`` and ``stop`` are honoured (the
+reference parsed and dropped them, handlers.go:2333-2340); ``top_k``,
+``seed``, ``logprobs`` and ``stream_options.include_usage`` are supported.
+"""
+from __future__ import annotations
+
+import json
+import time
+import uuid
+
+from aiohttp import web
+
+from ..engine.engine import SamplingParams
+from ..models.tokenizer import IncrementalDetokenizer, apply_chat_template
+from .helpers import dumps, read_json, write_error, write_json
+
+CHAT_TIMEOUT_S = 120.0
+
+
+def sampling_from_body(body: dict, max_len_left: int) -> SamplingParams:
+    def f(name, default):
+        v = body.get(name)
+        return default if v is None else v
+
+    stop = body.get("stop")
+    if isinstance(stop, str):
+        stop = [stop]
+    elif not isinstance(stop, list):
+        stop = []
+    max_tokens = body.get("max_tokens", body.get("max_completion_tokens"))
+    if max_tokens is None:
+        max_tokens = min(max_len_left, 1024)
+    opts = body.get("options") or {}  # Ollama-style options also accepted
+    return SamplingParams(
+        temperature=float(f("temperature", opts.get("temperature", 0.8))),
+        top_p=float(f("top_p", opts.get("top_p", 1.0))),
+        top_k=int(f("top_k", opts.get("top_k", 0))),
+        max_tokens=max(1, min(int(max_tokens), max_len_left)),
+        stop=[str(s) for s in stop][:16],
+        ignore_eos=bool(body.get("ignore_eos", False)),
+        seed=body.get("seed", opts.get("seed")),
+        logprobs=bool(body.get("logprobs", False)))
+
+
+class ChatHandler:
+    def __init__(self, state):
+        self.state = state
+
+    async def __call__(self, request: web.Request) -> web.StreamResponse:
+        st = self.state
+        if request.method != "POST":
+            return write_error(405, "method_not_allowed", "Only POST allowed")
+        try:
+            body = await read_json(request)
+        except ValueError as e:
+            if str(e) == "body_too_large":
+                return write_error(413, "body_too_large", "Request body exceeds 10MB")
+            return write_error(400, "invalid_json", "Invalid JSON body")
+        if not isinstance(body, dict):
+            return write_error(400, "invalid_json", "Invalid JSON body")
+        messages = body.get("messages")
+        if not isinstance(messages, list) or not messages:
+            return write_error(400, "messages_required", "Field 'messages' is required")
+        model = body.get("model") or ""
+        extra_headers = {}
+        if not model:
+            selector = getattr(st, "select_model", None)
+            selected = None
+            if selector is not None:
+                selected = await selector(request, body)
+            if not selected:
+                return write_error(400, "no_model", "Could not select a model. Specify 'model' "
+                                   "explicitly or seed model_rankings.")
+            model = selected
+            extra_headers["X-Selected-Model"] = model
+        if "/" in model:
+            cloud = getattr(st, "cloud_chat", None)
+            if cloud is None:
+                return write_error(503, "cloud_disabled",
+                                   "Cloud models are disabled (set LMX_ALLOW_CLOUD=1 and "
+                                   "OPENROUTER_API_KEY)")
+            return await cloud(request, body, model, extra_headers)
+        target = st.registry.select(model, "chat", getattr(st, "circuit", None))
+        if target is None:
+            st.metrics.chat_requests(model, "none", "no_device")
+            return write_error(503, "no_device", f"No online device has model '{model}'")
+        tok = target.tokenizer
+        try:
+            prompt_ids = apply_chat_template(tok, messages)
+        except Exception as e:
+            return write_error(400, "invalid_messages", str(e))
+        left = target.max_model_len - len(prompt_ids) - 1
+        if left < 1:
+            return write_error(400, "context_length_exceeded",
+                               f"prompt has {len(prompt_ids)} tokens; model context is "
+                               f"{target.max_model_len}")
+        params = sampling_from_body(body, left)
+        stream = bool(body.get("stream", False))
+        include_usage = bool((body.get("stream_options") or {}).get("include_usage", False))
+        target.inflight += 1
+        t0 = time.time()
+        try:
+            if stream:
+                return await self._stream(request, target, model, prompt_ids, params,
+                                          include_usage, extra_headers, t0)
+            return await self._sync(target, model, prompt_ids, params, extra_headers, t0)
+        finally:
+            target.inflight -= 1
+
+    async def _sync(self, target, model, prompt_ids, params, headers, t0):
+        st = self.state
+        detok = IncrementalDetokenizer(target.tokenizer, params.stop)
+        text, n_out, finish, lps = [], 0, "stop", []
+        gen = target.engine.generate(prompt_ids, params)
+        ttft = None
+        try:
+            async for it in gen:
+                if it.token >= 0:
+                    if ttft is None:
+                        ttft = time.time() - t0
+                    n_out += 1
+                    text.append(detok.push(it.token))
+                    if params.logprobs:
+                        lps.append(it.logprob)
+                    if detok.stopped:
+                        finish = "stop"
+                        break
+                if it.finish is not None:
+                    finish = it.finish
+                    break
+        finally:
+            await gen.aclose()
+        text.append(detok.flush())
+        if finish.startswith("error"):
+            self._record(target, model, "error", t0, len(prompt_ids), n_out, ttft)
+            return write_error(502, "engine_failed", finish)
+        self._record(target, model, "ok", t0, len(prompt_ids), n_out, ttft)
+        choice = {"index": 0, "message": {"role": "assistant", "content": "".join(text)},
+                  "finish_reason": finish if finish in ("stop", "length") else "stop"}
+        if params.logprobs:
+            choice["logprobs"] = {"content": [{"logprob": lp} for lp in lps]}
+        resp = {
+            "id": "chatcmpl-" + uuid.uuid4().hex[:24], "object": "chat.completion",
+            "created": int(time.time()), "model": model, "choices": [choice],
+            "usage": {"prompt_tokens": len(prompt_ids), "completion_tokens": n_out,
+                      "total_tokens": len(prompt_ids) + n_out}}
+        r = write_json(200, resp)
+        r.headers.update(headers)
+        return r
+
+    async def _stream(self, request, target, model, prompt_ids, params, include_usage, headers,
+                      t0):
+        st = self.state
+        resp = web.StreamResponse(status=200, headers={
+            "Content-Type": "text/event-stream", "Cache-Control": "no-cache",
+            "Connection": "keep-alive", **headers})
+        await resp.prepare(request)
+        chat_id = "chatcmpl-" + str(time.time_ns())
+        created = int(time.time())
+        head = ('data: {"id":"%s","object":"chat.completion.chunk","created":%d,"model":%s,'
+                '"choices":[{"index":0,"delta":' % (chat_id, created, json.dumps(model)))
+        detok = IncrementalDetokenizer(target.tokenizer, params.stop)
+        n_out, finish, first = 0, "stop", True
+        ttft = None
+        gen = target.engine.generate(prompt_ids, params)
+        status = "ok"
+        try:
+            async for it in gen:
+                if it.token >= 0:
+                    n_out += 1
+                    piece = detok.push(it.token)
+                    if piece or first:
+                        if ttft is None:
+                            ttft = time.time() - t0
+                        role = '"role":"assistant",' if first else ""
+                        first = False
+                        lp = (',"logprobs":{"content":[{"logprob":%.6f}]}' % it.logprob
+                              if params.logprobs else "")
+                        await resp.write((head + '{%s"content":%s}%s}]}\n\n'
+                                          % (role, json.dumps(piece, ensure_ascii=False), lp)
+                                          ).encode())
+                    if detok.stopped:
+                        finish = "stop"
+                        break
+                if it.finish is not None:
+                    finish = it.finish
+                    break
+            tail = detok.flush()
+            if tail:
+                await resp.write((head + '{"content":%s}}]}\n\n'
+                                  % json.dumps(tail, ensure_ascii=False)).encode())
+            if finish.startswith("error"):
+                status = "error"
+                finish = "error"
+            final = {"id": chat_id, "object": "chat.completion.chunk", "created": created,
+                     "model": model, "choices": [{"index": 0, "delta": {},
+                                                  "finish_reason": finish}]}
+            await resp.write(b"data: " + dumps(final).encode() + b"\n\n")
+            if include_usage:
+                usage = {"id": chat_id, "object": "chat.completion.chunk", "created": created,
+                         "model": model, "choices": [],
+                         "usage": {"prompt_tokens": len(prompt_ids), "completion_tokens": n_out,
+                                   "total_tokens": len(prompt_ids) + n_out}}
+                await resp.write(b"data: " + dumps(usage).encode() + b"\n\n")
+            await resp.write(b"data: [DONE]\n\n")
+        except (ConnectionResetError, ConnectionError):
+            status = "client_gone"
+        finally:
+            await gen.aclose()
+            self._record(target, model, status, t0, len(prompt_ids), n_out, ttft)
+        return resp
+
+    def _record(self, target, model, status, t0, n_in, n_out, ttft):
+        st = self.state
+        elapsed = time.time() - t0
+        m = st.metrics
+        m.chat_requests(model, target.device_id, status)
+        if status in ("ok", "client_gone"):
+            m.chat_duration(model, target.device_id, elapsed)
+            m.chat_tokens(model, "local", n_in, n_out)
+            if ttft is not None:
+                m.ttft(model, ttft)
+                if n_out > 1:
+                    m.inter_token(model, (elapsed - ttft) / (n_out - 1))
+        circuit = getattr(st, "circuit", None)
+        if circuit is not None:
+            circuit.record(target.device_id, status != "error")
+        hook = getattr(st, "on_chat_done", None)
+        if hook is not None:
+            hook(model, n_in, n_out, int(elapsed * 1000), status)

@@ -1,0 +1,89 @@
+"""Local model registry: which model runs on which GPU (or TP group) of this
+node, and device selection among replicas.
+
+This is the in-process replacement of the reference's ``SelectOllamaDevice``
+(core/internal/routing/router.go:277-331), which picked the Ollama host with
+the best benchmark tps and ignored both the circuit breaker and concurrency.
+Here selection
+  * skips replicas whose device circuit is degraded (policy/circuit.py),
+  * skips replicas at capacity (continuous-batching slots / KV pages),
+  * prefers the least loaded replica, breaking ties by measured tokens/s.
+"""
+from __future__ import annotations
+
+import threading
+from dataclasses import dataclass, field
+
+from ..models import config as mc
+
+
+@dataclass
+class LocalModel:
+    model_id: str
+    kind: str                 # "chat" | "embed"
+    device_id: str
+    engine: object            # AsyncEngine (chat) or EmbeddingEngine (embed)
+    tokenizer: object
+    cfg: object
+    max_model_len: int = 8192
+    capacity: int = 256       # concurrent sequences admitted by the engine
+    tps: float = 0.0          # last measured decode tokens/s (benchmarks)
+    inflight: int = 0
+    tags: dict = field(default_factory=dict)
+
+    def load(self) -> float:
+        return self.inflight / max(1, self.capacity)
+
+    def info(self) -> dict:
+        eng = getattr(self.engine, "engine", self.engine)
+        sched = getattr(eng, "sched", None)
+        d = {"model": self.model_id, "kind": self.kind, "device_id": self.device_id,
+             "inflight": self.inflight, "capacity": self.capacity, "tps": self.tps,
+             "params_b": getattr(self.cfg, "params_b", None),
+             "context_k": getattr(self.cfg, "context_k", None)}
+        if sched is not None:
+            d.update(kv_usage=round(sched.kv_usage, 4), running=sched.num_running,
+                     waiting=sched.num_waiting)
+        return d
+
+
+class ModelRegistry:
+    def __init__(self):
+        self._lock = threading.Lock()
+        self._models: dict[str, list[LocalModel]] = {}
+
+    @staticmethod
+    def canonical(name: str) -> str:
+        return mc.ALIASES.get(name, name)
+
+    def add(self, m: LocalModel) -> None:
+        with self._lock:
+            self._models.setdefault(self.canonical(m.model_id), []).append(m)
+
+    def remove_device(self, device_id: str) -> None:
+        with self._lock:
+            for k in list(self._models):
+                self._models[k] = [m for m in self._models[k] if m.device_id != device_id]
+                if not self._models[k]:
+                    del self._models[k]
+
+    def replicas(self, model: str) -> list[LocalModel]:
+        return list(self._models.get(self.canonical(model), []))
+
+    def all(self) -> list[LocalModel]:
+        with self._lock:
+            return [m for v in self._models.values() for m in v]
+
+    def model_ids(self, kind: str | None = None) -> list[str]:
+        return sorted({k for k, v in self._models.items()
+                       if any(kind is None or m.kind == kind for m in v)})
+
+    def select(self, model: str, kind: str, circuit=None) -> LocalModel | None:
+        cands = [m for m in self.replicas(model) if m.kind == kind]
+        if circuit is not None:
+            healthy = [m for m in cands if not circuit.is_degraded(m.device_id)]
+            cands = healthy or []
+        if not cands:
+            return None
+        free = [m for m in cands if m.inflight < m.capacity] or cands
+        return min(free, key=lambda m: (m.load(), -m.tps))

@@ -1,0 +1,141 @@
+"""Load generator for /v1/chat/completions (SSE) and /v1/embeddings.
+
+Methodology follows the reference's probe harness
+(scripts/probe_openrouter_models.py:113-123, 373-383): per request, TTFT =
+request start -> first SSE chunk carrying content; completion tokens from the
+stream's ``usage`` (stream_options.include_usage); p50/p95 by linear
+interpolation.
+
+Runs standalone (``python -m llm_mcp_amd.bench.loadgen --url ...``) or as the
+client subprocess of bench.py: then it reads one command per line on stdin
+("run" / "quit") and answers one JSON line per wave on stdout.
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import random
+import string
+import sys
+import time
+
+import aiohttp
+
+
+def percentile(xs: list[float], q: float) -> float:
+    """Linear-interpolation percentile (same definition as the reference probe)."""
+    if not xs:
+        return 0.0
+    s = sorted(xs)
+    k = (len(s) - 1) * q / 100.0
+    f = int(k)
+    c = min(f + 1, len(s) - 1)
+    return s[f] + (s[c] - s[f]) * (k - f)
+
+
+def synthetic_prompt(n_chars: int, rng: random.Random) -> str:
+    alphabet = string.ascii_letters + string.digits + "     "
+    return "".join(rng.choice(alphabet) for _ in range(n_chars))
+
+
+async def one_chat(session, url, model, prompt, max_tokens, temperature, top_p, ignore_eos=True):
+    body = {"model": model, "messages": [{"role": "user", "content": prompt}], "stream": True,
+            "max_tokens": max_tokens, "temperature": temperature, "top_p": top_p,
+            "ignore_eos": ignore_eos, "stream_options": {"include_usage": True}}
+    t0 = time.perf_counter()
+    ttft, last, toks, chunks = None, None, 0, 0
+    async with session.post(url + "/v1/chat/completions", json=body) as r:
+        if r.status != 200:
+            raise RuntimeError(f"HTTP {r.status}: {await r.text()}")
+        async for line in r.content:
+            if not line.startswith(b"data: "):
+                continue
+            data = line[6:].strip()
+            if data == b"[DONE]":
+                break
+            obj = json.loads(data)
+            if obj.get("usage"):
+                toks = obj["usage"]["completion_tokens"]
+                continue
+            ch = obj.get("choices") or []
+            if ch and "content" in (ch[0].get("delta") or {}):
+                now = time.perf_counter()
+                if ttft is None:
+                    ttft = now - t0
+                last = now
+                chunks += 1
+    t1 = time.perf_counter()
+    return {"ttft": ttft or (t1 - t0), "latency": t1 - t0, "tokens": toks or chunks,
+            "decode_s": (last - t0 - ttft) if (last and ttft) else 0.0}
+
+
+async def wave(url, model, concurrency, prompt_len, max_tokens, temperature, top_p, seed):
+    rng = random.Random(seed)
+    prompts = [synthetic_prompt(prompt_len, rng) for _ in range(concurrency)]
+    conn = aiohttp.TCPConnector(limit=0)
+    timeout = aiohttp.ClientTimeout(total=3600)
+    async with aiohttp.ClientSession(connector=conn, timeout=timeout) as s:
+        t0 = time.perf_counter()
+        res = await asyncio.gather(*[one_chat(s, url, model, p, max_tokens, temperature, top_p)
+                                     for p in prompts])
+        el = time.perf_counter() - t0
+    ttfts = [r["ttft"] for r in res]
+    tok = sum(r["tokens"] for r in res)
+    itl = [r["decode_s"] / (r["tokens"] - 1) for r in res if r["tokens"] > 1]
+    return {"elapsed": el, "tokens": tok, "requests": len(res), "ttfts": ttfts,
+            "ttft_p50": percentile(ttfts, 50), "ttft_p95": percentile(ttfts, 95),
+            "itl_p50": percentile(itl, 50), "tok_s": tok / el if el > 0 else 0.0}
+
+
+async def wait_ready(url, timeout=1800):
+    t_end = time.time() + timeout
+    async with aiohttp.ClientSession() as s:
+        while time.time() < t_end:
+            try:
+                async with s.get(url + "/health") as r:
+                    if r.status == 200:
+                        return True
+            except Exception:
+                pass
+            await asyncio.sleep(0.5)
+    return False
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--url", default="http://127.0.0.1:8080")
+    ap.add_argument("--model", default="llama-3-8b")
+    ap.add_argument("--concurrency", type=int, default=64)
+    ap.add_argument("--prompt-len", type=int, default=512)
+    ap.add_argument("--max-tokens", type=int, default=256)
+    ap.add_argument("--temperature", type=float, default=0.8)
+    ap.add_argument("--top-p", type=float, default=0.95)
+    ap.add_argument("--waves", type=int, default=1)
+    ap.add_argument("--serve-stdin", action="store_true",
+                    help="wait for 'run' commands on stdin (bench.py client mode)")
+    a = ap.parse_args(argv)
+    loop = asyncio.new_event_loop()
+    if a.serve_stdin:
+        ok = loop.run_until_complete(wait_ready(a.url))
+        print(json.dumps({"ready": ok}), flush=True)
+        i = 0
+        for line in sys.stdin:
+            cmd = line.strip()
+            if cmd == "quit":
+                break
+            if cmd.startswith("run"):
+                r = loop.run_until_complete(wave(a.url, a.model, a.concurrency, a.prompt_len,
+                                                 a.max_tokens, a.temperature, a.top_p, i))
+                i += 1
+                print(json.dumps(r), flush=True)
+        return
+    for i in range(a.waves):
+        r = loop.run_until_complete(wave(a.url, a.model, a.concurrency, a.prompt_len,
+                                         a.max_tokens, a.temperature, a.top_p, i))
+        r.pop("ttfts")
+        print(json.dumps(r), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,141 @@
+"""In-tree build of the native parts of llm_mcp_amd.
+
+Two shared objects are produced next to this file (so they travel with the
+repository snapshot to the GPU box and are visibly loaded from the tree):
+
+* ``_lmx_kernels*.so``  -- the gfx950 HIP kernels (hipcc --offload-arch=gfx950)
+  with their pybind11 bindings.  Linked against the HIP runtime that PyTorch
+  already loaded (same soname, ``libamdhip64.so.7``) so kernels and torch share
+  one runtime, one device context and the same streams.
+* ``_lmx_runtime*.so``  -- the CPU-side native runtime (C++17): lease job
+  queue, paged-KV block manager and continuous-batching scheduler.
+
+Usage: ``python -m llm_mcp_amd.build`` (or ``build_all()``); sources are
+rebuilt only when newer than their output.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+import sysconfig
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+CSRC = PKG / "csrc"
+BUILD = PKG / "build"
+ARCH = os.environ.get("LMX_OFFLOAD_ARCH", "gfx950")
+EXT = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+
+KERNEL_SOURCES = ["norm.hip", "rope_cache.hip", "attention.hip", "sampling.hip",
+                  "elementwise.hip", "gemm.hip"]
+RUNTIME_SOURCES = ["job_queue.cpp", "block_manager.cpp", "scheduler.cpp", "bindings.cpp"]
+
+
+def _py_includes() -> list[str]:
+    import pybind11
+    inc = {sysconfig.get_paths()["include"], sysconfig.get_paths()["platinclude"],
+           pybind11.get_include()}
+    return [f"-I{p}" for p in sorted(inc)]
+
+
+def _torch_libdir() -> str | None:
+    try:
+        import importlib.util
+        spec = importlib.util.find_spec("torch")
+        if spec and spec.origin:
+            d = Path(spec.origin).parent / "lib"
+            if (d / "libamdhip64.so").exists():
+                return str(d)
+    except Exception:
+        pass
+    return None
+
+
+def _run(cmd: list[str]) -> None:
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"build failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+
+
+def _stale(out: Path, deps: list[Path]) -> bool:
+    if not out.exists():
+        return True
+    t = out.stat().st_mtime
+    return any(d.stat().st_mtime > t for d in deps if d.exists())
+
+
+def kernels_path() -> Path:
+    return PKG / f"_lmx_kernels{EXT}"
+
+
+def runtime_path() -> Path:
+    return PKG / f"_lmx_runtime{EXT}"
+
+
+def build_kernels(force: bool = False, verbose: bool = False) -> Path:
+    kdir = CSRC / "kernels"
+    out = kernels_path()
+    headers = list(kdir.glob("*.h"))
+    srcs = [kdir / s for s in KERNEL_SOURCES]
+    objdir = BUILD / "kernels"
+    objdir.mkdir(parents=True, exist_ok=True)
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    common = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
+              "-munsafe-fp-atomics", f"-I{kdir}"]
+    objs = []
+    jobs = []
+    for s in srcs:
+        o = objdir / (s.stem + ".o")
+        objs.append(o)
+        if force or _stale(o, [s] + headers):
+            jobs.append(common + ["-c", str(s), "-o", str(o)])
+    bo = objdir / "bindings.o"
+    objs.append(bo)
+    bsrc = kdir / "bindings.cpp"
+    if force or _stale(bo, [bsrc]):
+        jobs.append([hipcc, "-O2", "-std=c++17", "-fPIC", "-x", "hip", f"--offload-arch={ARCH}",
+                     *_py_includes(), "-c", str(bsrc), "-o", str(bo)])
+    if jobs:
+        with ThreadPoolExecutor(max_workers=min(8, len(jobs))) as ex:
+            list(ex.map(_run, jobs))
+    if force or jobs or _stale(out, objs):
+        link = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(out),
+                *[str(o) for o in objs]]
+        tl = _torch_libdir()
+        if tl:
+            # resolve libamdhip64.so.7 to the copy torch loads (one HIP runtime per process)
+            link += [f"-L{tl}", f"-Wl,-rpath,{tl}"]
+        link += ["-lamdhip64"]
+        _run(link)
+        if verbose:
+            print(f"[build] {out.name}")
+    return out
+
+
+def build_runtime(force: bool = False, verbose: bool = False) -> Path:
+    rdir = CSRC / "runtime"
+    out = runtime_path()
+    srcs = [rdir / s for s in RUNTIME_SOURCES]
+    headers = list(rdir.glob("*.h"))
+    if force or _stale(out, srcs + headers):
+        cxx = os.environ.get("CXX", "g++")
+        cmd = [cxx, "-O2", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden", "-pthread",
+               f"-I{rdir}", *_py_includes(), *[str(s) for s in srcs], "-o", str(out)]
+        _run(cmd)
+        if verbose:
+            print(f"[build] {out.name}")
+    return out
+
+
+def build_all(force: bool = False, verbose: bool = False) -> None:
+    with ThreadPoolExecutor(max_workers=2) as ex:
+        fk = ex.submit(build_kernels, force, verbose)
+        fr = ex.submit(build_runtime, force, verbose)
+        fk.result()
+        fr.result()
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv, verbose=True)

@@ -1,0 +1,126 @@
+// pybind11 entry points of the HIP kernel library (_lmx_kernels).
+//
+// The Python side (llm_mcp_amd/ops/kernels.py) validates shapes, dtypes,
+// contiguity and device placement of torch tensors on the host and passes raw
+// device pointers plus the current HIP stream; nothing here allocates or
+// synchronises, so every launch is hipGraph-capturable.
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+#include <stdexcept>
+#include <string>
+
+namespace lmx {
+int rmsnorm(void*, void*, const void*, const void*, int, int, long, long, float, hipStream_t);
+int layernorm(void*, const void*, const void*, const void*, const void*, int, int, float,
+              hipStream_t);
+int rope_cache(void*, long, const int*, const float*, int, int, int, int, const int*, void*, void*,
+               int, int, hipStream_t);
+int kv_write(const void*, const void*, long, const int*, int, int, int, void*, void*, int,
+             hipStream_t);
+int paged_decode(const void*, long, const void*, const void*, const int*, int, const int*, void*,
+                 long, float*, float*, int, int, int, int, int, float, int, int, hipStream_t);
+int paged_prefill(const void*, long, const void*, const void*, const int*, int, const int*,
+                  const int*, const int*, int, void*, long, int, int, int, int, float, int,
+                  hipStream_t);
+int sample(const void*, int, long, int, int, const float*, const int*, const float*,
+           const uint64_t*, const int*, int*, float*, int, hipStream_t);
+int glu(void*, const void*, long, int, int, hipStream_t);
+int embed_gather(void*, const void*, const int*, int, int, int, int, hipStream_t);
+int mean_pool_l2(float*, const void*, const int*, int, int, int, int, hipStream_t);
+int bias_act(void*, const void*, long, int, int, hipStream_t);
+int gemm_nt(void*, const void*, const void*, const void*, const void*, int, int, int, long, long,
+            long, int, hipStream_t);
+}  // namespace lmx
+
+namespace py = pybind11;
+typedef unsigned long long uptr;
+
+template <typename T>
+static T* P(uptr p) { return reinterpret_cast<T*>(p); }
+static hipStream_t S(uptr s) { return reinterpret_cast<hipStream_t>(s); }
+
+static void check(int rc, const char* what) {
+  if (rc != 0) {
+    const char* es = rc > 0 ? hipGetErrorString((hipError_t)rc) : "invalid arguments";
+    throw std::runtime_error(std::string("lmx kernel ") + what + " failed (" + std::to_string(rc) +
+                             "): " + es);
+  }
+}
+
+PYBIND11_MODULE(_lmx_kernels, m) {
+  m.doc() = "llm_mcp_amd gfx950 HIP kernels";
+  m.def("rmsnorm", [](uptr out, uptr residual, uptr x, uptr w, int rows, int cols, long in_stride,
+                      long out_stride, float eps, uptr stream) {
+    check(lmx::rmsnorm(P<void>(out), P<void>(residual), P<void>(x), P<void>(w), rows, cols,
+                       in_stride, out_stride, eps, S(stream)),
+          "rmsnorm");
+  });
+  m.def("layernorm", [](uptr out, uptr x, uptr residual, uptr w, uptr b, int rows, int cols,
+                        float eps, uptr stream) {
+    check(lmx::layernorm(P<void>(out), P<void>(x), P<void>(residual), P<void>(w), P<void>(b), rows,
+                         cols, eps, S(stream)),
+          "layernorm");
+  });
+  m.def("rope_cache", [](uptr qkv, long qkv_stride, uptr positions, uptr cos_sin, int T, int Hq,
+                         int Hkv, int D, uptr slots, uptr kc, uptr vc, int BS, int rot_k,
+                         uptr stream) {
+    check(lmx::rope_cache(P<void>(qkv), qkv_stride, P<int>(positions), P<float>(cos_sin), T, Hq, Hkv,
+                          D, P<int>(slots), P<void>(kc), P<void>(vc), BS, rot_k, S(stream)),
+          "rope_cache");
+  });
+  m.def("kv_write", [](uptr k, uptr v, long stride, uptr slots, int T, int Hkv, int D, uptr kc,
+                       uptr vc, int BS, uptr stream) {
+    check(lmx::kv_write(P<void>(k), P<void>(v), stride, P<int>(slots), T, Hkv, D, P<void>(kc),
+                        P<void>(vc), BS, S(stream)),
+          "kv_write");
+  });
+  m.def("paged_decode", [](uptr q, long q_stride, uptr kc, uptr vc, uptr bt, int bt_stride,
+                           uptr ctx, uptr out, long out_stride, uptr part_o, uptr part_ml, int B,
+                           int Hq, int Hkv, int D, int BS, float scale, int part_tokens,
+                           int max_parts, uptr stream) {
+    check(lmx::paged_decode(P<void>(q), q_stride, P<void>(kc), P<void>(vc), P<int>(bt), bt_stride,
+                            P<int>(ctx), P<void>(out), out_stride, P<float>(part_o),
+                            P<float>(part_ml), B, Hq, Hkv, D, BS, scale, part_tokens, max_parts,
+                            S(stream)),
+          "paged_decode");
+  });
+  m.def("paged_prefill", [](uptr q, long q_stride, uptr kc, uptr vc, uptr bt, int bt_stride,
+                            uptr cu_q, uptr ctx, uptr tiles, int num_tiles, uptr out,
+                            long out_stride, int Hq, int Hkv, int D, int BS, float scale,
+                            int causal, uptr stream) {
+    check(lmx::paged_prefill(P<void>(q), q_stride, P<void>(kc), P<void>(vc), P<int>(bt),
+                             bt_stride, P<int>(cu_q), P<int>(ctx), P<int>(tiles), num_tiles,
+                             P<void>(out), out_stride, Hq, Hkv, D, BS, scale, causal, S(stream)),
+          "paged_prefill");
+  });
+  m.def("sample", [](uptr logits, int is_bf16, long stride, int B, int V, uptr temp, uptr topk,
+                     uptr topp, uptr seeds, uptr offsets, uptr out_tok, uptr out_lp,
+                     int max_rounds, uptr stream) {
+    check(lmx::sample(P<void>(logits), is_bf16, stride, B, V, P<float>(temp), P<int>(topk),
+                      P<float>(topp), P<uint64_t>(seeds), P<int>(offsets), P<int>(out_tok),
+                      P<float>(out_lp), max_rounds, S(stream)),
+          "sample");
+  });
+  m.def("glu", [](uptr out, uptr x, long rows, int I, int act, uptr stream) {
+    check(lmx::glu(P<void>(out), P<void>(x), rows, I, act, S(stream)), "glu");
+  });
+  m.def("embed_gather", [](uptr out, uptr table, uptr ids, int T, int d, int vs, int vr,
+                           uptr stream) {
+    check(lmx::embed_gather(P<void>(out), P<void>(table), P<int>(ids), T, d, vs, vr, S(stream)),
+          "embed_gather");
+  });
+  m.def("mean_pool_l2", [](uptr out, uptr h, uptr cu, int nseq, int d, int dims, int norm,
+                           uptr stream) {
+    check(lmx::mean_pool_l2(P<float>(out), P<void>(h), P<int>(cu), nseq, d, dims, norm, S(stream)),
+          "mean_pool_l2");
+  });
+  m.def("bias_act", [](uptr x, uptr bias, long rows, int n, int act, uptr stream) {
+    check(lmx::bias_act(P<void>(x), P<void>(bias), rows, n, act, S(stream)), "bias_act");
+  });
+  m.def("gemm_nt", [](uptr C, uptr A, uptr W, uptr bias, uptr residual, int M, int N, int K,
+                      long lda, long ldw, long ldc, int act, uptr stream) {
+    check(lmx::gemm_nt(P<void>(C), P<void>(A), P<void>(W), P<void>(bias), P<void>(residual), M, N,
+                       K, lda, ldw, ldc, act, S(stream)),
+          "gemm_nt");
+  });
+}

@@ -1,0 +1,165 @@
+// K8 / K9 / K10: fused element-wise and pooling ops.
+//   silu_mul      SwiGLU activation: out[t, i] = silu(x[t, i]) * x[t, I + i]
+//                 (x = fused gate|up projection output)
+//   gelu_mul      GeGLU variant, same layout
+//   embed_gather  token-embedding row gather, vocab-parallel aware: rows
+//                 outside [vocab_start, vocab_start + vocab_rows) are zeroed
+//                 (the TP all-reduce then sums the shards)
+//   mean_pool_l2  masked mean over each sequence's token rows (varlen,
+//                 cu_seqlens), optional Matryoshka truncation to `dims`, L2
+//                 normalisation, fp32 output -- the nomic-embed-text head.
+// All bf16 traffic is 16 B per lane.
+#include "common.h"
+
+namespace lmx {
+
+__device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float k0 = 0.7978845608f, k1 = 0.044715f;
+  return 0.5f * x * (1.f + tanhf(k0 * (x + k1 * x * x * x)));
+}
+
+template <int ACT>
+__global__ void __launch_bounds__(256) glu_kernel(bf16_t* __restrict__ out,
+                                                  const bf16_t* __restrict__ x, int I, long rows) {
+  const long nchunk = (long)rows * (I / 8);
+  const int cpr = I / 8;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < nchunk;
+       e += (long)gridDim.x * blockDim.x) {
+    const long r = e / cpr;
+    const int c = (int)(e % cpr);
+    const bf16_t* xr = x + r * (2L * I);
+    const u16x8 g = *reinterpret_cast<const u16x8*>(xr + c * 8);
+    const u16x8 u = *reinterpret_cast<const u16x8*>(xr + I + c * 8);
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float gv = bf2f(g.v[j]);
+      const float a = ACT == 0 ? silu(gv) : gelu_tanh(gv);
+      o.v[j] = f2bf(a * bf2f(u.v[j]));
+    }
+    *reinterpret_cast<u16x8*>(out + r * I + c * 8) = o;
+  }
+}
+
+int glu(void* out, const void* x, long rows, int I, int act, hipStream_t stream) {
+  if (rows <= 0) return 0;
+  if (I % 8 != 0) return -1;
+  const long nchunk = rows * (I / 8);
+  long blocks = (nchunk + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  if (act == 0)
+    glu_kernel<0><<<dim3((unsigned)blocks), dim3(256), 0, stream>>>((bf16_t*)out, (const bf16_t*)x, I, rows);
+  else
+    glu_kernel<1><<<dim3((unsigned)blocks), dim3(256), 0, stream>>>((bf16_t*)out, (const bf16_t*)x, I, rows);
+  return (int)hipGetLastError();
+}
+
+__global__ void __launch_bounds__(256) embed_gather_kernel(bf16_t* __restrict__ out,
+                                                           const bf16_t* __restrict__ table,
+                                                           const int* __restrict__ ids, int d,
+                                                           int vocab_start, int vocab_rows) {
+  const int t = blockIdx.x;
+  const int id = ids[t] - vocab_start;
+  const bool own = id >= 0 && id < vocab_rows;
+  const bf16_t* src = table + (long)(own ? id : 0) * d;
+  bf16_t* dst = out + (long)t * d;
+  for (int c = threadIdx.x; c < d / 8; c += blockDim.x) {
+    u16x8 v;
+    if (own) v = *reinterpret_cast<const u16x8*>(src + c * 8);
+    else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v.v[j] = 0;
+    }
+    *reinterpret_cast<u16x8*>(dst + c * 8) = v;
+  }
+}
+
+int embed_gather(void* out, const void* table, const int* ids, int T, int d, int vocab_start,
+                 int vocab_rows, hipStream_t stream) {
+  if (T <= 0) return 0;
+  if (d % 8 != 0) return -1;
+  embed_gather_kernel<<<dim3(T), dim3(256), 0, stream>>>((bf16_t*)out, (const bf16_t*)table, ids,
+                                                         d, vocab_start, vocab_rows);
+  return (int)hipGetLastError();
+}
+
+// grid (nseq), block 256; d <= 256 * 8
+__global__ void __launch_bounds__(256) mean_pool_l2_kernel(float* __restrict__ out,
+                                                           const bf16_t* __restrict__ h,
+                                                           const int* __restrict__ cu, int d,
+                                                           int dims, int normalize) {
+  __shared__ float scratch[16];
+  const int s = blockIdx.x;
+  const int t0 = cu[s], t1 = cu[s + 1];
+  const int c = threadIdx.x;  // 8-element chunk
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const bool active = c < d / 8;
+  if (active) {
+    for (int t = t0; t < t1; ++t) {
+      const u16x8 v = *reinterpret_cast<const u16x8*>(h + (long)t * d + c * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += bf2f(v.v[j]);
+    }
+  }
+  const float inv_n = t1 > t0 ? 1.f / (float)(t1 - t0) : 0.f;
+  float ss = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    acc[j] *= inv_n;
+    if (active && c * 8 + j < dims) ss += acc[j] * acc[j];
+  }
+  ss = block_sum(ss, scratch);
+  const float inv = normalize ? rsqrtf(fmaxf(ss, 1e-24f)) : 1.f;
+  if (active) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int col = c * 8 + j;
+      if (col < dims) out[(long)s * dims + col] = acc[j] * inv;
+    }
+  }
+}
+
+int mean_pool_l2(float* out, const void* h, const int* cu, int nseq, int d, int dims,
+                 int normalize, hipStream_t stream) {
+  if (nseq <= 0) return 0;
+  if (d % 8 != 0 || d > 2048 || dims > d || dims <= 0) return -1;
+  mean_pool_l2_kernel<<<dim3(nseq), dim3(256), 0, stream>>>(out, (const bf16_t*)h, cu, d, dims,
+                                                            normalize);
+  return (int)hipGetLastError();
+}
+
+// bias add (+ optional GELU/SiLU) in place on [rows, n] bf16 (used after
+// library GEMMs that do not fuse an epilogue)
+__global__ void __launch_bounds__(256) bias_act_kernel(bf16_t* __restrict__ x,
+                                                       const bf16_t* __restrict__ bias, int n,
+                                                       long rows, int act) {
+  const long nchunk = rows * (n / 8);
+  const int cpr = n / 8;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < nchunk;
+       e += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(e % cpr);
+    u16x8 v = *reinterpret_cast<u16x8*>(x + e * 8);
+    const u16x8 b = *reinterpret_cast<const u16x8*>(bias + c * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float f = bf2f(v.v[j]) + bf2f(b.v[j]);
+      if (act == 1) f = gelu_tanh(f);
+      else if (act == 2) f = silu(f);
+      v.v[j] = f2bf(f);
+    }
+    *reinterpret_cast<u16x8*>(x + e * 8) = v;
+  }
+}
+
+int bias_act(void* x, const void* bias, long rows, int n, int act, hipStream_t stream) {
+  if (rows <= 0) return 0;
+  if (n % 8 != 0) return -1;
+  long blocks = (rows * (n / 8) + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  bias_act_kernel<<<dim3((unsigned)blocks), dim3(256), 0, stream>>>((bf16_t*)x, (const bf16_t*)bias, n,
+                                                                 rows, act);
+  return (int)hipGetLastError();
+}
+
+}  // namespace lmx

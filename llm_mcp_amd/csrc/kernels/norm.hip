@@ -1,0 +1,163 @@
+// K1: RMSNorm (+ fused residual add) and LayerNorm (+ fused residual add, for
+// the post-norm nomic-bert encoder).  One workgroup per row, bf16 in/out, fp32
+// statistics, 16-byte vector loads, the whole row kept in registers so the
+// input is read from HBM exactly once.
+//
+// Replaces the normalisation Ollama/llama.cpp runs behind /api/chat and
+// /api/embed (reference: worker/llm_worker/main.py:222-261,
+// core/internal/api/handlers.go:1942-2015 only *call* it over HTTP).
+#include "common.h"
+
+namespace lmx {
+
+// VPT = 8-element chunks per thread. Row length = cols, multiple of 8.
+template <int VPT>
+__global__ void __launch_bounds__(256) rmsnorm_kernel(
+    bf16_t* __restrict__ out, bf16_t* __restrict__ residual,  // residual may be null
+    const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
+    int cols, long in_stride, long out_stride, float eps) {
+  __shared__ float scratch[16];
+  const int row = blockIdx.x;
+  const bf16_t* xr = x + (long)row * in_stride;
+  bf16_t* orow = out + (long)row * out_stride;
+  bf16_t* rr = residual ? residual + (long)row * cols : nullptr;
+  const int nchunk = cols >> 3;
+  float v[VPT][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = threadIdx.x + i * blockDim.x;
+    if (c < nchunk) {
+      u16x8 a = *reinterpret_cast<const u16x8*>(xr + c * 8);
+      if (rr) {
+        u16x8 b = *reinterpret_cast<const u16x8*>(rr + c * 8);
+        u16x8 h;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          // residual stream is kept in bf16 (as the model's hidden state is)
+          const uint16_t hb = f2bf(bf2f(a.v[j]) + bf2f(b.v[j]));
+          h.v[j] = hb;
+          v[i][j] = bf2f(hb);
+        }
+        *reinterpret_cast<u16x8*>(rr + c * 8) = h;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[i][j] = bf2f(a.v[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += v[i][j] * v[i][j];
+    }
+  }
+  ss = block_sum(ss, scratch);
+  const float inv = rsqrtf(ss / (float)cols + eps);
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = threadIdx.x + i * blockDim.x;
+    if (c < nchunk) {
+      u16x8 wv = *reinterpret_cast<const u16x8*>(w + c * 8);
+      u16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o.v[j] = f2bf(v[i][j] * inv * bf2f(wv.v[j]));
+      *reinterpret_cast<u16x8*>(orow + c * 8) = o;
+    }
+  }
+}
+
+template <int VPT>
+__global__ void __launch_bounds__(256) layernorm_kernel(
+    bf16_t* __restrict__ out, const bf16_t* __restrict__ x, const bf16_t* __restrict__ residual,
+    const bf16_t* __restrict__ w, const bf16_t* __restrict__ b, int cols, float eps) {
+  __shared__ float scratch[16];
+  const int row = blockIdx.x;
+  const bf16_t* xr = x + (long)row * cols;
+  const bf16_t* rr = residual ? residual + (long)row * cols : nullptr;
+  bf16_t* orow = out + (long)row * cols;
+  const int nchunk = cols >> 3;
+  float v[VPT][8];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = threadIdx.x + i * blockDim.x;
+    if (c < nchunk) {
+      u16x8 a = *reinterpret_cast<const u16x8*>(xr + c * 8);
+      u16x8 r;
+      if (rr) r = *reinterpret_cast<const u16x8*>(rr + c * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float t = bf2f(a.v[j]);
+        if (rr) t = bf2f(f2bf(t + bf2f(r.v[j])));
+        v[i][j] = t;
+        s += t;
+      }
+    }
+  }
+  const float mean = block_sum(s, scratch) / (float)cols;
+  float sq = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = threadIdx.x + i * blockDim.x;
+    if (c < nchunk) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { const float d = v[i][j] - mean; sq += d * d; }
+    }
+  }
+  const float inv = rsqrtf(block_sum(sq, scratch) / (float)cols + eps);
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = threadIdx.x + i * blockDim.x;
+    if (c < nchunk) {
+      u16x8 wv = *reinterpret_cast<const u16x8*>(w + c * 8);
+      u16x8 bv = *reinterpret_cast<const u16x8*>(b + c * 8);
+      u16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o.v[j] = f2bf((v[i][j] - mean) * inv * bf2f(wv.v[j]) + bf2f(bv.v[j]));
+      *reinterpret_cast<u16x8*>(orow + c * 8) = o;
+    }
+  }
+}
+
+static int pick_threads(int nchunk) {
+  int t = ((nchunk + 63) / 64) * 64;
+  return t > 256 ? 256 : (t < 64 ? 64 : t);
+}
+
+int rmsnorm(void* out, void* residual, const void* x, const void* w, int rows, int cols,
+            long in_stride, long out_stride, float eps, hipStream_t stream) {
+  if (cols % 8 != 0 || rows <= 0) return -1;
+  const int nchunk = cols / 8;
+  const int threads = pick_threads(nchunk);
+  const int vpt = (nchunk + threads - 1) / threads;
+  dim3 g(rows), b(threads);
+#define LMX_RMS(V)                                                                      \
+  rmsnorm_kernel<V><<<g, b, 0, stream>>>((bf16_t*)out, (bf16_t*)residual, (const bf16_t*)x, \
+                                         (const bf16_t*)w, cols, in_stride, out_stride, eps)
+  if (vpt <= 1) LMX_RMS(1);
+  else if (vpt <= 2) LMX_RMS(2);
+  else if (vpt <= 4) LMX_RMS(4);
+  else if (vpt <= 8) LMX_RMS(8);
+  else return -2;
+#undef LMX_RMS
+  return (int)hipGetLastError();
+}
+
+int layernorm(void* out, const void* x, const void* residual, const void* w, const void* b,
+              int rows, int cols, float eps, hipStream_t stream) {
+  if (cols % 8 != 0 || rows <= 0) return -1;
+  const int nchunk = cols / 8;
+  const int threads = pick_threads(nchunk);
+  const int vpt = (nchunk + threads - 1) / threads;
+  dim3 g(rows), bl(threads);
+#define LMX_LN(V)                                                                    \
+  layernorm_kernel<V><<<g, bl, 0, stream>>>((bf16_t*)out, (const bf16_t*)x,           \
+                                            (const bf16_t*)residual, (const bf16_t*)w, \
+                                            (const bf16_t*)b, cols, eps)
+  if (vpt <= 1) LMX_LN(1);
+  else if (vpt <= 2) LMX_LN(2);
+  else if (vpt <= 4) LMX_LN(4);
+  else if (vpt <= 8) LMX_LN(8);
+  else return -2;
+#undef LMX_LN
+  return (int)hipGetLastError();
+}
+
+}  // namespace lmx

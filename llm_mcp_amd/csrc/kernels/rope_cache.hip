@@ -1,0 +1,108 @@
+// K2 + K5: rotary embedding (neox / rotate-half form, as Llama-3 and
+// nomic-bert use) applied in place to the q and k heads of the fused QKV
+// projection output, fused with the scatter of k and v into the paged KV cache.
+//
+// KV-cache layout (MI355X-first, chosen for the MFMA operand maps of the
+// attention kernels, see decode_attn.hip):
+//   k_cache [num_blocks][Hkv][BS][D]   token-major: a K row is the 16-B A/B
+//                                      fragment source of S = K.Q^T
+//   v_cache [num_blocks][Hkv][D][BS]   d-major (transposed): 8 consecutive
+//                                      tokens of one d are the contiguous
+//                                      fragment of O^T = V^T.P^T
+// cos/sin come from a host-precomputed fp32 table [max_pos][D] (cos | sin),
+// so no transcendental runs on the device (guide App. B, element-wise).
+#include "common.h"
+
+namespace lmx {
+
+__global__ void __launch_bounds__(256) rope_cache_kernel(
+    bf16_t* __restrict__ qkv, long qkv_stride, const int* __restrict__ positions,
+    const float* __restrict__ cos_sin, int Hq, int Hkv, int D,
+    const int* __restrict__ slot_mapping, bf16_t* __restrict__ k_cache,
+    bf16_t* __restrict__ v_cache, int BS, int rotate_k_inplace) {
+  const int t = blockIdx.x;
+  const int half = D >> 1;
+  const int tph = half >> 2;  // threads per head, each owns 4 rotation pairs
+  bf16_t* row = qkv + (long)t * qkv_stride;
+  const int pos = positions[t];
+  const float* cs = cos_sin + (long)pos * D;
+  const int slot = slot_mapping ? slot_mapping[t] : -1;
+  const int blk = slot >= 0 ? slot / BS : 0, off = slot >= 0 ? slot % BS : 0;
+
+  // rotate q (and k) heads
+  const int nrot = (Hq + Hkv) * tph;
+  for (int it = threadIdx.x; it < nrot; it += blockDim.x) {
+    const int h = it / tph, i = (it % tph) * 4;
+    bf16_t* hp = row + (long)h * D;
+    const bf16x4_t x1 = *reinterpret_cast<const bf16x4_t*>(hp + i);
+    const bf16x4_t x2 = *reinterpret_cast<const bf16x4_t*>(hp + half + i);
+    const float4 c = *reinterpret_cast<const float4*>(cs + i);
+    const float4 s = *reinterpret_cast<const float4*>(cs + half + i);
+    const float cc[4] = {c.x, c.y, c.z, c.w}, ss[4] = {s.x, s.y, s.z, s.w};
+    bf16x4_t o1, o2;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float a = bf2f((uint16_t)x1[j]), b = bf2f((uint16_t)x2[j]);
+      o1[j] = (short)f2bf(a * cc[j] - b * ss[j]);
+      o2[j] = (short)f2bf(b * cc[j] + a * ss[j]);
+    }
+    const bool is_k = h >= Hq;
+    if (!is_k || rotate_k_inplace || slot < 0) {
+      *reinterpret_cast<bf16x4_t*>(hp + i) = o1;
+      *reinterpret_cast<bf16x4_t*>(hp + half + i) = o2;
+    }
+    if (is_k && slot >= 0 && k_cache) {
+      bf16_t* kp = k_cache + (((long)blk * Hkv + (h - Hq)) * BS + off) * D;
+      *reinterpret_cast<bf16x4_t*>(kp + i) = o1;
+      *reinterpret_cast<bf16x4_t*>(kp + half + i) = o2;
+    }
+  }
+  if (slot < 0 || !v_cache) return;
+  // v -> transposed cache page (2-B scatter; one token per block so a page
+  // row of BS tokens is completed by BS consecutive blocks, merged in L2)
+  const bf16_t* vrow = row + (long)(Hq + Hkv) * D;
+  const int nv = Hkv * D;
+  for (int it = threadIdx.x; it < nv; it += blockDim.x) {
+    const int h = it / D, d = it % D;
+    v_cache[(((long)blk * Hkv + h) * D + d) * BS + off] = vrow[it];
+  }
+}
+
+int rope_cache(void* qkv, long qkv_stride, const int* positions, const float* cos_sin, int T,
+               int Hq, int Hkv, int D, const int* slot_mapping, void* k_cache, void* v_cache,
+               int BS, int rotate_k_inplace, hipStream_t stream) {
+  if (T <= 0) return 0;
+  if (D % 8 != 0 || D > 256) return -1;
+  rope_cache_kernel<<<dim3(T), dim3(256), 0, stream>>>(
+      (bf16_t*)qkv, qkv_stride, positions, cos_sin, Hq, Hkv, D, slot_mapping,
+      (bf16_t*)k_cache, (bf16_t*)v_cache, BS, rotate_k_inplace);
+  return (int)hipGetLastError();
+}
+
+// Plain cache write (no rotation), used by the paged-cache tests and by
+// models without rotary embeddings.
+__global__ void kv_write_kernel(const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+                                long kv_stride, const int* __restrict__ slot_mapping, int Hkv,
+                                int D, bf16_t* __restrict__ k_cache, bf16_t* __restrict__ v_cache,
+                                int BS) {
+  const int t = blockIdx.x;
+  const int slot = slot_mapping[t];
+  if (slot < 0) return;
+  const int blk = slot / BS, off = slot % BS;
+  for (int it = threadIdx.x; it < Hkv * D; it += blockDim.x) {
+    const int h = it / D, d = it % D;
+    k_cache[(((long)blk * Hkv + h) * BS + off) * D + d] = k[(long)t * kv_stride + it];
+    v_cache[(((long)blk * Hkv + h) * D + d) * BS + off] = v[(long)t * kv_stride + it];
+  }
+}
+
+int kv_write(const void* k, const void* v, long kv_stride, const int* slot_mapping, int T, int Hkv,
+             int D, void* k_cache, void* v_cache, int BS, hipStream_t stream) {
+  if (T <= 0) return 0;
+  kv_write_kernel<<<dim3(T), dim3(256), 0, stream>>>((const bf16_t*)k, (const bf16_t*)v,
+                                                     kv_stride, slot_mapping, Hkv, D,
+                                                     (bf16_t*)k_cache, (bf16_t*)v_cache, BS);
+  return (int)hipGetLastError();
+}
+
+}  // namespace lmx

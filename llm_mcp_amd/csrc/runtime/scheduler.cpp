@@ -1,0 +1,200 @@
+#include "scheduler.h"
+
+#include <algorithm>
+#include <stdexcept>
+
+namespace lmxrt {
+
+Scheduler::Scheduler(int num_blocks, int block_size, int max_num_seqs, int max_batched_tokens,
+                     int max_model_len, bool prefix_cache)
+    : bm_(num_blocks, block_size, prefix_cache),
+      max_num_seqs_(max_num_seqs),
+      max_batched_tokens_(max_batched_tokens),
+      max_model_len_(max_model_len) {
+  if (max_num_seqs <= 0 || max_batched_tokens <= 0 || max_model_len <= 0)
+    throw std::invalid_argument("bad scheduler limits");
+  max_blocks_ = (max_model_len + block_size - 1) / block_size;
+}
+
+void Scheduler::add(int64_t id, const std::vector<int32_t>& prompt, int max_new,
+                    const std::vector<int32_t>& stop_ids, bool ignore_eos, int priority) {
+  if (seqs_.count(id)) throw std::invalid_argument("duplicate sequence id");
+  if (prompt.empty()) throw std::invalid_argument("empty prompt");
+  if ((int)prompt.size() >= max_model_len_)
+    throw std::invalid_argument("prompt longer than max_model_len");
+  const int pages = ((int)prompt.size() + bm_.block_size()) / bm_.block_size();
+  if (pages > bm_.num_blocks()) throw std::invalid_argument("prompt larger than the KV cache");
+  auto s = std::make_unique<Seq>();
+  s->id = id;
+  s->tokens = prompt;
+  s->prompt_len = (int)prompt.size();
+  s->max_new = std::max(1, std::min(max_new, max_model_len_ - (int)prompt.size()));
+  s->stop_ids = stop_ids;
+  s->ignore_eos = ignore_eos;
+  s->priority = priority;
+  s->arrival = arrival_++;
+  Seq* raw = s.get();
+  seqs_[id] = std::move(s);
+  // priority first (higher earlier), FIFO inside a priority
+  auto it = waiting_.end();
+  while (it != waiting_.begin() && (*(it - 1))->priority < priority) --it;
+  waiting_.insert(it, raw);
+}
+
+const Seq* Scheduler::get(int64_t id) const {
+  auto it = seqs_.find(id);
+  return it == seqs_.end() ? nullptr : it->second.get();
+}
+
+bool Scheduler::abort(int64_t id) {
+  auto it = seqs_.find(id);
+  if (it == seqs_.end()) return false;
+  Seq* s = it->second.get();
+  auto w = std::find(waiting_.begin(), waiting_.end(), s);
+  if (w != waiting_.end()) waiting_.erase(w);
+  auto r = std::find(running_.begin(), running_.end(), s);
+  if (r != running_.end()) running_.erase(r);
+  bm_.free_seq(id);
+  seqs_.erase(it);
+  return true;
+}
+
+void Scheduler::preempt(Seq* s) {
+  bm_.free_seq(s->id);
+  s->num_computed = 0;
+  s->scheduled = 0;
+  s->status = WAITING;
+  auto r = std::find(running_.begin(), running_.end(), s);
+  if (r != running_.end()) running_.erase(r);
+  waiting_.push_front(s);
+  plan_.preempted.push_back(s->id);
+  ++preemptions_;
+}
+
+void Scheduler::finish(Seq* s, int reason) {
+  s->status = FINISHED;
+  s->finish = reason;
+  bm_.free_seq(s->id);
+  auto r = std::find(running_.begin(), running_.end(), s);
+  if (r != running_.end()) running_.erase(r);
+}
+
+const StepPlan& Scheduler::schedule(int q_per_tile) {
+  if (q_per_tile <= 0) q_per_tile = 16;
+  StepPlan& p = plan_;
+  p.input_ids.clear(); p.positions.clear(); p.slots.clear();
+  p.seq_ids.clear(); p.qlens.clear(); p.context_lens.clear(); p.cu_q.clear();
+  p.block_tables.clear(); p.sample_rows.clear(); p.sample_seq.clear();
+  p.prefill_tiles.clear(); p.preempted.clear();
+  p.num_decode = 0; p.num_tokens = 0; p.num_prefill_tokens = 0; p.max_context = 0;
+  p.max_blocks = max_blocks_;
+  plan_seqs_.clear();
+
+  int budget = max_batched_tokens_;
+  std::vector<Seq*> decodes, prefills;
+  // 1. running sequences, oldest first
+  for (size_t i = 0; i < running_.size() && budget > 0;) {
+    Seq* s = running_[i];
+    const int remaining = (int)s->tokens.size() - s->num_computed;
+    if (remaining <= 0) { ++i; continue; }
+    const int n = std::min(remaining, budget);
+    bool preempted_self = false;
+    while (!bm_.ensure(s->id, s->num_computed + n)) {
+      Seq* victim = running_.back();
+      preempt(victim);
+      if (victim == s) { preempted_self = true; break; }
+    }
+    if (preempted_self) break;
+    s->scheduled = n;
+    budget -= n;
+    (n == 1 ? decodes : prefills).push_back(s);
+    ++i;
+  }
+  // 2. admit waiting sequences
+  while (!waiting_.empty() && budget > 0 && (int)running_.size() < max_num_seqs_) {
+    Seq* s = waiting_.front();
+    if (s->num_computed == 0 && !bm_.has(s->id))
+      s->num_computed = bm_.match_prefix(s->id, s->tokens.data(), (int)s->tokens.size());
+    const int remaining = (int)s->tokens.size() - s->num_computed;
+    const int n = std::min(remaining, budget);
+    if (!bm_.ensure(s->id, s->num_computed + n)) break;
+    waiting_.pop_front();
+    s->status = RUNNING;
+    running_.push_back(s);
+    s->scheduled = n;
+    budget -= n;
+    (n == 1 ? decodes : prefills).push_back(s);
+  }
+
+  // 3. flatten (decode rows first)
+  const int bs = bm_.block_size();
+  p.cu_q.push_back(0);
+  auto emit = [&](Seq* s, bool is_prefill, int prefill_idx) {
+    const int n = s->scheduled;
+    const std::vector<int32_t>& tab = bm_.table(s->id);
+    const int row0 = p.num_tokens;
+    for (int t = s->num_computed; t < s->num_computed + n; ++t) {
+      p.input_ids.push_back(s->tokens[t]);
+      p.positions.push_back(t);
+      p.slots.push_back(tab[t / bs] * bs + t % bs);
+    }
+    p.num_tokens += n;
+    const int ctx = s->num_computed + n;
+    p.seq_ids.push_back(s->id);
+    p.qlens.push_back(n);
+    p.context_lens.push_back(ctx);
+    p.cu_q.push_back(p.num_tokens);
+    p.max_context = std::max(p.max_context, ctx);
+    const size_t off = p.block_tables.size();
+    p.block_tables.resize(off + max_blocks_, 0);
+    std::copy(tab.begin(), tab.end(), p.block_tables.begin() + off);
+    if (ctx == (int)s->tokens.size()) {
+      p.sample_rows.push_back(row0 + n - 1);
+      p.sample_seq.push_back((int)plan_seqs_.size());
+    }
+    if (is_prefill) {
+      p.num_prefill_tokens += n;
+      for (int q0 = 0; q0 < n; q0 += q_per_tile) {
+        p.prefill_tiles.push_back(prefill_idx);
+        p.prefill_tiles.push_back(q0);
+      }
+    }
+    plan_seqs_.push_back(s);
+  };
+  for (Seq* s : decodes) emit(s, false, 0);
+  p.num_decode = (int)decodes.size();
+  int j = 0;
+  for (Seq* s : prefills) emit(s, true, j++);
+  return p;
+}
+
+std::vector<std::pair<int64_t, int>> Scheduler::update(const int32_t* sampled, int n) {
+  std::vector<std::pair<int64_t, int>> done;
+  if (n != (int)plan_.sample_rows.size()) throw std::invalid_argument("sample count mismatch");
+  for (Seq* s : plan_seqs_) {
+    s->num_computed += s->scheduled;
+    s->scheduled = 0;
+    bm_.commit(s->id, s->tokens.data(), s->num_computed);
+  }
+  for (int i = 0; i < n; ++i) {
+    Seq* s = plan_seqs_[plan_.sample_seq[i]];
+    const int32_t tok = sampled[i];
+    s->tokens.push_back(tok);
+    s->num_generated++;
+    int reason = FR_NONE;
+    if (!s->ignore_eos &&
+        std::find(s->stop_ids.begin(), s->stop_ids.end(), tok) != s->stop_ids.end())
+      reason = FR_STOP;
+    else if (s->num_generated >= s->max_new || (int)s->tokens.size() >= max_model_len_)
+      reason = FR_LENGTH;
+    if (reason != FR_NONE) {
+      finish(s, reason);
+      done.emplace_back(s->id, reason);
+    }
+  }
+  for (auto& d : done) seqs_.erase(d.first);
+  plan_seqs_.clear();
+  return done;
+}
+
+}  // namespace lmxrt

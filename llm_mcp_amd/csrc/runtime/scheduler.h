@@ -1,0 +1,102 @@
+// Continuous-batching step scheduler (native runtime).
+//
+// One instance per engine (per GPU, or per TP group on its leader rank).  Every
+// engine step asks `schedule()` for a StepPlan: a token-budgeted batch in which
+//   * every running sequence gets its next token (decode) or its next prefill
+//     chunk (chunked prefill, bounded by max_batched_tokens),
+//   * waiting sequences are admitted FIFO (priority first) while KV pages,
+//     batch slots and the token budget allow, reusing cached prefix pages,
+//   * when pages run out a running sequence is preempted by recompute (its
+//     pages are freed, it re-enters the front of the waiting queue with its
+//     generated tokens appended to the prompt).
+// The plan is written into flat int32 arrays in the exact layout the GPU
+// kernels consume (decode rows first, then prefill rows), so the Python side
+// does one host->device copy per step and no per-token Python work.
+//
+// This replaces the reference's one-job-per-worker execution
+// (worker/llm_worker/main.py:558-599): a GPU worker serves many claimed jobs
+// at once and admission is by KV pages rather than DEVICE_MAX_CONCURRENCY.
+#pragma once
+#include <cstdint>
+#include <deque>
+#include <memory>
+#include <unordered_map>
+#include <vector>
+
+#include "block_manager.h"
+
+namespace lmxrt {
+
+enum SeqStatus { WAITING = 0, RUNNING = 1, FINISHED = 2 };
+enum FinishReason { FR_NONE = 0, FR_STOP = 1, FR_LENGTH = 2, FR_ABORT = 3 };
+
+struct Seq {
+  int64_t id = 0;
+  std::vector<int32_t> tokens;  // prompt + generated
+  int prompt_len = 0;
+  int num_computed = 0;         // tokens whose KV is resident
+  int max_new = 0;
+  int num_generated = 0;
+  int priority = 0;
+  int64_t arrival = 0;
+  bool ignore_eos = false;
+  std::vector<int32_t> stop_ids;
+  int status = WAITING;
+  int finish = FR_NONE;
+  int scheduled = 0;            // tokens scheduled in the current plan
+};
+
+struct StepPlan {
+  // per token rows (T)
+  std::vector<int32_t> input_ids, positions, slots;
+  // per scheduled sequence (S), decode sequences first
+  std::vector<int64_t> seq_ids;
+  std::vector<int32_t> qlens, context_lens, cu_q;  // cu_q has S+1 entries
+  std::vector<int32_t> block_tables;               // S x max_blocks (0-padded)
+  std::vector<int32_t> sample_rows;                // token rows whose logits are sampled
+  std::vector<int32_t> sample_seq;                 // index into seq_ids for each sample row
+  std::vector<int32_t> prefill_tiles;              // (prefill-seq index, q_start) pairs
+  int num_decode = 0;                              // first num_decode sequences have qlen 1
+  int max_blocks = 0;
+  int num_tokens = 0;
+  int num_prefill_tokens = 0;
+  int max_context = 0;
+  std::vector<int64_t> preempted;
+};
+
+class Scheduler {
+ public:
+  Scheduler(int num_blocks, int block_size, int max_num_seqs, int max_batched_tokens,
+            int max_model_len, bool prefix_cache);
+
+  void add(int64_t id, const std::vector<int32_t>& prompt, int max_new,
+           const std::vector<int32_t>& stop_ids, bool ignore_eos, int priority);
+  bool abort(int64_t id);
+  // q_per_tile: queries per prefill workgroup (64 / G for the paged prefill kernel)
+  const StepPlan& schedule(int q_per_tile);
+  // sampled[i] is the token for plan.sample_rows[i]; returns finished (id, reason)
+  std::vector<std::pair<int64_t, int>> update(const int32_t* sampled, int n);
+
+  int num_waiting() const { return (int)waiting_.size(); }
+  int num_running() const { return (int)running_.size(); }
+  bool has_work() const { return !waiting_.empty() || !running_.empty(); }
+  BlockManager& blocks() { return bm_; }
+  const Seq* get(int64_t id) const;
+  int64_t preemptions() const { return preemptions_; }
+
+ private:
+  void preempt(Seq* s);
+  void finish(Seq* s, int reason);
+
+  BlockManager bm_;
+  int max_num_seqs_, max_batched_tokens_, max_model_len_, max_blocks_;
+  std::unordered_map<int64_t, std::unique_ptr<Seq>> seqs_;
+  std::deque<Seq*> waiting_;
+  std::vector<Seq*> running_;
+  std::vector<Seq*> plan_seqs_;
+  StepPlan plan_;
+  int64_t arrival_ = 0;
+  int64_t preemptions_ = 0;
+};
+
+}  // namespace lmxrt

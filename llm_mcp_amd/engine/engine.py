@@ -1,0 +1,502 @@
+"""In-process LLM serving engine (one per GPU, or per TP group on its leader).
+
+Replaces the reference's out-of-tree inference hop (core -> Ollama /api/chat,
+worker -> /api/generate).  Pieces:
+
+* native continuous-batching scheduler + paged-KV block manager
+  (csrc/runtime/scheduler.cpp) decides every step;
+* the step's metadata is packed into ONE pinned buffer and moved with ONE
+  host->device copy;
+* pure-decode steps replay a captured hipGraph per batch bucket (the whole
+  forward + sampling), mixed/prefill steps run eagerly;
+* results leave the engine thread as one batched event list per step
+  (``event_sink``), so the asyncio side wakes once per step, not per token.
+
+Thread model: a single engine thread owns the GPU stream, the scheduler and
+all device buffers.  ``submit`` / ``abort`` are thread-safe and only enqueue.
+"""
+from __future__ import annotations
+
+import itertools
+import logging
+import math
+import os
+import queue
+import threading
+import time
+from dataclasses import dataclass, field
+from typing import Callable
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..models.config import LlamaConfig
+from ..models.llama import LlamaModel, StepInputs, TPContext
+
+log = logging.getLogger("lmx.engine")
+
+BLOCK_SIZE = 32
+FINISH_REASONS = {1: "stop", 2: "length", 3: "abort"}
+
+
+@dataclass
+class SamplingParams:
+    temperature: float = 1.0
+    top_p: float = 1.0
+    top_k: int = 0
+    max_tokens: int = 256
+    stop: list[str] = field(default_factory=list)
+    stop_token_ids: list[int] = field(default_factory=list)
+    ignore_eos: bool = False
+    seed: int | None = None
+    logprobs: bool = False
+
+
+@dataclass
+class GenRequest:
+    prompt_ids: list[int]
+    params: SamplingParams
+    id: int = 0
+    priority: int = 0
+    user: object = None             # opaque handle for the event sink
+    arrival: float = 0.0
+    first_token_at: float = 0.0
+    num_generated: int = 0
+    finished: bool = False
+
+
+@dataclass
+class TokenEvent:
+    req: GenRequest
+    token: int
+    logprob: float
+    finish: str | None  # None while running
+
+
+@dataclass
+class EngineConfig:
+    model: str = "llama-3-8b"
+    max_num_seqs: int = 256
+    max_batched_tokens: int = 8192
+    max_model_len: int = 8192
+    kv_fraction: float = 0.6        # of free HBM after weights
+    kv_cache_gb: float | None = None
+    prefix_cache: bool = True
+    use_graphs: bool = True
+    part_tokens: int = 512
+    seed: int = 0
+
+
+class _Packer:
+    """Packs numpy arrays into one pinned host buffer and one device buffer
+    (16-byte aligned regions) so a step's metadata moves in one copy."""
+
+    def __init__(self, nbytes: int, device):
+        self.nbytes = nbytes
+        self.device = device
+        pin = device.type == "cuda"
+        self.host = torch.empty(nbytes, dtype=torch.uint8, pin_memory=pin)
+        self.dev = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        self.hnp = self.host.numpy()
+
+    def pack(self, items: list[tuple[str, np.ndarray]]) -> dict[str, torch.Tensor]:
+        off, spans = 0, []
+        for name, a in items:
+            a = np.ascontiguousarray(a)
+            n = a.nbytes
+            if off + n > self.nbytes:
+                raise RuntimeError("step metadata exceeds packer capacity")
+            self.hnp[off:off + n] = a.view(np.uint8).reshape(-1)
+            spans.append((name, off, a.dtype, a.shape))
+            off += (n + 15) & ~15
+        if off:
+            self.dev[:off].copy_(self.host[:off], non_blocking=True)
+        out = {}
+        for name, o, dt, shape in spans:
+            n = int(np.prod(shape)) * np.dtype(dt).itemsize
+            out[name] = self.dev[o:o + n].view(_TORCH_DT[np.dtype(dt)]).view(shape)
+        return out
+
+
+_TORCH_DT = {np.dtype(np.int32): torch.int32, np.dtype(np.int64): torch.int64,
+             np.dtype(np.float32): torch.float32}
+
+
+class _FixedMeta:
+    """Fixed-layout metadata block (pinned host mirror + device buffer): the
+    static inputs of the captured decode graphs are device views into it, so
+    a replay needs exactly one host->device copy."""
+
+    def __init__(self, fields: list[tuple[str, type, tuple]], device):
+        off, spans = 0, []
+        for name, dt, shape in fields:
+            n = int(np.prod(shape)) * np.dtype(dt).itemsize
+            spans.append((name, off, dt, shape, n))
+            off += (n + 15) & ~15
+        self.nbytes = off
+        self.host_t = torch.empty(off, dtype=torch.uint8, pin_memory=device.type == "cuda")
+        self.dev_t = torch.empty(off, dtype=torch.uint8, device=device)
+        hnp = self.host_t.numpy()
+        self.h, self.d = {}, {}
+        for name, o, dt, shape, n in spans:
+            self.h[name] = hnp[o:o + n].view(dt).reshape(shape)
+            self.d[name] = self.dev_t[o:o + n].view(_TORCH_DT[np.dtype(dt)]).view(shape)
+
+    def upload(self):
+        self.dev_t.copy_(self.host_t, non_blocking=True)
+
+
+class LLMEngine:
+    def __init__(self, ecfg: EngineConfig, device: str | torch.device = "cuda",
+                 model_cfg: LlamaConfig | None = None, tp: TPContext | None = None,
+                 event_sink: Callable[[list[TokenEvent]], None] | None = None,
+                 weights: dict | None = None):
+        from ..models import config as mc
+        from ..native import runtime
+        _runtime = runtime()
+        self.ecfg = ecfg
+        self.device = torch.device(device)
+        if self.device.type == "cuda" and self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        self.cfg = model_cfg or mc.resolve(ecfg.model)
+        self.max_model_len = min(ecfg.max_model_len, self.cfg.max_position)
+        self.model = LlamaModel(self.cfg, self.device, tp=tp, seed=ecfg.seed, weights=weights)
+        self.tp = self.model.tp
+        self.Hq, self.Hkv, self.D = self.model.Hq, self.model.Hkv, self.model.D
+        self.q_per_tile = ops.prefill_q_per_tile(self.Hq, self.Hkv)
+        self._alloc_kv()
+        self.sched = _runtime.Scheduler(self.num_blocks, BLOCK_SIZE, ecfg.max_num_seqs,
+                                        ecfg.max_batched_tokens, self.max_model_len,
+                                        ecfg.prefix_cache)
+        self.max_blocks = math.ceil(self.max_model_len / BLOCK_SIZE)
+        self.max_parts = max(1, min(16, math.ceil(self.max_model_len / ecfg.part_tokens)))
+        self.decode_ws = ops.DecodeWorkspace(ecfg.max_num_seqs, self.Hq, self.D, self.max_parts,
+                                             self.device)
+        T = ecfg.max_batched_tokens + ecfg.max_num_seqs
+        cap = 4 * (4 * T + ecfg.max_num_seqs * (self.max_blocks + 8) + 2 * T) + 16 * 64 + \
+            8 * ecfg.max_num_seqs * 4
+        self.packer = _Packer(cap, self.device)
+        self.event_sink = event_sink
+        self._intake: queue.SimpleQueue = queue.SimpleQueue()
+        self._aborts: queue.SimpleQueue = queue.SimpleQueue()
+        self._reqs: dict[int, GenRequest] = {}
+        self._ids = itertools.count(1)
+        self._wake = threading.Event()
+        self._stop = threading.Event()
+        self._thread: threading.Thread | None = None
+        self.graphs: dict[int, dict] = {}
+        self.stats = {"steps": 0, "decode_steps": 0, "graph_steps": 0, "prefill_tokens": 0,
+                      "generated_tokens": 0, "step_time_s": 0.0, "finished": 0}
+        if ecfg.use_graphs and self.device.type == "cuda":
+            self._capture_graphs()
+
+    # ------------------------------------------------------------ memory ----
+    def _alloc_kv(self):
+        cfg = self.cfg
+        per_block = cfg.num_layers * 2 * self.Hkv * BLOCK_SIZE * self.D * 2
+        if self.ecfg.kv_cache_gb is not None:
+            kv_bytes = int(self.ecfg.kv_cache_gb * (1 << 30))
+        elif self.device.type == "cuda":
+            free, _ = torch.cuda.mem_get_info(self.device)
+            kv_bytes = int(free * self.ecfg.kv_fraction)
+        else:
+            kv_bytes = 64 * per_block
+        self.num_blocks = max(16, kv_bytes // per_block)
+        # zero-filled: masked keys multiply P = 0 with V, which must be finite
+        self.kv = torch.zeros((cfg.num_layers, 2, self.num_blocks, self.Hkv, BLOCK_SIZE * self.D),
+                              dtype=torch.bfloat16, device=self.device)
+        self.k_caches = [self.kv[l, 0].view(self.num_blocks, self.Hkv, BLOCK_SIZE, self.D)
+                         for l in range(cfg.num_layers)]
+        self.v_caches = [self.kv[l, 1].view(self.num_blocks, self.Hkv, self.D, BLOCK_SIZE)
+                         for l in range(cfg.num_layers)]
+        log.info("KV cache: %d blocks x %d tokens (%.1f GB)", self.num_blocks, BLOCK_SIZE,
+                 self.kv.numel() * 2 / 1e9)
+
+    # ------------------------------------------------------------- graphs ---
+    def _graph_buckets(self) -> list[int]:
+        base = [1, 2, 4, 8, 16, 24, 32, 40, 48, 56, 64, 80, 96, 112, 128, 160, 192, 224, 256,
+                320, 384, 448, 512]
+        return [b for b in base if b <= self.ecfg.max_num_seqs]
+
+    def _graph_parts(self, B: int) -> int:
+        # enough split-K partitions to fill the chip for small batches; the
+        # kernel grows the partition length when a context needs more
+        return max(1, min(self.max_parts, 2048 // max(1, B * self.Hkv)))
+
+    def _capture_graphs(self):
+        t0 = time.time()
+        Bmax = max(self._graph_buckets())
+        dev = self.device
+        meta = _FixedMeta([
+            ("ids", np.int32, (Bmax,)), ("pos", np.int32, (Bmax,)), ("slots", np.int32, (Bmax,)),
+            ("ctx", np.int32, (Bmax,)), ("bt", np.int32, (Bmax, self.max_blocks)),
+            ("temp", np.float32, (Bmax,)), ("topk", np.int32, (Bmax,)),
+            ("topp", np.float32, (Bmax,)), ("seeds", np.int64, (Bmax,)),
+            ("offs", np.int32, (Bmax,))], dev)
+        h = meta.h
+        h["ids"][:] = 0; h["pos"][:] = 0; h["slots"][:] = -1; h["ctx"][:] = 1; h["bt"][:] = 0
+        h["temp"][:] = 0; h["topk"][:] = 0; h["topp"][:] = 1; h["seeds"][:] = 0; h["offs"][:] = 0
+        meta.upload()
+        self._gmeta = meta
+        g = dict(meta.d)
+        g.update({
+            "cu": torch.arange(Bmax + 1, dtype=torch.int32, device=dev),
+            "tiles": torch.zeros(2, dtype=torch.int32, device=dev),
+            "rows": torch.arange(Bmax, dtype=torch.int64, device=dev),
+            "tok": torch.zeros(Bmax, dtype=torch.int32, device=dev),
+            "lp": torch.zeros(Bmax, dtype=torch.float32, device=dev),
+        })
+        self._gbuf = g
+        pool = None
+        stream = torch.cuda.Stream(device=dev)
+        for B in sorted(self._graph_buckets(), reverse=True):
+            inp = StepInputs(g["ids"][:B], g["pos"][:B], g["slots"][:B], B, g["bt"][:B],
+                             g["ctx"][:B], g["cu"][:B + 1], g["tiles"], g["rows"][:B], B, B)
+            parts = self._graph_parts(B)
+            ws = ops.DecodeWorkspace.__new__(ops.DecodeWorkspace)
+            ws.max_parts, ws.part_o, ws.part_ml = parts, self.decode_ws.part_o, self.decode_ws.part_ml
+
+            def run(inp=inp, ws=ws, B=B):
+                logits = self.model.forward(inp, self.k_caches, self.v_caches, ws,
+                                            self.ecfg.part_tokens)
+                ops.sample(logits, g["temp"][:B], g["topk"][:B], g["topp"][:B], g["seeds"][:B],
+                           g["offs"][:B], g["tok"][:B], g["lp"][:B])
+
+            stream.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(stream):
+                run()  # warm-up (allocator, kernels, hipBLASLt heuristics)
+                run()
+            torch.cuda.current_stream(dev).wait_stream(stream)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph, pool=pool, stream=stream):
+                run()
+            pool = graph.pool()
+            self.graphs[B] = {"graph": graph, "parts": parts}
+        torch.cuda.synchronize(dev)
+        log.info("captured %d decode graphs in %.1fs", len(self.graphs), time.time() - t0)
+
+    # --------------------------------------------------------- public API ---
+    def submit(self, req: GenRequest) -> GenRequest:
+        if not req.id:
+            req.id = next(self._ids)
+        req.arrival = req.arrival or time.time()
+        self._intake.put(req)
+        self._wake.set()
+        return req
+
+    def abort(self, req_id: int) -> None:
+        self._aborts.put(req_id)
+        self._wake.set()
+
+    def start(self):
+        if self._thread is None:
+            self._stop.clear()
+            self._thread = threading.Thread(target=self._loop, name="lmx-engine", daemon=True)
+            self._thread.start()
+
+    def stop(self):
+        self._stop.set()
+        self._wake.set()
+        if self._thread is not None:
+            self._thread.join(timeout=30)
+            self._thread = None
+
+    @property
+    def num_active(self) -> int:
+        return len(self._reqs)
+
+    def _loop(self):
+        if self.device.type == "cuda":
+            torch.cuda.set_device(self.device)
+        while not self._stop.is_set():
+            try:
+                did = self.step()
+            except Exception:  # keep serving: fail the in-flight requests
+                log.exception("engine step failed")
+                self._fail_all("engine_error")
+                did = False
+            if not did:
+                self._wake.wait(timeout=0.05)
+                self._wake.clear()
+
+    def _fail_all(self, why: str):
+        evs = []
+        for rid, req in list(self._reqs.items()):
+            self.sched.abort(rid)
+            req.finished = True
+            evs.append(TokenEvent(req, -1, 0.0, "error"))
+        self._reqs.clear()
+        if evs and self.event_sink:
+            self.event_sink(evs)
+
+    def _drain(self):
+        evs = []
+        while True:
+            try:
+                rid = self._aborts.get_nowait()
+            except queue.Empty:
+                break
+            req = self._reqs.pop(rid, None)
+            if req is not None:
+                self.sched.abort(rid)
+                req.finished = True
+                evs.append(TokenEvent(req, -1, 0.0, "abort"))
+        while True:
+            try:
+                req = self._intake.get_nowait()
+            except queue.Empty:
+                break
+            p = req.params
+            stop_ids = list(p.stop_token_ids) + list(getattr(self.cfg, "eos_token_ids", ()))
+            try:
+                self.sched.add(req.id, list(req.prompt_ids), int(p.max_tokens), stop_ids,
+                               bool(p.ignore_eos), int(req.priority))
+                self._reqs[req.id] = req
+            except Exception as e:
+                req.finished = True
+                evs.append(TokenEvent(req, -1, 0.0, f"error:{e}"))
+        if evs and self.event_sink:
+            self.event_sink(evs)
+
+    # -------------------------------------------------------------- step ----
+    def _sampling_arrays(self, seq_ids: np.ndarray, sample_seq: np.ndarray, n_rows: int):
+        temp = np.zeros(n_rows, np.float32)
+        topk = np.zeros(n_rows, np.int32)
+        topp = np.ones(n_rows, np.float32)
+        seeds = np.zeros(n_rows, np.int64)
+        offs = np.zeros(n_rows, np.int32)
+        for i, si in enumerate(sample_seq):
+            req = self._reqs[int(seq_ids[si])]
+            p = req.params
+            temp[i] = p.temperature
+            topk[i] = p.top_k
+            topp[i] = p.top_p
+            seeds[i] = p.seed if p.seed is not None else (req.id * 2654435761) & 0x7FFFFFFF
+            offs[i] = req.num_generated
+        return temp, topk, topp, seeds, offs
+
+    def step(self) -> bool:
+        self._drain()
+        if not self.sched.has_work:
+            return False
+        t0 = time.perf_counter()
+        plan = self.sched.schedule(self.q_per_tile)
+        T = plan["num_tokens"]
+        if T == 0:
+            return False
+        seq_ids = plan["seq_ids"]
+        S = len(seq_ids)
+        nd = plan["num_decode"]
+        sample_seq = plan["sample_seq"]
+        N = len(sample_seq)
+        temp, topk, topp, seeds, offs = self._sampling_arrays(seq_ids, sample_seq, N)
+        bucket = None
+        if nd == S == T and self.graphs:
+            bucket = next((b for b in sorted(self.graphs) if b >= nd), None)
+        if bucket is not None:
+            toks, lps = self._run_graph(plan, bucket, temp, topk, topp, seeds, offs)
+        else:
+            toks, lps = self._run_eager(plan, temp, topk, topp, seeds, offs)
+        finished = self.sched.update(toks[:N])
+        dt = time.perf_counter() - t0
+        st = self.stats
+        st["steps"] += 1
+        st["step_time_s"] += dt
+        st["decode_steps"] += int(nd == S)
+        st["graph_steps"] += int(bucket is not None)
+        st["prefill_tokens"] += plan["num_prefill_tokens"]
+        st["generated_tokens"] += N
+        fin = {rid: FINISH_REASONS.get(r, "stop") for rid, r in finished}
+        evs = []
+        now = time.time()
+        for i in range(N):
+            rid = int(seq_ids[sample_seq[i]])
+            req = self._reqs.get(rid)
+            if req is None:
+                continue
+            if req.num_generated == 0:
+                req.first_token_at = now
+            req.num_generated += 1
+            reason = fin.get(rid)
+            if reason is not None:
+                req.finished = True
+                self._reqs.pop(rid, None)
+                st["finished"] += 1
+            evs.append(TokenEvent(req, int(toks[i]), float(lps[i]), reason))
+        if evs and self.event_sink:
+            self.event_sink(evs)
+        return True
+
+    def _run_eager(self, plan, temp, topk, topp, seeds, offs):
+        T = plan["num_tokens"]
+        S = len(plan["seq_ids"])
+        mb = plan["max_blocks"]
+        rows = plan["sample_rows"].astype(np.int64)
+        d = self.packer.pack([
+            ("ids", plan["input_ids"]), ("pos", plan["positions"]), ("slots", plan["slots"]),
+            ("ctx", plan["context_lens"]), ("cu", plan["cu_q"]),
+            ("bt", plan["block_tables"].reshape(S, mb)),
+            ("tiles", plan["prefill_tiles"] if len(plan["prefill_tiles"]) else
+             np.zeros(2, np.int32)),
+            ("rows", rows), ("temp", temp), ("topk", topk), ("topp", topp), ("seeds", seeds),
+            ("offs", offs)])
+        inp = StepInputs(d["ids"], d["pos"], d["slots"], plan["num_decode"], d["bt"], d["ctx"],
+                         d["cu"], d["tiles"], d["rows"], T, S)
+        ws = self.decode_ws
+        logits = self.model.forward(inp, self.k_caches, self.v_caches, ws, self.ecfg.part_tokens)
+        tok, lp = ops.sample(logits, d["temp"], d["topk"], d["topp"], d["seeds"], d["offs"])
+        return self._fetch(tok, lp)
+
+    def _run_graph(self, plan, B, temp, topk, topp, seeds, offs):
+        g, h = self._gbuf, self._gmeta.h
+        n = len(plan["seq_ids"])
+        mb = plan["max_blocks"]
+        # rows n..B-1 are padding: no cache write (slot -1), a 1-token context
+        for k, a, fill in (("ids", plan["input_ids"], 0), ("pos", plan["positions"], 0),
+                           ("slots", plan["slots"], -1), ("ctx", plan["context_lens"], 1),
+                           ("temp", temp, 0), ("topk", topk, 0), ("topp", topp, 1),
+                           ("seeds", seeds, 0), ("offs", offs, 0)):
+            h[k][:n] = a
+            h[k][n:B] = fill
+        h["bt"][:n] = plan["block_tables"].reshape(n, mb)
+        h["bt"][n:B] = 0
+        self._gmeta.upload()
+        self.graphs[B]["graph"].replay()
+        return self._fetch(g["tok"][:B], g["lp"][:B])
+
+    def _fetch(self, tok: torch.Tensor, lp: torch.Tensor):
+        if tok.is_cuda:
+            both = torch.cat([tok.view(torch.float32), lp]).cpu()
+            n = tok.numel()
+            return both[:n].view(torch.int32).numpy(), both[n:].numpy()
+        return tok.numpy(), lp.numpy()
+
+    # ----------------------------------------------------- offline helper ---
+    def generate(self, prompts: list[list[int]], params: SamplingParams,
+                 timeout: float = 600.0) -> list[list[int]]:
+        """Blocking batch generation (smoke tests, offline use); must not be
+        mixed with a running engine thread."""
+        outs: dict[int, list[int]] = {}
+        done: set[int] = set()
+        prev_sink = self.event_sink
+
+        def sink(evs):
+            for e in evs:
+                if e.token >= 0:
+                    outs.setdefault(e.req.id, []).append(e.token)
+                if e.finish is not None:
+                    done.add(e.req.id)
+
+        self.event_sink = sink
+        try:
+            reqs = [self.submit(GenRequest(list(p), params)) for p in prompts]
+            t_end = time.time() + timeout
+            while len(done) < len(reqs):
+                if not self.step() and time.time() > t_end:
+                    raise TimeoutError("generate timed out")
+                if time.time() > t_end:
+                    raise TimeoutError("generate timed out")
+        finally:
+            self.event_sink = prev_sink
+        return [outs.get(r.id, []) for r in reqs]

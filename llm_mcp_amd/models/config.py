@@ -1,0 +1,163 @@
+"""Model architecture configs (public HF config.json values) and the local
+model registry entries derived from them.
+
+The reference infers tier / thinking / context / kind from model *names*
+(core/internal/discovery/discovery.go:482-649).  Here they are derived from the
+architecture itself (`params_b`, `context_k`, `kind`), and the name heuristics
+are kept only for foreign names (policy/inference.py)."""
+from __future__ import annotations
+
+import json
+from dataclasses import asdict, dataclass, field
+from pathlib import Path
+
+
+@dataclass
+class LlamaConfig:
+    name: str = "llama-3-8b"
+    vocab_size: int = 128256
+    hidden_size: int = 4096
+    intermediate_size: int = 14336
+    num_layers: int = 32
+    num_heads: int = 32
+    num_kv_heads: int = 8
+    head_dim: int = 128
+    rope_theta: float = 500000.0
+    rope_scaling: dict | None = None
+    rms_eps: float = 1e-5
+    max_position: int = 8192
+    tie_embeddings: bool = False
+    bos_token_id: int = 128000
+    eos_token_ids: tuple = (128001, 128009)
+    family: str = "llama"
+    kind: str = "chat"
+
+    @property
+    def params(self) -> int:
+        d, I, L, V = self.hidden_size, self.intermediate_size, self.num_layers, self.vocab_size
+        qkv = d * (self.num_heads + 2 * self.num_kv_heads) * self.head_dim
+        o = self.num_heads * self.head_dim * d
+        mlp = 3 * d * I
+        emb = V * d * (1 if self.tie_embeddings else 2)
+        return L * (qkv + o + mlp + 2 * d) + emb + d
+
+    @property
+    def params_b(self) -> float:
+        return round(self.params / 1e9, 2)
+
+    @property
+    def context_k(self) -> int:
+        return self.max_position // 1024
+
+    def kv_bytes_per_token(self, tp: int = 1, dtype_bytes: int = 2) -> int:
+        kvh = max(1, self.num_kv_heads // tp)
+        return self.num_layers * 2 * kvh * self.head_dim * dtype_bytes
+
+    def to_dict(self) -> dict:
+        return asdict(self)
+
+
+@dataclass
+class NomicBertConfig:
+    """nomic-embed-text(-v1.5): post-norm BERT with rotary, SwiGLU, mean pool."""
+    name: str = "nomic-embed-text"
+    vocab_size: int = 30528
+    hidden_size: int = 768
+    intermediate_size: int = 3072
+    num_layers: int = 12
+    num_heads: int = 12
+    head_dim: int = 64
+    rope_theta: float = 1000.0
+    ln_eps: float = 1e-12
+    max_position: int = 8192
+    type_vocab_size: int = 2
+    qkv_bias: bool = False
+    mlp_bias: bool = False
+    family: str = "nomic-bert"
+    kind: str = "embed"
+    embed_dim: int = 768
+
+    @property
+    def params(self) -> int:
+        d, I, L = self.hidden_size, self.intermediate_size, self.num_layers
+        return L * (4 * d * d + 3 * d * I + 4 * d) + (self.vocab_size + self.type_vocab_size) * d
+
+    @property
+    def params_b(self) -> float:
+        return round(self.params / 1e9, 3)
+
+    @property
+    def context_k(self) -> int:
+        return self.max_position // 1024
+
+    def to_dict(self) -> dict:
+        return asdict(self)
+
+
+PRESETS: dict[str, object] = {
+    "llama-3-8b": LlamaConfig(),
+    "llama-3-70b": LlamaConfig(name="llama-3-70b", hidden_size=8192, intermediate_size=28672,
+                               num_layers=80, num_heads=64, num_kv_heads=8),
+    "llama-3.1-8b": LlamaConfig(name="llama-3.1-8b", max_position=131072,
+                                rope_scaling={"rope_type": "llama3", "factor": 8.0,
+                                              "low_freq_factor": 1.0, "high_freq_factor": 4.0,
+                                              "original_max_position_embeddings": 8192}),
+    "llama-3.2-1b": LlamaConfig(name="llama-3.2-1b", hidden_size=2048, intermediate_size=8192,
+                                num_layers=16, num_heads=32, num_kv_heads=8, head_dim=64,
+                                tie_embeddings=True, max_position=131072),
+    # tiny configs for tests / smoke (same code paths, D = 128 heads)
+    "tiny-llama": LlamaConfig(name="tiny-llama", vocab_size=512, hidden_size=256,
+                              intermediate_size=512, num_layers=2, num_heads=4, num_kv_heads=2,
+                              head_dim=128, max_position=2048, bos_token_id=506,
+                              eos_token_ids=(510,)),
+    "nomic-embed-text": NomicBertConfig(),
+    "tiny-nomic": NomicBertConfig(name="tiny-nomic", vocab_size=512, hidden_size=256,
+                                  intermediate_size=512, num_layers=2, num_heads=2, head_dim=128,
+                                  embed_dim=256, max_position=2048),
+}
+
+# OpenAI-style aliases (Ollama tags used by the reference's defaults)
+ALIASES = {
+    "llama3": "llama-3-8b", "llama3:8b": "llama-3-8b", "llama-3-8b-instruct": "llama-3-8b",
+    "meta-llama-3-8b": "llama-3-8b", "llama3:70b": "llama-3-70b",
+    "llama3.2:1b": "llama-3.2-1b", "nomic-embed-text:latest": "nomic-embed-text",
+    "nomic-embed-text-v1.5": "nomic-embed-text",
+}
+
+
+def resolve(name: str):
+    key = ALIASES.get(name, name)
+    if key not in PRESETS:
+        raise KeyError(f"unknown model {name!r}; known: {sorted(PRESETS)}")
+    return PRESETS[key]
+
+
+def from_hf_config(path: str | Path):
+    """Build a config from a HF config.json (local file; no network)."""
+    cfg = json.loads(Path(path).read_text())
+    arch = (cfg.get("architectures") or [""])[0]
+    if "Llama" in arch:
+        return LlamaConfig(
+            name=cfg.get("_name_or_path", "llama"), vocab_size=cfg["vocab_size"],
+            hidden_size=cfg["hidden_size"], intermediate_size=cfg["intermediate_size"],
+            num_layers=cfg["num_hidden_layers"], num_heads=cfg["num_attention_heads"],
+            num_kv_heads=cfg.get("num_key_value_heads", cfg["num_attention_heads"]),
+            head_dim=cfg.get("head_dim", cfg["hidden_size"] // cfg["num_attention_heads"]),
+            rope_theta=cfg.get("rope_theta", 10000.0), rope_scaling=cfg.get("rope_scaling"),
+            rms_eps=cfg.get("rms_norm_eps", 1e-5),
+            max_position=cfg.get("max_position_embeddings", 8192),
+            tie_embeddings=cfg.get("tie_word_embeddings", False),
+            bos_token_id=cfg.get("bos_token_id", 128000),
+            eos_token_ids=tuple(cfg["eos_token_id"]) if isinstance(cfg.get("eos_token_id"), list)
+            else (cfg.get("eos_token_id", 128001),))
+    if "NomicBert" in arch or cfg.get("model_type") == "nomic_bert":
+        return NomicBertConfig(
+            vocab_size=cfg["vocab_size"], hidden_size=cfg["n_embd"],
+            intermediate_size=cfg["n_inner"], num_layers=cfg["n_layer"],
+            num_heads=cfg["n_head"], head_dim=cfg["n_embd"] // cfg["n_head"],
+            rope_theta=cfg.get("rotary_emb_base", 1000.0),
+            ln_eps=cfg.get("layer_norm_epsilon", 1e-12),
+            max_position=cfg.get("n_positions", 8192),
+            qkv_bias=cfg.get("qkv_proj_bias", False), mlp_bias=cfg.get("mlp_fc1_bias", False),
+            embed_dim=cfg["n_embd"])
+    raise ValueError(f"unsupported architecture {arch!r}")

@@ -1,0 +1,176 @@
+"""Llama-3 family decoder (8B / 70B / 3.x) for the in-process serving engine.
+
+What the reference delegates to Ollama's /api/generate and /api/chat
+(worker/llm_worker/main.py:222-243, core/internal/api/handlers.go:2308-2587)
+runs here, on the GPU the worker owns:
+
+  embed_gather (K10) -> per layer:
+      rms_norm(+residual, K1) -> QKV GEMM (hipBLASLt) -> rope_and_cache (K2+K5)
+      -> paged attention: decode rows (K4) / prefill rows (K3)
+      -> O GEMM [+ RCCL all-reduce under TP] -> rms_norm(+residual)
+      -> gate|up GEMM -> silu_mul (K8) -> down GEMM [+ all-reduce]
+  -> final rms_norm on the sampled rows only -> LM head -> sampling (K6).
+
+Weights are fused per layer (QKV, gate|up) so each step issues 4 GEMMs per
+layer.  Tensor parallelism (Megatron column/row split) is built in: QKV and
+gate|up are split by heads / intermediate columns, O and down by rows, with
+one all-reduce after each (X1, X2); the LM head is vocab-split and gathered
+(X3).  Embeddings are replicated -- on a 288 GB part their memory is cheaper
+than an extra collective per step.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+import torch.nn.functional as F
+
+from .. import ops
+from ..ops import ref
+from .config import LlamaConfig
+
+
+@dataclass
+class StepInputs:
+    """Device tensors of one engine step (built from the scheduler's plan)."""
+    input_ids: torch.Tensor       # int32 [T]
+    positions: torch.Tensor       # int32 [T]
+    slots: torch.Tensor           # int32 [T]
+    num_decode: int               # first num_decode rows are decode rows (1 per seq)
+    block_tables: torch.Tensor    # int32 [S, max_blocks]
+    context_lens: torch.Tensor    # int32 [S]
+    cu_q: torch.Tensor            # int32 [S+1] (absolute token rows)
+    prefill_tiles: torch.Tensor   # int32 [2 * n_tiles] (prefill-seq index, q_start)
+    sample_rows: torch.Tensor     # int64 [N] token rows whose logits are needed
+    num_tokens: int
+    num_seqs: int
+
+
+class TPContext:
+    """Tensor-parallel placement of this rank (size 1 = no TP)."""
+
+    def __init__(self, rank: int = 0, size: int = 1, group=None):
+        self.rank, self.size, self.group = rank, size, group
+
+    def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
+        if self.size > 1:
+            torch.distributed.all_reduce(t, group=self.group)
+        return t
+
+    def all_gather_last(self, t: torch.Tensor) -> torch.Tensor:
+        if self.size == 1:
+            return t
+        parts = [torch.empty_like(t) for _ in range(self.size)]
+        torch.distributed.all_gather(parts, t.contiguous(), group=self.group)
+        return torch.cat(parts, dim=-1)
+
+
+class LlamaModel:
+    def __init__(self, cfg: LlamaConfig, device: torch.device | str = "cuda",
+                 dtype=torch.bfloat16, tp: TPContext | None = None, seed: int = 0,
+                 weights: dict | None = None):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.dtype = dtype
+        self.tp = tp or TPContext()
+        T = self.tp.size
+        if cfg.num_heads % T or cfg.intermediate_size % T:
+            raise ValueError("TP size must divide heads and intermediate size")
+        self.Hq = cfg.num_heads // T
+        self.Hkv = max(1, cfg.num_kv_heads // T)
+        if cfg.num_kv_heads % T and T % cfg.num_kv_heads:
+            raise ValueError("TP size incompatible with kv heads")
+        self.kv_replicas = max(1, T // cfg.num_kv_heads)
+        self.D = cfg.head_dim
+        self.I = cfg.intermediate_size // T
+        self.vocab_shard = (cfg.vocab_size + T - 1) // T
+        self.scale = 1.0 / math.sqrt(self.D)
+        self.cos_sin = ref.rope_cos_sin(cfg.max_position, self.D, cfg.rope_theta, self.device,
+                                        cfg.rope_scaling)
+        if weights is None:
+            weights = self._random_weights(seed)
+        self.w = weights
+
+    # ----------------------------------------------------------- weights ----
+    def _random_weights(self, seed: int) -> dict:
+        """Deterministic random init of this rank's shard (synthetic benchmark
+        weights; std 0.02 keeps activations finite through 80 layers)."""
+        cfg, dev, dt = self.cfg, self.device, self.dtype
+        g = torch.Generator(device=dev)
+        g.manual_seed(seed * 1000 + self.tp.rank)
+        d = cfg.hidden_size
+
+        def rnd(*shape, std=0.02):
+            t = torch.empty(shape, dtype=dt, device=dev)
+            t.normal_(0.0, std, generator=g)
+            return t
+
+        layers = []
+        qkv_rows = (self.Hq + 2 * self.Hkv) * self.D
+        for _ in range(cfg.num_layers):
+            layers.append({
+                "ln1": torch.ones(d, dtype=dt, device=dev),
+                "ln2": torch.ones(d, dtype=dt, device=dev),
+                "wqkv": rnd(qkv_rows, d),
+                "wo": rnd(d, self.Hq * self.D, std=0.02 / math.sqrt(2 * cfg.num_layers)),
+                "w_gate_up": rnd(2 * self.I, d),
+                "w_down": rnd(d, self.I, std=0.02 / math.sqrt(2 * cfg.num_layers)),
+            })
+        embed = rnd(cfg.vocab_size, d, std=1.0)
+        lm_head = embed[self.tp.rank * self.vocab_shard:(self.tp.rank + 1) * self.vocab_shard] \
+            if cfg.tie_embeddings else rnd(min(self.vocab_shard, cfg.vocab_size), d)
+        return {"embed": embed, "norm": torch.ones(d, dtype=dt, device=dev), "lm_head": lm_head,
+                "layers": layers}
+
+    def weight_bytes(self) -> int:
+        n = 0
+        for k, v in self.w.items():
+            if k == "layers":
+                for l in v:
+                    n += sum(t.numel() * t.element_size() for t in l.values())
+            else:
+                n += v.numel() * v.element_size()
+        return n
+
+    # ----------------------------------------------------------- forward ----
+    def forward(self, inp: StepInputs, k_caches: list, v_caches: list,
+                decode_ws: ops.DecodeWorkspace | None, part_tokens: int = 512) -> torch.Tensor:
+        """Returns logits [len(sample_rows), vocab] (bf16)."""
+        cfg, w = self.cfg, self.w
+        Hq, Hkv, D = self.Hq, self.Hkv, self.D
+        T, nd = inp.num_tokens, inp.num_decode
+        x = ops.embed_gather(w["embed"], inp.input_ids)
+        residual = None
+        attn = torch.empty((T, Hq * D), dtype=self.dtype, device=self.device)
+        for li, L in enumerate(w["layers"]):
+            if residual is None:
+                residual = x
+                h = ops.rms_norm(x, L["ln1"], cfg.rms_eps)
+            else:
+                h = ops.rms_norm(x, L["ln1"], cfg.rms_eps, residual=residual)
+            qkv = F.linear(h, L["wqkv"])
+            kc, vc = k_caches[li], v_caches[li]
+            ops.rope_and_cache(qkv, inp.positions, self.cos_sin, Hq, Hkv, D, inp.slots, kc, vc)
+            if nd > 0:
+                ops.paged_decode_attention(qkv[:nd], kc, vc, inp.block_tables,
+                                           inp.context_lens, self.scale, attn[:nd], decode_ws,
+                                           part_tokens, Hq=Hq)
+            if T > nd:
+                ops.paged_prefill_attention(qkv, kc, vc, inp.block_tables[nd:],
+                                            inp.cu_q[nd:], inp.context_lens[nd:],
+                                            inp.prefill_tiles, self.scale, attn, Hq=Hq)
+            o = self.tp.all_reduce(F.linear(attn, L["wo"]))
+            h = ops.rms_norm(o, L["ln2"], cfg.rms_eps, residual=residual)
+            gu = F.linear(h, L["w_gate_up"])
+            a = ops.silu_mul(gu)
+            x = self.tp.all_reduce(F.linear(a, L["w_down"]))
+        # final norm only on the rows we sample from
+        rows = inp.sample_rows
+        xs = x.index_select(0, rows)
+        rs = residual.index_select(0, rows)
+        hs = ops.rms_norm(xs, w["norm"], cfg.rms_eps, residual=rs)
+        logits = F.linear(hs, w["lm_head"])
+        if self.tp.size > 1:
+            logits = self.tp.all_gather_last(logits)[:, :cfg.vocab_size]
+        return logits

@@ -1,0 +1,322 @@
+"""Device ops of llm_mcp_amd.
+
+Every op dispatches on the tensor's device:
+  * GPU (ROCm/HIP) tensors -> the hand-written gfx950 kernels in
+    ``_lmx_kernels`` (csrc/kernels/*.hip).  If that extension is missing on a
+    GPU host the op raises -- there is no silent eager fallback.
+  * CPU tensors -> the PyTorch reference in ``ops.ref`` (tests and the CPU
+    plumbing configuration).
+
+Shapes, dtypes, contiguity and strides are validated here, on the host,
+before any launch, so a kernel never runs on operands that disagree with its
+grid assumptions.
+"""
+from __future__ import annotations
+
+import importlib
+
+import torch
+
+from . import ref
+
+_K = None
+_K_ERR: Exception | None = None
+
+
+def native():
+    """The loaded kernel extension (raises with the build hint if absent)."""
+    global _K, _K_ERR
+    if _K is None and _K_ERR is None:
+        try:
+            _K = importlib.import_module("llm_mcp_amd._lmx_kernels")
+        except Exception as e:  # pragma: no cover - depends on the build
+            _K_ERR = e
+    if _K is None:
+        raise RuntimeError(
+            "llm_mcp_amd HIP kernels are not built (python -m llm_mcp_amd.build): "
+            f"{_K_ERR}")
+    return _K
+
+
+def native_available() -> bool:
+    try:
+        native()
+        return True
+    except RuntimeError:
+        return False
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _ptr(t: torch.Tensor | None) -> int:
+    return 0 if t is None else t.data_ptr()
+
+
+def _chk(cond: bool, msg: str) -> None:
+    if not cond:
+        raise ValueError(msg)
+
+
+def _bf16(t: torch.Tensor, name: str) -> None:
+    _chk(t.dtype == torch.bfloat16, f"{name} must be bfloat16, got {t.dtype}")
+
+
+# ------------------------------------------------------------------ norms ---
+def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float,
+             residual: torch.Tensor | None = None,
+             out: torch.Tensor | None = None) -> torch.Tensor:
+    """y = rmsnorm(x [+ residual]) * w.  With ``residual`` the sum is written
+    back into ``residual`` (fused residual add).  ``x`` may be row-strided."""
+    if not x.is_cuda:
+        y = ref.rms_norm(x, w, eps, residual)
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
+    _bf16(x, "x"); _bf16(w, "w")
+    rows, cols = x.shape
+    _chk(x.stride(1) == 1 and w.numel() == cols and cols % 8 == 0, "rms_norm shape/stride")
+    if residual is not None:
+        _chk(residual.is_contiguous() and residual.shape == (rows, cols), "residual shape")
+    if out is None:
+        out = torch.empty((rows, cols), dtype=x.dtype, device=x.device)
+    native().rmsnorm(_ptr(out), _ptr(residual), _ptr(x), _ptr(w), rows, cols, x.stride(0),
+                     out.stride(0), float(eps), _stream())
+    return out
+
+
+def layer_norm(x, w, b, eps, residual=None):
+    if not x.is_cuda:
+        return ref.layer_norm(x, w, b, eps, residual)
+    _bf16(x, "x")
+    rows, cols = x.shape
+    _chk(x.is_contiguous() and cols % 8 == 0, "layer_norm shape")
+    out = torch.empty_like(x)
+    native().layernorm(_ptr(out), _ptr(x), _ptr(residual), _ptr(w), _ptr(b), rows, cols,
+                       float(eps), _stream())
+    return out
+
+
+# ------------------------------------------------------- rope / kv cache ----
+def rope_and_cache(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Tensor,
+                   Hq: int, Hkv: int, D: int, slots: torch.Tensor | None,
+                   k_cache: torch.Tensor | None, v_cache: torch.Tensor | None,
+                   rotate_k_inplace: bool = False) -> None:
+    """In-place rotary on q (and k) heads of the fused QKV rows; k and v are
+    scattered into the paged cache at ``slots`` (-1 = skip)."""
+    if not qkv.is_cuda:
+        ref.rope_cache(qkv, positions, cos_sin, Hq, Hkv, D, slots, k_cache, v_cache,
+                       rotate_k_inplace)
+        return
+    _bf16(qkv, "qkv")
+    T = qkv.shape[0]
+    _chk(qkv.stride(1) == 1 and qkv.shape[1] >= (Hq + 2 * Hkv) * D, "qkv shape")
+    _chk(positions.dtype == torch.int32 and positions.numel() >= T, "positions int32[T]")
+    _chk(cos_sin.dtype == torch.float32 and cos_sin.shape[1] == D, "cos_sin [P, D] fp32")
+    BS = 0
+    if k_cache is not None:
+        _chk(slots is not None and slots.dtype == torch.int32, "slots int32")
+        _chk(k_cache.shape[1] == Hkv and k_cache.shape[3] == D and v_cache.shape[2] == D,
+             "cache layout [NB,Hkv,BS,D] / [NB,Hkv,D,BS]")
+        BS = k_cache.shape[2]
+    native().rope_cache(_ptr(qkv), qkv.stride(0), _ptr(positions), _ptr(cos_sin), T, Hq, Hkv, D,
+                        _ptr(slots), _ptr(k_cache), _ptr(v_cache), BS,
+                        int(rotate_k_inplace), _stream())
+
+
+def kv_write(k, v, slots, k_cache, v_cache):
+    if not k.is_cuda:
+        ref.write_cache(k, v, slots, k_cache, v_cache)
+        return
+    T, Hkv, D = k.shape
+    _chk(k.stride(2) == 1 and k.stride(1) == D and v.stride(0) == k.stride(0), "k/v layout")
+    native().kv_write(_ptr(k), _ptr(v), k.stride(0), _ptr(slots), T, Hkv, D, _ptr(k_cache),
+                      _ptr(v_cache), k_cache.shape[2], _stream())
+
+
+# --------------------------------------------------------------- attention ---
+class DecodeWorkspace:
+    """Split-K scratch of the paged decode kernel, sized once (graph-safe)."""
+
+    def __init__(self, max_batch: int, Hq: int, D: int, max_parts: int, device):
+        self.max_parts = max_parts
+        self.part_o = torch.empty((max_batch, Hq, max_parts, D), dtype=torch.float32,
+                                  device=device)
+        self.part_ml = torch.empty((max_batch, Hq, max_parts, 2), dtype=torch.float32,
+                                   device=device)
+
+
+def paged_decode_attention(q: torch.Tensor, k_cache, v_cache, block_tables, context_lens,
+                           scale: float, out: torch.Tensor, ws: DecodeWorkspace | None = None,
+                           part_tokens: int = 512, Hq: int | None = None) -> torch.Tensor:
+    """q: [B, Hq*D] rows (row stride = q.stride(0)); out: [B, Hq*D]."""
+    B = q.shape[0]
+    NB, Hkv, BS, D = k_cache.shape
+    Hq = Hq or (q.shape[1] // D)
+    if not q.is_cuda:
+        o = ref.paged_decode(q[:, : Hq * D].reshape(B, Hq, D), k_cache, v_cache, block_tables,
+                             context_lens, scale)
+        out.copy_(o.reshape(B, Hq * D))
+        return out
+    _bf16(q, "q")
+    _chk(D in (64, 128) and BS == 32, "paged decode kernel needs D in (64,128), BS=32")
+    _chk(Hq % Hkv == 0 and Hq // Hkv <= 16, "GQA group must be <= 16")
+    _chk(block_tables.dtype == torch.int32 and context_lens.dtype == torch.int32, "int32 meta")
+    _chk(block_tables.shape[0] >= B and context_lens.numel() >= B, "meta rows")
+    _chk(part_tokens % 128 == 0, "part_tokens % 128")
+    max_parts = ws.max_parts if ws is not None else 1
+    native().paged_decode(_ptr(q), q.stride(0), _ptr(k_cache), _ptr(v_cache), _ptr(block_tables),
+                          block_tables.stride(0), _ptr(context_lens), _ptr(out), out.stride(0),
+                          _ptr(ws.part_o) if ws else 0, _ptr(ws.part_ml) if ws else 0, B, Hq, Hkv,
+                          D, BS, float(scale), part_tokens, max_parts, _stream())
+    return out
+
+
+def paged_prefill_attention(q: torch.Tensor, k_cache, v_cache, block_tables, cu_q,
+                            context_lens, tiles, scale: float, out: torch.Tensor,
+                            causal: bool = True, Hq: int | None = None) -> torch.Tensor:
+    """Varlen prefill. q/out: [T, Hq*D] rows; tiles: int32 [(seq, q_start)]
+    built with q_per_tile = 64 / G (see ``prefill_q_per_tile``)."""
+    NB, Hkv, BS, D = k_cache.shape
+    T = q.shape[0]
+    Hq = Hq or (q.shape[1] // D)
+    if not q.is_cuda:
+        o = ref.paged_prefill(q[:, : Hq * D].reshape(T, Hq, D), k_cache, v_cache, block_tables,
+                              cu_q, context_lens, scale, causal)
+        a, b = int(cu_q[0]), int(cu_q[len(context_lens)])
+        out[a:b].copy_(o.reshape(T, Hq * D)[a:b])
+        return out
+    _bf16(q, "q")
+    _chk(D in (64, 128) and BS == 32, "paged prefill kernel needs D in (64,128), BS=32")
+    _chk(Hq % Hkv == 0 and 16 % (Hq // Hkv) == 0, "GQA group must divide 16")
+    _chk(tiles.dtype == torch.int32 and cu_q.dtype == torch.int32, "int32 meta")
+    num_tiles = tiles.numel() // 2
+    native().paged_prefill(_ptr(q), q.stride(0), _ptr(k_cache), _ptr(v_cache),
+                           _ptr(block_tables), block_tables.stride(0), _ptr(cu_q),
+                           _ptr(context_lens), _ptr(tiles), num_tiles, _ptr(out), out.stride(0),
+                           Hq, Hkv, D, BS, float(scale), int(causal), _stream())
+    return out
+
+
+def prefill_q_per_tile(Hq: int, Hkv: int) -> int:
+    return 4 * (16 // (Hq // Hkv))
+
+
+# ---------------------------------------------------------------- sampling ---
+def sample(logits: torch.Tensor, temperature: torch.Tensor, top_k: torch.Tensor,
+           top_p: torch.Tensor, seeds: torch.Tensor, offsets: torch.Tensor,
+           out_tok: torch.Tensor | None = None, out_lp: torch.Tensor | None = None,
+           max_rounds: int = 32):
+    B, V = logits.shape
+    if not logits.is_cuda:
+        return ref.sample(logits, temperature, top_k, top_p, seeds, offsets)
+    _chk(logits.dtype in (torch.bfloat16, torch.float32) and logits.stride(1) == 1, "logits")
+    _chk(temperature.dtype == torch.float32 and top_p.dtype == torch.float32, "fp32 params")
+    _chk(top_k.dtype == torch.int32 and offsets.dtype == torch.int32, "int32 params")
+    _chk(seeds.dtype == torch.int64, "int64 seeds")
+    for t in (temperature, top_k, top_p, seeds, offsets):
+        _chk(t.numel() >= B and t.is_cuda, "sampling param rows")
+    if out_tok is None:
+        out_tok = torch.empty(B, dtype=torch.int32, device=logits.device)
+    if out_lp is None:
+        out_lp = torch.empty(B, dtype=torch.float32, device=logits.device)
+    native().sample(_ptr(logits), int(logits.dtype == torch.bfloat16), logits.stride(0), B, V,
+                    _ptr(temperature), _ptr(top_k), _ptr(top_p), _ptr(seeds), _ptr(offsets),
+                    _ptr(out_tok), _ptr(out_lp), max_rounds, _stream())
+    return out_tok, out_lp
+
+
+# ------------------------------------------------------------ elementwise ---
+def silu_mul(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    if not x.is_cuda:
+        y = ref.silu_mul(x)
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
+    _bf16(x, "x")
+    _chk(x.is_contiguous() and x.shape[-1] % 16 == 0, "silu_mul shape")
+    I = x.shape[-1] // 2
+    rows = x.numel() // x.shape[-1]
+    if out is None:
+        out = torch.empty(x.shape[:-1] + (I,), dtype=x.dtype, device=x.device)
+    native().glu(_ptr(out), _ptr(x), rows, I, 0, _stream())
+    return out
+
+
+def gelu_mul(x: torch.Tensor) -> torch.Tensor:
+    if not x.is_cuda:
+        return ref.gelu_mul(x)
+    _chk(x.is_contiguous() and x.shape[-1] % 16 == 0, "gelu_mul shape")
+    I = x.shape[-1] // 2
+    rows = x.numel() // x.shape[-1]
+    out = torch.empty(x.shape[:-1] + (I,), dtype=x.dtype, device=x.device)
+    native().glu(_ptr(out), _ptr(x), rows, I, 1, _stream())
+    return out
+
+
+def embed_gather(table: torch.Tensor, ids: torch.Tensor, vocab_start: int = 0,
+                 out: torch.Tensor | None = None) -> torch.Tensor:
+    """Rows of ``table`` (a vocab shard starting at vocab_start); ids outside
+    the shard give zero rows."""
+    rows, d = table.shape
+    if not table.is_cuda:
+        local = ids.long() - vocab_start
+        own = (local >= 0) & (local < rows)
+        y = table[local.clamp(0, rows - 1)] * own[:, None].to(table.dtype)
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
+    _chk(ids.dtype == torch.int32 and table.is_contiguous() and d % 8 == 0, "embed_gather")
+    T = ids.numel()
+    if out is None:
+        out = torch.empty((T, d), dtype=table.dtype, device=table.device)
+    native().embed_gather(_ptr(out), _ptr(table), _ptr(ids), T, d, vocab_start, rows, _stream())
+    return out
+
+
+def mean_pool_l2(h: torch.Tensor, cu: torch.Tensor, dims: int | None = None,
+                 normalize: bool = True) -> torch.Tensor:
+    T, d = h.shape
+    dims = dims or d
+    if not h.is_cuda:
+        return ref.mean_pool_l2(h, cu, dims, normalize)
+    _chk(h.is_contiguous() and d % 8 == 0 and 0 < dims <= d and cu.dtype == torch.int32,
+         "mean_pool_l2")
+    nseq = cu.numel() - 1
+    out = torch.empty((nseq, dims), dtype=torch.float32, device=h.device)
+    native().mean_pool_l2(_ptr(out), _ptr(h), _ptr(cu), nseq, d, dims, int(normalize), _stream())
+    return out
+
+
+ACT_NONE, ACT_GELU, ACT_SILU = 0, 1, 2
+
+
+def gemm_nt(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, act: int = 0,
+            residual: torch.Tensor | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
+    """act(a @ w^T + bias) (+ residual) on the hand-written MFMA GEMM."""
+    M, K = a.shape
+    N = w.shape[0]
+    if not a.is_cuda:
+        y = ref.gemm_nt(a, w, bias, act, residual)
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
+    _bf16(a, "a"); _bf16(w, "w")
+    _chk(w.shape[1] == K and a.stride(1) == 1 and w.stride(1) == 1, "gemm_nt shapes")
+    _chk(N % 128 == 0 and K % 64 == 0, "gemm_nt needs N % 128 == 0 and K % 64 == 0")
+    if out is None:
+        out = torch.empty((M, N), dtype=a.dtype, device=a.device)
+    if residual is not None:
+        _chk(residual.shape == (M, N) and residual.stride(0) == out.stride(0), "residual")
+    native().gemm_nt(_ptr(out), _ptr(a), _ptr(w), _ptr(bias), _ptr(residual), M, N, K,
+                     a.stride(0), w.stride(0), out.stride(0), act, _stream())
+    return out
+
+
+def gemm_nt_supported(N: int, K: int) -> bool:
+    return N % 128 == 0 and K % 64 == 0

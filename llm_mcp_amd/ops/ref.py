@@ -1,0 +1,218 @@
+"""Plain PyTorch (fp32-accumulating) reference implementations of every HIP
+kernel in ``csrc/kernels``.
+
+They serve two purposes:
+* numerics oracle for the kernel parity tests (``tests/test_kernels_gpu.py``);
+* the CPU execution path of the ops (tests, CPU-only plumbing configs).  A
+  CUDA/HIP tensor never takes this path: ``ops.kernels`` dispatches device
+  tensors to the native kernels and raises if the extension is missing.
+
+Cache layouts match the kernels: k_cache [NB, Hkv, BS, D], v_cache [NB, Hkv, D, BS].
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+
+def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float,
+             residual: torch.Tensor | None = None) -> torch.Tensor:
+    if residual is not None:
+        h = (x.float() + residual.float()).to(x.dtype)
+        residual.copy_(h)
+        x = h
+    xf = x.float()
+    y = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)
+    return (y * w.float()).to(x.dtype)
+
+
+def layer_norm(x, w, b, eps, residual=None):
+    if residual is not None:
+        x = (x.float() + residual.float()).to(x.dtype)
+    return torch.nn.functional.layer_norm(x.float(), (x.shape[-1],), w.float(), b.float(),
+                                          eps).to(x.dtype)
+
+
+def rope_cos_sin(max_pos: int, dim: int, theta: float, device=None,
+                 scaling: dict | None = None) -> torch.Tensor:
+    """[max_pos, dim] fp32 table: cos in [:, :dim/2], sin in [:, dim/2:]."""
+    inv = 1.0 / (theta ** (torch.arange(0, dim, 2, dtype=torch.float64) / dim))
+    if scaling and scaling.get("rope_type") == "llama3":
+        # Llama-3.1 frequency-dependent scaling
+        factor = scaling.get("factor", 8.0)
+        lo = scaling.get("low_freq_factor", 1.0)
+        hi = scaling.get("high_freq_factor", 4.0)
+        old = scaling.get("original_max_position_embeddings", 8192)
+        wavelen = 2 * math.pi / inv
+        lo_wl, hi_wl = old / lo, old / hi
+        smooth = (old / wavelen - lo) / (hi - lo)
+        scaled = torch.where(wavelen > lo_wl, inv / factor, inv)
+        mid = (wavelen <= lo_wl) & (wavelen >= hi_wl)
+        inv = torch.where(mid, (1 - smooth) * inv / factor + smooth * inv, scaled)
+    t = torch.arange(max_pos, dtype=torch.float64)
+    f = torch.outer(t, inv)
+    return torch.cat([f.cos(), f.sin()], dim=-1).float().to(device)
+
+
+def apply_rope(x: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Tensor) -> torch.Tensor:
+    """x [T, H, D] -> rotated (rotate-half form)."""
+    D = x.shape[-1]
+    cs = cos_sin[positions.long()]
+    cos, sin = cs[:, None, : D // 2], cs[:, None, D // 2:]
+    x1, x2 = x[..., : D // 2].float(), x[..., D // 2:].float()
+    return torch.cat([x1 * cos - x2 * sin, x2 * cos + x1 * sin], dim=-1).to(x.dtype)
+
+
+def rope_cache(qkv, positions, cos_sin, Hq, Hkv, D, slots, k_cache, v_cache, rotate_k_inplace):
+    T = qkv.shape[0]
+    v3 = qkv.view(T, -1, D)
+    q = apply_rope(v3[:, :Hq], positions, cos_sin)
+    k = apply_rope(v3[:, Hq:Hq + Hkv], positions, cos_sin)
+    v = v3[:, Hq + Hkv:Hq + 2 * Hkv]
+    v3[:, :Hq] = q
+    if rotate_k_inplace or k_cache is None:
+        v3[:, Hq:Hq + Hkv] = k
+    if k_cache is not None and slots is not None:
+        write_cache(k, v, slots, k_cache, v_cache)
+
+
+def write_cache(k, v, slots, k_cache, v_cache):
+    BS = k_cache.shape[2]
+    s = slots.long()
+    keep = s >= 0
+    s, k, v = s[keep], k[keep], v[keep]
+    blk, off = s // BS, s % BS
+    k_cache[blk, :, off, :] = k.to(k_cache.dtype)
+    v_cache[blk, :, :, off] = v.to(v_cache.dtype)
+
+
+def gather_kv(k_cache, v_cache, block_table, n):
+    """Dense K, V [n, Hkv, D] of one sequence from the paged cache."""
+    BS = k_cache.shape[2]
+    idx = torch.arange(n, device=k_cache.device)
+    blk = block_table.long()[idx // BS]
+    off = idx % BS
+    k = k_cache[blk, :, off, :]           # [n, Hkv, D]
+    v = v_cache[blk, :, :, off]           # [n, Hkv, D]
+    return k, v
+
+
+def attention_dense(q, k, v, scale, causal_offset: int | None):
+    """q [Tq, Hq, D], k/v [Tk, Hkv, D]; query i sees keys <= causal_offset + i."""
+    Hq, Hkv = q.shape[1], k.shape[1]
+    G = Hq // Hkv
+    kf = k.float().repeat_interleave(G, dim=1)
+    vf = v.float().repeat_interleave(G, dim=1)
+    s = torch.einsum("qhd,khd->hqk", q.float(), kf) * scale
+    if causal_offset is not None:
+        Tq, Tk = q.shape[0], k.shape[0]
+        qi = torch.arange(Tq, device=q.device)[:, None] + causal_offset
+        ki = torch.arange(Tk, device=q.device)[None, :]
+        s = s.masked_fill((ki > qi)[None], float("-inf"))
+    p = torch.softmax(s, dim=-1)
+    return torch.einsum("hqk,khd->qhd", p, vf)
+
+
+def paged_decode(q, k_cache, v_cache, block_tables, context_lens, scale):
+    """q [B, Hq, D] -> [B, Hq, D] (one query per sequence at position ctx-1)."""
+    out = torch.empty_like(q)
+    for b in range(q.shape[0]):
+        n = int(context_lens[b])
+        k, v = gather_kv(k_cache, v_cache, block_tables[b], n)
+        out[b] = attention_dense(q[b:b + 1], k, v, scale, None)[0].to(q.dtype)
+    return out
+
+
+def paged_prefill(q, k_cache, v_cache, block_tables, cu_q, context_lens, scale, causal=True):
+    """q [T, Hq, D] for a varlen batch; keys come from the paged cache."""
+    out = torch.empty_like(q)
+    for s in range(len(context_lens)):
+        a, b = int(cu_q[s]), int(cu_q[s + 1])
+        n = int(context_lens[s])
+        k, v = gather_kv(k_cache, v_cache, block_tables[s], n)
+        off = (n - (b - a)) if causal else None
+        out[a:b] = attention_dense(q[a:b], k, v, scale, off).to(q.dtype)
+    return out
+
+
+def silu_mul(x: torch.Tensor) -> torch.Tensor:
+    I = x.shape[-1] // 2
+    g, u = x[..., :I].float(), x[..., I:].float()
+    return (torch.nn.functional.silu(g) * u).to(x.dtype)
+
+
+def gelu_mul(x: torch.Tensor) -> torch.Tensor:
+    I = x.shape[-1] // 2
+    g, u = x[..., :I].float(), x[..., I:].float()
+    return (torch.nn.functional.gelu(g, approximate="tanh") * u).to(x.dtype)
+
+
+def mean_pool_l2(h, cu, dims, normalize=True):
+    outs = []
+    for s in range(len(cu) - 1):
+        a, b = int(cu[s]), int(cu[s + 1])
+        m = h[a:b].float().mean(0)[:dims]
+        if normalize:
+            m = m / m.norm().clamp_min(1e-12)
+        outs.append(m)
+    return torch.stack(outs)
+
+
+def gemm_nt(a, w, bias=None, act=0, residual=None):
+    y = a.float() @ w.float().t()
+    if bias is not None:
+        y = y + bias.float()
+    if act == 1:
+        y = torch.nn.functional.gelu(y, approximate="tanh")
+    elif act == 2:
+        y = torch.nn.functional.silu(y)
+    if residual is not None:
+        y = y + residual.float()
+    return y.to(a.dtype)
+
+
+def _uniform(seed: int, off: int, idx: torch.Tensor) -> torch.Tensor:
+    # host-side mirror of the kernel's counter-based hash is not needed for the
+    # CPU path; a seeded torch generator gives the same *distribution*.
+    g = torch.Generator().manual_seed((seed * 1000003 + off) & 0x7FFFFFFFFFFFFFFF)
+    return torch.rand(idx.shape, generator=g)
+
+
+def sample(logits, temperature, top_k, top_p, seeds, offsets):
+    """Greedy when temperature <= 0, else softmax(logits / T) truncated by
+    top-k / top-p.  Returns (tokens int32 [B], logprobs fp32 [B])."""
+    B, V = logits.shape
+    toks = torch.empty(B, dtype=torch.int32)
+    lps = torch.empty(B, dtype=torch.float32)
+    for b in range(B):
+        x = logits[b].float().cpu()
+        t = float(temperature[b])
+        k = int(top_k[b]) if top_k is not None else 0
+        if t <= 0 or k == 1:
+            j = int(torch.argmax(x))
+            toks[b] = j
+            lps[b] = float(torch.log_softmax(x, -1)[j])
+            continue
+        z = x / t
+        logp = torch.log_softmax(z, -1)
+        p = logp.exp()
+        keep = torch.ones(V, dtype=torch.bool)
+        if k > 0 and k < V:
+            kth = torch.topk(z, k).values[-1]
+            keep &= z >= kth
+        tp = float(top_p[b]) if top_p is not None else 1.0
+        if tp < 1.0:
+            sp, si = torch.sort(p, descending=True)
+            above = torch.cumsum(sp, 0) - sp
+            nucleus = torch.zeros(V, dtype=torch.bool)
+            nucleus[si[above < tp]] = True
+            keep &= nucleus
+        pk = torch.where(keep, p, torch.zeros_like(p))
+        u = _uniform(int(seeds[b]) if seeds is not None else 0,
+                     int(offsets[b]) if offsets is not None else 0, torch.zeros(1))
+        c = torch.cumsum(pk / pk.sum(), 0)
+        j = int(torch.searchsorted(c, u.clamp(max=float(c[-1]) - 1e-7)))
+        toks[b] = j
+        lps[b] = float(logp[j])
+    return toks, lps

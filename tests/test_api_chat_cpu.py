@@ -1,0 +1,102 @@
+"""/v1/chat/completions (sync + SSE) end to end on the CPU engine."""
+import asyncio
+import json
+
+import pytest
+from aiohttp.test_utils import TestClient, TestServer
+
+from llm_mcp_amd.api.app import ServingState, make_app
+from llm_mcp_amd.api.registry import LocalModel, ModelRegistry
+from llm_mcp_amd.engine.async_engine import AsyncEngine
+from llm_mcp_amd.engine.engine import EngineConfig, LLMEngine
+from llm_mcp_amd.models.tokenizer import for_model
+from llm_mcp_amd.utils.metrics import Metrics
+
+
+@pytest.fixture(scope="module")
+def engine():
+    e = LLMEngine(EngineConfig(model="tiny-llama", max_num_seqs=8, max_batched_tokens=256,
+                               max_model_len=512, use_graphs=False), device="cpu")
+    yield e
+    e.stop()
+
+
+def _state(engine):
+    aeng = AsyncEngine(engine)
+    reg = ModelRegistry()
+    reg.add(LocalModel("tiny-llama", "chat", "cpu0", aeng, for_model(engine.cfg), engine.cfg,
+                       max_model_len=512, capacity=8))
+    return ServingState(reg, Metrics()), aeng
+
+
+def _run(coro):
+    return asyncio.new_event_loop().run_until_complete(coro)
+
+
+def test_chat_sync_and_stream(engine):
+    async def go():
+        st, aeng = _state(engine)
+        async with TestClient(TestServer(make_app(st))) as c:
+            aeng.start(asyncio.get_running_loop())
+            r = await c.post("/v1/chat/completions", json={
+                "model": "tiny-llama", "messages": [{"role": "user", "content": "hi there"}],
+                "max_tokens": 5, "temperature": 0, "ignore_eos": True})
+            assert r.status == 200
+            j = await r.json()
+            assert j["object"] == "chat.completion"
+            assert j["usage"]["completion_tokens"] == 5
+            assert j["choices"][0]["finish_reason"] == "length"
+            r = await c.post("/v1/chat/completions", json={
+                "model": "tiny-llama", "messages": [{"role": "user", "content": "hi there"}],
+                "max_tokens": 5, "temperature": 0, "ignore_eos": True, "stream": True,
+                "stream_options": {"include_usage": True}})
+            assert r.status == 200
+            assert r.headers["Content-Type"].startswith("text/event-stream")
+            body = (await r.read()).decode()
+            frames = [f for f in body.split("\n\n") if f]
+            assert frames[-1] == "data: [DONE]"
+            chunks = [json.loads(f[6:]) for f in frames[:-1]]
+            assert all(ch["object"] == "chat.completion.chunk" for ch in chunks)
+            fin = [ch for ch in chunks if ch["choices"] and ch["choices"][0].get("finish_reason")]
+            assert fin and fin[-1]["choices"][0]["delta"] == {}
+            assert chunks[-1]["usage"]["completion_tokens"] == 5
+            # same greedy text both ways
+            text = "".join(ch["choices"][0]["delta"].get("content", "") for ch in chunks
+                           if ch["choices"])
+            assert text == j["choices"][0]["message"]["content"]
+            # errors keep the reference contract
+            r = await c.post("/v1/chat/completions", json={"model": "tiny-llama"})
+            assert r.status == 400 and (await r.json())["error"] == "messages_required"
+            r = await c.get("/v1/chat/completions")
+            assert r.status == 405
+            r = await c.post("/v1/chat/completions", json={
+                "model": "nope", "messages": [{"role": "user", "content": "x"}]})
+            assert r.status == 503 and (await r.json())["error"] == "no_device"
+            r = await c.post("/v1/chat/completions", json={
+                "model": "openai/gpt-4o", "messages": [{"role": "user", "content": "x"}]})
+            assert r.status == 503 and (await r.json())["error"] == "cloud_disabled"
+            m = await (await c.get("/metrics")).text()
+            assert "llmcore_chat_requests_total" in m and "llm_ttft_seconds" in m
+            aeng.stop()
+    _run(go())
+
+
+def test_stop_strings(engine):
+    async def go():
+        st, aeng = _state(engine)
+        async with TestClient(TestServer(make_app(st))) as c:
+            aeng.start(asyncio.get_running_loop())
+            r = await c.post("/v1/chat/completions", json={
+                "model": "tiny-llama", "messages": [{"role": "user", "content": "abc"}],
+                "max_tokens": 40, "temperature": 0, "ignore_eos": True})
+            full = (await r.json())["choices"][0]["message"]["content"]
+            assert len(full) > 4
+            stop = full[2:4]
+            r = await c.post("/v1/chat/completions", json={
+                "model": "tiny-llama", "messages": [{"role": "user", "content": "abc"}],
+                "max_tokens": 40, "temperature": 0, "ignore_eos": True, "stop": [stop]})
+            j = await r.json()
+            assert j["choices"][0]["message"]["content"] == full[:full.index(stop)]
+            assert j["choices"][0]["finish_reason"] == "stop"
+            aeng.stop()
+    _run(go())

@@ -1,0 +1,249 @@
+"""Numerics of every gfx950 HIP kernel against the plain PyTorch fp32
+reference of the same op (ops/ref.py)."""
+import math
+
+import pytest
+import torch
+
+from llm_mcp_amd import ops
+from llm_mcp_amd.ops import ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(autouse=True)
+def _native():
+    ops.native()  # GPU tests must exercise the HIP path: fail if it is missing
+    torch.manual_seed(0)
+
+
+def _bf(*shape, scale=1.0):
+    return (torch.randn(*shape, device=DEV) * scale).to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("rows,cols", [(1, 4096), (7, 4096), (300, 768), (64, 8192), (3, 256)])
+def test_rms_norm(rows, cols):
+    x, w = _bf(rows, cols), _bf(cols)
+    y = ops.rms_norm(x, w, 1e-5)
+    torch.testing.assert_close(y.float(), ref.rms_norm(x, w, 1e-5).float(), atol=2e-2, rtol=2e-2)
+    r = _bf(rows, cols)
+    r_ref = r.clone()
+    y2 = ops.rms_norm(x, w, 1e-5, residual=r)
+    y2_ref = ref.rms_norm(x, w, 1e-5, residual=r_ref)
+    torch.testing.assert_close(r.float(), r_ref.float(), atol=1e-2, rtol=1e-2)
+    torch.testing.assert_close(y2.float(), y2_ref.float(), atol=3e-2, rtol=3e-2)
+
+
+def test_rms_norm_strided_input():
+    x = _bf(16, 6144)[:, 1024:5120]
+    w = _bf(4096)
+    torch.testing.assert_close(ops.rms_norm(x, w, 1e-5).float(),
+                               ref.rms_norm(x.contiguous(), w, 1e-5).float(), atol=2e-2, rtol=2e-2)
+
+
+def test_layer_norm():
+    x, w, b, r = _bf(33, 768), _bf(768), _bf(768), _bf(33, 768)
+    torch.testing.assert_close(ops.layer_norm(x, w, b, 1e-12, r).float(),
+                               ref.layer_norm(x, w, b, 1e-12, r).float(), atol=3e-2, rtol=3e-2)
+
+
+def _cache(NB, Hkv, D, BS=32):
+    k = _bf(NB, Hkv, BS, D)
+    v = _bf(NB, Hkv, D, BS)
+    return k, v
+
+
+@pytest.mark.parametrize("Hq,Hkv,D", [(32, 8, 128), (8, 1, 128), (12, 12, 64), (4, 2, 128)])
+def test_rope_and_cache(Hq, Hkv, D):
+    T, NB = 37, 8
+    qkv = _bf(T, (Hq + 2 * Hkv) * D)
+    pos = torch.randint(0, 4000, (T,), device=DEV, dtype=torch.int32)
+    cs = ref.rope_cos_sin(4096, D, 500000.0, DEV)
+    slots = torch.randperm(NB * 32, device=DEV)[:T].to(torch.int32)
+    slots[3] = -1
+    kc, vc = torch.zeros(NB, Hkv, 32, D, device=DEV, dtype=torch.bfloat16), \
+        torch.zeros(NB, Hkv, D, 32, device=DEV, dtype=torch.bfloat16)
+    qkv0, kc0, vc0 = qkv.cpu(), kc.cpu(), vc.cpu()
+    ops.rope_and_cache(qkv, pos, cs, Hq, Hkv, D, slots, kc, vc)
+    ref.rope_cache(qkv0, pos.cpu(), cs.cpu(), Hq, Hkv, D, slots.cpu(), kc0, vc0, False)
+    torch.testing.assert_close(qkv[:, :Hq * D].float().cpu(), qkv0[:, :Hq * D].float(),
+                               atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(kc.cpu().float(), kc0.float(), atol=2e-2, rtol=2e-2)
+    assert torch.equal(vc.cpu(), vc0)
+
+
+def _random_tables(B, ctxs, NB, BS=32):
+    maxb = max(math.ceil(c / BS) for c in ctxs)
+    perm = torch.randperm(NB)
+    bt = torch.zeros(B, maxb, dtype=torch.int32)
+    k = 0
+    for b, c in enumerate(ctxs):
+        nb = math.ceil(c / BS)
+        bt[b, :nb] = perm[k:k + nb]
+        k += nb
+    return bt.to(DEV)
+
+
+@pytest.mark.parametrize("Hq,Hkv,D", [(32, 8, 128), (8, 1, 128), (64, 8, 128), (16, 16, 64)])
+@pytest.mark.parametrize("ctxs", [[1, 17, 32, 33, 500], [1024, 2047, 3000], [5000]])
+def test_paged_decode(Hq, Hkv, D, ctxs):
+    B = len(ctxs)
+    NB = sum(math.ceil(c / 32) for c in ctxs) + 4
+    kc, vc = _cache(NB, Hkv, D)
+    bt = _random_tables(B, ctxs, NB)
+    ctx = torch.tensor(ctxs, dtype=torch.int32, device=DEV)
+    q = _bf(B, (Hq + 2 * Hkv) * D)  # rows strided like the fused qkv buffer
+    out = torch.empty(B, Hq * D, dtype=torch.bfloat16, device=DEV)
+    ws = ops.DecodeWorkspace(B, Hq, D, 4, DEV)
+    scale = 1 / math.sqrt(D)
+    ops.paged_decode_attention(q, kc, vc, bt, ctx, scale, out, ws, part_tokens=512, Hq=Hq)
+    expect = ref.paged_decode(q[:, :Hq * D].reshape(B, Hq, D), kc, vc, bt, ctx, scale)
+    torch.testing.assert_close(out.float().view(B, Hq, D), expect.float(), atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("Hq,Hkv,D", [(32, 8, 128), (8, 1, 128), (12, 12, 64), (4, 4, 128)])
+def test_paged_prefill_varlen_with_prefix(Hq, Hkv, D):
+    qlens = [1, 70, 33, 256]
+    prefix = [0, 40, 0, 100]
+    ctxs = [q + p for q, p in zip(qlens, prefix)]
+    S = len(qlens)
+    NB = sum(math.ceil(c / 32) for c in ctxs) + 2
+    kc, vc = _cache(NB, Hkv, D)
+    bt = _random_tables(S, ctxs, NB)
+    cu = torch.tensor([0] + list(torch.cumsum(torch.tensor(qlens), 0)), dtype=torch.int32,
+                      device=DEV)
+    T = int(cu[-1])
+    q = _bf(T, (Hq + 2 * Hkv) * D)
+    qpt = ops.prefill_q_per_tile(Hq, Hkv)
+    tiles = []
+    for s, ql in enumerate(qlens):
+        for q0 in range(0, ql, qpt):
+            tiles += [s, q0]
+    tiles = torch.tensor(tiles, dtype=torch.int32, device=DEV)
+    ctx = torch.tensor(ctxs, dtype=torch.int32, device=DEV)
+    out = torch.zeros(T, Hq * D, dtype=torch.bfloat16, device=DEV)
+    scale = 1 / math.sqrt(D)
+    ops.paged_prefill_attention(q, kc, vc, bt, cu, ctx, tiles, scale, out, causal=True, Hq=Hq)
+    expect = ref.paged_prefill(q[:, :Hq * D].reshape(T, Hq, D), kc, vc, bt, cu, ctx, scale)
+    torch.testing.assert_close(out.float().view(T, Hq, D), expect.float(), atol=2e-2, rtol=2e-2)
+    # bidirectional (encoder) mode
+    out2 = torch.zeros_like(out)
+    ops.paged_prefill_attention(q, kc, vc, bt, cu, ctx, tiles, scale, out2, causal=False, Hq=Hq)
+    expect2 = ref.paged_prefill(q[:, :Hq * D].reshape(T, Hq, D), kc, vc, bt, cu, ctx, scale,
+                                causal=False)
+    torch.testing.assert_close(out2.float().view(T, Hq, D), expect2.float(), atol=2e-2, rtol=2e-2)
+
+
+def test_paged_decode_spike_rescale():
+    """Force the online-softmax rescale: one key scores far above the rest in a
+    late page (guide §5.4 rule 26)."""
+    Hq, Hkv, D, c = 32, 8, 128, 1500
+    NB = 64
+    kc, vc = _cache(NB, Hkv, D)
+    bt = _random_tables(1, [c], NB)
+    q = _bf(1, (Hq + 2 * Hkv) * D)
+    blk = int(bt[0, 1400 // 32])
+    kc[blk, :, 1400 % 32, :] = (q[0, :Hq * D].view(Hkv, Hq // Hkv, D)[:, 0, :] * 8).to(kc.dtype)
+    ctx = torch.tensor([c], dtype=torch.int32, device=DEV)
+    out = torch.empty(1, Hq * D, dtype=torch.bfloat16, device=DEV)
+    ws = ops.DecodeWorkspace(1, Hq, D, 8, DEV)
+    ops.paged_decode_attention(q, kc, vc, bt, ctx, 1 / math.sqrt(D), out, ws, 256, Hq=Hq)
+    expect = ref.paged_decode(q[:, :Hq * D].reshape(1, Hq, D), kc, vc, bt, ctx, 1 / math.sqrt(D))
+    torch.testing.assert_close(out.float().view(1, Hq, D), expect.float(), atol=2e-2, rtol=2e-2)
+
+
+def _params(B, t=1.0, k=0, p=1.0):
+    f = lambda v, dt: torch.full((B,), v, dtype=dt, device=DEV)
+    return (f(t, torch.float32), f(k, torch.int32), f(p, torch.float32),
+            torch.arange(B, dtype=torch.int64, device=DEV) * 7 + 1, f(0, torch.int32))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_sample_greedy_and_logprob(dtype):
+    B, V = 5, 128256
+    lg = (torch.randn(B, V, device=DEV) * 3).to(dtype)
+    tok, lp = ops.sample(lg, *_params(B, t=0.0))
+    assert torch.equal(tok.long(), lg.float().argmax(-1))
+    ref_lp = torch.log_softmax(lg.float(), -1).gather(1, tok.long()[:, None])[:, 0]
+    torch.testing.assert_close(lp, ref_lp, atol=1e-3, rtol=1e-3)
+
+
+def test_sample_distribution_matches_softmax():
+    V, B = 8, 4096
+    base = torch.tensor([2.0, 1.0, 0.5, 0.0, -1.0, -2.0, 0.3, 1.5], device=DEV)
+    lg = base.repeat(B, 1)
+    t, k, p, _, off = _params(B, t=0.7)
+    seeds = torch.arange(B, dtype=torch.int64, device=DEV) * 977 + 3
+    tok, _ = ops.sample(lg, t, k, p, seeds, off)
+    freq = torch.bincount(tok.long(), minlength=V).float() / B
+    expect = torch.softmax(base / 0.7, -1)
+    assert torch.allclose(freq, expect, atol=0.03), (freq, expect)
+
+
+def test_sample_top_k_top_p_support():
+    V, B = 1000, 2048
+    lg = torch.randn(V, device=DEV).repeat(B, 1) * 2
+    order = lg[0].argsort(descending=True)
+    seeds = torch.arange(B, dtype=torch.int64, device=DEV) * 31 + 5
+    t, k, p, _, off = _params(B, t=1.0, k=5)
+    tok, _ = ops.sample(lg, t, k, p, seeds, off)
+    assert set(tok.tolist()) <= set(order[:5].tolist())
+    assert len(set(tok.tolist())) > 1
+    # nucleus: expected support = smallest prefix with mass >= 0.5
+    probs = torch.softmax(lg[0], -1)[order]
+    above = torch.cumsum(probs, 0) - probs
+    nucleus = set(order[above < 0.5].tolist())
+    t, k, p, _, off = _params(B, t=1.0, p=0.5)
+    tok, _ = ops.sample(lg, t, k, p, seeds, off)
+    assert set(tok.tolist()) <= nucleus
+    # determinism: same seeds -> same tokens
+    tok2, _ = ops.sample(lg, t, k, p, seeds, off)
+    assert torch.equal(tok, tok2)
+
+
+def test_silu_mul_gelu_mul():
+    x = _bf(77, 2 * 14336 // 4)
+    torch.testing.assert_close(ops.silu_mul(x).float(), ref.silu_mul(x).float(), atol=2e-2,
+                               rtol=2e-2)
+    torch.testing.assert_close(ops.gelu_mul(x).float(), ref.gelu_mul(x).float(), atol=2e-2,
+                               rtol=2e-2)
+
+
+def test_embed_gather_vocab_shard():
+    table = _bf(1000, 256)
+    ids = torch.randint(0, 2000, (50,), device=DEV, dtype=torch.int32)
+    y = ops.embed_gather(table, ids, vocab_start=500)
+    local = ids.long() - 500
+    own = (local >= 0) & (local < 1000)
+    expect = table[local.clamp(0, 999)] * own[:, None].to(table.dtype)
+    assert torch.equal(y, expect)
+
+
+def test_mean_pool_l2_matryoshka():
+    h = _bf(100, 768)
+    cu = torch.tensor([0, 10, 11, 100], dtype=torch.int32, device=DEV)
+    for dims in (768, 256):
+        y = ops.mean_pool_l2(h, cu, dims)
+        torch.testing.assert_close(y, ref.mean_pool_l2(h, cu, dims), atol=1e-3, rtol=1e-3)
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 128, 64), (77, 768, 768), (256, 2304, 768),
+                                   (1000, 3072, 768), (130, 768, 3072), (512, 4096, 4096)])
+@pytest.mark.parametrize("act", [0, 1, 2])
+def test_gemm_nt(M, N, K, act):
+    a, w, b = _bf(M, K), _bf(N, K, scale=K ** -0.5), _bf(N)
+    r = _bf(M, N)
+    y = ops.gemm_nt(a, w, b, act, residual=r)
+    expect = ref.gemm_nt(a, w, b, act, r)
+    torch.testing.assert_close(y.float(), expect.float(), atol=3e-2, rtol=3e-2)
+
+
+def test_gemm_nt_identity_asymmetric():
+    """A = I with an asymmetric B catches a transposed C write (guide §3)."""
+    n = 128
+    a = torch.eye(n, device=DEV, dtype=torch.bfloat16)
+    w = torch.arange(n * n, device=DEV, dtype=torch.float32).view(n, n).remainder(97).to(
+        torch.bfloat16)
+    y = ops.gemm_nt(a, w)
+    assert torch.equal(y, w.t().contiguous())
