@@ -186,9 +186,9 @@ def main() -> None:
     except Exception:
         client.kill()
     engine.stop()
+    loop.call_soon_threadsafe(loop.stop)
     if world > 1:
         dist.destroy_process_group()
-    os._exit(0)
 
 
 if __name__ == "__main__":

@@ -187,7 +187,8 @@ class LLMEngine:
         self._thread: threading.Thread | None = None
         self.graphs: dict[int, dict] = {}
         self.stats = {"steps": 0, "decode_steps": 0, "graph_steps": 0, "prefill_tokens": 0,
-                      "generated_tokens": 0, "step_time_s": 0.0, "finished": 0}
+                      "generated_tokens": 0, "step_time_s": 0.0, "finished": 0,
+                      "t_schedule": 0.0, "t_gpu": 0.0, "t_update": 0.0, "t_events": 0.0}
         if ecfg.use_graphs and self.device.type == "cuda":
             self._capture_graphs()
 
@@ -391,6 +392,7 @@ class LLMEngine:
         sample_seq = plan["sample_seq"]
         N = len(sample_seq)
         temp, topk, topp, seeds, offs = self._sampling_arrays(seq_ids, sample_seq, N)
+        t1 = time.perf_counter()
         bucket = None
         if nd == S == T and self.graphs:
             bucket = next((b for b in sorted(self.graphs) if b >= nd), None)
@@ -398,9 +400,14 @@ class LLMEngine:
             toks, lps = self._run_graph(plan, bucket, temp, topk, topp, seeds, offs)
         else:
             toks, lps = self._run_eager(plan, temp, topk, topp, seeds, offs)
+        t2 = time.perf_counter()
         finished = self.sched.update(toks[:N])
-        dt = time.perf_counter() - t0
+        t3 = time.perf_counter()
+        dt = t3 - t0
         st = self.stats
+        st["t_schedule"] += t1 - t0
+        st["t_gpu"] += t2 - t1
+        st["t_update"] += t3 - t2
         st["steps"] += 1
         st["step_time_s"] += dt
         st["decode_steps"] += int(nd == S)
@@ -426,6 +433,7 @@ class LLMEngine:
             evs.append(TokenEvent(req, int(toks[i]), float(lps[i]), reason))
         if evs and self.event_sink:
             self.event_sink(evs)
+        st["t_events"] += time.perf_counter() - t3
         return True
 
     def _run_eager(self, plan, temp, topk, topp, seeds, offs):
