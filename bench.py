@@ -47,6 +47,8 @@ def main() -> None:
     ap.add_argument("--port-base", type=int, default=18080)
     ap.add_argument("--max-batched-tokens", type=int, default=16384)
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--inproc", action="store_true",
+                    help="serve HTTP from the GPU process (default: separate API process)")
     a = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -54,8 +56,15 @@ def main() -> None:
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     port = a.port_base + local_rank
     url = f"http://127.0.0.1:{port}"
+    sock = f"/tmp/lmx-bench-{os.getpid()}-{local_rank}.sock"
 
-    # client first: no process is started after this one touches the GPU
+    # children first: no process is started after this one touches the GPU
+    api_proc = None
+    if not a.inproc:
+        api_proc = subprocess.Popen(
+            [sys.executable, "-m", "llm_mcp_amd.api.serve", "--port", str(port),
+             "--engine", f"{a.model}=unix:{sock},device=gpu{local_rank}"],
+            stdout=subprocess.DEVNULL)
     client = subprocess.Popen(
         [sys.executable, "-m", "llm_mcp_amd.bench.loadgen", "--serve-stdin", "--url", url,
          "--model", a.model, "--concurrency", str(a.concurrency), "--prompt-len",
@@ -88,28 +97,38 @@ def main() -> None:
     engine = LLMEngine(ecfg, device=dev)
     log(f"engine ready in {time.time() - t_init:.1f}s: {engine.num_blocks} KV blocks, "
         f"{len(engine.graphs)} decode graphs, weights {engine.model.weight_bytes() / 1e9:.1f} GB")
-    aeng = AsyncEngine(engine)
-    reg = ModelRegistry()
-    reg.add(LocalModel(a.model, "chat", f"gpu{local_rank}", aeng, for_model(engine.cfg),
-                       engine.cfg, max_model_len=engine.max_model_len,
-                       capacity=ecfg.max_num_seqs))
-    state = ServingState(reg, Metrics())
+    loop = None
+    if a.inproc:
+        aeng = AsyncEngine(engine)
+        reg = ModelRegistry()
+        reg.add(LocalModel(a.model, "chat", f"gpu{local_rank}", aeng, for_model(engine.cfg),
+                           engine.cfg, max_model_len=engine.max_model_len,
+                           capacity=ecfg.max_num_seqs))
+        state = ServingState(reg, Metrics())
+        state.register_routes = lambda app: app.router.add_get(
+            "/ready", lambda r: __import__("aiohttp").web.json_response({"ready": True}))
 
-    from aiohttp import web
-    loop = asyncio.new_event_loop()
-    started = threading.Event()
+        from aiohttp import web
+        loop = asyncio.new_event_loop()
+        started = threading.Event()
 
-    def serve():
-        asyncio.set_event_loop(loop)
-        runner = web.AppRunner(make_app(state), access_log=None)
-        loop.run_until_complete(runner.setup())
-        loop.run_until_complete(web.TCPSite(runner, "127.0.0.1", port).start())
-        aeng.start(loop)
-        started.set()
-        loop.run_forever()
+        def serve():
+            asyncio.set_event_loop(loop)
+            runner = web.AppRunner(make_app(state), access_log=None)
+            loop.run_until_complete(runner.setup())
+            loop.run_until_complete(web.TCPSite(runner, "127.0.0.1", port).start())
+            aeng.start(loop)
+            started.set()
+            loop.run_forever()
 
-    threading.Thread(target=serve, daemon=True, name="http").start()
-    started.wait()
+        threading.Thread(target=serve, daemon=True, name="http").start()
+        started.wait()
+    else:
+        from llm_mcp_amd.engine.ipc import EngineServer
+        server = EngineServer(engine, sock, info={
+            "kind": "chat", "model": a.model, "device_id": f"gpu{local_rank}",
+            "max_model_len": engine.max_model_len, "capacity": ecfg.max_num_seqs})
+        server.start()
     ready = json.loads(client.stdout.readline())
     if not ready.get("ready"):
         raise RuntimeError("load generator could not reach the server")
@@ -176,6 +195,7 @@ def main() -> None:
                        "seq_len": a.prompt_len + a.max_tokens, "prompt_len": a.prompt_len,
                        "max_tokens": a.max_tokens, "parallelism": f"dp{world}",
                        "endpoint": "/v1/chat/completions stream=true",
+                       "serving": "in-process" if a.inproc else "api process + engine process (unix socket)",
                        "sampling": {"temperature": a.temperature, "top_p": a.top_p},
                        "engine_steps": st["steps"], "graph_steps": st["graph_steps"]},
         }
@@ -186,7 +206,16 @@ def main() -> None:
     except Exception:
         client.kill()
     engine.stop()
-    loop.call_soon_threadsafe(loop.stop)
+    if loop is not None:
+        loop.call_soon_threadsafe(loop.stop)
+    if api_proc is not None:
+        api_proc.terminate()
+        try:
+            api_proc.wait(timeout=10)
+        except Exception:
+            api_proc.kill()
+        if os.path.exists(sock):
+            os.unlink(sock)
     if world > 1:
         dist.destroy_process_group()
 

@@ -1,0 +1,92 @@
+"""``python -m llm_mcp_amd.api.serve`` -- the API ("core") process.
+
+Serves the OpenAI-compatible endpoints (and, with a store configured, the
+whole control plane) and forwards generation to engine worker processes over
+their Unix sockets (engine/ipc.py).  Engines are given as
+``--engine MODEL=unix:/path[,device=gpu0]`` (repeatable); the process keeps
+retrying until every engine socket is up, and ``GET /ready`` turns 200 once
+all are connected (``/health`` answers immediately, as in the reference).
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import logging
+import os
+
+from aiohttp import web
+
+from ..engine.ipc import EngineClient
+from ..models import config as mc
+from ..models.tokenizer import for_model
+from ..utils.metrics import Metrics
+from .app import ServingState, make_app
+from .helpers import write_json
+from .registry import LocalModel, ModelRegistry
+
+log = logging.getLogger("lmx.serve")
+
+
+def parse_engine_spec(spec: str) -> dict:
+    model, rest = spec.split("=", 1)
+    parts = rest.split(",")
+    out = {"model": model, "path": parts[0].removeprefix("unix:"), "device": "gpu0"}
+    for p in parts[1:]:
+        k, v = p.split("=", 1)
+        out[k] = v
+    return out
+
+
+async def attach_engines(state, specs: list[dict]):
+    clients = []
+    for s in specs:
+        c = EngineClient(s["path"])
+        clients.append((s, c))
+
+    async def one(s, c):
+        await c.connect()
+        info = await c.info(timeout=30)
+        cfg = mc.resolve(s["model"])
+        state.registry.add(LocalModel(
+            s["model"], info.get("kind", "chat"), s.get("device") or info.get("device_id", "gpu0"),
+            c, for_model(cfg, s.get("tokenizer")), cfg,
+            max_model_len=int(info.get("max_model_len", 8192)),
+            capacity=int(info.get("capacity", 256))))
+        log.info("engine %s on %s connected", s["model"], s["path"])
+
+    await asyncio.gather(*[one(s, c) for s, c in clients])
+    state.engines_ready = True
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--host", default=os.environ.get("LMX_HTTP_HOST", "127.0.0.1"))
+    ap.add_argument("--port", type=int, default=int(os.environ.get("LMX_HTTP_PORT", "8080")))
+    ap.add_argument("--engine", action="append", default=[],
+                    help="MODEL=unix:/path[,device=gpu0][,tokenizer=/dir]")
+    a = ap.parse_args(argv)
+    logging.basicConfig(level=os.environ.get("LOG_LEVEL", "INFO"))
+    state = ServingState(ModelRegistry(), Metrics(),
+                         version=os.environ.get("CORE_VERSION", "0.1.0"))
+    state.engines_ready = False
+    specs = [parse_engine_spec(s) for s in a.engine]
+
+    def register(app):
+        async def ready(request):
+            ok = getattr(state, "engines_ready", False)
+            return write_json(200 if ok else 503, {"ready": ok,
+                                                    "models": state.registry.model_ids()})
+        app.router.add_get("/ready", ready)
+
+    state.register_routes = register
+    app = make_app(state)
+
+    async def on_start(app):
+        app["_attach"] = asyncio.create_task(attach_engines(state, specs))
+
+    app.on_startup.append(on_start)
+    web.run_app(app, host=a.host, port=a.port, access_log=None, print=None)
+
+
+if __name__ == "__main__":
+    main()

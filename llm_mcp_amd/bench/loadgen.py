@@ -93,7 +93,7 @@ async def wait_ready(url, timeout=1800):
     async with aiohttp.ClientSession() as s:
         while time.time() < t_end:
             try:
-                async with s.get(url + "/health") as r:
+                async with s.get(url + "/ready") as r:
                     if r.status == 200:
                         return True
             except Exception:

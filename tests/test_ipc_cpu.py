@@ -1,0 +1,56 @@
+"""API process <-> engine process link (Unix socket, msgpack) on the CPU engine."""
+import asyncio
+import json
+import os
+import tempfile
+
+from aiohttp.test_utils import TestClient, TestServer
+
+from llm_mcp_amd.api.app import ServingState, make_app
+from llm_mcp_amd.api.registry import ModelRegistry
+from llm_mcp_amd.api.serve import attach_engines, parse_engine_spec
+from llm_mcp_amd.engine.engine import EngineConfig, LLMEngine
+from llm_mcp_amd.engine.ipc import EngineServer
+from llm_mcp_amd.utils.metrics import Metrics
+
+
+def test_chat_over_ipc():
+    e = LLMEngine(EngineConfig(model="tiny-llama", max_num_seqs=8, max_batched_tokens=256,
+                               max_model_len=512, use_graphs=False), device="cpu")
+    path = os.path.join(tempfile.mkdtemp(), "eng.sock")
+    srv = EngineServer(e, path, info={"kind": "chat", "max_model_len": 512, "capacity": 8})
+    srv.start()
+
+    async def go():
+        st = ServingState(ModelRegistry(), Metrics())
+        await attach_engines(st, [parse_engine_spec(f"tiny-llama=unix:{path},device=cpu0")])
+        m = st.registry.select("tiny-llama", "chat")
+        assert m is not None and m.max_model_len == 512 and m.device_id == "cpu0"
+        async with TestClient(TestServer(make_app(st))) as c:
+            outs = []
+            for stream in (False, True):
+                r = await c.post("/v1/chat/completions", json={
+                    "model": "tiny-llama", "messages": [{"role": "user", "content": "hello"}],
+                    "max_tokens": 6, "temperature": 0, "ignore_eos": True, "stream": stream})
+                assert r.status == 200
+                if stream:
+                    frames = [f for f in (await r.read()).decode().split("\n\n") if f]
+                    assert frames[-1] == "data: [DONE]"
+                    outs.append("".join(json.loads(f[6:])["choices"][0]["delta"].get("content", "")
+                                        for f in frames[:-1]))
+                else:
+                    outs.append((await r.json())["choices"][0]["message"]["content"])
+            assert outs[0] == outs[1]
+            # many concurrent streams over one connection
+            rs = await asyncio.gather(*[c.post("/v1/chat/completions", json={
+                "model": "tiny-llama", "messages": [{"role": "user", "content": f"q{i}"}],
+                "max_tokens": 4, "temperature": 0.7, "ignore_eos": True}) for i in range(12)])
+            for r in rs:
+                assert (await r.json())["usage"]["completion_tokens"] == 4
+            info = await m.engine.info()
+            assert info["stats"]["finished"] >= 14
+
+    try:
+        asyncio.new_event_loop().run_until_complete(go())
+    finally:
+        srv.stop()
