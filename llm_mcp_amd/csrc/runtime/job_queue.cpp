@@ -94,15 +94,32 @@ void JobQueue::bump() {
 void JobQueue::index_insert(const JobRow& j) {
   if (j.status == "queued" || j.status == "running")
     claimable_.insert(ReadyKey(-j.priority, j.queued_at, j.seq, j.id));
-  if (j.status == "running" && !j.device_id.empty()) running_per_device_[j.device_id]++;
+  if (j.status == "running" && !j.device_id.empty()) running_per_device_[j.device_id].insert(j.id);
 }
 
 void JobQueue::index_erase(const JobRow& j) {
   claimable_.erase(ReadyKey(-j.priority, j.queued_at, j.seq, j.id));
   if (j.status == "running" && !j.device_id.empty()) {
     auto it = running_per_device_.find(j.device_id);
-    if (it != running_per_device_.end() && --it->second <= 0) running_per_device_.erase(it);
+    if (it != running_per_device_.end()) {
+      it->second.erase(j.id);
+      if (it->second.empty()) running_per_device_.erase(it);
+    }
   }
+}
+
+// running jobs on a device whose lease is still live (the reference's
+// running_per_device CTE counts lease_until > now())
+int JobQueue::live_running(const std::string& dev, int64_t now, const std::string& except) const {
+  auto it = running_per_device_.find(dev);
+  if (it == running_per_device_.end()) return 0;
+  int n = 0;
+  for (const std::string& id : it->second) {
+    if (id == except) continue;
+    auto j = jobs_.find(id);
+    if (j != jobs_.end() && j->second.lease_until >= now) ++n;
+  }
+  return n;
 }
 
 void JobQueue::journal(const JobRow& j) {
@@ -257,12 +274,7 @@ bool JobQueue::claim(const std::string& worker_id, const ClaimFilter& f, int64_t
       int limit = f.device_max_concurrency;
       auto li = f.device_limits.find(dev);
       if (li != f.device_limits.end()) limit = li->second;
-      if (limit > 0) {
-        auto rc = running_per_device_.find(dev);
-        int running = rc == running_per_device_.end() ? 0 : rc->second;
-        if (j.status == "running" && j.device_id == dev) running--;  // reclaiming itself
-        if (running >= limit) continue;
-      }
+      if (limit > 0 && live_running(dev, now, j.id) >= limit) continue;
     }
     pick = &j;
     break;
@@ -478,10 +490,9 @@ std::vector<AttemptRow> JobQueue::attempts(const std::string& job_id) const {
   return it == attempts_.end() ? std::vector<AttemptRow>{} : it->second;
 }
 
-int JobQueue::running_on(const std::string& device_id) const {
+int JobQueue::running_on(const std::string& device_id, int64_t now) const {
   std::lock_guard<std::mutex> g(mu_);
-  auto it = running_per_device_.find(device_id);
-  return it == running_per_device_.end() ? 0 : it->second;
+  return live_running(device_id, now, "");
 }
 
 int64_t JobQueue::version() const {

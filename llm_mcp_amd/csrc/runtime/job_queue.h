@@ -32,6 +32,7 @@
 #include <set>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 namespace lmxrt {
@@ -88,7 +89,7 @@ class JobQueue {
   int stuck(int64_t now) const;  // running with expired lease
   std::vector<JobRow> list(const std::string& status, int limit) const;
   std::vector<AttemptRow> attempts(const std::string& job_id) const;
-  int running_on(const std::string& device_id) const;
+  int running_on(const std::string& device_id, int64_t now) const;  // live leases
   int64_t version() const;
   int64_t wait_change(int64_t since, int64_t timeout_ms);  // returns current version
   void compact();
@@ -110,7 +111,8 @@ class JobQueue {
   std::unordered_map<std::string, JobRow> jobs_;
   std::set<ReadyKey> claimable_;  // queued + running (lease may expire)
   std::unordered_map<std::string, std::vector<AttemptRow>> attempts_;
-  std::unordered_map<std::string, int> running_per_device_;
+  std::unordered_map<std::string, std::unordered_set<std::string>> running_per_device_;
+  int live_running(const std::string& dev, int64_t now, const std::string& except) const;
   std::string path_;
   FILE* jf_ = nullptr;
   int64_t seq_ = 0;

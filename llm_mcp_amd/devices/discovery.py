@@ -1,0 +1,148 @@
+"""Discovery runner (reference: core/internal/discovery/discovery.go:79-174
+and offline_handler.go).
+
+Per run:
+  1. enumerate this node's GPUs (rocm_enum) and upsert ``devices`` rows
+     ``<host>:gpu<i>`` with tags {engine, rocm, gfx, hbm_gb, cus, xgmi_peers,
+     engine_addr, capacity, models}; TP groups served by a multi-GPU engine are
+     registered as pseudo-devices ``<host>:tp<N>:gpu<a>-<b>``;
+  2. sync ``models`` / ``device_models`` from the local model registry
+     (metadata from the architecture, not the name) and mark models no longer
+     served as unavailable;
+  3. devices of this host that disappeared go offline and their running
+     jobs' leases are released so they can be reclaimed at once (the reference's
+     "60 s -> <5 s" recovery, offline_handler.go:12-38);
+  4. peer nodes (``LMX_PEER_NODES``, replaces the Tailscale mesh scan) are
+     polled at ``GET /v1/discovery/local`` and their devices upserted with the
+     peer's URL as ``engine_addr``.
+"""
+from __future__ import annotations
+
+import json
+import logging
+import os
+import threading
+import time
+import urllib.request
+
+from ..policy.inference import model_record
+from . import rocm_enum
+
+log = logging.getLogger("lmx.discovery")
+
+
+class DiscoveryRunner:
+    def __init__(self, store, registry=None, metrics=None, engine_addrs: dict | None = None):
+        self.store = store
+        self.registry = registry
+        self.metrics = metrics
+        self.engine_addrs = engine_addrs or {}
+        self._lock = threading.Lock()
+        self._last_run: float | None = None
+        self.last_result: dict = {}
+
+    def last_run(self) -> float | None:
+        with self._lock:
+            return self._last_run
+
+    def local_devices(self) -> list[dict]:
+        """This node's device records (also served to peers)."""
+        host = rocm_enum.host_id()
+        out = []
+        served: dict[str, list] = {}
+        if self.registry is not None:
+            for m in self.registry.all():
+                served.setdefault(m.device_id, []).append(m)
+        gpus = rocm_enum.enumerate_gpus()
+        for g in gpus:
+            did = rocm_enum.device_id(g.index, host)
+            ms = served.get(did, []) + served.get(f"gpu{g.index}", [])
+            out.append({
+                "id": did, "name": g.name or f"GPU {g.index}", "platform": "rocm",
+                "arch": g.gfx or "gfx950", "host": host,
+                "tags": {"engine": bool(ms) or True, "rocm": True, "gfx": g.gfx,
+                         "hbm_gb": g.hbm_gb, "cus": g.cus, "gpu_index": g.index,
+                         "xgmi_peers": g.xgmi_peers, "pci_bus": g.pci_bus,
+                         "temp_c": g.temp_c, "hbm_used_gb": g.hbm_used_gb,
+                         "engine_addr": self.engine_addrs.get(did, ""),
+                         "capacity": max([m.capacity for m in ms] or [0]) or None,
+                         "models": sorted({m.model_id for m in ms})},
+                "models": [(m.model_id, m.cfg, m.max_model_len) for m in ms]})
+        # multi-GPU (TP) engines registered under a group id
+        for dev, ms in served.items():
+            if ":tp" in dev and not any(d["id"] == dev for d in out):
+                out.append({"id": dev, "name": dev, "platform": "rocm", "arch": "gfx950",
+                            "host": host, "tags": {"engine": True, "rocm": True, "tp_group": True,
+                                                   "models": sorted({m.model_id for m in ms}),
+                                                   "capacity": max(m.capacity for m in ms)},
+                            "models": [(m.model_id, m.cfg, m.max_model_len) for m in ms]})
+        return out
+
+    def run(self) -> dict:
+        t0 = time.time()
+        status = "ok"
+        seen = []
+        try:
+            host = rocm_enum.host_id()
+            for d in self.local_devices():
+                self.store.upsert_device(d["id"], d["name"], d["platform"], d["arch"],
+                                         d["host"], d["tags"], "online", merge_tags=True)
+                seen.append(d["id"])
+                present = []
+                for mid, cfg, mml in d["models"]:
+                    rec = model_record(mid, cfg)
+                    self.store.upsert_model(mid, **rec)
+                    self.store.upsert_device_model(d["id"], mid, True,
+                                                   max_context_k=mml // 1024)
+                    present.append(mid)
+                self.store.mark_absent_models(d["id"], present)
+            gone = []
+            for d in self.store.list_devices():
+                if d.get("host") == host and d["id"] not in seen and d.get("status") == "online" \
+                        and (d.get("tags") or {}).get("rocm"):
+                    self.store.set_device_status(d["id"], "offline",
+                                                 {"last_error": "device disappeared",
+                                                  "last_error_at": time.time()})
+                    self.store.release_device_leases(d["id"])
+                    gone.append(d["id"])
+            peers = self._poll_peers()
+            res = {"devices": seen, "offline": gone, "peers": peers}
+        except Exception as e:  # discovery must not take the core down
+            log.exception("discovery failed")
+            status = "error"
+            res = {"error": str(e)}
+        dt = time.time() - t0
+        if self.metrics is not None:
+            self.metrics.discovery_runs.labels(status).inc()
+            self.metrics.discovery_duration.observe(dt)
+            self.metrics.devices_online.set(sum(1 for d in self.store.list_devices()
+                                                if d.get("status") == "online"))
+        with self._lock:
+            self._last_run = time.time()
+            self.last_result = res
+        return res
+
+    def _poll_peers(self) -> list[str]:
+        peers = [p.strip().rstrip("/") for p in os.environ.get("LMX_PEER_NODES", "").split(",")
+                 if p.strip()]
+        ok = []
+        for url in peers:
+            try:
+                with urllib.request.urlopen(url + "/v1/discovery/local", timeout=2) as r:
+                    data = json.loads(r.read())
+            except Exception:
+                for d in self.store.list_devices():
+                    if (d.get("tags") or {}).get("peer") == url:
+                        self.store.set_device_status(d["id"], "offline")
+                        self.store.release_device_leases(d["id"])
+                continue
+            for d in data.get("devices", []):
+                tags = dict(d.get("tags") or {})
+                tags.update(peer=url, engine_addr=url)
+                self.store.upsert_device(d["id"], d.get("name", ""), d.get("platform", "rocm"),
+                                         d.get("arch", ""), d.get("host", ""), tags, "online")
+                for mid in tags.get("models", []):
+                    self.store.upsert_model(mid, **model_record(mid))
+                    self.store.upsert_device_model(d["id"], mid, True)
+            ok.append(url)
+        return ok

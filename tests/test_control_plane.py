@@ -1,0 +1,219 @@
+"""HTTP control plane against the memory store (reference contracts:
+core/internal/api/handlers.go)."""
+import asyncio
+import json
+import time
+
+import pytest
+from aiohttp.test_utils import TestClient, TestServer
+
+from llm_mcp_amd.api.core import CoreState, create_core_app
+from llm_mcp_amd.store.memory import MemoryStore
+
+
+@pytest.fixture(autouse=True)
+def _env(monkeypatch):
+    monkeypatch.setenv("LMX_FAKE_GPUS", "2:288")
+    monkeypatch.setenv("LMX_NODE_ID", "node1")
+    monkeypatch.delenv("LMX_ALLOW_CLOUD", raising=False)
+    monkeypatch.setenv("DEVICE_MAX_CONCURRENCY", "1")
+
+
+def run(coro):
+    return asyncio.new_event_loop().run_until_complete(coro)
+
+
+def client(state=None):
+    st = state or CoreState(store=MemoryStore())
+    return st, TestClient(TestServer(create_core_app(st, background=False)))
+
+
+def test_health_version_metrics_405():
+    async def go():
+        st, c = client()
+        async with c:
+            assert (await (await c.get("/health")).json())["status"] == "ok"
+            assert "version" in await (await c.get("/version")).json()
+            r = await c.get("/v1/jobs")
+            assert r.status == 405 and (await r.json())["error"] == "method_not_allowed"
+            assert "llmcore_jobs_created_total" in await (await c.get("/metrics")).text()
+    run(go())
+
+
+def test_job_lifecycle_with_lease_tokens():
+    async def go():
+        st, c = client()
+        async with c:
+            r = await c.post("/v1/jobs", json={"kind": "echo", "payload": {"x": 1}})
+            assert r.status == 202
+            jid = (await r.json())["job_id"]
+            j = await (await c.get(f"/v1/jobs/{jid}")).json()
+            assert j["status"] == "queued" and j["payload"] == {"x": 1} and j["max_attempts"] == 3
+            assert (await c.get("/v1/jobs/not-a-uuid")).status == 404
+            r = await c.post("/v1/jobs", json={"payload": {}})
+            assert (await r.json())["error"] == "kind_required"
+            r = await c.post("/v1/jobs", data="{bad")
+            assert (await r.json())["error"] == "invalid_json"
+            r = await c.post("/v1/jobs", json={"kind": "x", "deadline_at": "tomorrow"})
+            assert (await r.json())["error"] == "invalid_deadline_at"
+            w = (await (await c.post("/v1/workers/register",
+                                     json={"worker": {"name": "w"}})).json())["worker_id"]
+            assert w.startswith("worker-")
+            r = await (await c.post("/v1/workers/claim", json={"worker_id": w,
+                                                               "lease_seconds": 30})).json()
+            job = r["job"]
+            assert job["id"] == jid and job["status"] == "running" and job["attempts"] == 1
+            tok = job["attempt_id"]
+            assert (await (await c.post("/v1/workers/claim", json={"worker_id": w})).json()) == {}
+            r = await c.post("/v1/workers/heartbeat", json={"worker_id": w, "job_id": jid,
+                                                            "attempt_id": tok})
+            assert (await r.json())["ok"] is True
+            # a stale token cannot complete the job
+            r = await c.post("/v1/workers/complete", json={"worker_id": w, "job_id": jid,
+                                                           "attempt_id": "bogus", "result": {}})
+            assert r.status == 409
+            r = await c.post("/v1/workers/complete", json={
+                "worker_id": w, "job_id": jid, "attempt_id": tok, "result": {"ok": True},
+                "metrics": {"tokens_in": 3, "tokens_out": 5, "provider": "local",
+                            "model": "m"}})
+            assert (await r.json())["ok"] is True
+            j = await (await c.get(f"/v1/jobs/{jid}")).json()
+            assert j["status"] == "done" and j["result"] == {"ok": True}
+            assert "lease_until" not in j
+            at = await (await c.get(f"/v1/jobs/{jid}/attempts")).json()
+            assert at["items"][0]["status"] == "done"
+    run(go())
+
+
+def test_fail_requeues_then_errors():
+    async def go():
+        st, c = client()
+        async with c:
+            jid = (await (await c.post("/v1/jobs", json={"kind": "k", "max_attempts": 2})).json())["job_id"]
+            for expect in ("queued", "error"):
+                job = (await (await c.post("/v1/workers/claim", json={"worker_id": "w1"})).json())["job"]
+                r = await c.post("/v1/workers/fail", json={"worker_id": "w1", "job_id": jid,
+                                                           "error": "boom",
+                                                           "attempt_id": job["attempt_id"]})
+                assert (await r.json())["status"] == expect
+            j = await (await c.get(f"/v1/jobs/{jid}")).json()
+            assert j["status"] == "error" and j["error"] == "boom" and j["attempts"] == 2
+            r = await c.post("/v1/workers/fail", json={"worker_id": "w1", "job_id":
+                                                       "00000000-0000-4000-8000-000000000000"})
+            assert r.status == 404
+    run(go())
+
+
+def test_job_stream_sse():
+    async def go():
+        st, c = client()
+        async with c:
+            jid = (await (await c.post("/v1/jobs", json={"kind": "k"})).json())["job_id"]
+            resp = await c.get(f"/v1/jobs/{jid}/stream")
+
+            async def worker():
+                await asyncio.sleep(0.1)
+                j = st.store.claim_job("w", [], 30)
+                await asyncio.sleep(0.1)
+                st.store.complete_job(jid, "w", {"r": 1}, {}, j["attempt_id"])
+
+            t = asyncio.create_task(worker())
+            body = (await resp.read()).decode()
+            await t
+            events = [json.loads(l[6:]) for l in body.split("\n") if l.startswith("data: ")]
+            assert [e["status"] for e in events] == ["queued", "running", "done"]
+            assert body.startswith("event: status\n")
+    run(go())
+
+
+def test_discovery_devices_dashboard_capacity():
+    async def go():
+        st, c = client()
+        async with c:
+            assert (await c.post("/v1/discovery/run")).status == 200
+            last = await (await c.get("/v1/discovery/last")).json()
+            assert last["last_run"]
+            devs = st.store.list_devices()
+            ids = sorted(d["id"] for d in devs)
+            assert ids == ["node1:gpu0", "node1:gpu1"]
+            assert devs[0]["tags"]["hbm_gb"] == 288 and devs[0]["tags"]["gfx"] == "gfx950"
+            d = await (await c.get("/v1/dashboard")).json()
+            for k in ("jobs", "benchmarks", "running_jobs", "devices", "hosts", "workers_online",
+                      "issues", "costs", "models_count", "updated_at"):
+                assert k in d
+            assert d["hosts"][0]["id"] == "node1" and len(d["hosts"][0]["nodes"]) == 2
+            cap = await (await c.get("/v1/debug/capacity")).json()
+            assert cap["total_slots"] == 2
+            h = await (await c.get("/v1/debug/health")).json()
+            assert set(h["checks"]) >= {"database", "queue", "hosts", "workers"}
+            acts = await (await c.get("/v1/debug/actions")).json()
+            assert acts["total"] == len(acts["endpoints"]) >= 24
+            t = await (await c.post("/v1/debug/test")).json()
+            assert [r["name"] for r in t["results"]] == ["db_ping", "db_read", "engine_ping",
+                                                         "job_create"]
+            # offline device releases its running leases immediately
+            jid = st.store.submit_job("k", {"device_id": "node1:gpu0"})
+            j = st.store.claim_job("w", [], 60, "node1:gpu0")
+            assert j["id"] == jid
+            await c.post("/v1/devices/offline", json={"device_id": "node1:gpu0", "reason": "x"})
+            assert st.store.get_device("node1:gpu0")["status"] == "offline"
+            assert st.store.get_job(jid)["lease_until"] is None
+    run(go())
+
+
+def test_llm_request_routing_and_deadline():
+    async def go():
+        st, c = client()
+        async with c:
+            r = await c.post("/v1/llm/request", json={"prompt": "hello", "model": "llama-3-8b"})
+            j = await r.json()
+            assert r.status == 202 and j["provider"] == "local" and j["kind"] == "engine.generate"
+            r = await c.post("/v1/llm/request", json={"prompt": "hi", "provider": "ollama"})
+            assert (await r.json())["kind"] == "ollama.generate"
+            r = await c.post("/v1/llm/request", json={"task": "embed", "prompt": "hi"})
+            assert (await r.json())["kind"] == "engine.embed"
+            r = await c.post("/v1/llm/request", json={"quality": "bogus", "prompt": "x"})
+            assert r.status == 400 and (await r.json())["error"] == "routing_failed"
+            # smart routing needs a served local model of the right tier
+            st.store.upsert_device("node1:gpu0", tags={"engine": True}, status="online")
+            st.store.upsert_model("llama-3-8b", provider="local", kind="chat", tier="large",
+                                  params_b=8.0, context_k=8)
+            st.store.upsert_device_model("node1:gpu0", "llama-3-8b")
+            r = await c.post("/v1/llm/request", json={"quality": "premium", "prompt": "hello"})
+            j = await r.json()
+            assert r.status == 202 and j["provider"] == "local"
+            job = st.store.get_job(j["job_id"])
+            assert job["payload"]["model"] == "llama-3-8b"
+            assert job["payload"]["device_id"] == "node1:gpu0"
+            assert job["payload"]["_tier"] == "large"
+            assert 85 < job["deadline_at"] - time.time() <= 90
+    run(go())
+
+
+def test_costs_feedback_stats_benchmarks():
+    async def go():
+        st, c = client()
+        async with c:
+            st.store.set_pricing("m1", 1.0, 2.0)
+            st.store.insert_cost(None, "m1", "openrouter", 1000, 1000,
+                                 st.store.calculate_job_cost("m1", 1000, 1000))
+            s = await (await c.get("/v1/costs/summary?period=week")).json()
+            assert abs(s["total_cost"] - 0.003) < 1e-9 and s["total_jobs"] == 1
+            assert s["by_provider"][0]["provider"] == "openrouter"
+            assert (await c.get("/v1/costs/summary?period=year")).status == 400
+            b = await (await c.get("/v1/costs/balance")).json()
+            assert b["openrouter_balance_usd"] is None and b["top_models"][0]["model"] == "m1"
+            r = await c.post("/v1/feedback", json={"model": "m1", "rating": "good"})
+            assert (await r.json()) == {"status": "ok", "model": "m1", "rating": "good"}
+            assert (await c.post("/v1/feedback", json={"model": "m1", "rating": "meh"})).status == 400
+            ms = await (await c.get("/v1/models/stats")).json()
+            assert ms["count"] == 1 and ms["models"][0]["feedback_score"] == 100.0
+            r = await c.post("/v1/benchmarks/run", json={"model": "llama-3-8b", "runs": 2})
+            j = await r.json()
+            assert r.status == 202 and len(j["job_ids"]) == 2 and j["kind"] == "benchmark.engine.generate"
+            st.store.insert_benchmark("d", "llama-3-8b", "generate", 10, 20, 100, 200.0)
+            items = (await (await c.get("/v1/benchmarks?limit=5")).json())["items"]
+            assert items[0]["tps"] == 200.0
+            r = await c.post("/v1/knowledge/ingest", json={"text": "short", "target": "lightrag"})
+            assert (await r.json())["error"] == "text_too_short"
+    run(go())
