@@ -62,7 +62,9 @@ class CoreState:
         self.discovery = DiscoveryRunner(self.store, self.registry, self.metrics, engine_addrs)
         self.control = ControlPlane(self)
         self.engines_ready = True
-        self.embed_handler = None
+        from .openai_embed import EmbeddingsHandler
+        self.embed_handler = EmbeddingsHandler(self)
+        self.cloud_embed = None
         self.cloud_chat = None
         self._tasks: list[asyncio.Task] = []
 

@@ -46,6 +46,7 @@ async def attach_engines(state, specs: list[dict]):
     async def one(s, c):
         await c.connect()
         info = await c.info(timeout=30)
+        info = {**info, **(info.get("models") or {}).get(s["model"], {})}
         cfg = mc.resolve(s["model"])
         state.registry.add(LocalModel(
             s["model"], info.get("kind", "chat"), s.get("device") or info.get("device_id", "gpu0"),

@@ -1,0 +1,156 @@
+"""Batched embedding engine (one per GPU that serves an embedding model).
+
+Requests (each a list of token-id sequences) queue up; the engine thread packs
+as many whole requests as fit ``max_batch_tokens`` into one varlen forward of
+the encoder, so concurrent /v1/embeddings calls share GEMMs (the reference
+made one Ollama HTTP call per request, core/internal/api/handlers.go:1942).
+Results are delivered to asyncio futures with one call_soon_threadsafe per
+batch."""
+from __future__ import annotations
+
+import asyncio
+import logging
+import queue
+import threading
+import time
+from dataclasses import dataclass, field
+
+import torch
+
+from ..models.config import NomicBertConfig
+from ..models.nomic_bert import NomicBertModel
+
+log = logging.getLogger("lmx.embed")
+
+
+@dataclass
+class EmbedRequest:
+    seqs: list[list[int]]
+    dims: int | None
+    future: object = None
+    loop: object = None
+    result: list | None = None
+    error: str | None = None
+    done: threading.Event = field(default_factory=threading.Event)
+
+
+class EmbeddingEngine:
+    def __init__(self, cfg: NomicBertConfig, device="cuda", max_batch_tokens: int = 32768,
+                 max_seq_len: int = 2048, seed: int = 0, weights=None):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.model = NomicBertModel(cfg, self.device, seed=seed, weights=weights)
+        self.max_batch_tokens = max_batch_tokens
+        self.max_seq_len = min(max_seq_len, cfg.max_position)
+        self._q: queue.SimpleQueue = queue.SimpleQueue()
+        self._stop = threading.Event()
+        self._thread = None
+        self.stats = {"batches": 0, "sequences": 0, "tokens": 0, "time_s": 0.0}
+
+    def start(self):
+        if self._thread is None:
+            self._stop.clear()
+            self._thread = threading.Thread(target=self._loop, daemon=True, name="lmx-embed")
+            self._thread.start()
+
+    def stop(self):
+        self._stop.set()
+        self._q.put(None)
+        if self._thread is not None:
+            self._thread.join(timeout=10)
+            self._thread = None
+
+    def _truncate(self, seqs):
+        return [s[: self.max_seq_len] if s else [0] for s in seqs]
+
+    # synchronous API (worker jobs, tests)
+    def embed_sync(self, seqs: list[list[int]], dims: int | None = None) -> list[list[float]]:
+        return self._run([EmbedRequest(self._truncate(seqs), dims)])[0]
+
+    # asyncio API
+    async def embed(self, seqs: list[list[int]], dims: int | None = None) -> list[list[float]]:
+        loop = asyncio.get_running_loop()
+        req = EmbedRequest(self._truncate(seqs), dims, loop.create_future(), loop)
+        self._q.put(req)
+        return await req.future
+
+    def _loop(self):
+        if self.device.type == "cuda":
+            torch.cuda.set_device(self.device)
+        pending: list[EmbedRequest] = []
+        while not self._stop.is_set():
+            if not pending:
+                item = self._q.get()
+                if item is None:
+                    break
+                pending.append(item)
+            while True:  # drain whatever else is waiting
+                try:
+                    item = self._q.get_nowait()
+                except queue.Empty:
+                    break
+                if item is None:
+                    self._stop.set()
+                    break
+                pending.append(item)
+            batch, ntok = [], 0
+            while pending:
+                n = sum(len(s) for s in pending[0].seqs)
+                if batch and ntok + n > self.max_batch_tokens:
+                    break
+                batch.append(pending.pop(0))
+                ntok += n
+            try:
+                outs = self._run(batch)
+                for r, o in zip(batch, outs):
+                    self._deliver(r, o, None)
+            except Exception as e:
+                log.exception("embedding batch failed")
+                for r in batch:
+                    self._deliver(r, None, str(e))
+
+    @staticmethod
+    def _deliver(r: EmbedRequest, out, err):
+        r.result, r.error = out, err
+        r.done.set()
+        if r.future is not None:
+            def _set(f=r.future):
+                if f.done():
+                    return
+                if err is None:
+                    f.set_result(out)
+                else:
+                    f.set_exception(RuntimeError(err))
+            r.loop.call_soon_threadsafe(_set)
+
+    @torch.no_grad()
+    def _run(self, batch: list[EmbedRequest]) -> list[list[list[float]]]:
+        t0 = time.perf_counter()
+        seqs = [s for r in batch for s in r.seqs]
+        lens = [len(s) for s in seqs]
+        cu = [0]
+        for n in lens:
+            cu.append(cu[-1] + n)
+        flat = [t for s in seqs for t in s]
+        ids = torch.tensor(flat, dtype=torch.int32).to(self.device, non_blocking=True)
+        cu_t = torch.tensor(cu, dtype=torch.int32).to(self.device, non_blocking=True)
+        dims = {r.dims or self.cfg.embed_dim for r in batch}
+        fused = len(dims) == 1
+        if fused:
+            # pooling, Matryoshka truncation and L2 norm fused in one kernel (K9)
+            full = self.model.forward(ids, cu_t, lens, dims=dims.pop(), normalize=True).cpu()
+        else:
+            full = self.model.forward(ids, cu_t, lens, dims=None, normalize=False).cpu()
+        outs, k = [], 0
+        for r in batch:
+            e = full[k:k + len(r.seqs)]
+            k += len(r.seqs)
+            if not fused:
+                e = e[:, :r.dims or self.cfg.embed_dim]
+                e = e / e.norm(dim=-1, keepdim=True).clamp_min(1e-12)
+            outs.append(e.float().tolist())
+        self.stats["batches"] += 1
+        self.stats["sequences"] += len(seqs)
+        self.stats["tokens"] += len(flat)
+        self.stats["time_s"] += time.perf_counter() - t0
+        return outs

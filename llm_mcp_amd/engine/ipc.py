@@ -69,15 +69,21 @@ class _Conn:
 class EngineServer:
     """Serves one LLMEngine over a Unix socket (runs in the GPU process)."""
 
-    def __init__(self, engine, path: str, info: dict | None = None):
+    def __init__(self, engine, path: str, info: dict | None = None, embed_engine=None,
+                 fallback_sink=None):
         self.engine = engine
+        self.embed_engine = embed_engine
+        # events of requests not submitted over IPC (e.g. the worker's own job
+        # runner, an AsyncEngine on the same engine) go to the fallback sink
+        self.fallback_sink = fallback_sink
         self.path = path
         self.info = dict(info or {})
         self._conns: dict[int, _Conn] = {}
         self._req_conn: dict[int, tuple[int, int]] = {}   # engine id -> (conn id, client rid)
         self._ids = itertools.count(1)
         self._lock = threading.Lock()
-        engine.event_sink = self._sink
+        if engine is not None:
+            engine.event_sink = self._sink
         self._sock: socket.socket | None = None
 
     def start(self) -> None:
@@ -88,10 +94,16 @@ class EngineServer:
         s.listen(16)
         self._sock = s
         threading.Thread(target=self._accept, daemon=True, name="ipc-accept").start()
-        self.engine.start()
+        if self.engine is not None:
+            self.engine.start()
+        if self.embed_engine is not None:
+            self.embed_engine.start()
 
     def stop(self) -> None:
-        self.engine.stop()
+        if self.engine is not None:
+            self.engine.stop()
+        if self.embed_engine is not None:
+            self.embed_engine.stop()
         if self._sock is not None:
             self._sock.close()
         if os.path.exists(self.path):
@@ -132,6 +144,8 @@ class EngineServer:
                                 break
                     if eid is not None:
                         self.engine.abort(eid)
+                elif op == "embed":
+                    self._embed(c, msg)
                 elif op == "info":
                     info = dict(self.info)
                     info.update(self.engine_info())
@@ -148,8 +162,26 @@ class EngineServer:
             for k in dead:
                 self.engine.abort(k)
 
+    def _embed(self, c: _Conn, msg: dict):
+        """Queue an embedding request on the batching embed engine; the reply
+        is sent from a helper thread once the batch containing it is done."""
+        if self.embed_engine is None:
+            c.send({"op": "emb", "tag": msg.get("tag"), "error": "no embedding model"})
+            return
+        from .embed_engine import EmbedRequest
+        req = EmbedRequest(self.embed_engine._truncate(msg["seqs"]), msg.get("dims"))
+        self.embed_engine._q.put(req)
+
+        def reply():
+            req.done.wait()
+            c.send({"op": "emb", "tag": msg.get("tag"), "vectors": req.result,
+                    "error": req.error})
+        threading.Thread(target=reply, daemon=True).start()
+
     def engine_info(self) -> dict:
         e = self.engine
+        if e is None:
+            return {"stats": dict(self.embed_engine.stats) if self.embed_engine else {}}
         s = e.sched
         return {"running": s.num_running, "waiting": s.num_waiting, "kv_usage": s.kv_usage,
                 "kv_free_blocks": s.kv_free_blocks, "stats": dict(e.stats)}
@@ -157,10 +189,12 @@ class EngineServer:
     # engine thread: one message per connection per step
     def _sink(self, evs: list[TokenEvent]):
         per: dict[int, list] = {}
+        other = []
         with self._lock:
             for e in evs:
                 m = self._req_conn.get(e.req.id)
                 if m is None:
+                    other.append(e)
                     continue
                 per.setdefault(m[0], []).append([m[1], e.token, e.logprob, e.finish])
                 if e.finish is not None:
@@ -170,6 +204,8 @@ class EngineServer:
             c = conns.get(cid)
             if c is not None:
                 c.send({"op": "ev", "ev": lst})
+        if other and self.fallback_sink is not None:
+            self.fallback_sink(other)
 
 
 class EngineClient:
@@ -214,6 +250,13 @@ class EngineClient:
                     f = self._info_waiters.pop(msg.get("tag"), None)
                     if f is not None and not f.done():
                         f.set_result(msg["info"])
+                elif op == "emb":
+                    f = self._info_waiters.pop(msg.get("tag"), None)
+                    if f is not None and not f.done():
+                        if msg.get("error"):
+                            f.set_exception(RuntimeError(msg["error"]))
+                        else:
+                            f.set_result(msg["vectors"])
         except (asyncio.IncompleteReadError, ConnectionError):
             pass
         finally:
@@ -232,6 +275,22 @@ class EngineClient:
         self._info_waiters[tag] = f
         self._send({"op": "info", "tag": tag})
         return await asyncio.wait_for(f, timeout)
+
+    async def embed(self, seqs, dims=None) -> list[list[float]]:
+        tag = next(self._ids)
+        f = asyncio.get_running_loop().create_future()
+        self._info_waiters[tag] = f
+        self._send({"op": "embed", "tag": tag, "seqs": [list(s) for s in seqs], "dims": dims})
+        return await f
+
+    async def complete(self, prompt_ids, params, priority=0):
+        toks, lps, fin = [], [], None
+        async for it in self.generate(prompt_ids, params, priority):
+            if it.token >= 0:
+                toks.append(it.token)
+                lps.append(it.logprob)
+            fin = it.finish
+        return toks, lps, fin
 
     async def generate(self, prompt_ids, params: SamplingParams, priority: int = 0,
                        stats: RequestStats | None = None):

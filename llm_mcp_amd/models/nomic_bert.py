@@ -1,0 +1,113 @@
+"""nomic-embed-text (NomicBert) encoder for ``/v1/embeddings`` and embed jobs.
+
+What the reference delegated to Ollama ``/api/embed``
+(core/internal/api/handlers.go:1942-2015, worker/llm_worker/main.py:246-261)
+runs in-process on the GPU:
+
+  embed_gather(word) + token_type row -> LayerNorm
+  per layer (post-norm BERT with rotary and SwiGLU):
+      QKV = gemm_nt (K7, hand-written MFMA GEMM)            [T, 3d]
+      rope + scatter K/V into a per-batch paged scratch cache (K2/K5)
+      bidirectional varlen attention on the paged kernel (K3, causal=0)
+      h = LayerNorm(x + gemm_nt(attn, Wo))                  (fused residual LN)
+      g = silu_mul(gemm_nt(h, [fc12; fc11]))                (K8)
+      x = LayerNorm(h + gemm_nt(g, fc2))
+  masked mean pool + Matryoshka truncation + L2 normalise (K9)
+
+All projections run on the hand-written gfx950 GEMM (``ops.gemm_nt``); the
+sequences of a batch are packed (cu_seqlens), never padded.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from .. import ops
+from ..ops import ref
+from .config import NomicBertConfig
+
+PAGE = 32
+
+
+class NomicBertModel:
+    def __init__(self, cfg: NomicBertConfig, device="cuda", dtype=torch.bfloat16, seed: int = 0,
+                 weights: dict | None = None):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.dtype = dtype
+        self.H, self.D = cfg.num_heads, cfg.head_dim
+        self.scale = 1.0 / math.sqrt(self.D)
+        self.cos_sin = ref.rope_cos_sin(cfg.max_position, self.D, cfg.rope_theta, self.device)
+        self.w = weights or self._random_weights(seed)
+
+    def _random_weights(self, seed):
+        cfg, dev, dt = self.cfg, self.device, self.dtype
+        g = torch.Generator(device=dev)
+        g.manual_seed(seed + 77)
+        d, I = cfg.hidden_size, cfg.intermediate_size
+
+        def rnd(*shape, std=0.02):
+            t = torch.empty(shape, dtype=dt, device=dev)
+            t.normal_(0.0, std, generator=g)
+            return t
+
+        ones = lambda: torch.ones(d, dtype=dt, device=dev)
+        zeros = lambda: torch.zeros(d, dtype=dt, device=dev)
+        layers = [{"wqkv": rnd(3 * d, d), "wo": rnd(d, d), "w_gate_up": rnd(2 * I, d),
+                   "w_down": rnd(d, I), "ln1_w": ones(), "ln1_b": zeros(), "ln2_w": ones(),
+                   "ln2_b": zeros()} for _ in range(cfg.num_layers)]
+        return {"word": rnd(cfg.vocab_size, d, std=1.0), "type": rnd(cfg.type_vocab_size, d),
+                "emb_ln_w": ones(), "emb_ln_b": zeros(), "layers": layers}
+
+    def _linear(self, x, w, residual=None):
+        if ops.gemm_nt_supported(w.shape[0], w.shape[1]):
+            return ops.gemm_nt(x, w, residual=residual)
+        y = torch.nn.functional.linear(x, w)
+        return y if residual is None else y + residual
+
+    @torch.no_grad()
+    def forward(self, ids: torch.Tensor, cu: torch.Tensor, lens: list[int],
+                dims: int | None = None, normalize: bool = True) -> torch.Tensor:
+        """ids int32 [T] packed, cu int32 [S+1] -> fp32 [S, dims] embeddings."""
+        cfg, w = self.cfg, self.w
+        H, D, d = self.H, self.D, cfg.hidden_size
+        T, S = ids.numel(), len(lens)
+        dev = self.device
+        # per-sequence page-aligned slots in a scratch paged K/V cache
+        pages = [max(1, math.ceil(n / PAGE)) for n in lens]
+        page_off = [0]
+        for p in pages:
+            page_off.append(page_off[-1] + p)
+        NB = page_off[-1]
+        slots, pos, tiles, bt = [], [], [], torch.zeros((S, max(pages)), dtype=torch.int32)
+        qpt = ops.prefill_q_per_tile(H, H)
+        for s, n in enumerate(lens):
+            base = page_off[s] * PAGE
+            slots.extend(range(base, base + n))
+            pos.extend(range(n))
+            bt[s, :pages[s]] = torch.arange(page_off[s], page_off[s + 1], dtype=torch.int32)
+            for q0 in range(0, n, qpt):
+                tiles += [s, q0]
+        meta = torch.tensor(slots + pos + tiles, dtype=torch.int32).to(dev, non_blocking=True)
+        slots_t, pos_t, tiles_t = meta[:T], meta[T:2 * T], meta[2 * T:]
+        bt = bt.to(dev, non_blocking=True)
+        ctx = torch.tensor(lens, dtype=torch.int32).to(dev, non_blocking=True)
+        kc = torch.zeros((NB, H, PAGE, D), dtype=self.dtype, device=dev)
+        vc = torch.zeros((NB, H, D, PAGE), dtype=self.dtype, device=dev)
+
+        x = ops.embed_gather(w["word"], ids)
+        x = ops.layer_norm(x, w["emb_ln_w"], w["emb_ln_b"], cfg.ln_eps,
+                           residual=w["type"][0:1].expand(T, d).contiguous())
+        attn = torch.empty((T, H * D), dtype=self.dtype, device=dev)
+        for L in w["layers"]:
+            qkv = self._linear(x, L["wqkv"])
+            ops.rope_and_cache(qkv, pos_t, self.cos_sin, H, H, D, slots_t, kc, vc)
+            ops.paged_prefill_attention(qkv, kc, vc, bt, cu, ctx, tiles_t, self.scale, attn,
+                                        causal=False, Hq=H)
+            o = self._linear(attn, L["wo"])
+            h = ops.layer_norm(o, L["ln1_w"], L["ln1_b"], cfg.ln_eps, residual=x)
+            g = ops.silu_mul(self._linear(h, L["w_gate_up"]))
+            m = self._linear(g, L["w_down"])
+            x = ops.layer_norm(m, L["ln2_w"], L["ln2_b"], cfg.ln_eps, residual=h)
+        return ops.mean_pool_l2(x, cu, dims or cfg.embed_dim, normalize)

@@ -35,7 +35,7 @@ class Metrics:
         self.discovery_duration = Histogram("llmcore_discovery_duration_seconds",
                                             "Discovery duration", registry=r)
         self.embedding_tokens = Counter("llmcore_embedding_input_tokens_total",
-                                        "Embedding input tokens", ["model"], registry=r)
+                                        "Embedding input tokens", ["model", "device"], registry=r)
         self.chat_requests_c = Counter("llmcore_chat_requests_total", "Chat requests",
                                        ["model", "provider", "status"], registry=r)
         self.chat_duration_h = Histogram(

@@ -1,0 +1,138 @@
+"""Claim -> heartbeat -> execute -> complete/fail loop of a GPU worker
+(reference: worker/llm_worker/main.py:536-599).
+
+Differences, MI355X-first:
+  * concurrency: a GPU worker keeps up to ``capacity`` jobs in flight, all fed
+    to the same continuous-batching engine (the reference ran one job at a time
+    per worker process);
+  * wake-up: long-poll claims (``wait_ms``) instead of a 1.5 s idle sleep;
+  * every call carries the lease token, so a worker whose lease expired cannot
+    overwrite the new owner's result;
+  * heartbeat every max(5, lease/2) s per in-flight job;
+  * a GPU/engine failure fails the job (requeued by attempts) and reports the
+    device offline so discovery/routing stop sending it work.
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+import os
+import socket
+import time
+
+from .jobs import JobError, JobRunner
+
+log = logging.getLogger("lmx.worker")
+
+NETWORK_TOKENS = ("connection refused", "timed out", "timeout", "no route",
+                  "network is unreachable")
+
+
+def should_mark_offline(exc: Exception) -> bool:
+    msg = str(exc).lower()
+    if "hip" in msg or "cuda" in msg or "device" in msg and "error" in msg:
+        return True
+    return any(t in msg for t in NETWORK_TOKENS)
+
+
+class WorkerAgent:
+    def __init__(self, client, runner: JobRunner, device_id: str, worker_id: str = "",
+                 kinds: list[str] | None = None, lease_s: int = 60, capacity: int = 64,
+                 name: str = "", tags: dict | None = None, mark_offline=None):
+        self.client = client  # rpc.client.CoreClient (sync; called via to_thread)
+        self.runner = runner
+        self.device_id = device_id
+        self.worker_id = worker_id
+        self.kinds = list(kinds or [])
+        self.lease_s = lease_s
+        self.capacity = capacity
+        self.name = name or socket.gethostname()
+        self.tags = dict(tags or {})
+        self.mark_offline = mark_offline  # callable(device_id, reason) or None
+        self.inflight: dict[str, asyncio.Task] = {}
+        self._stop = asyncio.Event()
+        self.stats = {"claimed": 0, "done": 0, "failed": 0, "lease_lost": 0}
+
+    async def register(self, retry_s: float = 2.0):
+        while not self._stop.is_set():
+            try:
+                self.worker_id = await asyncio.to_thread(
+                    self.client.register, self.worker_id, self.name, "rocm", "gfx950",
+                    socket.gethostname(), {**self.tags, "device_id": self.device_id})
+                log.info("registered as %s", self.worker_id)
+                return self.worker_id
+            except Exception as e:
+                log.warning("register failed: %s", e)
+                await asyncio.sleep(retry_s)
+
+    def stop(self):
+        self._stop.set()
+
+    async def run(self, max_jobs: int | None = None):
+        if not self.worker_id:
+            await self.register()
+        n = 0
+        while not self._stop.is_set():
+            if len(self.inflight) >= self.capacity:
+                await asyncio.wait(list(self.inflight.values()),
+                                   return_when=asyncio.FIRST_COMPLETED)
+                continue
+            try:
+                j = await asyncio.to_thread(self.client.claim, self.worker_id, self.kinds,
+                                            self.lease_s, self.device_id, 2000)
+            except Exception as e:
+                log.warning("claim failed: %s", e)
+                await asyncio.sleep(1.0)
+                continue
+            if j is None:
+                continue
+            self.stats["claimed"] += 1
+            t = asyncio.create_task(self._run_job(j))
+            self.inflight[j["id"]] = t
+            t.add_done_callback(lambda _t, jid=j["id"]: self.inflight.pop(jid, None))
+            n += 1
+            if max_jobs is not None and n >= max_jobs:
+                break
+        if self.inflight:
+            await asyncio.gather(*self.inflight.values(), return_exceptions=True)
+
+    async def _heartbeat(self, jid: str, token: str):
+        period = max(5.0, self.lease_s / 2)
+        while True:
+            await asyncio.sleep(period)
+            try:
+                ok = await asyncio.to_thread(self.client.heartbeat, self.worker_id, jid,
+                                             self.lease_s, token)
+                if not ok:
+                    log.warning("lease lost for %s", jid)
+                    self.stats["lease_lost"] += 1
+                    return
+            except Exception as e:
+                log.warning("heartbeat %s failed: %s", jid, e)
+
+    async def _run_job(self, j: dict):
+        jid, token = j["id"], j.get("attempt_id") or ""
+        hb = asyncio.create_task(self._heartbeat(jid, token))
+        t0 = time.time()
+        try:
+            result, metrics = await self.runner.handle(j["kind"], j.get("payload") or {})
+            metrics = dict(metrics or {})
+            metrics.setdefault("ms", int((time.time() - t0) * 1000))
+            ok = await asyncio.to_thread(self.client.complete, self.worker_id, jid, result,
+                                         metrics, token)
+            self.stats["done" if ok else "lease_lost"] += 1
+        except Exception as e:
+            self.stats["failed"] += 1
+            log.warning("job %s failed: %s", jid, e)
+            try:
+                await asyncio.to_thread(self.client.fail, self.worker_id, jid, str(e),
+                                        {"ms": int((time.time() - t0) * 1000)}, token)
+            except Exception as e2:
+                log.warning("fail report for %s failed: %s", jid, e2)
+            if not isinstance(e, JobError) and should_mark_offline(e) and self.mark_offline:
+                try:
+                    await asyncio.to_thread(self.mark_offline, self.device_id, str(e))
+                except Exception:
+                    pass
+        finally:
+            hb.cancel()

@@ -1,0 +1,138 @@
+"""GPU worker process: ``python -m llm_mcp_amd.worker.main --gpu 0 ...``.
+
+Owns one MI355X (or, with --tp N, leads a tensor-parallel group launched by
+torch.distributed.run): builds the chat engine (and optionally the embedding
+engine) on its device, serves the synchronous OpenAI path to the API process
+over a Unix socket (engine/ipc.py) and claims async jobs from the core over
+gRPC, executing them in-process on the same continuous-batching engine.
+Replaces worker/llm_worker/main.py (which forwarded every job to Ollama over
+HTTP)."""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import logging
+import os
+import signal
+
+log = logging.getLogger("lmx.worker")
+
+
+def build_parser():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpu", type=int, default=int(os.environ.get("LOCAL_RANK", "0")))
+    ap.add_argument("--chat-model", default=os.environ.get("LMX_CHAT_MODEL", "llama-3-8b"))
+    ap.add_argument("--embed-model", default=os.environ.get("LMX_EMBED_MODEL", ""))
+    ap.add_argument("--socket", default="")
+    ap.add_argument("--core", default=os.environ.get("CORE_GRPC_ADDR", "127.0.0.1:9090"))
+    ap.add_argument("--no-jobs", action="store_true", help="serve the sync path only")
+    ap.add_argument("--max-num-seqs", type=int, default=int(os.environ.get("LMX_MAX_BATCH", "256")))
+    ap.add_argument("--max-batched-tokens", type=int, default=8192)
+    ap.add_argument("--max-model-len", type=int, default=8192)
+    ap.add_argument("--kv-fraction", type=float, default=0.6)
+    ap.add_argument("--lease-seconds", type=int, default=int(os.environ.get("WORKER_LEASE_SECONDS", "60")))
+    ap.add_argument("--weights", default="", help="safetensors dir of real weights (optional)")
+    ap.add_argument("--tp", type=int, default=1)
+    return ap
+
+
+def main(argv=None):
+    a = build_parser().parse_args(argv)
+    logging.basicConfig(level=os.environ.get("LOG_LEVEL", "INFO"))
+    import torch
+
+    from ..api.registry import LocalModel, ModelRegistry
+    from ..devices import rocm_enum
+    from ..engine.async_engine import AsyncEngine
+    from ..engine.engine import EngineConfig, LLMEngine
+    from ..engine.ipc import EngineServer
+    from ..models import config as mc
+    from ..models.tokenizer import for_model
+    from .agent import WorkerAgent
+    from .jobs import JobRunner
+
+    if a.tp > 1:
+        from ..parallel.tp_worker import run_tp_worker
+        return run_tp_worker(a)
+
+    torch.cuda.set_device(a.gpu)
+    dev = torch.device("cuda", a.gpu)
+    device_id = rocm_enum.device_id(a.gpu)
+    reg = ModelRegistry()
+    engine = embed = None
+    weights = None
+    if a.chat_model:
+        cfg = mc.resolve(a.chat_model)
+        if a.weights:
+            from ..models.weights import load_llama_weights
+            weights = load_llama_weights(a.weights, cfg, dev)
+        ecfg = EngineConfig(model=a.chat_model, max_num_seqs=a.max_num_seqs,
+                            max_batched_tokens=a.max_batched_tokens,
+                            max_model_len=a.max_model_len, kv_fraction=a.kv_fraction)
+        if a.embed_model:
+            ecfg.kv_fraction = min(ecfg.kv_fraction, 0.5)
+    if a.embed_model:
+        from ..engine.embed_engine import EmbeddingEngine
+        embed = EmbeddingEngine(mc.resolve(a.embed_model), dev)
+        reg.add(LocalModel(a.embed_model, "embed", device_id, embed,
+                           for_model(embed.cfg), embed.cfg, embed.max_seq_len, capacity=1024))
+    if a.chat_model:
+        engine = LLMEngine(ecfg, device=dev, weights=weights)
+        aeng = AsyncEngine(engine)
+        reg.add(LocalModel(a.chat_model, "chat", device_id, aeng, for_model(engine.cfg),
+                           engine.cfg, engine.max_model_len, capacity=a.max_num_seqs))
+    sock = a.socket or f"/tmp/lmx-{rocm_enum.host_id()}-gpu{a.gpu}.sock"
+    info = {"device_id": device_id, "models": {}}
+    if engine is not None:
+        info["models"][a.chat_model] = {"kind": "chat", "max_model_len": engine.max_model_len,
+                                        "capacity": a.max_num_seqs}
+    if embed is not None:
+        info["models"][a.embed_model] = {"kind": "embed", "max_model_len": embed.max_seq_len,
+                                         "capacity": 1024}
+    server = EngineServer(engine, sock, info, embed_engine=embed,
+                          fallback_sink=aeng._sink if engine is not None else None)
+    if engine is not None:
+        engine.event_sink = server._sink
+
+    async def run():
+        loop = asyncio.get_running_loop()
+        if engine is not None:
+            aeng.loop = loop
+        server.start()
+        log.info("GPU %d serving %s on %s", a.gpu, list(info["models"]), sock)
+        stop = asyncio.Event()
+        for sig in (signal.SIGINT, signal.SIGTERM):
+            loop.add_signal_handler(sig, stop.set)
+        agent = None
+        if not a.no_jobs:
+            from ..rpc.client import CoreClient
+            client = CoreClient(a.core)
+
+            def mark_offline(dev_id, reason):
+                import json
+                import urllib.request
+                url = os.environ.get("CORE_HTTP_URL", "http://127.0.0.1:8080").rstrip("/")
+                req = urllib.request.Request(url + "/v1/devices/offline", method="POST",
+                                             data=json.dumps({"device_id": dev_id,
+                                                              "reason": reason}).encode(),
+                                             headers={"Content-Type": "application/json"})
+                urllib.request.urlopen(req, timeout=5).read()
+
+            runner = JobRunner(reg, device_id, report_benchmark=lambda **kw: client.report_benchmark(**kw))
+            agent = WorkerAgent(client, runner, device_id,
+                                worker_id=os.environ.get("WORKER_ID", f"worker-{device_id}"),
+                                lease_s=a.lease_seconds, capacity=a.max_num_seqs,
+                                tags={"engine": True, "models": list(info["models"])},
+                                mark_offline=mark_offline)
+            task = asyncio.create_task(agent.run())
+        await stop.wait()
+        if agent is not None:
+            agent.stop()
+            task.cancel()
+        server.stop()
+
+    asyncio.run(run())
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,97 @@
+"""submit -> claim -> heartbeat -> complete with the GPU worker agent running
+its in-process engines on CPU (BASELINE config 1: plumbing, no GPU)."""
+import asyncio
+import threading
+import time
+
+import pytest
+
+from llm_mcp_amd.api.core import CoreState
+from llm_mcp_amd.api.registry import LocalModel, ModelRegistry
+from llm_mcp_amd.engine.async_engine import AsyncEngine
+from llm_mcp_amd.engine.embed_engine import EmbeddingEngine
+from llm_mcp_amd.engine.engine import EngineConfig, LLMEngine
+from llm_mcp_amd.models import config as mc
+from llm_mcp_amd.models.tokenizer import for_model
+from llm_mcp_amd.rpc.client import CoreClient
+from llm_mcp_amd.rpc.server import start_grpc
+from llm_mcp_amd.store.memory import MemoryStore
+from llm_mcp_amd.worker.agent import WorkerAgent
+from llm_mcp_amd.worker.jobs import JobRunner
+
+
+@pytest.fixture(scope="module")
+def core():
+    st = CoreState(store=MemoryStore())
+    loop = asyncio.new_event_loop()
+    box = {}
+
+    def run():
+        asyncio.set_event_loop(loop)
+        box["srv"], box["port"] = loop.run_until_complete(start_grpc(st, "127.0.0.1:0"))
+        loop.run_forever()
+
+    threading.Thread(target=run, daemon=True).start()
+    while "port" not in box:
+        time.sleep(0.01)
+    yield st, f"127.0.0.1:{box['port']}"
+    loop.call_soon_threadsafe(loop.stop)
+
+
+def test_worker_executes_engine_jobs(core):
+    st, addr = core
+    client = CoreClient(addr)
+    eng = LLMEngine(EngineConfig(model="tiny-llama", max_num_seqs=8, max_batched_tokens=256,
+                                 max_model_len=512, use_graphs=False), device="cpu")
+    emb = EmbeddingEngine(mc.resolve("tiny-nomic"), device="cpu")
+
+    async def go():
+        aeng = AsyncEngine(eng)
+        aeng.start(asyncio.get_running_loop())
+        emb.start()
+        reg = ModelRegistry()
+        reg.add(LocalModel("tiny-llama", "chat", "n:gpu0", aeng, for_model(eng.cfg), eng.cfg,
+                           512, 8))
+        reg.add(LocalModel("tiny-nomic", "embed", "n:gpu0", emb, for_model(emb.cfg), emb.cfg,
+                           512, 64))
+        runner = JobRunner(reg, "n:gpu0",
+                           report_benchmark=lambda **kw: client.report_benchmark(**kw))
+        st.store.set_pricing("tiny-llama", 1.0, 2.0)
+        ids = {
+            "gen": client.submit("engine.generate", {"model": "tiny-llama", "prompt": "hello",
+                                                      "options": {"max_tokens": 5,
+                                                                  "temperature": 0,
+                                                                  "ignore_eos": True},
+                                                      "_price_in_1m": 1.0,
+                                                      "_price_out_1m": 2.0}),
+            "alias": client.submit("ollama.generate", {"model": "tiny-llama",
+                                                        "messages": [{"role": "user",
+                                                                      "content": "hi"}],
+                                                        "options": {"max_tokens": 3}}),
+            "emb": client.submit("engine.embed", {"model": "tiny-nomic", "prompt": "doc"}),
+            "bench": client.submit("benchmark.engine.generate",
+                                   {"model": "tiny-llama", "max_tokens": 8, "prompt_tokens": 16,
+                                    "concurrency": 2}),
+            "echo": client.submit("echo", {"a": 1}),
+        }
+        agent = WorkerAgent(client, runner, "n:gpu0", lease_s=30, capacity=8)
+        await agent.run(max_jobs=len(ids))
+        aeng.stop()
+        emb.stop()
+        return ids, agent
+
+    ids, agent = asyncio.new_event_loop().run_until_complete(go())
+    jobs = {k: client.get(v) for k, v in ids.items()}
+    assert all(j["status"] == "done" for j in jobs.values()), jobs
+    g = jobs["gen"]["result"]
+    assert g["ok"] and g["provider"] == "local" and g["tokens_out"] == 5 and g["device_id"] == "n:gpu0"
+    assert g["cost"].endswith("$") and float(g["cost"][:-1]) > 0
+    assert jobs["alias"]["result"]["tokens_out"] <= 3
+    assert len(jobs["emb"]["result"]["data"]["embedding"]) == 256
+    b = jobs["bench"]["result"]
+    assert b["tokens_out"] == 16 and b["tps"] > 0
+    assert st.store.list_benchmarks(1)[0]["model_id"] == "tiny-llama"
+    assert jobs["echo"]["result"] == {"ok": True, "echo": {"a": 1}}
+    # RecordCost on the gRPC completion path (reference gap fixed)
+    assert st.store.cost_summary(0)["total_jobs"] >= 1
+    assert agent.stats["done"] == 5
