@@ -102,6 +102,15 @@ class ControlPlane:
         r.add_route("*", "/v1/models/stats", self.models_stats)
         r.add_route("*", "/v1/models/sync", self.models_sync)
         r.add_route("*", "/v1/models", self.models_list)
+        r.add_route("GET", "/v1/alerts/snapshot", self.alerts_snapshot)
+
+    async def alerts_snapshot(self, request):
+        """Telemetry input (telemetry/alerts.py): counts, GPU devices, failed jobs."""
+        from ..telemetry.alerts import snapshot_from_store
+        thr = to_int(os.environ.get("ALERT_FAIL_THRESHOLD", "3"), 3)
+        temp = float(os.environ.get("LMX_ALERT_TEMP_C", "95"))
+        return write_json(200, await self.db(snapshot_from_store, self.store, self.st.circuit,
+                                             thr, temp))
 
     @staticmethod
     def _guard(request, method):
