@@ -149,6 +149,13 @@ def main() -> None:
         r = run_wave()
         log(f"warmup {w}: {r['tokens']} tok in {r['elapsed']:.2f}s ({r['tok_s']:.0f} tok/s), "
             f"ttft p50 {r['ttft_p50'] * 1e3:.0f} ms")
+    for k in engine.stats:
+        engine.stats[k] = type(engine.stats[k])(0)
+    import psutil
+    procs = {"engine": psutil.Process(), "loadgen": psutil.Process(client.pid)}
+    if api_proc is not None:
+        procs["api"] = psutil.Process(api_proc.pid)
+    cpu0 = {k: sum(p.cpu_times()[:2]) for k, p in procs.items()}
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -162,6 +169,14 @@ def main() -> None:
     barrier()
     elapsed = time.perf_counter() - t0
 
+    log("process CPU utilisation over the timed waves: " + ", ".join(
+        f"{k} {(sum(p.cpu_times()[:2]) - cpu0[k]) / elapsed * 100:.0f}%" for k, p in procs.items()))
+    st = engine.stats
+    ns = max(1, st["steps"])
+    log("engine host phases (ms/step avg over all steps): " + ", ".join(
+        f"{k[2:]} {st[k] / ns * 1e3:.3f}" for k in st if k.startswith("t_")) +
+        f"; steps {st['steps']} graph {st['graph_steps']}, decode step "
+        f"{st['decode_step_s'] / max(1, st['graph_steps']) * 1e3:.2f} ms")
     tokens = sum(r["tokens"] for r in results)
     ttfts = [t for r in results for t in r["ttfts"]]
     mine = {"tokens": tokens, "elapsed": elapsed, "ttfts": ttfts,

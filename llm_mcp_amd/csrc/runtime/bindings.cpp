@@ -62,7 +62,9 @@ PYBIND11_MODULE(_lmx_runtime, m) {
            py::arg("block_size"), py::arg("max_num_seqs"), py::arg("max_batched_tokens"),
            py::arg("max_model_len"), py::arg("prefix_cache") = true)
       .def("add", &Scheduler::add, py::arg("id"), py::arg("prompt"), py::arg("max_new"),
-           py::arg("stop_ids"), py::arg("ignore_eos") = false, py::arg("priority") = 0)
+           py::arg("stop_ids"), py::arg("ignore_eos") = false, py::arg("priority") = 0,
+           py::arg("temperature") = 1.f, py::arg("top_k") = 0, py::arg("top_p") = 1.f,
+           py::arg("seed") = 0)
       .def("abort", &Scheduler::abort)
       .def("schedule", [](Scheduler& s, int q_per_tile) {
         const StepPlan& p = s.schedule(q_per_tile);
@@ -77,6 +79,11 @@ PYBIND11_MODULE(_lmx_runtime, m) {
         d["block_tables"] = to_np(p.block_tables);
         d["sample_rows"] = to_np(p.sample_rows);
         d["sample_seq"] = to_np(p.sample_seq);
+        d["temp"] = to_np(p.sample_temp);
+        d["topk"] = to_np(p.sample_topk);
+        d["topp"] = to_np(p.sample_topp);
+        d["seeds"] = to_np(p.sample_seed);
+        d["offs"] = to_np(p.sample_off);
         d["prefill_tiles"] = to_np(p.prefill_tiles);
         d["num_decode"] = p.num_decode;
         d["max_blocks"] = p.max_blocks;

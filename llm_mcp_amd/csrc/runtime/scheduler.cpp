@@ -17,7 +17,8 @@ Scheduler::Scheduler(int num_blocks, int block_size, int max_num_seqs, int max_b
 }
 
 void Scheduler::add(int64_t id, const std::vector<int32_t>& prompt, int max_new,
-                    const std::vector<int32_t>& stop_ids, bool ignore_eos, int priority) {
+                    const std::vector<int32_t>& stop_ids, bool ignore_eos, int priority,
+                    float temperature, int top_k, float top_p, int64_t seed) {
   if (seqs_.count(id)) throw std::invalid_argument("duplicate sequence id");
   if (prompt.empty()) throw std::invalid_argument("empty prompt");
   if ((int)prompt.size() >= max_model_len_)
@@ -32,6 +33,10 @@ void Scheduler::add(int64_t id, const std::vector<int32_t>& prompt, int max_new,
   s->stop_ids = stop_ids;
   s->ignore_eos = ignore_eos;
   s->priority = priority;
+  s->temperature = temperature;
+  s->top_k = top_k;
+  s->top_p = top_p;
+  s->seed = seed;
   s->arrival = arrival_++;
   Seq* raw = s.get();
   seqs_[id] = std::move(s);
@@ -85,6 +90,8 @@ const StepPlan& Scheduler::schedule(int q_per_tile) {
   p.input_ids.clear(); p.positions.clear(); p.slots.clear();
   p.seq_ids.clear(); p.qlens.clear(); p.context_lens.clear(); p.cu_q.clear();
   p.block_tables.clear(); p.sample_rows.clear(); p.sample_seq.clear();
+  p.sample_temp.clear(); p.sample_topp.clear(); p.sample_topk.clear(); p.sample_off.clear();
+  p.sample_seed.clear();
   p.prefill_tiles.clear(); p.preempted.clear();
   p.num_decode = 0; p.num_tokens = 0; p.num_prefill_tokens = 0; p.max_context = 0;
   p.max_blocks = max_blocks_;
@@ -126,8 +133,14 @@ const StepPlan& Scheduler::schedule(int q_per_tile) {
     (n == 1 ? decodes : prefills).push_back(s);
   }
 
-  // 3. flatten (decode rows first)
+  // 3. flatten (decode rows first).  Block-table rows are only as wide as
+  // the longest table in this plan (the kernels take the row stride), so the
+  // per-step upload scales with the live context, not with max_model_len.
   const int bs = bm_.block_size();
+  int width = 1;
+  for (Seq* s : decodes) width = std::max(width, (int)bm_.table(s->id).size());
+  for (Seq* s : prefills) width = std::max(width, (int)bm_.table(s->id).size());
+  p.max_blocks = width;
   p.cu_q.push_back(0);
   auto emit = [&](Seq* s, bool is_prefill, int prefill_idx) {
     const int n = s->scheduled;
@@ -146,11 +159,16 @@ const StepPlan& Scheduler::schedule(int q_per_tile) {
     p.cu_q.push_back(p.num_tokens);
     p.max_context = std::max(p.max_context, ctx);
     const size_t off = p.block_tables.size();
-    p.block_tables.resize(off + max_blocks_, 0);
+    p.block_tables.resize(off + width, 0);
     std::copy(tab.begin(), tab.end(), p.block_tables.begin() + off);
     if (ctx == (int)s->tokens.size()) {
       p.sample_rows.push_back(row0 + n - 1);
       p.sample_seq.push_back((int)plan_seqs_.size());
+      p.sample_temp.push_back(s->temperature);
+      p.sample_topk.push_back(s->top_k);
+      p.sample_topp.push_back(s->top_p);
+      p.sample_seed.push_back(s->seed);
+      p.sample_off.push_back(s->num_generated);
     }
     if (is_prefill) {
       p.num_prefill_tokens += n;

@@ -41,6 +41,11 @@ struct Seq {
   int64_t arrival = 0;
   bool ignore_eos = false;
   std::vector<int32_t> stop_ids;
+  // sampling parameters travel with the sequence so the plan carries them
+  // as flat per-sample-row arrays (no per-request host work per step)
+  float temperature = 1.f, top_p = 1.f;
+  int top_k = 0;
+  int64_t seed = 0;
   int status = WAITING;
   int finish = FR_NONE;
   int scheduled = 0;            // tokens scheduled in the current plan
@@ -55,9 +60,12 @@ struct StepPlan {
   std::vector<int32_t> block_tables;               // S x max_blocks (0-padded)
   std::vector<int32_t> sample_rows;                // token rows whose logits are sampled
   std::vector<int32_t> sample_seq;                 // index into seq_ids for each sample row
+  std::vector<float> sample_temp, sample_topp;     // per sample row
+  std::vector<int32_t> sample_topk, sample_off;    // sample_off = tokens generated so far
+  std::vector<int64_t> sample_seed;
   std::vector<int32_t> prefill_tiles;              // (prefill-seq index, q_start) pairs
   int num_decode = 0;                              // first num_decode sequences have qlen 1
-  int max_blocks = 0;
+  int max_blocks = 0;                              // row width of block_tables (this plan)
   int num_tokens = 0;
   int num_prefill_tokens = 0;
   int max_context = 0;
@@ -70,7 +78,8 @@ class Scheduler {
             int max_model_len, bool prefix_cache);
 
   void add(int64_t id, const std::vector<int32_t>& prompt, int max_new,
-           const std::vector<int32_t>& stop_ids, bool ignore_eos, int priority);
+           const std::vector<int32_t>& stop_ids, bool ignore_eos, int priority,
+           float temperature = 1.f, int top_k = 0, float top_p = 1.f, int64_t seed = 0);
   bool abort(int64_t id);
   // q_per_tile: queries per prefill workgroup (64 / G for the paged prefill kernel)
   const StepPlan& schedule(int q_per_tile);

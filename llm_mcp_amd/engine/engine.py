@@ -119,6 +119,8 @@ class _Packer:
         return out
 
 
+_PLAN_KEY = {"ids": "input_ids", "pos": "positions", "ctx": "context_lens"}
+
 _TORCH_DT = {np.dtype(np.int32): torch.int32, np.dtype(np.int64): torch.int64,
              np.dtype(np.float32): torch.float32}
 
@@ -188,9 +190,17 @@ class LLMEngine:
         self.graphs: dict[int, dict] = {}
         self.stats = {"steps": 0, "decode_steps": 0, "graph_steps": 0, "prefill_tokens": 0,
                       "generated_tokens": 0, "step_time_s": 0.0, "finished": 0,
-                      "t_schedule": 0.0, "t_gpu": 0.0, "t_update": 0.0, "t_events": 0.0}
+                      "t_schedule": 0.0, "t_launch": 0.0, "t_events": 0.0, "t_wait": 0.0,
+                      "t_update": 0.0, "t_gpu": 0.0, "decode_step_s": 0.0}
+        self._pending = None
+        self._fetch_cpu = None
+        if self.device.type == "cuda":
+            self._hout = torch.zeros((2, ecfg.max_num_seqs), dtype=torch.int32, pin_memory=True)
+            self._hout_np = self._hout.numpy()
+            self._out_ev = torch.cuda.Event()
         if ecfg.use_graphs and self.device.type == "cuda":
             self._capture_graphs()
+        self._bucket_list = sorted(self.graphs)
 
     # ------------------------------------------------------------ memory ----
     def _alloc_kv(self):
@@ -322,6 +332,7 @@ class LLMEngine:
                 self._wake.clear()
 
     def _fail_all(self, why: str):
+        self._pending = None
         evs = []
         for rid, req in list(self._reqs.items()):
             self.sched.abort(rid)
@@ -350,9 +361,11 @@ class LLMEngine:
                 break
             p = req.params
             stop_ids = list(p.stop_token_ids) + list(getattr(self.cfg, "eos_token_ids", ()))
+            seed = p.seed if p.seed is not None else (req.id * 2654435761) & 0x7FFFFFFF
             try:
                 self.sched.add(req.id, list(req.prompt_ids), int(p.max_tokens), stop_ids,
-                               bool(p.ignore_eos), int(req.priority))
+                               bool(p.ignore_eos), int(req.priority), float(p.temperature),
+                               int(p.top_k), float(p.top_p), int(seed))
                 self._reqs[req.id] = req
             except Exception as e:
                 req.finished = True
@@ -361,65 +374,79 @@ class LLMEngine:
             self.event_sink(evs)
 
     # -------------------------------------------------------------- step ----
-    def _sampling_arrays(self, seq_ids: np.ndarray, sample_seq: np.ndarray, n_rows: int):
-        temp = np.zeros(n_rows, np.float32)
-        topk = np.zeros(n_rows, np.int32)
-        topp = np.ones(n_rows, np.float32)
-        seeds = np.zeros(n_rows, np.int64)
-        offs = np.zeros(n_rows, np.int32)
-        for i, si in enumerate(sample_seq):
-            req = self._reqs[int(seq_ids[si])]
-            p = req.params
-            temp[i] = p.temperature
-            topk[i] = p.top_k
-            topp[i] = p.top_p
-            seeds[i] = p.seed if p.seed is not None else (req.id * 2654435761) & 0x7FFFFFFF
-            offs[i] = req.num_generated
-        return temp, topk, topp, seeds, offs
-
     def step(self) -> bool:
+        """One engine step, software-pipelined against the GPU:
+
+            schedule(n) -> upload + launch(n) -> emit events of step n-1
+            -> wait for step n's tokens -> scheduler.update(n)
+
+        Building and delivering step n-1's events (TokenEvents, IPC msgpack,
+        SSE wake-ups) overlaps step n's kernels, so the host critical path is
+        only schedule + upload + launch + update (all native / array code;
+        sampling parameters come out of the native plan as flat arrays)."""
         self._drain()
         if not self.sched.has_work:
+            self._flush_pending()
             return False
         t0 = time.perf_counter()
         plan = self.sched.schedule(self.q_per_tile)
         T = plan["num_tokens"]
         if T == 0:
+            self._flush_pending()
             return False
-        seq_ids = plan["seq_ids"]
-        S = len(seq_ids)
+        S = len(plan["seq_ids"])
         nd = plan["num_decode"]
-        sample_seq = plan["sample_seq"]
-        N = len(sample_seq)
-        temp, topk, topp, seeds, offs = self._sampling_arrays(seq_ids, sample_seq, N)
-        t1 = time.perf_counter()
+        N = len(plan["sample_seq"])
         bucket = None
         if nd == S == T and self.graphs:
-            bucket = next((b for b in sorted(self.graphs) if b >= nd), None)
+            bucket = next((b for b in self._bucket_list if b >= nd), None)
+        t1 = time.perf_counter()
         if bucket is not None:
-            toks, lps = self._run_graph(plan, bucket, temp, topk, topp, seeds, offs)
+            tok, lp = self._run_graph(plan, bucket)
         else:
-            toks, lps = self._run_eager(plan, temp, topk, topp, seeds, offs)
+            tok, lp = self._run_eager(plan)
+        self._start_fetch(tok, lp, N)
         t2 = time.perf_counter()
-        finished = self.sched.update(toks[:N])
+        self._flush_pending()
         t3 = time.perf_counter()
-        dt = t3 - t0
+        toks, lps = self._finish_fetch(N)
+        t4 = time.perf_counter()
+        finished = self.sched.update(toks)
+        t5 = time.perf_counter()
+        self._pending = (plan["seq_ids"], plan["sample_seq"], toks, lps, finished)
+        if not self.sched.has_work:
+            self._flush_pending()
         st = self.stats
         st["t_schedule"] += t1 - t0
-        st["t_gpu"] += t2 - t1
-        st["t_update"] += t3 - t2
+        st["t_launch"] += t2 - t1
+        st["t_events"] += t3 - t2
+        st["t_wait"] += t4 - t3
+        st["t_update"] += t5 - t4
+        st["t_gpu"] += t4 - t1
         st["steps"] += 1
-        st["step_time_s"] += dt
+        st["step_time_s"] += t5 - t0
         st["decode_steps"] += int(nd == S)
         st["graph_steps"] += int(bucket is not None)
+        if bucket is not None:
+            st["decode_step_s"] += t5 - t0
         st["prefill_tokens"] += plan["num_prefill_tokens"]
         st["generated_tokens"] += N
+        return True
+
+    def _flush_pending(self):
+        """Turn the previous step's sampled tokens into TokenEvents."""
+        pend, self._pending = self._pending, None
+        if pend is None:
+            return
+        seq_ids, sample_seq, toks, lps, finished = pend
         fin = {rid: FINISH_REASONS.get(r, "stop") for rid, r in finished}
         evs = []
         now = time.time()
-        for i in range(N):
-            rid = int(seq_ids[sample_seq[i]])
-            req = self._reqs.get(rid)
+        reqs = self._reqs
+        rids = seq_ids[sample_seq].tolist()
+        tl, ll = toks.tolist(), lps.tolist()
+        for i, rid in enumerate(rids):
+            req = reqs.get(rid)
             if req is None:
                 continue
             if req.num_generated == 0:
@@ -428,15 +455,13 @@ class LLMEngine:
             reason = fin.get(rid)
             if reason is not None:
                 req.finished = True
-                self._reqs.pop(rid, None)
-                st["finished"] += 1
-            evs.append(TokenEvent(req, int(toks[i]), float(lps[i]), reason))
+                del reqs[rid]
+                self.stats["finished"] += 1
+            evs.append(TokenEvent(req, tl[i], ll[i], reason))
         if evs and self.event_sink:
             self.event_sink(evs)
-        st["t_events"] += time.perf_counter() - t3
-        return True
 
-    def _run_eager(self, plan, temp, topk, topp, seeds, offs):
+    def _run_eager(self, plan):
         T = plan["num_tokens"]
         S = len(plan["seq_ids"])
         mb = plan["max_blocks"]
@@ -447,38 +472,48 @@ class LLMEngine:
             ("bt", plan["block_tables"].reshape(S, mb)),
             ("tiles", plan["prefill_tiles"] if len(plan["prefill_tiles"]) else
              np.zeros(2, np.int32)),
-            ("rows", rows), ("temp", temp), ("topk", topk), ("topp", topp), ("seeds", seeds),
-            ("offs", offs)])
+            ("rows", rows), ("temp", plan["temp"]), ("topk", plan["topk"]),
+            ("topp", plan["topp"]), ("seeds", plan["seeds"]), ("offs", plan["offs"])])
         inp = StepInputs(d["ids"], d["pos"], d["slots"], plan["num_decode"], d["bt"], d["ctx"],
                          d["cu"], d["tiles"], d["rows"], T, S)
         ws = self.decode_ws
         logits = self.model.forward(inp, self.k_caches, self.v_caches, ws, self.ecfg.part_tokens)
-        tok, lp = ops.sample(logits, d["temp"], d["topk"], d["topp"], d["seeds"], d["offs"])
-        return self._fetch(tok, lp)
+        return ops.sample(logits, d["temp"], d["topk"], d["topp"], d["seeds"], d["offs"])
 
-    def _run_graph(self, plan, B, temp, topk, topp, seeds, offs):
+    def _run_graph(self, plan, B):
         g, h = self._gbuf, self._gmeta.h
         n = len(plan["seq_ids"])
         mb = plan["max_blocks"]
         # rows n..B-1 are padding: no cache write (slot -1), a 1-token context
-        for k, a, fill in (("ids", plan["input_ids"], 0), ("pos", plan["positions"], 0),
-                           ("slots", plan["slots"], -1), ("ctx", plan["context_lens"], 1),
-                           ("temp", temp, 0), ("topk", topk, 0), ("topp", topp, 1),
-                           ("seeds", seeds, 0), ("offs", offs, 0)):
-            h[k][:n] = a
-            h[k][n:B] = fill
-        h["bt"][:n] = plan["block_tables"].reshape(n, mb)
-        h["bt"][n:B] = 0
+        for k, fill in (("ids", 0), ("pos", 0), ("slots", -1), ("ctx", 1), ("temp", 0),
+                        ("topk", 0), ("topp", 1), ("seeds", 0), ("offs", 0)):
+            a = h[k]
+            a[:n] = plan[_PLAN_KEY.get(k, k)]
+            a[n:B] = fill
+        # only the live columns: stale entries beyond a row's context are
+        # never read (and always hold valid page ids)
+        h["bt"][:n, :mb] = plan["block_tables"].reshape(n, mb)
+        h["bt"][n:B, 0] = 0
         self._gmeta.upload()
         self.graphs[B]["graph"].replay()
-        return self._fetch(g["tok"][:B], g["lp"][:B])
+        return g["tok"][:B], g["lp"][:B]
 
-    def _fetch(self, tok: torch.Tensor, lp: torch.Tensor):
-        if tok.is_cuda:
-            both = torch.cat([tok.view(torch.float32), lp]).cpu()
-            n = tok.numel()
-            return both[:n].view(torch.int32).numpy(), both[n:].numpy()
-        return tok.numpy(), lp.numpy()
+    def _start_fetch(self, tok: torch.Tensor, lp: torch.Tensor, n: int):
+        """Queue the D2H copy of the sampled tokens/logprobs into pinned
+        memory behind the step's kernels (no sync here)."""
+        if not tok.is_cuda:
+            self._fetch_cpu = (tok[:n].numpy().copy(), lp[:n].numpy().copy())
+            return
+        self._hout[0, :n].copy_(tok[:n], non_blocking=True)
+        self._hout[1, :n].copy_(lp[:n].view(torch.int32), non_blocking=True)
+        self._out_ev.record()
+
+    def _finish_fetch(self, n: int):
+        if self.device.type != "cuda":
+            return self._fetch_cpu
+        self._out_ev.synchronize()
+        h = self._hout_np
+        return h[0, :n].copy(), h[1, :n].view(np.float32).copy()
 
     # ----------------------------------------------------- offline helper ---
     def generate(self, prompts: list[list[int]], params: SamplingParams,
