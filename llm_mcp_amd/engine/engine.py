@@ -153,7 +153,11 @@ class LLMEngine:
     def __init__(self, ecfg: EngineConfig, device: str | torch.device = "cuda",
                  model_cfg: LlamaConfig | None = None, tp: TPContext | None = None,
                  event_sink: Callable[[list[TokenEvent]], None] | None = None,
-                 weights: dict | None = None):
+                 weights: dict | None = None, plan_channel=None):
+        """``tp`` + ``plan_channel``: member of a tensor-parallel group.  The
+        leader (rank 0) schedules, publishes every step's plan and samples;
+        followers run ``run_follower()`` and execute the same forward on
+        their shard (parallel/tp_worker.py)."""
         from ..models import config as mc
         from ..native import runtime
         _runtime = runtime()
@@ -165,6 +169,8 @@ class LLMEngine:
         self.max_model_len = min(ecfg.max_model_len, self.cfg.max_position)
         self.model = LlamaModel(self.cfg, self.device, tp=tp, seed=ecfg.seed, weights=weights)
         self.tp = self.model.tp
+        self.is_leader = self.tp.rank == 0
+        self.chan = plan_channel
         self.Hq, self.Hkv, self.D = self.model.Hq, self.model.Hkv, self.model.D
         self.q_per_tile = ops.prefill_q_per_tile(self.Hq, self.Hkv)
         self._alloc_kv()
@@ -214,6 +220,13 @@ class LLMEngine:
         else:
             kv_bytes = 64 * per_block
         self.num_blocks = max(16, kv_bytes // per_block)
+        if self.tp.size > 1:
+            # the leader's scheduler hands out page ids for every rank
+            t = torch.tensor([self.num_blocks], dtype=torch.int64,
+                             device=self.device if self.device.type == "cuda" else "cpu")
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MIN,
+                                         group=self.tp.group)
+            self.num_blocks = int(t.item())
         # zero-filled: masked keys multiply P = 0 with V, which must be finite
         self.kv = torch.zeros((cfg.num_layers, 2, self.num_blocks, self.Hkv, BLOCK_SIZE * self.D),
                               dtype=torch.bfloat16, device=self.device)
@@ -271,8 +284,9 @@ class LLMEngine:
             def run(inp=inp, ws=ws, B=B):
                 logits = self.model.forward(inp, self.k_caches, self.v_caches, ws,
                                             self.ecfg.part_tokens)
-                ops.sample(logits, g["temp"][:B], g["topk"][:B], g["topp"][:B], g["seeds"][:B],
-                           g["offs"][:B], g["tok"][:B], g["lp"][:B])
+                if self.is_leader:
+                    ops.sample(logits, g["temp"][:B], g["topk"][:B], g["topp"][:B],
+                               g["seeds"][:B], g["offs"][:B], g["tok"][:B], g["lp"][:B])
 
             stream.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(stream):
@@ -312,6 +326,34 @@ class LLMEngine:
         if self._thread is not None:
             self._thread.join(timeout=30)
             self._thread = None
+
+    def release_followers(self):
+        """Leader: tell the TP followers to leave ``run_follower``."""
+        if self.chan is not None and self.is_leader:
+            self.chan.publish({"cmd": "stop"})
+
+    def run_follower(self) -> int:
+        """TP follower loop: execute the leader's plans until told to stop.
+        Returns the number of steps executed."""
+        from ..parallel.plan_channel import decode_plan
+        if self.device.type == "cuda":
+            torch.cuda.set_device(self.device)
+        n = 0
+        while True:
+            msg = self.chan.receive()
+            if msg.get("cmd") != "step":
+                return n
+            plan, bucket = decode_plan(msg)
+            if self.device.type == "cuda":
+                # the pinned staging buffers are reused: the previous step's
+                # uploads must have been consumed (the leader waits for its
+                # tokens every step, so this costs the followers nothing)
+                torch.cuda.current_stream(self.device).synchronize()
+            if bucket is not None:
+                self._run_graph(plan, bucket)
+            else:
+                self._run_eager(plan)
+            n += 1
 
     @property
     def num_active(self) -> int:
@@ -400,6 +442,9 @@ class LLMEngine:
         bucket = None
         if nd == S == T and self.graphs:
             bucket = next((b for b in self._bucket_list if b >= nd), None)
+        if self.chan is not None:
+            from ..parallel.plan_channel import encode_plan
+            self.chan.publish(encode_plan(plan, bucket))
         t1 = time.perf_counter()
         if bucket is not None:
             tok, lp = self._run_graph(plan, bucket)
@@ -478,6 +523,8 @@ class LLMEngine:
                          d["cu"], d["tiles"], d["rows"], T, S)
         ws = self.decode_ws
         logits = self.model.forward(inp, self.k_caches, self.v_caches, ws, self.ecfg.part_tokens)
+        if not self.is_leader:
+            return None, None
         return ops.sample(logits, d["temp"], d["topk"], d["topp"], d["seeds"], d["offs"])
 
     def _run_graph(self, plan, B):

@@ -1,0 +1,120 @@
+"""Leader -> follower step-plan channel for a tensor-parallel group (X4).
+
+Every rank of a TP group runs the same forward on its weight shard, so every
+rank needs the leader's scheduling decision for the step (token ids,
+positions, KV slots, block tables, prefill tiles, decode-graph bucket).  The
+group always lives on one node (TP over xGMI), so the plan travels through a
+shared-memory mailbox instead of a device collective: the followers never
+have to synchronise with their GPU to learn the step's shapes, and the
+leader pays one memcpy per step.
+
+Layout of the mailbox file (``/dev/shm``):
+    [0:8)    seq     (u64) -- bumped by the leader after the payload is written
+    [8:16)   nbytes  (u64)
+    [64 + 8r) ack[r] (u64) -- last seq follower r has copied out
+    [4096:)  payload (msgpack)
+The leader waits until every follower acked the previous message before
+overwriting the payload (single slot, so at most one plan in flight -- the
+followers' GPU work still runs asynchronously behind it).
+"""
+from __future__ import annotations
+
+import os
+import tempfile
+import time
+
+import msgpack
+import numpy as np
+
+_HDR = 4096
+PLAN_KEYS = ("input_ids", "positions", "slots", "context_lens", "cu_q", "block_tables",
+             "prefill_tiles", "sample_rows", "seq_ids", "temp", "topk", "topp", "seeds", "offs")
+PLAN_INTS = ("num_decode", "max_blocks", "num_tokens", "num_prefill_tokens", "max_context")
+
+
+def encode_plan(plan: dict, bucket: int | None) -> dict:
+    msg = {"cmd": "step", "bucket": bucket or 0}
+    for k in PLAN_KEYS:
+        a = np.ascontiguousarray(plan[k])
+        msg[k] = (a.dtype.str, a.shape[0], a.tobytes())
+    for k in PLAN_INTS:
+        msg[k] = int(plan[k])
+    return msg
+
+
+def decode_plan(msg: dict) -> tuple[dict, int | None]:
+    plan = {}
+    for k in PLAN_KEYS:
+        dt, n, b = msg[k]
+        plan[k] = np.frombuffer(b, dtype=np.dtype(dt), count=n)
+    for k in PLAN_INTS:
+        plan[k] = msg[k]
+    plan["sample_seq"] = np.arange(len(plan["sample_rows"]), dtype=np.int32)
+    return plan, (msg["bucket"] or None)
+
+
+def mailbox_path(tag: str) -> str:
+    base = "/dev/shm" if os.path.isdir("/dev/shm") else tempfile.gettempdir()
+    return os.path.join(base, f"lmx-tp-{tag}")
+
+
+class PlanChannel:
+    def __init__(self, path: str, rank: int, size: int, capacity: int = 64 << 20,
+                 create: bool | None = None):
+        self.path, self.rank, self.size = path, rank, size
+        create = (rank == 0) if create is None else create
+        total = _HDR + capacity
+        if create:
+            with open(path, "wb") as f:
+                f.truncate(total)
+        else:
+            deadline = time.time() + 120
+            while not os.path.exists(path) or os.path.getsize(path) < total:
+                if time.time() > deadline:
+                    raise TimeoutError(f"plan mailbox {path} never appeared")
+                time.sleep(0.01)
+        self.mm = np.memmap(path, dtype=np.uint8, mode="r+", shape=(total,))
+        self.ctl = self.mm[:_HDR].view(np.uint64)
+        self.capacity = capacity
+        self.owner = create
+        self._seq = int(self.ctl[0])
+
+    # ---------------------------------------------------------- leader ----
+    def publish(self, msg: dict, timeout: float = 300.0) -> None:
+        data = msgpack.packb(msg, use_bin_type=True)
+        if len(data) > self.capacity:
+            raise RuntimeError("plan exceeds mailbox capacity")
+        deadline = time.monotonic() + timeout
+        spins = 0
+        while any(int(self.ctl[8 + r]) < self._seq for r in range(1, self.size)):
+            spins += 1
+            if spins > 2000:
+                time.sleep(0.0002)
+                if time.monotonic() > deadline:
+                    raise TimeoutError("TP follower stopped acknowledging plans")
+        self.mm[_HDR:_HDR + len(data)] = np.frombuffer(data, dtype=np.uint8)
+        self.ctl[1] = len(data)
+        self._seq += 1
+        self.ctl[0] = self._seq   # x86-64 stores are not reordered after the payload
+
+    # -------------------------------------------------------- follower ----
+    def receive(self, idle_sleep: float = 0.0005) -> dict:
+        spins = 0
+        while int(self.ctl[0]) == self._seq:
+            spins += 1
+            if spins > 5000:
+                time.sleep(idle_sleep)
+        self._seq = int(self.ctl[0])
+        n = int(self.ctl[1])
+        data = bytes(self.mm[_HDR:_HDR + n])
+        self.ctl[8 + self.rank] = self._seq
+        return msgpack.unpackb(data, raw=False)
+
+    def close(self):
+        del self.ctl
+        self.mm._mmap.close()
+        if self.owner:
+            try:
+                os.unlink(self.path)
+            except FileNotFoundError:
+                pass

@@ -1,0 +1,107 @@
+"""Tensor-parallel serving group (Llama-3-70B TP=8 over xGMI).
+
+Launched by ``python -m llm_mcp_amd serve --tp N`` as one
+``torch.distributed.run`` group per N GPUs (one process per GPU, RCCL
+process group).  Rank 0 is the group's *leader*: it owns the continuous-
+batching scheduler, the engine <-> API socket and the job agent, exactly like
+a single-GPU worker, and publishes every step's plan on the shared-memory
+mailbox (plan_channel.py).  Ranks 1..N-1 are *followers*: they execute the
+same forward on their weight shard.  Per layer the group does two RCCL
+all-reduces (after the O and down projections, X1/X2) and one all-gather of
+the vocab-split logits per step (X3); the decode graphs capture those
+collectives together with the kernels.
+
+The reference has no model parallelism at all; its nearest
+notion is "one Ollama per host".
+"""
+from __future__ import annotations
+
+import logging
+import os
+
+import torch
+import torch.distributed as dist
+
+from ..models.llama import TPContext
+from .plan_channel import PlanChannel, mailbox_path
+
+log = logging.getLogger("lmx.tp")
+
+
+def init_group(device: torch.device | str | None = None) -> TPContext:
+    """Join the torchrun-launched group (env:// rendezvous, 127.0.0.1)."""
+    rank = int(os.environ.get("RANK", "0"))
+    size = int(os.environ.get("WORLD_SIZE", "1"))
+    if size == 1:
+        return TPContext()
+    if not dist.is_initialized():
+        dev = torch.device(device) if device is not None else None
+        if dev is not None and dev.type == "cuda":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+    return TPContext(rank, size, dist.group.WORLD)
+
+
+def attach_channel(engine, tp: TPContext, tag: str) -> PlanChannel | None:
+    """Leader creates the plan mailbox, followers attach after a barrier."""
+    if tp.size == 1:
+        return None
+    path = mailbox_path(tag)
+    ch = None
+    if tp.rank == 0:
+        ch = PlanChannel(path, 0, tp.size, create=True)
+    dist.barrier(group=tp.group)
+    if tp.rank:
+        ch = PlanChannel(path, tp.rank, tp.size, create=False)
+    engine.chan = ch
+    return ch
+
+
+def build_tp_engine(ecfg, device, tp: TPContext, tag: str, weights_path: str = "",
+                    model_cfg=None):
+    from ..engine.engine import LLMEngine
+    from ..models import config as mc
+    cfg = model_cfg or mc.resolve(ecfg.model)
+    weights = None
+    if weights_path:
+        from ..models.weights import load_llama_weights
+        weights = load_llama_weights(weights_path, cfg, device, tp.rank, tp.size)
+    eng = LLMEngine(ecfg, device=device, model_cfg=cfg, tp=tp, weights=weights)
+    attach_channel(eng, tp, tag)
+    return eng
+
+
+def run_tp_worker(a) -> None:
+    """Entry from worker/main.py when ``--tp N`` (one call per rank)."""
+    from ..devices import rocm_enum
+    from ..engine.engine import EngineConfig
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    tp = init_group(dev)
+    if tp.size != a.tp:
+        raise SystemExit(f"--tp {a.tp} but the launcher started {tp.size} ranks")
+    ecfg = EngineConfig(model=a.chat_model, max_num_seqs=a.max_num_seqs,
+                        max_batched_tokens=a.max_batched_tokens, max_model_len=a.max_model_len,
+                        kv_fraction=a.kv_fraction)
+    tag = f"{rocm_enum.host_id()}-{os.environ.get('MASTER_PORT', '0')}"
+    engine = build_tp_engine(ecfg, dev, tp, tag, a.weights)
+    log.info("TP rank %d/%d ready: %d KV blocks, %d graphs", tp.rank, tp.size,
+             engine.num_blocks, len(engine.graphs))
+    try:
+        if tp.rank == 0:
+            from ..worker.main import serve_engines
+            vis = os.environ.get("HIP_VISIBLE_DEVICES", "")
+            gpus = vis.split(",") if vis else [str(i) for i in range(tp.size)]
+            device_id = f"{rocm_enum.host_id()}:tp{tp.size}:gpu{gpus[0]}-{gpus[-1]}"
+            try:
+                serve_engines(a, engine, None, device_id)
+            finally:
+                engine.release_followers()
+        else:
+            engine.run_follower()
+    finally:
+        if engine.chan is not None:
+            engine.chan.close()
+        dist.destroy_process_group()

@@ -39,30 +39,24 @@ def build_parser():
 def main(argv=None):
     a = build_parser().parse_args(argv)
     logging.basicConfig(level=os.environ.get("LOG_LEVEL", "INFO"))
-    import torch
-
-    from ..api.registry import LocalModel, ModelRegistry
-    from ..devices import rocm_enum
-    from ..engine.async_engine import AsyncEngine
-    from ..engine.engine import EngineConfig, LLMEngine
-    from ..engine.ipc import EngineServer
-    from ..models import config as mc
-    from ..models.tokenizer import for_model
-    from .agent import WorkerAgent
-    from .jobs import JobRunner
-
     if a.tp > 1:
         from ..parallel.tp_worker import run_tp_worker
         return run_tp_worker(a)
+    import torch
+
+    from ..devices import rocm_enum
+    from ..engine.engine import EngineConfig, LLMEngine
+    from ..models import config as mc
 
     torch.cuda.set_device(a.gpu)
     dev = torch.device("cuda", a.gpu)
-    device_id = rocm_enum.device_id(a.gpu)
-    reg = ModelRegistry()
     engine = embed = None
-    weights = None
+    if a.embed_model:
+        from ..engine.embed_engine import EmbeddingEngine
+        embed = EmbeddingEngine(mc.resolve(a.embed_model), dev)
     if a.chat_model:
         cfg = mc.resolve(a.chat_model)
+        weights = None
         if a.weights:
             from ..models.weights import load_llama_weights
             weights = load_llama_weights(a.weights, cfg, dev)
@@ -71,35 +65,51 @@ def main(argv=None):
                             max_model_len=a.max_model_len, kv_fraction=a.kv_fraction)
         if a.embed_model:
             ecfg.kv_fraction = min(ecfg.kv_fraction, 0.5)
-    if a.embed_model:
-        from ..engine.embed_engine import EmbeddingEngine
-        embed = EmbeddingEngine(mc.resolve(a.embed_model), dev)
+        engine = LLMEngine(ecfg, device=dev, model_cfg=cfg, weights=weights)
+    serve_engines(a, engine, embed, rocm_enum.device_id(a.gpu))
+
+
+def serve_engines(a, engine, embed, device_id: str) -> None:
+    """Serve a chat engine and/or an embedding engine: the sync OpenAI path
+    over the Unix socket and the async job path via lease claims.  Used by the
+    single-GPU worker and by the leader of a TP group."""
+    from ..api.registry import LocalModel, ModelRegistry
+    from ..devices import rocm_enum
+    from ..engine.async_engine import AsyncEngine
+    from ..engine.ipc import EngineServer
+    from ..models.tokenizer import for_model
+    from .agent import WorkerAgent
+    from .jobs import JobRunner
+
+    reg = ModelRegistry()
+    aeng = None
+    if embed is not None:
         reg.add(LocalModel(a.embed_model, "embed", device_id, embed,
                            for_model(embed.cfg), embed.cfg, embed.max_seq_len, capacity=1024))
-    if a.chat_model:
-        engine = LLMEngine(ecfg, device=dev, weights=weights)
+    if engine is not None:
         aeng = AsyncEngine(engine)
         reg.add(LocalModel(a.chat_model, "chat", device_id, aeng, for_model(engine.cfg),
                            engine.cfg, engine.max_model_len, capacity=a.max_num_seqs))
-    sock = a.socket or f"/tmp/lmx-{rocm_enum.host_id()}-gpu{a.gpu}.sock"
+    sock = a.socket or f"/tmp/lmx-{rocm_enum.host_id()}-{device_id.rsplit(':', 1)[-1]}.sock"
     info = {"device_id": device_id, "models": {}}
     if engine is not None:
         info["models"][a.chat_model] = {"kind": "chat", "max_model_len": engine.max_model_len,
-                                        "capacity": a.max_num_seqs}
+                                        "capacity": a.max_num_seqs,
+                                        "tp": engine.tp.size}
     if embed is not None:
         info["models"][a.embed_model] = {"kind": "embed", "max_model_len": embed.max_seq_len,
                                          "capacity": 1024}
     server = EngineServer(engine, sock, info, embed_engine=embed,
-                          fallback_sink=aeng._sink if engine is not None else None)
+                          fallback_sink=aeng._sink if aeng is not None else None)
     if engine is not None:
         engine.event_sink = server._sink
 
     async def run():
         loop = asyncio.get_running_loop()
-        if engine is not None:
+        if aeng is not None:
             aeng.loop = loop
         server.start()
-        log.info("GPU %d serving %s on %s", a.gpu, list(info["models"]), sock)
+        log.info("%s serving %s on %s", device_id, list(info["models"]), sock)
         stop = asyncio.Event()
         for sig in (signal.SIGINT, signal.SIGTERM):
             loop.add_signal_handler(sig, stop.set)
@@ -118,7 +128,8 @@ def main(argv=None):
                                              headers={"Content-Type": "application/json"})
                 urllib.request.urlopen(req, timeout=5).read()
 
-            runner = JobRunner(reg, device_id, report_benchmark=lambda **kw: client.report_benchmark(**kw))
+            runner = JobRunner(reg, device_id,
+                               report_benchmark=lambda **kw: client.report_benchmark(**kw))
             agent = WorkerAgent(client, runner, device_id,
                                 worker_id=os.environ.get("WORKER_ID", f"worker-{device_id}"),
                                 lease_s=a.lease_seconds, capacity=a.max_num_seqs,
