@@ -77,7 +77,9 @@ class PlanChannel:
         self.ctl = self.mm[:_HDR].view(np.uint64)
         self.capacity = capacity
         self.owner = create
-        self._seq = int(self.ctl[0])
+        # a follower may attach after the leader already published: resume
+        # from its own ack slot (0 on a fresh mailbox), not from the head
+        self._seq = int(self.ctl[0]) if create else int(self.ctl[8 + rank])
 
     # ---------------------------------------------------------- leader ----
     def publish(self, msg: dict, timeout: float = 300.0) -> None:

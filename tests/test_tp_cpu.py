@@ -107,13 +107,19 @@ def test_tp2_generation_matches_single_process(full_model):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port, tag = _free_port(), f"test-{os.getpid()}-{_free_port()}"
-    procs = [ctx.Process(target=_rank_main, args=(r, 2, port, path, tag, q)) for r in range(2)]
+    procs = [ctx.Process(target=_rank_main, args=(r, 2, port, path, tag, q), daemon=True)
+             for r in range(2)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=300) for _ in procs]
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
+    try:
+        res = [q.get(timeout=240) for _ in procs]
+        for p in procs:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.kill()
     leader = next(r for r in res if r[0] == "leader")
     follower = next(r for r in res if r[0] == "follower")
     _, greedy, sampled, nb = leader
