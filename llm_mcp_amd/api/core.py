@@ -121,10 +121,11 @@ class CoreState:
             await asyncio.sleep(seconds)
 
     def _maintenance(self):
-        self.store.expire_deadlines()
-        keep_days = float(os.environ.get("LMX_JOB_RETENTION_DAYS", "7"))
-        if keep_days > 0:
-            self.store.purge_jobs(keep_days * 86400)
+        from ..planner.catalog import RetentionPlanner
+        if not hasattr(self, "_retention"):
+            self._retention = RetentionPlanner(
+                self.store, float(os.environ.get("LMX_JOB_RETENTION_DAYS", "7")))
+        self._retention.tick()
         for m in self.registry.all():
             info = m.info()
             if "kv_usage" in info:

@@ -129,6 +129,39 @@ def build_runtime(force: bool = False, verbose: bool = False) -> Path:
     return out
 
 
+SANITIZERS = {"tsan": ["-fsanitize=thread"],
+              "asan": ["-fsanitize=address,undefined", "-fno-omit-frame-pointer"]}
+
+
+def sanitize_runtime(which=("tsan", "asan"), verbose: bool = False) -> dict[str, str]:
+    """Build the runtime stress test (csrc/runtime/tests/stress.cpp) with host
+    sanitizers and run it; raises on any report.  Host code only -- GPU
+    sanitizers are not used on this hardware pool."""
+    rdir = CSRC / "runtime"
+    srcs = [rdir / s for s in RUNTIME_SOURCES if s != "bindings.cpp"]
+    out_dir = BUILD / "sanitize"
+    out_dir.mkdir(parents=True, exist_ok=True)
+    # ROCm's clang: its TSan runtime intercepts pthread_cond_clockwait (GCC 11's
+    # does not and reports a false "double lock" on condition-variable waits)
+    cxx = os.environ.get("LMX_SAN_CXX", "/opt/rocm/llvm/bin/clang++")
+    logs = {}
+    for name in which:
+        exe = out_dir / f"stress_{name}"
+        _run([cxx, "-O1", "-g", "-std=c++17", "-pthread", *SANITIZERS[name], f"-I{rdir}",
+              *[str(s) for s in srcs], str(rdir / "tests" / "stress.cpp"), "-o", str(exe)])
+        env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1",
+                   ASAN_OPTIONS="detect_leaks=1:halt_on_error=1",
+                   UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+        r = subprocess.run([str(exe), "1500", "2000"], capture_output=True, text=True, env=env,
+                           timeout=600)
+        logs[name] = r.stdout + r.stderr
+        if r.returncode != 0 or "ERROR: " in r.stderr or "runtime error" in r.stderr:
+            raise RuntimeError(f"{name} stress failed (rc {r.returncode}):\n{logs[name][-4000:]}")
+        if verbose:
+            print(f"[sanitize] {name}: {r.stdout.strip().splitlines()[-1]}")
+    return logs
+
+
 def build_all(force: bool = False, verbose: bool = False) -> None:
     with ThreadPoolExecutor(max_workers=2) as ex:
         fk = ex.submit(build_kernels, force, verbose)
@@ -138,4 +171,7 @@ def build_all(force: bool = False, verbose: bool = False) -> None:
 
 
 if __name__ == "__main__":
-    build_all(force="--force" in sys.argv, verbose=True)
+    if "--sanitize-runtime" in sys.argv:
+        sanitize_runtime(verbose=True)
+    else:
+        build_all(force="--force" in sys.argv, verbose=True)
