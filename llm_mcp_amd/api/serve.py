@@ -20,11 +20,14 @@ from ..engine.ipc import EngineClient
 from ..models import config as mc
 from ..models.tokenizer import for_model
 from ..utils.metrics import Metrics
+from ..policy.circuit import CircuitBreaker
 from .app import ServingState, make_app
 from .helpers import write_json
+from .openai_embed import EmbeddingsHandler
 from .registry import LocalModel, ModelRegistry
 
 log = logging.getLogger("lmx.serve")
+_ATTACH = web.AppKey("attach", asyncio.Task)
 
 
 def parse_engine_spec(spec: str) -> dict:
@@ -59,6 +62,36 @@ async def attach_engines(state, specs: list[dict]):
     state.engines_ready = True
 
 
+def make_serving_app(specs: list[dict], version: str | None = None):
+    """The API process's app: chat + embeddings + /ready over attached
+    engine sockets (attached on startup)."""
+    state = ServingState(ModelRegistry(), Metrics(),
+                         version=version or os.environ.get("CORE_VERSION", "0.1.0"),
+                         circuit=CircuitBreaker())
+    state.engines_ready = False
+
+    def register(app):
+        async def ready(request):
+            ok = getattr(state, "engines_ready", False)
+            return write_json(200 if ok else 503, {"ready": ok,
+                                                    "models": state.registry.model_ids()})
+        app.router.add_get("/ready", ready)
+        emb = EmbeddingsHandler(state)
+
+        async def embeddings(request):
+            return await emb(request)
+        app.router.add_route("*", "/v1/embeddings", embeddings)
+
+    state.register_routes = register
+    app = make_app(state)
+
+    async def on_start(app):
+        app[_ATTACH] = asyncio.create_task(attach_engines(state, specs))
+
+    app.on_startup.append(on_start)
+    return app, state
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--host", default=os.environ.get("LMX_HTTP_HOST", "127.0.0.1"))
@@ -67,25 +100,7 @@ def main(argv=None):
                     help="MODEL=unix:/path[,device=gpu0][,tokenizer=/dir]")
     a = ap.parse_args(argv)
     logging.basicConfig(level=os.environ.get("LOG_LEVEL", "INFO"))
-    state = ServingState(ModelRegistry(), Metrics(),
-                         version=os.environ.get("CORE_VERSION", "0.1.0"))
-    state.engines_ready = False
-    specs = [parse_engine_spec(s) for s in a.engine]
-
-    def register(app):
-        async def ready(request):
-            ok = getattr(state, "engines_ready", False)
-            return write_json(200 if ok else 503, {"ready": ok,
-                                                    "models": state.registry.model_ids()})
-        app.router.add_get("/ready", ready)
-
-    state.register_routes = register
-    app = make_app(state)
-
-    async def on_start(app):
-        app["_attach"] = asyncio.create_task(attach_engines(state, specs))
-
-    app.on_startup.append(on_start)
+    app, _ = make_serving_app([parse_engine_spec(s) for s in a.engine])
     web.run_app(app, host=a.host, port=a.port, access_log=None, print=None)
 
 

@@ -1,0 +1,304 @@
+"""Benchmarks for the BASELINE.json configs other than the headline chat SSE
+run (bench.py):
+
+  queue   submit -> claim -> heartbeat -> complete with echo workers on CPU
+          (config 1: plumbing, no GPU).  Core gRPC server + W worker agents
+          in one process; reports jobs/s and claim / end-to-end latency.
+          ``--store postgres`` uses DB_DSN (none in this image).
+  embed   /v1/embeddings nomic-embed-text bf16 on one GPU (config 2): API
+          process + GPU worker process (sync path over the engine socket) +
+          this process as the client; embeddings/s and p50/p95 latency.
+  mixed   mixed chat + embeddings jobs at 256 concurrent jobs through the
+          lease scheduler (config 5, on the GPUs given with --gpus): the
+          production launcher ``python -m llm_mcp_amd serve`` + async jobs
+          submitted over HTTP and awaited on the job SSE stream; jobs/s,
+          p50/p95 latency, error rate.
+
+Methodology follows the reference's probe harness (p50/p95 by linear
+interpolation, scripts/probe_openrouter_models.py:113-123).  This process
+never initialises the GPU: every GPU user is a child process.
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import random
+import socket
+import subprocess
+import sys
+import threading
+import time
+
+from .loadgen import percentile, synthetic_prompt
+
+
+def _log(msg: str) -> None:
+    print(f"[serving_bench] {msg}", file=sys.stderr, flush=True)
+
+
+def _port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+async def _wait_http(url: str, path: str = "/health", timeout: float = 900) -> None:
+    import aiohttp
+    t_end = time.time() + timeout
+    async with aiohttp.ClientSession() as s:
+        while time.time() < t_end:
+            try:
+                async with s.get(url + path) as r:
+                    if r.status == 200:
+                        return
+            except Exception:
+                pass
+            await asyncio.sleep(0.5)
+            if int(time.time()) % 15 == 0:
+                _log(f"waiting for {url}{path}")
+    raise TimeoutError(f"{url}{path} never became ready")
+
+
+# ------------------------------------------------------------------ queue ----
+def bench_queue(a) -> dict:
+    from ..api.core import CoreState, open_store
+    from ..api.registry import ModelRegistry
+    from ..rpc.client import CoreClient
+    from ..rpc.server import start_grpc
+    from ..worker.agent import WorkerAgent
+    from ..worker.jobs import JobRunner
+
+    st = CoreState(store=open_store(a.store))
+    loop = asyncio.new_event_loop()
+    box = {}
+
+    def serve():
+        asyncio.set_event_loop(loop)
+        box["srv"], box["port"] = loop.run_until_complete(start_grpc(st, "127.0.0.1:0"))
+        loop.run_forever()
+
+    threading.Thread(target=serve, daemon=True).start()
+    while "port" not in box:
+        time.sleep(0.01)
+    addr = f"127.0.0.1:{box['port']}"
+    client = CoreClient(addr)
+    # claim-latency probe on a populated queue (reference: ~19 ms with Postgres)
+    n_probe = 200
+    for i in range(n_probe + a.jobs):
+        client.submit("echo", {"i": i}, source="probe")
+    lat = []
+    for _ in range(n_probe):
+        t0 = time.perf_counter()
+        j = client.claim("probe", lease_seconds=30)
+        lat.append(time.perf_counter() - t0)
+        if j:
+            client.complete("probe", j["id"], {"ok": True}, attempt_id=j.get("attempt_id", ""))
+    # throughput: W agents drain a.jobs queued behind the rest end to end
+    ids = [client.submit("echo", {"i": i}, source="bench") for i in range(a.jobs)]
+    a.jobs *= 2
+
+    async def drain():
+        agents = [WorkerAgent(CoreClient(addr), JobRunner(ModelRegistry(), f"cpu{w}"),
+                              f"cpu{w}", worker_id=f"w{w}", lease_s=30, capacity=a.capacity)
+                  for w in range(a.workers)]
+        per = a.jobs // a.workers
+        await asyncio.gather(*[ag.run(max_jobs=per + (1 if w < a.jobs % a.workers else 0))
+                               for w, ag in enumerate(agents)])
+
+    t0 = time.perf_counter()
+    asyncio.new_event_loop().run_until_complete(drain())
+    el = time.perf_counter() - t0
+    done = sum(1 for i in ids if client.get(i)["status"] == "done")
+    loop.call_soon_threadsafe(loop.stop)
+    return {"config": "queue plumbing: submit->claim->heartbeat->complete, echo workers, CPU",
+            "store": st.store.backend, "jobs": a.jobs, "workers": a.workers, "done": done,
+            "jobs_per_s": round(a.jobs / el, 1),
+            "claim_p50_ms": round(percentile(lat, 50) * 1e3, 3),
+            "claim_p95_ms": round(percentile(lat, 95) * 1e3, 3)}
+
+
+# ------------------------------------------------------------------ embed ----
+async def _embed_load(url, model, concurrency, requests, batch, chars, seed=0):
+    import aiohttp
+    rng = random.Random(seed)
+    docs = [synthetic_prompt(chars, rng) for _ in range(64)]
+    lat = []
+    sem = asyncio.Semaphore(concurrency)
+
+    async def one(s, i):
+        inp = [docs[(i * batch + k) % len(docs)] for k in range(batch)]
+        async with sem:
+            t0 = time.perf_counter()
+            async with s.post(url + "/v1/embeddings", json={"model": model, "input": inp}) as r:
+                body = await r.json()
+                if r.status != 200:
+                    raise RuntimeError(f"HTTP {r.status}: {body}")
+            lat.append(time.perf_counter() - t0)
+            return len(body["data"]), body["usage"]["prompt_tokens"]
+
+    async with aiohttp.ClientSession(connector=aiohttp.TCPConnector(limit=0)) as s:
+        await asyncio.gather(*[one(s, i) for i in range(min(8, requests))])   # warm-up
+        lat.clear()
+        t0 = time.perf_counter()
+        res = await asyncio.gather(*[one(s, i) for i in range(requests)])
+        el = time.perf_counter() - t0
+    n = sum(r[0] for r in res)
+    toks = sum(r[1] for r in res)
+    return {"embeddings": n, "tokens": toks, "elapsed_s": round(el, 3),
+            "embeddings_per_s": round(n / el, 1), "tokens_per_s": round(toks / el, 1),
+            "p50_ms": round(percentile(lat, 50) * 1e3, 2),
+            "p95_ms": round(percentile(lat, 95) * 1e3, 2)}
+
+
+def bench_embed(a) -> dict:
+    sock = f"/tmp/lmx-embbench-{os.getpid()}.sock"
+    port = _port()
+    env = dict(os.environ)
+    worker = subprocess.Popen([sys.executable, "-m", "llm_mcp_amd.worker.main", "--gpu",
+                               str(a.gpu), "--chat-model", "", "--embed-model", a.model,
+                               "--socket", sock, "--no-jobs"], env=env)
+    api = subprocess.Popen([sys.executable, "-m", "llm_mcp_amd.api.serve", "--port", str(port),
+                            "--engine", f"{a.model}=unix:{sock},device=gpu{a.gpu}"],
+                           env=env, stdout=subprocess.DEVNULL)
+    url = f"http://127.0.0.1:{port}"
+    try:
+        loop = asyncio.new_event_loop()
+        loop.run_until_complete(_wait_http(url, "/ready"))
+        out = {"config": "/v1/embeddings nomic-embed-text bf16, 1x MI355X (sync path)",
+               "model": a.model, "concurrency": a.concurrency, "batch": a.batch,
+               "doc_chars": a.chars}
+        out.update(loop.run_until_complete(
+            _embed_load(url, a.model, a.concurrency, a.requests, a.batch, a.chars)))
+        out["single_p50"] = loop.run_until_complete(
+            _embed_load(url, a.model, 1, 64, 1, a.chars))["p50_ms"]
+        return out
+    finally:
+        for p in (api, worker):
+            p.terminate()
+        for p in (api, worker):
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+
+
+# ------------------------------------------------------------------ mixed ----
+async def _mixed_load(url, chat_model, embed_model, jobs, concurrency, embed_every, max_tokens,
+                      prompt_chars):
+    import aiohttp
+    rng = random.Random(1)
+    sem = asyncio.Semaphore(concurrency)
+    lat, errs, kinds = [], [], {}
+
+    async def one(s, i):
+        if i % embed_every == 0:
+            kind, payload = "engine.embed", {"model": embed_model,
+                                             "prompt": synthetic_prompt(prompt_chars, rng)}
+        else:
+            kind, payload = "engine.generate", {
+                "model": chat_model, "prompt": synthetic_prompt(prompt_chars, rng),
+                "options": {"max_tokens": max_tokens, "temperature": 0.8, "ignore_eos": True}}
+        async with sem:
+            t0 = time.perf_counter()
+            async with s.post(url + "/v1/jobs", json={"kind": kind, "payload": payload,
+                                                      "source": "bench"}) as r:
+                jid = (await r.json())["job_id"]
+            status = None
+            async with s.get(url + f"/v1/jobs/{jid}/stream") as r:
+                async for line in r.content:
+                    if line.startswith(b"data: "):
+                        d = json.loads(line[6:])
+                        status = d.get("status", status)
+                        if status in ("done", "error"):
+                            break
+            lat.append(time.perf_counter() - t0)
+            kinds[kind] = kinds.get(kind, 0) + 1
+            if status != "done":
+                errs.append(jid)
+            if len(lat) % 64 == 0:
+                _log(f"{len(lat)}/{jobs} jobs finished, {len(errs)} errors")
+
+    async with aiohttp.ClientSession(connector=aiohttp.TCPConnector(limit=0),
+                                     timeout=aiohttp.ClientTimeout(total=3600)) as s:
+        t0 = time.perf_counter()
+        await asyncio.gather(*[one(s, i) for i in range(jobs)])
+        el = time.perf_counter() - t0
+    return {"jobs": jobs, "by_kind": kinds, "elapsed_s": round(el, 2),
+            "jobs_per_s": round(jobs / el, 2), "p50_s": round(percentile(lat, 50), 3),
+            "p95_s": round(percentile(lat, 95), 3), "error_rate": round(len(errs) / jobs, 4)}
+
+
+def bench_mixed(a) -> dict:
+    port, gport = _port(), _port()
+    env = dict(os.environ, LMX_STORE=a.store)
+    cmd = [sys.executable, "-m", "llm_mcp_amd", "serve", "--gpus", a.gpus, "--http",
+           f"127.0.0.1:{port}", "--grpc", f"127.0.0.1:{gport}", "--chat-model", a.chat_model,
+           "--embed-model", a.model, "--max-num-seqs", str(a.concurrency)]
+    core = subprocess.Popen(cmd, env=env, start_new_session=True)
+    url = f"http://127.0.0.1:{port}"
+    try:
+        loop = asyncio.new_event_loop()
+        loop.run_until_complete(_wait_http(url, "/health"))
+        # workers register once their engines are up
+        loop.run_until_complete(_wait_workers(url, len(a.gpus.split(","))))
+        out = {"config": "mixed chat + embeddings jobs through the lease scheduler",
+               "gpus": a.gpus, "concurrency": a.concurrency, "chat_model": a.chat_model,
+               "embed_model": a.model, "embed_share": round(1 / a.embed_every, 3),
+               "max_tokens": a.max_tokens}
+        out.update(loop.run_until_complete(_mixed_load(
+            url, a.chat_model, a.model, a.jobs, a.concurrency, a.embed_every, a.max_tokens,
+            a.chars)))
+        return out
+    finally:
+        core.terminate()
+        try:
+            core.wait(timeout=60)
+        except subprocess.TimeoutExpired:
+            core.kill()
+
+
+async def _wait_workers(url: str, n: int, timeout: float = 900) -> None:
+    import aiohttp
+    t_end = time.time() + timeout
+    async with aiohttp.ClientSession() as s:
+        while time.time() < t_end:
+            try:
+                async with s.get(url + "/v1/dashboard") as r:
+                    d = await r.json()
+                    if d.get("workers_online", 0) >= n:
+                        return
+            except Exception:
+                pass
+            _log("waiting for workers to register")
+            await asyncio.sleep(5.0)
+    raise TimeoutError("workers never came online")
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("what", choices=["queue", "embed", "mixed"])
+    ap.add_argument("--store", default=os.environ.get("LMX_STORE", "memory"))
+    ap.add_argument("--jobs", type=int, default=2000)
+    ap.add_argument("--workers", type=int, default=4)
+    ap.add_argument("--capacity", type=int, default=16)
+    ap.add_argument("--gpu", type=int, default=0)
+    ap.add_argument("--gpus", default="0")
+    ap.add_argument("--model", default="nomic-embed-text")
+    ap.add_argument("--chat-model", default="llama-3-8b")
+    ap.add_argument("--concurrency", type=int, default=32)
+    ap.add_argument("--requests", type=int, default=512)
+    ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--chars", type=int, default=1024)
+    ap.add_argument("--embed-every", type=int, default=4)
+    ap.add_argument("--max-tokens", type=int, default=128)
+    a = ap.parse_args(argv)
+    fn = {"queue": bench_queue, "embed": bench_embed, "mixed": bench_mixed}[a.what]
+    print(json.dumps(fn(a)), flush=True)
+
+
+if __name__ == "__main__":
+    main()

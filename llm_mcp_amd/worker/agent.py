@@ -69,8 +69,9 @@ class WorkerAgent:
         self._stop.set()
 
     async def run(self, max_jobs: int | None = None):
-        if not self.worker_id:
-            await self.register()
+        # always (re-)register: a preset worker id must still appear in the
+        # devices table (dashboard workers_online, capacity, telemetry)
+        await self.register()
         n = 0
         while not self._stop.is_set():
             if len(self.inflight) >= self.capacity:

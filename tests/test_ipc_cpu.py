@@ -54,3 +54,36 @@ def test_chat_over_ipc():
         asyncio.new_event_loop().run_until_complete(go())
     finally:
         srv.stop()
+
+
+def test_embeddings_over_ipc_api_process_app():
+    """The API-only process (api/serve.py) serves /v1/embeddings from an
+    embedding engine living in another process's EngineServer."""
+    from llm_mcp_amd.api.serve import make_serving_app
+    from llm_mcp_amd.engine.embed_engine import EmbeddingEngine
+    from llm_mcp_amd.models import config as mc
+    emb = EmbeddingEngine(mc.resolve("tiny-nomic"), device="cpu")
+    path = os.path.join(tempfile.mkdtemp(), "emb.sock")
+    srv = EngineServer(None, path, info={"models": {"tiny-nomic": {
+        "kind": "embed", "max_model_len": 512, "capacity": 64}}}, embed_engine=emb)
+    srv.start()
+
+    async def go():
+        app, st = make_serving_app([parse_engine_spec(f"tiny-nomic=unix:{path},device=cpu0")])
+        async with TestClient(TestServer(app)) as c:
+            for _ in range(100):
+                if (await c.get("/ready")).status == 200:
+                    break
+                await asyncio.sleep(0.05)
+            r = await c.post("/v1/embeddings", json={"model": "tiny-nomic",
+                                                     "input": ["a doc", "another doc"],
+                                                     "dimensions": 64})
+            body = await r.json()
+            assert r.status == 200, body
+            assert len(body["data"]) == 2 and len(body["data"][0]["embedding"]) == 64
+            assert body["usage"]["prompt_tokens"] > 0
+
+    try:
+        asyncio.new_event_loop().run_until_complete(go())
+    finally:
+        srv.stop()
