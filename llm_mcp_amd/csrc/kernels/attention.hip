@@ -21,6 +21,8 @@
 //   prefill (K3): columns = (16/G queries) x (G heads): the K/V page read is
 //                 shared by all heads of the kv group; each wave walks its own
 //                 causal key range; varlen batches via a host-built tile list.
+#include <climits>
+
 #include "common.h"
 
 namespace lmx {
@@ -230,58 +232,225 @@ int paged_decode(const void* q, long q_stride, const void* k_cache, const void* 
 }
 
 // --------------------------------------------------------------- prefill ----
-// tiles[t] = {seq, q_start}; a workgroup serves 4 waves x (16/G) queries of
-// one (seq, kv head).  grid (num_tiles, Hkv), block 256.
+// Prefill / encoder attention (K3): flash-style, K/V tiles shared through LDS.
+//
+//   grid (num_tiles, Hkv), block 256 = 4 waves; tiles[t] = {seq, q_start}.
+//   A workgroup serves PQ = 4 * NG * (16/G) queries x G heads of one
+//   (seq, kv head): each wave owns NG groups of 16 "columns" (query, head)
+//   and keeps the S^T / O^T formulation of the decode kernel (softmax
+//   statistics and O accumulators on the same lane, P fed straight from the
+//   S accumulators as the PV B-operand via the permuted-k order).
+//   Per iteration one 64-key tile (two 32-token pages) of K and V is moved
+//   HBM -> LDS by global_load_lds (16 B per lane, no VGPR hop) into a double
+//   buffer; the next tile's DMA is issued before the current tile's MFMAs.
+//   The K image is [key][d] with its 16-B chunks XOR-swizzled by the key row
+//   and the V image [d][key] with its 8-B units swizzled by d/4, both applied
+//   on the global source address (the DMA writes lane-linear), so the
+//   fragment reads are bank-conflict free.
+//
 //  q:  [T_total][Hq][D] rows at q_stride (tokens of seq s start at cu_q[s])
 //  context_lens[s] = total keys of seq s (cached prefix + this chunk)
 //  causal: query i of the chunk sits at absolute position ctx - qlen + i.
+constexpr int PF_NG = 2;     // column groups per wave
+constexpr int PF_TK = 64;    // keys per LDS tile (two pages)
+
 template <int HD>
-__global__ void __launch_bounds__(256) paged_prefill_kernel(
+__device__ __forceinline__ int kswz(int r) {
+  return HD == 128 ? (r & 15) : ((r >> 1) & 7);
+}
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+__device__ __forceinline__ void pf_glds16(const void* g, void* lds) {
+  __builtin_amdgcn_global_load_lds(g, (lds_void_t*)lds, 16, 0, 0);
+}
+
+// DMA one 32-token page of K and of V into the LDS tile slot `pslot`.
+template <int HD>
+__device__ __forceinline__ void pf_stage_page(bf16_t* k_lds, bf16_t* v_lds,
+                                              const bf16_t* __restrict__ kp,
+                                              const bf16_t* __restrict__ vp) {
+  const int tid = threadIdx.x, wave = tid >> 6;
+  constexpr int PAGE = BS * HD;            // elements per page
+#pragma unroll
+  for (int j = 0; j < PAGE / 2048; ++j) {  // 2048 elements = 4 KB per instruction
+    const int off = j * 2048 + tid * 8;
+    // K: row = key, 16-B chunk position swizzled by the row
+    const int kr = off / HD, kpos = (off % HD) / 8;
+    pf_glds16(kp + kr * HD + 8 * (kpos ^ kswz<HD>(kr)), k_lds + j * 2048 + wave * 512);
+    // V: row = d (32 keys = 64 B), 16-B pair position swizzled by d/4
+    const int vd = off / BS, vq = (off % BS) / 8;
+    pf_glds16(vp + vd * BS + 8 * (vq ^ ((vd >> 2) & 3)), v_lds + j * 2048 + wave * 512);
+  }
+}
+
+template <int HD>
+__global__ void __launch_bounds__(256, 2) paged_prefill_kernel(
     const bf16_t* __restrict__ q, long q_stride, const bf16_t* __restrict__ k_cache,
     const bf16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ cu_q, const int* __restrict__ context_lens,
     const int* __restrict__ tiles, bf16_t* __restrict__ out, long out_stride, int Hq, int Hkv,
     float scale, int causal) {
+  extern __shared__ __attribute__((aligned(16))) char pf_smem[];
+  constexpr int PAGE = BS * HD;
+  // buffer b: K pages at b*4*PAGE + {0, PAGE}, V pages at b*4*PAGE + 2*PAGE + {0, PAGE}
+  bf16_t* const lds = reinterpret_cast<bf16_t*>(pf_smem);
+  constexpr int KS = HD / 32, NT = HD / 16;
+
   const int tile = blockIdx.x, kvh = blockIdx.y;
   const int seq = tiles[2 * tile], q_start = tiles[2 * tile + 1];
-  const int G = Hq / Hkv, QPW = 16 / G;  // queries per wave
+  const int G = Hq / Hkv, QG = 16 / G;            // queries per column group
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
   const int qbeg = cu_q[seq], qlen = cu_q[seq + 1] - qbeg;
   const int ctx = context_lens[seq];
-  const int qi = q_start + wave * QPW + c / G;  // query index inside the chunk
-  const int head = kvh * G + (c % G);
-  const bool valid = (c < QPW * G) && (qi < qlen);
-  const int lim = causal ? (ctx - qlen + qi) : (ctx - 1);
-  // the wave's key range: up to its last valid query's limit
-  const int qi_last = min(q_start + wave * QPW + QPW - 1, qlen - 1);
-  if (q_start + wave * QPW >= qlen) return;  // whole wave idle (no barriers below)
-  const int wave_lim = causal ? (ctx - qlen + qi_last) : (ctx - 1);
-
-  bf16x8_t qf[HD / 32];
-  const bf16_t* qrow = q + (long)(qbeg + (valid ? qi : 0)) * q_stride + (long)head * HD;
-#pragma unroll
-  for (int s = 0; s < HD / 32; ++s)
-    qf[s] = valid ? load_frag16B(qrow + 32 * s + 8 * g) : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
-
-  PageState<HD> st;
-  state_init(st);
-  const float scale_log2 = scale * LOG2E;
+  const int wg_q1 = min(q_start + 4 * PF_NG * QG, qlen);   // one past the WG's last query
+  const int wg_lim = causal ? (ctx - qlen + wg_q1 - 1) : (ctx - 1);
+  const int ntiles = wg_lim / PF_TK + 1;
+  const int last_page = (ctx - 1) / BS;
   const int* bt = block_tables + (long)seq * bt_stride;
-  const int npg = wave_lim / BS + 1;
-  const int my_lim = valid ? lim : -1;
-  for (int pg = 0; pg < npg; ++pg) {
-    const long blk = bt[pg];
-    const bf16_t* kp = k_cache + (blk * Hkv + kvh) * (BS * HD);
-    const bf16_t* vp = v_cache + (blk * Hkv + kvh) * (BS * HD);
-    process_page(st, qf, kp, vp, pg * BS, my_lim, scale_log2);
+
+  // this lane's columns
+  int lim[PF_NG];
+  bool valid[PF_NG];
+  int qi[PF_NG];
+  bf16x8_t qf[PF_NG][KS];
+#pragma unroll
+  for (int n = 0; n < PF_NG; ++n) {
+    qi[n] = q_start + (wave * PF_NG + n) * QG + c / G;
+    valid[n] = qi[n] < qlen;
+    lim[n] = valid[n] ? (causal ? (ctx - qlen + qi[n]) : (ctx - 1)) : -1;
+    const int head = kvh * G + (c % G);
+    const bf16_t* qrow = q + (long)(qbeg + (valid[n] ? qi[n] : 0)) * q_stride + (long)head * HD;
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+      qf[n][s] = valid[n] ? load_frag16B(qrow + 32 * s + 8 * g)
+                          : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
   }
-  if (!valid) return;
-  const float inv = st.l > 0.f ? 1.f / st.l : 0.f;
-  bf16_t* orow = out + (long)(qbeg + qi) * out_stride + (long)head * HD;
+  // smallest column limit of the wave: tiles below it need no mask
+  int wave_lo = INT_MAX;
 #pragma unroll
-  for (int i = 0; i < HD / 16; ++i)
+  for (int n = 0; n < PF_NG; ++n) wave_lo = min(wave_lo, valid[n] ? lim[n] : INT_MAX);
+  wave_lo = min(wave_lo, __shfl_xor(wave_lo, 1, 64));
+  wave_lo = min(wave_lo, __shfl_xor(wave_lo, 2, 64));
+  wave_lo = min(wave_lo, __shfl_xor(wave_lo, 4, 64));
+  wave_lo = min(wave_lo, __shfl_xor(wave_lo, 8, 64));
+  const bool wave_idle = q_start + wave * PF_NG * QG >= qlen;   // wave-uniform
+
+  float m[PF_NG], l[PF_NG];
+  f32x4_t acc[PF_NG][NT];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) orow[16 * i + 4 * g + r] = f2bf(st.acc[i][r] * inv);
+  for (int n = 0; n < PF_NG; ++n) {
+    m[n] = -INFINITY;
+    l[n] = 0.f;
+#pragma unroll
+    for (int i = 0; i < NT; ++i) acc[n][i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  }
+  const float scale_log2 = scale * LOG2E;
+
+  auto stage = [&](int t, int buf) {
+#pragma unroll
+    for (int pp = 0; pp < 2; ++pp) {
+      const int pg = min(2 * t + pp, last_page);
+      const long blk = bt[pg];
+      const bf16_t* kp = k_cache + (blk * Hkv + kvh) * PAGE;
+      const bf16_t* vp = v_cache + (blk * Hkv + kvh) * PAGE;
+      bf16_t* base = lds + buf * 4 * PAGE;
+      pf_stage_page<HD>(base + pp * PAGE, base + 2 * PAGE + pp * PAGE, kp, vp);
+    }
+  };
+
+  stage(0, 0);
+  for (int t = 0; t < ntiles; ++t) {
+    const int buf = t & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t + 1 < ntiles) stage(t + 1, buf ^ 1);
+    if (wave_idle) continue;
+    const bf16_t* kt = lds + buf * 4 * PAGE;
+    const bf16_t* vt = kt + 2 * PAGE;
+    const int key0 = t * PF_TK;
+    // S^T = K . Q^T for 4 key blocks of 16
+    f32x4_t s[PF_NG][4];
+#pragma unroll
+    for (int n = 0; n < PF_NG; ++n)
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) s[n][kb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      const int row = (kb & 1) * 16 + c;                 // key row inside its page
+      const bf16_t* krow = kt + (kb >> 1) * PAGE + row * HD;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const bf16x8_t kf = load_frag16B(krow + 8 * ((ks * 4 + g) ^ kswz<HD>(row)));
+#pragma unroll
+        for (int n = 0; n < PF_NG; ++n) s[n][kb] = mfma16(kf, qf[n][ks], s[n][kb]);
+      }
+    }
+    // online softmax per column group
+    const bool need_mask = key0 + PF_TK - 1 > wave_lo;
+    bf16x8_t pf[PF_NG][2];
+#pragma unroll
+    for (int n = 0; n < PF_NG; ++n) {
+      float x[16];
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = key0 + kb * 16 + 4 * g + r;
+          x[4 * kb + r] = (!need_mask || key <= lim[n]) ? s[n][kb][r] * scale_log2 : -INFINITY;
+        }
+      float mx = x[0];
+#pragma unroll
+      for (int j = 1; j < 16; ++j) mx = fmaxf(mx, x[j]);
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float m_new = fmaxf(m[n], mx);
+      const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
+      const float alpha = exp2f(m[n] - m_use);
+      float rs = 0.f;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) { x[j] = exp2f(x[j] - m_use); rs += x[j]; }
+      rs += __shfl_xor(rs, 16, 64);
+      rs += __shfl_xor(rs, 32, 64);
+      l[n] = l[n] * alpha + rs;
+      m[n] = m_new;
+#pragma unroll
+      for (int i = 0; i < NT; ++i) acc[n][i] *= alpha;
+      // page p: keys 4g+r (block 2p) then 16+4g+r (block 2p+1) -> permuted-k B operand
+#pragma unroll
+      for (int pp = 0; pp < 2; ++pp)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pf[n][pp][j] = (short)f2bf(x[8 * pp + j]);
+    }
+    // O^T += V^T . P^T
+#pragma unroll
+    for (int pp = 0; pp < 2; ++pp) {
+      const bf16_t* vpg = vt + pp * PAGE;
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+        const int d = 16 * i + c;
+        const int sw = 2 * ((d >> 2) & 3);
+        const bf16_t* vr = vpg + d * BS;
+        const bf16x8_t vf = load_frag_2x8B(vr + 4 * (g ^ sw), vr + 4 * ((4 + g) ^ sw));
+#pragma unroll
+        for (int n = 0; n < PF_NG; ++n) acc[n][i] = mfma16(vf, pf[n][pp], acc[n][i]);
+      }
+    }
+  }
+#pragma unroll
+  for (int n = 0; n < PF_NG; ++n) {
+    if (!valid[n]) continue;
+    const int head = kvh * G + (c % G);
+    const float inv = l[n] > 0.f ? 1.f / l[n] : 0.f;
+    bf16_t* orow = out + (long)(qbeg + qi[n]) * out_stride + (long)head * HD;
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+      bf16x4_t o4;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o4[r] = (short)f2bf(acc[n][i][r] * inv);
+      *reinterpret_cast<bf16x4_t*>(orow + 16 * i + 4 * g) = o4;
+    }
+  }
 }
 
 int paged_prefill(const void* q, long q_stride, const void* k_cache, const void* v_cache,
@@ -293,7 +462,8 @@ int paged_prefill(const void* q, long q_stride, const void* k_cache, const void*
   if ((D != 128 && D != 64) || block_size != BS) return -1;
   if (Hq % Hkv != 0 || 16 % (Hq / Hkv) != 0) return -2;
 #define LMX_PRE(HDV)                                                                          \
-  paged_prefill_kernel<HDV><<<dim3(num_tiles, Hkv), dim3(256), 0, stream>>>(                  \
+  paged_prefill_kernel<HDV><<<dim3(num_tiles, Hkv), dim3(256), 2 * 4 * BS * HDV * 2,         \
+                              stream>>>(                                                      \
       (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, \
       bt_stride, cu_q, context_lens, tiles, (bf16_t*)out, out_stride, Hq, Hkv, scale, causal);
   if (D == 128) { LMX_PRE(128) } else { LMX_PRE(64) }

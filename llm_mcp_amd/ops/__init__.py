@@ -178,7 +178,7 @@ def paged_prefill_attention(q: torch.Tensor, k_cache, v_cache, block_tables, cu_
                             context_lens, tiles, scale: float, out: torch.Tensor,
                             causal: bool = True, Hq: int | None = None) -> torch.Tensor:
     """Varlen prefill. q/out: [T, Hq*D] rows; tiles: int32 [(seq, q_start)]
-    built with q_per_tile = 64 / G (see ``prefill_q_per_tile``)."""
+    built with q_per_tile = 128 / G (see ``prefill_q_per_tile``)."""
     NB, Hkv, BS, D = k_cache.shape
     T = q.shape[0]
     Hq = Hq or (q.shape[1] // D)
@@ -200,8 +200,12 @@ def paged_prefill_attention(q: torch.Tensor, k_cache, v_cache, block_tables, cu_
     return out
 
 
+PREFILL_GROUPS_PER_WAVE = 2   # PF_NG in csrc/kernels/attention.hip
+
+
 def prefill_q_per_tile(Hq: int, Hkv: int) -> int:
-    return 4 * (16 // (Hq // Hkv))
+    """Queries per prefill workgroup: 4 waves x PF_NG column groups x 16/G."""
+    return 4 * PREFILL_GROUPS_PER_WAVE * (16 // (Hq // Hkv))
 
 
 # ---------------------------------------------------------------- sampling ---

@@ -247,3 +247,33 @@ def test_gemm_nt_identity_asymmetric():
         torch.bfloat16)
     y = ops.gemm_nt(a, w)
     assert torch.equal(y, w.t().contiguous())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("Hq,Hkv,D", [(32, 8, 128), (12, 12, 64)])
+def test_paged_prefill_long_multi_tile(Hq, Hkv, D):
+    """Several 64-key LDS tiles per workgroup, a ragged last page and a long
+    cached prefix (chunked prefill continuation)."""
+    qlens, prefix = [517, 190], [300, 0]
+    ctxs = [q + p for q, p in zip(qlens, prefix)]
+    S = len(qlens)
+    NB = sum(math.ceil(c / 32) for c in ctxs) + 3
+    kc, vc = _cache(NB, Hkv, D)
+    bt = _random_tables(S, ctxs, NB)
+    cu = torch.tensor([0] + list(torch.cumsum(torch.tensor(qlens), 0)), dtype=torch.int32,
+                      device=DEV)
+    T = int(cu[-1])
+    q = _bf(T, (Hq + 2 * Hkv) * D)
+    qpt = ops.prefill_q_per_tile(Hq, Hkv)
+    tiles = [v for s, ql in enumerate(qlens) for q0 in range(0, ql, qpt) for v in (s, q0)]
+    tiles = torch.tensor(tiles, dtype=torch.int32, device=DEV)
+    ctx = torch.tensor(ctxs, dtype=torch.int32, device=DEV)
+    scale = 1 / math.sqrt(D)
+    for causal in (True, False):
+        out = torch.zeros(T, Hq * D, dtype=torch.bfloat16, device=DEV)
+        ops.paged_prefill_attention(q, kc, vc, bt, cu, ctx, tiles, scale, out, causal=causal,
+                                    Hq=Hq)
+        expect = ref.paged_prefill(q[:, :Hq * D].reshape(T, Hq, D), kc, vc, bt, cu, ctx, scale,
+                                   causal=causal)
+        torch.testing.assert_close(out.float().view(T, Hq, D), expect.float(), atol=2e-2,
+                                   rtol=2e-2)
