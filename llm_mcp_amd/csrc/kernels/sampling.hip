@@ -25,10 +25,30 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   return z ^ (z >> 31);
 }
 
-// uniform in (0,1) from (seed, offset, round, index)
-__device__ __forceinline__ float uniform01(uint64_t seed, uint64_t off, int i) {
-  const uint64_t h = mix64(seed ^ mix64(off * 0x9E3779B97F4A7C15ULL + (uint64_t)i));
-  return ((float)(h >> 40) + 0.5f) * (1.0f / 16777216.0f);
+__device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+
+// Per element: a 32-bit counter hash keyed by a 64-bit (seed, offset, round)
+// key mixed once per row-round (the 64-bit mixing stays off the per-element
+// path: 64-bit multiplies are multi-instruction on CDNA).
+struct RowKey { uint32_t k0, k1; };
+
+__device__ __forceinline__ RowKey row_key(uint64_t seed, uint64_t off, int round) {
+  const uint64_t h = mix64(seed ^ mix64(off * 0x9E3779B97F4A7C15ULL + (uint64_t)round));
+  return RowKey{(uint32_t)h, (uint32_t)(h >> 32)};
+}
+
+// Gumbel(0,1) noise for element i
+__device__ __forceinline__ float gumbel(RowKey k, int i) {
+  const uint32_t h = lowbias32(lowbias32((uint32_t)i * 0x9E3779B9u ^ k.k0) ^ k.k1);
+  const float u = ((float)(h >> 8) + 0.5f) * (1.0f / 16777216.0f);
+  return -__logf(-__logf(u));
 }
 
 template <typename T>
@@ -37,6 +57,26 @@ template <>
 __device__ __forceinline__ float ld<float>(const float* p, int i) { return p[i]; }
 template <>
 __device__ __forceinline__ float ld<bf16_t>(const bf16_t* p, int i) { return bf2f(p[i]); }
+
+// Visit every element of a row: 16-B vector loads (8 bf16 / 4 fp32 per lane
+// and iteration) when the row is 16-B aligned, scalar tail / fallback.
+template <typename T, typename F>
+__device__ __forceinline__ void scan_row(const T* __restrict__ x, int V, F&& f) {
+  constexpr int VEC = 16 / sizeof(T);
+  typedef T vec_t __attribute__((ext_vector_type(VEC)));
+  int done = 0;
+  if ((reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+    const int nv = V / VEC;
+    const vec_t* xv = reinterpret_cast<const vec_t*>(x);
+    for (int b = threadIdx.x; b < nv; b += blockDim.x) {
+      const vec_t w = xv[b];
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) f(b * VEC + j, ld<T>(reinterpret_cast<const T*>(&w), j));
+    }
+    done = nv * VEC;
+  }
+  for (int i = done + threadIdx.x; i < V; i += blockDim.x) f(i, ld<T>(x, i));
+}
 
 struct ArgMax { float v; int i; };
 
@@ -65,77 +105,127 @@ __device__ __forceinline__ ArgMax block_argmax(ArgMax a, float* sv, int* si) {
   return r;
 }
 
+// online (max, sum exp((x - max) * inv_t)) pair
+struct MaxSum { float m, s; };
+
+__device__ __forceinline__ MaxSum ms_combine(MaxSum a, MaxSum b, float inv_t) {
+  const float m = fmaxf(a.m, b.m);
+  if (m == -INFINITY) return MaxSum{m, 0.f};
+  return MaxSum{m, a.s * __expf((a.m - m) * inv_t) + b.s * __expf((b.m - m) * inv_t)};
+}
+
+__device__ __forceinline__ MaxSum block_maxsum(MaxSum a, float inv_t, float* sv, float* sv2) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+    a = ms_combine(a, MaxSum{__shfl_xor(a.m, o, 64), __shfl_xor(a.s, o, 64)}, inv_t);
+  __syncthreads();
+  if (lane == 0) { sv[wid] = a.m; sv2[wid] = a.s; }
+  __syncthreads();
+  MaxSum r{-INFINITY, 0.f};
+  if (lane < nw) r = MaxSum{sv[lane], sv2[lane]};
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+    r = ms_combine(r, MaxSum{__shfl_xor(r.m, o, 64), __shfl_xor(r.s, o, 64)}, inv_t);
+  return r;
+}
+
+// Pass structure (the row is 128256 logits = 256 KB in bf16; B rows do not
+// fit the L2s, so passes are the cost):
+//   pass 1: online max + softmax normaliser + the first Gumbel-max draw,
+//           all from one read of the row;
+//   pass 2 (only with top-k/top-p): mass and count strictly above the
+//           draw -> accept (~1 - top_p rejections) or pivot and redraw.
 template <typename T>
 __global__ void __launch_bounds__(1024) sample_kernel(
     const T* __restrict__ logits, long stride, int V, const float* __restrict__ temperature,
     const int* __restrict__ top_k, const float* __restrict__ top_p,
     const uint64_t* __restrict__ seeds, const int* __restrict__ offsets, int* __restrict__ out_tok,
     float* __restrict__ out_logprob, int max_rounds) {
-  __shared__ float sv[16];
+  __shared__ float sv[16], sv2[16];
   __shared__ int si[16];
   const int row = blockIdx.x;
   const T* x = logits + (long)row * stride;
   const float temp = temperature ? temperature[row] : 0.f;
-  // pass 1: max (and argmax for greedy)
-  ArgMax am{-INFINITY, 0x7fffffff};
-  for (int i = threadIdx.x; i < V; i += blockDim.x) {
-    const float v = ld<T>(x, i);
-    if (v > am.v) { am.v = v; am.i = i; }
-  }
-  am = block_argmax(am, sv, si);
-  const float xmax = am.v;
   const int kk = top_k ? top_k[row] : 0;
   if (!(temp > 0.f) || kk == 1) {
+    // greedy: argmax (+ log-softmax of the winner at T = 1)
+    ArgMax am{-INFINITY, 0x7fffffff};
+    MaxSum ms{-INFINITY, 0.f};
+    const bool want_lp = out_logprob != nullptr;
+    scan_row(x, V, [&](int i, float v) {
+      if (v > am.v) { am.v = v; am.i = i; }
+      if (want_lp) {
+        if (v > ms.m) { ms.s = ms.s * __expf(ms.m - v) + 1.f; ms.m = v; }
+        else ms.s += __expf(v - ms.m);
+      }
+    });
+    am = block_argmax(am, sv, si);
+    if (out_logprob) ms = block_maxsum(ms, 1.f, sv, sv2);
     if (threadIdx.x == 0) {
       out_tok[row] = am.i;
-      if (out_logprob) out_logprob[row] = 0.f;  // filled by pass 2 below when requested
+      if (out_logprob) out_logprob[row] = am.v - ms.m - __logf(ms.s);
     }
-    if (!out_logprob) return;
-    float s = 0.f;
-    for (int i = threadIdx.x; i < V; i += blockDim.x) s += __expf(ld<T>(x, i) - xmax);
-    s = block_sum(s, sv);
-    if (threadIdx.x == 0) out_logprob[row] = -__logf(s);
     return;
   }
   const float inv_t = 1.f / temp;
-  // pass 2: softmax normaliser of z = (x - max)/T
-  float s = 0.f;
-  for (int i = threadIdx.x; i < V; i += blockDim.x) s += __expf((ld<T>(x, i) - xmax) * inv_t);
-  const float S = block_sum(s, sv);
-  const float tp = top_p ? top_p[row] : 1.f;
-  const bool truncate = (tp < 1.f) || (kk > 0 && kk < V);
   const uint64_t seed = seeds ? seeds[row] : 0x1234ULL;
   const uint64_t off = offsets ? (uint64_t)offsets[row] : 0ULL;
-  float pivot = -INFINITY;
-  int chosen = -1;
-  for (int round = 0; round < (truncate ? max_rounds : 1); ++round) {
-    ArgMax g{-INFINITY, 0x7fffffff};
-    const uint64_t roff = off * 64 + round;
-    for (int i = threadIdx.x; i < V; i += blockDim.x) {
-      const float z = (ld<T>(x, i) - xmax) * inv_t;
-      if (z > pivot) {
-        const float u = uniform01(seed, roff, i);
-        const float key = z - __logf(-__logf(u));
-        if (key > g.v) { g.v = key; g.i = i; }
+  // pass 1
+  RowKey key = row_key(seed, off, 0);
+  ArgMax g{-INFINITY, 0x7fffffff};
+  MaxSum ms{-INFINITY, 0.f};
+  scan_row(x, V, [&](int i, float v) {
+    if (v > ms.m) { ms.s = ms.s * __expf((ms.m - v) * inv_t) + 1.f; ms.m = v; }
+    else ms.s += __expf((v - ms.m) * inv_t);
+    const float k = v * inv_t + gumbel(key, i);
+    if (k > g.v) { g.v = k; g.i = i; }
+  });
+  g = block_argmax(g, sv, si);
+  ms = block_maxsum(ms, inv_t, sv, sv2);
+  const float xmax = ms.m, S = ms.s;        // z_i = (x_i - xmax) / T, S = sum exp(z)
+  const float tp = top_p ? top_p[row] : 1.f;
+  const bool truncate = (tp < 1.f) || (kk > 0 && kk < V);
+  int chosen = g.i;
+  if (truncate) {
+    float pivot = -INFINITY;
+    chosen = -1;
+    int j = g.i;
+    for (int round = 0; round < max_rounds; ++round) {
+      if (round > 0) {
+        // redraw restricted to z > pivot
+        key = row_key(seed, off, round);
+        ArgMax h{-INFINITY, 0x7fffffff};
+        scan_row(x, V, [&](int i, float v) {
+          const float z = (v - xmax) * inv_t;
+          if (z > pivot) {
+            const float k = z + gumbel(key, i);
+            if (k > h.v) { h.v = k; h.i = i; }
+          }
+        });
+        j = block_argmax(h, sv, si).i;
       }
+      float mass = 0.f, cnt = 0.f;
+      // z > zj  <=>  x > xj (T > 0): compare raw logits, exp only above
+      const float xj = ld<T>(x, j);
+      scan_row(x, V, [&](int i, float v) {
+        if (v > xj) { mass += __expf((v - xmax) * inv_t); cnt += 1.f; }
+      });
+      mass = block_sum(mass, sv) / S;
+      cnt = block_sum(cnt, sv);
+      const bool in_p = mass < tp;
+      const bool in_k = (kk <= 0) || (cnt < (float)kk);
+      if (in_p && in_k) { chosen = j; break; }
+      pivot = (xj - xmax) * inv_t;
     }
-    g = block_argmax(g, sv, si);
-    const int j = g.i;
-    if (!truncate) { chosen = j; break; }
-    const float zj = (ld<T>(x, j) - xmax) * inv_t;
-    float mass = 0.f, cnt = 0.f;
-    for (int i = threadIdx.x; i < V; i += blockDim.x) {
-      const float z = (ld<T>(x, i) - xmax) * inv_t;
-      if (z > zj) { mass += __expf(z); cnt += 1.f; }
+    if (chosen < 0) {   // fallback: the argmax is inside every truncation
+      ArgMax am{-INFINITY, 0x7fffffff};
+      scan_row(x, V, [&](int i, float v) {
+        if (v > am.v) { am.v = v; am.i = i; }
+      });
+      chosen = block_argmax(am, sv, si).i;
     }
-    mass = block_sum(mass, sv) / S;
-    cnt = block_sum(cnt, sv);
-    const bool in_p = mass < tp;
-    const bool in_k = (kk <= 0) || (cnt < (float)kk);
-    if (in_p && in_k) { chosen = j; break; }
-    pivot = zj;
   }
-  if (chosen < 0) chosen = am.i;
   if (threadIdx.x == 0) {
     out_tok[row] = chosen;
     if (out_logprob) out_logprob[row] = (ld<T>(x, chosen) - xmax) * inv_t - __logf(S);
