@@ -49,6 +49,9 @@ def main() -> None:
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--inproc", action="store_true",
                     help="serve HTTP from the GPU process (default: separate API process)")
+    ap.add_argument("--rehearse-on-one-gpu", action="store_true",
+                    help="multi-rank rehearsal on a 1-GPU box: every rank uses device 0, gloo "
+                         "process group, a fixed KV budget (never used for reported numbers)")
     a = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -83,17 +86,22 @@ def main() -> None:
     from llm_mcp_amd.models.tokenizer import for_model
     from llm_mcp_amd.utils.metrics import Metrics
 
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    gpu = 0 if a.rehearse_on_one_gpu else local_rank
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if a.rehearse_on_one_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
     ops.native()  # fail loudly if the HIP kernels are missing
 
     t_init = time.time()
     ecfg = EngineConfig(model=a.model, max_num_seqs=max(a.concurrency, 1),
                         max_batched_tokens=a.max_batched_tokens,
                         max_model_len=min(8192, a.prompt_len + a.max_tokens + 64),
-                        use_graphs=not a.no_graphs, seed=rank)
+                        use_graphs=not a.no_graphs, seed=rank,
+                        kv_cache_gb=24 if a.rehearse_on_one_gpu else None)
     engine = LLMEngine(ecfg, device=dev)
     log(f"engine ready in {time.time() - t_init:.1f}s: {engine.num_blocks} KV blocks, "
         f"{len(engine.graphs)} decode graphs, weights {engine.model.weight_bytes() / 1e9:.1f} GB")
