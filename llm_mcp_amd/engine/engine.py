@@ -222,8 +222,9 @@ class LLMEngine:
         self.num_blocks = max(16, kv_bytes // per_block)
         if self.tp.size > 1:
             # the leader's scheduler hands out page ids for every rank
+            gloo = torch.distributed.get_backend(self.tp.group) == "gloo"
             t = torch.tensor([self.num_blocks], dtype=torch.int64,
-                             device=self.device if self.device.type == "cuda" else "cpu")
+                             device="cpu" if gloo else self.device)
             torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MIN,
                                          group=self.tp.group)
             self.num_blocks = int(t.item())

@@ -55,15 +55,27 @@ class TPContext:
 
     def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
         if self.size > 1:
-            torch.distributed.all_reduce(t, group=self.group)
+            if self._host_staged(t):
+                h = t.cpu()
+                torch.distributed.all_reduce(h, group=self.group)
+                t.copy_(h)
+            else:
+                torch.distributed.all_reduce(t, group=self.group)
         return t
+
+    def _host_staged(self, t: torch.Tensor) -> bool:
+        # gloo only reduces device tensors; it gathers host tensors
+        return t.is_cuda and torch.distributed.get_backend(self.group) == "gloo"
 
     def all_gather_last(self, t: torch.Tensor) -> torch.Tensor:
         if self.size == 1:
             return t
-        parts = [torch.empty_like(t) for _ in range(self.size)]
-        torch.distributed.all_gather(parts, t.contiguous(), group=self.group)
-        return torch.cat(parts, dim=-1)
+        src = t.contiguous()
+        if self._host_staged(src):
+            src = src.cpu()
+        parts = [torch.empty_like(src) for _ in range(self.size)]
+        torch.distributed.all_gather(parts, src, group=self.group)
+        return torch.cat(parts, dim=-1).to(t.device, non_blocking=True)
 
 
 class LlamaModel:

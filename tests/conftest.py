@@ -14,9 +14,12 @@ def pytest_configure(config):
 
 
 def _has_gpu() -> bool:
+    # device_count() does not initialise HIP on this image (is_available() does):
+    # GPU tests that spawn rank processes must run before the parent touches
+    # the device (tests/test_00_tp_gpu.py)
     try:
         import torch
-        return torch.cuda.is_available()
+        return torch.cuda.device_count() > 0
     except Exception:
         return False
 

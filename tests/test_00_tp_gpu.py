@@ -1,0 +1,83 @@
+"""Tensor-parallel engine group on the GPU kernels (runs first in the GPU
+session: the rank processes are spawned before this pytest process touches
+the device).
+
+A 1-GPU box cannot host two RCCL ranks, so the two ranks share cuda:0 over a
+gloo process group (device tensors staged through the host where gloo needs
+it).  Everything else is the production TP path: per-rank shards from the HF
+safetensors loader, the leader's plan mailbox, the HIP kernels on each shard,
+all-reduces after the O and down projections and the vocab-split LM head."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+PROMPTS = [list(range(10, 50)), list(range(5, 100)), [7] * 33, [3]]
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank(rank, size, port, ckpt, tag, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(size), LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+
+    from llm_mcp_amd.engine.engine import EngineConfig, SamplingParams
+    from llm_mcp_amd.parallel.tp_worker import build_tp_engine, init_group
+    torch.cuda.set_device(0)
+    tp = init_group("cpu")   # gloo group, GPU tensors
+    ecfg = EngineConfig(model="tiny-llama", max_num_seqs=8, max_batched_tokens=64,
+                        max_model_len=512, use_graphs=False, kv_cache_gb=0.05)
+    eng = build_tp_engine(ecfg, torch.device("cuda", 0), tp, tag, weights_path=ckpt)
+    try:
+        if rank == 0:
+            out = eng.generate(PROMPTS, SamplingParams(temperature=0, max_tokens=6,
+                                                       ignore_eos=True))
+            eng.release_followers()
+            q.put(("leader", out))
+        else:
+            q.put(("follower", eng.run_follower()))
+    finally:
+        eng.chan.close()
+        dist.destroy_process_group()
+
+
+def test_tp2_group_on_gpu_kernels(tmp_path):
+    from llm_mcp_amd.models import config as mc
+    from llm_mcp_amd.models.llama import LlamaModel
+    from llm_mcp_amd.models.weights import save_hf_llama
+    from tests.dense_ref import assert_greedy_consistent
+    cfg = mc.resolve("tiny-llama")
+    full = LlamaModel(cfg, "cpu", seed=11)          # CPU only in this process
+    save_hf_llama(full.w, cfg, str(tmp_path))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    tag = f"gputest-{os.getpid()}-{_free_port()}"
+    port = _free_port()
+    procs = [ctx.Process(target=_rank, args=(r, 2, port, str(tmp_path), tag, q), daemon=True)
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        res = dict(q.get(timeout=400) for _ in procs)
+        for p in procs:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+    assert res["follower"] > 0
+    for prompt, out in zip(PROMPTS, res["leader"]):
+        assert len(out) == 6
+        assert_greedy_consistent(full, prompt, out)
