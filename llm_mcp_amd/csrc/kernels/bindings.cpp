@@ -28,6 +28,8 @@ int glu(void*, const void*, long, int, int, hipStream_t);
 int embed_gather(void*, const void*, const int*, int, int, int, int, hipStream_t);
 int mean_pool_l2(float*, const void*, const int*, int, int, int, int, hipStream_t);
 int bias_act(void*, const void*, long, int, int, hipStream_t);
+int gemm_splitk(void*, const void*, const void*, float*, int*, int, int, int, long, long, long,
+                int, hipStream_t);
 int gemm_nt(void*, const void*, const void*, const void*, const void*, int, int, int, long, long,
             long, int, hipStream_t);
 }  // namespace lmx
@@ -116,6 +118,12 @@ PYBIND11_MODULE(_lmx_kernels, m) {
   });
   m.def("bias_act", [](uptr x, uptr bias, long rows, int n, int act, uptr stream) {
     check(lmx::bias_act(P<void>(x), P<void>(bias), rows, n, act, S(stream)), "bias_act");
+  });
+  m.def("gemm_splitk", [](uptr C, uptr A, uptr W, uptr slabs, uptr tickets, int M, int N, int K,
+                          long lda, long ldw, long ldc, int splits, uptr stream) {
+    check(lmx::gemm_splitk(P<void>(C), P<void>(A), P<void>(W), P<float>(slabs), P<int>(tickets), M,
+                           N, K, lda, ldw, ldc, splits, S(stream)),
+          "gemm_splitk");
   });
   m.def("gemm_nt", [](uptr C, uptr A, uptr W, uptr bias, uptr residual, int M, int N, int K,
                       long lda, long ldw, long ldc, int act, uptr stream) {

@@ -152,4 +152,212 @@ int gemm_nt(void* C, const void* A, const void* W, const void* bias, const void*
   return (int)hipGetLastError();
 }
 
+// --------------------------------------------------------------------------
+// Decode-shape GEMM (M <= 256):  C[M,N] = A[M,K] . W[N,K]^T, bf16 out.
+//
+// hipBLASLt picks 48-96 workgroup tilings for the QKV / O projections at
+// M = 256 (a fifth of the 256 CUs) and the in-graph step runs them 2-4x off
+// the weight-streaming roofline (profiles/r1_gemm_decode_shapes.md).  This
+// kernel follows the guide's M = 256 projection recipe instead:
+//   * one workgroup = all BM rows x 64 columns, K split S ways so that
+//     (N/64) * S ~ one workgroup per CU;
+//   * 512 threads = 8 waves; BM = 256: 8 x 1 waves of 32 rows; BM = 128:
+//     4 x 2; BM = 64: 2 x 4 (wave tile 32 x 64/WN, 16x16x32 MFMA);
+//   * A (activations, L2-resident, re-read by every column tile) and W (read
+//     once from HBM) move by global_load_lds into an XOR-swizzled [row][64]
+//     image, double-buffered (BK = 64);
+//   * split-K partials: fp32 slabs + arrival ticket; the last-arriving slice
+//     sums the slabs and writes the bf16 tile (agent-scope release/acquire,
+//     counters zeroed by the launcher's memset node).
+// --------------------------------------------------------------------------
+constexpr int SK_BN = 64, SK_BK = 64, SK_THREADS = 512;
+
+template <int BM>
+__device__ __forceinline__ void sk_stage(bf16_t* lds_a, bf16_t* lds_w,
+                                         const bf16_t* __restrict__ A, long lda, int M,
+                                         const bf16_t* __restrict__ W, long ldw, int n0, int k0) {
+  const int t = threadIdx.x, wave = t >> 6;
+  // 512 threads x 16 B = 64 rows x 64 bf16 per instruction
+#pragma unroll
+  for (int i = 0; i < BM / 64; ++i) {
+    const int r = i * 64 + (t >> 3), c = t & 7;
+    const int gr = r < M ? r : M - 1;   // clamped rows are masked at the store
+    glds16(A + (long)gr * lda + k0 + 8 * (c ^ swz(r)), lds_a + i * 64 * SK_BK + wave * 8 * SK_BK);
+  }
+  const int r = t >> 3, c = t & 7;
+  glds16(W + (long)(n0 + r) * ldw + k0 + 8 * (c ^ swz(r)), lds_w + wave * 8 * SK_BK);
+}
+
+template <int CNT>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(CNT) : "memory");
+}
+
+// stages in the LDS ring: enough K-steps in flight to cover HBM latency with
+// one workgroup per CU (a 2-stage ring leaves one in flight: latency-bound)
+template <int BM> struct SkCfg;
+template <> struct SkCfg<64> { static constexpr int NST = 6; };
+template <> struct SkCfg<128> { static constexpr int NST = 4; };
+template <> struct SkCfg<256> { static constexpr int NST = 3; };
+
+template <int BM>
+__global__ void __launch_bounds__(SK_THREADS, 1) gemm_splitk_kernel(
+    bf16_t* __restrict__ C, const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
+    float* __restrict__ slabs, int* __restrict__ tickets, int M, int N, int K, long lda,
+    long ldw, long ldc, int splits) {
+  constexpr int WM = BM / 32, WN = 8 / WM, NJ = 4 / WN;   // waves along M / N, col tiles
+  constexpr int NST = SkCfg<BM>::NST;
+  constexpr int LPS = BM / 64 + 1;                         // glds per thread per stage
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* const lds = reinterpret_cast<bf16_t*>(smem);
+  constexpr int STAGE = (BM + SK_BN) * SK_BK;              // elements per stage
+
+  const int tiles_n = N / SK_BN;
+  const int nwg = tiles_n * splits;
+  const int wg = xcd_remap(blockIdx.x, nwg);
+  // the K slices of one column tile get neighbouring ids (same XCD after the
+  // remap), so the last arriver reads its partner slabs from its own L2
+  const int tn = wg / splits, ks = wg % splits;
+  const int n0 = tn * SK_BN;
+  const int kc = K / splits, kbeg = ks * kc;
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wr = wave % WM, wc = wave / WM;
+  const int fr = lane & 15, fg = lane >> 4;
+
+  f32x4_t acc[2][NJ];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = kc / SK_BK;
+  // prologue: NST-1 stages in flight
+#pragma unroll
+  for (int p = 0; p < NST - 1; ++p)
+    if (p < nk) {
+      bf16_t* b = lds + p * STAGE;
+      sk_stage<BM>(b, b + BM * SK_BK, A, lda, M, W, ldw, n0, kbeg + p * SK_BK);
+    }
+  for (int t = 0; t < nk; ++t) {
+    // stage t landed when at most (stages issued after it) x LPS loads remain
+    if (t + NST - 2 < nk) vm_wait<(NST - 2) * LPS>(); else vm_wait<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();      // raw: __syncthreads would drain the ring
+    if (t + NST - 1 < nk) {            // refill the slot every wave finished at t-1
+      bf16_t* b = lds + ((t + NST - 1) % NST) * STAGE;
+      sk_stage<BM>(b, b + BM * SK_BK, A, lda, M, W, ldw, n0, kbeg + (t + NST - 1) * SK_BK);
+    }
+    const bf16_t* a_t = lds + (t % NST) * STAGE;
+    const bf16_t* w_t = a_t + BM * SK_BK;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8_t af[2], bw[NJ];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = lds_frag(a_t, wr * 32 + i * 16 + fr, kk * 4 + fg);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        bw[j] = lds_frag(w_t, wc * (SK_BN / WN) + j * 16 + fr, kk * 4 + fg);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = mfma16(af[i], bw[j], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
+  vm_wait<0>();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // acc[i][j]: row = wr*32 + 16i + 4fg + r, col = n0 + wc*(64/WN) + 16j + fr
+  if (splits == 1) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int col = n0 + wc * (SK_BN / WN) + 16 * j + fr;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = wr * 32 + 16 * i + 4 * fg + r;
+          if (row < M) C[(long)row * ldc + col] = f2bf(acc[i][j][r]);
+        }
+      }
+    return;
+  }
+  // split-K: publish this slice's fp32 partial tile
+  float* slab = slabs + (long)ks * M * N;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int col = n0 + wc * (SK_BN / WN) + 16 * j + fr;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wr * 32 + 16 * i + 4 * fg + r;
+        if (row < M) slab[(long)row * N + col] = acc[i][j][r];
+      }
+    }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int* flag = reinterpret_cast<int*>(smem);   // reuse the one LDS array (no 2nd __shared__)
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int old = __hip_atomic_fetch_add(&tickets[tn], 1, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+    *flag = (old == splits - 1);
+  }
+  __syncthreads();
+  if (!*flag) return;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    tickets[tn] = 0;   // re-armed for the next call (the memset node also zeroes it)
+  }
+  __syncthreads();
+  // last arriver: C[:, n0:n0+64] = sum_s slab[s]   (float4 per thread, 16 per row)
+  for (int e = threadIdx.x; e < M * (SK_BN / 4); e += SK_THREADS) {
+    const int row = e / (SK_BN / 4), c4 = (e % (SK_BN / 4)) * 4;
+    float4 sum = {0.f, 0.f, 0.f, 0.f};
+    for (int s2 = 0; s2 < splits; ++s2) {
+      const float4 v = *reinterpret_cast<const float4*>(slabs + (long)s2 * M * N +
+                                                        (long)row * N + n0 + c4);
+      sum.x += v.x; sum.y += v.y; sum.z += v.z; sum.w += v.w;
+    }
+    bf16x4_t o;
+    o[0] = (short)f2bf(sum.x); o[1] = (short)f2bf(sum.y);
+    o[2] = (short)f2bf(sum.z); o[3] = (short)f2bf(sum.w);
+    *reinterpret_cast<bf16x4_t*>(C + (long)row * ldc + n0 + c4) = o;
+  }
+}
+
+int gemm_splitk(void* C, const void* A, const void* W, float* slabs, int* tickets, int M, int N,
+                int K, long lda, long ldw, long ldc, int splits, hipStream_t stream) {
+  if (M <= 0) return 0;
+  if (M > 256 || N % SK_BN != 0 || splits < 1 || K % (splits * SK_BK) != 0) return -1;
+  if (splits > 1 && (slabs == nullptr || tickets == nullptr)) return -2;
+  const int BM = M <= 64 ? 64 : (M <= 128 ? 128 : 256);
+  const int nwg = (N / SK_BN) * splits;
+  const int nst = BM == 64 ? SkCfg<64>::NST : (BM == 128 ? SkCfg<128>::NST : SkCfg<256>::NST);
+  const size_t smem = (size_t)nst * (BM + SK_BN) * SK_BK * sizeof(bf16_t);
+  if (splits > 1) {
+    const hipError_t e = hipMemsetAsync(tickets, 0, sizeof(int) * (N / SK_BN), stream);
+    if (e != hipSuccess) return (int)e;
+  }
+  static bool attr_set[3] = {false, false, false};   // > 64 KiB dynamic LDS (BM = 256)
+#define LMX_SK(BMV)                                                                          \
+  if (!attr_set[BMV / 128]) {                                                                \
+    hipFuncSetAttribute((const void*)gemm_splitk_kernel<BMV>,                                 \
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);               \
+    attr_set[BMV / 128] = true;                                                              \
+  }                                                                                          \
+  gemm_splitk_kernel<BMV><<<dim3(nwg), dim3(SK_THREADS), smem, stream>>>(                    \
+      (bf16_t*)C, (const bf16_t*)A, (const bf16_t*)W, slabs, tickets, M, N, K, lda, ldw, ldc,  \
+      splits);
+  if (BM == 64) { LMX_SK(64) } else if (BM == 128) { LMX_SK(128) } else { LMX_SK(256) }
+#undef LMX_SK
+  return (int)hipGetLastError();
+}
+
 }  // namespace lmx

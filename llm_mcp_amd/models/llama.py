@@ -161,7 +161,7 @@ class LlamaModel:
                 h = ops.rms_norm(x, L["ln1"], cfg.rms_eps)
             else:
                 h = ops.rms_norm(x, L["ln1"], cfg.rms_eps, residual=residual)
-            qkv = F.linear(h, L["wqkv"])
+            qkv = ops.linear(h, L["wqkv"])
             kc, vc = k_caches[li], v_caches[li]
             ops.rope_and_cache(qkv, inp.positions, self.cos_sin, Hq, Hkv, D, inp.slots, kc, vc)
             if nd > 0:
@@ -172,11 +172,11 @@ class LlamaModel:
                 ops.paged_prefill_attention(qkv, kc, vc, inp.block_tables[nd:],
                                             inp.cu_q[nd:], inp.context_lens[nd:],
                                             inp.prefill_tiles, self.scale, attn, Hq=Hq)
-            o = self.tp.all_reduce(F.linear(attn, L["wo"]))
+            o = self.tp.all_reduce(ops.linear(attn, L["wo"]))
             h = ops.rms_norm(o, L["ln2"], cfg.rms_eps, residual=residual)
-            gu = F.linear(h, L["w_gate_up"])
+            gu = ops.linear(h, L["w_gate_up"])
             a = ops.silu_mul(gu)
-            x = self.tp.all_reduce(F.linear(a, L["w_down"]))
+            x = self.tp.all_reduce(ops.linear(a, L["w_down"]))
         # final norm only on the rows we sample from
         rows = inp.sample_rows
         xs = x.index_select(0, rows)

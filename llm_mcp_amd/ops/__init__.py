@@ -324,3 +324,91 @@ def gemm_nt(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, 
 
 def gemm_nt_supported(N: int, K: int) -> bool:
     return N % 128 == 0 and K % 64 == 0
+
+
+# ------------------------------------------------------- decode GEMM (M<=256) --
+_SK_WS: dict = {}        # (device, stream) -> (slabs fp32, tickets int32)
+SPLITK_MAX_M = 256
+
+
+def splitk_splits(N: int, K: int, target_blocks: int = 256) -> int:
+    """K-split so that (N/64) * splits ~ one workgroup per CU (guide: 'Projection
+    GEMM at M = 256', decomposition first)."""
+    tiles = N // 64
+    s = max(1, min(8, round(target_blocks / max(1, tiles))))
+    while s > 1 and K % (s * 64) != 0:
+        s -= 1
+    return s
+
+
+def gemm_splitk_supported(M: int, N: int, K: int) -> bool:
+    return 0 < M <= SPLITK_MAX_M and N % 64 == 0 and K % 64 == 0
+
+
+def _sk_workspace(dev: torch.device, n_floats: int, n_tickets: int):
+    key = (dev.index, _stream())
+    ws = _SK_WS.get(key)
+    if ws is None or ws[0].numel() < n_floats or ws[1].numel() < n_tickets:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("gemm_splitk workspace must be allocated before graph capture "
+                               "(run the shape once eagerly)")
+        n_floats = max(n_floats, ws[0].numel() if ws else 0)
+        n_tickets = max(n_tickets, 4096, ws[1].numel() if ws else 0)
+        ws = (torch.empty(n_floats, dtype=torch.float32, device=dev),
+              torch.zeros(n_tickets, dtype=torch.int32, device=dev))
+        _SK_WS[key] = ws
+    return ws
+
+
+def gemm_splitk(a: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None,
+                splits: int | None = None) -> torch.Tensor:
+    """a @ w^T for decode-sized M (<= 256) on the split-K MFMA kernel."""
+    M, K = a.shape
+    N = w.shape[0]
+    if not a.is_cuda:
+        y = ref.gemm_nt(a, w, None, 0, None)
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
+    _bf16(a, "a"); _bf16(w, "w")
+    _chk(gemm_splitk_supported(M, N, K), f"gemm_splitk shape M={M} N={N} K={K}")
+    _chk(w.shape[1] == K and a.stride(1) == 1 and w.stride(1) == 1, "gemm_splitk layout")
+    _chk(a.stride(0) % 8 == 0 and w.stride(0) % 8 == 0 and a.data_ptr() % 16 == 0
+         and w.data_ptr() % 16 == 0, "gemm_splitk operands need 16-B aligned rows")
+    s = splits or splitk_splits(N, K)
+    _chk(K % (s * 64) == 0, "K must split into 64-multiples")
+    if out is None:
+        out = torch.empty((M, N), dtype=a.dtype, device=a.device)
+    _chk(out.shape == (M, N) and out.stride(1) == 1 and out.stride(0) % 4 == 0
+         and out.data_ptr() % 8 == 0, "gemm_splitk output layout")
+    slabs, tickets = (None, None)
+    if s > 1:
+        slabs, tickets = _sk_workspace(a.device, s * M * N, N // 64)
+    native().gemm_splitk(_ptr(out), _ptr(a), _ptr(w), _ptr(slabs), _ptr(tickets), M, N, K,
+                         a.stride(0), w.stride(0), out.stride(0), s, _stream())
+    return out
+
+
+def splitk_preferred(M: int, N: int, K: int) -> bool:
+    """Measured dispatch (profiles/r1_splitk_gemm.md, cold weights on MI355X):
+    the split-K kernel beats hipBLASLt for wide gate/up projections at
+    M <= 32, for the long-K down projection at 48 <= M <= 160 and for
+    square projections at M <= 16; hipBLASLt wins elsewhere."""
+    if not gemm_splitk_supported(M, N, K):
+        return False
+    if N >= 16384 and K <= 8192:
+        return M <= 32
+    if K >= 8192:
+        return 48 <= M <= 160
+    if N == K:
+        return M <= 16
+    return False
+
+
+def linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """x @ w^T: the split-K MFMA kernel where it was measured faster, else
+    hipBLASLt (torch F.linear)."""
+    if x.is_cuda and x.dim() == 2 and splitk_preferred(x.shape[0], w.shape[0], w.shape[1]):
+        return gemm_splitk(x, w)
+    return torch.nn.functional.linear(x, w)

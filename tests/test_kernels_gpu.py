@@ -277,3 +277,39 @@ def test_paged_prefill_long_multi_tile(Hq, Hkv, D):
                                    causal=causal)
         torch.testing.assert_close(out.float().view(T, Hq, D), expect.float(), atol=2e-2,
                                    rtol=2e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M", [1, 7, 64, 100, 256])
+@pytest.mark.parametrize("N,K,splits", [(384, 1024, 1), (6144, 4096, 2), (1024, 3584, 4),
+                                        (640, 2048, 8)])
+def test_gemm_splitk_vs_fp32(M, N, K, splits):
+    a = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) * K ** -0.5).to(torch.bfloat16)
+    out = ops.gemm_splitk(a, w, splits=splits)
+    expect = a.float() @ w.float().t()
+    torch.testing.assert_close(out.float(), expect, atol=2e-2, rtol=2e-2)
+    # twice in a row: tickets re-armed, slabs reused
+    out2 = ops.gemm_splitk(a, w, splits=splits)
+    assert torch.equal(out, out2)
+
+
+@pytest.mark.gpu
+def test_gemm_splitk_in_graph_strided_input():
+    M, K, N = 48, 4096, 6144
+    x = torch.randn(M, K + 64, device=DEV).to(torch.bfloat16)[:, :K]   # row stride K + 64
+    w = (torch.randn(N, K, device=DEV) * K ** -0.5).to(torch.bfloat16)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    ops.gemm_splitk(x, w, out)                       # allocates the workspace eagerly
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        ops.gemm_splitk(x, w, out)
+    torch.cuda.current_stream().wait_stream(s)
+    with torch.cuda.graph(g, stream=s):
+        ops.gemm_splitk(x, w, out)
+    x.copy_(torch.randn(M, K + 64, device=DEV).to(torch.bfloat16)[:, :K])
+    g.replay()
+    torch.cuda.synchronize()
+    torch.testing.assert_close(out.float(), x.float() @ w.float().t(), atol=2e-2, rtol=2e-2)
