@@ -74,7 +74,10 @@ class ChatHandler:
         if not isinstance(messages, list) or not messages:
             return write_error(400, "messages_required", "Field 'messages' is required")
         model = body.get("model") or ""
-        extra_headers = {}
+        # request id: honoured from the client or minted here,
+        # echoed on the response and logged with the completion record
+        rid = request.headers.get("X-Request-ID") or uuid.uuid4().hex
+        extra_headers = {"X-Request-ID": rid}
         if not model:
             selector = getattr(st, "select_model", None)
             selected = None

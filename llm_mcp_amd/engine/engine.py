@@ -33,6 +33,7 @@ import torch
 from .. import ops
 from ..models.config import LlamaConfig
 from ..models.llama import LlamaModel, StepInputs, TPContext
+from ..utils.faults import faults
 
 log = logging.getLogger("lmx.engine")
 
@@ -200,6 +201,11 @@ class LLMEngine:
                       "t_update": 0.0, "t_gpu": 0.0, "decode_step_s": 0.0}
         self._pending = None
         self._fetch_cpu = None
+        self._step_started = 0.0
+        self._last_error = None
+        # LMX_TORCH_PROFILE=/dir[:steps]: torch.profiler timeline of N steps
+        self._prof = None
+        self._prof_spec = os.environ.get("LMX_TORCH_PROFILE", "")
         if self.device.type == "cuda":
             self._hout = torch.zeros((2, ecfg.max_num_seqs), dtype=torch.int32, pin_memory=True)
             self._hout_np = self._hout.numpy()
@@ -363,11 +369,16 @@ class LLMEngine:
     def _loop(self):
         if self.device.type == "cuda":
             torch.cuda.set_device(self.device)
+        if self._prof_spec:
+            d, _, n = self._prof_spec.partition(":")
+            self.start_profile(d, int(n or 20))
         while not self._stop.is_set():
             try:
                 did = self.step()
-            except Exception:  # keep serving: fail the in-flight requests
+            except Exception as e:  # keep serving: fail the in-flight requests
                 log.exception("engine step failed")
+                if "hip" in str(e).lower():
+                    self._last_error = str(e)[:200]
                 self._fail_all("engine_error")
                 did = False
             if not did:
@@ -417,6 +428,19 @@ class LLMEngine:
             self.event_sink(evs)
 
     # -------------------------------------------------------------- step ----
+    def healthy(self, timeout_s: float | None = None) -> tuple[bool, str]:
+        """Watchdog view for the worker agent: a step in flight for longer
+        than LMX_STEP_TIMEOUT (default 120 s) or an engine error means the
+        GPU is hung or broken."""
+        limit = timeout_s if timeout_s is not None else float(
+            os.environ.get("LMX_STEP_TIMEOUT", "120"))
+        if self._last_error is not None:
+            return False, f"engine error: {self._last_error}"
+        t = self._step_started
+        if t and time.monotonic() - t > limit:
+            return False, f"engine step running for {time.monotonic() - t:.0f}s"
+        return True, ""
+
     def step(self) -> bool:
         """One engine step, software-pipelined against the GPU:
 
@@ -431,6 +455,20 @@ class LLMEngine:
         if not self.sched.has_work:
             self._flush_pending()
             return False
+        self._step_started = time.monotonic()
+        try:
+            return self._step()
+        finally:
+            self._step_started = 0.0
+
+    def _step(self) -> bool:
+        fl = faults()
+        if fl:
+            if fl.hit("step_hang"):
+                time.sleep(float(os.environ.get("LMX_FAULT_HANG_S", "5")))
+            fl.maybe_raise("gpu_error", "HIP error: injected device fault")
+        if self._prof is not None:
+            self._prof_tick()
         t0 = time.perf_counter()
         plan = self.sched.schedule(self.q_per_tile)
         T = plan["num_tokens"]
@@ -478,6 +516,27 @@ class LLMEngine:
         st["prefill_tokens"] += plan["num_prefill_tokens"]
         st["generated_tokens"] += N
         return True
+
+    def start_profile(self, out_dir: str, steps: int = 20):
+        """Record a torch.profiler (ROCm/roctracer) timeline of the next
+        ``steps`` engine steps into ``out_dir`` (chrome trace)."""
+        from torch.profiler import ProfilerActivity, profile
+        acts = [ProfilerActivity.CPU] + ([ProfilerActivity.CUDA]
+                                         if self.device.type == "cuda" else [])
+        self._prof = profile(activities=acts, record_shapes=False)
+        self._prof.__enter__()
+        self._prof_left = steps
+        self._prof_dir = out_dir
+
+    def _prof_tick(self):
+        self._prof_left -= 1
+        if self._prof_left < 0:
+            self._prof.__exit__(None, None, None)
+            os.makedirs(self._prof_dir, exist_ok=True)
+            path = os.path.join(self._prof_dir, f"engine_steps_{os.getpid()}.json")
+            self._prof.export_chrome_trace(path)
+            log.info("engine profile written to %s", path)
+            self._prof = None
 
     def _flush_pending(self):
         """Turn the previous step's sampled tokens into TokenEvents."""

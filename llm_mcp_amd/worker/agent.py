@@ -20,6 +20,7 @@ import os
 import socket
 import time
 
+from ..utils.faults import faults
 from .jobs import JobError, JobRunner
 
 log = logging.getLogger("lmx.worker")
@@ -38,7 +39,8 @@ def should_mark_offline(exc: Exception) -> bool:
 class WorkerAgent:
     def __init__(self, client, runner: JobRunner, device_id: str, worker_id: str = "",
                  kinds: list[str] | None = None, lease_s: int = 60, capacity: int = 64,
-                 name: str = "", tags: dict | None = None, mark_offline=None):
+                 name: str = "", tags: dict | None = None, mark_offline=None,
+                 health=None):
         self.client = client  # rpc.client.CoreClient (sync; called via to_thread)
         self.runner = runner
         self.device_id = device_id
@@ -49,6 +51,10 @@ class WorkerAgent:
         self.name = name or socket.gethostname()
         self.tags = dict(tags or {})
         self.mark_offline = mark_offline  # callable(device_id, reason) or None
+        # callable() -> (ok, reason): a hung or failed engine stops heartbeating
+        # so the core requeues its leases when they expire
+        self.health = health
+        self._reported_unhealthy = False
         self.inflight: dict[str, asyncio.Task] = {}
         self._stop = asyncio.Event()
         self.stats = {"claimed": 0, "done": 0, "failed": 0, "lease_lost": 0}
@@ -88,6 +94,9 @@ class WorkerAgent:
             if j is None:
                 continue
             self.stats["claimed"] += 1
+            if faults().hit("claim_drop"):     # vanish with the lease: it must expire
+                self.stats["dropped"] = self.stats.get("dropped", 0) + 1
+                continue
             t = asyncio.create_task(self._run_job(j))
             self.inflight[j["id"]] = t
             t.add_done_callback(lambda _t, jid=j["id"]: self.inflight.pop(jid, None))
@@ -101,6 +110,18 @@ class WorkerAgent:
         period = max(5.0, self.lease_s / 2)
         while True:
             await asyncio.sleep(period)
+            if self.health is not None:
+                ok, why = self.health()
+                if not ok:
+                    # let the lease lapse: the core hands the job to another GPU
+                    log.error("engine unhealthy (%s): not extending %s", why, jid)
+                    if not self._reported_unhealthy and self.mark_offline:
+                        self._reported_unhealthy = True
+                        try:
+                            await asyncio.to_thread(self.mark_offline, self.device_id, why)
+                        except Exception:
+                            pass
+                    continue
             try:
                 ok = await asyncio.to_thread(self.client.heartbeat, self.worker_id, jid,
                                              self.lease_s, token)
@@ -116,6 +137,7 @@ class WorkerAgent:
         hb = asyncio.create_task(self._heartbeat(jid, token))
         t0 = time.time()
         try:
+            faults().maybe_raise("job_crash", "injected job crash")
             result, metrics = await self.runner.handle(j["kind"], j.get("payload") or {})
             metrics = dict(metrics or {})
             metrics.setdefault("ms", int((time.time() - t0) * 1000))

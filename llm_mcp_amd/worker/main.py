@@ -134,7 +134,8 @@ def serve_engines(a, engine, embed, device_id: str) -> None:
                                 worker_id=os.environ.get("WORKER_ID", f"worker-{device_id}"),
                                 lease_s=a.lease_seconds, capacity=a.max_num_seqs,
                                 tags={"engine": True, "models": list(info["models"])},
-                                mark_offline=mark_offline)
+                                mark_offline=mark_offline,
+                                health=engine.healthy if engine is not None else None)
             task = asyncio.create_task(agent.run())
         await stop.wait()
         if agent is not None:
