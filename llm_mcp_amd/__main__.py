@@ -8,6 +8,7 @@
   bridge     HTTP bridge (:3333)
   telemetry  alert loop
   build      compile the native extensions in-tree
+  config     print every environment setting (typed, defaults, current)
 
 The parent of ``serve`` never initialises HIP: GPUs are enumerated from sysfs
 and every worker is spawned before anything touches a device.
@@ -163,7 +164,11 @@ def main(argv=None):
     sub.add_parser("bridge")
     sub.add_parser("telemetry")
     sub.add_parser("build")
+    sub.add_parser("config")
     args, rest = ap.parse_known_args(argv)
+    if args.cmd != "config":
+        from . import settings
+        settings.validate()
     if args.cmd == "serve":
         cmd_serve(args)
     elif args.cmd == "core":
@@ -181,6 +186,9 @@ def main(argv=None):
     elif args.cmd == "telemetry":
         from .telemetry.alerts import main as tm
         tm()
+    elif args.cmd == "config":
+        from .settings import table
+        print(table())
     elif args.cmd == "build":
         from .build import build_all
         build_all(force="--force" in rest, verbose=True)

@@ -1,0 +1,123 @@
+"""Typed settings: every environment variable the framework reads, with its
+type, default and meaning.
+
+The reference is configured by environment variables only, scattered over
+the Go core, the Python worker, the bridge and telemetry
+(core/internal/config/config.go:9-34, worker/llm_worker/main.py:52-539,
+mcp/src/index.ts:7-10, telemetry/llm_telemetry/main.py:139-145).  The same
+names are honoured here (compatibility), the dead ones are dropped, and the
+new ones carry the LMX_ prefix.  ``python -m llm_mcp_amd config`` prints the
+table with the current values (secrets masked); ``validate()`` type-checks
+the environment at process start.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+
+
+@dataclass(frozen=True)
+class Var:
+    name: str
+    type: type
+    default: object
+    doc: str
+    secret: bool = False
+
+
+VARS: list[Var] = [
+    # ---- control plane (reference names) ----
+    Var("CORE_HTTP_ADDR", str, ":8080", "core HTTP listen address"),
+    Var("CORE_GRPC_ADDR", str, ":9090", "core gRPC address (listen on core, dial on workers)"),
+    Var("CORE_HTTP_URL", str, "http://127.0.0.1:8080", "core URL used by workers / bridge"),
+    Var("CORE_VERSION", str, "0.1.0", "version reported by /health (falls back to LLM_MCP_VERSION)"),
+    Var("DB_DSN", str, "", "Postgres DSN (postgres://user:pass@host:5432/db?sslmode=disable)",
+        secret=True),
+    Var("DISCOVERY_INTERVAL", int, 0, "seconds between discovery runs (0 = off)"),
+    Var("DEVICE_LIMITS_INTERVAL", int, 0, "seconds between device-limit refreshes"),
+    Var("DEVICE_MAX_CONCURRENCY", int, 1, "jobs per device for devices without a capacity tag"),
+    Var("DEVICE_LIMITS_JSON", str, "", "per-device limit specs (JSON, '*' = default)"),
+    Var("DEVICE_LIMITS_FILE", str, "", "file with the device limit specs"),
+    Var("STRICT_MODEL_LIMITS", int, 0, "1: unknown model size/context counts as too large"),
+    Var("OPENROUTER_API_KEY", str, "", "cloud catalogue / cloud provider key", secret=True),
+    Var("OPENROUTER_BASE_URL", str, "https://openrouter.ai/api/v1", "OpenRouter API base"),
+    Var("OPENAI_API_KEY", str, "", "OpenAI key (cloud provider)", secret=True),
+    Var("OPENAI_BASE_URL", str, "https://api.openai.com/v1", "OpenAI API base"),
+    Var("CLOUD_EMBED_DIMENSIONS", int, 0, "Matryoshka truncation for cloud embeddings"),
+    Var("LIGHTRAG_URL", str, "", "knowledge ingest target (LightRAG)"),
+    Var("LIGHTRAG_API_KEY", str, "", "LightRAG key (no built-in default)", secret=True),
+    Var("MEM0_URL", str, "", "knowledge ingest target (mem0)"),
+    # ---- worker (reference names) ----
+    Var("WORKER_ID", str, "", "worker id (default worker-<device>)"),
+    Var("WORKER_LEASE_SECONDS", int, 60, "lease length; heartbeat every max(5, lease/2) s"),
+    Var("WORKER_KINDS", str, "", "comma list of job kinds this worker claims (empty = all)"),
+    # ---- bridge / MCP / telemetry (reference names) ----
+    Var("MCP_HTTP_ADDR", str, "0.0.0.0:3333", "HTTP bridge listen address"),
+    Var("BACKEND_URL", str, "http://localhost:3333", "MCP tool server -> bridge URL"),
+    Var("MCP_PORT", int, 8765, "MCP streamable-HTTP port (mcp --http)"),
+    Var("TELEMETRY_CHECK_INTERVAL", int, 30, "alert loop period (s)"),
+    Var("ALERT_FAIL_THRESHOLD", int, 3, "attempts before a failed job is alerted"),
+    Var("TELEGRAM_BOT_TOKEN", str, "", "Telegram alert sink", secret=True),
+    Var("TELEGRAM_CHAT_ID", str, "", "Telegram chat (REPORT_CHAT_ID also accepted)"),
+    Var("ALERT_WEBHOOK_URL", str, "", "webhook alert sink"),
+    Var("LOG_LEVEL", str, "INFO", "python logging level"),
+    # ---- MI355X serving (new) ----
+    Var("LMX_STORE", str, "memory", "memory[:journal] | postgres"),
+    Var("LMX_JOURNAL", str, "", "native queue journal file (crash durability, memory store)"),
+    Var("LMX_SNAPSHOT", str, "", "catalog snapshot file (memory store)"),
+    Var("LMX_GPUS", str, "", "GPUs served by `serve` (e.g. 0-7); default all enumerated"),
+    Var("LMX_CHAT_MODEL", str, "llama-3-8b", "chat model preset / alias"),
+    Var("LMX_EMBED_MODEL", str, "", "embedding model preset (e.g. nomic-embed-text)"),
+    Var("LMX_TP", int, 1, "tensor-parallel degree of a chat-model group"),
+    Var("LMX_MAX_BATCH", int, 256, "max concurrent sequences per engine"),
+    Var("LMX_ALLOW_CLOUD", int, 0, "1: allow cloud providers (never on the GPU hot path)"),
+    Var("LMX_JOB_RETENTION_DAYS", float, 7.0, "purge finished jobs older than this"),
+    Var("LMX_MAINTENANCE_INTERVAL", int, 60, "seconds between store maintenance ticks"),
+    Var("LMX_JOB_STREAM_MAX_S", int, 3600, "max duration of one /v1/jobs/{id}/stream"),
+    Var("LMX_PEER_NODES", str, "", "other nodes' core URLs polled by discovery"),
+    Var("LMX_NODE_ID", str, "", "host id used in device ids (default hostname)"),
+    Var("LMX_FAKE_GPUS", int, 0, "enumerate N fake GPUs (tests / CPU hosts)"),
+    Var("LMX_ALERT_TEMP_C", float, 95.0, "GPU temperature alert threshold"),
+    Var("LMX_STEP_TIMEOUT", float, 120.0, "engine watchdog: a longer step marks the GPU hung"),
+    Var("LMX_TORCH_PROFILE", str, "", "dir[:steps] -- torch.profiler timeline of engine steps"),
+    Var("LMX_FAULT", str, "", "fault injection spec (job_crash:p,claim_drop:p,gpu_error:p,...)"),
+    Var("LMX_FAULT_SEED", int, 0, "fault injection RNG seed"),
+    Var("LMX_AUTOBUILD", int, 1, "build missing native extensions on import"),
+    Var("LMX_OFFLOAD_ARCH", str, "gfx950", "hipcc --offload-arch for the kernels"),
+    Var("HSA_ENABLE_IPC_MODE_LEGACY", str, "0", "keep 0: dmabuf IPC for RCCL between ranks"),
+]
+
+_BY_NAME = {v.name: v for v in VARS}
+
+
+class SettingsError(ValueError):
+    pass
+
+
+def get(name: str):
+    """Typed value of a registered variable (environment or default)."""
+    v = _BY_NAME[name]
+    raw = os.environ.get(name)
+    if raw is None or raw == "":
+        if name == "CORE_VERSION" and os.environ.get("LLM_MCP_VERSION"):
+            return os.environ["LLM_MCP_VERSION"]
+        return v.default
+    try:
+        return v.type(raw)
+    except ValueError as e:
+        raise SettingsError(f"{name}={raw!r} is not a valid {v.type.__name__}") from e
+
+
+def validate() -> dict:
+    """Type-check every registered variable present in the environment."""
+    return {v.name: get(v.name) for v in VARS}
+
+
+def table(mask: bool = True) -> str:
+    rows = ["| variable | type | default | current | meaning |", "|---|---|---|---|---|"]
+    for v in VARS:
+        cur = os.environ.get(v.name, "")
+        if cur and v.secret and mask:
+            cur = "***"
+        rows.append(f"| `{v.name}` | {v.type.__name__} | `{v.default}` | `{cur}` | {v.doc} |")
+    return "\n".join(rows)
