@@ -22,6 +22,7 @@ import json
 import logging
 import os
 import threading
+import re
 import time
 import urllib.request
 
@@ -29,6 +30,15 @@ from ..policy.inference import model_record
 from . import rocm_enum
 
 log = logging.getLogger("lmx.discovery")
+
+
+def tp_members(dev: str, host: str) -> tuple[int, list[str]]:
+    """``<host>:tp8:gpu0-7`` -> (8, [<host>:gpu0, ..., <host>:gpu7])."""
+    m = re.search(r":tp(\d+):gpu(\d+)-(\d+)$", dev)
+    if not m:
+        return 0, []
+    tp, a, b = (int(x) for x in m.groups())
+    return tp, [rocm_enum.device_id(i, host) for i in range(a, b + 1)]
 
 
 class DiscoveryRunner:
@@ -71,8 +81,10 @@ class DiscoveryRunner:
         # multi-GPU (TP) engines registered under a group id
         for dev, ms in served.items():
             if ":tp" in dev and not any(d["id"] == dev for d in out):
+                tp, members = tp_members(dev, host)
                 out.append({"id": dev, "name": dev, "platform": "rocm", "arch": "gfx950",
                             "host": host, "tags": {"engine": True, "rocm": True, "tp_group": True,
+                                                   "tp": tp, "members": members,
                                                    "models": sorted({m.model_id for m in ms}),
                                                    "capacity": max(m.capacity for m in ms)},
                             "models": [(m.model_id, m.cfg, m.max_model_len) for m in ms]})

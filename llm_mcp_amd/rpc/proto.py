@@ -19,9 +19,9 @@ SCALARS = {"string": F.TYPE_STRING, "int32": F.TYPE_INT32, "int64": F.TYPE_INT64
            "bytes": F.TYPE_BYTES, "uint32": F.TYPE_UINT32, "uint64": F.TYPE_UINT64}
 
 
-def parse(text: str) -> descriptor_pb2.FileDescriptorProto:
+def parse(text: str, name: str = "llm.proto") -> descriptor_pb2.FileDescriptorProto:
     text = re.sub(r"//[^\n]*", "", text)
-    fd = descriptor_pb2.FileDescriptorProto(name="llm.proto", syntax="proto3")
+    fd = descriptor_pb2.FileDescriptorProto(name=name, syntax="proto3")
     fd.package = re.search(r"package\s+([\w.]+)\s*;", text).group(1)
     for name, body in re.findall(r"message\s+(\w+)\s*\{([^}]*)\}", text):
         m = fd.message_type.add(name=name)
@@ -36,10 +36,12 @@ def parse(text: str) -> descriptor_pb2.FileDescriptorProto:
                 f.type_name = f".{fd.package}.{typ}"
     for sname, body in re.findall(r"service\s+(\w+)\s*\{(.*?)\n\}", text, re.S):
         s = fd.service.add(name=sname)
-        for mname, inp, stream, out in re.findall(
-                r"rpc\s+(\w+)\s*\(\s*(\w+)\s*\)\s*returns\s*\(\s*(stream\s+)?(\w+)\s*\)", body):
+        for mname, cstream, inp, stream, out in re.findall(
+                r"rpc\s+(\w+)\s*\(\s*(stream\s+)?(\w+)\s*\)\s*returns\s*\(\s*(stream\s+)?(\w+)\s*\)",
+                body):
             s.method.add(name=mname, input_type=f".{fd.package}.{inp}",
-                         output_type=f".{fd.package}.{out}", server_streaming=bool(stream))
+                         output_type=f".{fd.package}.{out}", server_streaming=bool(stream),
+                         client_streaming=bool(cstream))
     return fd
 
 
@@ -52,6 +54,16 @@ METHODS = {m.name: (m.input_type.rsplit(".", 1)[1], m.output_type.rsplit(".", 1)
                     m.server_streaming) for m in FILE.service[0].method}
 msgs = {m.name: message_factory.GetMessageClass(_pool.FindMessageTypeByName(f"{PACKAGE}.{m.name}"))
         for m in FILE.message_type}
+
+
+# server reflection messages (separate pool: their own package)
+REFLECTION_FILE = parse(PROTO.with_name("reflection.proto").read_text(), "reflection.proto")
+_rpool = descriptor_pool.DescriptorPool()
+_rpool.Add(REFLECTION_FILE)
+REFLECTION_SERVICE = f"{REFLECTION_FILE.package}.{REFLECTION_FILE.service[0].name}"
+reflection = {m.name: message_factory.GetMessageClass(
+    _rpool.FindMessageTypeByName(f"{REFLECTION_FILE.package}.{m.name}"))
+    for m in REFLECTION_FILE.message_type}
 
 
 def __getattr__(name):  # pb.SubmitJobRequest etc.

@@ -181,12 +181,58 @@ def generic_handler(service: CoreService):
     return grpc.method_handlers_generic_handler(pb.SERVICE, handlers)
 
 
+def reflection_handler():
+    """grpc.reflection.v1alpha.ServerReflection (and the v1 name) over the
+    runtime-built descriptors, so grpcurl / grpc_cli can list and describe
+    llmmcp.v1.Core.  The reference documents reflection but never registers
+    it (doc/README.md:352-357 vs core/cmd/core/main.go:92-93)."""
+    R = pb.reflection
+    services = [pb.SERVICE, pb.REFLECTION_SERVICE]
+    files = {pb.FILE.name: pb.FILE, pb.REFLECTION_FILE.name: pb.REFLECTION_FILE}
+
+    def file_for_symbol(sym: str):
+        for f in files.values():
+            if sym == f.package or sym.startswith(f.package + "."):
+                return f
+        return None
+
+    async def info(request_iterator, context):
+        async for req in request_iterator:
+            resp = R["ServerReflectionResponse"](valid_host=req.host, original_request=req)
+            f = None
+            if req.list_services:
+                resp.list_services_response.service.extend(
+                    [R["ServiceResponse"](name=n) for n in services])
+            elif req.file_by_filename or req.file_containing_symbol:
+                f = files.get(req.file_by_filename) if req.file_by_filename else \
+                    file_for_symbol(req.file_containing_symbol)
+                if f is None:
+                    resp.error_response.error_code = grpc.StatusCode.NOT_FOUND.value[0]
+                    resp.error_response.error_message = "symbol or file not found"
+                else:
+                    resp.file_descriptor_response.file_descriptor_proto.append(
+                        f.SerializeToString())
+            else:
+                resp.error_response.error_code = grpc.StatusCode.UNIMPLEMENTED.value[0]
+                resp.error_response.error_message = "request kind not supported"
+            yield resp
+
+    h = grpc.stream_stream_rpc_method_handler(
+        info, request_deserializer=R["ServerReflectionRequest"].FromString,
+        response_serializer=R["ServerReflectionResponse"].SerializeToString)
+    return [grpc.method_handlers_generic_handler(pb.REFLECTION_SERVICE,
+                                                 {"ServerReflectionInfo": h}),
+            grpc.method_handlers_generic_handler("grpc.reflection.v1.ServerReflection",
+                                                 {"ServerReflectionInfo": h})]
+
+
 async def start_grpc(state, addr: str | None = None):
     addr = addr or os.environ.get("CORE_GRPC_ADDR", ":9090")
     if addr.startswith(":"):
         addr = "0.0.0.0" + addr
     server = grpc.aio.server()
-    server.add_generic_rpc_handlers((generic_handler(CoreService(state)),))
+    server.add_generic_rpc_handlers((generic_handler(CoreService(state)),
+                                     *reflection_handler()))
     port = server.add_insecure_port(addr)
     await server.start()
     log.info("gRPC listening on %s", addr)

@@ -75,3 +75,47 @@ def test_grpc_claim_long_poll_wakes_on_submit(core):
     jid = c.submit("k", {})
     th.join(10)
     assert out["job"]["id"] == jid and out["dt"] < 3.0
+
+
+def test_server_reflection_lists_and_describes_core():
+    import asyncio
+    import threading
+    import time
+
+    import grpc
+    from google.protobuf import descriptor_pb2
+
+    from llm_mcp_amd.api.core import CoreState
+    from llm_mcp_amd.rpc import proto as pb
+    from llm_mcp_amd.rpc.server import start_grpc
+    from llm_mcp_amd.store.memory import MemoryStore
+
+    loop = asyncio.new_event_loop()
+    box = {}
+
+    def run():
+        asyncio.set_event_loop(loop)
+        box["srv"], box["port"] = loop.run_until_complete(
+            start_grpc(CoreState(store=MemoryStore()), "127.0.0.1:0"))
+        loop.run_forever()
+
+    threading.Thread(target=run, daemon=True).start()
+    while "port" not in box:
+        time.sleep(0.01)
+    R = pb.reflection
+    ch = grpc.insecure_channel(f"127.0.0.1:{box['port']}")
+    call = ch.stream_stream(f"/{pb.REFLECTION_SERVICE}/ServerReflectionInfo",
+                            request_serializer=R["ServerReflectionRequest"].SerializeToString,
+                            response_deserializer=R["ServerReflectionResponse"].FromString)
+    reqs = [R["ServerReflectionRequest"](list_services="*"),
+            R["ServerReflectionRequest"](file_containing_symbol="llmmcp.v1.Core"),
+            R["ServerReflectionRequest"](file_containing_symbol="nope.Nothing")]
+    out = list(call(iter(reqs)))
+    names = [s.name for s in out[0].list_services_response.service]
+    assert "llmmcp.v1.Core" in names
+    fd = descriptor_pb2.FileDescriptorProto.FromString(
+        out[1].file_descriptor_response.file_descriptor_proto[0])
+    assert fd.package == "llmmcp.v1" and "ClaimJob" in [m.name for m in fd.service[0].method]
+    assert out[2].error_response.error_code == grpc.StatusCode.NOT_FOUND.value[0]
+    ch.close()
+    loop.call_soon_threadsafe(loop.stop)
