@@ -150,6 +150,33 @@ class _FixedMeta:
         self.dev_t.copy_(self.host_t, non_blocking=True)
 
 
+_TUNING_LOADED = False
+
+
+def _load_gemm_tuning() -> None:
+    """Load the cold-cache hipBLASLt solution table for the served shapes
+    (bench/tune_gemms.py) into PyTorch TunableOp, tuning disabled at serve
+    time.  LMX_TUNABLEOP=0 turns it off; shapes absent from the table keep
+    the library heuristic; a table from another ROCm / hipBLASLt build is
+    rejected by TunableOp's validators."""
+    global _TUNING_LOADED
+    if _TUNING_LOADED or os.environ.get("LMX_TUNABLEOP", "1") != "1":
+        return
+    _TUNING_LOADED = True
+    path = os.environ.get("LMX_TUNABLEOP_FILE") or os.path.join(
+        os.path.dirname(os.path.dirname(__file__)), "config", "tunableop_gfx950.csv")
+    if not os.path.exists(path):
+        return
+    tun = torch.cuda.tunable
+    tun.enable(True)
+    tun.tuning_enable(False)
+    tun.record_untuned_enable(False)
+    ok = tun.read_file(path)
+    log.info("GEMM tuning table %s: %s", path, "loaded" if ok else "rejected")
+    if not ok:
+        tun.enable(False)
+
+
 class LLMEngine:
     def __init__(self, ecfg: EngineConfig, device: str | torch.device = "cuda",
                  model_cfg: LlamaConfig | None = None, tp: TPContext | None = None,
@@ -168,6 +195,8 @@ class LLMEngine:
             self.device = torch.device("cuda", torch.cuda.current_device())
         self.cfg = model_cfg or mc.resolve(ecfg.model)
         self.max_model_len = min(ecfg.max_model_len, self.cfg.max_position)
+        if self.device.type == "cuda":
+            _load_gemm_tuning()
         self.model = LlamaModel(self.cfg, self.device, tp=tp, seed=ecfg.seed, weights=weights)
         self.tp = self.model.tp
         self.is_leader = self.tp.rank == 0

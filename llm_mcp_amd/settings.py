@@ -83,6 +83,8 @@ VARS: list[Var] = [
     Var("LMX_FAULT", str, "", "fault injection spec (job_crash:p,claim_drop:p,gpu_error:p,...)"),
     Var("LMX_FAULT_SEED", int, 0, "fault injection RNG seed"),
     Var("LMX_AUTOBUILD", int, 1, "build missing native extensions on import"),
+    Var("LMX_TUNABLEOP", int, 1, "load the cold-cache hipBLASLt solution table at engine start"),
+    Var("LMX_TUNABLEOP_FILE", str, "", "solution table (default llm_mcp_amd/config/tunableop_gfx950.csv)"),
     Var("LMX_OFFLOAD_ARCH", str, "gfx950", "hipcc --offload-arch for the kernels"),
     Var("HSA_ENABLE_IPC_MODE_LEGACY", str, "0", "keep 0: dmabuf IPC for RCCL between ranks"),
 ]
