@@ -14,7 +14,7 @@ int rmsnorm(void*, void*, const void*, const void*, int, int, long, long, float,
 int layernorm(void*, const void*, const void*, const void*, const void*, int, int, float,
               hipStream_t);
 int rope_cache(void*, long, const int*, const float*, int, int, int, int, const int*, void*, void*,
-               int, int, hipStream_t);
+               int, int, int, hipStream_t);
 int kv_write(const void*, const void*, long, const int*, int, int, int, void*, void*, int,
              hipStream_t);
 int paged_decode(const void*, long, const void*, const void*, const int*, int, const int*, void*,
@@ -65,9 +65,10 @@ PYBIND11_MODULE(_lmx_kernels, m) {
   });
   m.def("rope_cache", [](uptr qkv, long qkv_stride, uptr positions, uptr cos_sin, int T, int Hq,
                          int Hkv, int D, uptr slots, uptr kc, uptr vc, int BS, int rot_k,
-                         uptr stream) {
+                         int tile_from, uptr stream) {
     check(lmx::rope_cache(P<void>(qkv), qkv_stride, P<int>(positions), P<float>(cos_sin), T, Hq, Hkv,
-                          D, P<int>(slots), P<void>(kc), P<void>(vc), BS, rot_k, S(stream)),
+                          D, P<int>(slots), P<void>(kc), P<void>(vc), BS, rot_k, tile_from,
+                          S(stream)),
           "rope_cache");
   });
   m.def("kv_write", [](uptr k, uptr v, long stride, uptr slots, int T, int Hkv, int D, uptr kc,

@@ -59,6 +59,10 @@ __device__ __forceinline__ float apply_act(float v, int act) {
   return v;
 }
 
+// Two-buffer loop (vmcnt(0) + barrier per K-step); 2-3 workgroups per CU
+// hide the latency.  A 3-slot counted-vmcnt ring at 1 workgroup per CU was
+// measured 1.4-1.6x SLOWER on the nomic shapes (K = 768 / 3072), as the
+// guide predicts for the 128^2 structure.
 __global__ void __launch_bounds__(256, 2) gemm_nt_kernel(
     bf16_t* __restrict__ C, const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
     const bf16_t* __restrict__ bias, const bf16_t* __restrict__ residual, int M, int N, int K,
@@ -89,18 +93,8 @@ __global__ void __launch_bounds__(256, 2) gemm_nt_kernel(
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   const int nk = K / GBK;
-  stage_tile(lds, A, lda, m0, M, 0);
-  stage_tile(lds + GBM * GBK, W, ldw, n0, N, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int t = 0; t < nk; ++t) {
-    const int cur = t & 1;
-    if (t + 1 < nk) {
-      bf16_t* nb = lds + (cur ^ 1) * 2 * GBM * GBK;
-      stage_tile(nb, A, lda, m0, M, (t + 1) * GBK);
-      stage_tile(nb + GBM * GBK, W, ldw, n0, N, (t + 1) * GBK);
-    }
-    const bf16_t* a_t = lds + cur * 2 * GBM * GBK;
+  constexpr int STAGE = 2 * GBM * GBK;     // A + B tile elements
+  auto compute = [&](const bf16_t* a_t) {
     const bf16_t* b_t = a_t + GBM * GBK;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -109,33 +103,52 @@ __global__ void __launch_bounds__(256, 2) gemm_nt_kernel(
       for (int i = 0; i < 4; ++i) af[i] = lds_frag(a_t, wr * 64 + i * 16 + fr, ks * 4 + fg);
 #pragma unroll
       for (int j = 0; j < 4; ++j) bfr[j] = lds_frag(b_t, wc * 64 + j * 16 + fr, ks * 4 + fg);
+      // operands swapped (D = W_tile . A_tile^T): a lane's 4 accumulator
+      // registers are 4 consecutive output COLUMNS of one row, so the
+      // epilogue stores 8 B per lane instead of four scattered 2-B stores
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(bfr[j], af[i], acc[i][j]);
       __builtin_amdgcn_s_setprio(0);
     }
+  };
+  stage_tile(lds, A, lda, m0, M, 0);
+  stage_tile(lds + GBM * GBK, W, ldw, n0, N, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int t = 0; t < nk; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < nk) {
+      bf16_t* nb = lds + (cur ^ 1) * STAGE;
+      stage_tile(nb, A, lda, m0, M, (t + 1) * GBK);
+      stage_tile(nb + GBM * GBK, W, ldw, n0, N, (t + 1) * GBK);
+    }
+    compute(lds + cur * STAGE);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
-  // epilogue: acc[i][j] is the 16x16 tile with S^T-free standard map
-  //   row = m0 + wr*64 + 16i + 4fg + r, col = n0 + wc*64 + 16j + fr
+  // epilogue: acc[i][j][r] = C[row][col + r] with
+  //   row = m0 + wr*64 + 16i + fr, col = n0 + wc*64 + 16j + 4fg
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int col = n0 + wc * 64 + 16 * j + fr;
-    const float bv = bias ? bf2f(bias[col]) : 0.f;
+  for (int i = 0; i < 4; ++i) {
+    const int row = m0 + wr * 64 + 16 * i + fr;
+    if (row >= M) continue;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int j = 0; j < 4; ++j) {
+      const int col = n0 + wc * 64 + 16 * j + 4 * fg;
+      bf16x4_t bv4 = {0, 0, 0, 0}, rv4 = {0, 0, 0, 0};
+      if (bias) bv4 = *reinterpret_cast<const bf16x4_t*>(bias + col);
+      if (residual) rv4 = *reinterpret_cast<const bf16x4_t*>(residual + (long)row * ldc + col);
+      bf16x4_t o;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wr * 64 + 16 * i + 4 * fg + r;
-        if (row < M) {
-          float v = apply_act(acc[i][j][r] + bv, act);
-          if (residual) v += bf2f(residual[(long)row * ldc + col]);
-          C[(long)row * ldc + col] = f2bf(v);
-        }
+        float v = apply_act(acc[i][j][r] + (bias ? bf2f((uint16_t)bv4[r]) : 0.f), act);
+        if (residual) v += bf2f((uint16_t)rv4[r]);
+        o[r] = (short)f2bf(v);
       }
+      *reinterpret_cast<bf16x4_t*>(C + (long)row * ldc + col) = o;
     }
   }
 }
@@ -348,7 +361,7 @@ int gemm_splitk(void* C, const void* A, const void* W, float* slabs, int* ticket
   static bool attr_set[3] = {false, false, false};   // > 64 KiB dynamic LDS (BM = 256)
 #define LMX_SK(BMV)                                                                          \
   if (!attr_set[BMV / 128]) {                                                                \
-    hipFuncSetAttribute((const void*)gemm_splitk_kernel<BMV>,                                 \
+    (void)hipFuncSetAttribute((const void*)gemm_splitk_kernel<BMV>,                                 \
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);               \
     attr_set[BMV / 128] = true;                                                              \
   }                                                                                          \

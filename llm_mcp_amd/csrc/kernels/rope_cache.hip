@@ -68,14 +68,107 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(
   }
 }
 
+// Prefill rows: 32 consecutive tokens per workgroup.  Rotation and the K
+// write as above; V goes through an LDS tile so that the transposed cache page
+// ([D][BS]) is written in whole rows -- a thread stores 8 consecutive tokens
+// of one d (16 B) whenever their slots are consecutive and 8-aligned (always
+// true inside a prefill chunk), and a wave covers 16 full 64-B page rows.
+// The per-token kernel's 2-B scatter remains for decode rows (one token per
+// page per step, nothing to coalesce).
+constexpr int RT = 32;
+
+__global__ void __launch_bounds__(256) rope_cache_tiled_kernel(
+    bf16_t* __restrict__ qkv, long qkv_stride, const int* __restrict__ positions,
+    const float* __restrict__ cos_sin, int row0, int T, int Hq, int Hkv, int D,
+    const int* __restrict__ slot_mapping, bf16_t* __restrict__ k_cache,
+    bf16_t* __restrict__ v_cache, int BS, int rotate_k_inplace) {
+  __shared__ __attribute__((aligned(16))) bf16_t vt[RT * (256 + 8)];
+  __shared__ int sslot[RT];
+  const int t0 = row0 + blockIdx.x * RT;
+  const int nt = min(RT, T - t0);
+  const int half = D >> 1, tph = half >> 2;
+  if (threadIdx.x < RT)
+    sslot[threadIdx.x] = (threadIdx.x < nt && slot_mapping) ? slot_mapping[t0 + threadIdx.x] : -1;
+  __syncthreads();
+  const int per_tok = (Hq + Hkv) * tph;
+  for (int it = threadIdx.x; it < nt * per_tok; it += blockDim.x) {
+    const int tt = it / per_tok, rem = it - tt * per_tok;
+    const int h = rem / tph, i = (rem % tph) * 4;
+    bf16_t* hp = qkv + (long)(t0 + tt) * qkv_stride + (long)h * D;
+    const float* cs = cos_sin + (long)positions[t0 + tt] * D;
+    const int slot = sslot[tt];
+    const bf16x4_t x1 = *reinterpret_cast<const bf16x4_t*>(hp + i);
+    const bf16x4_t x2 = *reinterpret_cast<const bf16x4_t*>(hp + half + i);
+    const float4 c = *reinterpret_cast<const float4*>(cs + i);
+    const float4 sn = *reinterpret_cast<const float4*>(cs + half + i);
+    const float cc[4] = {c.x, c.y, c.z, c.w}, ss[4] = {sn.x, sn.y, sn.z, sn.w};
+    bf16x4_t o1, o2;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float a = bf2f((uint16_t)x1[j]), b = bf2f((uint16_t)x2[j]);
+      o1[j] = (short)f2bf(a * cc[j] - b * ss[j]);
+      o2[j] = (short)f2bf(b * cc[j] + a * ss[j]);
+    }
+    const bool is_k = h >= Hq;
+    if (!is_k || rotate_k_inplace || slot < 0) {
+      *reinterpret_cast<bf16x4_t*>(hp + i) = o1;
+      *reinterpret_cast<bf16x4_t*>(hp + half + i) = o2;
+    }
+    if (is_k && slot >= 0 && k_cache) {
+      bf16_t* kp = k_cache + (((long)(slot / BS) * Hkv + (h - Hq)) * BS + slot % BS) * D;
+      *reinterpret_cast<bf16x4_t*>(kp + i) = o1;
+      *reinterpret_cast<bf16x4_t*>(kp + half + i) = o2;
+    }
+  }
+  if (!v_cache || !slot_mapping) return;
+  const int LD = D + 8, chunks = D / 8;
+  for (int h = 0; h < Hkv; ++h) {
+    for (int it = threadIdx.x; it < nt * chunks; it += blockDim.x) {
+      const int tt = it / chunks, c = it - tt * chunks;
+      const bf16_t* src = qkv + (long)(t0 + tt) * qkv_stride + (long)(Hq + Hkv + h) * D + 8 * c;
+      *reinterpret_cast<u16x8*>(&vt[tt * LD + 8 * c]) = *reinterpret_cast<const u16x8*>(src);
+    }
+    __syncthreads();
+    for (int it = threadIdx.x; it < D * (RT / 8); it += blockDim.x) {
+      const int d = it / (RT / 8), tt0 = (it % (RT / 8)) * 8;
+      if (tt0 >= nt) continue;
+      const int s0 = sslot[tt0];
+      bool vec = tt0 + 8 <= nt && s0 >= 0 && (s0 % 8) == 0 && BS % 8 == 0;
+#pragma unroll
+      for (int j = 1; j < 8; ++j) vec = vec && sslot[tt0 + j] == s0 + j;
+      if (vec) {
+        u16x8 w;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) w.v[j] = vt[(tt0 + j) * LD + d];
+        *reinterpret_cast<u16x8*>(v_cache + (((long)(s0 / BS) * Hkv + h) * D + d) * BS +
+                                  s0 % BS) = w;
+      } else {
+        for (int j = 0; j < 8 && tt0 + j < nt; ++j) {
+          const int sl = sslot[tt0 + j];
+          if (sl >= 0)
+            v_cache[(((long)(sl / BS) * Hkv + h) * D + d) * BS + sl % BS] =
+                vt[(tt0 + j) * LD + d];
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
 int rope_cache(void* qkv, long qkv_stride, const int* positions, const float* cos_sin, int T,
                int Hq, int Hkv, int D, const int* slot_mapping, void* k_cache, void* v_cache,
-               int BS, int rotate_k_inplace, hipStream_t stream) {
+               int BS, int rotate_k_inplace, int tile_from, hipStream_t stream) {
   if (T <= 0) return 0;
   if (D % 8 != 0 || D > 256) return -1;
-  rope_cache_kernel<<<dim3(T), dim3(256), 0, stream>>>(
-      (bf16_t*)qkv, qkv_stride, positions, cos_sin, Hq, Hkv, D, slot_mapping,
-      (bf16_t*)k_cache, (bf16_t*)v_cache, BS, rotate_k_inplace);
+  const int n1 = tile_from < 0 ? 0 : (tile_from > T ? T : tile_from);
+  if (n1 > 0)
+    rope_cache_kernel<<<dim3(n1), dim3(256), 0, stream>>>(
+        (bf16_t*)qkv, qkv_stride, positions, cos_sin, Hq, Hkv, D, slot_mapping,
+        (bf16_t*)k_cache, (bf16_t*)v_cache, BS, rotate_k_inplace);
+  if (T > n1)
+    rope_cache_tiled_kernel<<<dim3((T - n1 + RT - 1) / RT), dim3(256), 0, stream>>>(
+        (bf16_t*)qkv, qkv_stride, positions, cos_sin, n1, T, Hq, Hkv, D, slot_mapping,
+        (bf16_t*)k_cache, (bf16_t*)v_cache, BS, rotate_k_inplace);
   return (int)hipGetLastError();
 }
 

@@ -163,7 +163,8 @@ class LlamaModel:
                 h = ops.rms_norm(x, L["ln1"], cfg.rms_eps, residual=residual)
             qkv = ops.linear(h, L["wqkv"])
             kc, vc = k_caches[li], v_caches[li]
-            ops.rope_and_cache(qkv, inp.positions, self.cos_sin, Hq, Hkv, D, inp.slots, kc, vc)
+            ops.rope_and_cache(qkv, inp.positions, self.cos_sin, Hq, Hkv, D, inp.slots, kc, vc,
+                               tile_from=nd)
             if nd > 0:
                 ops.paged_decode_attention(qkv[:nd], kc, vc, inp.block_tables,
                                            inp.context_lens, self.scale, attn[:nd], decode_ws,

@@ -103,9 +103,12 @@ def layer_norm(x, w, b, eps, residual=None):
 def rope_and_cache(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Tensor,
                    Hq: int, Hkv: int, D: int, slots: torch.Tensor | None,
                    k_cache: torch.Tensor | None, v_cache: torch.Tensor | None,
-                   rotate_k_inplace: bool = False) -> None:
+                   rotate_k_inplace: bool = False, tile_from: int | None = None) -> None:
     """In-place rotary on q (and k) heads of the fused QKV rows; k and v are
-    scattered into the paged cache at ``slots`` (-1 = skip)."""
+    scattered into the paged cache at ``slots`` (-1 = skip).  Rows from
+    ``tile_from`` on (prefill chunks: consecutive slots) use the 32-token
+    tiled kernel with coalesced transposed-V page writes; rows before it
+    (decode: one token per page) the per-token kernel.  Default: all tiled."""
     if not qkv.is_cuda:
         ref.rope_cache(qkv, positions, cos_sin, Hq, Hkv, D, slots, k_cache, v_cache,
                        rotate_k_inplace)
@@ -123,7 +126,8 @@ def rope_and_cache(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Te
         BS = k_cache.shape[2]
     native().rope_cache(_ptr(qkv), qkv.stride(0), _ptr(positions), _ptr(cos_sin), T, Hq, Hkv, D,
                         _ptr(slots), _ptr(k_cache), _ptr(v_cache), BS,
-                        int(rotate_k_inplace), _stream())
+                        int(rotate_k_inplace), 0 if tile_from is None else int(tile_from),
+                        _stream())
 
 
 def kv_write(k, v, slots, k_cache, v_cache):
@@ -315,8 +319,13 @@ def gemm_nt(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, 
     _chk(N % 128 == 0 and K % 64 == 0, "gemm_nt needs N % 128 == 0 and K % 64 == 0")
     if out is None:
         out = torch.empty((M, N), dtype=a.dtype, device=a.device)
+    # the epilogue stores / loads 4 bf16 (8 B) per lane
+    _chk(out.stride(1) == 1 and out.stride(0) % 4 == 0 and out.data_ptr() % 8 == 0,
+         "gemm_nt output rows must be 8-B aligned")
+    _chk(bias is None or bias.data_ptr() % 8 == 0, "gemm_nt bias must be 8-B aligned")
     if residual is not None:
-        _chk(residual.shape == (M, N) and residual.stride(0) == out.stride(0), "residual")
+        _chk(residual.shape == (M, N) and residual.stride(0) == out.stride(0)
+             and residual.data_ptr() % 8 == 0, "residual")
     native().gemm_nt(_ptr(out), _ptr(a), _ptr(w), _ptr(bias), _ptr(residual), M, N, K,
                      a.stride(0), w.stride(0), out.stride(0), act, _stream())
     return out

@@ -55,17 +55,23 @@ def _cache(NB, Hkv, D, BS=32):
 
 
 @pytest.mark.parametrize("Hq,Hkv,D", [(32, 8, 128), (8, 1, 128), (12, 12, 64), (4, 2, 128)])
-def test_rope_and_cache(Hq, Hkv, D):
-    T, NB = 37, 8
+@pytest.mark.parametrize("layout", ["scattered", "chunks"])
+@pytest.mark.parametrize("tile_from", [None, 5, 1000])
+def test_rope_and_cache(Hq, Hkv, D, layout, tile_from):
+    T, NB = 77, 8
     qkv = _bf(T, (Hq + 2 * Hkv) * D)
     pos = torch.randint(0, 4000, (T,), device=DEV, dtype=torch.int32)
     cs = ref.rope_cos_sin(4096, D, 500000.0, DEV)
-    slots = torch.randperm(NB * 32, device=DEV)[:T].to(torch.int32)
+    if layout == "scattered":
+        slots = torch.randperm(NB * 32, device=DEV)[:T].to(torch.int32)
+    else:   # prefill-like runs: consecutive slots starting mid-page, page jumps
+        slots = torch.cat([torch.arange(45, 45 + 40), torch.arange(160, 160 + 37)]).to(
+            torch.int32).to(DEV)
     slots[3] = -1
     kc, vc = torch.zeros(NB, Hkv, 32, D, device=DEV, dtype=torch.bfloat16), \
         torch.zeros(NB, Hkv, D, 32, device=DEV, dtype=torch.bfloat16)
     qkv0, kc0, vc0 = qkv.cpu(), kc.cpu(), vc.cpu()
-    ops.rope_and_cache(qkv, pos, cs, Hq, Hkv, D, slots, kc, vc)
+    ops.rope_and_cache(qkv, pos, cs, Hq, Hkv, D, slots, kc, vc, tile_from=tile_from)
     ref.rope_cache(qkv0, pos.cpu(), cs.cpu(), Hq, Hkv, D, slots.cpu(), kc0, vc0, False)
     torch.testing.assert_close(qkv[:, :Hq * D].float().cpu(), qkv0[:, :Hq * D].float(),
                                atol=2e-2, rtol=2e-2)
