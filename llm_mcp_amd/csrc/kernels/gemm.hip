@@ -131,6 +131,42 @@ __global__ void __launch_bounds__(256, 2) gemm_nt_kernel(
   }
   // epilogue: acc[i][j][r] = C[row][col + r] with
   //   row = m0 + wr*64 + 16i + fr, col = n0 + wc*64 + 16j + 4fg
+  if (act == 3) {
+    // fused SwiGLU (K8): W rows are interleaved per 128-column tile as
+    // [64 gate | 64 up] of the same 64 channels (host: ops.interleave_gate_up),
+    // so the wc = 1 waves hand their up values to the wc = 0 waves through
+    // the (now idle) LDS and C has N/2 columns: silu(gate) * up.
+    float* up = reinterpret_cast<float*>(smem);   // [128 rows][64 + 4] fp32
+    constexpr int ULD = 68;
+    if (wc == 1) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          *reinterpret_cast<f32x4_t*>(up + (wr * 64 + 16 * i + fr) * ULD + 16 * j + 4 * fg) =
+              acc[i][j];
+    }
+    __syncthreads();
+    if (wc == 1) return;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = m0 + wr * 64 + 16 * i + fr;
+      if (row >= M) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const f32x4_t u = *reinterpret_cast<const f32x4_t*>(
+            up + (wr * 64 + 16 * i + fr) * ULD + 16 * j + 4 * fg);
+        bf16x4_t o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float g = acc[i][j][r];
+          o[r] = (short)f2bf(g / (1.f + __expf(-g)) * u[r]);
+        }
+        *reinterpret_cast<bf16x4_t*>(C + (long)row * ldc + (n0 >> 1) + 16 * j + 4 * fg) = o;
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int row = m0 + wr * 64 + 16 * i + fr;

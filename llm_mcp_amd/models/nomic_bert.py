@@ -40,6 +40,10 @@ class NomicBertModel:
         self.scale = 1.0 / math.sqrt(self.D)
         self.cos_sin = ref.rope_cos_sin(cfg.max_position, self.D, cfg.rope_theta, self.device)
         self.w = weights or self._random_weights(seed)
+        # gate/up rows interleaved per 64 channels for the fused SwiGLU epilogue
+        for L in self.w["layers"]:
+            if "w_gu_il" not in L and ops.gemm_nt_supported(*L["w_gate_up"].shape):
+                L["w_gu_il"] = ops.interleave_gate_up(L["w_gate_up"])
 
     def _random_weights(self, seed):
         cfg, dev, dt = self.cfg, self.device, self.dtype
@@ -107,7 +111,10 @@ class NomicBertModel:
                                         causal=False, Hq=H)
             o = self._linear(attn, L["wo"])
             h = ops.layer_norm(o, L["ln1_w"], L["ln1_b"], cfg.ln_eps, residual=x)
-            g = ops.silu_mul(self._linear(h, L["w_gate_up"]))
+            if "w_gu_il" in L:   # K8 fused into the GEMM epilogue
+                g = ops.gemm_nt(h, L["w_gu_il"], act=ops.ACT_SWIGLU)
+            else:
+                g = ops.silu_mul(self._linear(h, L["w_gate_up"]))
             m = self._linear(g, L["w_down"])
             x = ops.layer_norm(m, L["ln2_w"], L["ln2_b"], cfg.ln_eps, residual=h)
         return ops.mean_pool_l2(x, cu, dims or cfg.embed_dim, normalize)

@@ -303,11 +303,35 @@ def mean_pool_l2(h: torch.Tensor, cu: torch.Tensor, dims: int | None = None,
 ACT_NONE, ACT_GELU, ACT_SILU = 0, 1, 2
 
 
+ACT_SWIGLU = 3
+
+
+def interleave_gate_up(w: torch.Tensor) -> torch.Tensor:
+    """[gate(I); up(I)] rows -> per 64 channels [gate 64 | up 64], the layout
+    of gemm_nt's fused SwiGLU epilogue (act=3)."""
+    I2, d = w.shape
+    I = I2 // 2
+    _chk(I % 64 == 0, "intermediate size must be a multiple of 64")
+    return w.view(2, I // 64, 64, d).transpose(0, 1).reshape(I2, d).contiguous()
+
+
 def gemm_nt(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, act: int = 0,
             residual: torch.Tensor | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
-    """act(a @ w^T + bias) (+ residual) on the hand-written MFMA GEMM."""
+    """act(a @ w^T + bias) (+ residual) on the hand-written MFMA GEMM.
+    act=3 (ACT_SWIGLU): ``w`` from ``interleave_gate_up``; returns
+    silu(gate) * up with N/2 columns."""
     M, K = a.shape
     N = w.shape[0]
+    if act == ACT_SWIGLU:
+        _chk(bias is None and residual is None, "SwiGLU epilogue takes no bias/residual")
+        if not a.is_cuda:
+            I = N // 2
+            y = (a.float() @ w.float().t()).view(M, I // 64, 2, 64)
+            y = (torch.nn.functional.silu(y[:, :, 0]) * y[:, :, 1]).reshape(M, I).to(a.dtype)
+            if out is not None:
+                out.copy_(y)
+                return out
+            return y
     if not a.is_cuda:
         y = ref.gemm_nt(a, w, bias, act, residual)
         if out is not None:
@@ -318,7 +342,8 @@ def gemm_nt(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, 
     _chk(w.shape[1] == K and a.stride(1) == 1 and w.stride(1) == 1, "gemm_nt shapes")
     _chk(N % 128 == 0 and K % 64 == 0, "gemm_nt needs N % 128 == 0 and K % 64 == 0")
     if out is None:
-        out = torch.empty((M, N), dtype=a.dtype, device=a.device)
+        out = torch.empty((M, N // 2 if act == ACT_SWIGLU else N), dtype=a.dtype,
+                          device=a.device)
     # the epilogue stores / loads 4 bf16 (8 B) per lane
     _chk(out.stride(1) == 1 and out.stride(0) % 4 == 0 and out.data_ptr() % 8 == 0,
          "gemm_nt output rows must be 8-B aligned")

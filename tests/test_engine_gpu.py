@@ -37,3 +37,29 @@ def test_llama3_8b_decode_step_runs():
     assert all(0 <= t < 128256 for o in outs for t in o)
     assert e.stats["graph_steps"] > 0
     torch.cuda.synchronize()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("preset", ["tiny-nomic", "nomic-2layer"])
+def test_nomic_bert_gpu_matches_cpu_reference(preset):
+    """Encoder on the HIP kernels (gemm_nt incl. the fused SwiGLU epilogue,
+    tiled rope/cache, bidirectional paged prefill, LayerNorm, mean-pool) vs
+    the same weights on the fp32-reference CPU path."""
+    import dataclasses
+
+    from llm_mcp_amd.models import config as mc
+    from llm_mcp_amd.models.nomic_bert import NomicBertModel
+    cfg = mc.resolve("tiny-nomic") if preset == "tiny-nomic" else \
+        dataclasses.replace(mc.resolve("nomic-embed-text"), num_layers=2)
+    g = NomicBertModel(cfg, "cuda", seed=3)
+    wc = {k: (v.cpu() if hasattr(v, "cpu") else [{kk: vv.cpu() for kk, vv in L.items()}
+                                                  for L in v]) for k, v in g.w.items()}
+    c = NomicBertModel(cfg, "cpu", weights=wc)
+    lens = [30, 1, 39, 70]
+    ids = torch.randint(0, 500, (sum(lens),), dtype=torch.int32)
+    cu = torch.tensor([0] + list(torch.cumsum(torch.tensor(lens), 0)), dtype=torch.int32)
+    a = g.forward(ids.cuda(), cu.cuda(), lens).cpu()
+    b = c.forward(ids, cu, lens)
+    cos = torch.nn.functional.cosine_similarity(a, b, dim=-1)
+    assert float(cos.min()) > 0.999, cos
+    assert float((a - b).abs().max()) < 2e-2

@@ -319,3 +319,15 @@ def test_gemm_splitk_in_graph_strided_input():
     g.replay()
     torch.cuda.synchronize()
     torch.testing.assert_close(out.float(), x.float() @ w.float().t(), atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M", [5, 128, 333])
+def test_gemm_nt_fused_swiglu(M):
+    K, I = 768, 3072
+    a = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(2 * I, K, device=DEV) * K ** -0.5).to(torch.bfloat16)
+    out = ops.gemm_nt(a, ops.interleave_gate_up(w), act=ops.ACT_SWIGLU)
+    y = a.float() @ w.float().t()
+    expect = torch.nn.functional.silu(y[:, :I]) * y[:, I:]
+    torch.testing.assert_close(out.float(), expect, atol=2e-2, rtol=2e-2)
