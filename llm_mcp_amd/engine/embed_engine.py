@@ -15,6 +15,7 @@ import threading
 import time
 from dataclasses import dataclass, field
 
+import numpy as np
 import torch
 
 from ..models.config import NomicBertConfig
@@ -78,8 +79,9 @@ class EmbeddingEngine:
         if self.device.type == "cuda":
             torch.cuda.set_device(self.device)
         pending: list[EmbedRequest] = []
+        inflight = None
         while not self._stop.is_set():
-            if not pending:
+            if not pending and inflight is None:
                 item = self._q.get()
                 if item is None:
                     break
@@ -100,14 +102,35 @@ class EmbeddingEngine:
                     break
                 batch.append(pending.pop(0))
                 ntok += n
-            try:
-                outs = self._run(batch)
-                for r, o in zip(batch, outs):
-                    self._deliver(r, o, None)
-            except Exception as e:
-                log.exception("embedding batch failed")
-                for r in batch:
-                    self._deliver(r, None, str(e))
+            # two batches in flight: batch n+1's host prep and launch overlap
+            # batch n's kernels; batch n is finished (synced) afterwards
+            launched = None
+            if batch:
+                try:
+                    launched = self._launch(batch)
+                except Exception as e:
+                    log.exception("embedding batch failed")
+                    for r in batch:
+                        self._deliver(r, None, str(e))
+            if inflight is not None:
+                self._complete(inflight)
+            inflight = launched
+            if inflight is not None and not pending and self._q.empty():
+                self._complete(inflight)
+                inflight = None
+        if inflight is not None:
+            self._complete(inflight)
+
+    def _complete(self, launched):
+        batch = launched[0]
+        try:
+            outs = self._finish(launched)
+            for r, o in zip(batch, outs):
+                self._deliver(r, o, None)
+        except Exception as e:
+            log.exception("embedding batch failed")
+            for r in batch:
+                self._deliver(r, None, str(e))
 
     @staticmethod
     def _deliver(r: EmbedRequest, out, err):
@@ -123,24 +146,39 @@ class EmbeddingEngine:
                     f.set_exception(RuntimeError(err))
             r.loop.call_soon_threadsafe(_set)
 
-    @torch.no_grad()
     def _run(self, batch: list[EmbedRequest]) -> list[list[list[float]]]:
+        return self._finish(self._launch(batch))
+
+    @torch.no_grad()
+    def _launch(self, batch: list[EmbedRequest]):
+        """Queue one varlen encoder forward; returns the pending result."""
         t0 = time.perf_counter()
         seqs = [s for r in batch for s in r.seqs]
         lens = [len(s) for s in seqs]
-        cu = [0]
-        for n in lens:
-            cu.append(cu[-1] + n)
-        flat = [t for s in seqs for t in s]
-        ids = torch.tensor(flat, dtype=torch.int32).to(self.device, non_blocking=True)
-        cu_t = torch.tensor(cu, dtype=torch.int32).to(self.device, non_blocking=True)
+        flat = np.concatenate([np.asarray(s, dtype=np.int32) for s in seqs])
+        cu = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+        ids = torch.from_numpy(flat).to(self.device, non_blocking=True)
+        cu_t = torch.from_numpy(cu).to(self.device, non_blocking=True)
         dims = {r.dims or self.cfg.embed_dim for r in batch}
         fused = len(dims) == 1
         if fused:
             # pooling, Matryoshka truncation and L2 norm fused in one kernel (K9)
-            full = self.model.forward(ids, cu_t, lens, dims=dims.pop(), normalize=True).cpu()
+            dev_out = self.model.forward(ids, cu_t, lens, dims=dims.pop(), normalize=True)
         else:
-            full = self.model.forward(ids, cu_t, lens, dims=None, normalize=False).cpu()
+            dev_out = self.model.forward(ids, cu_t, lens, dims=None, normalize=False)
+        if self.device.type == "cuda":
+            host = torch.empty(dev_out.shape, dtype=dev_out.dtype, pin_memory=True)
+            host.copy_(dev_out, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+        else:
+            host, ev = dev_out, None
+        return batch, host, ev, fused, len(flat), t0
+
+    def _finish(self, launched) -> list[list[list[float]]]:
+        batch, full, ev, fused, ntok, t0 = launched
+        if ev is not None:
+            ev.synchronize()
         outs, k = [], 0
         for r in batch:
             e = full[k:k + len(r.seqs)]
@@ -150,7 +188,7 @@ class EmbeddingEngine:
                 e = e / e.norm(dim=-1, keepdim=True).clamp_min(1e-12)
             outs.append(e.float().tolist())
         self.stats["batches"] += 1
-        self.stats["sequences"] += len(seqs)
-        self.stats["tokens"] += len(flat)
+        self.stats["sequences"] += sum(len(r.seqs) for r in batch)
+        self.stats["tokens"] += ntok
         self.stats["time_s"] += time.perf_counter() - t0
         return outs

@@ -21,6 +21,8 @@ from __future__ import annotations
 
 import math
 
+import numpy as np
+
 import torch
 
 from .. import ops
@@ -78,24 +80,30 @@ class NomicBertModel:
         H, D, d = self.H, self.D, cfg.hidden_size
         T, S = ids.numel(), len(lens)
         dev = self.device
-        # per-sequence page-aligned slots in a scratch paged K/V cache
-        pages = [max(1, math.ceil(n / PAGE)) for n in lens]
-        page_off = [0]
-        for p in pages:
-            page_off.append(page_off[-1] + p)
-        NB = page_off[-1]
-        slots, pos, tiles, bt = [], [], [], torch.zeros((S, max(pages)), dtype=torch.int32)
+        # per-sequence page-aligned slots in a scratch paged K/V cache, built
+        # with array ops (no per-token Python work on the host critical path)
+        ln = np.asarray(lens, dtype=np.int64)
+        pages = np.maximum(1, -(-ln // PAGE))
+        page_off = np.concatenate([[0], np.cumsum(pages)])
+        NB = int(page_off[-1])
+        cu_h = np.concatenate([[0], np.cumsum(ln)])
+        within = np.arange(T, dtype=np.int64) - np.repeat(cu_h[:-1], ln)
+        slots = np.repeat(page_off[:-1] * PAGE, ln) + within
         qpt = ops.prefill_q_per_tile(H, H)
-        for s, n in enumerate(lens):
-            base = page_off[s] * PAGE
-            slots.extend(range(base, base + n))
-            pos.extend(range(n))
-            bt[s, :pages[s]] = torch.arange(page_off[s], page_off[s + 1], dtype=torch.int32)
-            for q0 in range(0, n, qpt):
-                tiles += [s, q0]
-        meta = torch.tensor(slots + pos + tiles, dtype=torch.int32).to(dev, non_blocking=True)
+        nt = -(-ln // qpt)
+        tile_seq = np.repeat(np.arange(S), nt)
+        tile_q0 = (np.arange(int(nt.sum())) - np.repeat(np.concatenate([[0], np.cumsum(nt)])[:-1],
+                                                        nt)) * qpt
+        tiles = np.stack([tile_seq, tile_q0], 1).reshape(-1)
+        maxp = int(pages.max())
+        bt_np = np.zeros((S, maxp), dtype=np.int32)
+        col = np.arange(maxp)
+        mask = col[None, :] < pages[:, None]
+        bt_np[mask] = np.arange(NB, dtype=np.int32)
+        meta = torch.from_numpy(np.concatenate([slots, within, tiles]).astype(np.int32))
+        meta = meta.pin_memory().to(dev, non_blocking=True) if dev.type == "cuda" else meta
         slots_t, pos_t, tiles_t = meta[:T], meta[T:2 * T], meta[2 * T:]
-        bt = bt.to(dev, non_blocking=True)
+        bt = torch.from_numpy(bt_np).to(dev, non_blocking=True)
         ctx = torch.tensor(lens, dtype=torch.int32).to(dev, non_blocking=True)
         kc = torch.zeros((NB, H, PAGE, D), dtype=self.dtype, device=dev)
         vc = torch.zeros((NB, H, D, PAGE), dtype=self.dtype, device=dev)
