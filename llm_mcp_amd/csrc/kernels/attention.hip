@@ -299,7 +299,9 @@ __global__ void __launch_bounds__(256, 2) paged_prefill_kernel(
 
   const int tile = blockIdx.x, kvh = blockIdx.y;
   const int seq = tiles[2 * tile], q_start = tiles[2 * tile + 1];
-  const int G = Hq / Hkv, QG = 16 / G;            // queries per column group
+  // queries per 16-lane column group; with G not dividing 16 (e.g. Qwen2.5's
+  // 7) the last 16 - QG*G lanes of a group are idle
+  const int G = Hq / Hkv, QG = 16 / G;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
   const int qbeg = cu_q[seq], qlen = cu_q[seq + 1] - qbeg;
   const int ctx = context_lens[seq];
@@ -317,7 +319,7 @@ __global__ void __launch_bounds__(256, 2) paged_prefill_kernel(
 #pragma unroll
   for (int n = 0; n < PF_NG; ++n) {
     qi[n] = q_start + (wave * PF_NG + n) * QG + c / G;
-    valid[n] = qi[n] < qlen;
+    valid[n] = c < QG * G && qi[n] < qlen;
     lim[n] = valid[n] ? (causal ? (ctx - qlen + qi[n]) : (ctx - 1)) : -1;
     const int head = kvh * G + (c % G);
     const bf16_t* qrow = q + (long)(qbeg + (valid[n] ? qi[n] : 0)) * q_stride + (long)head * HD;
@@ -460,7 +462,7 @@ int paged_prefill(const void* q, long q_stride, const void* k_cache, const void*
                   int causal, hipStream_t stream) {
   if (num_tiles <= 0) return 0;
   if ((D != 128 && D != 64) || block_size != BS) return -1;
-  if (Hq % Hkv != 0 || 16 % (Hq / Hkv) != 0) return -2;
+  if (Hq % Hkv != 0 || Hq / Hkv > 16) return -2;
 #define LMX_PRE(HDV)                                                                          \
   paged_prefill_kernel<HDV><<<dim3(num_tiles, Hkv), dim3(256), 2 * 4 * BS * HDV * 2,         \
                               stream>>>(                                                      \

@@ -31,11 +31,14 @@ class LlamaConfig:
     eos_token_ids: tuple = (128001, 128009)
     family: str = "llama"
     kind: str = "chat"
+    qkv_bias: bool = False          # Qwen2 / Qwen2.5: biased q/k/v projections
 
     @property
     def params(self) -> int:
         d, I, L, V = self.hidden_size, self.intermediate_size, self.num_layers, self.vocab_size
         qkv = d * (self.num_heads + 2 * self.num_kv_heads) * self.head_dim
+        if self.qkv_bias:
+            qkv += (self.num_heads + 2 * self.num_kv_heads) * self.head_dim
         o = self.num_heads * self.head_dim * d
         mlp = 3 * d * I
         emb = V * d * (1 if self.tie_embeddings else 2)
@@ -110,6 +113,22 @@ PRESETS: dict[str, object] = {
                               intermediate_size=512, num_layers=2, num_heads=4, num_kv_heads=2,
                               head_dim=128, max_position=2048, bos_token_id=506,
                               eos_token_ids=(510,)),
+    # Qwen2.5 (biased QKV, GQA group 7 / 7 -- not a divisor of 16)
+    "qwen2.5-7b": LlamaConfig(name="qwen2.5-7b", vocab_size=152064, hidden_size=3584,
+                              intermediate_size=18944, num_layers=28, num_heads=28,
+                              num_kv_heads=4, head_dim=128, rope_theta=1000000.0, rms_eps=1e-6,
+                              max_position=32768, bos_token_id=151643,
+                              eos_token_ids=(151643, 151645), family="qwen2", qkv_bias=True),
+    "qwen2.5-0.5b": LlamaConfig(name="qwen2.5-0.5b", vocab_size=151936, hidden_size=896,
+                                intermediate_size=4864, num_layers=24, num_heads=14,
+                                num_kv_heads=2, head_dim=64, rope_theta=1000000.0, rms_eps=1e-6,
+                                max_position=32768, tie_embeddings=True, bos_token_id=151643,
+                                eos_token_ids=(151643, 151645), family="qwen2", qkv_bias=True),
+    "tiny-qwen": LlamaConfig(name="tiny-qwen", vocab_size=512, hidden_size=448,
+                             intermediate_size=512, num_layers=2, num_heads=7, num_kv_heads=1,
+                             head_dim=64, rope_theta=1000000.0, rms_eps=1e-6, max_position=2048,
+                             bos_token_id=506, eos_token_ids=(510,), family="qwen2",
+                             qkv_bias=True),
     "nomic-embed-text": NomicBertConfig(),
     "tiny-nomic": NomicBertConfig(name="tiny-nomic", vocab_size=512, hidden_size=256,
                                   intermediate_size=512, num_layers=2, num_heads=2, head_dim=128,
@@ -122,6 +141,8 @@ ALIASES = {
     "meta-llama-3-8b": "llama-3-8b", "llama3:70b": "llama-3-70b",
     "llama3.2:1b": "llama-3.2-1b", "nomic-embed-text:latest": "nomic-embed-text",
     "nomic-embed-text-v1.5": "nomic-embed-text",
+    "qwen2.5:7b": "qwen2.5-7b", "qwen2.5:0.5b": "qwen2.5-0.5b",
+    "qwen2.5-7b-instruct": "qwen2.5-7b",
 }
 
 
@@ -136,7 +157,8 @@ def from_hf_config(path: str | Path):
     """Build a config from a HF config.json (local file; no network)."""
     cfg = json.loads(Path(path).read_text())
     arch = (cfg.get("architectures") or [""])[0]
-    if "Llama" in arch:
+    if "Llama" in arch or "Qwen2" in arch or "Mistral" in arch:
+        qwen = "Qwen2" in arch
         return LlamaConfig(
             name=cfg.get("_name_or_path", "llama"), vocab_size=cfg["vocab_size"],
             hidden_size=cfg["hidden_size"], intermediate_size=cfg["intermediate_size"],
@@ -149,7 +171,9 @@ def from_hf_config(path: str | Path):
             tie_embeddings=cfg.get("tie_word_embeddings", False),
             bos_token_id=cfg.get("bos_token_id", 128000),
             eos_token_ids=tuple(cfg["eos_token_id"]) if isinstance(cfg.get("eos_token_id"), list)
-            else (cfg.get("eos_token_id", 128001),))
+            else (cfg.get("eos_token_id", 128001),),
+            family="qwen2" if qwen else ("mistral" if "Mistral" in arch else "llama"),
+            qkv_bias=qwen)
     if "NomicBert" in arch or cfg.get("model_type") == "nomic_bert":
         return NomicBertConfig(
             vocab_size=cfg["vocab_size"], hidden_size=cfg["n_embd"],

@@ -121,7 +121,11 @@ class LlamaModel:
         layers = []
         qkv_rows = (self.Hq + 2 * self.Hkv) * self.D
         for _ in range(cfg.num_layers):
-            layers.append({
+            if cfg.qkv_bias:
+                layers.append({"bqkv": rnd(qkv_rows, std=0.02)})
+            else:
+                layers.append({})
+            layers[-1].update({
                 "ln1": torch.ones(d, dtype=dt, device=dev),
                 "ln2": torch.ones(d, dtype=dt, device=dev),
                 "wqkv": rnd(qkv_rows, d),
@@ -162,6 +166,8 @@ class LlamaModel:
             else:
                 h = ops.rms_norm(x, L["ln1"], cfg.rms_eps, residual=residual)
             qkv = ops.linear(h, L["wqkv"])
+            if "bqkv" in L:          # Qwen2: biased q/k/v
+                qkv += L["bqkv"]
             kc, vc = k_caches[li], v_caches[li]
             ops.rope_and_cache(qkv, inp.positions, self.cos_sin, Hq, Hkv, D, inp.slots, kc, vc,
                                tile_from=nd)

@@ -72,7 +72,14 @@ def shard_llama(full: dict, cfg: LlamaConfig, rank: int, size: int) -> dict:
         k = wqkv[qn + r["kv"][0]:qn + r["kv"][1]]
         v = wqkv[qn + kvn + r["kv"][0]:qn + kvn + r["kv"][1]]
         gu = L["w_gate_up"]
+        extra = {}
+        if "bqkv" in L:
+            b = L["bqkv"]
+            extra["bqkv"] = torch.cat([
+                b[r["q"][0]:r["q"][1]], b[qn + r["kv"][0]:qn + r["kv"][1]],
+                b[qn + kvn + r["kv"][0]:qn + kvn + r["kv"][1]]]).contiguous()
         layers.append({
+            **extra,
             "ln1": L["ln1"], "ln2": L["ln2"],
             "wqkv": torch.cat([q, k, v]).contiguous(),
             "wo": L["wo"][:, r["q"][0]:r["q"][1]].contiguous(),
@@ -150,7 +157,13 @@ def load_llama_weights(path: str, cfg: LlamaConfig, device, rank: int = 0, size:
         v = rd.rows(p + "self_attn.v_proj.weight", *r["kv"])
         g = rd.rows(p + "mlp.gate_proj.weight", *r["i"])
         u = rd.rows(p + "mlp.up_proj.weight", *r["i"])
+        extra = {}
+        if cfg.qkv_bias:
+            extra["bqkv"] = put(torch.cat([rd.rows(p + "self_attn.q_proj.bias", *r["q"]),
+                                           rd.rows(p + "self_attn.k_proj.bias", *r["kv"]),
+                                           rd.rows(p + "self_attn.v_proj.bias", *r["kv"])]))
         layers.append({
+            **extra,
             "ln1": put(rd.rows(p + "input_layernorm.weight")),
             "ln2": put(rd.rows(p + "post_attention_layernorm.weight")),
             "wqkv": put(torch.cat([q, k, v])),
@@ -187,9 +200,14 @@ def save_hf_llama(full: dict, cfg: LlamaConfig, path: str) -> None:
         out[p + "mlp.gate_proj.weight"] = L["w_gate_up"][:I]
         out[p + "mlp.up_proj.weight"] = L["w_gate_up"][I:]
         out[p + "mlp.down_proj.weight"] = L["w_down"]
+        if "bqkv" in L:
+            out[p + "self_attn.q_proj.bias"] = L["bqkv"][:qn]
+            out[p + "self_attn.k_proj.bias"] = L["bqkv"][qn:qn + kvn]
+            out[p + "self_attn.v_proj.bias"] = L["bqkv"][qn + kvn:]
     save_file({k: v.detach().to("cpu").contiguous() for k, v in out.items()},
               os.path.join(path, "model.safetensors"))
-    hf = {"architectures": ["LlamaForCausalLM"], "vocab_size": cfg.vocab_size,
+    arch = "Qwen2ForCausalLM" if cfg.qkv_bias else "LlamaForCausalLM"
+    hf = {"architectures": [arch], "vocab_size": cfg.vocab_size,
           "hidden_size": cfg.hidden_size, "intermediate_size": cfg.intermediate_size,
           "num_hidden_layers": cfg.num_layers, "num_attention_heads": cfg.num_heads,
           "num_key_value_heads": cfg.num_kv_heads, "head_dim": cfg.head_dim,

@@ -17,6 +17,8 @@ def dense_logits(model, tokens: list[int]) -> torch.Tensor:
     for L in w["layers"]:
         h = ref.rms_norm(x, L["ln1"].float(), cfg.rms_eps)
         qkv = h @ L["wqkv"].float().t()
+        if "bqkv" in L:
+            qkv = qkv + L["bqkv"].float()
         T = qkv.shape[0]
         q = qkv[:, :Hq * D].view(T, Hq, D)
         k = qkv[:, Hq * D:(Hq + Hkv) * D].view(T, Hkv, D)

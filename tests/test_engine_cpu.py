@@ -66,3 +66,15 @@ def test_logits_close_to_dense():
     logits = e.model.forward(inp, e.k_caches, e.v_caches, None)
     ref = dense_logits(e.model, p)
     assert torch.allclose(logits[0].float(), ref, atol=5e-2, rtol=5e-2)
+
+
+def test_qwen2_biased_qkv_group7_matches_dense():
+    """Qwen2-style model: biased q/k/v and a GQA group of 7 (not a divisor of
+    16) through the engine vs the dense fp32 reference."""
+    e = _engine(model="tiny-qwen")
+    assert e.cfg.qkv_bias and e.Hq // e.Hkv == 7
+    prompts = [list(range(10, 50)), [7] * 33, [3]]
+    outs = e.generate(prompts, SamplingParams(temperature=0, max_tokens=5, ignore_eos=True))
+    for p, o in zip(prompts, outs):
+        assert len(o) == 5
+        assert_greedy_consistent(e.model, p, o)

@@ -91,7 +91,8 @@ def _random_tables(B, ctxs, NB, BS=32):
     return bt.to(DEV)
 
 
-@pytest.mark.parametrize("Hq,Hkv,D", [(32, 8, 128), (8, 1, 128), (64, 8, 128), (16, 16, 64)])
+@pytest.mark.parametrize("Hq,Hkv,D", [(32, 8, 128), (8, 1, 128), (64, 8, 128), (16, 16, 64),
+                                     (28, 4, 128), (14, 2, 64)])
 @pytest.mark.parametrize("ctxs", [[1, 17, 32, 33, 500], [1024, 2047, 3000], [5000]])
 def test_paged_decode(Hq, Hkv, D, ctxs):
     B = len(ctxs)
@@ -108,7 +109,8 @@ def test_paged_decode(Hq, Hkv, D, ctxs):
     torch.testing.assert_close(out.float().view(B, Hq, D), expect.float(), atol=2e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("Hq,Hkv,D", [(32, 8, 128), (8, 1, 128), (12, 12, 64), (4, 4, 128)])
+@pytest.mark.parametrize("Hq,Hkv,D", [(32, 8, 128), (8, 1, 128), (12, 12, 64), (4, 4, 128),
+                                     (28, 4, 128), (7, 1, 64)])
 def test_paged_prefill_varlen_with_prefix(Hq, Hkv, D):
     qlens = [1, 70, 33, 256]
     prefix = [0, 40, 0, 100]

@@ -131,3 +131,13 @@ def test_tp2_generation_matches_single_process(full_model):
     # same seeds + same logits (up to bf16 reduction order) -> same samples
     agree = sum(a == b for x, y in zip(sampled, ref_sampled) for a, b in zip(x, y))
     assert agree >= 8, (sampled, ref_sampled)
+
+
+def test_qwen_loader_roundtrip_with_bias(tmp_path):
+    cfg = mc.resolve("tiny-qwen")
+    m = LlamaModel(cfg, "cpu", seed=5)
+    save_hf_llama(m.w, cfg, str(tmp_path))
+    assert mc.from_hf_config(str(tmp_path / "config.json")).qkv_bias
+    a = load_llama_weights(str(tmp_path), cfg, "cpu")
+    for la, lb in zip(a["layers"], m.w["layers"]):
+        assert torch.equal(la["bqkv"], lb["bqkv"]) and torch.equal(la["wqkv"], lb["wqkv"])
