@@ -122,6 +122,8 @@ class CoreState:
 
     def _maintenance(self):
         from ..planner.catalog import RetentionPlanner
+        if not hasattr(self, "_comm_seen"):
+            self._comm_seen: set[str] = set()
         if not hasattr(self, "_retention"):
             self._retention = RetentionPlanner(
                 self.store, float(os.environ.get("LMX_JOB_RETENTION_DAYS", "7")))
@@ -130,6 +132,13 @@ class CoreState:
             info = m.info()
             if "kv_usage" in info:
                 self.metrics.kv_usage.labels(m.device_id).set(info["kv_usage"])
+            comm = info.get("tp_comm") or {}
+            if comm and m.device_id not in self._comm_seen:
+                # the TP group's start-up all-reduce probe (parallel/tp_worker.py)
+                self._comm_seen.add(m.device_id)
+                for path, by_size in comm.items():
+                    for us in by_size.values():
+                        self.metrics.allreduce.labels(path).observe(us / 1e6)
 
     async def start_background(self, app=None):
         disc = env_int("DISCOVERY_INTERVAL", 0)

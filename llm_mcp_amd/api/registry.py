@@ -44,6 +44,9 @@ class LocalModel:
         if sched is not None:
             d.update(kv_usage=round(sched.kv_usage, 4), running=sched.num_running,
                      waiting=sched.num_waiting)
+        comm = getattr(eng, "tp_comm", None) or self.tags.get("tp_comm")
+        if comm:
+            d["tp_comm"] = comm       # TP all-reduce probe, us by message size
         return d
 
 

@@ -55,7 +55,8 @@ async def attach_engines(state, specs: list[dict]):
             s["model"], info.get("kind", "chat"), s.get("device") or info.get("device_id", "gpu0"),
             c, for_model(cfg, s.get("tokenizer")), cfg,
             max_model_len=int(info.get("max_model_len", 8192)),
-            capacity=int(info.get("capacity", 256))))
+            capacity=int(info.get("capacity", 256)),
+            tags={"tp_comm": info.get("tp_comm") or {}}))
         log.info("engine %s on %s connected", s["model"], s["path"])
 
     await asyncio.gather(*[one(s, c) for s, c in clients])

@@ -1,0 +1,220 @@
+// X1/X2: tensor-parallel all-reduce over peer memory (xGMI), bf16 sum with
+// fp32 accumulation, for the decode-sized messages of a TP group.
+//
+// Why not only RCCL: a ring moves 2(W-1)/W * S bytes through ONE xGMI link per
+// direction and pays 2(W-1) latency hops; decode all-reduces (T x d x 2 B =
+// 16 KB ... 4 MB at d = 8192) are latency-bound.  MI355X peers are fully
+// connected (7 links per GPU), so here every rank reads its peers' buffers
+// directly, all links at once:
+//   * one-shot (small S): every rank reads all W inputs and sums;
+//     one hop, W-1 x S bytes per rank spread over W-1 links;
+//   * two-shot (larger S): reduce-scatter (rank r sums shard r from all peers)
+//     then all-gather (read every other reduced shard from its owner);
+//     2 (W-1)/W x S bytes per rank, still all links in parallel.
+// Buffers: each rank owns one hipExtMallocWithFlags(hipDeviceMallocUncached)
+// region mapped into every peer by hipIpcOpenMemHandle.  Uncached (MTYPE UC)
+// memory makes a peer's stores visible once they complete, so a publish is
+// "stores; s_waitcnt vmcnt(0); barrier; flag store" with no L2 write-back.
+// Layout of a region (bytes):
+//   [0, 256)           control: epoch (u32), arrival ticket (u32), error (u32)
+//   [256, 256 + 4 KB)  flags[2 phases][64 blocks][8 ranks] (u32 epochs)
+//   [8 KB, ...)        2 parities x {input copy (slot_bytes), result (slot_bytes)}
+// Epochs live on the device (read at kernel start, advanced by the last block
+// to finish) so a captured hipGraph replays correctly.  Consecutive calls
+// alternate the data parity; a rank can only reach call e + 2 after every
+// peer has signalled in call e + 1, i.e. after the peers' call-e kernels (and
+// their reads of parity e) completed, so no trailing barrier is needed.
+// Every wait is bounded (spin_max polls): a missing peer sets the error word
+// and the kernel still exits, so the grid always drains.
+#include <cstring>
+
+#include "common.h"
+
+namespace lmx {
+
+constexpr int AR_MAX_W = 8, AR_MAX_BLOCKS = 64, AR_THREADS = 512;
+constexpr long AR_CTL = 0, AR_FLAGS = 256, AR_DATA = 8192;
+
+struct ArPeers {
+  char* p[AR_MAX_W];
+};
+
+__device__ __forceinline__ uint32_t* ar_flags(char* base, int phase) {
+  return reinterpret_cast<uint32_t*>(base + AR_FLAGS) + phase * AR_MAX_BLOCKS * AR_MAX_W;
+}
+
+// block-level rendezvous of block b across the W ranks
+template <int W>
+__device__ __forceinline__ void ar_barrier(const ArPeers& peers, int rank, int phase, int b,
+                                           uint32_t e, int spin_max) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");       // this thread's slot stores landed
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t < W) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __hip_atomic_store(ar_flags(peers.p[t], phase) + b * AR_MAX_W + rank, e, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint32_t* mine = ar_flags(peers.p[rank], phase) + b * AR_MAX_W + t;
+    int it = 0;
+    while ((int)(__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
+      if (++it > spin_max) {
+        __hip_atomic_store(reinterpret_cast<uint32_t*>(peers.p[rank] + AR_CTL) + 2, 1u,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ void add8(float (&acc)[8], const u16x8& v) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] += bf2f(v.v[j]);
+}
+
+__device__ __forceinline__ u16x8 pack8(const float (&acc)[8]) {
+  u16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o.v[j] = f2bf(acc[j]);
+  return o;
+}
+
+template <int W>
+__global__ void __launch_bounds__(AR_THREADS) allreduce_kernel(
+    u16x8* out, const u16x8* inp, long n8, int rank, ArPeers peers,
+    long slot_bytes, int two_shot, int spin_max) {
+  char* own = peers.p[rank];
+  uint32_t* ctl = reinterpret_cast<uint32_t*>(own + AR_CTL);
+  const uint32_t e = ctl[0] + 1u;
+  const long par_off = AR_DATA + (long)(e & 1u) * 2 * slot_bytes;
+  const int b = blockIdx.x, nb = gridDim.x, t = threadIdx.x;
+  auto in_slot = [&](int q) { return reinterpret_cast<u16x8*>(peers.p[q] + par_off); };
+  auto res_slot = [&](int q) { return reinterpret_cast<u16x8*>(peers.p[q] + par_off + slot_bytes); };
+
+  if (!two_shot) {
+    const long per = (n8 + nb - 1) / nb, lo = b * per, hi = min(n8, lo + per);
+    u16x8* mine = in_slot(rank);
+    for (long i = lo + t; i < hi; i += AR_THREADS) mine[i] = inp[i];
+    ar_barrier<W>(peers, rank, 0, b, e, spin_max);
+    for (long i = lo + t; i < hi; i += AR_THREADS) {
+      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < W; ++q) add8(acc, in_slot(q)[i]);   // rank order: same sum everywhere
+      out[i] = pack8(acc);
+    }
+  } else {
+    const long s = n8 / W;                        // shard length (host: n8 % W == 0)
+    const long per = (s + nb - 1) / nb, lo = b * per, hi = min(s, lo + per);
+    u16x8* mine = in_slot(rank);
+#pragma unroll
+    for (int q = 0; q < W; ++q)
+      for (long i = lo + t; i < hi; i += AR_THREADS) mine[q * s + i] = inp[q * s + i];
+    ar_barrier<W>(peers, rank, 0, b, e, spin_max);
+    u16x8* res = res_slot(rank);
+    for (long i = lo + t; i < hi; i += AR_THREADS) {
+      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < W; ++q) add8(acc, in_slot(q)[rank * s + i]);
+      const u16x8 o = pack8(acc);
+      res[rank * s + i] = o;
+      out[rank * s + i] = o;
+    }
+    ar_barrier<W>(peers, rank, 1, b, e, spin_max);
+#pragma unroll
+    for (int q = 0; q < W; ++q) {
+      if (q == rank) continue;
+      const u16x8* src = res_slot(q);
+      for (long i = lo + t; i < hi; i += AR_THREADS) out[q * s + i] = src[q * s + i];
+    }
+  }
+  // the last block to finish advances the epoch for the next call
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) {
+    const uint32_t old = __hip_atomic_fetch_add(ctl + 1, 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+    if (old == (uint32_t)(nb - 1)) {
+      __hip_atomic_store(ctl + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ctl, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// ----------------------------------------------------------------- host ----
+long ar_region_bytes(long slot_bytes) { return AR_DATA + 4 * slot_bytes; }
+
+int ar_alloc(void** ptr, long slot_bytes) {
+  const size_t n = (size_t)ar_region_bytes(slot_bytes);
+  hipError_t e = hipExtMallocWithFlags(ptr, n, hipDeviceMallocUncached);
+  if (e != hipSuccess) return (int)e;
+  e = hipMemset(*ptr, 0, n);
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  return (int)e;
+}
+
+int ar_free(void* ptr) { return (int)hipFree(ptr); }
+
+int ar_ipc_handle(void* ptr, void* handle_out /* 64 B */) {
+  hipIpcMemHandle_t h;
+  const hipError_t e = hipIpcGetMemHandle(&h, ptr);
+  if (e != hipSuccess) return (int)e;
+  memcpy(handle_out, &h, sizeof(h));
+  return 0;
+}
+
+int ar_ipc_open(void** ptr, const void* handle /* 64 B */) {
+  hipIpcMemHandle_t h;
+  memcpy(&h, handle, sizeof(h));
+  return (int)hipIpcOpenMemHandle(ptr, h, hipIpcMemLazyEnablePeerAccess);
+}
+
+int ar_ipc_close(void* ptr) { return (int)hipIpcCloseMemHandle(ptr); }
+
+int ar_ipc_handle_size() { return (int)sizeof(hipIpcMemHandle_t); }
+
+// error word of this rank's region (device -> host read, synchronous)
+int ar_error(void* own, int clear) {
+  uint32_t v = 0;
+  hipError_t e = hipMemcpy(&v, (char*)own + AR_CTL + 8, 4, hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return -(int)e;
+  if (clear && v) {
+    const uint32_t z = 0;
+    e = hipMemcpy((char*)own + AR_CTL + 8, &z, 4, hipMemcpyHostToDevice);
+    if (e != hipSuccess) return -(int)e;
+  }
+  return (int)v;
+}
+
+int allreduce(void* out, const void* inp, long nbytes, int rank, int world,
+              const unsigned long long* peer_ptrs, long slot_bytes, int two_shot, int blocks,
+              int spin_max, hipStream_t stream) {
+  if (nbytes <= 0) return 0;
+  if (world < 2 || world > AR_MAX_W || rank < 0 || rank >= world) return -1;
+  if (nbytes % 16 != 0 || nbytes > slot_bytes) return -2;
+  const long n8 = nbytes / 16;
+  if (two_shot && n8 % world != 0) return -3;
+  if (blocks < 1 || blocks > AR_MAX_BLOCKS) return -4;
+  if (((uintptr_t)out | (uintptr_t)inp) % 16 != 0) return -5;
+  ArPeers p;
+  for (int q = 0; q < AR_MAX_W; ++q) p.p[q] = q < world ? (char*)peer_ptrs[q] : nullptr;
+  for (int q = 0; q < world; ++q)
+    if (!p.p[q]) return -6;
+#define LMX_AR(WV)                                                                             \
+  allreduce_kernel<WV><<<dim3(blocks), dim3(AR_THREADS), 0, stream>>>(                         \
+      (u16x8*)out, (const u16x8*)inp, n8, rank, p, slot_bytes, two_shot, spin_max);
+  switch (world) {
+    case 2: LMX_AR(2) break;
+    case 3: LMX_AR(3) break;
+    case 4: LMX_AR(4) break;
+    case 5: LMX_AR(5) break;
+    case 6: LMX_AR(6) break;
+    case 7: LMX_AR(7) break;
+    default: LMX_AR(8) break;
+  }
+#undef LMX_AR
+  return (int)hipGetLastError();
+}
+
+}  // namespace lmx

@@ -6,6 +6,9 @@
 // synchronises, so every launch is hipGraph-capturable.
 #include <hip/hip_runtime.h>
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+#include <string>
+#include <vector>
 #include <stdexcept>
 #include <string>
 
@@ -32,6 +35,16 @@ int gemm_splitk(void*, const void*, const void*, float*, int*, int, int, int, lo
                 int, hipStream_t);
 int gemm_nt(void*, const void*, const void*, const void*, const void*, int, int, int, long, long,
             long, int, hipStream_t);
+long ar_region_bytes(long);
+int ar_alloc(void**, long);
+int ar_free(void*);
+int ar_ipc_handle(void*, void*);
+int ar_ipc_open(void**, const void*);
+int ar_ipc_close(void*);
+int ar_ipc_handle_size();
+int ar_error(void*, int);
+int allreduce(void*, const void*, long, int, int, const unsigned long long*, long, int, int, int,
+              hipStream_t);
 }  // namespace lmx
 
 namespace py = pybind11;
@@ -125,6 +138,41 @@ PYBIND11_MODULE(_lmx_kernels, m) {
     check(lmx::gemm_splitk(P<void>(C), P<void>(A), P<void>(W), P<float>(slabs), P<int>(tickets), M,
                            N, K, lda, ldw, ldc, splits, S(stream)),
           "gemm_splitk");
+  });
+  // ---- peer-memory all-reduce (allreduce.hip) ----
+  m.def("ar_region_bytes", [](long slot) { return lmx::ar_region_bytes(slot); });
+  m.def("ar_alloc", [](long slot) {
+    void* p = nullptr;
+    check(lmx::ar_alloc(&p, slot), "ar_alloc");
+    return (uptr)p;
+  });
+  m.def("ar_free", [](uptr p) { check(lmx::ar_free(P<void>(p)), "ar_free"); });
+  m.def("ar_ipc_handle", [](uptr p) {
+    std::string h((size_t)lmx::ar_ipc_handle_size(), '\0');
+    check(lmx::ar_ipc_handle(P<void>(p), h.data()), "ar_ipc_handle");
+    return py::bytes(h);
+  });
+  m.def("ar_ipc_open", [](py::bytes handle) {
+    std::string h = handle;
+    if ((int)h.size() != lmx::ar_ipc_handle_size())
+      throw std::runtime_error("ar_ipc_open: bad handle size");
+    void* p = nullptr;
+    check(lmx::ar_ipc_open(&p, h.data()), "ar_ipc_open");
+    return (uptr)p;
+  });
+  m.def("ar_ipc_close", [](uptr p) { check(lmx::ar_ipc_close(P<void>(p)), "ar_ipc_close"); });
+  m.def("ar_error", [](uptr own, int clear) {
+    const int v = lmx::ar_error(P<void>(own), clear);
+    if (v < 0) check(-v, "ar_error");
+    return v;
+  });
+  m.def("allreduce", [](uptr out, uptr inp, long nbytes, int rank, int world,
+                        std::vector<unsigned long long> peers, long slot_bytes, int two_shot,
+                        int blocks, int spin_max, uptr stream) {
+    if ((int)peers.size() < world) throw std::runtime_error("allreduce: peers < world");
+    check(lmx::allreduce(P<void>(out), P<void>(inp), nbytes, rank, world, peers.data(), slot_bytes,
+                         two_shot, blocks, spin_max, S(stream)),
+          "allreduce");
   });
   m.def("gemm_nt", [](uptr C, uptr A, uptr W, uptr bias, uptr residual, int M, int N, int K,
                       long lda, long ldw, long ldc, int act, uptr stream) {

@@ -184,7 +184,8 @@ class EngineServer:
             return {"stats": dict(self.embed_engine.stats) if self.embed_engine else {}}
         s = e.sched
         return {"running": s.num_running, "waiting": s.num_waiting, "kv_usage": s.kv_usage,
-                "kv_free_blocks": s.kv_free_blocks, "stats": dict(e.stats)}
+                "kv_free_blocks": s.kv_free_blocks, "stats": dict(e.stats),
+                "tp_comm": getattr(e, "tp_comm", {})}
 
     # engine thread: one message per connection per step
     def _sink(self, evs: list[TokenEvent]):

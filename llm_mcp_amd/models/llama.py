@@ -52,10 +52,13 @@ class TPContext:
 
     def __init__(self, rank: int = 0, size: int = 1, group=None):
         self.rank, self.size, self.group = rank, size, group
+        self.peer = None      # parallel.peer_allreduce.PeerAllReduce when enabled
 
     def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
         if self.size > 1:
-            if self._host_staged(t):
+            if self.peer is not None and self.peer.supports(t):
+                self.peer(t)     # one kernel over peer memory (decode sizes)
+            elif self._host_staged(t):
                 h = t.cpu()
                 torch.distributed.all_reduce(h, group=self.group)
                 t.copy_(h)

@@ -1,0 +1,180 @@
+"""Peer-memory all-reduce for decode-sized TP messages (X1/X2 over xGMI).
+
+Wraps csrc/kernels/allreduce.hip.  Every rank allocates one uncached device
+region, exports it with ``hipIpcGetMemHandle``, the handles are exchanged
+over the TP process group (``all_gather_object``), and every rank maps all
+peer regions with ``hipIpcOpenMemHandle``.  A call is then ONE kernel launch
+with no host involvement, so it is captured into the decode hipGraphs like
+any other op.  RCCL stays the path for messages larger than a slot (prefill)
+and for anything the kernel does not cover (non-bf16, unaligned).
+
+Selection: one-shot (every rank reads all W inputs) up to ``oneshot_max``
+bytes, two-shot (reduce-scatter + all-gather through peer memory) above.
+The crossover and the slot size are env-tunable (LMX_AR_ONESHOT_MAX,
+LMX_AR_SLOT_MB); the defaults come from the per-link arithmetic in
+SURVEY §2.3 (one-shot moves (W-1) x S per rank, two-shot 2 (W-1)/W x S, both
+over all W-1 links at once, vs a ring's 2 (W-1)/W x S over one link).
+
+A self-test against the process group's own all-reduce runs at setup; a
+mismatch, a bounded-wait timeout (error word set by the kernel) or any HIP
+error disables the path and the group falls back to RCCL.
+"""
+from __future__ import annotations
+
+import logging
+import os
+
+import torch
+import torch.distributed as dist
+
+from ..native import kernels as native
+
+log = logging.getLogger("lmx.tp")
+
+MAX_WORLD, MAX_BLOCKS = 8, 64
+
+
+class PeerAllReduce:
+    def __init__(self, group, rank: int, world: int, device: torch.device,
+                 slot_bytes: int | None = None, oneshot_max: int | None = None,
+                 spin_max: int = 1 << 22):
+        if not 2 <= world <= MAX_WORLD:
+            raise ValueError(f"peer all-reduce supports 2..{MAX_WORLD} ranks, got {world}")
+        self.group, self.rank, self.world, self.device = group, rank, world, device
+        self.slot = int(slot_bytes or float(os.environ.get("LMX_AR_SLOT_MB", "16")) * (1 << 20))
+        self.slot -= self.slot % (16 * world)
+        self.oneshot_max = int(oneshot_max or os.environ.get("LMX_AR_ONESHOT_MAX", 512 << 10))
+        self.spin_max = spin_max
+        self.k = native()
+        self.own, self.peers, self.calls = None, [], 0
+        # every rank reaches the handle exchange, even when its own
+        # allocation failed, so a local failure cannot strand the others
+        mine, why = b"", ""
+        try:
+            self.own = self.k.ar_alloc(self.slot)
+            mine = self.k.ar_ipc_handle(self.own)
+        except RuntimeError as ex:
+            why = str(ex)
+        handles = [None] * world
+        dist.all_gather_object(handles, mine, group=group)
+        if not all(handles):
+            self.close()
+            raise RuntimeError(f"peer all-reduce: a rank could not export its region ({why})")
+        try:
+            for q in range(world):
+                self.peers.append(self.own if q == rank else self.k.ar_ipc_open(handles[q]))
+        except Exception:
+            self.close()
+            raise
+
+    # ------------------------------------------------------------------ api --
+    def supports(self, t: torch.Tensor) -> bool:
+        n = t.numel() * t.element_size()
+        return (t.is_cuda and t.dtype == torch.bfloat16 and t.is_contiguous()
+                and 0 < n <= self.slot and n % 16 == 0 and t.data_ptr() % 16 == 0)
+
+    def plan(self, nbytes: int) -> tuple[int, int]:
+        """(two_shot, blocks) for a message of nbytes."""
+        n8 = nbytes // 16
+        two = int(nbytes > self.oneshot_max and n8 % self.world == 0)
+        per_rank = nbytes // self.world if two else nbytes
+        blocks = max(1, min(MAX_BLOCKS, per_rank // (16 << 10)))
+        return two, blocks
+
+    def __call__(self, t: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        """Sum of ``t`` over the group, in place unless ``out`` is given."""
+        out = t if out is None else out
+        n = t.numel() * t.element_size()
+        two, blocks = self.plan(n)
+        self.k.allreduce(out.data_ptr(), t.data_ptr(), n, self.rank, self.world, self.peers,
+                         self.slot, two, blocks, self.spin_max,
+                         torch.cuda.current_stream(t.device).cuda_stream)
+        self.calls += 1
+        return out
+
+    def error(self, clear: bool = False) -> int:
+        """Non-zero when a kernel gave up waiting for a peer (synchronous)."""
+        return self.k.ar_error(self.own, int(clear))
+
+    def close(self) -> None:
+        if self.own is None:
+            return
+        if self.peers:
+            torch.cuda.synchronize(self.device)
+        for q, p in enumerate(self.peers):
+            if q != self.rank:
+                try:
+                    self.k.ar_ipc_close(p)
+                except RuntimeError:
+                    pass
+        self.peers = []
+        self.k.ar_free(self.own)
+        self.own = None
+
+    # ------------------------------------------------------------ self-test --
+    def self_test(self, reference_all_reduce, sizes=(4096, 64 << 10, 1 << 20)) -> bool:
+        """Compare against ``reference_all_reduce`` (the group's RCCL / gloo
+        path) on seeded data; every rank must agree on the verdict."""
+        ok = True
+        g = torch.Generator(device="cpu").manual_seed(1234 + self.rank)
+        for n in sizes:
+            n = min(n, self.slot)
+            x = (torch.randn(n // 2, generator=g) * (self.rank + 1)).to(
+                torch.bfloat16).to(self.device)
+            want = reference_all_reduce(x.clone()).float()
+            try:
+                got = self(x.clone()).float()
+                torch.cuda.synchronize(self.device)
+                err = (got - want).abs().max().item()
+                timed_out = self.error(clear=True)
+            except RuntimeError as ex:
+                err, timed_out = float("inf"), str(ex)
+            tol = 2e-2 * max(1.0, want.abs().max().item())
+            if not (err <= tol) or timed_out:
+                log.warning("peer all-reduce self-test failed at %d B (max err %.3g, %s)", n,
+                            err, timed_out or "no timeout")
+                ok = False
+        return ok
+
+
+_CPU_GROUPS: dict = {}
+
+
+def _cpu_group(group):
+    """A gloo twin of ``group`` for host-side control values."""
+    if dist.get_backend(group) == "gloo":
+        return group
+    key = id(group)
+    if key not in _CPU_GROUPS:
+        _CPU_GROUPS[key] = dist.new_group(backend="gloo")
+    return _CPU_GROUPS[key]
+
+
+def _agree(ok: bool, group) -> bool:
+    flag = torch.tensor([int(ok)], dtype=torch.int32)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=_cpu_group(group))
+    return bool(flag.item())
+
+
+def setup(tp, device: torch.device) -> PeerAllReduce | None:
+    """Enable the peer all-reduce on a TP context when possible (LMX_CUSTOM_AR=0
+    disables it).  Collective: every rank of the group must call it."""
+    if tp.size < 2 or device.type != "cuda" or os.environ.get("LMX_CUSTOM_AR", "1") == "0":
+        return None
+    ar, ok = None, True
+    try:
+        ar = PeerAllReduce(tp.group, tp.rank, tp.size, device)
+    except Exception as ex:   # IPC unavailable (no peer access, old driver ...)
+        log.warning("peer all-reduce unavailable: %s", ex)
+        ok = False
+    if not _agree(ok, tp.group):          # symmetric: everyone built it, or nobody uses it
+        if ar is not None:
+            ar.close()
+        return None
+    if not _agree(ar.self_test(tp.all_reduce), tp.group):
+        ar.close()
+        return None
+    tp.peer = ar
+    log.info("peer all-reduce enabled: world %d, slot %d MB, one-shot <= %d KB",
+             tp.size, ar.slot >> 20, ar.oneshot_max >> 10)
+    return ar

@@ -58,6 +58,45 @@ def attach_channel(engine, tp: TPContext, tag: str) -> PlanChannel | None:
     return ch
 
 
+def probe_allreduce(tp: TPContext, device: torch.device, sizes=(16 << 10, 256 << 10, 1 << 20,
+                                                                4 << 20), iters: int = 20) -> dict:
+    """Time the group's all-reduce paths on decode-sized bf16 messages
+    (collective: all ranks call it).  Returns {path: {bytes: us}}; exported
+    as rccl_allreduce_seconds{group=path} by the serving process."""
+    out: dict[str, dict[int, float]] = {}
+    paths = [("rccl", None)]
+    if tp.peer is not None:
+        paths.append(("peer", tp.peer))
+    for name, peer in paths:
+        res = {}
+        for n in sizes:
+            x = torch.zeros(n // 2, dtype=torch.bfloat16, device=device)
+            if peer is not None and not peer.supports(x):
+                continue
+
+            def call():
+                if peer is not None:
+                    peer(x)
+                else:
+                    saved, tp.peer = tp.peer, None
+                    try:
+                        tp.all_reduce(x)
+                    finally:
+                        tp.peer = saved
+            for _ in range(3):
+                call()
+            torch.cuda.synchronize(device)
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(iters):
+                call()
+            e.record()
+            torch.cuda.synchronize(device)
+            res[n] = round(s.elapsed_time(e) / iters * 1e3, 1)
+        out[name] = res
+    return out
+
+
 def build_tp_engine(ecfg, device, tp: TPContext, tag: str, weights_path: str = "",
                     model_cfg=None):
     from ..engine.engine import LLMEngine
@@ -67,7 +106,15 @@ def build_tp_engine(ecfg, device, tp: TPContext, tag: str, weights_path: str = "
     if weights_path:
         from ..models.weights import load_llama_weights
         weights = load_llama_weights(weights_path, cfg, device, tp.rank, tp.size)
+    dev = torch.device(device)
+    comm = {}
+    if dev.type == "cuda" and tp.size > 1:
+        from .peer_allreduce import setup as setup_peer_ar
+        setup_peer_ar(tp, dev)
+        comm = probe_allreduce(tp, dev)
+        log.info("TP all-reduce us by message size: %s", comm)
     eng = LLMEngine(ecfg, device=device, model_cfg=cfg, tp=tp, weights=weights)
+    eng.tp_comm = comm
     attach_channel(eng, tp, tag)
     return eng
 

@@ -86,6 +86,11 @@ def test_lease_queue_matches_model(ops):
             got = q.get_job(k)
             if m["status"] == "queued" and m["attempts"] >= m["max"]:
                 assert got["status"] in ("queued", "error")   # swept at next claim
+            elif m["status"] == "running" and m["lease"] < now[0] and m["attempts"] >= m["max"]:
+                # expired with no attempt left: a claim may sweep it to error
+                assert got["status"] in ("running", "error")
+                if got["status"] == "error":
+                    m.update(status="error", token=None)
             else:
                 assert got["status"] == m["status"], (k, got, m)
             assert got["attempts"] == m["attempts"]
