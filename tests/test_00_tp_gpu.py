@@ -4,7 +4,9 @@ the device).
 
 A 1-GPU box cannot host two RCCL ranks, so the two ranks share cuda:0 over a
 gloo process group (device tensors staged through the host where gloo needs
-it).  Everything else is the production TP path: per-rank shards from the HF
+it).  Everything else is the production TP path (the all-reduces run on
+the peer-memory kernel, parallel/peer_allreduce.py, whose IPC regions the two
+processes map on the same device): per-rank shards from the HF
 safetensors loader, the leader's plan mailbox, the HIP kernels on each shard,
 all-reduces after the O and down projections and the vocab-split LM head."""
 import os
@@ -45,6 +47,7 @@ def _rank(rank, size, port, ckpt, tag, q):
                                                        ignore_eos=True))
             eng.release_followers()
             q.put(("leader", out))
+            q.put(("comm", eng.tp_comm))
         else:
             q.put(("follower", eng.run_follower()))
     finally:
@@ -69,7 +72,7 @@ def test_tp2_group_on_gpu_kernels(tmp_path):
     for p in procs:
         p.start()
     try:
-        res = dict(q.get(timeout=400) for _ in procs)
+        res = dict(q.get(timeout=400) for _ in range(len(procs) + 1))
         for p in procs:
             p.join(timeout=60)
             assert p.exitcode == 0
@@ -78,6 +81,8 @@ def test_tp2_group_on_gpu_kernels(tmp_path):
             if p.is_alive():
                 p.kill()
     assert res["follower"] > 0
+    # the all-reduces ran on the peer-memory kernel (IPC regions on the one GPU)
+    assert res["comm"].get("peer"), res["comm"]
     for prompt, out in zip(PROMPTS, res["leader"]):
         assert len(out) == 6
         assert_greedy_consistent(full, prompt, out)
