@@ -12,19 +12,33 @@ Per run:
   3. devices of this host that disappeared go offline and their running
      jobs' leases are released so they can be reclaimed at once (the reference's
      "60 s -> <5 s" recovery, offline_handler.go:12-38);
-  4. peer nodes (``LMX_PEER_NODES``, replaces the Tailscale mesh scan) are
-     polled at ``GET /v1/discovery/local`` and their devices upserted with the
-     peer's URL as ``engine_addr``.
+  4. peer nodes are polled at ``GET /v1/discovery/local`` (concurrently, 2 s
+     timeout) and their devices upserted with the peer's URL as
+     ``engine_addr``; an unreachable peer's devices go offline with their
+     leases released.  Peer sources, as the reference's mesh scan
+     (discovery.go:88-174, 299-420, 755-877):
+       * ``LMX_PEER_NODES`` -- explicit core URLs;
+       * ``DISCOVERY_EXTRA_ENDPOINTS`` (alias ``OLLAMA_EXTRA_ENDPOINTS``) --
+         ``host:port`` list;
+       * Tailscale -- ``tailscale status --json`` Self/Peers (online ones are
+         probed on every ``LMX_PEER_PORTS`` port, default 8080; nodes the mesh
+         reports offline have their devices taken offline at once);
+       * ``DISCOVERY_SCAN_SUBNETS=1`` + ``DISCOVERY_SUBNETS`` (CIDR list, at
+         most 1024 hosts) -- LAN scan on the same ports.
 """
 from __future__ import annotations
 
+import ipaddress
 import json
 import logging
 import os
-import threading
 import re
+import shutil
+import subprocess
+import threading
 import time
 import urllib.request
+from concurrent.futures import ThreadPoolExecutor
 
 from ..policy.inference import model_record
 from . import rocm_enum
@@ -134,21 +148,105 @@ class DiscoveryRunner:
             self.last_result = res
         return res
 
+    # ------------------------------------------------------------- mesh --
+    @staticmethod
+    def _ports() -> list[int]:
+        return [int(p) for p in os.environ.get("LMX_PEER_PORTS", "8080").split(",") if p.strip()]
+
+    def _tailscale_status(self) -> dict | None:
+        """``tailscale status --json`` (LMX_TAILSCALE_STATUS_FILE overrides it
+        with a saved status document, used by tests and air-gapped setups)."""
+        path = os.environ.get("LMX_TAILSCALE_STATUS_FILE", "")
+        try:
+            if path:
+                with open(path) as f:
+                    return json.load(f)
+            if os.environ.get("LMX_DISCOVERY_TAILSCALE", "1") == "0":
+                return None
+            exe = shutil.which("tailscale")
+            if not exe:
+                return None
+            out = subprocess.run([exe, "status", "--json"], capture_output=True, timeout=10,
+                                 check=True).stdout
+            return json.loads(out)
+        except (OSError, ValueError, subprocess.SubprocessError) as e:
+            log.warning("tailscale status unavailable: %s", e)
+            return None
+
+    def _peer_urls(self) -> tuple[list[str], list[str]]:
+        """(urls to probe, hosts the mesh reports offline)."""
+        urls = [p.strip().rstrip("/") for p in os.environ.get("LMX_PEER_NODES", "").split(",")
+                if p.strip()]
+        extra = os.environ.get("DISCOVERY_EXTRA_ENDPOINTS") or os.environ.get(
+            "OLLAMA_EXTRA_ENDPOINTS", "")
+        for ep in (e.strip() for e in extra.split(",")):
+            if ep:
+                urls.append(ep.rstrip("/") if "://" in ep else "http://" + ep)
+        offline_hosts: list[str] = []
+        st = self._tailscale_status()
+        if st:
+            for node in (st.get("Peer") or {}).values():
+                name = (node.get("DNSName") or "").rstrip(".") or node.get("HostName", "")
+                ips = node.get("TailscaleIPs") or []
+                addr = ips[0] if ips else name       # mesh IPs route without MagicDNS
+                if not addr:
+                    continue
+                if not node.get("Online", False):
+                    offline_hosts += [h for h in (name, node.get("HostName", "")) if h]
+                    continue
+                urls += [f"http://{addr}:{p}" for p in self._ports()]
+        if os.environ.get("DISCOVERY_SCAN_SUBNETS", "0") == "1":
+            hosts: list[str] = []
+            for cidr in os.environ.get("DISCOVERY_SUBNETS", "").split(","):
+                if not cidr.strip():
+                    continue
+                try:
+                    net = ipaddress.ip_network(cidr.strip(), strict=False)
+                except ValueError:
+                    log.warning("bad subnet %r", cidr)
+                    continue
+                hs = list(net.hosts()) or [net.network_address]
+                hosts += [str(h) for h in hs[:1024 - len(hosts)]]
+                if len(hosts) >= 1024:
+                    break
+            urls += [f"http://{h}:{p}" for h in hosts for p in self._ports()]
+        return list(dict.fromkeys(urls)), offline_hosts
+
+    @staticmethod
+    def _probe(url: str) -> dict | None:
+        try:
+            with urllib.request.urlopen(url + "/v1/discovery/local", timeout=2) as r:
+                data = json.loads(r.read())
+            return data if isinstance(data, dict) and "devices" in data else None
+        except Exception:
+            return None
+
+    def _take_offline(self, pred, reason: str) -> None:
+        for d in self.store.list_devices():
+            if d.get("status") == "online" and pred(d):
+                self.store.set_device_status(d["id"], "offline",
+                                             {"last_error": reason, "last_error_at": time.time()})
+                self.store.release_device_leases(d["id"])
+
     def _poll_peers(self) -> list[str]:
-        peers = [p.strip().rstrip("/") for p in os.environ.get("LMX_PEER_NODES", "").split(",")
-                 if p.strip()]
+        urls, offline_hosts = self._peer_urls()
+        if offline_hosts:
+            dead = set(offline_hosts)
+            self._take_offline(lambda d: d.get("host") in dead, "mesh reports node offline")
+        if not urls:
+            return []
+        with ThreadPoolExecutor(max_workers=min(32, len(urls))) as ex:
+            results = list(ex.map(self._probe, urls))
         ok = []
-        for url in peers:
-            try:
-                with urllib.request.urlopen(url + "/v1/discovery/local", timeout=2) as r:
-                    data = json.loads(r.read())
-            except Exception:
-                for d in self.store.list_devices():
-                    if (d.get("tags") or {}).get("peer") == url:
-                        self.store.set_device_status(d["id"], "offline")
-                        self.store.release_device_leases(d["id"])
+        me = rocm_enum.host_id()
+        for url, data in zip(urls, results):
+            if data is None:
+                self._take_offline(lambda d, u=url: (d.get("tags") or {}).get("peer") == u,
+                                   "peer unreachable")
                 continue
             for d in data.get("devices", []):
+                if d.get("host") == me:
+                    continue          # our own core answering through the mesh
                 tags = dict(d.get("tags") or {})
                 tags.update(peer=url, engine_addr=url)
                 self.store.upsert_device(d["id"], d.get("name", ""), d.get("platform", "rocm"),

@@ -75,6 +75,13 @@ VARS: list[Var] = [
     Var("LMX_MAINTENANCE_INTERVAL", int, 60, "seconds between store maintenance ticks"),
     Var("LMX_JOB_STREAM_MAX_S", int, 3600, "max duration of one /v1/jobs/{id}/stream"),
     Var("LMX_PEER_NODES", str, "", "other nodes' core URLs polled by discovery"),
+    Var("LMX_PEER_PORTS", str, "8080", "core ports probed on mesh / subnet hosts"),
+    Var("LMX_DISCOVERY_TAILSCALE", int, 1, "probe Tailscale peers when the tailscale CLI exists"),
+    Var("LMX_TAILSCALE_STATUS_FILE", str, "", "saved 'tailscale status --json' document to use instead of the CLI"),
+    Var("DISCOVERY_EXTRA_ENDPOINTS", str, "", "extra peer host:port list (alias OLLAMA_EXTRA_ENDPOINTS)"),
+    Var("OLLAMA_EXTRA_ENDPOINTS", str, "", "reference name of DISCOVERY_EXTRA_ENDPOINTS"),
+    Var("DISCOVERY_SCAN_SUBNETS", int, 0, "scan DISCOVERY_SUBNETS for peer cores"),
+    Var("DISCOVERY_SUBNETS", str, "", "CIDR list scanned when DISCOVERY_SCAN_SUBNETS=1 (max 1024 hosts)"),
     Var("LMX_NODE_ID", str, "", "host id used in device ids (default hostname)"),
     Var("LMX_FAKE_GPUS", int, 0, "enumerate N fake GPUs (tests / CPU hosts)"),
     Var("LMX_ALERT_TEMP_C", float, 95.0, "GPU temperature alert threshold"),
