@@ -239,7 +239,7 @@ class LLMEngine:
             self._hout = torch.zeros((2, ecfg.max_num_seqs), dtype=torch.int32, pin_memory=True)
             self._hout_np = self._hout.numpy()
             self._out_ev = torch.cuda.Event()
-        if ecfg.use_graphs and self.device.type == "cuda":
+        if ecfg.use_graphs and self.device.type == "cuda" and not ops.debug_sync():
             self._capture_graphs()
         self._bucket_list = sorted(self.graphs)
 

@@ -23,12 +23,46 @@ _K = None
 _K_ERR: Exception | None = None
 
 
+class _SyncedKernels:
+    """LMX_DEBUG_SYNC=1: every kernel launch is followed by a device
+    synchronize, so an asynchronous fault (bad address, NaN trap, a hung
+    wave) is reported by the launch that caused it, named, instead of by a
+    later unrelated call -- the HIP_LAUNCH_BLOCKING / AMD_SERIALIZE_KERNEL
+    style debug mode of SURVEY §5.2 for this package's own kernels.  The
+    engine disables hipGraph capture in this mode."""
+
+    def __init__(self, mod):
+        self._mod = mod
+
+    def __getattr__(self, name):
+        fn = getattr(self._mod, name)
+        if not callable(fn):
+            return fn
+
+        def call(*a, **kw):
+            r = fn(*a, **kw)
+            if not torch.cuda.is_current_stream_capturing():
+                try:
+                    torch.cuda.synchronize()
+                except RuntimeError as e:
+                    raise RuntimeError(f"lmx kernel {name} faulted: {e}") from e
+            return r
+        return call
+
+
+def debug_sync() -> bool:
+    import os
+    return os.environ.get("LMX_DEBUG_SYNC", "0") == "1"
+
+
 def native():
     """The loaded kernel extension (raises with the build hint if absent)."""
     global _K, _K_ERR
     if _K is None and _K_ERR is None:
         try:
             _K = importlib.import_module("llm_mcp_amd._lmx_kernels")
+            if debug_sync():
+                _K = _SyncedKernels(_K)
         except Exception as e:  # pragma: no cover - depends on the build
             _K_ERR = e
     if _K is None:

@@ -90,6 +90,7 @@ VARS: list[Var] = [
     Var("LMX_FAULT", str, "", "fault injection spec (job_crash:p,claim_drop:p,gpu_error:p,...)"),
     Var("LMX_FAULT_SEED", int, 0, "fault injection RNG seed"),
     Var("LMX_AUTOBUILD", int, 1, "build missing native extensions on import"),
+    Var("LMX_DEBUG_SYNC", int, 0, "synchronize after every HIP kernel launch and name the faulting kernel (disables graphs)"),
     Var("LMX_CUSTOM_AR", int, 1, "TP all-reduce over IPC-mapped peer memory for decode sizes (0 = RCCL only)"),
     Var("LMX_AR_SLOT_MB", float, 16.0, "peer all-reduce: largest message (MB) per rank region slot"),
     Var("LMX_AR_ONESHOT_MAX", int, 524288, "peer all-reduce: one-shot up to this many bytes, two-shot above"),

@@ -33,3 +33,36 @@ def test_every_env_read_in_the_package_is_registered():
                 "OPENROUTER_MODEL", "LMX_FAULT_HANG_S", "LMX_HTTP_HOST", "LMX_HTTP_PORT"}
     missing = sorted(n for n in names - launcher if n not in settings._BY_NAME)
     assert not missing, missing
+
+
+def test_debug_sync_wrapper_names_the_faulting_kernel(monkeypatch):
+    import torch
+
+    from llm_mcp_amd import ops
+
+    class Mod:
+        answer = 42
+
+        @staticmethod
+        def good(x):
+            return x + 1
+
+        @staticmethod
+        def bad():
+            return None
+
+    calls = []
+    monkeypatch.setattr(torch.cuda, "is_current_stream_capturing", lambda: False)
+
+    def sync():
+        calls.append(1)
+        if len(calls) == 2:
+            raise RuntimeError("HIP error: an illegal memory access")
+    monkeypatch.setattr(torch.cuda, "synchronize", sync)
+    k = ops._SyncedKernels(Mod())
+    assert k.answer == 42 and k.good(1) == 2 and calls == [1]
+    try:
+        k.bad()
+        raise AssertionError("expected the fault")
+    except RuntimeError as e:
+        assert "lmx kernel bad faulted" in str(e)
