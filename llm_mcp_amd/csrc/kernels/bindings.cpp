@@ -17,7 +17,7 @@ int rmsnorm(void*, void*, const void*, const void*, int, int, long, long, float,
 int layernorm(void*, const void*, const void*, const void*, const void*, int, int, float,
               hipStream_t);
 int rope_cache(void*, long, const int*, const float*, int, int, int, int, const int*, void*, void*,
-               int, int, int, hipStream_t);
+               int, int, int, const void*, const void*, float, hipStream_t);
 int kv_write(const void*, const void*, long, const int*, int, int, int, void*, void*, int,
              hipStream_t);
 int paged_decode(const void*, long, const void*, const void*, const int*, int, const int*, void*,
@@ -78,10 +78,10 @@ PYBIND11_MODULE(_lmx_kernels, m) {
   });
   m.def("rope_cache", [](uptr qkv, long qkv_stride, uptr positions, uptr cos_sin, int T, int Hq,
                          int Hkv, int D, uptr slots, uptr kc, uptr vc, int BS, int rot_k,
-                         int tile_from, uptr stream) {
+                         int tile_from, uptr q_norm, uptr k_norm, float eps, uptr stream) {
     check(lmx::rope_cache(P<void>(qkv), qkv_stride, P<int>(positions), P<float>(cos_sin), T, Hq, Hkv,
                           D, P<int>(slots), P<void>(kc), P<void>(vc), BS, rot_k, tile_from,
-                          S(stream)),
+                          P<void>(q_norm), P<void>(k_norm), eps, S(stream)),
           "rope_cache");
   });
   m.def("kv_write", [](uptr k, uptr v, long stride, uptr slots, int T, int Hkv, int D, uptr kc,

@@ -15,11 +15,32 @@
 
 namespace lmx {
 
+// Optional per-head RMSNorm of q and k before the rotation (Qwen3's q_norm /
+// k_norm).  The 16 lanes that own one head (tph = D/8 lanes x 8 elements)
+// are consecutive and 16-aligned in every loop below, so the head's sum of
+// squares is a 16-wide xor-shuffle reduction; normalisation stays in fp32
+// through the rotation (one bf16 rounding).
+__device__ __forceinline__ void qk_norm(float (&a)[4], float (&b)[4], const bf16_t* w, int i,
+                                        int half, int D, float eps) {
+  float ss = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) ss += a[j] * a[j] + b[j] * b[j];
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 16);
+  const float r = rsqrtf(ss / (float)D + eps);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    a[j] *= r * bf2f(w[i + j]);
+    b[j] *= r * bf2f(w[half + i + j]);
+  }
+}
+
 __global__ void __launch_bounds__(256) rope_cache_kernel(
     bf16_t* __restrict__ qkv, long qkv_stride, const int* __restrict__ positions,
     const float* __restrict__ cos_sin, int Hq, int Hkv, int D,
     const int* __restrict__ slot_mapping, bf16_t* __restrict__ k_cache,
-    bf16_t* __restrict__ v_cache, int BS, int rotate_k_inplace) {
+    bf16_t* __restrict__ v_cache, int BS, int rotate_k_inplace,
+    const bf16_t* __restrict__ q_norm, const bf16_t* __restrict__ k_norm, float eps) {
   const int t = blockIdx.x;
   const int half = D >> 1;
   const int tph = half >> 2;  // threads per head, each owns 4 rotation pairs
@@ -39,14 +60,17 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(
     const float4 c = *reinterpret_cast<const float4*>(cs + i);
     const float4 s = *reinterpret_cast<const float4*>(cs + half + i);
     const float cc[4] = {c.x, c.y, c.z, c.w}, ss[4] = {s.x, s.y, s.z, s.w};
+    const bool is_k = h >= Hq;
+    float a[4], b[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) a[j] = bf2f((uint16_t)x1[j]), b[j] = bf2f((uint16_t)x2[j]);
+    if (q_norm) qk_norm(a, b, is_k ? k_norm : q_norm, i, half, D, eps);
     bf16x4_t o1, o2;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const float a = bf2f((uint16_t)x1[j]), b = bf2f((uint16_t)x2[j]);
-      o1[j] = (short)f2bf(a * cc[j] - b * ss[j]);
-      o2[j] = (short)f2bf(b * cc[j] + a * ss[j]);
+      o1[j] = (short)f2bf(a[j] * cc[j] - b[j] * ss[j]);
+      o2[j] = (short)f2bf(b[j] * cc[j] + a[j] * ss[j]);
     }
-    const bool is_k = h >= Hq;
     if (!is_k || rotate_k_inplace || slot < 0) {
       *reinterpret_cast<bf16x4_t*>(hp + i) = o1;
       *reinterpret_cast<bf16x4_t*>(hp + half + i) = o2;
@@ -81,7 +105,8 @@ __global__ void __launch_bounds__(256) rope_cache_tiled_kernel(
     bf16_t* __restrict__ qkv, long qkv_stride, const int* __restrict__ positions,
     const float* __restrict__ cos_sin, int row0, int T, int Hq, int Hkv, int D,
     const int* __restrict__ slot_mapping, bf16_t* __restrict__ k_cache,
-    bf16_t* __restrict__ v_cache, int BS, int rotate_k_inplace) {
+    bf16_t* __restrict__ v_cache, int BS, int rotate_k_inplace,
+    const bf16_t* __restrict__ q_norm, const bf16_t* __restrict__ k_norm, float eps) {
   __shared__ __attribute__((aligned(16))) bf16_t vt[RT * (256 + 8)];
   __shared__ int sslot[RT];
   const int t0 = row0 + blockIdx.x * RT;
@@ -102,14 +127,17 @@ __global__ void __launch_bounds__(256) rope_cache_tiled_kernel(
     const float4 c = *reinterpret_cast<const float4*>(cs + i);
     const float4 sn = *reinterpret_cast<const float4*>(cs + half + i);
     const float cc[4] = {c.x, c.y, c.z, c.w}, ss[4] = {sn.x, sn.y, sn.z, sn.w};
+    const bool is_k = h >= Hq;
+    float a[4], b[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) a[j] = bf2f((uint16_t)x1[j]), b[j] = bf2f((uint16_t)x2[j]);
+    if (q_norm) qk_norm(a, b, is_k ? k_norm : q_norm, i, half, D, eps);
     bf16x4_t o1, o2;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const float a = bf2f((uint16_t)x1[j]), b = bf2f((uint16_t)x2[j]);
-      o1[j] = (short)f2bf(a * cc[j] - b * ss[j]);
-      o2[j] = (short)f2bf(b * cc[j] + a * ss[j]);
+      o1[j] = (short)f2bf(a[j] * cc[j] - b[j] * ss[j]);
+      o2[j] = (short)f2bf(b[j] * cc[j] + a[j] * ss[j]);
     }
-    const bool is_k = h >= Hq;
     if (!is_k || rotate_k_inplace || slot < 0) {
       *reinterpret_cast<bf16x4_t*>(hp + i) = o1;
       *reinterpret_cast<bf16x4_t*>(hp + half + i) = o2;
@@ -157,18 +185,22 @@ __global__ void __launch_bounds__(256) rope_cache_tiled_kernel(
 
 int rope_cache(void* qkv, long qkv_stride, const int* positions, const float* cos_sin, int T,
                int Hq, int Hkv, int D, const int* slot_mapping, void* k_cache, void* v_cache,
-               int BS, int rotate_k_inplace, int tile_from, hipStream_t stream) {
+               int BS, int rotate_k_inplace, int tile_from, const void* q_norm,
+               const void* k_norm, float eps, hipStream_t stream) {
   if (T <= 0) return 0;
   if (D % 8 != 0 || D > 256) return -1;
+  if ((q_norm == nullptr) != (k_norm == nullptr) || (q_norm && D != 128)) return -1;
   const int n1 = tile_from < 0 ? 0 : (tile_from > T ? T : tile_from);
   if (n1 > 0)
     rope_cache_kernel<<<dim3(n1), dim3(256), 0, stream>>>(
         (bf16_t*)qkv, qkv_stride, positions, cos_sin, Hq, Hkv, D, slot_mapping,
-        (bf16_t*)k_cache, (bf16_t*)v_cache, BS, rotate_k_inplace);
+        (bf16_t*)k_cache, (bf16_t*)v_cache, BS, rotate_k_inplace, (const bf16_t*)q_norm,
+        (const bf16_t*)k_norm, eps);
   if (T > n1)
     rope_cache_tiled_kernel<<<dim3((T - n1 + RT - 1) / RT), dim3(256), 0, stream>>>(
         (bf16_t*)qkv, qkv_stride, positions, cos_sin, n1, T, Hq, Hkv, D, slot_mapping,
-        (bf16_t*)k_cache, (bf16_t*)v_cache, BS, rotate_k_inplace);
+        (bf16_t*)k_cache, (bf16_t*)v_cache, BS, rotate_k_inplace, (const bf16_t*)q_norm,
+        (const bf16_t*)k_norm, eps);
   return (int)hipGetLastError();
 }
 

@@ -32,6 +32,7 @@ class LlamaConfig:
     family: str = "llama"
     kind: str = "chat"
     qkv_bias: bool = False          # Qwen2 / Qwen2.5: biased q/k/v projections
+    qk_norm: bool = False           # Qwen3: per-head RMSNorm of q and k before RoPE
 
     @property
     def params(self) -> int:
@@ -42,7 +43,8 @@ class LlamaConfig:
         o = self.num_heads * self.head_dim * d
         mlp = 3 * d * I
         emb = V * d * (1 if self.tie_embeddings else 2)
-        return L * (qkv + o + mlp + 2 * d) + emb + d
+        qkn = 2 * self.head_dim if self.qk_norm else 0
+        return L * (qkv + o + mlp + 2 * d + qkn) + emb + d
 
     @property
     def params_b(self) -> float:
@@ -97,6 +99,18 @@ class NomicBertConfig:
         return asdict(self)
 
 
+_LLAMA32_ROPE = {"rope_type": "llama3", "factor": 32.0, "low_freq_factor": 1.0,
+                 "high_freq_factor": 4.0, "original_max_position_embeddings": 8192}
+
+
+def _qwen3(name, **kw):
+    base = dict(name=name, vocab_size=151936, head_dim=128, rope_theta=1000000.0, rms_eps=1e-6,
+                max_position=40960, bos_token_id=151643, eos_token_ids=(151645, 151643),
+                family="qwen3", qk_norm=True)
+    base.update(kw)
+    return LlamaConfig(**base)
+
+
 PRESETS: dict[str, object] = {
     "llama-3-8b": LlamaConfig(),
     "llama-3-70b": LlamaConfig(name="llama-3-70b", hidden_size=8192, intermediate_size=28672,
@@ -107,7 +121,13 @@ PRESETS: dict[str, object] = {
                                               "original_max_position_embeddings": 8192}),
     "llama-3.2-1b": LlamaConfig(name="llama-3.2-1b", hidden_size=2048, intermediate_size=8192,
                                 num_layers=16, num_heads=32, num_kv_heads=8, head_dim=64,
-                                tie_embeddings=True, max_position=131072),
+                                tie_embeddings=True, max_position=131072,
+                                rope_scaling=_LLAMA32_ROPE),
+    # the reference's default OLLAMA_MODEL (llama3.2:3b); GQA group 3
+    "llama-3.2-3b": LlamaConfig(name="llama-3.2-3b", hidden_size=3072, intermediate_size=8192,
+                                num_layers=28, num_heads=24, num_kv_heads=8, head_dim=128,
+                                tie_embeddings=True, max_position=131072,
+                                rope_scaling=_LLAMA32_ROPE),
     # tiny configs for tests / smoke (same code paths, D = 128 heads)
     "tiny-llama": LlamaConfig(name="tiny-llama", vocab_size=512, hidden_size=256,
                               intermediate_size=512, num_layers=2, num_heads=4, num_kv_heads=2,
@@ -129,6 +149,16 @@ PRESETS: dict[str, object] = {
                              head_dim=64, rope_theta=1000000.0, rms_eps=1e-6, max_position=2048,
                              bos_token_id=506, eos_token_ids=(510,), family="qwen2",
                              qkv_bias=True),
+    # Qwen3 (per-head q/k RMSNorm; num_heads x head_dim may differ from hidden)
+    "qwen3-8b": _qwen3("qwen3-8b", hidden_size=4096, intermediate_size=12288, num_layers=36,
+                       num_heads=32, num_kv_heads=8),
+    "qwen3-32b": _qwen3("qwen3-32b", hidden_size=5120, intermediate_size=25600, num_layers=64,
+                        num_heads=64, num_kv_heads=8),
+    "qwen3-0.6b": _qwen3("qwen3-0.6b", hidden_size=1024, intermediate_size=3072, num_layers=28,
+                         num_heads=16, num_kv_heads=8, tie_embeddings=True),
+    "tiny-qwen3": _qwen3("tiny-qwen3", vocab_size=512, hidden_size=256, intermediate_size=512,
+                         num_layers=2, num_heads=4, num_kv_heads=2, max_position=2048,
+                         bos_token_id=506, eos_token_ids=(510,)),
     "nomic-embed-text": NomicBertConfig(),
     "tiny-nomic": NomicBertConfig(name="tiny-nomic", vocab_size=512, hidden_size=256,
                                   intermediate_size=512, num_layers=2, num_heads=2, head_dim=128,
@@ -139,7 +169,10 @@ PRESETS: dict[str, object] = {
 ALIASES = {
     "llama3": "llama-3-8b", "llama3:8b": "llama-3-8b", "llama-3-8b-instruct": "llama-3-8b",
     "meta-llama-3-8b": "llama-3-8b", "llama3:70b": "llama-3-70b",
-    "llama3.2:1b": "llama-3.2-1b", "nomic-embed-text:latest": "nomic-embed-text",
+    "llama3.2:1b": "llama-3.2-1b", "llama3.2:3b": "llama-3.2-3b", "llama3.2": "llama-3.2-3b",
+    "nomic-embed-text:latest": "nomic-embed-text",
+    "qwen3:8b": "qwen3-8b", "qwen3:32b": "qwen3-32b", "qwen3:0.6b": "qwen3-0.6b",
+    "qwen3": "qwen3-8b",
     "nomic-embed-text-v1.5": "nomic-embed-text",
     "qwen2.5:7b": "qwen2.5-7b", "qwen2.5:0.5b": "qwen2.5-0.5b",
     "qwen2.5-7b-instruct": "qwen2.5-7b",
@@ -157,8 +190,9 @@ def from_hf_config(path: str | Path):
     """Build a config from a HF config.json (local file; no network)."""
     cfg = json.loads(Path(path).read_text())
     arch = (cfg.get("architectures") or [""])[0]
-    if "Llama" in arch or "Qwen2" in arch or "Mistral" in arch:
+    if "Llama" in arch or "Qwen2" in arch or "Qwen3" in arch or "Mistral" in arch:
         qwen = "Qwen2" in arch
+        qwen3 = "Qwen3" in arch
         return LlamaConfig(
             name=cfg.get("_name_or_path", "llama"), vocab_size=cfg["vocab_size"],
             hidden_size=cfg["hidden_size"], intermediate_size=cfg["intermediate_size"],
@@ -172,8 +206,9 @@ def from_hf_config(path: str | Path):
             bos_token_id=cfg.get("bos_token_id", 128000),
             eos_token_ids=tuple(cfg["eos_token_id"]) if isinstance(cfg.get("eos_token_id"), list)
             else (cfg.get("eos_token_id", 128001),),
-            family="qwen2" if qwen else ("mistral" if "Mistral" in arch else "llama"),
-            qkv_bias=qwen)
+            family="qwen2" if qwen else ("qwen3" if qwen3 else
+                                         ("mistral" if "Mistral" in arch else "llama")),
+            qkv_bias=qwen or bool(cfg.get("attention_bias", False)), qk_norm=qwen3)
     if "NomicBert" in arch or cfg.get("model_type") == "nomic_bert":
         return NomicBertConfig(
             vocab_size=cfg["vocab_size"], hidden_size=cfg["n_embd"],

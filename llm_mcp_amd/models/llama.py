@@ -124,10 +124,12 @@ class LlamaModel:
         layers = []
         qkv_rows = (self.Hq + 2 * self.Hkv) * self.D
         for _ in range(cfg.num_layers):
+            layers.append({})
             if cfg.qkv_bias:
-                layers.append({"bqkv": rnd(qkv_rows, std=0.02)})
-            else:
-                layers.append({})
+                layers[-1]["bqkv"] = rnd(qkv_rows, std=0.02)
+            if cfg.qk_norm:          # around 1, like trained q/k norm gains
+                layers[-1]["q_norm"] = (1.0 + rnd(self.D, std=0.1)).to(dt)
+                layers[-1]["k_norm"] = (1.0 + rnd(self.D, std=0.1)).to(dt)
             layers[-1].update({
                 "ln1": torch.ones(d, dtype=dt, device=dev),
                 "ln2": torch.ones(d, dtype=dt, device=dev),
@@ -173,7 +175,8 @@ class LlamaModel:
                 qkv += L["bqkv"]
             kc, vc = k_caches[li], v_caches[li]
             ops.rope_and_cache(qkv, inp.positions, self.cos_sin, Hq, Hkv, D, inp.slots, kc, vc,
-                               tile_from=nd)
+                               tile_from=nd, q_norm=L.get("q_norm"), k_norm=L.get("k_norm"),
+                               eps=cfg.rms_eps)
             if nd > 0:
                 ops.paged_decode_attention(qkv[:nd], kc, vc, inp.block_tables,
                                            inp.context_lens, self.scale, attn[:nd], decode_ws,

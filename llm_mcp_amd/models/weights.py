@@ -72,7 +72,7 @@ def shard_llama(full: dict, cfg: LlamaConfig, rank: int, size: int) -> dict:
         k = wqkv[qn + r["kv"][0]:qn + r["kv"][1]]
         v = wqkv[qn + kvn + r["kv"][0]:qn + kvn + r["kv"][1]]
         gu = L["w_gate_up"]
-        extra = {}
+        extra = {k: L[k] for k in ("q_norm", "k_norm") if k in L}   # per-head: replicated
         if "bqkv" in L:
             b = L["bqkv"]
             extra["bqkv"] = torch.cat([
@@ -158,6 +158,9 @@ def load_llama_weights(path: str, cfg: LlamaConfig, device, rank: int = 0, size:
         g = rd.rows(p + "mlp.gate_proj.weight", *r["i"])
         u = rd.rows(p + "mlp.up_proj.weight", *r["i"])
         extra = {}
+        if cfg.qk_norm:
+            extra["q_norm"] = put(rd.rows(p + "self_attn.q_norm.weight"))
+            extra["k_norm"] = put(rd.rows(p + "self_attn.k_norm.weight"))
         if cfg.qkv_bias:
             extra["bqkv"] = put(torch.cat([rd.rows(p + "self_attn.q_proj.bias", *r["q"]),
                                            rd.rows(p + "self_attn.k_proj.bias", *r["kv"]),
@@ -200,13 +203,17 @@ def save_hf_llama(full: dict, cfg: LlamaConfig, path: str) -> None:
         out[p + "mlp.gate_proj.weight"] = L["w_gate_up"][:I]
         out[p + "mlp.up_proj.weight"] = L["w_gate_up"][I:]
         out[p + "mlp.down_proj.weight"] = L["w_down"]
+        if "q_norm" in L:
+            out[p + "self_attn.q_norm.weight"] = L["q_norm"]
+            out[p + "self_attn.k_norm.weight"] = L["k_norm"]
         if "bqkv" in L:
             out[p + "self_attn.q_proj.bias"] = L["bqkv"][:qn]
             out[p + "self_attn.k_proj.bias"] = L["bqkv"][qn:qn + kvn]
             out[p + "self_attn.v_proj.bias"] = L["bqkv"][qn + kvn:]
     save_file({k: v.detach().to("cpu").contiguous() for k, v in out.items()},
               os.path.join(path, "model.safetensors"))
-    arch = "Qwen2ForCausalLM" if cfg.qkv_bias else "LlamaForCausalLM"
+    arch = ("Qwen3ForCausalLM" if cfg.qk_norm else
+            "Qwen2ForCausalLM" if cfg.qkv_bias else "LlamaForCausalLM")
     hf = {"architectures": [arch], "vocab_size": cfg.vocab_size,
           "hidden_size": cfg.hidden_size, "intermediate_size": cfg.intermediate_size,
           "num_hidden_layers": cfg.num_layers, "num_attention_heads": cfg.num_heads,

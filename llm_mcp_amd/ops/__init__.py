@@ -137,16 +137,24 @@ def layer_norm(x, w, b, eps, residual=None):
 def rope_and_cache(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Tensor,
                    Hq: int, Hkv: int, D: int, slots: torch.Tensor | None,
                    k_cache: torch.Tensor | None, v_cache: torch.Tensor | None,
-                   rotate_k_inplace: bool = False, tile_from: int | None = None) -> None:
+                   rotate_k_inplace: bool = False, tile_from: int | None = None,
+                   q_norm: torch.Tensor | None = None, k_norm: torch.Tensor | None = None,
+                   eps: float = 1e-6) -> None:
     """In-place rotary on q (and k) heads of the fused QKV rows; k and v are
     scattered into the paged cache at ``slots`` (-1 = skip).  Rows from
     ``tile_from`` on (prefill chunks: consecutive slots) use the 32-token
     tiled kernel with coalesced transposed-V page writes; rows before it
-    (decode: one token per page) the per-token kernel.  Default: all tiled."""
+    (decode: one token per page) the per-token kernel.  Default: all tiled.
+    ``q_norm`` / ``k_norm`` ([D] weights, D = 128): per-head RMSNorm of q and
+    k before the rotation (Qwen3), fused into the same pass."""
     if not qkv.is_cuda:
         ref.rope_cache(qkv, positions, cos_sin, Hq, Hkv, D, slots, k_cache, v_cache,
-                       rotate_k_inplace)
+                       rotate_k_inplace, q_norm, k_norm, eps)
         return
+    if q_norm is not None:
+        _chk(k_norm is not None and D == 128 and q_norm.numel() == D and k_norm.numel() == D
+             and q_norm.dtype == torch.bfloat16 and k_norm.dtype == torch.bfloat16,
+             "q_norm / k_norm: bf16 [128] both")
     _bf16(qkv, "qkv")
     T = qkv.shape[0]
     _chk(qkv.stride(1) == 1 and qkv.shape[1] >= (Hq + 2 * Hkv) * D, "qkv shape")
@@ -161,7 +169,7 @@ def rope_and_cache(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Te
     native().rope_cache(_ptr(qkv), qkv.stride(0), _ptr(positions), _ptr(cos_sin), T, Hq, Hkv, D,
                         _ptr(slots), _ptr(k_cache), _ptr(v_cache), BS,
                         int(rotate_k_inplace), 0 if tile_from is None else int(tile_from),
-                        _stream())
+                        _ptr(q_norm), _ptr(k_norm), float(eps), _stream())
 
 
 def kv_write(k, v, slots, k_cache, v_cache):

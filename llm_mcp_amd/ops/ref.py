@@ -64,11 +64,21 @@ def apply_rope(x: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Tensor) 
     return torch.cat([x1 * cos - x2 * sin, x2 * cos + x1 * sin], dim=-1).to(x.dtype)
 
 
-def rope_cache(qkv, positions, cos_sin, Hq, Hkv, D, slots, k_cache, v_cache, rotate_k_inplace):
+def head_norm(x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
+    """Per-head RMSNorm over the last dim, kept in fp32 (Qwen3 q_norm/k_norm)."""
+    xf = x.float()
+    return xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * w.float()
+
+
+def rope_cache(qkv, positions, cos_sin, Hq, Hkv, D, slots, k_cache, v_cache, rotate_k_inplace,
+               q_norm=None, k_norm=None, eps=1e-6):
     T = qkv.shape[0]
     v3 = qkv.view(T, -1, D)
-    q = apply_rope(v3[:, :Hq], positions, cos_sin)
-    k = apply_rope(v3[:, Hq:Hq + Hkv], positions, cos_sin)
+    qh, kh = v3[:, :Hq], v3[:, Hq:Hq + Hkv]
+    if q_norm is not None:
+        qh, kh = head_norm(qh, q_norm, eps), head_norm(kh, k_norm, eps)
+    q = apply_rope(qh, positions, cos_sin).to(qkv.dtype)
+    k = apply_rope(kh, positions, cos_sin).to(qkv.dtype)
     v = v3[:, Hq + Hkv:Hq + 2 * Hkv]
     v3[:, :Hq] = q
     if rotate_k_inplace or k_cache is None:

@@ -23,8 +23,11 @@ def dense_logits(model, tokens: list[int]) -> torch.Tensor:
         q = qkv[:, :Hq * D].view(T, Hq, D)
         k = qkv[:, Hq * D:(Hq + Hkv) * D].view(T, Hkv, D)
         v = qkv[:, (Hq + Hkv) * D:].view(T, Hkv, D)
-        q = ref.apply_rope(q, pos, model.cos_sin)
-        k = ref.apply_rope(k, pos, model.cos_sin)
+        if "q_norm" in L:     # Qwen3 per-head q/k RMSNorm
+            q = ref.head_norm(q, L["q_norm"], cfg.rms_eps)
+            k = ref.head_norm(k, L["k_norm"], cfg.rms_eps)
+        q = ref.apply_rope(q, pos, model.cos_sin).float()
+        k = ref.apply_rope(k, pos, model.cos_sin).float()
         a = ref.attention_dense(q, k, v, 1.0 / math.sqrt(D), 0).reshape(T, Hq * D)
         x = x + a @ L["wo"].float().t()
         h = ref.rms_norm(x, L["ln2"].float(), cfg.rms_eps)

@@ -78,3 +78,16 @@ def test_qwen2_biased_qkv_group7_matches_dense():
     for p, o in zip(prompts, outs):
         assert len(o) == 5
         assert_greedy_consistent(e.model, p, o)
+
+
+def test_qwen3_qk_norm_matches_dense():
+    """Qwen3-style model: per-head q/k RMSNorm before RoPE and
+    num_heads * head_dim (512) != hidden (256), vs the dense fp32 reference."""
+    e = _engine(model="tiny-qwen3")
+    assert e.cfg.qk_norm and e.Hq * e.D != e.cfg.hidden_size
+    assert "q_norm" in e.model.w["layers"][0]
+    prompts = [list(range(10, 50)), [7] * 33, [3]]
+    outs = e.generate(prompts, SamplingParams(temperature=0, max_tokens=5, ignore_eos=True))
+    for p, o in zip(prompts, outs):
+        assert len(o) == 5
+        assert_greedy_consistent(e.model, p, o)

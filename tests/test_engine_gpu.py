@@ -74,3 +74,14 @@ def test_qwen2_group7_on_gpu_kernels():
     for p, o in zip(prompts, outs):
         assert len(o) == 6
         assert_greedy_consistent(e.model, p, o)
+
+
+@pytest.mark.gpu
+def test_qwen3_qk_norm_on_gpu_kernels():
+    e = LLMEngine(EngineConfig(model="tiny-qwen3", max_num_seqs=8, max_batched_tokens=128,
+                               max_model_len=512, kv_cache_gb=0.05), device="cuda")
+    prompts = [list(range(10, 80)), [7] * 33, [3]]
+    outs = e.generate(prompts, SamplingParams(temperature=0, max_tokens=6, ignore_eos=True))
+    for p, o in zip(prompts, outs):
+        assert len(o) == 6
+        assert_greedy_consistent(e.model, p, o)

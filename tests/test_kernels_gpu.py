@@ -58,6 +58,17 @@ def _cache(NB, Hkv, D, BS=32):
 @pytest.mark.parametrize("layout", ["scattered", "chunks"])
 @pytest.mark.parametrize("tile_from", [None, 5, 1000])
 def test_rope_and_cache(Hq, Hkv, D, layout, tile_from):
+    _rope_case(Hq, Hkv, D, layout, tile_from, qk_norm=False)
+
+
+@pytest.mark.parametrize("Hq,Hkv", [(32, 8), (16, 8), (4, 2)])
+@pytest.mark.parametrize("tile_from", [None, 5, 1000])
+def test_rope_and_cache_qk_norm(Hq, Hkv, tile_from):
+    """Qwen3: per-head q/k RMSNorm fused before the rotation (both kernels)."""
+    _rope_case(Hq, Hkv, 128, "chunks", tile_from, qk_norm=True)
+
+
+def _rope_case(Hq, Hkv, D, layout, tile_from, qk_norm):
     T, NB = 77, 8
     qkv = _bf(T, (Hq + 2 * Hkv) * D)
     pos = torch.randint(0, 4000, (T,), device=DEV, dtype=torch.int32)
@@ -71,8 +82,16 @@ def test_rope_and_cache(Hq, Hkv, D, layout, tile_from):
     kc, vc = torch.zeros(NB, Hkv, 32, D, device=DEV, dtype=torch.bfloat16), \
         torch.zeros(NB, Hkv, D, 32, device=DEV, dtype=torch.bfloat16)
     qkv0, kc0, vc0 = qkv.cpu(), kc.cpu(), vc.cpu()
-    ops.rope_and_cache(qkv, pos, cs, Hq, Hkv, D, slots, kc, vc, tile_from=tile_from)
-    ref.rope_cache(qkv0, pos.cpu(), cs.cpu(), Hq, Hkv, D, slots.cpu(), kc0, vc0, False)
+    qn = kn = None
+    if qk_norm:
+        qn = (1 + 0.2 * torch.randn(D, device=DEV)).to(torch.bfloat16)
+        kn = (1 + 0.2 * torch.randn(D, device=DEV)).to(torch.bfloat16)
+        qkv.mul_(3.0)                      # the norm must really rescale
+        qkv0 = qkv.cpu()
+    ops.rope_and_cache(qkv, pos, cs, Hq, Hkv, D, slots, kc, vc, tile_from=tile_from,
+                       q_norm=qn, k_norm=kn, eps=1e-6)
+    ref.rope_cache(qkv0, pos.cpu(), cs.cpu(), Hq, Hkv, D, slots.cpu(), kc0, vc0, False,
+                   None if qn is None else qn.cpu(), None if kn is None else kn.cpu(), 1e-6)
     torch.testing.assert_close(qkv[:, :Hq * D].float().cpu(), qkv0[:, :Hq * D].float(),
                                atol=2e-2, rtol=2e-2)
     torch.testing.assert_close(kc.cpu().float(), kc0.float(), atol=2e-2, rtol=2e-2)
@@ -92,7 +111,7 @@ def _random_tables(B, ctxs, NB, BS=32):
 
 
 @pytest.mark.parametrize("Hq,Hkv,D", [(32, 8, 128), (8, 1, 128), (64, 8, 128), (16, 16, 64),
-                                     (28, 4, 128), (14, 2, 64)])
+                                     (28, 4, 128), (14, 2, 64), (24, 8, 128)])
 @pytest.mark.parametrize("ctxs", [[1, 17, 32, 33, 500], [1024, 2047, 3000], [5000]])
 def test_paged_decode(Hq, Hkv, D, ctxs):
     B = len(ctxs)
@@ -110,7 +129,7 @@ def test_paged_decode(Hq, Hkv, D, ctxs):
 
 
 @pytest.mark.parametrize("Hq,Hkv,D", [(32, 8, 128), (8, 1, 128), (12, 12, 64), (4, 4, 128),
-                                     (28, 4, 128), (7, 1, 64)])
+                                     (28, 4, 128), (7, 1, 64), (24, 8, 128)])
 def test_paged_prefill_varlen_with_prefix(Hq, Hkv, D):
     qlens = [1, 70, 33, 256]
     prefix = [0, 40, 0, 100]

@@ -141,3 +141,18 @@ def test_qwen_loader_roundtrip_with_bias(tmp_path):
     a = load_llama_weights(str(tmp_path), cfg, "cpu")
     for la, lb in zip(a["layers"], m.w["layers"]):
         assert torch.equal(la["bqkv"], lb["bqkv"]) and torch.equal(la["wqkv"], lb["wqkv"])
+
+
+def test_qwen3_loader_roundtrip_and_tp_shards(tmp_path):
+    cfg = mc.resolve("tiny-qwen3")
+    m = LlamaModel(cfg, "cpu", seed=9)
+    save_hf_llama(m.w, cfg, str(tmp_path))
+    hf = mc.from_hf_config(str(tmp_path / "config.json"))
+    assert hf.qk_norm and not hf.qkv_bias and hf.family == "qwen3"
+    for size in (1, 2):
+        for rank in range(size):
+            a = load_llama_weights(str(tmp_path), cfg, "cpu", rank, size)
+            b = shard_llama(m.w, cfg, rank, size)
+            for la, lb in zip(a["layers"], b["layers"]):
+                assert set(la) == set(lb)
+                assert torch.equal(la["q_norm"], lb["q_norm"]) and torch.equal(la["wqkv"], lb["wqkv"])
