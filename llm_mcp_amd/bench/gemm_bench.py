@@ -32,20 +32,25 @@ def main(argv=None):
     ap.add_argument("--ms", default="64,128,256,2048,16384")
     ap.add_argument("--model", default="llama", choices=["llama", "nomic"])
     ap.add_argument("--ours", action="store_true")
+    ap.add_argument("--impls", default="128,256x256,256x128")
     a = ap.parse_args(argv)
     from llm_mcp_amd import ops
     shapes = LLAMA8B if a.model == "llama" else NOMIC
     for M in [int(x) for x in a.ms.split(",")]:
         for N, K in shapes:
-            x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
-            w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * K ** -0.5
+            x = torch.rand(M, K, device="cuda", dtype=torch.bfloat16) * 2 - 1
+            w = (torch.rand(N, K, device="cuda", dtype=torch.bfloat16) * 2 - 1) * K ** -0.5
             t = timeit(lambda: F.linear(x, w))
             rec = {"M": M, "N": N, "K": K, "hipblaslt_us": round(t, 1),
                    "hipblaslt_tflops": round(2 * M * N * K / t / 1e6, 1),
                    "hipblaslt_weight_tbs": round(N * K * 2 / t / 1e6, 2)}
             if a.ours and ops.gemm_nt_supported(N, K):
-                t2 = timeit(lambda: ops.gemm_nt(x, w))
-                rec.update(ours_us=round(t2, 1), ours_tflops=round(2 * M * N * K / t2 / 1e6, 1))
+                for impl in a.impls.split(","):
+                    if impl.startswith("256") and N % 256 and impl == "256x256":
+                        continue
+                    t2 = timeit(lambda: ops.gemm_nt(x, w, impl=impl))
+                    rec[f"ours{impl}_us"] = round(t2, 1)
+                    rec[f"ours{impl}_tflops"] = round(2 * M * N * K / t2 / 1e6, 1)
             print(json.dumps(rec), flush=True)
 
 
