@@ -32,7 +32,6 @@ def main(argv=None):
     ap.add_argument("--ms", default="64,128,256,2048,16384")
     ap.add_argument("--model", default="llama", choices=["llama", "nomic"])
     ap.add_argument("--ours", action="store_true")
-    ap.add_argument("--impls", default="128,256x256,256x128")
     a = ap.parse_args(argv)
     from llm_mcp_amd import ops
     shapes = LLAMA8B if a.model == "llama" else NOMIC
@@ -45,12 +44,8 @@ def main(argv=None):
                    "hipblaslt_tflops": round(2 * M * N * K / t / 1e6, 1),
                    "hipblaslt_weight_tbs": round(N * K * 2 / t / 1e6, 2)}
             if a.ours and ops.gemm_nt_supported(N, K):
-                for impl in a.impls.split(","):
-                    if impl.startswith("256") and N % 256 and impl == "256x256":
-                        continue
-                    t2 = timeit(lambda: ops.gemm_nt(x, w, impl=impl))
-                    rec[f"ours{impl}_us"] = round(t2, 1)
-                    rec[f"ours{impl}_tflops"] = round(2 * M * N * K / t2 / 1e6, 1)
+                t2 = timeit(lambda: ops.gemm_nt(x, w))
+                rec.update(ours_us=round(t2, 1), ours_tflops=round(2 * M * N * K / t2 / 1e6, 1))
             print(json.dumps(rec), flush=True)
 
 

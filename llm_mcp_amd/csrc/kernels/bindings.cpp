@@ -35,8 +35,6 @@ int gemm_splitk(void*, const void*, const void*, float*, int*, int, int, int, lo
                 int, hipStream_t);
 int gemm_nt(void*, const void*, const void*, const void*, const void*, int, int, int, long, long,
             long, int, hipStream_t);
-int gemm_nt256(void*, const void*, const void*, const void*, const void*, int, int, int, long,
-               long, long, int, int, hipStream_t);
 long ar_region_bytes(long);
 int ar_alloc(void**, long);
 int ar_free(void*);
@@ -181,11 +179,5 @@ PYBIND11_MODULE(_lmx_kernels, m) {
     check(lmx::gemm_nt(P<void>(C), P<void>(A), P<void>(W), P<void>(bias), P<void>(residual), M, N,
                        K, lda, ldw, ldc, act, S(stream)),
           "gemm_nt");
-  });
-  m.def("gemm_nt256", [](uptr C, uptr A, uptr W, uptr bias, uptr residual, int M, int N, int K,
-                         long lda, long ldw, long ldc, int act, int tn, uptr stream) {
-    check(lmx::gemm_nt256(P<void>(C), P<void>(A), P<void>(W), P<void>(bias), P<void>(residual), M,
-                          N, K, lda, ldw, ldc, act, tn, S(stream)),
-          "gemm_nt256");
   });
 }

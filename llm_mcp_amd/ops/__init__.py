@@ -358,15 +358,11 @@ def interleave_gate_up(w: torch.Tensor) -> torch.Tensor:
 
 
 def gemm_nt(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, act: int = 0,
-            residual: torch.Tensor | None = None, out: torch.Tensor | None = None,
-            impl: str = "auto") -> torch.Tensor:
+            residual: torch.Tensor | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
     """act(a @ w^T + bias) (+ residual) on the hand-written MFMA GEMM.
     act=3 (ACT_SWIGLU): ``w`` from ``interleave_gate_up``; returns
     silu(gate) * up with N/2 columns.
-
-    impl: "128" = 128x128 two-buffer kernel (gemm.hip), "256" / "256x128" /
-    "256x256" = 256-row ring kernel (gemm256.hip, tile width picked by wave
-    quantisation or forced), "auto" = the 256-row kernel from M >= 256."""
+    (A 256-row ring variant was measured and dropped: profiles/r1_gemm256_study.md.)"""
     M, K = a.shape
     N = w.shape[0]
     if act == ACT_SWIGLU:
@@ -398,15 +394,6 @@ def gemm_nt(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, 
     if residual is not None:
         _chk(residual.shape == (M, N) and residual.stride(0) == out.stride(0)
              and residual.data_ptr() % 8 == 0, "residual")
-    if impl == "auto":
-        impl = "256" if M >= 256 and K % 32 == 0 else "128"
-    if impl.startswith("256"):
-        variant = {"256": 0, "256x256": 1, "256x128": 2, "256x128w4": 3}[impl]
-        _chk(K % 32 == 0 and N % (256 if variant == 1 else 128) == 0,
-             "gemm_nt256 needs K % 32 == 0 and N % tile width == 0")
-        native().gemm_nt256(_ptr(out), _ptr(a), _ptr(w), _ptr(bias), _ptr(residual), M, N, K,
-                            a.stride(0), w.stride(0), out.stride(0), act, variant, _stream())
-        return out
     native().gemm_nt(_ptr(out), _ptr(a), _ptr(w), _ptr(bias), _ptr(residual), M, N, K,
                      a.stride(0), w.stride(0), out.stride(0), act, _stream())
     return out

@@ -353,42 +353,3 @@ def test_gemm_nt_fused_swiglu(M):
     expect = torch.nn.functional.silu(y[:, :I]) * y[:, I:]
     torch.testing.assert_close(out.float(), expect, atol=2e-2, rtol=2e-2)
 
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("impl", ["256x256", "256x128", "256x128w4"])
-@pytest.mark.parametrize("M,N,K,act", [(256, 256, 64, 0), (300, 768, 768, 1), (4096, 2304, 768, 0),
-                                       (1000, 512, 3072, 2), (77, 1024, 4096, 0)])
-def test_gemm_nt256(impl, M, N, K, act):
-    """256-row ring GEMM (gemm256.hip) vs fp32: ragged M tails, bias, GELU/SiLU,
-    residual, K from 2 to 128 ring stages."""
-    a, w, b = _bf(M, K), _bf(N, K, scale=K ** -0.5), _bf(N)
-    r = _bf(M, N)
-    y = ops.gemm_nt(a, w, b, act, residual=r, impl=impl)
-    expect = ref.gemm_nt(a, w, b, act, r)
-    torch.testing.assert_close(y.float(), expect.float(), atol=3e-2, rtol=3e-2)
-    y2 = ops.gemm_nt(a, w, impl=impl)
-    torch.testing.assert_close(y2.float(), (a.float() @ w.float().t()), atol=3e-2, rtol=3e-2)
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("impl", ["256x256", "256x128", "256x128w4"])
-def test_gemm_nt256_identity_asymmetric(impl):
-    n = 512
-    a = torch.eye(n, device=DEV, dtype=torch.bfloat16)
-    w = torch.arange(n * n, device=DEV, dtype=torch.float32).view(n, n).remainder(97).to(
-        torch.bfloat16)
-    y = ops.gemm_nt(a, w, impl=impl)
-    assert torch.equal(y, w.t().contiguous())
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("impl", ["256x256", "256x128", "256x128w4"])
-@pytest.mark.parametrize("M", [256, 333, 2048])
-def test_gemm_nt256_fused_swiglu(impl, M):
-    K, I = 768, 3072
-    a = torch.randn(M, K, device=DEV).to(torch.bfloat16)
-    w = (torch.randn(2 * I, K, device=DEV) * K ** -0.5).to(torch.bfloat16)
-    out = ops.gemm_nt(a, ops.interleave_gate_up(w), act=ops.ACT_SWIGLU, impl=impl)
-    y = a.float() @ w.float().t()
-    expect = torch.nn.functional.silu(y[:, :I]) * y[:, I:]
-    torch.testing.assert_close(out.float(), expect, atol=2e-2, rtol=2e-2)
