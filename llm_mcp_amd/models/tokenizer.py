@@ -173,11 +173,15 @@ def _content_text(c) -> str:
 
 
 def messages_to_prompt(messages: list[dict]) -> str:
-    """Reference flattening (router.go:379-391): one 'role: content' line per message."""
+    """Reference flattening (router.go:379-391): one 'role: content' line per
+    message; messages with neither role nor content are skipped."""
     lines = []
-    for m in messages:
+    for m in messages or []:
+        content = _content_text(m.get("content", ""))
+        if not m.get("role") and not content:
+            continue
         role = m.get("role") or "user"
-        lines.append(f"{role}: {_content_text(m.get('content', ''))}")
+        lines.append(f"{role}: {content}")
     return "\n".join(lines)
 
 
