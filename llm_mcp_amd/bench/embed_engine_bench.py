@@ -1,4 +1,5 @@
-"""Embedding engine throughput without HTTP (nomic-embed-text bf16): docs of
+"""Embedding engine throughput without HTTP (nomic-embed-text or a BERT
+embedder, bf16): docs of
 --doc-len tokens in batches of --batch-tokens; reports embeddings/s, tok/s."""
 import argparse
 import json
@@ -15,9 +16,11 @@ def main():
     ap.add_argument("--docs", type=int, default=512)
     ap.add_argument("--doc-len", type=int, default=1024)
     ap.add_argument("--batch-tokens", type=int, default=32768)
+    ap.add_argument("--model", default="nomic-embed-text")
     a = ap.parse_args()
-    e = EmbeddingEngine(mc.resolve("nomic-embed-text"), device="cuda",
-                        max_batch_tokens=a.batch_tokens)
+    cfg = mc.resolve(a.model)
+    a.doc_len = min(a.doc_len, cfg.max_position)
+    e = EmbeddingEngine(cfg, device="cuda", max_batch_tokens=a.batch_tokens)
     g = torch.Generator().manual_seed(0)
     docs = [torch.randint(1000, 30000, (a.doc_len,), generator=g).tolist()
             for _ in range(a.docs)]
@@ -29,7 +32,7 @@ def main():
         e.embed_sync(docs[i:i + per])
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    print(json.dumps({"docs": a.docs, "doc_len": a.doc_len, "batch_docs": per,
+    print(json.dumps({"model": a.model, "docs": a.docs, "doc_len": a.doc_len, "batch_docs": per,
                       "emb_per_s": round(a.docs / el, 1),
                       "tok_per_s": round(a.docs * a.doc_len / el, 1)}), flush=True)
 

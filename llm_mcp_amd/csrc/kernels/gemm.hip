@@ -56,6 +56,7 @@ __device__ __forceinline__ float apply_act(float v, int act) {
     return 0.5f * v * (1.f + tanhf(k0 * (v + k1 * v * v * v)));
   }
   if (act == 2) return v / (1.f + __expf(-v));
+  if (act == 4) return 0.5f * v * (1.f + erff(v * 0.70710678118f));   // exact GELU (BERT)
   return v;
 }
 

@@ -18,7 +18,8 @@ from dataclasses import dataclass, field
 import numpy as np
 import torch
 
-from ..models.config import NomicBertConfig
+from ..models.bert import BertModel
+from ..models.config import BertConfig, NomicBertConfig
 from ..models.nomic_bert import NomicBertModel
 
 log = logging.getLogger("lmx.embed")
@@ -36,11 +37,13 @@ class EmbedRequest:
 
 
 class EmbeddingEngine:
-    def __init__(self, cfg: NomicBertConfig, device="cuda", max_batch_tokens: int = 32768,
-                 max_seq_len: int = 2048, seed: int = 0, weights=None):
+    def __init__(self, cfg: NomicBertConfig | BertConfig, device="cuda",
+                 max_batch_tokens: int = 32768, max_seq_len: int = 2048, seed: int = 0,
+                 weights=None):
         self.cfg = cfg
         self.device = torch.device(device)
-        self.model = NomicBertModel(cfg, self.device, seed=seed, weights=weights)
+        model_cls = BertModel if isinstance(cfg, BertConfig) else NomicBertModel
+        self.model = model_cls(cfg, self.device, seed=seed, weights=weights)
         self.max_batch_tokens = max_batch_tokens
         self.max_seq_len = min(max_seq_len, cfg.max_position)
         self._q: queue.SimpleQueue = queue.SimpleQueue()

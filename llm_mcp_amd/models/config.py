@@ -99,6 +99,43 @@ class NomicBertConfig:
         return asdict(self)
 
 
+@dataclass
+class BertConfig:
+    """Classic BERT encoder (absolute positions, post-norm, exact-GELU FFN with
+    biases); ``pooling`` = "cls" (mxbai / bge / arctic) or "mean"."""
+    name: str = "mxbai-embed-large"
+    vocab_size: int = 30522
+    hidden_size: int = 1024
+    intermediate_size: int = 4096
+    num_layers: int = 24
+    num_heads: int = 16
+    head_dim: int = 64
+    ln_eps: float = 1e-12
+    max_position: int = 512
+    type_vocab_size: int = 2
+    pooling: str = "cls"
+    family: str = "bert"
+    kind: str = "embed"
+    embed_dim: int = 1024
+
+    @property
+    def params(self) -> int:
+        d, I, L = self.hidden_size, self.intermediate_size, self.num_layers
+        return (L * (4 * d * d + 2 * d * I + 9 * d + I)
+                + (self.vocab_size + self.max_position + self.type_vocab_size + 2) * d)
+
+    @property
+    def params_b(self) -> float:
+        return round(self.params / 1e9, 3)
+
+    @property
+    def context_k(self) -> int:
+        return max(1, self.max_position // 1024)
+
+    def to_dict(self) -> dict:
+        return asdict(self)
+
+
 _LLAMA32_ROPE = {"rope_type": "llama3", "factor": 32.0, "low_freq_factor": 1.0,
                  "high_freq_factor": 4.0, "original_max_position_embeddings": 8192}
 
@@ -160,6 +197,21 @@ PRESETS: dict[str, object] = {
                          num_layers=2, num_heads=4, num_kv_heads=2, max_position=2048,
                          bos_token_id=506, eos_token_ids=(510,)),
     "nomic-embed-text": NomicBertConfig(),
+    # BERT-architecture embedders (Ollama: mxbai-embed-large, bge-large, snowflake-arctic-embed)
+    "mxbai-embed-large": BertConfig(),
+    "bge-large-en-v1.5": BertConfig(name="bge-large-en-v1.5"),
+    "bge-base-en-v1.5": BertConfig(name="bge-base-en-v1.5", hidden_size=768,
+                                   intermediate_size=3072, num_layers=12, num_heads=12,
+                                   embed_dim=768),
+    "snowflake-arctic-embed-m": BertConfig(name="snowflake-arctic-embed-m", hidden_size=768,
+                                           intermediate_size=3072, num_layers=12, num_heads=12,
+                                           embed_dim=768),
+    "tiny-bert": BertConfig(name="tiny-bert", vocab_size=512, hidden_size=256,
+                            intermediate_size=512, num_layers=2, num_heads=4, head_dim=64,
+                            embed_dim=256, max_position=256),
+    "tiny-bert-mean": BertConfig(name="tiny-bert-mean", vocab_size=512, hidden_size=256,
+                                 intermediate_size=512, num_layers=2, num_heads=2, head_dim=128,
+                                 embed_dim=256, max_position=256, pooling="mean"),
     "tiny-nomic": NomicBertConfig(name="tiny-nomic", vocab_size=512, hidden_size=256,
                                   intermediate_size=512, num_layers=2, num_heads=2, head_dim=128,
                                   embed_dim=256, max_position=2048),
@@ -176,6 +228,10 @@ ALIASES = {
     "nomic-embed-text-v1.5": "nomic-embed-text",
     "qwen2.5:7b": "qwen2.5-7b", "qwen2.5:0.5b": "qwen2.5-0.5b",
     "qwen2.5-7b-instruct": "qwen2.5-7b",
+    "mxbai-embed-large:latest": "mxbai-embed-large", "mxbai-embed-large:335m": "mxbai-embed-large",
+    "mixedbread-ai/mxbai-embed-large-v1": "mxbai-embed-large",
+    "bge-large": "bge-large-en-v1.5", "bge-large:335m": "bge-large-en-v1.5",
+    "snowflake-arctic-embed:110m": "snowflake-arctic-embed-m",
 }
 
 
@@ -219,4 +275,13 @@ def from_hf_config(path: str | Path):
             max_position=cfg.get("n_positions", 8192),
             qkv_bias=cfg.get("qkv_proj_bias", False), mlp_bias=cfg.get("mlp_fc1_bias", False),
             embed_dim=cfg["n_embd"])
+    if arch in ("BertModel", "BertForMaskedLM") or cfg.get("model_type") == "bert":
+        d, H = cfg["hidden_size"], cfg["num_attention_heads"]
+        return BertConfig(
+            name=cfg.get("_name_or_path", "bert"), vocab_size=cfg["vocab_size"], hidden_size=d,
+            intermediate_size=cfg["intermediate_size"], num_layers=cfg["num_hidden_layers"],
+            num_heads=H, head_dim=d // H, ln_eps=cfg.get("layer_norm_eps", 1e-12),
+            max_position=cfg.get("max_position_embeddings", 512),
+            type_vocab_size=cfg.get("type_vocab_size", 2), embed_dim=d,
+            pooling=cfg.get("pooling", "cls"))
     raise ValueError(f"unsupported architecture {arch!r}")

@@ -126,3 +126,27 @@ class NomicBertModel:
             m = self._linear(g, L["w_down"])
             x = ops.layer_norm(m, L["ln2_w"], L["ln2_b"], cfg.ln_eps, residual=h)
         return ops.mean_pool_l2(x, cu, dims or cfg.embed_dim, normalize)
+
+
+def load_nomic_weights(path: str, cfg: NomicBertConfig, device, dtype=torch.bfloat16) -> dict:
+    """HF nomic-embed-text(-v1.5) safetensors -> NomicBertModel weights.
+    The gated MLP computes fc11(x) * silu(fc12(x)) (fc12 is the gate), so the
+    fused projection is [fc12; fc11]."""
+    from .weights import _Reader
+    r = _Reader(path)
+
+    def t(name):
+        return r.rows(name).to(device=device, dtype=dtype).contiguous()
+
+    layers = []
+    for i in range(cfg.num_layers):
+        b = f"encoder.layers.{i}."
+        layers.append({
+            "wqkv": t(b + "attn.Wqkv.weight"), "wo": t(b + "attn.out_proj.weight"),
+            "w_gate_up": torch.cat([t(b + "mlp.fc12.weight"), t(b + "mlp.fc11.weight")]),
+            "w_down": t(b + "mlp.fc2.weight"),
+            "ln1_w": t(b + "norm1.weight"), "ln1_b": t(b + "norm1.bias"),
+            "ln2_w": t(b + "norm2.weight"), "ln2_b": t(b + "norm2.bias")})
+    return {"word": t("embeddings.word_embeddings.weight"),
+            "type": t("embeddings.token_type_embeddings.weight"),
+            "emb_ln_w": t("emb_ln.weight"), "emb_ln_b": t("emb_ln.bias"), "layers": layers}

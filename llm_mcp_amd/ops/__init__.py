@@ -346,6 +346,7 @@ ACT_NONE, ACT_GELU, ACT_SILU = 0, 1, 2
 
 
 ACT_SWIGLU = 3
+ACT_GELU_ERF = 4   # exact (erf) GELU, BERT FFNs
 
 
 def interleave_gate_up(w: torch.Tensor) -> torch.Tensor:

@@ -177,6 +177,8 @@ def gemm_nt(a, w, bias=None, act=0, residual=None):
         y = torch.nn.functional.gelu(y, approximate="tanh")
     elif act == 2:
         y = torch.nn.functional.silu(y)
+    elif act == 4:
+        y = torch.nn.functional.gelu(y)
     if residual is not None:
         y = y + residual.float()
     return y.to(a.dtype)

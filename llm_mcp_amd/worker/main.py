@@ -32,6 +32,8 @@ def build_parser():
     ap.add_argument("--kv-fraction", type=float, default=0.6)
     ap.add_argument("--lease-seconds", type=int, default=int(os.environ.get("WORKER_LEASE_SECONDS", "60")))
     ap.add_argument("--weights", default="", help="safetensors dir of real weights (optional)")
+    ap.add_argument("--embed-weights", default="",
+                    help="safetensors dir of the embedding model (nomic-bert or BERT; optional)")
     ap.add_argument("--tp", type=int, default=1)
     return ap
 
@@ -53,7 +55,14 @@ def main(argv=None):
     engine = embed = None
     if a.embed_model:
         from ..engine.embed_engine import EmbeddingEngine
-        embed = EmbeddingEngine(mc.resolve(a.embed_model), dev)
+        ecfg_e = mc.resolve(a.embed_model)
+        ew = None
+        if a.embed_weights:
+            from ..models.bert import load_bert_weights
+            from ..models.nomic_bert import load_nomic_weights
+            loader = load_bert_weights if isinstance(ecfg_e, mc.BertConfig) else load_nomic_weights
+            ew = loader(a.embed_weights, ecfg_e, dev)
+        embed = EmbeddingEngine(ecfg_e, dev, weights=ew)
     if a.chat_model:
         cfg = mc.resolve(a.chat_model)
         weights = None

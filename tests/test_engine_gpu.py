@@ -66,6 +66,32 @@ def test_nomic_bert_gpu_matches_cpu_reference(preset):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("preset", ["tiny-bert", "tiny-bert-mean", "mxbai-2layer"])
+def test_bert_gpu_matches_cpu_reference(preset):
+    """BERT encoder on the HIP kernels (gemm_nt with fused bias / exact GELU /
+    residual, kv_write, bidirectional paged prefill, LayerNorm, CLS or mean
+    pooling) vs the same weights on the fp32-reference CPU path."""
+    import dataclasses
+
+    from llm_mcp_amd.models import config as mc
+    from llm_mcp_amd.models.bert import BertModel
+    cfg = mc.resolve(preset) if preset.startswith("tiny") else \
+        dataclasses.replace(mc.resolve("mxbai-embed-large"), num_layers=2)
+    g = BertModel(cfg, "cuda", seed=3)
+    wc = {k: (v.cpu() if hasattr(v, "cpu") else [{kk: vv.cpu() for kk, vv in L.items()}
+                                                  for L in v]) for k, v in g.w.items()}
+    c = BertModel(cfg, "cpu", weights=wc)
+    lens = [30, 1, 39, 70]
+    ids = torch.randint(0, 500, (sum(lens),), dtype=torch.int32)
+    cu = torch.tensor([0] + list(torch.cumsum(torch.tensor(lens), 0)), dtype=torch.int32)
+    a = g.forward(ids.cuda(), cu.cuda(), lens).cpu()
+    b = c.forward(ids, cu, lens)
+    cos = torch.nn.functional.cosine_similarity(a, b, dim=-1)
+    assert float(cos.min()) > 0.999, cos
+    assert float((a - b).abs().max()) < 2e-2
+
+
+@pytest.mark.gpu
 def test_qwen2_group7_on_gpu_kernels():
     e = LLMEngine(EngineConfig(model="tiny-qwen", max_num_seqs=8, max_batched_tokens=128,
                                max_model_len=512, kv_cache_gb=0.05), device="cuda")

@@ -257,7 +257,7 @@ def test_mean_pool_l2_matryoshka():
 
 @pytest.mark.parametrize("M,N,K", [(1, 128, 64), (77, 768, 768), (256, 2304, 768),
                                    (1000, 3072, 768), (130, 768, 3072), (512, 4096, 4096)])
-@pytest.mark.parametrize("act", [0, 1, 2])
+@pytest.mark.parametrize("act", [0, 1, 2, 4])
 def test_gemm_nt(M, N, K, act):
     a, w, b = _bf(M, K), _bf(N, K, scale=K ** -0.5), _bf(N)
     r = _bf(M, N)
