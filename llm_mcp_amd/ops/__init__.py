@@ -469,17 +469,21 @@ def gemm_splitk(a: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = Non
 
 
 def splitk_preferred(M: int, N: int, K: int) -> bool:
-    """Measured dispatch (profiles/r1_splitk_gemm.md, cold weights on MI355X):
-    the split-K kernel beats hipBLASLt for wide gate/up projections at
-    M <= 32, for the long-K down projection at 48 <= M <= 160 and for
-    square projections at M <= 16; hipBLASLt wins elsewhere."""
+    """Measured dispatch (profiles/r1_splitk_gemm.md, cold weights on MI355X,
+    Llama-3-8B and -70B shapes): the split-K kernel beats hipBLASLt for wide
+    d=4096 gate/up projections at M <= 32, for long-K down projections
+    (K >= 16384 at 48 <= M <= 256, K 8192-16384 at 48 <= M <= 160) and for
+    d=4096 square projections at M <= 16; hipBLASLt wins elsewhere (incl. the
+    70B QKV / O projections at K = 8192)."""
     if not gemm_splitk_supported(M, N, K):
         return False
-    if N >= 16384 and K <= 8192:
+    if N >= 16384 and K <= 4096:
         return M <= 32
-    if K >= 8192:
+    if K >= 16384:
+        return 48 <= M <= 256
+    if K > 8192:
         return 48 <= M <= 160
-    if N == K:
+    if N == K and K <= 4096:
         return M <= 16
     return False
 
