@@ -12,7 +12,9 @@ Contract kept from the reference (core/internal/api/handlers.go:2087-2587):
   * non-stream: ``chat.completion`` with ``usage``.
 Defect fixed: ``max_tokens``, ``top_p`` and ``stop`` are honoured (the
 reference parsed and dropped them, handlers.go:2333-2340); ``top_k``,
-``seed``, ``logprobs`` and ``stream_options.include_usage`` are supported.
+``seed``, ``logprobs``, ``stream_options.include_usage`` and the OpenAI
+``presence_penalty`` / ``frequency_penalty`` (plus ``repetition_penalty`` and
+Ollama's ``options.repeat_penalty`` / ``repeat_last_n``) are supported.
 """
 from __future__ import annotations
 
@@ -51,7 +53,18 @@ def sampling_from_body(body: dict, max_len_left: int) -> SamplingParams:
         stop=[str(s) for s in stop][:16],
         ignore_eos=bool(body.get("ignore_eos", False)),
         seed=body.get("seed", opts.get("seed")),
-        logprobs=bool(body.get("logprobs", False)))
+        logprobs=bool(body.get("logprobs", False)),
+        presence_penalty=float(f("presence_penalty", opts.get("presence_penalty", 0.0))),
+        frequency_penalty=float(f("frequency_penalty", opts.get("frequency_penalty", 0.0))),
+        repetition_penalty=float(f("repetition_penalty", opts.get("repeat_penalty", 1.0))),
+        penalty_last_n=penalty_window(opts.get("repeat_last_n", 64)))
+
+
+def penalty_window(n) -> int:
+    """Ollama repeat_last_n: -1 = whole context (capped at the kernel's 64-token
+    window), 0 = off."""
+    n = int(n)
+    return 64 if n < 0 else min(n, 64)
 
 
 class ChatHandler:

@@ -28,6 +28,8 @@ int paged_prefill(const void*, long, const void*, const void*, const int*, int, 
 int sample(const void*, int, long, int, int, const float*, const int*, const float*,
            const uint64_t*, const int*, int*, float*, int, hipStream_t);
 int glu(void*, const void*, long, int, int, hipStream_t);
+int apply_penalties(void*, long, int, int, const int*, const int*, const float*, const int*, int,
+                    hipStream_t);
 int embed_gather(void*, const void*, const int*, int, int, int, int, hipStream_t);
 int mean_pool_l2(float*, const void*, const int*, int, int, int, int, hipStream_t);
 int bias_act(void*, const void*, long, int, int, hipStream_t);
@@ -173,6 +175,12 @@ PYBIND11_MODULE(_lmx_kernels, m) {
     check(lmx::allreduce(P<void>(out), P<void>(inp), nbytes, rank, world, peers.data(), slot_bytes,
                          two_shot, blocks, spin_max, S(stream)),
           "allreduce");
+  });
+  m.def("apply_penalties", [](uptr logits, long ld, int B, int V, uptr win, uptr ngen, uptr pen,
+                              uptr on, int W, uptr stream) {
+    check(lmx::apply_penalties(P<void>(logits), ld, B, V, P<const int>(win), P<const int>(ngen),
+                               P<const float>(pen), P<const int>(on), W, S(stream)),
+          "apply_penalties");
   });
   m.def("gemm_nt", [](uptr C, uptr A, uptr W, uptr bias, uptr residual, int M, int N, int K,
                       long lda, long ldw, long ldc, int act, uptr stream) {

@@ -247,4 +247,49 @@ int sample(const void* logits, int logits_bf16, long stride, int B, int V, const
   return (int)hipGetLastError();
 }
 
+// --------------------------------------------------------------------------
+// Repetition / presence / frequency penalties applied to the logits in place,
+// before sampling.  One wave per sampled row, lane i owns entry i of the row's
+// right-aligned window of the last W (<= 64) context tokens (-1 = empty); the
+// last ngen entries are generated tokens.  The lane holding the FIRST
+// occurrence of a token applies, once:
+//   repetition (HF / Ollama repeat_penalty, over every window token):
+//       l = l > 0 ? l / r : l * r
+//   presence / frequency (OpenAI, over the generated part of the window):
+//       l -= frequency * count + presence * (count > 0)
+// `on` (device flag, may be null) lets a captured graph skip the kernel for
+// steps without penalised rows.
+__global__ void __launch_bounds__(64) penalty_kernel(bf16_t* __restrict__ logits, long ld, int V,
+                                                     const int* __restrict__ win,
+                                                     const int* __restrict__ ngen,
+                                                     const float* __restrict__ pen,
+                                                     const int* __restrict__ on, int W) {
+  if (on != nullptr && on[0] == 0) return;
+  __shared__ int ids[64];
+  const int row = blockIdx.x, lane = threadIdx.x;
+  const int t = lane < W ? win[(long)row * W + lane] : -1;
+  ids[lane] = t;
+  __syncthreads();
+  if (t < 0 || t >= V) return;
+  for (int j = 0; j < lane; ++j)
+    if (ids[j] == t) return;                   // not the first occurrence
+  const int g0 = W - ngen[row];
+  int cnt = 0;
+  for (int j = lane > g0 ? lane : g0; j < W; ++j) cnt += ids[j] == t;
+  const float rep = pen[3 * row], pres = pen[3 * row + 1], freq = pen[3 * row + 2];
+  bf16_t* p = logits + (long)row * ld + t;
+  float l = bf2f(*p);
+  if (rep != 1.f) l = l > 0.f ? l / rep : l * rep;
+  l -= freq * (float)cnt + (cnt > 0 ? pres : 0.f);
+  *p = f2bf(l);
+}
+
+int apply_penalties(void* logits, long ld, int B, int V, const int* win, const int* ngen,
+                    const float* pen, const int* on, int W, hipStream_t stream) {
+  if (B <= 0) return 0;
+  if (W <= 0 || W > 64) return -1;
+  penalty_kernel<<<dim3(B), dim3(64), 0, stream>>>((bf16_t*)logits, ld, V, win, ngen, pen, on, W);
+  return (int)hipGetLastError();
+}
+
 }  // namespace lmx

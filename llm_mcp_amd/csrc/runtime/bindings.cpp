@@ -66,6 +66,8 @@ PYBIND11_MODULE(_lmx_runtime, m) {
            py::arg("temperature") = 1.f, py::arg("top_k") = 0, py::arg("top_p") = 1.f,
            py::arg("seed") = 0)
       .def("abort", &Scheduler::abort)
+      .def("set_penalties", &Scheduler::set_penalties, py::arg("id"), py::arg("repetition"),
+           py::arg("presence"), py::arg("frequency"), py::arg("last_n"))
       .def("schedule", [](Scheduler& s, int q_per_tile) {
         const StepPlan& p = s.schedule(q_per_tile);
         py::dict d;
@@ -85,6 +87,13 @@ PYBIND11_MODULE(_lmx_runtime, m) {
         d["seeds"] = to_np(p.sample_seed);
         d["offs"] = to_np(p.sample_off);
         d["prefill_tiles"] = to_np(p.prefill_tiles);
+        d["any_penalty"] = p.any_penalty;
+        if (p.any_penalty) {
+          d["pen_window"] = to_np(p.pen_window);
+          d["pen_ngen"] = to_np(p.pen_ngen);
+          d["pen_params"] = to_np(p.pen_params);
+        }
+        d["pen_window_len"] = kPenWindow;
         d["num_decode"] = p.num_decode;
         d["max_blocks"] = p.max_blocks;
         d["num_tokens"] = p.num_tokens;

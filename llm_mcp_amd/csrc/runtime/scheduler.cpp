@@ -46,6 +46,19 @@ void Scheduler::add(int64_t id, const std::vector<int32_t>& prompt, int max_new,
   waiting_.insert(it, raw);
 }
 
+bool Scheduler::set_penalties(int64_t id, float repetition, float presence, float frequency,
+                              int last_n) {
+  auto it = seqs_.find(id);
+  if (it == seqs_.end()) return false;
+  if (!(repetition > 0.f)) throw std::invalid_argument("repetition penalty must be > 0");
+  Seq* s = it->second.get();
+  s->rep_pen = repetition;
+  s->pres_pen = presence;
+  s->freq_pen = frequency;
+  s->pen_last_n = std::max(0, std::min(last_n, kPenWindow));
+  return true;
+}
+
 const Seq* Scheduler::get(int64_t id) const {
   auto it = seqs_.find(id);
   return it == seqs_.end() ? nullptr : it->second.get();
@@ -93,6 +106,8 @@ const StepPlan& Scheduler::schedule(int q_per_tile) {
   p.sample_temp.clear(); p.sample_topp.clear(); p.sample_topk.clear(); p.sample_off.clear();
   p.sample_seed.clear();
   p.prefill_tiles.clear(); p.preempted.clear();
+  p.any_penalty = false;
+  p.pen_window.clear(); p.pen_ngen.clear(); p.pen_params.clear();
   p.num_decode = 0; p.num_tokens = 0; p.num_prefill_tokens = 0; p.max_context = 0;
   p.max_blocks = max_blocks_;
   plan_seqs_.clear();
@@ -169,6 +184,7 @@ const StepPlan& Scheduler::schedule(int q_per_tile) {
       p.sample_topp.push_back(s->top_p);
       p.sample_seed.push_back(s->seed);
       p.sample_off.push_back(s->num_generated);
+      p.any_penalty |= s->penalized();
     }
     if (is_prefill) {
       p.num_prefill_tokens += n;
@@ -183,6 +199,24 @@ const StepPlan& Scheduler::schedule(int q_per_tile) {
   p.num_decode = (int)decodes.size();
   int j = 0;
   for (Seq* s : prefills) emit(s, true, j++);
+  if (p.any_penalty) {
+    const size_t n = p.sample_rows.size();
+    p.pen_window.assign(n * kPenWindow, -1);
+    p.pen_ngen.assign(n, 0);
+    p.pen_params.assign(n * 3, 0.f);
+    for (size_t i = 0; i < n; ++i) {
+      const Seq* s = plan_seqs_[p.sample_seq[i]];
+      p.pen_params[3 * i] = 1.f;
+      if (!s->penalized()) continue;
+      const int len = (int)s->tokens.size(), w = std::min(s->pen_last_n, len);
+      std::copy(s->tokens.end() - w, s->tokens.end(),
+                p.pen_window.begin() + (i + 1) * kPenWindow - w);
+      p.pen_ngen[i] = std::min(w, s->num_generated);
+      p.pen_params[3 * i] = s->rep_pen;
+      p.pen_params[3 * i + 1] = s->pres_pen;
+      p.pen_params[3 * i + 2] = s->freq_pen;
+    }
+  }
   return p;
 }
 

@@ -46,10 +46,17 @@ struct Seq {
   float temperature = 1.f, top_p = 1.f;
   int top_k = 0;
   int64_t seed = 0;
+  // repetition (HF / Ollama repeat_penalty), presence and frequency (OpenAI)
+  // penalties over the last pen_last_n context tokens (<= kPenWindow)
+  float rep_pen = 1.f, pres_pen = 0.f, freq_pen = 0.f;
+  int pen_last_n = 0;
+  bool penalized() const { return pen_last_n > 0 && (rep_pen != 1.f || pres_pen != 0.f || freq_pen != 0.f); }
   int status = WAITING;
   int finish = FR_NONE;
   int scheduled = 0;            // tokens scheduled in the current plan
 };
+
+constexpr int kPenWindow = 64;   // token window of the penalty kernel (one wave per row)
 
 struct StepPlan {
   // per token rows (T)
@@ -64,6 +71,12 @@ struct StepPlan {
   std::vector<int32_t> sample_topk, sample_off;    // sample_off = tokens generated so far
   std::vector<int64_t> sample_seed;
   std::vector<int32_t> prefill_tiles;              // (prefill-seq index, q_start) pairs
+  // penalties (filled only when some sampled row is penalised): per sample
+  // row the last kPenWindow context tokens right-aligned (-1 padded), how
+  // many of them are generated tokens, and (repetition, presence, frequency)
+  bool any_penalty = false;
+  std::vector<int32_t> pen_window, pen_ngen;
+  std::vector<float> pen_params;
   int num_decode = 0;                              // first num_decode sequences have qlen 1
   int max_blocks = 0;                              // row width of block_tables (this plan)
   int num_tokens = 0;
@@ -81,6 +94,7 @@ class Scheduler {
            const std::vector<int32_t>& stop_ids, bool ignore_eos, int priority,
            float temperature = 1.f, int top_k = 0, float top_p = 1.f, int64_t seed = 0);
   bool abort(int64_t id);
+  bool set_penalties(int64_t id, float repetition, float presence, float frequency, int last_n);
   // q_per_tile: queries per prefill workgroup (64 / G for the paged prefill kernel)
   const StepPlan& schedule(int q_per_tile);
   // sampled[i] is the token for plan.sample_rows[i]; returns finished (id, reason)

@@ -52,6 +52,18 @@ class SamplingParams:
     ignore_eos: bool = False
     seed: int | None = None
     logprobs: bool = False
+    # repetition (HF / Ollama repeat_penalty) over the last penalty_last_n
+    # context tokens; presence / frequency (OpenAI) over the generated tokens
+    # inside that window (window <= 64 tokens, the penalty kernel's wave)
+    repetition_penalty: float = 1.0
+    presence_penalty: float = 0.0
+    frequency_penalty: float = 0.0
+    penalty_last_n: int = 64
+
+    def penalized(self) -> bool:
+        return self.penalty_last_n > 0 and (self.repetition_penalty != 1.0 or
+                                            self.presence_penalty != 0.0 or
+                                            self.frequency_penalty != 0.0)
 
 
 @dataclass
@@ -119,6 +131,8 @@ class _Packer:
             out[name] = self.dev[o:o + n].view(_TORCH_DT[np.dtype(dt)]).view(shape)
         return out
 
+
+PEN_WINDOW = 64   # kPenWindow of csrc/runtime/scheduler.h (one wave per row in the kernel)
 
 _PLAN_KEY = {"ids": "input_ids", "pos": "positions", "ctx": "context_lens"}
 
@@ -213,7 +227,7 @@ class LLMEngine:
                                              self.device)
         T = ecfg.max_batched_tokens + ecfg.max_num_seqs
         cap = 4 * (4 * T + ecfg.max_num_seqs * (self.max_blocks + 8) + 2 * T) + 16 * 64 + \
-            8 * ecfg.max_num_seqs * 4
+            8 * ecfg.max_num_seqs * 4 + 4 * ecfg.max_num_seqs * (PEN_WINDOW + 4)
         self.packer = _Packer(cap, self.device)
         self.event_sink = event_sink
         self._intake: queue.SimpleQueue = queue.SimpleQueue()
@@ -293,10 +307,18 @@ class LLMEngine:
             ("ctx", np.int32, (Bmax,)), ("bt", np.int32, (Bmax, self.max_blocks)),
             ("temp", np.float32, (Bmax,)), ("topk", np.int32, (Bmax,)),
             ("topp", np.float32, (Bmax,)), ("seeds", np.int64, (Bmax,)),
-            ("offs", np.int32, (Bmax,))], dev)
+            ("offs", np.int32, (Bmax,)), ("pen_on", np.int32, (1,))], dev)
+        # penalty inputs: uploaded only on steps with penalised rows (the
+        # captured kernel returns at once when pen_on == 0)
+        pmeta = _FixedMeta([("win", np.int32, (Bmax, PEN_WINDOW)), ("ngen", np.int32, (Bmax,)),
+                            ("pen", np.float32, (Bmax, 3))], dev)
+        pmeta.h["win"][:] = -1; pmeta.h["ngen"][:] = 0; pmeta.h["pen"][:] = 0
+        pmeta.upload()
+        self._pmeta = pmeta
         h = meta.h
         h["ids"][:] = 0; h["pos"][:] = 0; h["slots"][:] = -1; h["ctx"][:] = 1; h["bt"][:] = 0
         h["temp"][:] = 0; h["topk"][:] = 0; h["topp"][:] = 1; h["seeds"][:] = 0; h["offs"][:] = 0
+        h["pen_on"][:] = 0
         meta.upload()
         self._gmeta = meta
         g = dict(meta.d)
@@ -321,6 +343,9 @@ class LLMEngine:
                 logits = self.model.forward(inp, self.k_caches, self.v_caches, ws,
                                             self.ecfg.part_tokens)
                 if self.is_leader:
+                    pd = pmeta.d
+                    ops.apply_penalties(logits, pd["win"][:B], pd["ngen"][:B], pd["pen"][:B],
+                                        on=g["pen_on"])
                     ops.sample(logits, g["temp"][:B], g["topk"][:B], g["topp"][:B],
                                g["seeds"][:B], g["offs"][:B], g["tok"][:B], g["lp"][:B])
 
@@ -449,6 +474,10 @@ class LLMEngine:
                 self.sched.add(req.id, list(req.prompt_ids), int(p.max_tokens), stop_ids,
                                bool(p.ignore_eos), int(req.priority), float(p.temperature),
                                int(p.top_k), float(p.top_p), int(seed))
+                if p.penalized():
+                    self.sched.set_penalties(req.id, float(p.repetition_penalty),
+                                             float(p.presence_penalty),
+                                             float(p.frequency_penalty), int(p.penalty_last_n))
                 self._reqs[req.id] = req
             except Exception as e:
                 req.finished = True
@@ -600,20 +629,28 @@ class LLMEngine:
         S = len(plan["seq_ids"])
         mb = plan["max_blocks"]
         rows = plan["sample_rows"].astype(np.int64)
-        d = self.packer.pack([
+        items = [
             ("ids", plan["input_ids"]), ("pos", plan["positions"]), ("slots", plan["slots"]),
             ("ctx", plan["context_lens"]), ("cu", plan["cu_q"]),
             ("bt", plan["block_tables"].reshape(S, mb)),
             ("tiles", plan["prefill_tiles"] if len(plan["prefill_tiles"]) else
              np.zeros(2, np.int32)),
             ("rows", rows), ("temp", plan["temp"]), ("topk", plan["topk"]),
-            ("topp", plan["topp"]), ("seeds", plan["seeds"]), ("offs", plan["offs"])])
+            ("topp", plan["topp"]), ("seeds", plan["seeds"]), ("offs", plan["offs"])]
+        pen = bool(plan.get("any_penalty")) and self.is_leader
+        if pen:   # one pack, one upload: the pinned staging buffer is reused per call
+            N = len(plan["sample_rows"])
+            items += [("win", plan["pen_window"].reshape(N, PEN_WINDOW)),
+                      ("ngen", plan["pen_ngen"]), ("pen", plan["pen_params"].reshape(N, 3))]
+        d = self.packer.pack(items)
         inp = StepInputs(d["ids"], d["pos"], d["slots"], plan["num_decode"], d["bt"], d["ctx"],
                          d["cu"], d["tiles"], d["rows"], T, S)
         ws = self.decode_ws
         logits = self.model.forward(inp, self.k_caches, self.v_caches, ws, self.ecfg.part_tokens)
         if not self.is_leader:
             return None, None
+        if pen:
+            ops.apply_penalties(logits, d["win"], d["ngen"], d["pen"])
         return ops.sample(logits, d["temp"], d["topk"], d["topp"], d["seeds"], d["offs"])
 
     def _run_graph(self, plan, B):
@@ -630,6 +667,15 @@ class LLMEngine:
         # never read (and always hold valid page ids)
         h["bt"][:n, :mb] = plan["block_tables"].reshape(n, mb)
         h["bt"][n:B, 0] = 0
+        pen = bool(plan.get("any_penalty")) and self.is_leader
+        h["pen_on"][0] = int(pen)
+        if pen:
+            ph = self._pmeta.h
+            ph["win"][:n] = plan["pen_window"].reshape(n, -1)
+            ph["win"][n:B] = -1
+            ph["ngen"][:n] = plan["pen_ngen"]
+            ph["pen"][:n] = plan["pen_params"].reshape(n, 3)
+            self._pmeta.upload()
         self._gmeta.upload()
         self.graphs[B]["graph"].replay()
         return g["tok"][:B], g["lp"][:B]

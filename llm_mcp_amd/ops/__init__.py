@@ -278,6 +278,27 @@ def sample(logits: torch.Tensor, temperature: torch.Tensor, top_k: torch.Tensor,
     return out_tok, out_lp
 
 
+def apply_penalties(logits: torch.Tensor, window: torch.Tensor, ngen: torch.Tensor,
+                    pen: torch.Tensor, on: torch.Tensor | None = None) -> torch.Tensor:
+    """Repetition / presence / frequency penalties on logits [B, V] in place
+    (K6 prologue).  window int32 [B, W<=64] right-aligned context tokens (-1
+    padded), ngen int32 [B] generated tokens at its tail, pen fp32 [B, 3] =
+    (repetition, presence, frequency); ``on`` int32 [1] device flag."""
+    B, V = logits.shape
+    if not logits.is_cuda:
+        if on is not None and int(on[0]) == 0:
+            return logits
+        return ref.apply_penalties(logits, window, ngen, pen)
+    _chk(logits.dtype == torch.bfloat16 and logits.stride(1) == 1, "bf16 logits rows")
+    _chk(window.dtype == torch.int32 and window.is_contiguous() and window.shape[0] >= B
+         and window.shape[1] <= 64, "penalty window")
+    _chk(ngen.dtype == torch.int32 and pen.dtype == torch.float32 and pen.is_contiguous(),
+         "penalty params")
+    native().apply_penalties(_ptr(logits), logits.stride(0), B, V, _ptr(window), _ptr(ngen),
+                             _ptr(pen), _ptr(on), window.shape[1], _stream())
+    return logits
+
+
 # ------------------------------------------------------------ elementwise ---
 def silu_mul(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     if not x.is_cuda:

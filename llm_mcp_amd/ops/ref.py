@@ -228,3 +228,25 @@ def sample(logits, temperature, top_k, top_p, seeds, offsets):
         toks[b] = j
         lps[b] = float(logp[j])
     return toks, lps
+
+
+def apply_penalties(logits, window, ngen, pen):
+    """In place: repetition (every window token), presence / frequency (counts
+    over the generated tail of the right-aligned window)."""
+    B, W = window.shape
+    for b in range(B):
+        ids = window[b].tolist()
+        g0 = W - int(ngen[b])
+        rep, pres, freq = (float(v) for v in pen[b])
+        seen = set()
+        for i, t in enumerate(ids):
+            if t < 0 or t in seen or t >= logits.shape[1]:
+                continue
+            seen.add(t)
+            cnt = sum(1 for j in range(max(i, g0), W) if ids[j] == t)
+            x = float(logits[b, t])
+            if rep != 1.0:
+                x = x / rep if x > 0 else x * rep
+            x -= freq * cnt + (pres if cnt > 0 else 0.0)
+            logits[b, t] = x
+    return logits

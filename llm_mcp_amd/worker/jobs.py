@@ -44,19 +44,31 @@ def calc_cost(payload: dict, tokens_in: int, tokens_out: int) -> str:
     return f"{pin / 1e6 * tokens_in + pout / 1e6 * tokens_out:.5f}$"
 
 
-def sampling_from_payload(payload: dict, default_max: int = 512) -> SamplingParams:
+def sampling_from_payload(payload: dict, default_max: int = 512,
+                          ollama_defaults: bool = False) -> SamplingParams:
+    """Job payload (+ Ollama ``options``) -> SamplingParams.  ``ollama.*``
+    kinds get Ollama's generation defaults (repeat_penalty 1.1 over the last
+    64 tokens), which the reference's jobs received from their Ollama
+    backend (worker/llm_worker/main.py:222-243)."""
     o = dict(payload.get("options") or {})
-    for k in ("temperature", "top_p", "top_k", "max_tokens", "stop", "seed"):
+    for k in ("temperature", "top_p", "top_k", "max_tokens", "stop", "seed", "presence_penalty",
+              "frequency_penalty", "repetition_penalty"):
         if payload.get(k) is not None:
             o.setdefault(k, payload[k])
     stop = o.get("stop") or []
     if isinstance(stop, str):
         stop = [stop]
     max_tokens = o.get("max_tokens", o.get("num_predict", default_max))
+    rep = o.get("repetition_penalty", o.get("repeat_penalty", 1.1 if ollama_defaults else 1.0))
+    last_n = int(o.get("repeat_last_n", 64))
     return SamplingParams(temperature=float(o.get("temperature", 0.8)),
                           top_p=float(o.get("top_p", 1.0)), top_k=int(o.get("top_k", 0)),
                           max_tokens=max(1, int(max_tokens)), stop=list(stop),
-                          seed=o.get("seed"), ignore_eos=bool(o.get("ignore_eos", False)))
+                          seed=o.get("seed"), ignore_eos=bool(o.get("ignore_eos", False)),
+                          repetition_penalty=float(rep),
+                          presence_penalty=float(o.get("presence_penalty", 0.0)),
+                          frequency_penalty=float(o.get("frequency_penalty", 0.0)),
+                          penalty_last_n=64 if last_n < 0 else min(last_n, 64))
 
 
 class JobRunner:
@@ -134,7 +146,7 @@ class JobRunner:
         left = m.max_model_len - len(ids) - 1
         if left < 1:
             raise JobError("context_length_exceeded")
-        sp = sampling_from_payload(payload)
+        sp = sampling_from_payload(payload, ollama_defaults=kind.startswith("ollama."))
         sp.max_tokens = min(sp.max_tokens, left)
         text, n_out, ttft, el, fin = await self._generate(m, ids, sp)
         thinking = ""

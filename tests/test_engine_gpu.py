@@ -4,7 +4,7 @@ import pytest
 import torch
 
 from llm_mcp_amd import ops
-from llm_mcp_amd.engine.engine import EngineConfig, LLMEngine, SamplingParams
+from llm_mcp_amd.engine.engine import EngineConfig, GenRequest, LLMEngine, SamplingParams
 from tests.dense_ref import assert_greedy_consistent
 
 pytestmark = pytest.mark.gpu
@@ -111,3 +111,38 @@ def test_qwen3_qk_norm_on_gpu_kernels():
     for p, o in zip(prompts, outs):
         assert len(o) == 6
         assert_greedy_consistent(e.model, p, o)
+
+
+@pytest.mark.gpu
+def test_penalties_in_graph_and_eager():
+    """Penalised rows inside the captured decode graph (penalty block uploaded,
+    pen_on flag) and on the eager path: greedy tokens never repeat one of the
+    last 64 context tokens; unpenalised rows in the same batch are unchanged."""
+    e = LLMEngine(EngineConfig(model="tiny-llama", max_num_seqs=8, max_batched_tokens=256,
+                               max_model_len=512, kv_cache_gb=0.05), device="cuda")
+    assert e.graphs, "decode graphs expected"
+    prompts = [list(range(5, 45)), [9] * 20 + list(range(100, 120))]
+    base = e.generate(prompts, SamplingParams(temperature=0, max_tokens=40, ignore_eos=True))
+    pen = SamplingParams(temperature=0, max_tokens=40, ignore_eos=True, repetition_penalty=1e4,
+                         presence_penalty=1e3, penalty_last_n=64)
+    reqs = [e.submit(GenRequest(list(prompts[0]), pen)),
+            e.submit(GenRequest(list(prompts[1]), SamplingParams(temperature=0, max_tokens=40,
+                                                                 ignore_eos=True)))]
+    outs = {r.id: [] for r in reqs}
+    done = set()
+
+    def sink(evs):
+        for ev in evs:
+            if ev.token >= 0:
+                outs[ev.req.id].append(ev.token)
+            if ev.finish is not None:
+                done.add(ev.req.id)
+    e.event_sink = sink
+    while len(done) < 2:
+        e.step()
+    ctx = list(prompts[0])
+    for t in outs[reqs[0].id]:
+        assert t not in ctx[-64:]
+        ctx.append(t)
+    assert outs[reqs[1].id] == base[1]
+    assert e.stats["graph_steps"] > 0

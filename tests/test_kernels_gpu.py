@@ -353,3 +353,23 @@ def test_gemm_nt_fused_swiglu(M):
     expect = torch.nn.functional.silu(y[:, :I]) * y[:, I:]
     torch.testing.assert_close(out.float(), expect, atol=2e-2, rtol=2e-2)
 
+
+
+@pytest.mark.gpu
+def test_apply_penalties_vs_reference():
+    B, V, W = 37, 128256, 64
+    g = torch.Generator().manual_seed(3)
+    logits = (torch.randn(B, V, generator=g) * 3).to(torch.bfloat16)
+    win = torch.randint(0, 300, (B, W), generator=g, dtype=torch.int32)   # many repeats
+    win[::3, : W // 2] = -1                                               # short windows
+    ngen = torch.randint(0, W + 1, (B,), generator=g, dtype=torch.int32)
+    pen = torch.stack([torch.rand(B, generator=g) + 0.5, torch.rand(B, generator=g),
+                       torch.rand(B, generator=g)], 1).float()
+    pen[::5] = torch.tensor([1.0, 0.0, 0.0])                              # neutral rows
+    expect = ref.apply_penalties(logits.float().clone(), win, ngen, pen)
+    got = ops.apply_penalties(logits.cuda(), win.cuda(), ngen.cuda(), pen.cuda()).float().cpu()
+    torch.testing.assert_close(got, expect.to(torch.bfloat16).float(), atol=1e-2, rtol=1e-2)
+    off = torch.zeros(1, dtype=torch.int32, device=DEV)
+    lg = logits.cuda()
+    assert torch.equal(ops.apply_penalties(lg.clone(), win.cuda(), ngen.cuda(), pen.cuda(), on=off),
+                       lg)
