@@ -125,15 +125,145 @@ class ChatHandler:
         params = sampling_from_body(body, left)
         stream = bool(body.get("stream", False))
         include_usage = bool((body.get("stream_options") or {}).get("include_usage", False))
+        n = body.get("n")
+        try:
+            n = 1 if n is None else int(n)
+        except (TypeError, ValueError):
+            n = 0
+        if not 1 <= n <= 16:
+            return write_error(400, "invalid_n", "'n' must be an integer in [1, 16]")
         target.inflight += 1
         t0 = time.time()
         try:
+            if n > 1:
+                return await self._multi(request, target, model, prompt_ids, params, n, stream,
+                                         include_usage, extra_headers, t0)
             if stream:
                 return await self._stream(request, target, model, prompt_ids, params,
                                           include_usage, extra_headers, t0)
             return await self._sync(target, model, prompt_ids, params, extra_headers, t0)
         finally:
             target.inflight -= 1
+
+    async def _multi(self, request, target, model, prompt_ids, params, n, stream, include_usage,
+                     headers, t0):
+        """``n`` choices: n engine requests of the same prompt (seeds seed+i, or
+        distinct per-request seeds), batched by the engine like any other
+        concurrent requests; streamed chunks carry their choice ``index``."""
+        import asyncio
+        import dataclasses
+        base = params.seed if params.seed is not None else uuid.uuid4().int & 0x7FFFFFFF
+        plist = [dataclasses.replace(params, seed=base + i) for i in range(n)]
+        q: asyncio.Queue = asyncio.Queue()
+        stats = {"ttft": None, "n_out": 0, "errors": 0}
+
+        async def run(i, sp):
+            detok = IncrementalDetokenizer(target.tokenizer, sp.stop)
+            finish, lps = "stop", []
+            gen = target.engine.generate(prompt_ids, sp)
+            try:
+                async for it in gen:
+                    if it.token >= 0:
+                        stats["n_out"] += 1
+                        if stats["ttft"] is None:
+                            stats["ttft"] = time.time() - t0
+                        piece = detok.push(it.token)
+                        if sp.logprobs:
+                            lps.append(it.logprob)
+                        await q.put((i, piece, None, it.logprob))
+                        if detok.stopped:
+                            break
+                    if it.finish is not None:
+                        finish = it.finish
+                        break
+            finally:
+                await gen.aclose()
+            tail = detok.flush()
+            if finish.startswith("error"):
+                stats["errors"] += 1
+                finish = "error"
+            elif finish not in ("stop", "length"):
+                finish = "stop"
+            await q.put((i, tail, finish, None))
+
+        tasks = [asyncio.ensure_future(run(i, sp)) for i, sp in enumerate(plist)]
+        chat_id = "chatcmpl-" + uuid.uuid4().hex[:24]
+        created = int(time.time())
+        status = "ok"
+        try:
+            if not stream:
+                texts, fins, lps = [[] for _ in range(n)], [None] * n, [[] for _ in range(n)]
+                left = n
+                while left:
+                    i, piece, fin, lp = await q.get()
+                    texts[i].append(piece)
+                    if fin is not None:
+                        fins[i] = fin
+                        left -= 1
+                    elif lp is not None and params.logprobs:
+                        lps[i].append(lp)
+                if stats["errors"]:
+                    status = "error"
+                    return write_error(502, "engine_failed", "a choice failed in the engine")
+                choices = []
+                for i in range(n):
+                    c = {"index": i, "message": {"role": "assistant", "content": "".join(texts[i])},
+                         "finish_reason": fins[i]}
+                    if params.logprobs:
+                        c["logprobs"] = {"content": [{"logprob": v} for v in lps[i]]}
+                    choices.append(c)
+                resp = {"id": chat_id, "object": "chat.completion", "created": created,
+                        "model": model, "choices": choices,
+                        "usage": {"prompt_tokens": len(prompt_ids),
+                                  "completion_tokens": stats["n_out"],
+                                  "total_tokens": len(prompt_ids) + stats["n_out"]}}
+                r = write_json(200, resp)
+                r.headers.update(headers)
+                return r
+            resp = web.StreamResponse(status=200, headers={
+                "Content-Type": "text/event-stream", "Cache-Control": "no-cache",
+                "Connection": "keep-alive", **headers})
+            await resp.prepare(request)
+            started = [False] * n
+            left = n
+
+            def chunk(i, delta, fin=None):
+                return b"data: " + dumps({"id": chat_id, "object": "chat.completion.chunk",
+                                          "created": created, "model": model,
+                                          "choices": [{"index": i, "delta": delta,
+                                                       "finish_reason": fin}]}).encode() + b"\n\n"
+            try:
+                while left:
+                    i, piece, fin, _ = await q.get()
+                    if piece or not started[i]:
+                        delta = {"content": piece}
+                        if not started[i]:
+                            delta["role"] = "assistant"
+                            started[i] = True
+                        await resp.write(chunk(i, delta))
+                    if fin is not None:
+                        left -= 1
+                        await resp.write(chunk(i, {}, fin))
+                if stats["errors"]:
+                    status = "error"
+                if include_usage:
+                    await resp.write(b"data: " + dumps({
+                        "id": chat_id, "object": "chat.completion.chunk", "created": created,
+                        "model": model, "choices": [],
+                        "usage": {"prompt_tokens": len(prompt_ids),
+                                  "completion_tokens": stats["n_out"],
+                                  "total_tokens": len(prompt_ids) + stats["n_out"]}}).encode()
+                        + b"\n\n")
+                await resp.write(b"data: [DONE]\n\n")
+            except (ConnectionResetError, ConnectionError):
+                status = "client_gone"
+            return resp
+        finally:
+            for t in tasks:
+                t.cancel()
+            await asyncio.gather(*tasks, return_exceptions=True)
+            self._record(target, model, status, t0, len(prompt_ids), stats["n_out"],
+                         stats["ttft"])
 
     async def _sync(self, target, model, prompt_ids, params, headers, t0):
         st = self.state

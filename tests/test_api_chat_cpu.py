@@ -100,3 +100,42 @@ def test_stop_strings(engine):
             assert j["choices"][0]["finish_reason"] == "stop"
             aeng.stop()
     _run(go())
+
+
+def test_n_choices_sync_and_stream(engine):
+    """OpenAI ``n``: n engine requests (seeds seed+i), choices by index; greedy
+    choices agree, sampled ones differ; streamed chunks carry their index and
+    every index gets its own finish chunk."""
+    async def go():
+        st, aeng = _state(engine)
+        async with TestClient(TestServer(make_app(st))) as c:
+            aeng.start(asyncio.get_running_loop())
+            msg = [{"role": "user", "content": "tell me"}]
+            r = await c.post("/v1/chat/completions", json={
+                "model": "tiny-llama", "messages": msg, "n": 3, "max_tokens": 6,
+                "temperature": 0, "ignore_eos": True})
+            j = await r.json()
+            assert r.status == 200 and [ch["index"] for ch in j["choices"]] == [0, 1, 2]
+            texts = {ch["message"]["content"] for ch in j["choices"]}
+            assert len(texts) == 1 and j["usage"]["completion_tokens"] == 18
+            r = await c.post("/v1/chat/completions", json={
+                "model": "tiny-llama", "messages": msg, "n": 4, "max_tokens": 12,
+                "temperature": 1.5, "seed": 7, "ignore_eos": True})
+            j = await r.json()
+            assert len({ch["message"]["content"] for ch in j["choices"]}) > 1
+            r = await c.post("/v1/chat/completions", json={
+                "model": "tiny-llama", "messages": msg, "n": 2, "max_tokens": 5,
+                "temperature": 0.9, "ignore_eos": True, "stream": True,
+                "stream_options": {"include_usage": True}})
+            frames = [f for f in (await r.read()).decode().split("\n\n") if f]
+            assert frames[-1] == "data: [DONE]"
+            chunks = [json.loads(f[6:]) for f in frames[:-1]]
+            fins = [ch["choices"][0]["index"] for ch in chunks
+                    if ch["choices"] and ch["choices"][0].get("finish_reason")]
+            assert sorted(fins) == [0, 1]
+            assert chunks[-1]["usage"]["completion_tokens"] == 10
+            r = await c.post("/v1/chat/completions", json={
+                "model": "tiny-llama", "messages": msg, "n": 0})
+            assert r.status == 400 and (await r.json())["error"] == "invalid_n"
+            aeng.stop()
+    _run(go())
