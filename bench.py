@@ -159,6 +159,7 @@ def main() -> None:
             f"ttft p50 {r['ttft_p50'] * 1e3:.0f} ms")
     for k in engine.stats:
         engine.stats[k] = type(engine.stats[k])(0)
+    engine.ttft_samples.clear()
     import psutil
     procs = {"engine": psutil.Process(), "loadgen": psutil.Process(client.pid)}
     if api_proc is not None:
@@ -185,6 +186,11 @@ def main() -> None:
         f"{k[2:]} {st[k] / ns * 1e3:.3f}" for k in st if k.startswith("t_")) +
         f"; steps {st['steps']} graph {st['graph_steps']}, decode step "
         f"{st['decode_step_s'] / max(1, st['graph_steps']) * 1e3:.2f} ms")
+    if engine.ttft_samples:
+        from llm_mcp_amd.bench.loadgen import percentile as _pct
+        et = [f - a for a, f in engine.ttft_samples]
+        log(f"engine-side TTFT (submit -> first token emitted) p50 {_pct(et, 50) * 1e3:.0f} ms, "
+            f"p95 {_pct(et, 95) * 1e3:.0f} ms over {len(et)} requests")
     tokens = sum(r["tokens"] for r in results)
     ttfts = [t for r in results for t in r["ttfts"]]
     mine = {"tokens": tokens, "elapsed": elapsed, "ttfts": ttfts,

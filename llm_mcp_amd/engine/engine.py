@@ -244,6 +244,9 @@ class LLMEngine:
                       "t_update": 0.0, "t_gpu": 0.0, "decode_step_s": 0.0}
         self._pending = None
         self._fetch_cpu = None
+        # (arrival, first token) wall times of recent requests: engine-side TTFT
+        import collections
+        self.ttft_samples: collections.deque = collections.deque(maxlen=65536)
         self._step_started = 0.0
         self._last_error = None
         # LMX_TORCH_PROFILE=/dir[:steps]: torch.profiler timeline of N steps
@@ -307,9 +310,9 @@ class LLMEngine:
             ("ctx", np.int32, (Bmax,)), ("bt", np.int32, (Bmax, self.max_blocks)),
             ("temp", np.float32, (Bmax,)), ("topk", np.int32, (Bmax,)),
             ("topp", np.float32, (Bmax,)), ("seeds", np.int64, (Bmax,)),
-            ("offs", np.int32, (Bmax,)), ("pen_on", np.int32, (1,))], dev)
-        # penalty inputs: uploaded only on steps with penalised rows (the
-        # captured kernel returns at once when pen_on == 0)
+            ("offs", np.int32, (Bmax,))], dev)
+        # penalty inputs: uploaded only on steps with penalised rows, read by
+        # the lazily captured penalty variants of the decode graphs
         pmeta = _FixedMeta([("win", np.int32, (Bmax, PEN_WINDOW)), ("ngen", np.int32, (Bmax,)),
                             ("pen", np.float32, (Bmax, 3))], dev)
         pmeta.h["win"][:] = -1; pmeta.h["ngen"][:] = 0; pmeta.h["pen"][:] = 0
@@ -318,7 +321,6 @@ class LLMEngine:
         h = meta.h
         h["ids"][:] = 0; h["pos"][:] = 0; h["slots"][:] = -1; h["ctx"][:] = 1; h["bt"][:] = 0
         h["temp"][:] = 0; h["topk"][:] = 0; h["topp"][:] = 1; h["seeds"][:] = 0; h["offs"][:] = 0
-        h["pen_on"][:] = 0
         meta.upload()
         self._gmeta = meta
         g = dict(meta.d)
@@ -330,37 +332,48 @@ class LLMEngine:
             "lp": torch.zeros(Bmax, dtype=torch.float32, device=dev),
         })
         self._gbuf = g
-        pool = None
-        stream = torch.cuda.Stream(device=dev)
+        self._gpool = None
+        self._gstream = torch.cuda.Stream(device=dev)
+        self.pen_graphs: dict[int, dict] = {}
         for B in sorted(self._graph_buckets(), reverse=True):
-            inp = StepInputs(g["ids"][:B], g["pos"][:B], g["slots"][:B], B, g["bt"][:B],
-                             g["ctx"][:B], g["cu"][:B + 1], g["tiles"], g["rows"][:B], B, B)
-            parts = self._graph_parts(B)
-            ws = ops.DecodeWorkspace.__new__(ops.DecodeWorkspace)
-            ws.max_parts, ws.part_o, ws.part_ml = parts, self.decode_ws.part_o, self.decode_ws.part_ml
-
-            def run(inp=inp, ws=ws, B=B):
-                logits = self.model.forward(inp, self.k_caches, self.v_caches, ws,
-                                            self.ecfg.part_tokens)
-                if self.is_leader:
-                    pd = pmeta.d
-                    ops.apply_penalties(logits, pd["win"][:B], pd["ngen"][:B], pd["pen"][:B],
-                                        on=g["pen_on"])
-                    ops.sample(logits, g["temp"][:B], g["topk"][:B], g["topp"][:B],
-                               g["seeds"][:B], g["offs"][:B], g["tok"][:B], g["lp"][:B])
-
-            stream.wait_stream(torch.cuda.current_stream(dev))
-            with torch.cuda.stream(stream):
-                run()  # warm-up (allocator, kernels, hipBLASLt heuristics)
-                run()
-            torch.cuda.current_stream(dev).wait_stream(stream)
-            graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph, pool=pool, stream=stream):
-                run()
-            pool = graph.pool()
-            self.graphs[B] = {"graph": graph, "parts": parts}
+            self.graphs[B] = self._capture_bucket(B, penalties=False)
         torch.cuda.synchronize(dev)
         log.info("captured %d decode graphs in %.1fs", len(self.graphs), time.time() - t0)
+
+    def _capture_bucket(self, B: int, penalties: bool) -> dict:
+        """Capture the decode step of bucket B.  Penalty variants (the penalty
+        kernel ahead of the sampler) are captured lazily, the first time a
+        step of that bucket carries a penalised row, so batches without
+        penalties replay graphs without the extra node."""
+        g, dev, stream = self._gbuf, self.device, self._gstream
+        pmeta = self._pmeta
+        inp = StepInputs(g["ids"][:B], g["pos"][:B], g["slots"][:B], B, g["bt"][:B],
+                         g["ctx"][:B], g["cu"][:B + 1], g["tiles"], g["rows"][:B], B, B)
+        parts = self._graph_parts(B)
+        ws = ops.DecodeWorkspace.__new__(ops.DecodeWorkspace)
+        ws.max_parts, ws.part_o, ws.part_ml = parts, self.decode_ws.part_o, self.decode_ws.part_ml
+
+        def run():
+            logits = self.model.forward(inp, self.k_caches, self.v_caches, ws,
+                                        self.ecfg.part_tokens)
+            if self.is_leader:
+                if penalties:
+                    pd = pmeta.d
+                    ops.apply_penalties(logits, pd["win"][:B], pd["ngen"][:B], pd["pen"][:B])
+                ops.sample(logits, g["temp"][:B], g["topk"][:B], g["topp"][:B],
+                           g["seeds"][:B], g["offs"][:B], g["tok"][:B], g["lp"][:B])
+
+        stream.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(stream):
+            run()  # warm-up (allocator, kernels, hipBLASLt heuristics)
+            if not penalties:
+                run()
+        torch.cuda.current_stream(dev).wait_stream(stream)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, pool=self._gpool, stream=stream):
+            run()
+        self._gpool = graph.pool()
+        return {"graph": graph, "parts": parts}
 
     # --------------------------------------------------------- public API ---
     def submit(self, req: GenRequest) -> GenRequest:
@@ -614,6 +627,7 @@ class LLMEngine:
                 continue
             if req.num_generated == 0:
                 req.first_token_at = now
+                self.ttft_samples.append((req.arrival, now))
             req.num_generated += 1
             reason = fin.get(rid)
             if reason is not None:
@@ -657,6 +671,18 @@ class LLMEngine:
         g, h = self._gbuf, self._gmeta.h
         n = len(plan["seq_ids"])
         mb = plan["max_blocks"]
+        pen = bool(plan.get("any_penalty")) and self.is_leader
+        if pen and B not in self.pen_graphs:
+            # one-time capture of this bucket's penalty variant; its warm-up
+            # run must not write the KV cache: no slots, 1-token contexts
+            h["slots"][:B] = -1
+            h["ctx"][:B] = 1
+            h["bt"][:B, 0] = 0
+            self._gmeta.upload()
+            t0 = time.time()
+            self.pen_graphs[B] = self._capture_bucket(B, penalties=True)
+            log.info("captured the penalty decode graph of bucket %d in %.2fs", B,
+                     time.time() - t0)
         # rows n..B-1 are padding: no cache write (slot -1), a 1-token context
         for k, fill in (("ids", 0), ("pos", 0), ("slots", -1), ("ctx", 1), ("temp", 0),
                         ("topk", 0), ("topp", 1), ("seeds", 0), ("offs", 0)):
@@ -667,8 +693,6 @@ class LLMEngine:
         # never read (and always hold valid page ids)
         h["bt"][:n, :mb] = plan["block_tables"].reshape(n, mb)
         h["bt"][n:B, 0] = 0
-        pen = bool(plan.get("any_penalty")) and self.is_leader
-        h["pen_on"][0] = int(pen)
         if pen:
             ph = self._pmeta.h
             ph["win"][:n] = plan["pen_window"].reshape(n, -1)
@@ -677,7 +701,7 @@ class LLMEngine:
             ph["pen"][:n] = plan["pen_params"].reshape(n, 3)
             self._pmeta.upload()
         self._gmeta.upload()
-        self.graphs[B]["graph"].replay()
+        (self.pen_graphs if pen else self.graphs)[B]["graph"].replay()
         return g["tok"][:B], g["lp"][:B]
 
     def _start_fetch(self, tok: torch.Tensor, lp: torch.Tensor, n: int):
