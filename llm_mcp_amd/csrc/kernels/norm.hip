@@ -48,13 +48,20 @@ __global__ void __launch_bounds__(256) rmsnorm_kernel(
       for (int j = 0; j < 8; ++j) ss += v[i][j] * v[i][j];
     }
   }
+  // gain loads issued before the reduction: their latency overlaps it
+  u16x8 wvs[VPT];
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = threadIdx.x + i * blockDim.x;
+    if (c < nchunk) wvs[i] = *reinterpret_cast<const u16x8*>(w + c * 8);
+  }
   ss = block_sum(ss, scratch);
   const float inv = rsqrtf(ss / (float)cols + eps);
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
     const int c = threadIdx.x + i * blockDim.x;
     if (c < nchunk) {
-      u16x8 wv = *reinterpret_cast<const u16x8*>(w + c * 8);
+      const u16x8 wv = wvs[i];
       u16x8 o;
 #pragma unroll
       for (int j = 0; j < 8; ++j) o.v[j] = f2bf(v[i][j] * inv * bf2f(wv.v[j]));

@@ -10,7 +10,11 @@ Differences, MI355X-first:
     overwrite the new owner's result;
   * heartbeat every max(5, lease/2) s per in-flight job;
   * a GPU/engine failure fails the job (requeued by attempts) and reports the
-    device offline so discovery/routing stop sending it work.
+    device offline so discovery/routing stop sending it work;
+  * admission by KV capacity, not a fixed DEVICE_MAX_CONCURRENCY (SURVEY
+    §7.5 item 4): while the engine's queue is backed up or its paged KV cache
+    is nearly full the agent stops claiming, so queued jobs stay in the shared
+    queue for a less loaded GPU instead of waiting behind this one.
 """
 from __future__ import annotations
 
@@ -40,7 +44,7 @@ class WorkerAgent:
     def __init__(self, client, runner: JobRunner, device_id: str, worker_id: str = "",
                  kinds: list[str] | None = None, lease_s: int = 60, capacity: int = 64,
                  name: str = "", tags: dict | None = None, mark_offline=None,
-                 health=None):
+                 health=None, admit=None):
         self.client = client  # rpc.client.CoreClient (sync; called via to_thread)
         self.runner = runner
         self.device_id = device_id
@@ -55,6 +59,8 @@ class WorkerAgent:
         # so the core requeues its leases when they expire
         self.health = health
         self._reported_unhealthy = False
+        # callable() -> (ok, reason): engine-side admission (KV pages, backlog)
+        self.admit = admit
         self.inflight: dict[str, asyncio.Task] = {}
         self._stop = asyncio.Event()
         self.stats = {"claimed": 0, "done": 0, "failed": 0, "lease_lost": 0}
@@ -84,6 +90,13 @@ class WorkerAgent:
                 await asyncio.wait(list(self.inflight.values()),
                                    return_when=asyncio.FIRST_COMPLETED)
                 continue
+            if self.admit is not None and self.inflight:
+                ok, _why = self.admit()
+                if not ok:
+                    self.stats["admission_waits"] = self.stats.get("admission_waits", 0) + 1
+                    await asyncio.wait(list(self.inflight.values()), timeout=0.05,
+                                       return_when=asyncio.FIRST_COMPLETED)
+                    continue
             try:
                 j = await asyncio.to_thread(self.client.claim, self.worker_id, self.kinds,
                                             self.lease_s, self.device_id, 2000)
@@ -159,3 +172,18 @@ class WorkerAgent:
                     pass
         finally:
             hb.cancel()
+
+
+def engine_admission(engine, max_waiting: int | None = None, kv_high: float = 0.92):
+    """Admission predicate for a chat engine: claim more work only while the
+    engine's waiting queue is short and its KV cache has headroom."""
+    limit = max_waiting if max_waiting is not None else max(4, engine.ecfg.max_num_seqs // 4)
+
+    def admit():
+        s = engine.sched
+        if s.num_waiting >= limit:
+            return False, f"engine backlog {s.num_waiting}"
+        if s.kv_usage >= kv_high:
+            return False, f"kv cache {s.kv_usage:.0%} full"
+        return True, ""
+    return admit

@@ -87,7 +87,7 @@ def serve_engines(a, engine, embed, device_id: str) -> None:
     from ..engine.async_engine import AsyncEngine
     from ..engine.ipc import EngineServer
     from ..models.tokenizer import for_model
-    from .agent import WorkerAgent
+    from .agent import WorkerAgent, engine_admission
     from .jobs import JobRunner
 
     reg = ModelRegistry()
@@ -144,7 +144,8 @@ def serve_engines(a, engine, embed, device_id: str) -> None:
                                 lease_s=a.lease_seconds, capacity=a.max_num_seqs,
                                 tags={"engine": True, "models": list(info["models"])},
                                 mark_offline=mark_offline,
-                                health=engine.healthy if engine is not None else None)
+                                health=engine.healthy if engine is not None else None,
+                                admit=engine_admission(engine) if engine is not None else None)
             task = asyncio.create_task(agent.run())
         await stop.wait()
         if agent is not None:

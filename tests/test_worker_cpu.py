@@ -95,3 +95,54 @@ def test_worker_executes_engine_jobs(core):
     # RecordCost on the gRPC completion path (reference gap fixed)
     assert st.store.cost_summary(0)["total_jobs"] >= 1
     assert agent.stats["done"] == 5
+
+
+def test_admission_gate_leaves_jobs_for_other_workers(core):
+    """A worker whose engine reports no headroom keeps at most the jobs it
+    already holds; the rest stay queued and are claimed by another worker
+    (admission by engine capacity, not a fixed per-device concurrency)."""
+    st, addr = core
+    client = CoreClient(addr)
+
+    class Slow:
+        """Stands in for a JobRunner: holds every job until released."""
+        def __init__(self):
+            self.release = asyncio.Event()
+            self.seen = 0
+
+        async def handle(self, kind, payload):
+            self.seen += 1
+            await self.release.wait()
+            return {"ok": True}, {"ms": 1}
+
+    for dev in ("n:gpu1", "n:gpu2"):   # GPU devices admit their batching capacity
+        st.store.upsert_device(dev, name=dev, tags={"capacity": 8})
+
+    async def go():
+        ids = [client.submit("gate.test", {"i": i}) for i in range(6)]
+        busy, free = Slow(), Slow()
+        gated = {"n": 0}
+
+        def admit():          # the "busy" GPU: full after its first job
+            gated["n"] += 1
+            return False, "kv cache 97% full"
+        a = WorkerAgent(client, busy, "n:gpu1", kinds=["gate.test"], lease_s=30, capacity=8,
+                        admit=admit)
+        b = WorkerAgent(client, free, "n:gpu2", kinds=["gate.test"], lease_s=30, capacity=8)
+        ta = asyncio.ensure_future(a.run())
+        await asyncio.sleep(0.5)          # a claims one job, then the gate closes
+        assert busy.seen == 1 and gated["n"] > 0
+        tb = asyncio.ensure_future(b.run(max_jobs=5))
+        for _ in range(100):
+            if free.seen == 5:
+                break
+            await asyncio.sleep(0.05)
+        assert free.seen == 5 and busy.seen == 1
+        busy.release.set()
+        free.release.set()
+        await tb
+        a.stop()
+        await asyncio.wait_for(ta, 10)
+        return ids
+    ids = asyncio.new_event_loop().run_until_complete(go())
+    assert all(client.get(i)["status"] == "done" for i in ids)
