@@ -31,7 +31,7 @@ int glu(void*, const void*, long, int, int, hipStream_t);
 int apply_penalties(void*, long, int, int, const int*, const int*, const float*, const int*, int,
                     hipStream_t);
 int embed_gather(void*, const void*, const int*, int, int, int, int, hipStream_t);
-int mean_pool_l2(float*, const void*, const int*, int, int, int, int, hipStream_t);
+int mean_pool_l2(float*, float*, const void*, const int*, int, int, int, int, int, hipStream_t);
 int bias_act(void*, const void*, long, int, int, hipStream_t);
 int gemm_splitk(void*, const void*, const void*, float*, int*, int, int, int, long, long, long,
                 int, hipStream_t);
@@ -127,9 +127,10 @@ PYBIND11_MODULE(_lmx_kernels, m) {
     check(lmx::embed_gather(P<void>(out), P<void>(table), P<int>(ids), T, d, vs, vr, S(stream)),
           "embed_gather");
   });
-  m.def("mean_pool_l2", [](uptr out, uptr h, uptr cu, int nseq, int d, int dims, int norm,
-                           uptr stream) {
-    check(lmx::mean_pool_l2(P<float>(out), P<void>(h), P<int>(cu), nseq, d, dims, norm, S(stream)),
+  m.def("mean_pool_l2", [](uptr out, uptr acc, uptr h, uptr cu, int nseq, int T, int d, int dims,
+                           int norm, uptr stream) {
+    check(lmx::mean_pool_l2(P<float>(out), P<float>(acc), P<void>(h), P<int>(cu), nseq, T, d, dims,
+                            norm, S(stream)),
           "mean_pool_l2");
   });
   m.def("bias_act", [](uptr x, uptr bias, long rows, int n, int act, uptr stream) {

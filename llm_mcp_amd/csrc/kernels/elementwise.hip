@@ -120,12 +120,104 @@ __global__ void __launch_bounds__(256) mean_pool_l2_kernel(float* __restrict__ o
   }
 }
 
-int mean_pool_l2(float* out, const void* h, const int* cu, int nseq, int d, int dims,
-                 int normalize, hipStream_t stream) {
+// Two-stage varlen pooling.  Stage 1 spreads the token rows over
+// ceil(T / POOL_ROWS) blocks (one 16 B chunk of a row per lane) and adds each
+// block's per-sequence partial sums into an fp32 accumulator [nseq, d] with
+// global atomics; stage 2 (one block per sequence) scales by 1/len, truncates
+// to `dims` and L2-normalises.  The one-block-per-sequence kernel above walked
+// all rows of a sequence on one CU and was latency-bound (311 us for a
+// 64 x 512-token batch) -- it is kept for batches of many short sequences,
+// where one block per sequence already fills the chip without atomics.
+constexpr int POOL_ROWS = 32;
+
+__device__ __forceinline__ void pool_flush(float* __restrict__ dst, float (&a)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    atomicAdd(dst + j, a[j]);
+    a[j] = 0.f;
+  }
+}
+
+// grid (ceil(T / POOL_ROWS)), block = d/8 lanes rounded up to a wave
+__global__ void __launch_bounds__(256) pool_partial_kernel(float* __restrict__ acc,
+                                                           const bf16_t* __restrict__ h,
+                                                           const int* __restrict__ cu, int nseq,
+                                                           int T, int d) {
+  const int c = threadIdx.x;
+  if (c >= d / 8) return;
+  const int tend = min(T, cu[nseq]);  // rows past the last sequence are padding
+  const int r0 = blockIdx.x * POOL_ROWS;
+  const int r1 = min(r0 + POOL_ROWS, tend);
+  if (r0 >= r1) return;
+  int lo = 0, hi = nseq - 1;  // last sequence starting at or before r0
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (cu[mid] <= r0) lo = mid;
+    else hi = mid - 1;
+  }
+  int s = lo, end = cu[s + 1], n = 0;
+  float a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int t = r0; t < r1; ++t) {
+    while (t >= end) {  // t < tend <= cu[nseq] keeps s < nseq
+      if (n) pool_flush(acc + (long)s * d + c * 8, a);
+      n = 0;
+      ++s;
+      end = cu[s + 1];
+    }
+    const u16x8 v = *reinterpret_cast<const u16x8*>(h + (long)t * d + c * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] += bf2f(v.v[j]);
+    ++n;
+  }
+  if (n) pool_flush(acc + (long)s * d + c * 8, a);
+}
+
+// grid (nseq), block 256; d <= 2048
+__global__ void __launch_bounds__(256) pool_finish_kernel(float* __restrict__ out,
+                                                          const float* __restrict__ acc,
+                                                          const int* __restrict__ cu, int d,
+                                                          int dims, int normalize) {
+  __shared__ float scratch[16];
+  const int s = blockIdx.x;
+  const int len = cu[s + 1] - cu[s];
+  const float inv_n = len > 0 ? 1.f / (float)len : 0.f;
+  float v[8];
+  float ss = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int col = threadIdx.x + j * 256;
+    v[j] = col < dims ? acc[(long)s * d + col] * inv_n : 0.f;
+    ss += v[j] * v[j];
+  }
+  ss = block_sum(ss, scratch);
+  const float inv = normalize ? rsqrtf(fmaxf(ss, 1e-24f)) : 1.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int col = threadIdx.x + j * 256;
+    if (col < dims) out[(long)s * dims + col] = v[j] * inv;
+  }
+}
+
+// acc: fp32 workspace [nseq, d] (zeroed here, on the stream).  Batches of few
+// sequences (fewer than one block's worth of rows per CU) keep the one-pass
+// kernel, which needs no atomics.
+int mean_pool_l2(float* out, float* acc, const void* h, const int* cu, int nseq, int T, int d,
+                 int dims, int normalize, hipStream_t stream) {
   if (nseq <= 0) return 0;
-  if (d % 8 != 0 || d > 2048 || dims > d || dims <= 0) return -1;
-  mean_pool_l2_kernel<<<dim3(nseq), dim3(256), 0, stream>>>(out, (const bf16_t*)h, cu, d, dims,
-                                                            normalize);
+  if (d % 8 != 0 || d > 2048 || dims > d || dims <= 0 || T < 0) return -1;
+  if (acc == nullptr) {
+    mean_pool_l2_kernel<<<dim3(nseq), dim3(256), 0, stream>>>(out, (const bf16_t*)h, cu, d, dims,
+                                                              normalize);
+    return (int)hipGetLastError();
+  }
+  hipError_t e = hipMemsetAsync(acc, 0, sizeof(float) * (size_t)nseq * d, stream);
+  if (e != hipSuccess) return (int)e;
+  if (T > 0) {
+    const int lanes = ((d / 8 + 63) / 64) * 64;
+    pool_partial_kernel<<<dim3((T + POOL_ROWS - 1) / POOL_ROWS), dim3(lanes), 0, stream>>>(
+        acc, (const bf16_t*)h, cu, nseq, T, d);
+  }
+  pool_finish_kernel<<<dim3(nseq), dim3(256), 0, stream>>>(out, acc, cu, d, dims, normalize);
   return (int)hipGetLastError();
 }
 

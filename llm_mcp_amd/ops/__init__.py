@@ -359,8 +359,16 @@ def mean_pool_l2(h: torch.Tensor, cu: torch.Tensor, dims: int | None = None,
          "mean_pool_l2")
     nseq = cu.numel() - 1
     out = torch.empty((nseq, dims), dtype=torch.float32, device=h.device)
-    native().mean_pool_l2(_ptr(out), _ptr(h), _ptr(cu), nseq, d, dims, int(normalize), _stream())
+    # one block per sequence when that already gives >= half the row-tiled
+    # grid (many short sequences); row-tiled two-stage pooling otherwise
+    acc = None if 2 * nseq >= (T + POOL_ROWS - 1) // POOL_ROWS else \
+        torch.empty((nseq, d), dtype=torch.float32, device=h.device)
+    native().mean_pool_l2(_ptr(out), 0 if acc is None else _ptr(acc), _ptr(h), _ptr(cu), nseq, T,
+                          d, dims, int(normalize), _stream())
     return out
+
+
+POOL_ROWS = 32  # rows per block of the two-stage pooling kernel (elementwise.hip)
 
 
 ACT_NONE, ACT_GELU, ACT_SILU = 0, 1, 2

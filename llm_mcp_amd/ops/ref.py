@@ -162,7 +162,8 @@ def mean_pool_l2(h, cu, dims, normalize=True):
     outs = []
     for s in range(len(cu) - 1):
         a, b = int(cu[s]), int(cu[s + 1])
-        m = h[a:b].float().mean(0)[:dims]
+        m = h[a:b].float().mean(0)[:dims] if b > a else \
+            torch.zeros(dims, dtype=torch.float32, device=h.device)
         if normalize:
             m = m / m.norm().clamp_min(1e-12)
         outs.append(m)

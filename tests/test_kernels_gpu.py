@@ -255,6 +255,19 @@ def test_mean_pool_l2_matryoshka():
         torch.testing.assert_close(y, ref.mean_pool_l2(h, cu, dims), atol=1e-3, rtol=1e-3)
 
 
+@pytest.mark.parametrize("d", [768, 1024])
+def test_mean_pool_l2_row_tiled(d):
+    """Two-stage (row-tiled + atomics) path: long sequences, an empty one, a
+    sequence boundary inside a row tile, and padding rows past cu[-1]."""
+    lens = [512, 0, 45, 1, 700, 300]
+    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device=DEV)
+    h = _bf(int(cu[-1]) + 40, d)
+    assert 2 * (len(lens)) < (h.shape[0] + ops.POOL_ROWS - 1) // ops.POOL_ROWS
+    for dims, norm in ((d, True), (256, True), (d, False)):
+        y = ops.mean_pool_l2(h, cu, dims, norm)
+        torch.testing.assert_close(y, ref.mean_pool_l2(h, cu, dims, norm), atol=1e-3, rtol=1e-3)
+
+
 @pytest.mark.parametrize("M,N,K", [(1, 128, 64), (77, 768, 768), (256, 2304, 768),
                                    (1000, 3072, 768), (130, 768, 3072), (512, 4096, 4096)])
 @pytest.mark.parametrize("act", [0, 1, 2, 4])
