@@ -43,6 +43,8 @@ def job_json(j: dict) -> dict:
         out["error"] = j["error"]
     if j.get("attempt_id"):
         out["attempt_id"] = j["attempt_id"]
+    if j.get("progress") is not None and j["status"] == "running":
+        out["progress"] = j["progress"]
     return out
 
 
@@ -183,9 +185,11 @@ class ControlPlane:
         return write_json(200, job_json(j))
 
     async def job_stream(self, request, jid):
-        """SSE: initial status, then every status change until done/error.
-        Change notification = the store's job version counter (NOTIFY
-        job_update equivalent), with a 15 s fallback re-read."""
+        """SSE: initial status, then every status change until done/error,
+        plus ``event: progress`` frames while the job runs (the worker's
+        progress reports: tokens generated so far, ttft).  Change notification
+        = the store's job version counter (NOTIFY job_update equivalent), with
+        a 15 s fallback re-read."""
         if not UUID_RE.match(jid):
             return write_error(404, "not_found", "Resource not found")
         j = await self.db(self.store.get_job, jid)
@@ -195,7 +199,7 @@ class ControlPlane:
                                            "Cache-Control": "no-cache",
                                            "Connection": "keep-alive"})
         await resp.prepare(request)
-        last = None
+        last = last_prog = None
         ver = self.store.job_version()
         deadline = time.time() + float(os.environ.get("LMX_JOB_STREAM_MAX_S", "3600"))
         try:
@@ -206,6 +210,10 @@ class ControlPlane:
                 if j["status"] != last:
                     await resp.write(sse_frame("status", job_json(j)))
                     last = j["status"]
+                prog = j.get("progress") if j["status"] == "running" else None
+                if prog is not None and prog != last_prog:
+                    await resp.write(sse_frame("progress", {"id": j["id"], "progress": prog}))
+                    last_prog = prog
                 if j["status"] in ("done", "error"):
                     break
                 ver = await asyncio.to_thread(self.store.wait_job_change, ver, 15.0)
@@ -334,8 +342,10 @@ class ControlPlane:
             return write_error(400, "worker_id_job_id_required",
                                "Fields worker_id and job_id are required")
         ext = to_int(body.get("extend_seconds"), 0) or 30
+        prog = body.get("progress")
         ok = await self.db(self.store.heartbeat, jid, wid, ext,
-                           str(body.get("attempt_id") or body.get("lease_token") or ""))
+                           str(body.get("attempt_id") or body.get("lease_token") or ""),
+                           prog if isinstance(prog, dict) else None)
         await self.db(self.store.set_device_status, wid, "online")
         return write_json(200, {"ok": bool(ok)})
 

@@ -172,6 +172,7 @@ PYBIND11_MODULE(_lmx_runtime, m) {
       .def("running_on", &JobQueue::running_on)
       .def_property_readonly("version", &JobQueue::version)
       .def("wait_change", &JobQueue::wait_change, py::call_guard<py::gil_scoped_release>())
+      .def("notify_change", &JobQueue::notify_change)
       .def("compact", &JobQueue::compact)
       .def("__len__", &JobQueue::size);
 }

@@ -506,6 +506,11 @@ int64_t JobQueue::wait_change(int64_t since, int64_t timeout_ms) {
   return version_;
 }
 
+void JobQueue::notify_change() {
+  std::lock_guard<std::mutex> g(mu_);
+  bump();
+}
+
 size_t JobQueue::size() const {
   std::lock_guard<std::mutex> g(mu_);
   return jobs_.size();

@@ -92,6 +92,7 @@ class JobQueue {
   int running_on(const std::string& device_id, int64_t now) const;  // live leases
   int64_t version() const;
   int64_t wait_change(int64_t since, int64_t timeout_ms);  // returns current version
+  void notify_change();  // wake wait_change() for state kept outside the queue (job progress)
   void compact();
   size_t size() const;
 

@@ -57,6 +57,12 @@ class CoreClient:
             worker_id=worker_id, job_id=job_id, extend_seconds=extend_seconds,
             attempt_id=attempt_id)).ok
 
+    def progress(self, worker_id, job_id, progress: dict, extend_seconds=30, attempt_id=""):
+        """Heartbeat carrying a progress report (job SSE ``event: progress``)."""
+        return self.call("Heartbeat", pb.HeartbeatRequest(
+            worker_id=worker_id, job_id=job_id, extend_seconds=extend_seconds,
+            attempt_id=attempt_id, progress_json=json.dumps(progress))).ok
+
     def complete(self, worker_id, job_id, result, metrics=None, attempt_id=""):
         return self.call("CompleteJob", pb.CompleteJobRequest(
             worker_id=worker_id, job_id=job_id, result_json=json.dumps(result),

@@ -117,8 +117,9 @@ class CoreService:
         return pb.ClaimJobResponse(job=job_msg(j)) if j else pb.ClaimJobResponse()
 
     async def Heartbeat(self, req, ctx):
+        prog = sanitize_json(req.progress_json) if req.progress_json else None
         ok = await self._db(self.store.heartbeat, req.job_id, req.worker_id,
-                            req.extend_seconds or 30, req.attempt_id)
+                            req.extend_seconds or 30, req.attempt_id, prog)
         return pb.HeartbeatResponse(ok=bool(ok))
 
     async def CompleteJob(self, req, ctx):

@@ -55,6 +55,7 @@ class MemoryStore:
         self.rankings: dict[str, dict] = {}
         self.stats: dict[str, dict] = {}
         self.device_metrics: list[dict] = []
+        self.progress: dict[str, dict] = {}  # running job -> last worker progress report
         if snapshot_path and os.path.exists(snapshot_path):
             self._load_snapshot()
 
@@ -95,7 +96,8 @@ class MemoryStore:
                 "result": _loads(r["result"], None), "error": r["error"] or None,
                 "priority": r["priority"], "queued_at": _s(r["queued_at"]),
                 "updated_at": _s(r["updated_at"]), "source": r["source"],
-                "device_id": r["device_id"] or None, "worker_id": r["worker_id"] or None}
+                "device_id": r["device_id"] or None, "worker_id": r["worker_id"] or None,
+                "progress": self.progress.get(r["id"])}
 
     def submit_job(self, kind, payload, priority=0, source="", max_attempts=3,
                    deadline_at=None, status="queued"):
@@ -136,17 +138,31 @@ class MemoryStore:
         j["attempt_id"] = r["attempt_id"]
         return j
 
-    def heartbeat(self, job_id, worker_id, extend_s, token=""):
-        return self.q.heartbeat(job_id, worker_id, token or "", int(extend_s * 1000),
-                                _ms(self.clock()))
+    def heartbeat(self, job_id, worker_id, extend_s, token="", progress=None):
+        """Extend the lease; a ``progress`` dict (tokens generated so far, ...)
+        from the lease owner is kept with the job and wakes job streams."""
+        ok = self.q.heartbeat(job_id, worker_id, token or "", int(extend_s * 1000),
+                              _ms(self.clock()))
+        if ok and isinstance(progress, dict):
+            with self._lock:
+                self.progress[job_id] = progress
+            self.q.notify_change()
+        return ok
 
     def complete_job(self, job_id, worker_id, result, metrics, token=""):
-        return self.q.complete(job_id, worker_id, token or "", json.dumps(result or {}),
-                               json.dumps(metrics or {}), _ms(self.clock()))
+        ok = self.q.complete(job_id, worker_id, token or "", json.dumps(result or {}),
+                             json.dumps(metrics or {}), _ms(self.clock()))
+        if ok:
+            with self._lock:
+                self.progress.pop(job_id, None)
+        return ok
 
     def fail_job(self, job_id, worker_id, error, metrics, token=""):
         st = self.q.fail(job_id, worker_id, token or "", error or "", json.dumps(metrics or {}),
                          _ms(self.clock()))
+        if st:
+            with self._lock:
+                self.progress.pop(job_id, None)
         return st or None
 
     def release_device_leases(self, device_id):

@@ -30,7 +30,7 @@ _SCHEMA = os.path.join(os.path.dirname(__file__), "schema.sql")
 
 _JOB_COLS = ("id::text AS id, kind, payload, status, attempts, max_attempts, lease_until, "
              "deadline_at, result, error, priority, queued_at, updated_at, source, device_id, "
-             "worker_id")
+             "worker_id, progress")
 
 
 def _job(r: dict | None) -> dict | None:
@@ -197,11 +197,14 @@ class PostgresStore:
     _OWNS = ("status = 'running' AND (($3 <> '' AND lease_token::text = $3) OR "
              "($3 = '' AND worker_id = $2))")
 
-    def heartbeat(self, job_id, worker_id, extend_s, token=""):
+    def heartbeat(self, job_id, worker_id, extend_s, token="", progress=None):
+        # a progress change NOTIFYs job_update (trigger), waking job streams
         return self._n(
             f"UPDATE jobs SET lease_until = now() + make_interval(secs => $4), "
+            f"progress = COALESCE($5::jsonb, progress), "
             f"updated_at = now() WHERE id = $1::uuid AND {self._OWNS}",
-            job_id, worker_id, token or "", float(extend_s)) == 1
+            job_id, worker_id, token or "", float(extend_s),
+            progress if isinstance(progress, dict) else None) == 1
 
     def complete_job(self, job_id, worker_id, result, metrics, token=""):
         with self.pool.conn() as c, c.transaction():

@@ -105,6 +105,8 @@ CREATE TABLE IF NOT EXISTS jobs (
 ALTER TABLE jobs ADD COLUMN IF NOT EXISTS device_id   TEXT;
 ALTER TABLE jobs ADD COLUMN IF NOT EXISTS worker_id   TEXT;
 ALTER TABLE jobs ADD COLUMN IF NOT EXISTS lease_token UUID;
+-- lmx: last progress report of the lease owner (tokens so far), streamed by SSE
+ALTER TABLE jobs ADD COLUMN IF NOT EXISTS progress    JSONB;
 CREATE INDEX IF NOT EXISTS jobs_claim ON jobs (status, priority DESC, queued_at);
 CREATE INDEX IF NOT EXISTS jobs_lease ON jobs (lease_until);
 CREATE INDEX IF NOT EXISTS jobs_device_running ON jobs (device_id) WHERE status = 'running';
@@ -164,7 +166,8 @@ $$ LANGUAGE sql STABLE;
 
 CREATE OR REPLACE FUNCTION notify_job_status_change() RETURNS trigger AS $$
 BEGIN
-  IF TG_OP = 'INSERT' OR NEW.status IS DISTINCT FROM OLD.status THEN
+  IF TG_OP = 'INSERT' OR NEW.status IS DISTINCT FROM OLD.status
+     OR NEW.progress IS DISTINCT FROM OLD.progress THEN
     PERFORM pg_notify('job_update', NEW.id::text);
   END IF;
   RETURN NEW;

@@ -8,7 +8,9 @@ Differences, MI355X-first:
   * wake-up: long-poll claims (``wait_ms``) instead of a 1.5 s idle sleep;
   * every call carries the lease token, so a worker whose lease expired cannot
     overwrite the new owner's result;
-  * heartbeat every max(5, lease/2) s per in-flight job;
+  * heartbeat every max(5, lease/2) s per in-flight job; while a job reports
+    progress (tokens generated so far) a changed report rides on a heartbeat
+    every ``progress_s`` (job SSE ``event: progress``);
   * a GPU/engine failure fails the job (requeued by attempts) and reports the
     device offline so discovery/routing stop sending it work;
   * admission by KV capacity, not a fixed DEVICE_MAX_CONCURRENCY (SURVEY
@@ -44,7 +46,7 @@ class WorkerAgent:
     def __init__(self, client, runner: JobRunner, device_id: str, worker_id: str = "",
                  kinds: list[str] | None = None, lease_s: int = 60, capacity: int = 64,
                  name: str = "", tags: dict | None = None, mark_offline=None,
-                 health=None, admit=None):
+                 health=None, admit=None, progress_s: float | None = None):
         self.client = client  # rpc.client.CoreClient (sync; called via to_thread)
         self.runner = runner
         self.device_id = device_id
@@ -61,6 +63,9 @@ class WorkerAgent:
         self._reported_unhealthy = False
         # callable() -> (ok, reason): engine-side admission (KV pages, backlog)
         self.admit = admit
+        # progress report cadence (s); a report is sent only when it changed
+        self.progress_s = progress_s if progress_s is not None else \
+            float(os.environ.get("LMX_PROGRESS_S", "2"))
         self.inflight: dict[str, asyncio.Task] = {}
         self._stop = asyncio.Event()
         self.stats = {"claimed": 0, "done": 0, "failed": 0, "lease_lost": 0}
@@ -119,10 +124,19 @@ class WorkerAgent:
         if self.inflight:
             await asyncio.gather(*self.inflight.values(), return_exceptions=True)
 
-    async def _heartbeat(self, jid: str, token: str):
+    async def _heartbeat(self, jid: str, token: str, prog: dict | None = None):
+        """Lease extension every max(5, lease/2) s.  While the job updates
+        ``prog`` (tokens so far) a changed report is sent every ``progress_s``
+        instead, as a heartbeat carrying it (job SSE ``event: progress``)."""
         period = max(5.0, self.lease_s / 2)
+        send_prog = getattr(self.client, "progress", None) if prog is not None else None
+        tick = min(period, self.progress_s) if send_prog is not None else period
+        last_ext, sent = time.monotonic(), None
         while True:
-            await asyncio.sleep(period)
+            await asyncio.sleep(tick)
+            changed = send_prog is not None and bool(prog) and prog != sent
+            if not changed and time.monotonic() - last_ext < period - 1e-3:
+                continue
             if self.health is not None:
                 ok, why = self.health()
                 if not ok:
@@ -136,8 +150,16 @@ class WorkerAgent:
                             pass
                     continue
             try:
-                ok = await asyncio.to_thread(self.client.heartbeat, self.worker_id, jid,
-                                             self.lease_s, token)
+                if changed:
+                    snap = dict(prog)
+                    ok = await asyncio.to_thread(send_prog, self.worker_id, jid, snap,
+                                                 self.lease_s, token)
+                    sent = snap
+                    self.stats["progress_sent"] = self.stats.get("progress_sent", 0) + 1
+                else:
+                    ok = await asyncio.to_thread(self.client.heartbeat, self.worker_id, jid,
+                                                 self.lease_s, token)
+                last_ext = time.monotonic()
                 if not ok:
                     log.warning("lease lost for %s", jid)
                     self.stats["lease_lost"] += 1
@@ -147,11 +169,13 @@ class WorkerAgent:
 
     async def _run_job(self, j: dict):
         jid, token = j["id"], j.get("attempt_id") or ""
-        hb = asyncio.create_task(self._heartbeat(jid, token))
+        prog: dict = {}
+        hb = asyncio.create_task(self._heartbeat(jid, token, prog))
         t0 = time.time()
         try:
             faults().maybe_raise("job_crash", "injected job crash")
-            result, metrics = await self.runner.handle(j["kind"], j.get("payload") or {})
+            result, metrics = await self.runner.handle(j["kind"], j.get("payload") or {},
+                                                       progress=prog)
             metrics = dict(metrics or {})
             metrics.setdefault("ms", int((time.time() - t0) * 1000))
             ok = await asyncio.to_thread(self.client.complete, self.worker_id, jid, result,

@@ -88,10 +88,14 @@ class JobRunner:
             raise JobError(f"model '{name}' ({kind}) is not served on {self.device_id}")
         return m
 
-    async def _generate(self, m, prompt_ids, sp):
+    async def _generate(self, m, prompt_ids, sp, progress: dict | None = None):
+        """Run one request on the engine; ``progress`` (the agent's per-job
+        report dict) is updated in place with tokens_out / ttft_ms."""
         from ..models.tokenizer import IncrementalDetokenizer
         detok = IncrementalDetokenizer(m.tokenizer, sp.stop)
         parts, n, ttft, t0 = [], 0, None, time.time()
+        if progress is not None:
+            progress.update(tokens_in=len(prompt_ids), tokens_out=0)
         fin = "stop"
         m.inflight += 1
         try:
@@ -101,7 +105,11 @@ class JobRunner:
                     if it.token >= 0:
                         if ttft is None:
                             ttft = time.time() - t0
+                            if progress is not None:
+                                progress["ttft_ms"] = int(ttft * 1000)
                         n += 1
+                        if progress is not None:
+                            progress["tokens_out"] = n
                         parts.append(detok.push(it.token))
                         if detok.stopped:
                             break
@@ -118,9 +126,10 @@ class JobRunner:
         el = time.time() - t0
         return "".join(parts), n, ttft or el, el, fin
 
-    async def handle(self, kind: str, payload: dict) -> tuple[dict, dict]:
+    async def handle(self, kind: str, payload: dict,
+                     progress: dict | None = None) -> tuple[dict, dict]:
         if kind in ("engine.generate", "ollama.generate", "engine.chat"):
-            return await self.generate(payload, kind)
+            return await self.generate(payload, kind, progress)
         if kind in ("engine.embed", "ollama.embed"):
             return await self.embed(payload)
         if kind.startswith("benchmark.") and kind.endswith(".generate"):
@@ -132,7 +141,7 @@ class JobRunner:
             return await cloud_chat(kind, payload)
         return {"ok": True, "echo": payload}, {"ms": 0}
 
-    async def generate(self, payload: dict, kind: str):
+    async def generate(self, payload: dict, kind: str, progress: dict | None = None):
         model = payload.get("model") or ""
         m = self._model(model, "chat")
         tok = m.tokenizer
@@ -148,7 +157,7 @@ class JobRunner:
             raise JobError("context_length_exceeded")
         sp = sampling_from_payload(payload, ollama_defaults=kind.startswith("ollama."))
         sp.max_tokens = min(sp.max_tokens, left)
-        text, n_out, ttft, el, fin = await self._generate(m, ids, sp)
+        text, n_out, ttft, el, fin = await self._generate(m, ids, sp, progress)
         thinking = ""
         if "<think>" in text:
             thinking, text = split_thinking(text)

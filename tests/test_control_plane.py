@@ -126,6 +126,50 @@ def test_job_stream_sse():
     run(go())
 
 
+def test_job_stream_progress_events():
+    """Worker progress reports (heartbeat ``progress``) reach job SSE clients
+    as ``event: progress`` frames and GET /v1/jobs/{id} while running."""
+    async def go():
+        st, c = client()
+        async with c:
+            jid = (await (await c.post("/v1/jobs", json={"kind": "k"})).json())["job_id"]
+            resp = await c.get(f"/v1/jobs/{jid}/stream")
+            seen = {}
+
+            async def worker():
+                await asyncio.sleep(0.1)
+                j = st.store.claim_job("w", [], 30)
+                for n in (1, 5):
+                    await asyncio.sleep(0.1)
+                    r = await c.post("/v1/workers/heartbeat", json={
+                        "worker_id": "w", "job_id": jid, "attempt_id": j["attempt_id"],
+                        "progress": {"tokens_out": n}})
+                    assert (await r.json())["ok"] is True
+                seen["running"] = await (await c.get(f"/v1/jobs/{jid}")).json()
+                # a stale lease token cannot publish progress
+                r = await c.post("/v1/workers/heartbeat", json={
+                    "worker_id": "w", "job_id": jid, "attempt_id": "bogus",
+                    "progress": {"tokens_out": 99}})
+                assert (await r.json())["ok"] is False
+                await asyncio.sleep(0.1)
+                st.store.complete_job(jid, "w", {"r": 1}, {}, j["attempt_id"])
+
+            t = asyncio.create_task(worker())
+            body = (await resp.read()).decode()
+            await t
+            frames = [f for f in body.split("\n\n") if f.strip()]
+            kinds = [f.split("\n")[0][len("event: "):] for f in frames]
+            data = [json.loads(f.split("\n")[1][len("data: "):]) for f in frames]
+            prog = [d["progress"]["tokens_out"] for k, d in zip(kinds, data) if k == "progress"]
+            assert prog == [1, 5]
+            assert [d["status"] for k, d in zip(kinds, data) if k == "status"] == \
+                ["queued", "running", "done"]
+            assert seen["running"]["progress"] == {"tokens_out": 5}
+            done = await (await c.get(f"/v1/jobs/{jid}")).json()
+            assert done["status"] == "done" and "progress" not in done
+    run(go())
+
+
 def test_discovery_devices_dashboard_capacity():
     async def go():
         st, c = client()

@@ -97,6 +97,37 @@ def test_worker_executes_engine_jobs(core):
     assert agent.stats["done"] == 5
 
 
+def test_progress_over_grpc_and_agent(core):
+    """CoreClient.progress (a Heartbeat with progress_json) lands on the job;
+    the agent forwards a running job's progress dict while it changes."""
+    st, addr = core
+    client = CoreClient(addr)
+    jid = client.submit("prog.test", {})
+    j = client.claim("w-prog", ["prog.test"], 30, "", 0)
+    assert j and j["id"] == jid
+    assert client.progress("w-prog", jid, {"tokens_out": 7}, 30, j["attempt_id"])
+    assert st.store.get_job(jid)["progress"] == {"tokens_out": 7}
+    assert not client.progress("w-prog", jid, {"tokens_out": 8}, 30, "stale-token")
+    assert client.complete("w-prog", jid, {"ok": True}, {}, j["attempt_id"])
+
+    class Ticking:
+        async def handle(self, kind, payload, progress=None):
+            for n in range(1, 4):
+                progress["tokens_out"] = n
+                await asyncio.sleep(0.15)
+            return {"ok": True}, {"ms": 1}
+
+    async def go():
+        jid2 = client.submit("prog.agent", {})
+        agent = WorkerAgent(client, Ticking(), "n:gpu3", kinds=["prog.agent"], lease_s=30,
+                            capacity=2, progress_s=0.05)
+        await agent.run(max_jobs=1)
+        return jid2, agent
+    jid2, agent = asyncio.new_event_loop().run_until_complete(go())
+    assert agent.stats["progress_sent"] >= 2
+    assert client.get(jid2)["status"] == "done"
+
+
 def test_admission_gate_leaves_jobs_for_other_workers(core):
     """A worker whose engine reports no headroom keeps at most the jobs it
     already holds; the rest stay queued and are claimed by another worker
@@ -110,7 +141,7 @@ def test_admission_gate_leaves_jobs_for_other_workers(core):
             self.release = asyncio.Event()
             self.seen = 0
 
-        async def handle(self, kind, payload):
+        async def handle(self, kind, payload, progress=None):
             self.seen += 1
             await self.release.wait()
             return {"ok": True}, {"ms": 1}
