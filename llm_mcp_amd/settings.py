@@ -59,6 +59,12 @@ VARS: list[Var] = [
     Var("ALERT_FAIL_THRESHOLD", int, 3, "attempts before a failed job is alerted"),
     Var("TELEGRAM_BOT_TOKEN", str, "", "Telegram alert sink", secret=True),
     Var("TELEGRAM_CHAT_ID", str, "", "Telegram chat (REPORT_CHAT_ID also accepted)"),
+    Var("TELEGRAM_USE_MCP", bool, False, "send alerts through a telegram-mcp gateway"),
+    Var("TELEGRAM_MCP_BASE_URL", str, "http://tgapi:8000", "telegram-mcp gateway URL"),
+    Var("TELEGRAM_MCP_CHAT_ID", str, "", "chat for the gateway route (else TELEGRAM_CHAT_ID)"),
+    Var("TELEGRAM_MCP_BOT_ID", int, 0, "gateway bot id (optional)"),
+    Var("TELEGRAM_MCP_FALLBACK_DIRECT", bool, True,
+        "fall back to the Bot API when the gateway fails"),
     Var("ALERT_WEBHOOK_URL", str, "", "webhook alert sink"),
     Var("LOG_LEVEL", str, "INFO", "python logging level"),
     # ---- MI355X serving (new) ----
@@ -116,6 +122,13 @@ def get(name: str):
         if name == "CORE_VERSION" and os.environ.get("LLM_MCP_VERSION"):
             return os.environ["LLM_MCP_VERSION"]
         return v.default
+    if v.type is bool:
+        s = raw.strip().lower()
+        if s in ("1", "true", "yes", "y", "on"):
+            return True
+        if s in ("0", "false", "no", "n", "off"):
+            return False
+        raise SettingsError(f"{name}={raw!r} is not a valid bool")
     try:
         return v.type(raw)
     except ValueError as e:

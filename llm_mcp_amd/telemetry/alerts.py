@@ -9,7 +9,8 @@ failed jobs (ids de-duplicated, at most 100 remembered).  GPU alerts are added
 for the MI355X fleet: junction temperature above LMX_ALERT_TEMP_C and a
 degraded device circuit.  Sinks: log (always), webhook (ALERT_WEBHOOK_URL),
 Telegram Bot API (TELEGRAM_BOT_TOKEN + TELEGRAM_CHAT_ID; edit-in-place, HTML
-<pre>, honours 429 retry_after).
+<pre>, honours 429 retry_after), or a telegram-mcp gateway (TELEGRAM_USE_MCP=1)
+with the Bot API as fallback.
 """
 from __future__ import annotations
 
@@ -88,8 +89,17 @@ class WebhookSink:
                 return r.status < 300
 
 
+def _pre(text: str) -> str:
+    return f"<pre>{html.escape(text, quote=False)}</pre>"
+
+
 class TelegramSink:
-    """Direct Bot API client (edit-in-place of the last alert message)."""
+    """Direct Bot API client.  The first alert is sent with sendMessage; later
+    alerts replace it in place with editMessageText (one live status message
+    per chat, reference telemetry/llm_telemetry/telegram_gateway.py:85-101).
+    429 answers are retried after ``retry_after``; "message is not modified"
+    counts as delivered; an edit of a message that no longer exists falls
+    back to a fresh sendMessage."""
 
     def __init__(self, token: str, chat_id: str, base: str = "https://api.telegram.org"):
         self.url = f"{base}/bot{token}"
@@ -108,23 +118,106 @@ class TelegramSink:
                     return data
         return {"ok": False}
 
-    async def send(self, text: str):
-        body = {"chat_id": self.chat_id, "text": f"<pre>{html.escape(text)}</pre>",
-                "parse_mode": "HTML"}
+    async def send_or_edit(self, text: str) -> bool:
+        body = {"chat_id": self.chat_id, "text": _pre(text), "parse_mode": "HTML",
+                "disable_web_page_preview": True}
+        if self.last_id is not None:
+            r = await self._call("editMessageText", {**body, "message_id": self.last_id})
+            if r.get("ok") or "not modified" in str(r.get("description", "")).lower():
+                return True
+            self.last_id = None          # deleted / too old to edit: post a new one
         r = await self._call("sendMessage", body)
         if r.get("ok"):
             self.last_id = (r.get("result") or {}).get("message_id")
         return bool(r.get("ok"))
+
+    send = send_or_edit
+
+
+class McpTelegramSink:
+    """Telegram through a telegram-mcp gateway (TELEGRAM_USE_MCP=1,
+    reference telegram_gateway.py:104-170): POST {base}/api/messages creates
+    the status message, PATCH {base}/api/messages/{id} edits it (the gateway's
+    internal id, optional bot_id).  The reference drove the gateway through
+    its private telegram_api_client package, which is not available here, so
+    the two HTTP routes are this framework's contract (parity unpinned)."""
+
+    def __init__(self, base: str, chat_id: str, bot_id: int | None = None):
+        self.base = base.rstrip("/")
+        self.chat_id = chat_id
+        self.bot_id = bot_id
+        self.msg_id: int | None = None
+
+    async def send_or_edit(self, text: str) -> bool:
+        body = {"chat_id": self.chat_id, "text": _pre(text), "parse_mode": "HTML",
+                "disable_web_page_preview": True}
+        if self.bot_id is not None:
+            body["bot_id"] = self.bot_id
+        async with aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=15)) as s:
+            if self.msg_id is not None:
+                async with s.patch(f"{self.base}/api/messages/{self.msg_id}", json=body) as r:
+                    if r.status < 300:
+                        return True
+                self.msg_id = None
+            async with s.post(f"{self.base}/api/messages", json=body) as r:
+                if r.status >= 300:
+                    return False
+                data = await r.json(content_type=None)
+        mid = (data or {}).get("id")
+        if mid is None:
+            return False
+        self.msg_id = int(mid)
+        return True
+
+    send = send_or_edit
+
+
+class GatewaySink:
+    """Primary route with a fallback (MCP gateway first, direct Bot API when
+    it fails and TELEGRAM_MCP_FALLBACK_DIRECT allows, reference
+    telemetry/llm_telemetry/main.py:196-211)."""
+
+    def __init__(self, primary, fallback=None):
+        self.primary, self.fallback = primary, fallback
+
+    async def send(self, text: str) -> bool:
+        ok = False
+        if self.primary is not None:
+            try:
+                ok = await self.primary.send_or_edit(text)
+            except Exception as e:
+                log.warning("telegram mcp send failed: %s", e)
+        if not ok and self.fallback is not None:
+            ok = await self.fallback.send_or_edit(text)
+        if not ok:
+            log.warning("alert send failed (all telegram routes)")
+        return ok
+
+
+def _env_on(name: str, default: bool) -> bool:
+    v = os.environ.get(name, "").strip().lower()
+    return default if not v else v in ("1", "true", "yes", "y", "on")
 
 
 def sinks_from_env() -> list:
     s: list = [LogSink()]
     if os.environ.get("ALERT_WEBHOOK_URL"):
         s.append(WebhookSink(os.environ["ALERT_WEBHOOK_URL"]))
-    tok = os.environ.get("TELEGRAM_BOT_TOKEN")
-    chat = os.environ.get("TELEGRAM_CHAT_ID") or os.environ.get("REPORT_CHAT_ID")
-    if tok and chat:
-        s.append(TelegramSink(tok, chat))
+    tok = os.environ.get("TELEGRAM_BOT_TOKEN", "").strip()
+    chat = (os.environ.get("TELEGRAM_MCP_CHAT_ID") or os.environ.get("TELEGRAM_CHAT_ID")
+            or os.environ.get("REPORT_CHAT_ID") or "").strip()
+    if not chat:
+        return s
+    direct = TelegramSink(tok, chat) if tok else None
+    if _env_on("TELEGRAM_USE_MCP", False):
+        bot = os.environ.get("TELEGRAM_MCP_BOT_ID", "").strip()
+        mcp = McpTelegramSink(os.environ.get("TELEGRAM_MCP_BASE_URL", "").strip()
+                              or "http://tgapi:8000", chat,
+                              int(bot) if bot.lstrip("-").isdigit() else None)
+        fb = direct if _env_on("TELEGRAM_MCP_FALLBACK_DIRECT", True) else None
+        s.append(GatewaySink(mcp, fb))
+    elif direct is not None:
+        s.append(GatewaySink(None, direct))
     return s
 
 

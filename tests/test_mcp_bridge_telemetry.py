@@ -127,3 +127,91 @@ def test_telemetry_alerts_baseline_transitions_and_dedupe():
     run(go())
     assert format_alert({"queued": 3, "running": 0, "devices": [], "failed_jobs": []},
                         set(), []).endswith("Queue stuck: 3 queued, 0 running")
+
+
+def test_telegram_sinks_edit_in_place_and_gateway_fallback(monkeypatch):
+    """Bot API sink: sendMessage once, then editMessageText of that message
+    ("not modified" counts as sent, a vanished message is re-sent); gateway
+    sink: POST then PATCH, falling back to the Bot API when it fails."""
+    from aiohttp import web
+    from aiohttp.test_utils import TestServer
+    from llm_mcp_amd.telemetry import alerts as al
+
+    calls = []
+    state = {"gw_up": True, "next_edit": "ok"}
+
+    async def bot(request):
+        body = await request.json()
+        method = request.match_info["method"]
+        calls.append(("bot", method, body.get("message_id"), body["text"]))
+        if method == "sendMessage":
+            return web.json_response({"ok": True, "result": {"message_id": 100 + len(calls)}})
+        mode, state["next_edit"] = state["next_edit"], "ok"
+        if mode == "same":
+            return web.json_response({"ok": False, "description":
+                                      "Bad Request: message is not modified"}, status=400)
+        if mode == "gone":
+            return web.json_response({"ok": False, "description":
+                                      "Bad Request: message to edit not found"}, status=400)
+        return web.json_response({"ok": True, "result": {}})
+
+    async def gw_post(request):
+        body = await request.json()
+        calls.append(("gw", "post", None, body["text"]))
+        if not state["gw_up"]:
+            return web.json_response({"error": "down"}, status=503)
+        return web.json_response({"id": 7})
+
+    async def gw_patch(request):
+        calls.append(("gw", "patch", request.match_info["mid"], (await request.json())["text"]))
+        if not state["gw_up"]:
+            return web.json_response({"error": "down"}, status=503)
+        return web.json_response({"ok": True})
+
+    app = web.Application()
+    app.router.add_post("/botTOK/{method}", bot)
+    app.router.add_post("/api/messages", gw_post)
+    app.router.add_patch("/api/messages/{mid}", gw_patch)
+
+    async def go():
+        srv = TestServer(app)
+        await srv.start_server()
+        base = str(srv.make_url("")).rstrip("/")
+        try:
+            direct = al.TelegramSink("TOK", "42", base=base)
+            assert await direct.send_or_edit("a <b>")
+            first = direct.last_id
+            assert await direct.send_or_edit("b")
+            state["next_edit"] = "same"
+            assert await direct.send_or_edit("b")
+            state["next_edit"] = "gone"
+            assert await direct.send_or_edit("c")
+            assert direct.last_id != first
+            kinds = [(c[1], c[2]) for c in calls if c[0] == "bot"]
+            assert kinds[0] == ("sendMessage", None) and kinds[1] == ("editMessageText", first)
+            assert kinds[-2][0] == "editMessageText" and kinds[-1][0] == "sendMessage"
+            assert calls[0][3] == "<pre>a &lt;b&gt;</pre>"
+
+            calls.clear()
+            g = al.GatewaySink(al.McpTelegramSink(base, "42", bot_id=3),
+                               al.TelegramSink("TOK", "42", base=base))
+            assert await g.send("x") and await g.send("y")
+            assert [(c[0], c[1]) for c in calls] == [("gw", "post"), ("gw", "patch")]
+            state["gw_up"] = False
+            calls.clear()
+            assert await g.send("z")        # gateway down -> Bot API
+            assert [c[0] for c in calls][-1] == "bot"
+        finally:
+            await srv.close()
+    run(go())
+
+    monkeypatch.setenv("TELEGRAM_CHAT_ID", "42")
+    monkeypatch.setenv("TELEGRAM_BOT_TOKEN", "t")
+    monkeypatch.setenv("TELEGRAM_USE_MCP", "1")
+    monkeypatch.setenv("TELEGRAM_MCP_FALLBACK_DIRECT", "0")
+    sinks = al.sinks_from_env()
+    gw = [s for s in sinks if isinstance(s, al.GatewaySink)][0]
+    assert isinstance(gw.primary, al.McpTelegramSink) and gw.fallback is None
+    monkeypatch.setenv("TELEGRAM_USE_MCP", "0")
+    gw = [s for s in al.sinks_from_env() if isinstance(s, al.GatewaySink)][0]
+    assert gw.primary is None and isinstance(gw.fallback, al.TelegramSink)
