@@ -7,7 +7,8 @@ from __future__ import annotations
 
 from aiohttp import web
 
-from .helpers import write_json
+from ..utils import tracing
+from .helpers import write_error, write_json
 from .openai_chat import ChatHandler
 
 
@@ -25,7 +26,7 @@ STATE_KEY = web.AppKey("state", object)
 
 
 def make_app(state) -> web.Application:
-    app = web.Application(client_max_size=10 << 20)
+    app = web.Application(client_max_size=10 << 20, middlewares=[tracing.aiohttp_middleware()])
     app[STATE_KEY] = state
     chat_handler = ChatHandler(state)
 
@@ -39,6 +40,17 @@ def make_app(state) -> web.Application:
         return web.Response(body=state.metrics.render(),
                             headers={"Content-Type": "text/plain; version=0.0.4"})
 
+    async def trace(request):
+        """Spans recorded in this process for one request ID."""
+        if request.method != "GET":
+            return write_error(405, "method_not_allowed", "Method not allowed")
+        rid = tracing.clean_id(request.match_info.get("rid", ""))
+        spans = tracing.RING.find(rid) if rid else []
+        if not spans:
+            return write_error(404, "not_found", "No spans recorded for this request id")
+        return write_json(200, {"request_id": rid, "spans": spans})
+
+    app.router.add_route("*", "/v1/debug/trace/{rid}", trace)
     app.router.add_route("*", "/health", health)
     app.router.add_route("*", "/version", health)
     app.router.add_route("GET", "/metrics", metrics)

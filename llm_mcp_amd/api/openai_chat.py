@@ -26,6 +26,7 @@ from aiohttp import web
 
 from ..engine.engine import SamplingParams
 from ..models.tokenizer import IncrementalDetokenizer, apply_chat_template
+from ..utils import tracing
 from .helpers import dumps, read_json, write_error, write_json
 
 CHAT_TIMEOUT_S = 120.0
@@ -89,8 +90,9 @@ class ChatHandler:
         model = body.get("model") or ""
         # request id: honoured from the client or minted here,
         # echoed on the response and logged with the completion record
-        rid = request.headers.get("X-Request-ID") or uuid.uuid4().hex
-        extra_headers = {"X-Request-ID": rid}
+        rid = tracing.current_request_id.get() or tracing.clean_id(
+            request.headers.get(tracing.HEADER)) or tracing.new_id()
+        extra_headers = {tracing.HEADER: rid}
         if not model:
             selector = getattr(st, "select_model", None)
             selected = None
@@ -263,7 +265,7 @@ class ChatHandler:
                 t.cancel()
             await asyncio.gather(*tasks, return_exceptions=True)
             self._record(target, model, status, t0, len(prompt_ids), stats["n_out"],
-                         stats["ttft"])
+                         stats["ttft"], headers.get(tracing.HEADER, ""), n=n)
 
     async def _sync(self, target, model, prompt_ids, params, headers, t0):
         st = self.state
@@ -290,9 +292,11 @@ class ChatHandler:
             await gen.aclose()
         text.append(detok.flush())
         if finish.startswith("error"):
-            self._record(target, model, "error", t0, len(prompt_ids), n_out, ttft)
+            self._record(target, model, "error", t0, len(prompt_ids), n_out, ttft,
+                         headers.get(tracing.HEADER, ""))
             return write_error(502, "engine_failed", finish)
-        self._record(target, model, "ok", t0, len(prompt_ids), n_out, ttft)
+        self._record(target, model, "ok", t0, len(prompt_ids), n_out, ttft,
+                         headers.get(tracing.HEADER, ""))
         choice = {"index": 0, "message": {"role": "assistant", "content": "".join(text)},
                   "finish_reason": finish if finish in ("stop", "length") else "stop"}
         if params.logprobs:
@@ -365,12 +369,21 @@ class ChatHandler:
             status = "client_gone"
         finally:
             await gen.aclose()
-            self._record(target, model, status, t0, len(prompt_ids), n_out, ttft)
+            self._record(target, model, status, t0, len(prompt_ids), n_out, ttft,
+                         headers.get(tracing.HEADER, ""))
         return resp
 
-    def _record(self, target, model, status, t0, n_in, n_out, ttft):
+    def _record(self, target, model, status, t0, n_in, n_out, ttft, rid="", n=1):
         st = self.state
         elapsed = time.time() - t0
+        # per-request span: TTFT = queue + prefill, decode = first -> last token
+        tracing.record_span(
+            "chat", rid, model=model, device_id=target.device_id, status=status, n=n,
+            prompt_tokens=n_in, completion_tokens=n_out, total_ms=elapsed * 1e3,
+            ttft_ms=None if ttft is None else ttft * 1e3,
+            decode_ms=None if ttft is None else (elapsed - ttft) * 1e3,
+            itl_ms=(elapsed - ttft) / (n_out - 1) * 1e3 if ttft is not None and n_out > 1
+            else None)
         m = st.metrics
         m.chat_requests(model, target.device_id, status)
         if status in ("ok", "client_gone"):

@@ -20,6 +20,7 @@ from aiohttp import ClientSession, ClientTimeout, web
 from ..policy import limits as lim
 from ..policy.router import QUALITY_TIMEOUTS, RoutingError, parse_payload_model_device
 from ..store.base import COST_PERIODS, iso, parse_iso
+from ..utils import tracing
 from .helpers import read_json, sse_frame, to_int, write_error, write_json
 
 UUID_RE = re.compile(r"^[0-9a-f]{8}-[0-9a-f]{4}-[0-9a-f]{4}-[0-9a-f]{4}-[0-9a-f]{12}$")
@@ -157,6 +158,7 @@ class ControlPlane:
                 ok, why = await self.db(lim.model_allowed, self.store, dev, model)
                 if not ok:
                     return write_error(400, "model_not_allowed", "Model not allowed on device: " + why)
+        payload = tracing.tag_payload(payload, tracing.client_request_id(request))
         jid = await self.db(self.store.submit_job, kind, payload, to_int(body.get("priority"), 0),
                             str(body.get("source") or ""), max_attempts, deadline)
         self.st.metrics.jobs_created.labels(kind).inc()
@@ -406,6 +408,8 @@ class ControlPlane:
             secs = QUALITY_TIMEOUTS.get(str(body.get("quality") or "").strip().lower())
             if secs:
                 deadline = time.time() + secs
+        if isinstance(payload, dict):
+            payload = tracing.tag_payload(payload, tracing.client_request_id(request))
         jid = await self.db(self.store.submit_job, kind, payload, to_int(body.get("priority"), 0),
                             str(body.get("source") or ""), to_int(body.get("max_attempts"), 0) or 3,
                             deadline)

@@ -23,14 +23,18 @@ class CoreClient:
             self._stubs[name] = mk(path, request_serializer=pb.msgs[inp].SerializeToString,
                                    response_deserializer=pb.msgs[out].FromString)
 
-    def call(self, name: str, req, timeout: float | None = None):
-        return self._stubs[name](req, timeout=timeout or self.timeout)
+    def call(self, name: str, req, timeout: float | None = None, metadata=None):
+        return self._stubs[name](req, timeout=timeout or self.timeout, metadata=metadata)
 
     # convenience ------------------------------------------------------------
-    def submit(self, kind, payload=None, priority=0, source="", max_attempts=0, deadline_at=""):
+    def submit(self, kind, payload=None, priority=0, source="", max_attempts=0, deadline_at="",
+               request_id=""):
+        """``request_id`` travels as ``x-request-id`` call metadata and is kept
+        in the job payload (utils/tracing.py)."""
+        md = (("x-request-id", request_id),) if request_id else None
         return self.call("SubmitJob", pb.SubmitJobRequest(
             kind=kind, payload_json=json.dumps(payload or {}), priority=priority, source=source,
-            max_attempts=max_attempts, deadline_at=deadline_at)).job_id
+            max_attempts=max_attempts, deadline_at=deadline_at), metadata=md).job_id
 
     def get(self, job_id):
         return job_dict(self.call("GetJob", pb.GetJobRequest(job_id=job_id)).job)

@@ -20,6 +20,7 @@ import time
 import grpc
 
 from ..store.base import iso, parse_iso
+from ..utils import tracing
 from . import proto as pb
 
 log = logging.getLogger("lmx.grpc")
@@ -69,7 +70,16 @@ class CoreService:
                 deadline = parse_iso(req.deadline_at)
             except ValueError:
                 await ctx.abort(grpc.StatusCode.INVALID_ARGUMENT, "invalid_deadline_at")
-        jid = await self._db(self.store.submit_job, req.kind, sanitize_json(req.payload_json),
+        payload = sanitize_json(req.payload_json)
+        if isinstance(payload, dict):
+            # request id from the call metadata (utils/tracing.py), as X-Request-ID over HTTP
+            rid = ""
+            for item in ctx.invocation_metadata() or ():
+                k, v = item if isinstance(item, tuple) else (item.key, item.value)
+                if k == "x-request-id":
+                    rid = tracing.clean_id(v)
+            payload = tracing.tag_payload(payload, rid)
+        jid = await self._db(self.store.submit_job, req.kind, payload,
                              req.priority, req.source, req.max_attempts or 3, deadline)
         self.st.metrics.jobs_created.labels(req.kind).inc()
         return pb.SubmitJobResponse(job_id=jid)

@@ -26,6 +26,8 @@ import os
 import socket
 import time
 
+from ..store.base import parse_iso
+from ..utils import tracing
 from ..utils.faults import faults
 from .jobs import JobError, JobRunner
 
@@ -172,18 +174,36 @@ class WorkerAgent:
         prog: dict = {}
         hb = asyncio.create_task(self._heartbeat(jid, token, prog))
         t0 = time.time()
+        # correlation: the submitter's X-Request-ID if it rode in the payload,
+        # else the job id (utils/tracing.py)
+        rid = tracing.payload_request_id(j.get("payload")) or jid
+        q = j.get("queued_at")
+        try:   # ISO string (HTTP / gRPC) or epoch seconds (in-process store)
+            queued = float(q) if isinstance(q, (int, float)) else parse_iso(q)
+        except (TypeError, ValueError, AttributeError):
+            queued = None
+        span = {"job_id": jid, "kind": j.get("kind", ""), "device_id": self.device_id,
+                "attempt": j.get("attempts"),
+                "queue_wait_ms": None if queued is None else max(0.0, t0 - queued) * 1e3}
         try:
             faults().maybe_raise("job_crash", "injected job crash")
             result, metrics = await self.runner.handle(j["kind"], j.get("payload") or {},
                                                        progress=prog)
             metrics = dict(metrics or {})
             metrics.setdefault("ms", int((time.time() - t0) * 1000))
+            metrics.setdefault("request_id", rid)
             ok = await asyncio.to_thread(self.client.complete, self.worker_id, jid, result,
                                          metrics, token)
             self.stats["done" if ok else "lease_lost"] += 1
+            tracing.record_span("job.attempt", rid, status="done" if ok else "lease_lost",
+                                run_ms=(time.time() - t0) * 1e3, ttft_ms=prog.get("ttft_ms"),
+                                tokens_in=prog.get("tokens_in"),
+                                tokens_out=prog.get("tokens_out"), **span)
         except Exception as e:
             self.stats["failed"] += 1
             log.warning("job %s failed: %s", jid, e)
+            tracing.record_span("job.attempt", rid, status="failed", error=str(e)[:200],
+                                run_ms=(time.time() - t0) * 1e3, **span)
             try:
                 await asyncio.to_thread(self.client.fail, self.worker_id, jid, str(e),
                                         {"ms": int((time.time() - t0) * 1000)}, token)

@@ -49,9 +49,11 @@ def test_chat_sync_and_stream(engine):
             r = await c.post("/v1/chat/completions", json={
                 "model": "tiny-llama", "messages": [{"role": "user", "content": "hi there"}],
                 "max_tokens": 5, "temperature": 0, "ignore_eos": True, "stream": True,
-                "stream_options": {"include_usage": True}})
+                "stream_options": {"include_usage": True}},
+                headers={"X-Request-ID": "chat-trace-1"})
             assert r.status == 200
             assert r.headers["Content-Type"].startswith("text/event-stream")
+            assert r.headers["X-Request-ID"] == "chat-trace-1"
             body = (await r.read()).decode()
             frames = [f for f in body.split("\n\n") if f]
             assert frames[-1] == "data: [DONE]"
@@ -64,6 +66,11 @@ def test_chat_sync_and_stream(engine):
             text = "".join(ch["choices"][0]["delta"].get("content", "") for ch in chunks
                            if ch["choices"])
             assert text == j["choices"][0]["message"]["content"]
+            # the stream's span is recorded under the client's request id
+            tr = await (await c.get("/v1/debug/trace/chat-trace-1")).json()
+            sp = tr["spans"][-1]
+            assert sp["span"] == "chat" and sp["status"] == "ok"
+            assert sp["completion_tokens"] == 5 and 0 <= sp["ttft_ms"] <= sp["total_ms"]
             # errors keep the reference contract
             r = await c.post("/v1/chat/completions", json={"model": "tiny-llama"})
             assert r.status == 400 and (await r.json())["error"] == "messages_required"

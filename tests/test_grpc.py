@@ -58,6 +58,9 @@ def test_grpc_worker_protocol(core):
     assert c.report_benchmark("dev0", "llama-3-8b", "generate", 10, 100, 500, 200.0)
     assert st.store.list_benchmarks(1)[0]["tps"] == 200.0
     assert c.report_metrics({"id": wid, "name": "w"}, {"gpu_util": 90})
+    # request id via call metadata lands in the payload
+    j3 = c.submit("echo", {"a": 1}, request_id="grpc-trace-1")
+    assert c.get(j3)["payload"] == {"a": 1, "_request_id": "grpc-trace-1"}
 
 
 def test_grpc_claim_long_poll_wakes_on_submit(core):
