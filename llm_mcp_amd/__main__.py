@@ -40,6 +40,85 @@ def _gpu_list(spec: str) -> list[int]:
     return out
 
 
+def plan_placement(gpus: list[int], chat_model: str = "", embed_model: str = "",
+                   embed_gpus: list[int] | None = None, tp: int = 1,
+                   registry: str = "") -> list[dict]:
+    """Which worker process serves what (SURVEY §5.6 ``LMX_MODEL_REGISTRY``).
+
+    Without a registry every GPU gets ``chat_model`` (TP groups of ``tp``
+    consecutive GPUs when tp > 1) and ``embed_model`` on ``embed_gpus``.  A
+    registry places models per GPU set, entries separated by ``;``::
+
+        GPUS:MODEL          single-GPU chat engines on each listed GPU
+        GPUS:tpN:MODEL      TP=N groups over the listed GPUs (N consecutive each)
+        GPUS:embed:MODEL    embedding engine on each listed GPU
+
+    e.g. ``0-3:llama-3-8b;4-7:tp4:llama-3-70b;0-3:embed:nomic-embed-text``.
+    A GPU holds at most one chat engine (or one TP rank) and one embedder;
+    TP ranks carry no embedder.  Returns launch entries
+    ``{"gpus": [...], "tp": n, "chat": model | "", "embed": model | ""}``.
+    """
+    if not registry:
+        if tp > 1:
+            if len(gpus) % tp:
+                raise ValueError(f"{len(gpus)} GPUs do not split into TP={tp} groups")
+            return [{"gpus": gpus[i:i + tp], "tp": tp, "chat": chat_model, "embed": ""}
+                    for i in range(0, len(gpus), tp)]
+        eg = set(gpus if embed_gpus is None else embed_gpus)
+        return [{"gpus": [g], "tp": 1, "chat": chat_model,
+                 "embed": embed_model if embed_model and g in eg else ""} for g in gpus]
+    single: dict[int, dict] = {}
+    groups: list[dict] = []
+    in_group: set[int] = set()
+    for raw in registry.split(";"):
+        ent = raw.strip()
+        if not ent:
+            continue
+        parts = ent.split(":")
+        if len(parts) == 2:
+            gspec, role, model = parts[0], "chat", parts[1]
+        elif len(parts) == 3:
+            gspec, role, model = parts
+        else:
+            raise ValueError(f"bad registry entry {ent!r}")
+        model = model.strip()
+        role = role.strip().lower()
+        sel = _gpu_list(gspec)
+        if not sel or not model:
+            raise ValueError(f"bad registry entry {ent!r}")
+        unknown = [g for g in sel if g not in gpus]
+        if unknown:
+            raise ValueError(f"registry entry {ent!r}: GPUs {unknown} are not served")
+        if role.startswith("tp"):
+            n = int(role[2:])
+            if n < 1 or len(sel) % n:
+                raise ValueError(f"registry entry {ent!r}: {len(sel)} GPUs do not split into "
+                                 f"TP={n} groups")
+            for i in range(0, len(sel), n):
+                grp = sel[i:i + n]
+                for g in grp:
+                    if g in in_group or (g in single and single[g]["chat"]) or \
+                            (n > 1 and g in single):
+                        raise ValueError(f"GPU {g} is placed twice")
+                if n == 1:
+                    single.setdefault(grp[0], {"gpus": grp, "tp": 1, "chat": "", "embed": ""})
+                    single[grp[0]]["chat"] = model
+                else:
+                    in_group.update(grp)
+                    groups.append({"gpus": grp, "tp": n, "chat": model, "embed": ""})
+            continue
+        if role not in ("chat", "embed"):
+            raise ValueError(f"registry entry {ent!r}: role must be tpN, chat or embed")
+        for g in sel:
+            if g in in_group:
+                raise ValueError(f"GPU {g} is a TP rank and cannot host {model}")
+            w = single.setdefault(g, {"gpus": [g], "tp": 1, "chat": "", "embed": ""})
+            if w[role]:
+                raise ValueError(f"GPU {g} already has a {role} model ({w[role]})")
+            w[role] = model
+    return [single[g] for g in sorted(single)] + groups
+
+
 async def run_core(args, specs, procs=()):
     from aiohttp import web
 
@@ -92,37 +171,41 @@ def cmd_serve(args):
     gpus = _gpu_list(args.gpus) if args.gpus else [g.index for g in rocm_enum.enumerate_gpus()]
     if not gpus:
         sys.exit("no GPUs found (set --gpus or LMX_FAKE_GPUS)")
-    embed_gpus = set(_gpu_list(args.embed_gpus)) if args.embed_gpus else set(gpus)
+    try:
+        plan = plan_placement(gpus, args.chat_model, args.embed_model,
+                              _gpu_list(args.embed_gpus) if args.embed_gpus else None,
+                              args.tp, args.registry)
+    except ValueError as e:
+        sys.exit(f"placement: {e}")
     host = rocm_enum.host_id()
     procs, specs = [], []
     env = dict(os.environ)
     env.setdefault("CORE_GRPC_ADDR", "127.0.0.1" + args.grpc[args.grpc.rfind(":"):])
     env.setdefault("CORE_HTTP_URL", "http://127.0.0.1" + args.http[args.http.rfind(":"):])
-    if args.tp > 1:
-        groups = [gpus[i:i + args.tp] for i in range(0, len(gpus), args.tp)]
-        for grp in groups:
-            sock = f"/tmp/lmx-{host}-tp{args.tp}-gpu{grp[0]}.sock"
+    for w in plan:
+        grp, tp = w["gpus"], w["tp"]
+        if tp > 1:
+            sock = f"/tmp/lmx-{host}-tp{tp}-gpu{grp[0]}.sock"
             e = dict(env, HIP_VISIBLE_DEVICES=",".join(map(str, grp)))
             cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
                    f"--nproc-per-node={len(grp)}", "--master-addr", "127.0.0.1",
                    "--master-port", str(29500 + grp[0]), "-m", "llm_mcp_amd.worker.main",
-                   "--tp", str(args.tp), "--chat-model", args.chat_model, "--socket", sock]
+                   "--tp", str(tp), "--chat-model", w["chat"], "--socket", sock]
             procs.append(subprocess.Popen(cmd, env=e))
-            specs.append({"model": args.chat_model, "path": sock,
-                          "device": f"{host}:tp{args.tp}:gpu{grp[0]}-{grp[-1]}"})
-    else:
-        for g in gpus:
-            sock = f"/tmp/lmx-{host}-gpu{g}.sock"
-            cmd = [sys.executable, "-m", "llm_mcp_amd.worker.main", "--gpu", str(g),
-                   "--chat-model", args.chat_model, "--socket", sock,
-                   "--max-num-seqs", str(args.max_num_seqs)]
-            if args.embed_model and g in embed_gpus:
-                cmd += ["--embed-model", args.embed_model]
-            procs.append(subprocess.Popen(cmd, env=env))
-            if args.chat_model:
-                specs.append({"model": args.chat_model, "path": sock, "device": f"gpu{g}"})
-            if args.embed_model and g in embed_gpus:
-                specs.append({"model": args.embed_model, "path": sock, "device": f"gpu{g}"})
+            specs.append({"model": w["chat"], "path": sock,
+                          "device": f"{host}:tp{tp}:gpu{grp[0]}-{grp[-1]}"})
+            continue
+        g = grp[0]
+        sock = f"/tmp/lmx-{host}-gpu{g}.sock"
+        cmd = [sys.executable, "-m", "llm_mcp_amd.worker.main", "--gpu", str(g),
+               "--chat-model", w["chat"], "--socket", sock,
+               "--max-num-seqs", str(args.max_num_seqs)]
+        if w["embed"]:
+            cmd += ["--embed-model", w["embed"]]
+        procs.append(subprocess.Popen(cmd, env=env))
+        for m in (w["chat"], w["embed"]):
+            if m:
+                specs.append({"model": m, "path": sock, "device": f"gpu{g}"})
     try:
         asyncio.run(run_core(args, specs, procs))
     finally:
@@ -156,7 +239,11 @@ def main(argv=None):
             p.add_argument("--embed-model", default=os.environ.get("LMX_EMBED_MODEL", ""))
             p.add_argument("--embed-gpus", default="")
             p.add_argument("--tp", type=int, default=int(os.environ.get("LMX_TP", "1")))
-            p.add_argument("--max-num-seqs", type=int, default=256)
+            p.add_argument("--max-num-seqs", type=int,
+                           default=int(os.environ.get("LMX_MAX_BATCH", "256")))
+            p.add_argument("--registry", default=os.environ.get("LMX_MODEL_REGISTRY", ""),
+                           help="per-GPU placement, e.g. '0-3:llama-3-8b;4-7:tp4:llama-3-70b;"
+                                "0-3:embed:nomic-embed-text' (overrides --chat-model/--tp)")
         else:
             p.add_argument("--engine", action="append", default=[])
     sub.add_parser("worker", add_help=False)
