@@ -16,11 +16,16 @@ layer.  Tensor parallelism (Megatron column/row split) is built in: QKV and
 gate|up are split by heads / intermediate columns, O and down by rows, with
 one all-reduce after each (X1, X2); the LM head is vocab-split and gathered
 (X3).  Embeddings are replicated -- on a 288 GB part their memory is cheaper
-than an extra collective per step.
+than an extra collective per step.  Long steps (>= LMX_SP_MIN_TOKENS tokens)
+switch to sequence parallelism: each all-reduce becomes a reduce-scatter over
+token rows, RMSNorm + residual run on the rank's row block, and an all-gather
+feeds the next column-parallel GEMM (TPContext.reduce_scatter_rows /
+all_gather_rows).
 """
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 
 import torch
@@ -50,9 +55,52 @@ class StepInputs:
 class TPContext:
     """Tensor-parallel placement of this rank (size 1 = no TP)."""
 
-    def __init__(self, rank: int = 0, size: int = 1, group=None):
+    def __init__(self, rank: int = 0, size: int = 1, group=None,
+                 sp_min_tokens: int | None = None):
         self.rank, self.size, self.group = rank, size, group
         self.peer = None      # parallel.peer_allreduce.PeerAllReduce when enabled
+        # Sequence parallelism (SURVEY.md §2.4 "SP" row): steps with at least
+        # this many tokens keep the residual stream row-sharded across the TP
+        # group -- reduce-scatter after the row-parallel O / down GEMMs,
+        # RMSNorm + residual add on T/size rows, all-gather before the
+        # column-parallel QKV / gate-up GEMMs.  Same bytes on the wire as the
+        # all-reduce, 1/size of the norm work and residual memory.
+        if sp_min_tokens is None:
+            sp_min_tokens = int(os.environ.get("LMX_SP_MIN_TOKENS", "2048"))
+        self.sp_min_tokens = sp_min_tokens if sp_min_tokens > 0 else 1 << 62
+
+    def use_sp(self, num_tokens: int) -> bool:
+        return self.size > 1 and num_tokens >= self.sp_min_tokens
+
+    def reduce_scatter_rows(self, t: torch.Tensor, padded_rows: int) -> torch.Tensor:
+        """Sum ``t`` [T, d] over the group and return this rank's block of
+        ``padded_rows // size`` rows (rows past T count as zero)."""
+        rows, d = t.shape
+        if rows < padded_rows:
+            p = torch.zeros((padded_rows, d), dtype=t.dtype, device=t.device)
+            p[:rows] = t
+            t = p
+        s = padded_rows // self.size
+        if not t.is_cuda or self._host_staged(t):
+            # gloo: no reduce-scatter of device tensors -> all-reduce + slice
+            self.all_reduce(t)
+            return t[self.rank * s:(self.rank + 1) * s].clone()
+        out = torch.empty((s, d), dtype=t.dtype, device=t.device)
+        torch.distributed.reduce_scatter_tensor(out, t.contiguous(), group=self.group)
+        return out
+
+    def all_gather_rows(self, t: torch.Tensor) -> torch.Tensor:
+        """Concatenate every rank's [s, d] block into [size * s, d]."""
+        src = t.contiguous()
+        if not src.is_cuda or self._host_staged(src):
+            src = src.cpu()
+            parts = [torch.empty_like(src) for _ in range(self.size)]
+            torch.distributed.all_gather(parts, src, group=self.group)
+            return torch.cat(parts, dim=0).to(t.device, non_blocking=True)
+        out = torch.empty((self.size * src.shape[0], src.shape[1]), dtype=src.dtype,
+                          device=src.device)
+        torch.distributed.all_gather_into_tensor(out, src, group=self.group)
+        return out
 
     def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
         if self.size > 1:
@@ -161,7 +209,18 @@ class LlamaModel:
         cfg, w = self.cfg, self.w
         Hq, Hkv, D = self.Hq, self.Hkv, self.D
         T, nd = inp.num_tokens, inp.num_decode
-        x = ops.embed_gather(w["embed"], inp.input_ids)
+        tp = self.tp
+        sp = tp.use_sp(T)
+        if sp:
+            # residual stream row-sharded: this rank owns rows [rank*s, (rank+1)*s)
+            Tp = -(-T // tp.size) * tp.size
+            s = Tp // tp.size
+            ids = inp.input_ids
+            if Tp > T:
+                ids = torch.cat([ids, ids.new_zeros(Tp - T)])
+            x = ops.embed_gather(w["embed"], ids[tp.rank * s:(tp.rank + 1) * s].contiguous())
+        else:
+            x = ops.embed_gather(w["embed"], inp.input_ids)
         residual = None
         attn = torch.empty((T, Hq * D), dtype=self.dtype, device=self.device)
         for li, L in enumerate(w["layers"]):
@@ -170,6 +229,8 @@ class LlamaModel:
                 h = ops.rms_norm(x, L["ln1"], cfg.rms_eps)
             else:
                 h = ops.rms_norm(x, L["ln1"], cfg.rms_eps, residual=residual)
+            if sp:
+                h = tp.all_gather_rows(h)[:T]
             qkv = ops.linear(h, L["wqkv"])
             if "bqkv" in L:          # Qwen2: biased q/k/v
                 qkv += L["bqkv"]
@@ -185,16 +246,24 @@ class LlamaModel:
                 ops.paged_prefill_attention(qkv, kc, vc, inp.block_tables[nd:],
                                             inp.cu_q[nd:], inp.context_lens[nd:],
                                             inp.prefill_tiles, self.scale, attn, Hq=Hq)
-            o = self.tp.all_reduce(ops.linear(attn, L["wo"]))
+            o = ops.linear(attn, L["wo"])
+            o = tp.reduce_scatter_rows(o, Tp) if sp else tp.all_reduce(o)
             h = ops.rms_norm(o, L["ln2"], cfg.rms_eps, residual=residual)
+            if sp:
+                h = tp.all_gather_rows(h)[:T]
             gu = ops.linear(h, L["w_gate_up"])
             a = ops.silu_mul(gu)
-            x = self.tp.all_reduce(ops.linear(a, L["w_down"]))
+            x = ops.linear(a, L["w_down"])
+            x = tp.reduce_scatter_rows(x, Tp) if sp else tp.all_reduce(x)
         # final norm only on the rows we sample from
         rows = inp.sample_rows
-        xs = x.index_select(0, rows)
-        rs = residual.index_select(0, rows)
-        hs = ops.rms_norm(xs, w["norm"], cfg.rms_eps, residual=rs)
+        if sp:
+            hs = tp.all_gather_rows(ops.rms_norm(x, w["norm"], cfg.rms_eps,
+                                                 residual=residual))[:T].index_select(0, rows)
+        else:
+            xs = x.index_select(0, rows)
+            rs = residual.index_select(0, rows)
+            hs = ops.rms_norm(xs, w["norm"], cfg.rms_eps, residual=rs)
         logits = F.linear(hs, w["lm_head"])
         if self.tp.size > 1:
             logits = self.tp.all_gather_last(logits)[:, :cfg.vocab_size]

@@ -82,6 +82,7 @@ VARS: list[Var] = [
     Var("LMX_JOB_RETENTION_DAYS", float, 7.0, "purge finished jobs older than this"),
     Var("LMX_MAINTENANCE_INTERVAL", int, 60, "seconds between store maintenance ticks"),
     Var("LMX_JOB_STREAM_MAX_S", int, 3600, "max duration of one /v1/jobs/{id}/stream"),
+    Var("LMX_SP_MIN_TOKENS", int, 2048, "TP: steps with at least this many tokens run sequence-parallel (reduce-scatter/all-gather residual stream); 0 disables"),
     Var("LMX_PROGRESS_S", float, 2.0, "worker: cadence of job progress reports (tokens so far)"),
     Var("LMX_PEER_NODES", str, "", "other nodes' core URLs polled by discovery"),
     Var("LMX_PEER_PORTS", str, "8080", "core ports probed on mesh / subnet hosts"),

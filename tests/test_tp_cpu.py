@@ -32,9 +32,10 @@ def _ecfg():
                         max_model_len=512, use_graphs=False)
 
 
-def _rank_main(rank, size, port, ckpt, tag, q):
+def _rank_main(rank, size, port, ckpt, tag, q, sp_min_tokens=0):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
-                      WORLD_SIZE=str(size), LOCAL_RANK=str(rank))
+                      WORLD_SIZE=str(size), LOCAL_RANK=str(rank),
+                      LMX_SP_MIN_TOKENS=str(sp_min_tokens))
     torch.set_num_threads(2)
     import torch.distributed as dist
 
@@ -98,7 +99,12 @@ def test_plan_roundtrip(tmp_path):
     leader.close()
 
 
-def test_tp2_generation_matches_single_process(full_model):
+@pytest.mark.parametrize("sp_min_tokens", [0, 7])
+def test_tp2_generation_matches_single_process(full_model, sp_min_tokens):
+    """sp_min_tokens=7: every prefill / mixed step of >= 7 tokens runs
+    sequence-parallel (reduce-scatter + row-sharded RMSNorm + all-gather),
+    odd token counts included (padded rows); pure decode steps stay on the
+    all-reduce path."""
     m, path = full_model
     single = LLMEngine(_ecfg(), device="cpu", model_cfg=m.cfg, weights=m.w)
     ref_sampled = single.generate(PROMPTS[:2], SamplingParams(temperature=0.8, top_p=0.9,
@@ -107,7 +113,7 @@ def test_tp2_generation_matches_single_process(full_model):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port, tag = _free_port(), f"test-{os.getpid()}-{_free_port()}"
-    procs = [ctx.Process(target=_rank_main, args=(r, 2, port, path, tag, q), daemon=True)
+    procs = [ctx.Process(target=_rank_main, args=(r, 2, port, path, tag, q, sp_min_tokens), daemon=True)
              for r in range(2)]
     for p in procs:
         p.start()
