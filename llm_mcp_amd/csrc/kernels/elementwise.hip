@@ -19,39 +19,36 @@ __device__ __forceinline__ float gelu_tanh(float x) {
   return 0.5f * x * (1.f + tanhf(k0 * (x + k1 * x * x * x)));
 }
 
+// grid (rows, ceil(I/8 / 256)), block 256: one 16-byte chunk of gate and up
+// per thread.  2-D grid, so no per-element 64-bit division (multi-instruction
+// on CDNA); a 256-row decode step launches 256 x 14 workgroups for Llama-3-8B.
 template <int ACT>
 __global__ void __launch_bounds__(256) glu_kernel(bf16_t* __restrict__ out,
-                                                  const bf16_t* __restrict__ x, int I, long rows) {
-  const long nchunk = (long)rows * (I / 8);
-  const int cpr = I / 8;
-  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < nchunk;
-       e += (long)gridDim.x * blockDim.x) {
-    const long r = e / cpr;
-    const int c = (int)(e % cpr);
-    const bf16_t* xr = x + r * (2L * I);
-    const u16x8 g = *reinterpret_cast<const u16x8*>(xr + c * 8);
-    const u16x8 u = *reinterpret_cast<const u16x8*>(xr + I + c * 8);
-    u16x8 o;
+                                                  const bf16_t* __restrict__ x, int I) {
+  const int c = blockIdx.y * 256 + threadIdx.x;
+  if (c >= I / 8) return;
+  const long r = blockIdx.x;
+  const bf16_t* xr = x + r * (2L * I);
+  const u16x8 g = *reinterpret_cast<const u16x8*>(xr + c * 8);
+  const u16x8 u = *reinterpret_cast<const u16x8*>(xr + I + c * 8);
+  u16x8 o;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float gv = bf2f(g.v[j]);
-      const float a = ACT == 0 ? silu(gv) : gelu_tanh(gv);
-      o.v[j] = f2bf(a * bf2f(u.v[j]));
-    }
-    *reinterpret_cast<u16x8*>(out + r * I + c * 8) = o;
+  for (int j = 0; j < 8; ++j) {
+    const float gv = bf2f(g.v[j]);
+    const float a = ACT == 0 ? silu(gv) : gelu_tanh(gv);
+    o.v[j] = f2bf(a * bf2f(u.v[j]));
   }
+  *reinterpret_cast<u16x8*>(out + r * I + c * 8) = o;
 }
 
 int glu(void* out, const void* x, long rows, int I, int act, hipStream_t stream) {
   if (rows <= 0) return 0;
-  if (I % 8 != 0) return -1;
-  const long nchunk = rows * (I / 8);
-  long blocks = (nchunk + 255) / 256;
-  if (blocks > 4096) blocks = 4096;
+  if (I % 8 != 0 || rows > 0x7fffffffL) return -1;
+  const dim3 grid((unsigned)rows, (unsigned)((I / 8 + 255) / 256));
   if (act == 0)
-    glu_kernel<0><<<dim3((unsigned)blocks), dim3(256), 0, stream>>>((bf16_t*)out, (const bf16_t*)x, I, rows);
+    glu_kernel<0><<<grid, dim3(256), 0, stream>>>((bf16_t*)out, (const bf16_t*)x, I);
   else
-    glu_kernel<1><<<dim3((unsigned)blocks), dim3(256), 0, stream>>>((bf16_t*)out, (const bf16_t*)x, I, rows);
+    glu_kernel<1><<<grid, dim3(256), 0, stream>>>((bf16_t*)out, (const bf16_t*)x, I);
   return (int)hipGetLastError();
 }
 

@@ -229,8 +229,9 @@ def test_sample_top_k_top_p_support():
     assert torch.equal(tok, tok2)
 
 
-def test_silu_mul_gelu_mul():
-    x = _bf(77, 2 * 14336 // 4)
+@pytest.mark.parametrize("rows,I", [(77, 14336 // 4), (256, 14336), (3, 16), (1, 8 * 257)])
+def test_silu_mul_gelu_mul(rows, I):
+    x = _bf(rows, 2 * I)
     torch.testing.assert_close(ops.silu_mul(x).float(), ref.silu_mul(x).float(), atol=2e-2,
                                rtol=2e-2)
     torch.testing.assert_close(ops.gelu_mul(x).float(), ref.gelu_mul(x).float(), atol=2e-2,
