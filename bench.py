@@ -2,38 +2,53 @@
 """Headline benchmark: tokens/s + p50 TTFT via /v1/chat/completions,
 Llama-3-8B (bf16, random-init weights, synthetic prompts) on N MI355X.
 
-One process per GPU (torchrun / torch.distributed.run, RCCL process group):
-every rank serves a full data-parallel Llama-3-8B replica behind its own
-OpenAI-compatible HTTP server (aiohttp, SSE streaming, in-process engine with
-the gfx950 HIP kernels) and drives it with its own load-generator subprocess
-(started before the GPU is initialised).  One "step" = one wave of
-``--concurrency`` concurrent streaming chat requests per GPU, each with a
-``--prompt-len``-token synthetic prompt and ``--max-tokens`` generated tokens
-(ignore_eos).  W untimed warmup waves, then exactly K timed waves bracketed by
-barrier + device synchronize on both sides; the job value is the total
-completion tokens of all ranks divided by the slowest rank's time.
+Topology -- the product's serving path, one front door for the whole node:
 
-Prints ONE JSON line on rank 0 (driver contract).
+  rank r (one process per GPU, torch.distributed.run; the bench starts the
+          ranks itself when run without a launcher and --gpus > 1)
+      one Llama-3-8B engine on cuda:r (continuous batching, the gfx950 HIP
+      kernels, captured decode graphs) served on an engine socket
+      (engine/ipc.py) -- the GPU worker of ``python -m llm_mcp_amd serve``
+  rank 0, before it touches the GPU, also starts
+      * the FRONT DOOR: A API processes (api/serve.py) sharing ONE port via
+        SO_REUSEPORT, each attached to all N engines and routing every
+        stream with ModelRegistry.select (least loaded healthy replica)
+      * L load-generator processes (bench/loadgen.py) that together keep
+        N x C streaming chat requests in flight against that one port
+
+One "step" = one wave of N x ``--concurrency`` concurrent streaming chat
+requests (``--prompt-len``-char synthetic prompt, ``--max-tokens`` generated,
+ignore_eos).  W untimed warmup waves, then exactly K timed waves bracketed by
+a barrier + ``torch.cuda.synchronize()`` on both sides on every rank; the
+elapsed time is the max over ranks and the value is all completion tokens
+streamed to the clients divided by it (weak scaling: C streams per GPU).
+
+Prints ONE JSON line on rank 0 (driver contract).  ``--gpus`` must equal the
+launcher's WORLD_SIZE (a mismatch exits non-zero).  ``--rehearse-on-one-gpu``
+runs every rank on cuda:0 (a plumbing rehearsal on a 1-GPU box; its line is
+flagged and is never an N-GPU number).
 """
 from __future__ import annotations
 
 import argparse
-import asyncio
 import json
+import math
 import os
+import socket
 import subprocess
 import sys
-import threading
 import time
 
 BASELINE = None  # the reference publishes no throughput number (BASELINE.json "published": {})
+METRIC = "tokens/sec + p50 TTFT via /v1/chat/completions, Llama-3-8B at 1/2/4/8 MI355X"
+HERE = os.path.dirname(os.path.abspath(__file__))
 
 
 def log(msg: str) -> None:
     print(f"[bench r{os.environ.get('RANK', '0')}] {msg}", file=sys.stderr, flush=True)
 
 
-def main() -> None:
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
@@ -44,56 +59,102 @@ def main() -> None:
     ap.add_argument("--max-tokens", type=int, default=256)
     ap.add_argument("--temperature", type=float, default=0.8)
     ap.add_argument("--top-p", type=float, default=0.95)
-    ap.add_argument("--port-base", type=int, default=18080)
     ap.add_argument("--max-batched-tokens", type=int, default=16384)
+    ap.add_argument("--api-procs", type=int, default=0,
+                    help="front-door API processes on the shared port (0: ceil(N/2))")
+    ap.add_argument("--loadgen-procs", type=int, default=0,
+                    help="load-generator processes (0: N)")
     ap.add_argument("--no-graphs", action="store_true")
-    ap.add_argument("--inproc", action="store_true",
-                    help="serve HTTP from the GPU process (default: separate API process)")
     ap.add_argument("--rehearse-on-one-gpu", action="store_true",
-                    help="multi-rank rehearsal on a 1-GPU box: every rank uses device 0, gloo "
-                         "process group, a fixed KV budget (never used for reported numbers)")
-    a = ap.parse_args()
+                    help="multi-rank rehearsal on a 1-GPU box: every rank uses device 0 with a "
+                         "fixed KV budget (never used for reported numbers)")
+    return ap.parse_args(argv)
 
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    port = a.port_base + local_rank
+
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def self_launch(a) -> None:
+    """--gpus N > 1 without a launcher: start N ranks as CHILD processes
+    (nothing here has touched the GPU) and exit with their status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={a.gpus}", "--master-addr", "127.0.0.1",
+           "--master-port", str(free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    log("launching " + " ".join(cmd[2:]))
+    sys.exit(subprocess.call(cmd))
+
+
+def start_front_door(a, world: int, tag: str, socks: list[str]):
+    """Rank 0, before any HIP call: the API processes (one shared port) and
+    the load generators.  Returns (api procs, loadgen procs, url, ready files)."""
+    port = free_port()
     url = f"http://127.0.0.1:{port}"
-    sock = f"/tmp/lmx-bench-{os.getpid()}-{local_rank}.sock"
-
-    # children first: no process is started after this one touches the GPU
-    api_proc = None
-    if not a.inproc:
-        api_proc = subprocess.Popen(
+    n_api = a.api_procs or max(1, math.ceil(world / 2))
+    n_lg = a.loadgen_procs or world
+    engines = []
+    for r, s in enumerate(socks):
+        engines += ["--engine", f"{a.model}=unix:{s},device=gpu{r}"]
+    env = dict(os.environ, LOG_LEVEL=os.environ.get("LMX_BENCH_API_LOG", "WARNING"))
+    apis, ready_files = [], []
+    for i in range(n_api):
+        rf = f"/tmp/lmx-bench-{tag}-api{i}.ready"
+        if os.path.exists(rf):
+            os.unlink(rf)
+        ready_files.append(rf)
+        apis.append(subprocess.Popen(
             [sys.executable, "-m", "llm_mcp_amd.api.serve", "--port", str(port),
-             "--engine", f"{a.model}=unix:{sock},device=gpu{local_rank}"],
-            stdout=subprocess.DEVNULL)
-    client = subprocess.Popen(
-        [sys.executable, "-m", "llm_mcp_amd.bench.loadgen", "--serve-stdin", "--url", url,
-         "--model", a.model, "--concurrency", str(a.concurrency), "--prompt-len",
-         str(a.prompt_len), "--max-tokens", str(a.max_tokens), "--temperature",
-         str(a.temperature), "--top-p", str(a.top_p)],
-        stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
+             "--reuse-port", "--ready-file", rf] + engines,
+            cwd=HERE, env=env, stdout=subprocess.DEVNULL))
+    total = a.concurrency * world
+    per = [total // n_lg + (1 if i < total % n_lg else 0) for i in range(n_lg)]
+    lgs = []
+    for i, c in enumerate(per):
+        lgs.append(subprocess.Popen(
+            [sys.executable, "-m", "llm_mcp_amd.bench.loadgen", "--serve-stdin", "--url", url,
+             "--model", a.model, "--concurrency", str(c), "--prompt-len", str(a.prompt_len),
+             "--max-tokens", str(a.max_tokens), "--temperature", str(a.temperature),
+             "--top-p", str(a.top_p), "--seed-base", str(i + 1)],
+            cwd=HERE, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True))
+    return apis, lgs, url, ready_files
+
+
+def main() -> None:
+    a = parse()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        self_launch(a)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != a.gpus:
+        sys.exit(f"bench.py: --gpus {a.gpus} but the launcher started WORLD_SIZE={world} ranks")
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # all ranks of one launch share their parent (the torchrun agent)
+    tag = str(os.getppid() if "WORLD_SIZE" in os.environ and world > 1 else os.getpid())
+    socks = [f"/tmp/lmx-bench-{tag}-{r}.sock" for r in range(world)]
+
+    apis, lgs, ready_files = [], [], []
+    if rank == 0:
+        # children first: no process is started after this one touches the GPU
+        apis, lgs, url, ready_files = start_front_door(a, world, tag, socks)
 
     import torch
     import torch.distributed as dist
 
     from llm_mcp_amd import ops
-    from llm_mcp_amd.api.app import ServingState, make_app
-    from llm_mcp_amd.api.registry import LocalModel, ModelRegistry
-    from llm_mcp_amd.engine.async_engine import AsyncEngine
     from llm_mcp_amd.engine.engine import EngineConfig, LLMEngine
-    from llm_mcp_amd.models.tokenizer import for_model
-    from llm_mcp_amd.utils.metrics import Metrics
+    from llm_mcp_amd.engine.ipc import EngineServer
 
     gpu = 0 if a.rehearse_on_one_gpu else local_rank
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
     if world > 1:
-        if a.rehearse_on_one_gpu:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=dev)
+        # control plane only (barriers, timing, per-GPU stats): data-parallel
+        # serving exchanges no tensors between GPUs
+        import datetime
+        os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
+        dist.init_process_group("gloo", timeout=datetime.timedelta(minutes=60))
     ops.native()  # fail loudly if the HIP kernels are missing
 
     t_init = time.time()
@@ -103,148 +164,164 @@ def main() -> None:
                         use_graphs=not a.no_graphs, seed=rank,
                         kv_cache_gb=24 if a.rehearse_on_one_gpu else None)
     engine = LLMEngine(ecfg, device=dev)
-    log(f"engine ready in {time.time() - t_init:.1f}s: {engine.num_blocks} KV blocks, "
-        f"{len(engine.graphs)} decode graphs, weights {engine.model.weight_bytes() / 1e9:.1f} GB")
-    loop = None
-    if a.inproc:
-        aeng = AsyncEngine(engine)
-        reg = ModelRegistry()
-        reg.add(LocalModel(a.model, "chat", f"gpu{local_rank}", aeng, for_model(engine.cfg),
-                           engine.cfg, max_model_len=engine.max_model_len,
-                           capacity=ecfg.max_num_seqs))
-        state = ServingState(reg, Metrics())
-        state.register_routes = lambda app: app.router.add_get(
-            "/ready", lambda r: __import__("aiohttp").web.json_response({"ready": True}))
-
-        from aiohttp import web
-        loop = asyncio.new_event_loop()
-        started = threading.Event()
-
-        def serve():
-            asyncio.set_event_loop(loop)
-            runner = web.AppRunner(make_app(state), access_log=None)
-            loop.run_until_complete(runner.setup())
-            loop.run_until_complete(web.TCPSite(runner, "127.0.0.1", port).start())
-            aeng.start(loop)
-            started.set()
-            loop.run_forever()
-
-        threading.Thread(target=serve, daemon=True, name="http").start()
-        started.wait()
-    else:
-        from llm_mcp_amd.engine.ipc import EngineServer
-        server = EngineServer(engine, sock, info={
-            "kind": "chat", "model": a.model, "device_id": f"gpu{local_rank}",
-            "max_model_len": engine.max_model_len, "capacity": ecfg.max_num_seqs})
-        server.start()
-    ready = json.loads(client.stdout.readline())
-    if not ready.get("ready"):
-        raise RuntimeError("load generator could not reach the server")
-
-    def run_wave():
-        client.stdin.write("run\n")
-        client.stdin.flush()
-        line = client.stdout.readline()
-        if not line:
-            raise RuntimeError("load generator exited")
-        return json.loads(line)
+    log(f"engine ready on cuda:{gpu} in {time.time() - t_init:.1f}s: {engine.num_blocks} KV "
+        f"blocks, {len(engine.graphs)} decode graphs, "
+        f"weights {engine.model.weight_bytes() / 1e9:.1f} GB")
+    server = EngineServer(engine, socks[rank], info={
+        "kind": "chat", "model": a.model, "device_id": f"gpu{rank}",
+        "max_model_len": engine.max_model_len, "capacity": ecfg.max_num_seqs})
+    server.start()
 
     def barrier():
         if world > 1:
             dist.barrier()
 
-    for w in range(a.warmup):
-        r = run_wave()
-        log(f"warmup {w}: {r['tokens']} tok in {r['elapsed']:.2f}s ({r['tok_s']:.0f} tok/s), "
-            f"ttft p50 {r['ttft_p50'] * 1e3:.0f} ms")
+    def waves(n: int, label: str) -> list[dict]:
+        out = []
+        for k in range(n):
+            for p in lgs:
+                p.stdin.write("run\n")
+                p.stdin.flush()
+            parts = []
+            for p in lgs:
+                line = p.stdout.readline()
+                if not line:
+                    raise RuntimeError("load generator exited")
+                parts.append(json.loads(line))
+            r = {"tokens": sum(x["tokens"] for x in parts),
+                 "elapsed": max(x["elapsed"] for x in parts),
+                 "requests": sum(x["requests"] for x in parts),
+                 "ttfts": [t for x in parts for t in x["ttfts"]],
+                 "itls": [t for x in parts for t in x["itls"]]}
+            out.append(r)
+            from llm_mcp_amd.bench.loadgen import percentile as pct
+            log(f"{label} {k}: {r['requests']} streams, {r['tokens']} tok in {r['elapsed']:.2f}s "
+                f"({r['tokens'] / r['elapsed']:.0f} tok/s), ttft p50 "
+                f"{pct(r['ttfts'], 50) * 1e3:.0f} ms, itl p50 {pct(r['itls'], 50) * 1e3:.1f} ms")
+        return out
+
+    import psutil
+    if rank == 0:
+        t_wait = time.time()
+        while not all(os.path.exists(f) for f in ready_files):
+            if any(p.poll() is not None for p in apis):
+                raise RuntimeError("a front-door API process exited")
+            if time.time() - t_wait > 1800:
+                raise RuntimeError("front door never attached every engine")
+            time.sleep(0.2)
+        for p in lgs:
+            ready = json.loads(p.stdout.readline())
+            if not ready.get("ready"):
+                raise RuntimeError("load generator could not reach the front door")
+        log(f"front door up: {len(apis)} API processes on {url}, {len(lgs)} load generators, "
+            f"{a.concurrency * world} streams per wave over {world} engines")
+    barrier()
+    if rank == 0:
+        waves(a.warmup, "warmup")
+    barrier()
+
     for k in engine.stats:
         engine.stats[k] = type(engine.stats[k])(0)
     engine.ttft_samples.clear()
-    import psutil
-    procs = {"engine": psutil.Process(), "loadgen": psutil.Process(client.pid)}
-    if api_proc is not None:
-        procs["api"] = psutil.Process(api_proc.pid)
-    cpu0 = {k: sum(p.cpu_times()[:2]) for k, p in procs.items()}
+    procs = {"engine": [psutil.Process()]}
+    if rank == 0:
+        procs["api"] = [psutil.Process(p.pid) for p in apis]
+        procs["loadgen"] = [psutil.Process(p.pid) for p in lgs]
+
+    def cpu_s(ps):
+        return sum(sum(p.cpu_times()[:2]) for p in ps)
+    cpu0 = {k: cpu_s(v) for k, v in procs.items()}
+
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    results = []
-    for k in range(a.steps):
-        r = run_wave()
-        results.append(r)
-        log(f"step {k}: {r['tokens']} tok in {r['elapsed']:.2f}s ({r['tok_s']:.0f} tok/s), "
-            f"ttft p50 {r['ttft_p50'] * 1e3:.0f} ms, itl p50 {r['itl_p50'] * 1e3:.1f} ms")
+    results = waves(a.steps, "step") if rank == 0 else []
+    barrier()           # the other ranks serve until rank 0's waves are done
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
 
-    log("process CPU utilisation over the timed waves: " + ", ".join(
-        f"{k} {(sum(p.cpu_times()[:2]) - cpu0[k]) / elapsed * 100:.0f}%" for k, p in procs.items()))
+    cpu = {k: (cpu_s(v) - cpu0[k]) / elapsed * 100 for k, v in procs.items()}
     st = engine.stats
     ns = max(1, st["steps"])
+    log("process CPU % over the timed waves: " + ", ".join(f"{k} {v:.0f}%" for k, v in cpu.items()))
     log("engine host phases (ms/step avg over all steps): " + ", ".join(
         f"{k[2:]} {st[k] / ns * 1e3:.3f}" for k in st if k.startswith("t_")) +
         f"; steps {st['steps']} graph {st['graph_steps']}, decode step "
         f"{st['decode_step_s'] / max(1, st['graph_steps']) * 1e3:.2f} ms")
-    if engine.ttft_samples:
-        from llm_mcp_amd.bench.loadgen import percentile as _pct
-        et = [f - a for a, f in engine.ttft_samples]
-        log(f"engine-side TTFT (submit -> first token emitted) p50 {_pct(et, 50) * 1e3:.0f} ms, "
-            f"p95 {_pct(et, 95) * 1e3:.0f} ms over {len(et)} requests")
-    tokens = sum(r["tokens"] for r in results)
-    ttfts = [t for r in results for t in r["ttfts"]]
-    mine = {"tokens": tokens, "elapsed": elapsed, "ttfts": ttfts,
-            "itl": [r["itl_p50"] for r in results]}
+    mine = {"rank": rank, "elapsed": elapsed, "gen_tokens": int(st["generated_tokens"]),
+            "finished": int(st["finished"]), "steps": int(st["steps"]),
+            "graph_steps": int(st["graph_steps"]),
+            "decode_ms": st["decode_step_s"] / max(1, st["graph_steps"]) * 1e3,
+            "engine_cpu_pct": cpu["engine"]}
     if world > 1:
         allr = [None] * world
         dist.all_gather_object(allr, mine)
     else:
         allr = [mine]
-    client.stdin.write("quit\n")
-    client.stdin.flush()
+
+    for p in lgs:
+        p.stdin.write("quit\n")
+        p.stdin.flush()
     if rank == 0:
         from llm_mcp_amd.bench.loadgen import percentile
-        tot = sum(x["tokens"] for x in allr)
         slow = max(x["elapsed"] for x in allr)
-        all_ttft = [t for x in allr for t in x["ttfts"]]
-        value = tot / slow
-        st = engine.stats
+        tokens = sum(r["tokens"] for r in results)
+        ttfts = [t for r in results for t in r["ttfts"]]
+        itls = [t for r in results for t in r["itls"]]
+        value = tokens / slow
+        per_gpu = [round(x["gen_tokens"] / slow, 1) for x in allr]
+        nz = [v for v in per_gpu if v > 0]
         out = {
-            "metric": "tokens/sec + p50 TTFT via /v1/chat/completions, Llama-3-8B at 1/2/4/8 MI355X",
+            "metric": METRIC,
             "value": round(value, 1), "unit": "tokens/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(slow / a.steps * 1e3, 2),
             "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None if BASELINE is None else round(value / BASELINE, 3),
             "dtype": "bf16",
             "data": "synthetic prompts, random-init weights",
-            "ttft_p50_ms": round(percentile(all_ttft, 50) * 1e3, 1),
-            "ttft_p95_ms": round(percentile(all_ttft, 95) * 1e3, 1),
-            "itl_p50_ms": round(percentile([i for x in allr for i in x["itl"]], 50) * 1e3, 2),
+            "ttft_p50_ms": round(percentile(ttfts, 50) * 1e3, 1),
+            "ttft_p95_ms": round(percentile(ttfts, 95) * 1e3, 1),
+            "itl_p50_ms": round(percentile(itls, 50) * 1e3, 2),
+            "per_gpu_tok_s": per_gpu,
+            "gpu_balance_max_over_min": round(max(nz) / min(nz), 3) if nz else None,
+            "decode_step_ms": [round(x["decode_ms"], 2) for x in allr],
+            "front_door_cpu_pct": round(cpu.get("api", 0.0), 1),
+            "loadgen_cpu_pct": round(cpu.get("loadgen", 0.0), 1),
+            "engine_cpu_pct": [round(x["engine_cpu_pct"], 1) for x in allr],
             "config": {"model": a.model, "global_batch": a.concurrency * world,
                        "seq_len": a.prompt_len + a.max_tokens, "prompt_len": a.prompt_len,
                        "max_tokens": a.max_tokens, "parallelism": f"dp{world}",
                        "endpoint": "/v1/chat/completions stream=true",
-                       "serving": "in-process" if a.inproc else "api process + engine process (unix socket)",
+                       "serving": f"{world} engine rank(s) behind one front door: {len(apis)} "
+                                  f"API process(es) on one SO_REUSEPORT port, replica "
+                                  f"selection per stream; {len(lgs)} load generator(s)",
                        "sampling": {"temperature": a.temperature, "top_p": a.top_p},
-                       "engine_steps": st["steps"], "graph_steps": st["graph_steps"]},
+                       "engine_steps": sum(x["steps"] for x in allr),
+                       "graph_steps": sum(x["graph_steps"] for x in allr)},
         }
+        if a.rehearse_on_one_gpu:
+            out["rehearsal_one_gpu"] = True
+            out["config"]["parallelism"] += " (rehearsal: every rank on cuda:0, NOT an "\
+                                            f"{world}-GPU number)"
         print(json.dumps(out), flush=True)
     barrier()
-    try:
-        client.wait(timeout=30)
-    except Exception:
-        client.kill()
-    engine.stop()
-    if loop is not None:
-        loop.call_soon_threadsafe(loop.stop)
-    if api_proc is not None:
-        api_proc.terminate()
+    for p in lgs:
         try:
-            api_proc.wait(timeout=10)
-        except Exception:
-            api_proc.kill()
-        if os.path.exists(sock):
-            os.unlink(sock)
+            p.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            p.kill()
+    server.stop()
+    for p in apis:
+        p.terminate()
+    for p in apis:
+        try:
+            p.wait(timeout=10)
+        except subprocess.TimeoutExpired:
+            p.kill()
+    for f in ready_files:
+        if os.path.exists(f):
+            os.unlink(f)
     if world > 1:
         dist.destroy_process_group()
 

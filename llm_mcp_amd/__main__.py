@@ -153,17 +153,90 @@ async def run_core(args, specs, procs=()):
 
     async def watch():
         while not stop.is_set():
-            for p in procs:
-                if p.poll() is not None:
-                    log.error("worker pid %d exited with %s", p.pid, p.returncode)
-                    await asyncio.to_thread(st.discovery.run)
-            await asyncio.sleep(5)
+            died = await asyncio.to_thread(procs.poll) if isinstance(procs, Supervisor) else []
+            if died:
+                # replicas of a dead worker already left the registry (its engine
+                # link closed, api/serve.py); discovery marks its devices' state
+                await asyncio.to_thread(st.discovery.run)
+            await asyncio.sleep(SUPERVISE_TICK_S)
 
     w = asyncio.create_task(watch())
     await stop.wait()
     w.cancel()
+    for t in getattr(st, "engine_links", []):
+        t.cancel()
     await grpc_srv.stop(5)   # drain gRPC too (the reference only shut down HTTP)
     await runner.cleanup()
+
+
+SUPERVISE_TICK_S = 1.0
+
+
+class Supervisor:
+    """Keeps the GPU worker processes of ``serve`` alive.
+
+    Each worker is a child process started from a command line; the parent
+    (which never initialises HIP) starts a FRESH child when one exits -- never
+    a re-exec of a process that touched the GPU -- with exponential backoff
+    (``LMX_RESTART_BACKOFF_S`` doubling up to ``LMX_RESTART_MAX_S``; reset
+    after a worker stayed up for a minute).  The reference gets the same
+    behaviour from its process manager (compose.yml:117,133,149
+    ``restart: unless-stopped``, k8s Deployments)."""
+
+    def __init__(self, restart: bool = True):
+        self.restart = restart
+        self.entries: list[dict] = []
+        self.base = float(os.environ.get("LMX_RESTART_BACKOFF_S", "1"))
+        self.cap = float(os.environ.get("LMX_RESTART_MAX_S", "60"))
+
+    def spawn(self, cmd: list[str], env: dict, name: str) -> subprocess.Popen:
+        import time
+        p = subprocess.Popen(cmd, env=env)
+        self.entries.append({"cmd": cmd, "env": env, "name": name, "proc": p,
+                             "started": time.time(), "backoff": self.base,
+                             "restart_at": None, "restarts": 0})
+        return p
+
+    def poll(self) -> list[str]:
+        """Reap exited workers and (re)start the ones whose backoff expired.
+        Returns the names of workers found dead on this tick."""
+        import time
+        now, died = time.time(), []
+        for e in self.entries:
+            p = e["proc"]
+            if p is not None and p.poll() is not None:
+                log.error("worker %s (pid %d) exited with %s", e["name"], p.pid, p.returncode)
+                died.append(e["name"])
+                if now - e["started"] > 60:
+                    e["backoff"] = self.base
+                e["proc"] = None
+                e["restart_at"] = now + e["backoff"] if self.restart else None
+                e["backoff"] = min(self.cap, e["backoff"] * 2)
+            if e["proc"] is None and e["restart_at"] is not None and now >= e["restart_at"]:
+                e["proc"] = subprocess.Popen(e["cmd"], env=e["env"])
+                e["started"], e["restart_at"] = now, None
+                e["restarts"] += 1
+                log.warning("worker %s restarted (pid %d, restart #%d)", e["name"],
+                            e["proc"].pid, e["restarts"])
+        return died
+
+    def __iter__(self):
+        return iter([e["proc"] for e in self.entries if e["proc"] is not None])
+
+    def __len__(self):
+        return len(self.entries)
+
+    def stop(self, timeout: float = 20) -> None:
+        for e in self.entries:
+            e["restart_at"] = None
+        live = [e["proc"] for e in self.entries if e["proc"] is not None]
+        for p in live:
+            p.terminate()
+        for p in live:
+            try:
+                p.wait(timeout=timeout)
+            except subprocess.TimeoutExpired:
+                p.kill()
 
 
 def cmd_serve(args):
@@ -178,44 +251,42 @@ def cmd_serve(args):
     except ValueError as e:
         sys.exit(f"placement: {e}")
     host = rocm_enum.host_id()
-    procs, specs = [], []
+    sup = Supervisor(restart=not args.no_restart)
+    specs = []
     env = dict(os.environ)
     env.setdefault("CORE_GRPC_ADDR", "127.0.0.1" + args.grpc[args.grpc.rfind(":"):])
     env.setdefault("CORE_HTTP_URL", "http://127.0.0.1" + args.http[args.http.rfind(":"):])
+    sock_dir = args.socket_dir or "/tmp"
+    extra = ["--cpu"] if args.cpu else []
     for w in plan:
         grp, tp = w["gpus"], w["tp"]
         if tp > 1:
-            sock = f"/tmp/lmx-{host}-tp{tp}-gpu{grp[0]}.sock"
+            sock = os.path.join(sock_dir, f"lmx-{host}-tp{tp}-gpu{grp[0]}.sock")
             e = dict(env, HIP_VISIBLE_DEVICES=",".join(map(str, grp)))
             cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
                    f"--nproc-per-node={len(grp)}", "--master-addr", "127.0.0.1",
                    "--master-port", str(29500 + grp[0]), "-m", "llm_mcp_amd.worker.main",
-                   "--tp", str(tp), "--chat-model", w["chat"], "--socket", sock]
-            procs.append(subprocess.Popen(cmd, env=e))
+                   "--tp", str(tp), "--chat-model", w["chat"], "--socket", sock,
+                   "--max-num-seqs", str(args.max_num_seqs)] + extra
+            sup.spawn(cmd, e, f"tp{tp}:gpu{grp[0]}-{grp[-1]}")
             specs.append({"model": w["chat"], "path": sock,
                           "device": f"{host}:tp{tp}:gpu{grp[0]}-{grp[-1]}"})
             continue
         g = grp[0]
-        sock = f"/tmp/lmx-{host}-gpu{g}.sock"
+        sock = os.path.join(sock_dir, f"lmx-{host}-gpu{g}.sock")
         cmd = [sys.executable, "-m", "llm_mcp_amd.worker.main", "--gpu", str(g),
                "--chat-model", w["chat"], "--socket", sock,
-               "--max-num-seqs", str(args.max_num_seqs)]
+               "--max-num-seqs", str(args.max_num_seqs)] + extra
         if w["embed"]:
             cmd += ["--embed-model", w["embed"]]
-        procs.append(subprocess.Popen(cmd, env=env))
+        sup.spawn(cmd, env, f"gpu{g}")
         for m in (w["chat"], w["embed"]):
             if m:
                 specs.append({"model": m, "path": sock, "device": f"gpu{g}"})
     try:
-        asyncio.run(run_core(args, specs, procs))
+        asyncio.run(run_core(args, specs, sup))
     finally:
-        for p in procs:
-            p.terminate()
-        for p in procs:
-            try:
-                p.wait(timeout=20)
-            except subprocess.TimeoutExpired:
-                p.kill()
+        sup.stop()
 
 
 def cmd_core(args):
@@ -244,6 +315,11 @@ def main(argv=None):
             p.add_argument("--registry", default=os.environ.get("LMX_MODEL_REGISTRY", ""),
                            help="per-GPU placement, e.g. '0-3:llama-3-8b;4-7:tp4:llama-3-70b;"
                                 "0-3:embed:nomic-embed-text' (overrides --chat-model/--tp)")
+            p.add_argument("--no-restart", action="store_true",
+                           help="do not restart GPU workers that exit")
+            p.add_argument("--socket-dir", default=os.environ.get("LMX_SOCKET_DIR", ""))
+            p.add_argument("--cpu", action="store_true",
+                           help="workers run their engines on the CPU (tests / plumbing)")
         else:
             p.add_argument("--engine", action="append", default=[])
     sub.add_parser("worker", add_help=False)

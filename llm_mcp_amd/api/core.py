@@ -102,7 +102,8 @@ class CoreState:
 
         async def ready(request):
             return write_json(200 if self.engines_ready else 503,
-                              {"ready": self.engines_ready, "models": self.registry.model_ids()})
+                              {"ready": self.engines_ready, "models": self.registry.model_ids(),
+                               "replicas": len(self.registry.all())})
         app.router.add_get("/ready", ready)
         if self.embed_handler is not None:
             h = self.embed_handler

@@ -44,6 +44,13 @@ class LocalModel:
         if sched is not None:
             d.update(kv_usage=round(sched.kv_usage, 4), running=sched.num_running,
                      waiting=sched.num_waiting)
+        else:
+            # engine in a worker process: the link's last polled info (api/serve.py)
+            live = self.tags.get("live") or {}
+            if "kv_usage" in live:
+                d.update(kv_usage=round(float(live["kv_usage"]), 4),
+                         running=int(live.get("running", 0)),
+                         waiting=int(live.get("waiting", 0)))
         comm = getattr(eng, "tp_comm", None) or self.tags.get("tp_comm")
         if comm:
             d["tp_comm"] = comm       # TP all-reduce probe, us by message size
@@ -62,6 +69,16 @@ class ModelRegistry:
     def add(self, m: LocalModel) -> None:
         with self._lock:
             self._models.setdefault(self.canonical(m.model_id), []).append(m)
+
+    def remove(self, m: LocalModel) -> None:
+        """Drop one replica (by identity), e.g. when its worker died."""
+        with self._lock:
+            k = self.canonical(m.model_id)
+            lst = [x for x in self._models.get(k, []) if x is not m]
+            if lst:
+                self._models[k] = lst
+            else:
+                self._models.pop(k, None)
 
     def remove_device(self, device_id: str) -> None:
         with self._lock:

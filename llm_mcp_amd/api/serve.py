@@ -6,6 +6,18 @@ their Unix sockets (engine/ipc.py).  Engines are given as
 ``--engine MODEL=unix:/path[,device=gpu0]`` (repeatable); the process keeps
 retrying until every engine socket is up, and ``GET /ready`` turns 200 once
 all are connected (``/health`` answers immediately, as in the reference).
+
+Engine links are supervised: when a worker process dies its replicas leave
+the registry (new requests route to the survivors, its in-flight streams end
+with ``finish_reason: "error"``) and the link re-attaches as soon as a
+replacement worker opens the socket again -- the in-process form of the
+reference's restartable worker units (compose.yml:117,133,149
+``restart: unless-stopped``).
+
+Several API processes can share one port (``--reuse-port``, SO_REUSEPORT):
+the kernel spreads client connections over them and every process balances
+its own streams over all engines, so one event loop does not bound the
+node's SSE rate (bench.py runs the front door this way).
 """
 from __future__ import annotations
 
@@ -29,6 +41,8 @@ from .registry import LocalModel, ModelRegistry
 log = logging.getLogger("lmx.serve")
 _ATTACH = web.AppKey("attach", asyncio.Task)
 
+LIVE_INFO_S = float(os.environ.get("LMX_ENGINE_INFO_S", "5"))
+
 
 def parse_engine_spec(spec: str) -> dict:
     model, rest = spec.split("=", 1)
@@ -40,30 +54,67 @@ def parse_engine_spec(spec: str) -> dict:
     return out
 
 
-async def attach_engines(state, specs: list[dict]):
-    clients = []
-    for s in specs:
+async def _link(state, s: dict, first: asyncio.Future, supervise: bool) -> None:
+    """One engine link: connect, register the replica, keep its live info
+    (KV usage, running / waiting, step stats) fresh, and on disconnect drop
+    the replica and re-attach when the socket comes back."""
+    cfg = mc.resolve(s["model"])
+    tok = for_model(cfg, s.get("tokenizer"))
+    while True:
         c = EngineClient(s["path"])
-        clients.append((s, c))
-
-    async def one(s, c):
         await c.connect()
-        info = await c.info(timeout=30)
-        info = {**info, **(info.get("models") or {}).get(s["model"], {})}
-        cfg = mc.resolve(s["model"])
-        state.registry.add(LocalModel(
-            s["model"], info.get("kind", "chat"), s.get("device") or info.get("device_id", "gpu0"),
-            c, for_model(cfg, s.get("tokenizer")), cfg,
-            max_model_len=int(info.get("max_model_len", 8192)),
-            capacity=int(info.get("capacity", 256)),
-            tags={"tp_comm": info.get("tp_comm") or {}}))
-        log.info("engine %s on %s connected", s["model"], s["path"])
+        try:
+            info = await c.info(timeout=30)
+        except (ConnectionError, asyncio.TimeoutError) as e:
+            log.warning("engine %s on %s: info failed (%s); retrying", s["model"], s["path"], e)
+            await c.close()
+            await asyncio.sleep(0.5)
+            continue
+        minfo = {**info, **(info.get("models") or {}).get(s["model"], {})}
+        lm = LocalModel(
+            s["model"], minfo.get("kind", "chat"),
+            s.get("device") or minfo.get("device_id", "gpu0"), c, tok, cfg,
+            max_model_len=int(minfo.get("max_model_len", 8192)),
+            capacity=int(minfo.get("capacity", 256)),
+            tags={"tp_comm": minfo.get("tp_comm") or {}, "live": info})
+        state.registry.add(lm)
+        log.info("engine %s on %s connected (%s)", s["model"], s["path"], lm.device_id)
+        if not first.done():
+            first.set_result(True)
 
-    await asyncio.gather(*[one(s, c) for s, c in clients])
+        async def poll():
+            while c.connected.is_set():
+                await asyncio.sleep(LIVE_INFO_S)
+                try:
+                    lm.tags["live"] = await c.info(timeout=LIVE_INFO_S)
+                except (ConnectionError, asyncio.TimeoutError, RuntimeError):
+                    pass
+
+        poller = asyncio.create_task(poll())
+        await c.wait_closed()
+        poller.cancel()
+        state.registry.remove(lm)
+        log.error("engine %s on %s (%s) disconnected; replica removed", s["model"],
+                  s["path"], lm.device_id)
+        if not supervise:
+            return
+        await asyncio.sleep(0.5)
+
+
+async def attach_engines(state, specs: list[dict], supervise: bool = True):
+    """Attach every engine; returns once each has connected once (then
+    ``state.engines_ready``).  The link tasks stay alive on
+    ``state.engine_links`` and re-attach restarted workers."""
+    loop = asyncio.get_running_loop()
+    firsts = [loop.create_future() for _ in specs]
+    links = [asyncio.create_task(_link(state, s, f, supervise)) for s, f in zip(specs, firsts)]
+    state.engine_links = getattr(state, "engine_links", []) + links
+    if firsts:
+        await asyncio.gather(*firsts)
     state.engines_ready = True
 
 
-def make_serving_app(specs: list[dict], version: str | None = None):
+def make_serving_app(specs: list[dict], version: str | None = None, ready_file: str = ""):
     """The API process's app: chat + embeddings + /ready over attached
     engine sockets (attached on startup)."""
     state = ServingState(ModelRegistry(), Metrics(),
@@ -75,7 +126,8 @@ def make_serving_app(specs: list[dict], version: str | None = None):
         async def ready(request):
             ok = getattr(state, "engines_ready", False)
             return write_json(200 if ok else 503, {"ready": ok,
-                                                    "models": state.registry.model_ids()})
+                                                    "models": state.registry.model_ids(),
+                                                    "replicas": len(state.registry.all())})
         app.router.add_get("/ready", ready)
         emb = EmbeddingsHandler(state)
 
@@ -86,10 +138,21 @@ def make_serving_app(specs: list[dict], version: str | None = None):
     state.register_routes = register
     app = make_app(state)
 
+    async def attach():
+        await attach_engines(state, specs)
+        if ready_file:
+            with open(ready_file, "w") as f:
+                f.write(str(os.getpid()))
+
     async def on_start(app):
-        app[_ATTACH] = asyncio.create_task(attach_engines(state, specs))
+        app[_ATTACH] = asyncio.create_task(attach())
+
+    async def on_cleanup(app):
+        for t in getattr(state, "engine_links", []):
+            t.cancel()
 
     app.on_startup.append(on_start)
+    app.on_cleanup.append(on_cleanup)
     return app, state
 
 
@@ -99,10 +162,15 @@ def main(argv=None):
     ap.add_argument("--port", type=int, default=int(os.environ.get("LMX_HTTP_PORT", "8080")))
     ap.add_argument("--engine", action="append", default=[],
                     help="MODEL=unix:/path[,device=gpu0][,tokenizer=/dir]")
+    ap.add_argument("--reuse-port", action="store_true",
+                    help="SO_REUSEPORT: several API processes serve one port")
+    ap.add_argument("--ready-file", default="",
+                    help="written once every engine is attached")
     a = ap.parse_args(argv)
     logging.basicConfig(level=os.environ.get("LOG_LEVEL", "INFO"))
-    app, _ = make_serving_app([parse_engine_spec(s) for s in a.engine])
-    web.run_app(app, host=a.host, port=a.port, access_log=None, print=None)
+    app, _ = make_serving_app([parse_engine_spec(s) for s in a.engine], ready_file=a.ready_file)
+    web.run_app(app, host=a.host, port=a.port, access_log=None, print=None,
+                reuse_port=a.reuse_port or None)
 
 
 if __name__ == "__main__":

@@ -83,7 +83,7 @@ async def wave(url, model, concurrency, prompt_len, max_tokens, temperature, top
     ttfts = [r["ttft"] for r in res]
     tok = sum(r["tokens"] for r in res)
     itl = [r["decode_s"] / (r["tokens"] - 1) for r in res if r["tokens"] > 1]
-    return {"elapsed": el, "tokens": tok, "requests": len(res), "ttfts": ttfts,
+    return {"elapsed": el, "tokens": tok, "requests": len(res), "ttfts": ttfts, "itls": itl,
             "ttft_p50": percentile(ttfts, 50), "ttft_p95": percentile(ttfts, 95),
             "itl_p50": percentile(itl, 50), "tok_s": tok / el if el > 0 else 0.0}
 
@@ -112,6 +112,9 @@ def main(argv=None):
     ap.add_argument("--temperature", type=float, default=0.8)
     ap.add_argument("--top-p", type=float, default=0.95)
     ap.add_argument("--waves", type=int, default=1)
+    ap.add_argument("--seed-base", type=int, default=0,
+                    help="distinct per load-generator process (distinct prompts, no "
+                         "accidental prefix-cache hits across generators)")
     ap.add_argument("--serve-stdin", action="store_true",
                     help="wait for 'run' commands on stdin (bench.py client mode)")
     a = ap.parse_args(argv)
@@ -126,14 +129,17 @@ def main(argv=None):
                 break
             if cmd.startswith("run"):
                 r = loop.run_until_complete(wave(a.url, a.model, a.concurrency, a.prompt_len,
-                                                 a.max_tokens, a.temperature, a.top_p, i))
+                                                 a.max_tokens, a.temperature, a.top_p,
+                                                 (a.seed_base << 20) + i))
                 i += 1
                 print(json.dumps(r), flush=True)
         return
     for i in range(a.waves):
         r = loop.run_until_complete(wave(a.url, a.model, a.concurrency, a.prompt_len,
-                                         a.max_tokens, a.temperature, a.top_p, i))
+                                         a.max_tokens, a.temperature, a.top_p,
+                                         (a.seed_base << 20) + i))
         r.pop("ttfts")
+        r.pop("itls")
         print(json.dumps(r), flush=True)
 
 

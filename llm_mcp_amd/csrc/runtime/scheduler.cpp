@@ -139,7 +139,14 @@ const StepPlan& Scheduler::schedule(int q_per_tile) {
       s->num_computed = bm_.match_prefix(s->id, s->tokens.data(), (int)s->tokens.size());
     const int remaining = (int)s->tokens.size() - s->num_computed;
     const int n = std::min(remaining, budget);
-    if (!bm_.ensure(s->id, s->num_computed + n)) break;
+    if (!bm_.ensure(s->id, s->num_computed + n)) {
+      // a waiting sequence must not keep the prefix pages it just matched:
+      // with every runner preempted, waiting sequences each pinning their
+      // cached prefix could fill the cache and admit nobody (deadlock)
+      bm_.free_seq(s->id);
+      s->num_computed = 0;
+      break;
+    }
     waiting_.pop_front();
     s->status = RUNNING;
     running_.push_back(s);
@@ -237,7 +244,9 @@ std::vector<std::pair<int64_t, int>> Scheduler::update(const int32_t* sampled, i
     if (!s->ignore_eos &&
         std::find(s->stop_ids.begin(), s->stop_ids.end(), tok) != s->stop_ids.end())
       reason = FR_STOP;
-    else if (s->num_generated >= s->max_new || (int)s->tokens.size() >= max_model_len_)
+    else if (s->num_generated >= s->max_new || (int)s->tokens.size() >= max_model_len_ ||
+             // a sequence longer than the whole KV cache could never be re-admitted
+             (int)s->tokens.size() >= bm_.num_blocks() * bm_.block_size())
       reason = FR_LENGTH;
     if (reason != FR_NONE) {
       finish(s, reason);

@@ -264,6 +264,16 @@ class EngineClient:
             self.connected.clear()
             for q in self._queues.values():
                 q.put_nowait(StreamItem(-1, 0.0, "error:engine_disconnected"))
+            for f in self._info_waiters.values():
+                if not f.done():
+                    f.set_exception(ConnectionError("engine disconnected"))
+            self._info_waiters.clear()
+
+    async def wait_closed(self) -> None:
+        """Return once the link to the engine process is gone (the worker
+        died or closed its socket); pending streams have been failed by then."""
+        if self._reader_task is not None:
+            await asyncio.wait([self._reader_task])
 
     def _send(self, obj):
         if self._writer is None or not self.connected.is_set():

@@ -66,7 +66,7 @@ class TPContext:
         # column-parallel QKV / gate-up GEMMs.  Same bytes on the wire as the
         # all-reduce, 1/size of the norm work and residual memory.
         if sp_min_tokens is None:
-            sp_min_tokens = int(os.environ.get("LMX_SP_MIN_TOKENS", "2048"))
+            sp_min_tokens = int(os.environ.get("LMX_SP_MIN_TOKENS", "0"))
         self.sp_min_tokens = sp_min_tokens if sp_min_tokens > 0 else 1 << 62
 
     def use_sp(self, num_tokens: int) -> bool:

@@ -11,6 +11,9 @@ leader pays one memcpy per step.
 Layout of the mailbox file (``/dev/shm``):
     [0:8)    seq     (u64) -- bumped by the leader after the payload is written
     [8:16)   nbytes  (u64)
+    [16:24)  beat    (u64) -- leader heartbeat, wall-clock ns, rewritten every
+                              ``BEAT_S`` by a leader thread (also while idle)
+    [24:32)  pid     (u64) -- leader process id
     [64 + 8r) ack[r] (u64) -- last seq follower r has copied out
     [4096:)  payload (msgpack)
 The leader waits until every follower acked the previous message before
@@ -21,6 +24,7 @@ from __future__ import annotations
 
 import os
 import tempfile
+import threading
 import time
 
 import msgpack
@@ -30,6 +34,16 @@ _HDR = 4096
 PLAN_KEYS = ("input_ids", "positions", "slots", "context_lens", "cu_q", "block_tables",
              "prefill_tiles", "sample_rows", "seq_ids", "temp", "topk", "topp", "seeds", "offs")
 PLAN_INTS = ("num_decode", "max_blocks", "num_tokens", "num_prefill_tokens", "max_context")
+BEAT_S = 1.0
+
+
+class LeaderLost(RuntimeError):
+    """The TP leader died or stopped beating: the follower must exit so its
+    launcher can tear the group down (and the supervisor start a new one)."""
+
+
+def leader_timeout_s() -> float:
+    return float(os.environ.get("LMX_TP_LEADER_TIMEOUT_S", "30"))
 
 
 def encode_plan(plan: dict, bucket: int | None) -> dict:
@@ -80,6 +94,37 @@ class PlanChannel:
         # a follower may attach after the leader already published: resume
         # from its own ack slot (0 on a fresh mailbox), not from the head
         self._seq = int(self.ctl[0]) if create else int(self.ctl[8 + rank])
+        self._beat_stop = threading.Event()
+        self._beat_thread = None
+        if create:
+            self.ctl[3] = os.getpid()
+            self.ctl[2] = time.time_ns()
+            self._beat_thread = threading.Thread(target=self._beat, daemon=True, name="tp-beat")
+            self._beat_thread.start()
+
+    def _beat(self):
+        while not self._beat_stop.wait(BEAT_S):
+            try:
+                self.ctl[2] = time.time_ns()
+            except (TypeError, ValueError, AttributeError):
+                return   # mailbox closed
+
+    def leader_alive(self, timeout_s: float | None = None) -> tuple[bool, str]:
+        """Follower-side liveness of the leader: its pid exists and its
+        heartbeat is younger than ``timeout_s``."""
+        pid = int(self.ctl[3])
+        if pid:
+            try:
+                os.kill(pid, 0)
+            except ProcessLookupError:
+                return False, f"leader pid {pid} is gone"
+            except PermissionError:
+                pass
+        age = (time.time_ns() - int(self.ctl[2])) / 1e9
+        lim = leader_timeout_s() if timeout_s is None else timeout_s
+        if int(self.ctl[2]) and age > lim:
+            return False, f"leader heartbeat is {age:.1f}s old (limit {lim:.0f}s)"
+        return True, ""
 
     # ---------------------------------------------------------- leader ----
     def publish(self, msg: dict, timeout: float = 300.0) -> None:
@@ -100,12 +145,22 @@ class PlanChannel:
         self.ctl[0] = self._seq   # x86-64 stores are not reordered after the payload
 
     # -------------------------------------------------------- follower ----
-    def receive(self, idle_sleep: float = 0.0005) -> dict:
+    def receive(self, idle_sleep: float = 0.0005, timeout_s: float | None = None) -> dict:
+        """Next plan.  Raises ``LeaderLost`` when the leader process is gone or
+        its heartbeat is older than ``timeout_s`` (LMX_TP_LEADER_TIMEOUT_S),
+        so a crashed leader never strands the followers' GPUs."""
         spins = 0
+        next_check = 0.0
         while int(self.ctl[0]) == self._seq:
             spins += 1
             if spins > 5000:
                 time.sleep(idle_sleep)
+                now = time.monotonic()
+                if now >= next_check:
+                    next_check = now + 0.5
+                    ok, why = self.leader_alive(timeout_s)
+                    if not ok:
+                        raise LeaderLost(why)
         self._seq = int(self.ctl[0])
         n = int(self.ctl[1])
         data = bytes(self.mm[_HDR:_HDR + n])
@@ -113,6 +168,9 @@ class PlanChannel:
         return msgpack.unpackb(data, raw=False)
 
     def close(self):
+        self._beat_stop.set()
+        if self._beat_thread is not None:
+            self._beat_thread.join(timeout=5)
         del self.ctl
         self.mm._mmap.close()
         if self.owner:

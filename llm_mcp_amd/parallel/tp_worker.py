@@ -23,7 +23,7 @@ import torch
 import torch.distributed as dist
 
 from ..models.llama import TPContext
-from .plan_channel import PlanChannel, mailbox_path
+from .plan_channel import LeaderLost, PlanChannel, mailbox_path
 
 log = logging.getLogger("lmx.tp")
 
@@ -124,8 +124,11 @@ def run_tp_worker(a) -> None:
     from ..devices import rocm_enum
     from ..engine.engine import EngineConfig
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    if getattr(a, "cpu", False):
+        dev = torch.device("cpu")      # gloo group (tests / plumbing)
+    else:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
     tp = init_group(dev)
     if tp.size != a.tp:
         raise SystemExit(f"--tp {a.tp} but the launcher started {tp.size} ranks")
@@ -147,7 +150,15 @@ def run_tp_worker(a) -> None:
             finally:
                 engine.release_followers()
         else:
-            engine.run_follower()
+            try:
+                engine.run_follower()
+            except LeaderLost as e:
+                # the group is gone: exit non-zero at once (a collective
+                # teardown could wait forever on the dead leader) so the
+                # launcher ends the group and the supervisor starts a new one
+                log.error("TP rank %d: %s; exiting", tp.rank, e)
+                logging.shutdown()
+                os._exit(3)
     finally:
         if engine.chan is not None:
             engine.chan.close()

@@ -82,7 +82,12 @@ VARS: list[Var] = [
     Var("LMX_JOB_RETENTION_DAYS", float, 7.0, "purge finished jobs older than this"),
     Var("LMX_MAINTENANCE_INTERVAL", int, 60, "seconds between store maintenance ticks"),
     Var("LMX_JOB_STREAM_MAX_S", int, 3600, "max duration of one /v1/jobs/{id}/stream"),
-    Var("LMX_SP_MIN_TOKENS", int, 2048, "TP: steps with at least this many tokens run sequence-parallel (reduce-scatter/all-gather residual stream); 0 disables"),
+    Var("LMX_SP_MIN_TOKENS", int, 0, "TP: steps with at least this many tokens run sequence-parallel (reduce-scatter/all-gather residual stream); 0 disables (default until the RCCL branch is measured on a multi-GPU node)"),
+    Var("LMX_TP_LEADER_TIMEOUT_S", float, 30.0, "TP follower: exit when the leader's mailbox heartbeat is older than this (or its pid is gone)"),
+    Var("LMX_ENGINE_INFO_S", float, 5.0, "API process: cadence of live engine info polls (KV usage, running, waiting)"),
+    Var("LMX_RESTART_BACKOFF_S", float, 1.0, "serve: first restart delay of a dead GPU worker (doubles per consecutive death)"),
+    Var("LMX_RESTART_MAX_S", float, 60.0, "serve: cap of the worker restart backoff"),
+    Var("LMX_SOCKET_DIR", str, "", "serve: directory of the engine sockets (default /tmp)"),
     Var("LMX_PROGRESS_S", float, 2.0, "worker: cadence of job progress reports (tokens so far)"),
     Var("LMX_PEER_NODES", str, "", "other nodes' core URLs polled by discovery"),
     Var("LMX_PEER_PORTS", str, "8080", "core ports probed on mesh / subnet hosts"),

@@ -35,6 +35,8 @@ def build_parser():
     ap.add_argument("--embed-weights", default="",
                     help="safetensors dir of the embedding model (nomic-bert or BERT; optional)")
     ap.add_argument("--tp", type=int, default=1)
+    ap.add_argument("--cpu", action="store_true",
+                    help="run the engines on the CPU (tests / plumbing; device ids stay gpuN)")
     return ap
 
 
@@ -50,8 +52,11 @@ def main(argv=None):
     from ..engine.engine import EngineConfig, LLMEngine
     from ..models import config as mc
 
-    torch.cuda.set_device(a.gpu)
-    dev = torch.device("cuda", a.gpu)
+    if a.cpu:
+        dev = torch.device("cpu")
+    else:
+        torch.cuda.set_device(a.gpu)
+        dev = torch.device("cuda", a.gpu)
     engine = embed = None
     if a.embed_model:
         from ..engine.embed_engine import EmbeddingEngine

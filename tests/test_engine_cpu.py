@@ -91,3 +91,24 @@ def test_qwen3_qk_norm_matches_dense():
     for p, o in zip(prompts, outs):
         assert len(o) == 5
         assert_greedy_consistent(e.model, p, o)
+
+
+def test_waiting_sequences_do_not_pin_prefix_pages():
+    """Regression: preempted sequences sharing a cached prefix used to keep the
+    pages matched at (failed) re-admission, filling the KV cache with waiting
+    sequences and admitting nobody -- every request stalled forever."""
+    import threading
+    e = LLMEngine(EngineConfig(model="tiny-llama", max_num_seqs=16, max_batched_tokens=2048,
+                               max_model_len=1024, use_graphs=False), device="cpu")
+    assert e.num_blocks == 64
+    shared = list(range(100, 140))
+    prompts = [shared + [200 + i, 300 + i] for i in range(8)]
+    out = {}
+    t = threading.Thread(target=lambda: out.setdefault("o", e.generate(
+        prompts, SamplingParams(temperature=0.7, max_tokens=300, ignore_eos=True, seed=3))),
+        daemon=True)
+    t.start()
+    t.join(timeout=240)
+    assert not t.is_alive(), (e.sched.num_running, e.sched.num_waiting, e.sched.kv_usage)
+    assert [len(o) for o in out["o"]] == [300] * 8
+    assert e.sched.preemptions > 0
