@@ -27,7 +27,7 @@ int paged_prefill(const void*, long, const void*, const void*, const int*, int, 
                   hipStream_t);
 int sample(const void*, int, long, int, int, const float*, const int*, const float*,
            const uint64_t*, const int*, int*, float*, int, hipStream_t);
-int glu(void*, const void*, long, int, int, hipStream_t);
+int glu(void*, const void*, long, int, int, int, hipStream_t);
 int apply_penalties(void*, long, int, int, const int*, const int*, const float*, const int*, int,
                     hipStream_t);
 int embed_gather(void*, const void*, const int*, int, int, int, int, hipStream_t);
@@ -37,6 +37,12 @@ int gemm_splitk(void*, const void*, const void*, float*, int*, int, int, int, lo
                 int, hipStream_t);
 int gemm_nt(void*, const void*, const void*, const void*, const void*, int, int, int, long, long,
             long, int, hipStream_t);
+int dgemm(void*, const void*, const void*, float*, unsigned*, int, int, int, int, long, long, long,
+          int, int, int, hipStream_t);
+int dgemm_num_configs();
+int rmsnorm_slabs(void*, void*, const float*, int, long, const void*, int, int, long, float,
+                  hipStream_t);
+int dgemm_config(int, int*, int*);
 long ar_region_bytes(long);
 int ar_alloc(void**, long);
 int ar_free(void*);
@@ -119,8 +125,8 @@ PYBIND11_MODULE(_lmx_kernels, m) {
                       P<float>(out_lp), max_rounds, S(stream)),
           "sample");
   });
-  m.def("glu", [](uptr out, uptr x, long rows, int I, int act, uptr stream) {
-    check(lmx::glu(P<void>(out), P<void>(x), rows, I, act, S(stream)), "glu");
+  m.def("glu", [](uptr out, uptr x, long rows, int I, int act, int block, uptr stream) {
+    check(lmx::glu(P<void>(out), P<void>(x), rows, I, act, block, S(stream)), "glu");
   });
   m.def("embed_gather", [](uptr out, uptr table, uptr ids, int T, int d, int vs, int vr,
                            uptr stream) {
@@ -141,6 +147,28 @@ PYBIND11_MODULE(_lmx_kernels, m) {
     check(lmx::gemm_splitk(P<void>(C), P<void>(A), P<void>(W), P<float>(slabs), P<int>(tickets), M,
                            N, K, lda, ldw, ldc, splits, S(stream)),
           "gemm_splitk");
+  });
+  m.def("dgemm", [](uptr C, uptr A, uptr W, uptr slabs, uptr tickets, int n_tickets, int M, int N,
+                    int K, long lda, long ldw, long ldc, int cfg, int splits, int epi,
+                    uptr stream) {
+    check(lmx::dgemm(P<void>(C), P<void>(A), P<void>(W), P<float>(slabs), P<unsigned>(tickets),
+                     n_tickets, M, N, K, lda, ldw, ldc, cfg, splits, epi, S(stream)),
+          "dgemm");
+  });
+  m.def("rmsnorm_slabs", [](uptr out, uptr residual, uptr slabs, int nsl, long slab_stride,
+                            uptr w, int rows, int cols, long out_stride, float eps, uptr stream) {
+    check(lmx::rmsnorm_slabs(P<void>(out), P<void>(residual), P<float>(slabs), nsl, slab_stride,
+                             P<void>(w), rows, cols, out_stride, eps, S(stream)),
+          "rmsnorm_slabs");
+  });
+  m.def("dgemm_configs", []() {
+    std::vector<std::pair<int, int>> out;
+    for (int i = 0; i < lmx::dgemm_num_configs(); ++i) {
+      int bm = 0, bn = 0;
+      lmx::dgemm_config(i, &bm, &bn);
+      out.emplace_back(bm, bn);
+    }
+    return out;
   });
   // ---- peer-memory all-reduce (allreduce.hip) ----
   m.def("ar_region_bytes", [](long slot) { return lmx::ar_region_bytes(slot); });

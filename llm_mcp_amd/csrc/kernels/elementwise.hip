@@ -22,15 +22,22 @@ __device__ __forceinline__ float gelu_tanh(float x) {
 // grid (rows, ceil(I/8 / 256)), block 256: one 16-byte chunk of gate and up
 // per thread.  2-D grid, so no per-element 64-bit division (multi-instruction
 // on CDNA); a 256-row decode step launches 256 x 14 workgroups for Llama-3-8B.
+// ``block`` > 0: the gate|up columns are interleaved per block (the layout of
+// the fused-SwiGLU decode GEMM weights, dgemm.hip): gate channel i sits at
+// column (i / block) * 2 * block + i % block and its up partner block later.
 template <int ACT>
 __global__ void __launch_bounds__(256) glu_kernel(bf16_t* __restrict__ out,
-                                                  const bf16_t* __restrict__ x, int I) {
+                                                  const bf16_t* __restrict__ x, int I,
+                                                  int block) {
   const int c = blockIdx.y * 256 + threadIdx.x;
   if (c >= I / 8) return;
   const long r = blockIdx.x;
   const bf16_t* xr = x + r * (2L * I);
-  const u16x8 g = *reinterpret_cast<const u16x8*>(xr + c * 8);
-  const u16x8 u = *reinterpret_cast<const u16x8*>(xr + I + c * 8);
+  const int gi = c * 8;
+  const int go = block > 0 ? (gi / block) * 2 * block + gi % block : gi;
+  const int uo = block > 0 ? go + block : I + gi;
+  const u16x8 g = *reinterpret_cast<const u16x8*>(xr + go);
+  const u16x8 u = *reinterpret_cast<const u16x8*>(xr + uo);
   u16x8 o;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -41,14 +48,16 @@ __global__ void __launch_bounds__(256) glu_kernel(bf16_t* __restrict__ out,
   *reinterpret_cast<u16x8*>(out + r * I + c * 8) = o;
 }
 
-int glu(void* out, const void* x, long rows, int I, int act, hipStream_t stream) {
+int glu(void* out, const void* x, long rows, int I, int act, int block, hipStream_t stream) {
   if (rows <= 0) return 0;
-  if (I % 8 != 0 || rows > 0x7fffffffL) return -1;
+  if (I % 8 != 0 || rows > 0x7fffffffL || block < 0 || block % 8 != 0 ||
+      (block > 0 && I % block != 0))
+    return -1;
   const dim3 grid((unsigned)rows, (unsigned)((I / 8 + 255) / 256));
   if (act == 0)
-    glu_kernel<0><<<grid, dim3(256), 0, stream>>>((bf16_t*)out, (const bf16_t*)x, I);
+    glu_kernel<0><<<grid, dim3(256), 0, stream>>>((bf16_t*)out, (const bf16_t*)x, I, block);
   else
-    glu_kernel<1><<<grid, dim3(256), 0, stream>>>((bf16_t*)out, (const bf16_t*)x, I);
+    glu_kernel<1><<<grid, dim3(256), 0, stream>>>((bf16_t*)out, (const bf16_t*)x, I, block);
   return (int)hipGetLastError();
 }
 

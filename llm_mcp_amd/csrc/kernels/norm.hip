@@ -70,6 +70,67 @@ __global__ void __launch_bounds__(256) rmsnorm_kernel(
   }
 }
 
+// RMSNorm whose input is the S fp32 split-K partial slabs of the preceding
+// projection (dgemm.hip epi 2, "partials only"): the K-split reduction, the
+// residual add and the norm in one pass, so the projection needs neither a
+// reduction pass nor a bf16 output round trip.  residual += sum_s slab[s]
+// (rounded to bf16 once, as the bf16 hidden state), out = rms_norm(residual).
+template <int VPT>
+__global__ void __launch_bounds__(256) rmsnorm_slabs_kernel(
+    bf16_t* __restrict__ out, bf16_t* __restrict__ residual, const float* __restrict__ slabs,
+    int S, long slab_stride, const bf16_t* __restrict__ w, int cols, long out_stride,
+    float eps) {
+  __shared__ float scratch[16];
+  const int row = blockIdx.x;
+  const float* xr = slabs + (long)row * cols;
+  bf16_t* orow = out + (long)row * out_stride;
+  bf16_t* rr = residual + (long)row * cols;
+  const int nchunk = cols >> 3;
+  float v[VPT][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = threadIdx.x + i * blockDim.x;
+    if (c < nchunk) {
+      f32x4_t a0 = *reinterpret_cast<const f32x4_t*>(xr + c * 8);
+      f32x4_t a1 = *reinterpret_cast<const f32x4_t*>(xr + c * 8 + 4);
+      for (int s = 1; s < S; ++s) {
+        a0 += *reinterpret_cast<const f32x4_t*>(xr + s * slab_stride + c * 8);
+        a1 += *reinterpret_cast<const f32x4_t*>(xr + s * slab_stride + c * 8 + 4);
+      }
+      const u16x8 b = *reinterpret_cast<const u16x8*>(rr + c * 8);
+      u16x8 h;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint16_t hb = f2bf((j < 4 ? a0[j] : a1[j - 4]) + bf2f(b.v[j]));
+        h.v[j] = hb;
+        v[i][j] = bf2f(hb);
+        ss += v[i][j] * v[i][j];
+      }
+      *reinterpret_cast<u16x8*>(rr + c * 8) = h;
+    }
+  }
+  u16x8 wvs[VPT];
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = threadIdx.x + i * blockDim.x;
+    if (c < nchunk) wvs[i] = *reinterpret_cast<const u16x8*>(w + c * 8);
+  }
+  ss = block_sum(ss, scratch);
+  const float inv = rsqrtf(ss / (float)cols + eps);
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = threadIdx.x + i * blockDim.x;
+    if (c < nchunk) {
+      const u16x8 wv = wvs[i];
+      u16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o.v[j] = f2bf(v[i][j] * inv * bf2f(wv.v[j]));
+      *reinterpret_cast<u16x8*>(orow + c * 8) = o;
+    }
+  }
+}
+
 template <int VPT>
 __global__ void __launch_bounds__(256) layernorm_kernel(
     bf16_t* __restrict__ out, const bf16_t* __restrict__ x, const bf16_t* __restrict__ residual,
@@ -144,6 +205,27 @@ int rmsnorm(void* out, void* residual, const void* x, const void* w, int rows, i
   else if (vpt <= 8) LMX_RMS(8);
   else return -2;
 #undef LMX_RMS
+  return (int)hipGetLastError();
+}
+
+int rmsnorm_slabs(void* out, void* residual, const float* slabs, int S, long slab_stride,
+                  const void* w, int rows, int cols, long out_stride, float eps,
+                  hipStream_t stream) {
+  if (cols % 8 != 0 || rows <= 0 || S < 1 || residual == nullptr) return -1;
+  const int nchunk = cols / 8;
+  const int threads = pick_threads(nchunk);
+  const int vpt = (nchunk + threads - 1) / threads;
+  dim3 g(rows), b(threads);
+#define LMX_RMSS(V)                                                                         \
+  rmsnorm_slabs_kernel<V><<<g, b, 0, stream>>>((bf16_t*)out, (bf16_t*)residual, slabs, S,   \
+                                               slab_stride, (const bf16_t*)w, cols,         \
+                                               out_stride, eps)
+  if (vpt <= 1) LMX_RMSS(1);
+  else if (vpt <= 2) LMX_RMSS(2);
+  else if (vpt <= 4) LMX_RMSS(4);
+  else if (vpt <= 8) LMX_RMSS(8);
+  else return -2;
+#undef LMX_RMSS
   return (int)hipGetLastError();
 }
 

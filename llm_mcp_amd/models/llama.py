@@ -154,6 +154,15 @@ class LlamaModel:
         if weights is None:
             weights = self._random_weights(seed)
         self.w = weights
+        # fused-SwiGLU decode GEMM (K11 epi=1): gate|up rows interleaved per
+        # BN/2 channels when the measured dispatch table uses it for this shape
+        self.gu_block = 0
+        if self.device.type == "cuda":
+            blk = ops.swiglu_block(2 * self.I, cfg.hidden_size)
+            if blk:
+                for L in self.w["layers"]:
+                    L["w_gate_up"] = ops.interleave_gate_up(L["w_gate_up"], blk)
+                self.gu_block = blk
 
     # ----------------------------------------------------------- weights ----
     def _random_weights(self, seed: int) -> dict:
@@ -246,15 +255,23 @@ class LlamaModel:
                 ops.paged_prefill_attention(qkv, kc, vc, inp.block_tables[nd:],
                                             inp.cu_q[nd:], inp.context_lens[nd:],
                                             inp.prefill_tiles, self.scale, attn, Hq=Hq)
-            o = ops.linear(attn, L["wo"])
-            o = tp.reduce_scatter_rows(o, Tp) if sp else tp.all_reduce(o)
+            # TP = 1: the O projection may hand its split-K partials straight
+            # to the residual-add RMSNorm (ops.Partials; K11 epi 2)
+            o = ops.linear(attn, L["wo"], defer=tp.size == 1)
+            if tp.size > 1:
+                o = tp.reduce_scatter_rows(o, Tp) if sp else tp.all_reduce(o)
             h = ops.rms_norm(o, L["ln2"], cfg.rms_eps, residual=residual)
             if sp:
                 h = tp.all_gather_rows(h)[:T]
-            gu = ops.linear(h, L["w_gate_up"])
-            a = ops.silu_mul(gu)
-            x = ops.linear(a, L["w_down"])
-            x = tp.reduce_scatter_rows(x, Tp) if sp else tp.all_reduce(x)
+            if self.gu_block:
+                a = ops.linear_swiglu(h, L["w_gate_up"], self.gu_block)
+            else:
+                a = ops.silu_mul(ops.linear(h, L["w_gate_up"]))
+            # down's partials go to the next layer's input norm (not after the
+            # last layer: the final norm runs on the sampled rows only)
+            x = ops.linear(a, L["w_down"], defer=tp.size == 1 and li + 1 < len(w["layers"]))
+            if tp.size > 1:
+                x = tp.reduce_scatter_rows(x, Tp) if sp else tp.all_reduce(x)
         # final norm only on the rows we sample from
         rows = inp.sample_rows
         if sp:
@@ -264,7 +281,7 @@ class LlamaModel:
             xs = x.index_select(0, rows)
             rs = residual.index_select(0, rows)
             hs = ops.rms_norm(xs, w["norm"], cfg.rms_eps, residual=rs)
-        logits = F.linear(hs, w["lm_head"])
+        logits = ops.linear(hs, w["lm_head"])
         if self.tp.size > 1:
             logits = self.tp.all_gather_last(logits)[:, :cfg.vocab_size]
         return logits

@@ -98,11 +98,36 @@ def _bf16(t: torch.Tensor, name: str) -> None:
 
 
 # ------------------------------------------------------------------ norms ---
-def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float,
+class Partials:
+    """Split-K fp32 partial slabs [S, M, N] of a projection whose K reduction
+    is deferred to the consuming kernel (dgemm epi 2 -> rms_norm)."""
+    __slots__ = ("slabs", "S", "M", "N")
+
+    def __init__(self, slabs: torch.Tensor, S: int, M: int, N: int):
+        self.slabs, self.S, self.M, self.N = slabs, S, M, N
+
+    @property
+    def shape(self):
+        return (self.M, self.N)
+
+    def sum(self) -> torch.Tensor:
+        return self.slabs.sum(0)
+
+
+def rms_norm(x, w: torch.Tensor, eps: float,
              residual: torch.Tensor | None = None,
              out: torch.Tensor | None = None) -> torch.Tensor:
     """y = rmsnorm(x [+ residual]) * w.  With ``residual`` the sum is written
-    back into ``residual`` (fused residual add).  ``x`` may be row-strided."""
+    back into ``residual`` (fused residual add).  ``x`` may be row-strided, or
+    ``Partials`` (deferred split-K slabs, summed here; needs ``residual``)."""
+    if isinstance(x, Partials):
+        _chk(residual is not None and residual.is_contiguous()
+             and residual.shape == (x.M, x.N), "rms_norm over partials needs the residual")
+        if out is None:
+            out = torch.empty((x.M, x.N), dtype=residual.dtype, device=residual.device)
+        native().rmsnorm_slabs(_ptr(out), _ptr(residual), _ptr(x.slabs), x.S, x.M * x.N,
+                               _ptr(w), x.M, x.N, out.stride(0), float(eps), _stream())
+        return out
     if not x.is_cuda:
         y = ref.rms_norm(x, w, eps, residual)
         if out is not None:
@@ -300,9 +325,17 @@ def apply_penalties(logits: torch.Tensor, window: torch.Tensor, ngen: torch.Tens
 
 
 # ------------------------------------------------------------ elementwise ---
-def silu_mul(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+def deinterleave_gate_up(x: torch.Tensor, block: int) -> torch.Tensor:
+    """Inverse column permutation of ``interleave_gate_up(w, block)``'s output."""
+    I = x.shape[-1] // 2
+    return x.view(*x.shape[:-1], I // block, 2, block).transpose(-3, -2).reshape(x.shape)
+
+
+def silu_mul(x: torch.Tensor, out: torch.Tensor | None = None, block: int = 0) -> torch.Tensor:
+    """silu(gate) * up of a fused gate|up projection output; ``block`` > 0:
+    the columns are interleaved per block (``interleave_gate_up(w, block)``)."""
     if not x.is_cuda:
-        y = ref.silu_mul(x)
+        y = ref.silu_mul(deinterleave_gate_up(x, block) if block else x)
         if out is not None:
             out.copy_(y)
             return out
@@ -310,10 +343,11 @@ def silu_mul(x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     _bf16(x, "x")
     _chk(x.is_contiguous() and x.shape[-1] % 16 == 0, "silu_mul shape")
     I = x.shape[-1] // 2
+    _chk(block % 8 == 0 and (block == 0 or I % block == 0), "silu_mul interleave block")
     rows = x.numel() // x.shape[-1]
     if out is None:
         out = torch.empty(x.shape[:-1] + (I,), dtype=x.dtype, device=x.device)
-    native().glu(_ptr(out), _ptr(x), rows, I, 0, _stream())
+    native().glu(_ptr(out), _ptr(x), rows, I, 0, block, _stream())
     return out
 
 
@@ -324,7 +358,7 @@ def gelu_mul(x: torch.Tensor) -> torch.Tensor:
     I = x.shape[-1] // 2
     rows = x.numel() // x.shape[-1]
     out = torch.empty(x.shape[:-1] + (I,), dtype=x.dtype, device=x.device)
-    native().glu(_ptr(out), _ptr(x), rows, I, 1, _stream())
+    native().glu(_ptr(out), _ptr(x), rows, I, 1, 0, _stream())
     return out
 
 
@@ -378,13 +412,14 @@ ACT_SWIGLU = 3
 ACT_GELU_ERF = 4   # exact (erf) GELU, BERT FFNs
 
 
-def interleave_gate_up(w: torch.Tensor) -> torch.Tensor:
-    """[gate(I); up(I)] rows -> per 64 channels [gate 64 | up 64], the layout
-    of gemm_nt's fused SwiGLU epilogue (act=3)."""
+def interleave_gate_up(w: torch.Tensor, block: int = 64) -> torch.Tensor:
+    """[gate(I); up(I)] rows -> per ``block`` channels [gate block | up block],
+    the layout of the fused SwiGLU epilogues (gemm_nt act=3: block 64;
+    dgemm epi=1: block BN/2)."""
     I2, d = w.shape
     I = I2 // 2
-    _chk(I % 64 == 0, "intermediate size must be a multiple of 64")
-    return w.view(2, I // 64, 64, d).transpose(0, 1).reshape(I2, d).contiguous()
+    _chk(I % block == 0, f"intermediate size must be a multiple of {block}")
+    return w.view(2, I // block, block, d).transpose(0, 1).reshape(I2, d).contiguous()
 
 
 def gemm_nt(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, act: int = 0,
@@ -517,9 +552,157 @@ def splitk_preferred(M: int, N: int, K: int) -> bool:
     return False
 
 
-def linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-    """x @ w^T: the split-K MFMA kernel where it was measured faster, else
-    hipBLASLt (torch F.linear)."""
-    if x.is_cuda and x.dim() == 2 and splitk_preferred(x.shape[0], w.shape[0], w.shape[1]):
-        return gemm_splitk(x, w)
+def linear(x: torch.Tensor, w: torch.Tensor, defer: bool = False):
+    """x @ w^T: the decode GEMM (K11) where the measured table picks it, the
+    older split-K kernel where it was measured faster, else hipBLASLt.
+    ``defer``: the caller feeds the result to ``rms_norm(..., residual=)``,
+    so a table entry for the partials-only form (epi 2) may return
+    ``Partials`` and leave the K reduction to the norm."""
+    if x.is_cuda and x.dim() == 2:
+        M, N, K = x.shape[0], w.shape[0], w.shape[1]
+        if defer:
+            ch = dgemm_choice(M, N, K, epi=2)
+            if ch is not None:
+                return dgemm_partials(x, w, ch[0], ch[1])
+        ch = dgemm_choice(M, N, K)
+        if ch is not None:
+            return dgemm(x, w, ch[0], ch[1])
+        if splitk_preferred(M, N, K):
+            return gemm_splitk(x, w)
     return torch.nn.functional.linear(x, w)
+
+
+def linear_swiglu(x: torch.Tensor, w: torch.Tensor, block: int) -> torch.Tensor:
+    """silu(gate) * up of x @ w^T for gate|up weights interleaved per
+    ``block`` channels: the fused-epilogue decode GEMM where the table picks
+    it (its BN must be 2 * block), else the library GEMM + the GLU kernel."""
+    if x.is_cuda and x.dim() == 2:
+        ch = dgemm_choice(x.shape[0], w.shape[0], w.shape[1], epi=1)
+        if ch is not None and DGEMM_CONFIGS[ch[0]][1] == 2 * block:
+            return dgemm(x, w, ch[0], ch[1], epi=1)
+    return silu_mul(linear(x, w), block=block)
+
+
+def swiglu_block(N: int, K: int) -> int:
+    """Interleave block of the gate|up weights for the fused decode GEMM of
+    this shape (BN/2 of the measured configurations), 0 = not fused."""
+    bns = {DGEMM_CONFIGS[cfg][1] for m, cfg, s in _dg_table().get((N, K, 1), ()) if cfg >= 0}
+    return min(bns) // 2 if bns else 0
+
+
+# ---------------------------------------------------------------------------
+# K11: decode-shape projection GEMM (csrc/kernels/dgemm.hip)
+# ---------------------------------------------------------------------------
+# (BM, BN) of each kernel configuration id, in the order of kDgCfgs
+DGEMM_CONFIGS = [(256, 128), (128, 128), (64, 128), (256, 64), (128, 64), (64, 64), (128, 256),
+                 (64, 64), (128, 64), (64, 128), (128, 128), (128, 256), (256, 128), (256, 256)]
+DGEMM_MAX_M = 256
+_DG_WS: dict = {}          # (device, stream) -> (slabs fp32, tickets uint32)
+_DG_TICKETS = 8192
+DGEMM_TABLE: dict | None = None
+DGEMM_CALLS = [0]          # host-side launch count (tests: the K11 path really ran)
+
+
+def _dg_table() -> dict:
+    """Measured dispatch: {(N, K, epi): [(M_max, cfg, splits), ...]} from
+    config/dgemm_gfx950.json (bench/dgemm_bench.py --write).  A shape or M
+    absent from the table stays on hipBLASLt.  LMX_DGEMM=0 disables."""
+    global DGEMM_TABLE
+    if DGEMM_TABLE is None:
+        import json
+        import os
+        DGEMM_TABLE = {}
+        path = os.environ.get("LMX_DGEMM_TABLE") or os.path.join(
+            os.path.dirname(os.path.dirname(__file__)), "config", "dgemm_gfx950.json")
+        if os.environ.get("LMX_DGEMM", "1") == "1" and os.path.exists(path):
+            with open(path) as f:
+                raw = json.load(f)
+            for e in raw.get("entries", []):
+                key = (int(e["N"]), int(e["K"]), int(e.get("epi", 0)))
+                DGEMM_TABLE.setdefault(key, []).append(
+                    (int(e["m_max"]), int(e["cfg"]), int(e["splits"])))
+            for v in DGEMM_TABLE.values():
+                v.sort()
+    return DGEMM_TABLE
+
+
+def dgemm_choice(M: int, N: int, K: int, epi: int = 0) -> tuple[int, int] | None:
+    """(cfg, splits) for this decode GEMM, or None (use the library)."""
+    if not 0 < M <= DGEMM_MAX_M:
+        return None
+    for m_max, cfg, s in _dg_table().get((N, K, epi), ()):
+        if M <= m_max:
+            return (cfg, s) if cfg >= 0 else None   # cfg -1: the library won this bucket
+    return None
+
+
+def _dg_workspace(dev: torch.device, n_floats: int):
+    key = (dev.index, _stream())
+    ws = _DG_WS.get(key)
+    if ws is None or ws[0].numel() < n_floats:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("dgemm workspace must be allocated before graph capture "
+                               "(run the shape once eagerly)")
+        n_floats = max(n_floats, ws[0].numel() if ws else 0, 1 << 20)
+        tickets = ws[1] if ws else torch.zeros(_DG_TICKETS, dtype=torch.int32, device=dev)
+        ws = (torch.empty(n_floats, dtype=torch.float32, device=dev), tickets)
+        _DG_WS[key] = ws
+    return ws
+
+
+def dgemm(a: torch.Tensor, w: torch.Tensor, cfg: int, splits: int, epi: int = 0,
+          out: torch.Tensor | None = None) -> torch.Tensor:
+    """a @ w^T for decode-sized M on the K11 kernel; epi=1: ``w`` interleaved
+    per BN-column tile as [BN/2 gate | BN/2 up] rows (``interleave_gate_up``
+    with ``block=BN/2``) and the result is silu(gate) * up (N/2 columns)."""
+    M, K = a.shape
+    N = w.shape[0]
+    bm, bn = DGEMM_CONFIGS[cfg]
+    ncols = N // 2 if epi else N
+    if not a.is_cuda:
+        y = a.float() @ w.float().t()
+        if epi:
+            y = y.view(M, N // bn, 2, bn // 2)
+            y = (torch.nn.functional.silu(y[:, :, 0]) * y[:, :, 1]).reshape(M, ncols)
+        y = y.to(a.dtype)
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
+    _bf16(a, "a"); _bf16(w, "w")
+    _chk(0 < M <= DGEMM_MAX_M and N % bn == 0 and K % (64 * splits) == 0,
+         f"dgemm shape M={M} N={N} K={K} cfg={cfg} splits={splits}")
+    _chk(w.shape[1] == K and a.stride(1) == 1 and w.stride(1) == 1, "dgemm layout")
+    _chk(a.stride(0) % 8 == 0 and w.stride(0) % 8 == 0 and a.data_ptr() % 16 == 0
+         and w.data_ptr() % 16 == 0, "dgemm operands need 16-B aligned rows")
+    if out is None:
+        out = torch.empty((M, ncols), dtype=a.dtype, device=a.device)
+    _chk(out.shape == (M, ncols) and out.stride(1) == 1 and out.stride(0) % 4 == 0
+         and out.data_ptr() % 8 == 0, "dgemm output layout")
+    slabs = tickets = None
+    if splits > 1:
+        _chk(-(-M // bm) * (N // bn) <= _DG_TICKETS, "dgemm tile count")
+        slabs, tickets = _dg_workspace(a.device, splits * M * N)
+    native().dgemm(_ptr(out), _ptr(a), _ptr(w), _ptr(slabs), _ptr(tickets), _DG_TICKETS, M, N, K,
+                   a.stride(0), w.stride(0), out.stride(0), cfg, splits, epi, _stream())
+    DGEMM_CALLS[0] += 1
+    return out
+
+
+def dgemm_partials(a: torch.Tensor, w: torch.Tensor, cfg: int, splits: int) -> Partials:
+    """K11 with the partials-only epilogue: S fp32 slabs, no reduction pass
+    (the consumer -- ``rms_norm`` -- sums them)."""
+    M, K = a.shape
+    N = w.shape[0]
+    bm, bn = DGEMM_CONFIGS[cfg]
+    _bf16(a, "a"); _bf16(w, "w")
+    _chk(0 < M <= DGEMM_MAX_M and N % bn == 0 and K % (64 * splits) == 0,
+         f"dgemm_partials shape M={M} N={N} K={K} cfg={cfg} splits={splits}")
+    _chk(w.shape[1] == K and a.stride(1) == 1 and w.stride(1) == 1, "dgemm layout")
+    _chk(a.stride(0) % 8 == 0 and w.stride(0) % 8 == 0 and a.data_ptr() % 16 == 0
+         and w.data_ptr() % 16 == 0, "dgemm operands need 16-B aligned rows")
+    slabs, tickets = _dg_workspace(a.device, splits * M * N)
+    native().dgemm(0, _ptr(a), _ptr(w), _ptr(slabs), _ptr(tickets), _DG_TICKETS, M, N, K,
+                   a.stride(0), w.stride(0), N, cfg, splits, 2, _stream())
+    DGEMM_CALLS[0] += 1
+    return Partials(slabs[:splits * M * N].view(splits, M, N), splits, M, N)

@@ -32,6 +32,9 @@ def dense_logits(model, tokens: list[int]) -> torch.Tensor:
         x = x + a @ L["wo"].float().t()
         h = ref.rms_norm(x, L["ln2"].float(), cfg.rms_eps)
         gu = h @ L["w_gate_up"].float().t()
+        if getattr(model, "gu_block", 0):      # fused-SwiGLU weight layout (K11)
+            from llm_mcp_amd.ops import deinterleave_gate_up
+            gu = deinterleave_gate_up(gu, model.gu_block)
         x = x + ref.silu_mul(gu) @ L["w_down"].float().t()
     h = ref.rms_norm(x[-1:], w["norm"].float(), cfg.rms_eps)
     return (h @ w["lm_head"].float().t())[0]

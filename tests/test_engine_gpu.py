@@ -146,3 +146,27 @@ def test_penalties_in_graph_and_eager():
         ctx.append(t)
     assert outs[reqs[1].id] == base[1]
     assert e.stats["graph_steps"] > 0
+
+
+@pytest.mark.parametrize("graphs", [False, True])
+def test_llama3_8b_shapes_on_decode_gemm_match_dense(graphs):
+    """Two layers of Llama-3-8B (the served d=4096 / I=14336 / vocab 128256
+    shapes, so the measured K11 table applies): prefill of 48 prompts in one
+    step (T <= 256) and decode at M = 48 run on the decode GEMM -- fused
+    SwiGLU gate/up, split-K partials summed inside the residual-add RMSNorm --
+    and every greedy token is (near-)argmax of the dense fp32 forward."""
+    import dataclasses
+
+    from llm_mcp_amd.models import config as mc
+    ops.native()
+    cfg = dataclasses.replace(mc.resolve("llama-3-8b"), num_layers=2)
+    n0 = ops.DGEMM_CALLS[0]
+    e = LLMEngine(EngineConfig(model="llama-3-8b", max_num_seqs=64, max_batched_tokens=512,
+                               max_model_len=512, use_graphs=graphs, kv_cache_gb=1),
+                  device="cuda", model_cfg=cfg)
+    assert e.model.gu_block == 64, "fused SwiGLU layout not selected from the table"
+    prompts = [[(17 * i + 3 * j) % 120000 + 100 for j in range(4)] for i in range(48)]
+    outs = e.generate(prompts, SamplingParams(temperature=0, max_tokens=3, ignore_eos=True))
+    assert ops.DGEMM_CALLS[0] > n0
+    for p, o in list(zip(prompts, outs))[::7]:
+        assert_greedy_consistent(e.model, p, o, tol=0.08)

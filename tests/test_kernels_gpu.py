@@ -387,3 +387,70 @@ def test_apply_penalties_vs_reference():
     lg = logits.cuda()
     assert torch.equal(ops.apply_penalties(lg.clone(), win.cuda(), ngen.cuda(), pen.cuda(), on=off),
                        lg)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", list(range(14)))
+@pytest.mark.parametrize("M", [1, 37, 64, 130, 256])
+def test_dgemm_configs_vs_fp32(cfg, M):
+    """K11 decode GEMM: every tile configuration, split-K 1/2/4, both
+    epilogues, against an fp32 PyTorch reference (rows past M masked)."""
+    bm, bn = ops.DGEMM_CONFIGS[cfg]
+    K, N = 1024, 2 * 1024
+    a = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) * K ** -0.5).to(torch.bfloat16)
+    y = a.float() @ w.float().t()
+    for s in (1, 2, 4):
+        out = ops.dgemm(a, w, cfg, s)
+        torch.testing.assert_close(out.float(), y, atol=2e-2, rtol=2e-2)
+        out2 = ops.dgemm(a, w, cfg, s)            # tickets re-armed by the last arriver
+        assert torch.equal(out, out2)
+        # fused SwiGLU on weights interleaved per BN-column tile
+        I = N // 2
+        wil = w.view(2, I // (bn // 2), bn // 2, K).transpose(0, 1).reshape(N, K).contiguous()
+        g = torch.nn.functional.silu(y[:, :I]) * y[:, I:]
+        out3 = ops.dgemm(a, wil, cfg, s, epi=1)
+        torch.testing.assert_close(out3.float(), g, atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.gpu
+def test_dgemm_in_graph_strided_input_long_k():
+    M, K, N = 96, 14336, 4096
+    x = torch.randn(M, K + 64, device=DEV).to(torch.bfloat16)[:, :K]   # row stride K + 64
+    w = (torch.randn(N, K, device=DEV) * K ** -0.5).to(torch.bfloat16)
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    ops.dgemm(x, w, 0, 8, out=out)                # allocates the workspace eagerly
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        ops.dgemm(x, w, 0, 8, out=out)
+    torch.cuda.current_stream().wait_stream(s)
+    with torch.cuda.graph(g, stream=s):
+        ops.dgemm(x, w, 0, 8, out=out)
+    for _ in range(3):
+        x.copy_(torch.randn(M, K + 64, device=DEV).to(torch.bfloat16)[:, :K])
+        g.replay()
+        torch.cuda.synchronize()
+        torch.testing.assert_close(out.float(), x.float() @ w.float().t(), atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg,splits", [(0, 8), (5, 1), (1, 4), (13, 16)])
+def test_dgemm_partials_into_rmsnorm(cfg, splits):
+    """K11 partials-only epilogue summed by the residual-add RMSNorm equals the
+    fp32 reference of norm(residual + x @ w^T)."""
+    M, K, N = 200, 4096, 4096
+    a = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) * K ** -0.5).to(torch.bfloat16)
+    g = (1.0 + 0.1 * torch.randn(N, device=DEV)).to(torch.bfloat16)
+    res = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+    r_ref = (res.float() + a.float() @ w.float().t()).to(torch.bfloat16)
+    expect = ref.rms_norm(r_ref.float(), g.float(), 1e-5)
+    p = ops.dgemm_partials(a, w, cfg, splits)
+    assert p.slabs.shape == (splits, M, N)
+    torch.testing.assert_close(p.sum(), a.float() @ w.float().t(), atol=2e-2, rtol=2e-2)
+    r2 = res.clone()
+    out = ops.rms_norm(p, g, 1e-5, residual=r2)
+    torch.testing.assert_close(r2.float(), r_ref.float(), atol=3e-2, rtol=2e-2)
+    torch.testing.assert_close(out.float(), expect.float(), atol=3e-2, rtol=3e-2)

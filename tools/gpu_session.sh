@@ -26,6 +26,13 @@ for step in "$@"; do
       run rehearse2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
           --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus 2 --steps 2 --warmup 1 \
           --concurrency 64 --rehearse-on-one-gpu || exit $? ;;
+    dgemm_tests)
+      run dgemm_tests 600 python -u -m pytest tests/test_kernels_gpu.py -k dgemm -x -q --timeout 120 \
+          --timeout-method thread -p no:cacheprovider || exit $? ;;
+    dgemm_bench)
+      run dgemm_bench 900 python -u -m llm_mcp_amd.bench.dgemm_bench --json gpurun_out/dgemm_rows.json \
+          --write || exit $?
+      cp llm_mcp_amd/config/dgemm_gfx950.json gpurun_out/ ;;
     smoke)
       run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     *)
