@@ -109,7 +109,12 @@ __global__ void __launch_bounds__(DTHREADS, 2) dgemm_kernel(
   // different k-offsets, so their concurrent reads of the shared activation
   // rows (and of their W rows, all at the same 8-KB-strided offsets
   // otherwise) spread over the L2 / HBM channels instead of camping on one
-  const int rot = ROT ? (tn * 5) % nk : 0;
+  // ROT 2 also staggers the M-tiles that share a W panel by 2 K-steps: the
+  // leader's W reads miss to HBM, its followers re-read those lines from the
+  // XCD's L2 two steps later (short latency) instead of merging into the same
+  // in-flight misses -- per-CU throughput is bounded by the L1's outstanding
+  // misses x their latency (profiles/r2_pmc_dgemm.md)
+  const int rot = ROT == 0 ? 0 : ((tn * 5 + (ROT == 2 ? 2 * tm : 0)) % nk);
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wr = wave % WM, wc = wave / WM;
@@ -308,6 +313,12 @@ static const DgCfg kDgCfgs[] = {
     {128, 256, 2, 3},   // 11
     {256, 128, 4, 3},   // 12
     {256, 256, 4, 2},   // 13
+    // M-tile stagger (ROT 2)
+    {64, 64, 2, 6},     // 14
+    {128, 64, 4, 4},    // 15
+    {64, 128, 2, 5},    // 16
+    {128, 128, 2, 4},   // 17
+    {128, 256, 2, 3},   // 18
 };
 constexpr int kNumDgCfgs = sizeof(kDgCfgs) / sizeof(kDgCfgs[0]);
 
@@ -382,6 +393,11 @@ int dgemm(void* C, const void* A, const void* W, float* slabs, unsigned* tickets
     LMX_DG(11, 128, 256, 2, 3, 1)
     LMX_DG(12, 256, 128, 4, 3, 1)
     LMX_DG(13, 256, 256, 4, 2, 1)
+    LMX_DG(14, 64, 64, 2, 6, 2)
+    LMX_DG(15, 128, 64, 4, 4, 2)
+    LMX_DG(16, 64, 128, 2, 5, 2)
+    LMX_DG(17, 128, 128, 2, 4, 2)
+    LMX_DG(18, 128, 256, 2, 3, 2)
   }
 #undef LMX_DG
   return -1;

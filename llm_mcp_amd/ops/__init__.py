@@ -595,7 +595,8 @@ def swiglu_block(N: int, K: int) -> int:
 # ---------------------------------------------------------------------------
 # (BM, BN) of each kernel configuration id, in the order of kDgCfgs
 DGEMM_CONFIGS = [(256, 128), (128, 128), (64, 128), (256, 64), (128, 64), (64, 64), (128, 256),
-                 (64, 64), (128, 64), (64, 128), (128, 128), (128, 256), (256, 128), (256, 256)]
+                 (64, 64), (128, 64), (64, 128), (128, 128), (128, 256), (256, 128), (256, 256),
+                 (64, 64), (128, 64), (64, 128), (128, 128), (128, 256)]
 DGEMM_MAX_M = 256
 _DG_WS: dict = {}          # (device, stream) -> (slabs fp32, tickets uint32)
 _DG_TICKETS = 8192

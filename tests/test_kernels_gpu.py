@@ -390,7 +390,7 @@ def test_apply_penalties_vs_reference():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg", list(range(14)))
+@pytest.mark.parametrize("cfg", list(range(19)))
 @pytest.mark.parametrize("M", [1, 37, 64, 130, 256])
 def test_dgemm_configs_vs_fp32(cfg, M):
     """K11 decode GEMM: every tile configuration, split-K 1/2/4, both

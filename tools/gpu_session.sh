@@ -33,6 +33,36 @@ for step in "$@"; do
       run dgemm_bench 900 python -u -m llm_mcp_amd.bench.dgemm_bench --json gpurun_out/dgemm_rows.json \
           --write || exit $?
       cp llm_mcp_amd/config/dgemm_gfx950.json gpurun_out/ ;;
+    prof_engine)
+      rm -rf gpurun_out/prof_engine
+      run prof_engine 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_engine -o run \
+          -- python3 -m llm_mcp_amd.bench.engine_bench --batch 256 --max-tokens 64 || exit $? ;;
+    pmc_dgemm)
+      # three counter passes over K11 vs the library on one shape (PMC_ARGS="N K M CFG S EPI")
+      for pass in \
+        "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE GRBM_COUNT" \
+        "FETCH_SIZE TCC_HIT_sum TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum TD_TD_BUSY_sum TD_TC_STALL_sum SQ_INSTS_VMEM SQ_INST_LEVEL_VMEM GRBM_GUI_ACTIVE" \
+        "TCC_MISS_sum TCC_HIT_sum TCC_TAG_STALL_sum TCC_EA0_RDREQ_DRAM_sum TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_READ_REQ_sum TCP_PENDING_STALL_CYCLES_sum TCP_UTCL1_TRANSLATION_MISS_sum" ; do
+        n=$(( ${n:-0} + 1 ))
+        rm -rf gpurun_out/pmc_dgemm_$n
+        run pmc_dgemm_$n 120 timeout -s KILL 100 rocprofv3 --pmc $pass --kernel-trace -d gpurun_out/pmc_dgemm_$n \
+            -o run --output-format csv -- python3 tools/prof_dgemm_probe.py $PMC_ARGS || exit $?
+      done ;;
+    pmc_engine)
+      # counter passes over a short eager engine run (every kernel of prefill + decode)
+      n=0
+      for pass in \
+        "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE GRBM_COUNT" \
+        "FETCH_SIZE TCC_HIT_sum SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_INSTS_LDS GRBM_GUI_ACTIVE" \
+        "WRITE_SIZE TCC_MISS_sum TCC_HIT_sum TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_READ_REQ_sum TCP_PENDING_STALL_CYCLES_sum" ; do
+        n=$(( n + 1 ))
+        rm -rf gpurun_out/pmc_engine_$n
+        run pmc_engine_$n 300 timeout -s KILL 280 rocprofv3 --pmc $pass --kernel-trace -d gpurun_out/pmc_engine_$n \
+            -o run --output-format csv -- python3 -m llm_mcp_amd.bench.engine_bench --batch 128 \
+            --prompt-len 512 --max-tokens 8 --no-graphs --max-batched-tokens 16384 || exit $?
+      done ;;
+    list_counters)
+      run list_counters 120 rocprofv3 -L || exit $? ;;
     smoke)
       run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     *)
