@@ -170,6 +170,12 @@ PRESETS: dict[str, object] = {
                               intermediate_size=512, num_layers=2, num_heads=4, num_kv_heads=2,
                               head_dim=128, max_position=2048, bos_token_id=506,
                               eos_token_ids=(510,)),
+    # the Llama-3-70B head layout shrunk (64 q / 8 kv heads -> 16 / 8): splits
+    # over TP = 8 like 70B does (per rank 2 q heads and 1 kv head, I / 8 = 128)
+    "tiny-llama-tp8": LlamaConfig(name="tiny-llama-tp8", vocab_size=1024, hidden_size=512,
+                                  intermediate_size=1024, num_layers=2, num_heads=16,
+                                  num_kv_heads=8, head_dim=128, max_position=2048,
+                                  bos_token_id=1018, eos_token_ids=(1022,)),
     # Qwen2.5 (biased QKV, GQA group 7 / 7 -- not a divisor of 16)
     "qwen2.5-7b": LlamaConfig(name="qwen2.5-7b", vocab_size=152064, hidden_size=3584,
                               intermediate_size=18944, num_layers=28, num_heads=28,

@@ -118,15 +118,27 @@ class TPContext:
         # gloo only reduces device tensors; it gathers host tensors
         return t.is_cuda and torch.distributed.get_backend(self.group) == "gloo"
 
-    def all_gather_last(self, t: torch.Tensor) -> torch.Tensor:
+    def gather_last_to_leader(self, t: torch.Tensor) -> torch.Tensor | None:
+        """Vocab-parallel logits [B, V/size] -> [B, V] on rank 0 (the only rank
+        that samples); followers get None and assemble nothing.  RCCL: one
+        all_gather_into_tensor (graph-capturable, one collective per step) and
+        the column interleave on the leader only; gloo: a gather to rank 0."""
         if self.size == 1:
             return t
         src = t.contiguous()
-        if self._host_staged(src):
-            src = src.cpu()
-        parts = [torch.empty_like(src) for _ in range(self.size)]
-        torch.distributed.all_gather(parts, src, group=self.group)
-        return torch.cat(parts, dim=-1).to(t.device, non_blocking=True)
+        B, Vs = src.shape
+        if not src.is_cuda or self._host_staged(src):
+            h = src.cpu()
+            parts = [torch.empty_like(h) for _ in range(self.size)] if self.rank == 0 else None
+            torch.distributed.gather(h, parts, dst=0, group=self.group)
+            if self.rank:
+                return None
+            return torch.cat(parts, dim=-1).to(t.device, non_blocking=True)
+        out = torch.empty((self.size * B, Vs), dtype=src.dtype, device=src.device)
+        torch.distributed.all_gather_into_tensor(out, src, group=self.group)
+        if self.rank:
+            return None
+        return out.view(self.size, B, Vs).permute(1, 0, 2).reshape(B, self.size * Vs)
 
 
 class LlamaModel:
@@ -283,5 +295,7 @@ class LlamaModel:
             hs = ops.rms_norm(xs, w["norm"], cfg.rms_eps, residual=rs)
         logits = ops.linear(hs, w["lm_head"])
         if self.tp.size > 1:
-            logits = self.tp.all_gather_last(logits)[:, :cfg.vocab_size]
+            logits = self.tp.gather_last_to_leader(logits)
+            if logits is not None:
+                logits = logits[:, :cfg.vocab_size]
         return logits

@@ -42,6 +42,22 @@ class LeaderLost(RuntimeError):
     launcher can tear the group down (and the supervisor start a new one)."""
 
 
+def _pid_alive(pid: int) -> bool:
+    """True while ``pid`` runs (a zombie -- exited, not yet reaped by its
+    parent -- counts as dead)."""
+    try:
+        os.kill(pid, 0)
+    except ProcessLookupError:
+        return False
+    except PermissionError:
+        return True
+    try:
+        with open(f"/proc/{pid}/stat") as f:
+            return f.read().rsplit(")", 1)[1].split()[0] != "Z"
+    except (OSError, IndexError):
+        return True
+
+
 def leader_timeout_s() -> float:
     return float(os.environ.get("LMX_TP_LEADER_TIMEOUT_S", "30"))
 
@@ -113,13 +129,8 @@ class PlanChannel:
         """Follower-side liveness of the leader: its pid exists and its
         heartbeat is younger than ``timeout_s``."""
         pid = int(self.ctl[3])
-        if pid:
-            try:
-                os.kill(pid, 0)
-            except ProcessLookupError:
-                return False, f"leader pid {pid} is gone"
-            except PermissionError:
-                pass
+        if pid and not _pid_alive(pid):
+            return False, f"leader pid {pid} is gone"
         age = (time.time_ns() - int(self.ctl[2])) / 1e9
         lim = leader_timeout_s() if timeout_s is None else timeout_s
         if int(self.ctl[2]) and age > lim:

@@ -92,7 +92,7 @@ def _rank(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_peer_allreduce_matches_fp32_sum(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

@@ -29,16 +29,18 @@ def _free_port() -> int:
     return p
 
 
-def _rank(rank, size, port, ckpt, tag, q):
+def _rank(rank, size, port, ckpt, tag, q, model="tiny-llama"):
+    # sequence parallelism forced on every prefill step of >= 16 tokens (the
+    # gloo group takes its host-staged reduce-scatter / all-gather branch)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
-                      WORLD_SIZE=str(size), LOCAL_RANK=str(rank))
+                      WORLD_SIZE=str(size), LOCAL_RANK=str(rank), LMX_SP_MIN_TOKENS="16")
     import torch.distributed as dist
 
     from llm_mcp_amd.engine.engine import EngineConfig, SamplingParams
     from llm_mcp_amd.parallel.tp_worker import build_tp_engine, init_group
     torch.cuda.set_device(0)
     tp = init_group("cpu")   # gloo group, GPU tensors
-    ecfg = EngineConfig(model="tiny-llama", max_num_seqs=8, max_batched_tokens=64,
+    ecfg = EngineConfig(model=model, max_num_seqs=8, max_batched_tokens=64,
                         max_model_len=512, use_graphs=False, kv_cache_gb=0.05)
     eng = build_tp_engine(ecfg, torch.device("cuda", 0), tp, tag, weights_path=ckpt)
     try:
@@ -49,26 +51,28 @@ def _rank(rank, size, port, ckpt, tag, q):
             q.put(("leader", out))
             q.put(("comm", eng.tp_comm))
         else:
-            q.put(("follower", eng.run_follower()))
+            q.put((f"follower{rank}", eng.run_follower()))
     finally:
         eng.chan.close()
         dist.destroy_process_group()
 
 
-def test_tp2_group_on_gpu_kernels(tmp_path):
+@pytest.mark.parametrize("size,model", [(2, "tiny-llama"), (4, "tiny-llama-tp8")])
+def test_tp_group_on_gpu_kernels(tmp_path, size, model):
+    """TP=2, and TP=4 of the 70B-shaped tiny model (4 q / 2 kv heads per rank)."""
     from llm_mcp_amd.models import config as mc
     from llm_mcp_amd.models.llama import LlamaModel
     from llm_mcp_amd.models.weights import save_hf_llama
     from tests.dense_ref import assert_greedy_consistent
-    cfg = mc.resolve("tiny-llama")
+    cfg = mc.resolve(model)
     full = LlamaModel(cfg, "cpu", seed=11)          # CPU only in this process
     save_hf_llama(full.w, cfg, str(tmp_path))
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     tag = f"gputest-{os.getpid()}-{_free_port()}"
     port = _free_port()
-    procs = [ctx.Process(target=_rank, args=(r, 2, port, str(tmp_path), tag, q), daemon=True)
-             for r in range(2)]
+    procs = [ctx.Process(target=_rank, args=(r, size, port, str(tmp_path), tag, q, model),
+                         daemon=True) for r in range(size)]
     for p in procs:
         p.start()
     try:
@@ -80,7 +84,7 @@ def test_tp2_group_on_gpu_kernels(tmp_path):
         for p in procs:
             if p.is_alive():
                 p.kill()
-    assert res["follower"] > 0
+    assert all(res[f"follower{r}"] > 0 for r in range(1, size))
     # the all-reduces ran on the peer-memory kernel (IPC regions on the one GPU)
     assert res["comm"].get("peer"), res["comm"]
     for prompt, out in zip(PROMPTS, res["leader"]):

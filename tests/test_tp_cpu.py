@@ -27,21 +27,21 @@ def _free_port() -> int:
     return p
 
 
-def _ecfg():
-    return EngineConfig(model="tiny-llama", max_num_seqs=8, max_batched_tokens=64,
+def _ecfg(model="tiny-llama"):
+    return EngineConfig(model=model, max_num_seqs=8, max_batched_tokens=64,
                         max_model_len=512, use_graphs=False)
 
 
-def _rank_main(rank, size, port, ckpt, tag, q, sp_min_tokens=0):
+def _rank_main(rank, size, port, ckpt, tag, q, sp_min_tokens=0, model="tiny-llama"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(size), LOCAL_RANK=str(rank),
                       LMX_SP_MIN_TOKENS=str(sp_min_tokens))
-    torch.set_num_threads(2)
+    torch.set_num_threads(2 if size <= 2 else 1)
     import torch.distributed as dist
 
     from llm_mcp_amd.parallel.tp_worker import build_tp_engine, init_group
     tp = init_group("cpu")
-    eng = build_tp_engine(_ecfg(), "cpu", tp, tag, weights_path=ckpt)
+    eng = build_tp_engine(_ecfg(model), "cpu", tp, tag, weights_path=ckpt)
     try:
         if rank == 0:
             greedy = eng.generate(PROMPTS, SamplingParams(temperature=0, max_tokens=6,
@@ -162,3 +162,111 @@ def test_qwen3_loader_roundtrip_and_tp_shards(tmp_path):
             for la, lb in zip(a["layers"], b["layers"]):
                 assert set(la) == set(lb)
                 assert torch.equal(la["q_norm"], lb["q_norm"]) and torch.equal(la["wqkv"], lb["wqkv"])
+
+
+
+@pytest.fixture(scope="module")
+def full_model_tp8(tmp_path_factory):
+    cfg = mc.resolve("tiny-llama-tp8")
+    m = LlamaModel(cfg, "cpu", seed=5)
+    path = str(tmp_path_factory.mktemp("ckpt8"))
+    save_hf_llama(m.w, cfg, path)
+    return m, path
+
+
+@pytest.mark.timeout(600)
+def test_tp8_generation_with_sp_matches_dense(full_model_tp8):
+    """World size 8 (the 70B TP=8 layout: 2 q heads and 1 kv head per rank,
+    vocab-parallel LM head gathered to the leader only), sequence-parallel
+    forced on every step of >= 5 tokens, 8 gloo ranks on the CPU."""
+    m, path = full_model_tp8
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port, tag = _free_port(), f"test8-{os.getpid()}-{_free_port()}"
+    procs = [ctx.Process(target=_rank_main, args=(r, 8, port, path, tag, q, 5, "tiny-llama-tp8"),
+                         daemon=True) for r in range(8)]
+    for p in procs:
+        p.start()
+    try:
+        res = [q.get(timeout=500) for _ in procs]
+        for p in procs:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+    leader = next(r for r in res if r[0] == "leader")
+    followers = [r for r in res if r[0] == "follower"]
+    assert len(followers) == 7 and all(f[1] > 0 and f[2] == leader[3] for f in followers)
+    for p, o in zip(PROMPTS, leader[1]):
+        assert len(o) == 6
+        assert_greedy_consistent(m, p, o)
+
+
+def _leader_then_die(path, q):
+    ch = PlanChannel(path, 0, 2, capacity=1 << 20, create=True)
+    ch.publish({"cmd": "step-noop"})
+    q.put("published")
+    import time
+    time.sleep(600)          # killed by the test
+
+
+def _follower(path, q):
+    os.environ["LMX_TP_LEADER_TIMEOUT_S"] = "20"
+    from llm_mcp_amd.parallel.plan_channel import LeaderLost
+    ch = PlanChannel(path, 1, 2, capacity=1 << 20, create=False)
+    assert ch.receive()["cmd"] == "step-noop"
+    q.put("first")
+    try:
+        ch.receive()          # the leader is killed while we wait here
+    except LeaderLost as e:
+        q.put(f"lost: {e}")
+        raise SystemExit(3)
+    q.put("unexpected message")
+
+
+def test_follower_exits_when_the_leader_dies(tmp_path):
+    """A killed TP leader must not strand its followers: the mailbox carries
+    the leader's pid and a heartbeat, and a waiting follower raises
+    LeaderLost (the TP worker then exits non-zero) within seconds."""
+    import signal
+    import time
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    path = str(tmp_path / "mb")
+    lead = ctx.Process(target=_leader_then_die, args=(path, q), daemon=True)
+    lead.start()
+    assert q.get(timeout=60) == "published"
+    fol = ctx.Process(target=_follower, args=(path, q), daemon=True)
+    fol.start()
+    try:
+        assert q.get(timeout=60) == "first"
+        t0 = time.time()
+        os.kill(lead.pid, signal.SIGKILL)
+        msg = q.get(timeout=30)
+        fol.join(timeout=30)
+        assert msg.startswith("lost:") and "gone" in msg, msg
+        assert fol.exitcode == 3 and time.time() - t0 < 30
+    finally:
+        for p in (lead, fol):
+            if p.is_alive():
+                p.kill()
+
+
+def test_follower_exits_on_stale_heartbeat(tmp_path):
+    """Leader process alive but wedged (no heartbeat): the follower gives up
+    after LMX_TP_LEADER_TIMEOUT_S."""
+    import time
+    leader = PlanChannel(str(tmp_path / "mb"), 0, 2, capacity=1 << 20, create=True)
+    leader._beat_stop.set()                     # freeze the heartbeat
+    leader._beat_thread.join()
+    leader.ctl[2] = time.time_ns() - int(60e9)  # last beat a minute ago
+    follower = PlanChannel(str(tmp_path / "mb"), 1, 2, capacity=1 << 20, create=False)
+    from llm_mcp_amd.parallel.plan_channel import LeaderLost
+    t0 = time.time()
+    with pytest.raises(LeaderLost, match="heartbeat"):
+        follower.receive(timeout_s=5)
+    assert time.time() - t0 < 10
+    follower.close()
+    leader.close()

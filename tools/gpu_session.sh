@@ -63,6 +63,9 @@ for step in "$@"; do
       done ;;
     list_counters)
       run list_counters 120 rocprofv3 -L || exit $? ;;
+    tp_tests)
+      run tp_tests 600 python -u -m pytest tests/test_00_peer_ar_gpu.py tests/test_00_tp_gpu.py -x -v \
+          --timeout 300 --timeout-method thread -p no:cacheprovider || exit $? ;;
     smoke)
       run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     *)
