@@ -148,5 +148,6 @@ class RetentionPlanner:
 
     def tick(self) -> dict:
         expired = self.store.expire_deadlines()
+        exhausted = self.store.sweep_exhausted()
         purged = self.store.purge_jobs(self.retention_s) if self.retention_s > 0 else 0
-        return {"deadline_expired": expired, "purged": purged}
+        return {"deadline_expired": expired, "attempts_exhausted": exhausted, "purged": purged}

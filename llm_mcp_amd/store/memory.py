@@ -171,6 +171,9 @@ class MemoryStore:
     def expire_deadlines(self):
         return self.q.expire_deadlines(_ms(self.clock()))
 
+    def sweep_exhausted(self):
+        return 0      # the native queue retires attempt-capped rows inside claim()
+
     def purge_jobs(self, older_than_s):
         return self.q.purge_finished(_ms(self.clock() - older_than_s))
 

@@ -138,12 +138,11 @@ class PostgresStore:
 
     def claim_job(self, worker_id, kinds, lease_s, worker_device="", device_max_concurrency=1,
                   check_online=True):
+        # The claim transaction locks exactly one row, by SKIP LOCKED: expired
+        # deadlines and attempt-capped rows are filtered out here and retired
+        # by the maintenance sweep (expire_deadlines / sweep_exhausted, also
+        # SKIP LOCKED), so concurrent claimers never queue on each other.
         with self.pool.conn() as c, c.transaction():
-            # deadline / attempt-cap sweep (the reference never enforced deadline_at)
-            c.query("UPDATE jobs SET status = 'error', error = 'deadline_exceeded', "
-                    "lease_until = NULL, lease_token = NULL, updated_at = now() "
-                    "WHERE status IN ('queued', 'running') AND deadline_at IS NOT NULL "
-                    "AND deadline_at < now() AND (status = 'queued' OR lease_until < now())")
             limits = self._limits(c)
             r = c.one(
                 f"""
@@ -159,6 +158,7 @@ class PostgresStore:
                   LEFT JOIN devices d ON d.id = j.device_id
                   WHERE (j.status = 'queued' OR (j.status = 'running' AND j.lease_until < now()))
                     AND j.attempts < j.max_attempts
+                    AND (j.deadline_at IS NULL OR j.deadline_at >= now())
                     AND (cardinality($2::text[]) = 0 OR j.kind = ANY($2::text[]))
                     AND (j.device_id IS NULL OR $3 = '' OR j.device_id = $3)
                     AND (NOT $5 OR j.device_id IS NULL OR d.status = 'online')
@@ -185,9 +185,6 @@ class PostgresStore:
                 worker_id, list(kinds or []), worker_device or "",
                 int(device_max_concurrency or 0), bool(check_online), limits, float(lease_s))
             if r is None:
-                # attempt-capped rows that were still queued
-                c.query("UPDATE jobs SET status = 'error', error = 'attempts_exhausted', "
-                        "updated_at = now() WHERE status = 'queued' AND attempts >= max_attempts")
                 return None
             c.query("INSERT INTO job_attempts (id, job_id, worker_id, status) "
                     "VALUES ($1::uuid, $2::uuid, $3, 'running')",
@@ -240,10 +237,24 @@ class PostgresStore:
                        "WHERE status = 'running' AND device_id = $1", device_id)
 
     def expire_deadlines(self):
+        """Retire jobs past deadline_at (queued, or running with a lapsed
+        lease: a live lease finishes its attempt).  Rows another transaction
+        holds (a claim in progress) are skipped, not waited for."""
         return self._n("UPDATE jobs SET status = 'error', error = 'deadline_exceeded', "
                        "lease_until = NULL, lease_token = NULL, updated_at = now() "
-                       "WHERE status IN ('queued', 'running') AND deadline_at IS NOT NULL "
-                       "AND deadline_at < now()")
+                       "WHERE id IN (SELECT id FROM jobs WHERE status IN ('queued', 'running') "
+                       "AND deadline_at IS NOT NULL AND deadline_at < now() "
+                       "AND (status = 'queued' OR lease_until < now()) "
+                       "FOR UPDATE SKIP LOCKED)")
+
+    def sweep_exhausted(self):
+        """Queued (or lease-lapsed) rows whose attempts reached max_attempts ->
+        error 'attempts_exhausted' (they can never be claimed again)."""
+        return self._n("UPDATE jobs SET status = 'error', error = 'attempts_exhausted', "
+                       "lease_until = NULL, lease_token = NULL, updated_at = now() "
+                       "WHERE id IN (SELECT id FROM jobs WHERE attempts >= max_attempts "
+                       "AND (status = 'queued' OR (status = 'running' AND lease_until < now())) "
+                       "FOR UPDATE SKIP LOCKED)")
 
     def purge_jobs(self, older_than_s):
         return self._n("DELETE FROM jobs WHERE status IN ('done', 'error') "

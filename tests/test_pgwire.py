@@ -142,6 +142,14 @@ def test_postgres_store_statement_wiring():
         assert "FOR UPDATE OF j SKIP LOCKED" in sql
         assert p[1] == '{"engine.generate"}' and json.loads(p[5]) == {"n:gpu0": 256}
         assert any(q.startswith("INSERT INTO job_attempts") for q, _ in h.seen)
+        # the claim transaction takes no row locks outside SKIP LOCKED: the
+        # deadline / attempts sweeps moved to the maintenance loop
+        assert not any("deadline_exceeded" in q or "attempts_exhausted" in q for q, _ in h.seen)
+        assert "deadline_at >= now()" in sql
+        st.expire_deadlines()
+        st.sweep_exhausted()
+        sweeps = [q for q, _ in h.seen if "deadline_exceeded" in q or "attempts_exhausted" in q]
+        assert len(sweeps) == 2 and all("FOR UPDATE SKIP LOCKED" in q for q in sweeps)
         assert st.complete_job(jid, "w1", {"ok": True}, {"ms": 5}, token=j["attempt_id"])
         assert st.job_counts() == {"queued": 4, "running": 1, "done": 0, "error": 0}
         v = st.job_version()

@@ -66,6 +66,13 @@ for step in "$@"; do
     tp_tests)
       run tp_tests 600 python -u -m pytest tests/test_00_peer_ar_gpu.py tests/test_00_tp_gpu.py -x -v \
           --timeout 300 --timeout-method thread -p no:cacheprovider || exit $? ;;
+    tune70b)
+      run tune70b 900 python -u -m llm_mcp_amd.bench.tune_gemms --model llama-3-70b --tp 8 \
+          --out gpurun_out/tunableop_70b_tp8.csv --max-ms 40 || exit $? ;;
+    dgemm70b)
+      run dgemm70b 600 python -u -m llm_mcp_amd.bench.dgemm_bench --model llama-3-70b --tp 8 \
+          --json gpurun_out/dgemm_rows_70b.json --write || exit $?
+      cp llm_mcp_amd/config/dgemm_gfx950.json gpurun_out/dgemm_gfx950_70b.json ;;
     smoke)
       run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     *)
