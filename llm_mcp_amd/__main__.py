@@ -131,12 +131,20 @@ async def run_core(args, specs, procs=()):
     for s in specs:
         dev = s.get("device", "gpu0")
         if dev.startswith("gpu"):
-            dev = rocm_enum.device_id(int(dev[3:]))
+            idx, _, rep = dev[3:].partition(".")
+            dev = rocm_enum.device_id(int(idx)) + (f".{rep}" if rep else "")
             s["device"] = dev
         addrs[dev] = "unix:" + s["path"]
     st = CoreState(engine_addrs=addrs)
     st.engines_ready = not specs
     app = create_core_app(st)
+    if isinstance(procs, Supervisor):
+        from .api.helpers import write_json
+
+        async def workers(request):
+            """Supervised GPU worker processes: pid, alive, restarts."""
+            return write_json(200, {"workers": procs.status()})
+        app.router.add_get("/v1/debug/workers", workers)
     runner = web.AppRunner(app, access_log=None)
     await runner.setup()
     host, port = args.http.rsplit(":", 1)
@@ -220,6 +228,11 @@ class Supervisor:
                             e["proc"].pid, e["restarts"])
         return died
 
+    def status(self) -> list[dict]:
+        return [{"name": e["name"], "pid": e["proc"].pid if e["proc"] is not None else None,
+                 "alive": e["proc"] is not None and e["proc"].poll() is None,
+                 "restarts": e["restarts"]} for e in self.entries]
+
     def __iter__(self):
         return iter([e["proc"] for e in self.entries if e["proc"] is not None])
 
@@ -258,6 +271,8 @@ def cmd_serve(args):
     env.setdefault("CORE_HTTP_URL", "http://127.0.0.1" + args.http[args.http.rfind(":"):])
     sock_dir = args.socket_dir or "/tmp"
     extra = ["--cpu"] if args.cpu else []
+    plan = [dict(w, replica=k) for w in plan for k in range(max(1, args.replicas_per_gpu))
+            if k == 0 or w["tp"] == 1]
     for w in plan:
         grp, tp = w["gpus"], w["tp"]
         if tp > 1:
@@ -272,17 +287,22 @@ def cmd_serve(args):
             specs.append({"model": w["chat"], "path": sock,
                           "device": f"{host}:tp{tp}:gpu{grp[0]}-{grp[-1]}"})
             continue
-        g = grp[0]
-        sock = os.path.join(sock_dir, f"lmx-{host}-gpu{g}.sock")
+        g, k = grp[0], w["replica"]
+        name = f"gpu{g}" + (f".r{k}" if k else "")
+        sock = os.path.join(sock_dir, f"lmx-{host}-{name}.sock")
         cmd = [sys.executable, "-m", "llm_mcp_amd.worker.main", "--gpu", str(g),
                "--chat-model", w["chat"], "--socket", sock,
                "--max-num-seqs", str(args.max_num_seqs)] + extra
+        if k:
+            cmd += ["--replica", str(k)]
+        if args.kv_fraction:
+            cmd += ["--kv-fraction", str(args.kv_fraction)]
         if w["embed"]:
             cmd += ["--embed-model", w["embed"]]
-        sup.spawn(cmd, env, f"gpu{g}")
+        sup.spawn(cmd, env, name)
         for m in (w["chat"], w["embed"]):
             if m:
-                specs.append({"model": m, "path": sock, "device": f"gpu{g}"})
+                specs.append({"model": m, "path": sock, "device": name})
     try:
         asyncio.run(run_core(args, specs, sup))
     finally:
@@ -320,6 +340,11 @@ def main(argv=None):
             p.add_argument("--socket-dir", default=os.environ.get("LMX_SOCKET_DIR", ""))
             p.add_argument("--cpu", action="store_true",
                            help="workers run their engines on the CPU (tests / plumbing)")
+            p.add_argument("--replicas-per-gpu", type=int, default=1,
+                           help="single-GPU workers per GPU (1-GPU rehearsals of a multi-GPU "
+                                "node; device ids gpuN.rk)")
+            p.add_argument("--kv-fraction", type=float, default=0.0,
+                           help="KV cache share of free HBM per worker (0: worker default)")
         else:
             p.add_argument("--engine", action="append", default=[])
     sub.add_parser("worker", add_help=False)

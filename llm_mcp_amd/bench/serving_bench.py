@@ -188,13 +188,37 @@ def bench_embed(a) -> dict:
 
 # ------------------------------------------------------------------ mixed ----
 async def _mixed_load(url, chat_model, embed_model, jobs, concurrency, embed_every, max_tokens,
-                      prompt_chars):
+                      prompt_chars, sync_every=0):
+    """``sync_every`` k > 0: every k-th request is a synchronous
+    /v1/chat/completions call (replica selection + circuit breaker on the
+    hot path) instead of an async job."""
     import aiohttp
     rng = random.Random(1)
     sem = asyncio.Semaphore(concurrency)
     lat, errs, kinds = [], [], {}
+    per_dev: dict[str, int] = {}
+    requeued = [0]
+    sync = {"ok": 0, "error": 0}
+
+    async def one_sync(s, i):
+        body = {"model": chat_model, "max_tokens": max_tokens, "temperature": 0.8,
+                "ignore_eos": True,
+                "messages": [{"role": "user", "content": synthetic_prompt(prompt_chars, rng)}]}
+        async with sem:
+            t0 = time.perf_counter()
+            try:
+                async with s.post(url + "/v1/chat/completions", json=body) as r:
+                    ok = r.status == 200
+                    await r.read()
+            except aiohttp.ClientError:
+                ok = False
+            lat.append(time.perf_counter() - t0)
+            sync["ok" if ok else "error"] += 1
+            kinds["chat.sync"] = kinds.get("chat.sync", 0) + 1
 
     async def one(s, i):
+        if sync_every and i % sync_every == 1:
+            return await one_sync(s, i)
         if i % embed_every == 0:
             kind, payload = "engine.embed", {"model": embed_model,
                                              "prompt": synthetic_prompt(prompt_chars, rng)}
@@ -219,6 +243,12 @@ async def _mixed_load(url, chat_model, embed_model, jobs, concurrency, embed_eve
             kinds[kind] = kinds.get(kind, 0) + 1
             if status != "done":
                 errs.append(jid)
+            else:
+                async with s.get(url + f"/v1/jobs/{jid}") as r:
+                    jj = await r.json()
+                d = ((jj.get("result") or {}).get("device_id") or jj.get("device_id") or "?")
+                per_dev[d] = per_dev.get(d, 0) + 1
+                requeued[0] += int((jj.get("attempts") or 1) > 1)
             if len(lat) % 64 == 0:
                 _log(f"{len(lat)}/{jobs} jobs finished, {len(errs)} errors")
 
@@ -227,31 +257,75 @@ async def _mixed_load(url, chat_model, embed_model, jobs, concurrency, embed_eve
         t0 = time.perf_counter()
         await asyncio.gather(*[one(s, i) for i in range(jobs)])
         el = time.perf_counter() - t0
+    n_async = jobs - sync["ok"] - sync["error"]
     return {"jobs": jobs, "by_kind": kinds, "elapsed_s": round(el, 2),
             "jobs_per_s": round(jobs / el, 2), "p50_s": round(percentile(lat, 50), 3),
-            "p95_s": round(percentile(lat, 95), 3), "error_rate": round(len(errs) / jobs, 4)}
+            "p95_s": round(percentile(lat, 95), 3),
+            "error_rate": round(len(errs) / max(1, n_async), 4),
+            "jobs_done_by_device": per_dev, "jobs_requeued": requeued[0],
+            "sync_chat": sync}
 
 
 def bench_mixed(a) -> dict:
     port, gport = _port(), _port()
     env = dict(os.environ, LMX_STORE=a.store)
+    if a.fault:
+        env.update(LMX_FAULT=a.fault, LMX_FAULT_DEVICE=a.fault_device)
     cmd = [sys.executable, "-m", "llm_mcp_amd", "serve", "--gpus", a.gpus, "--http",
            f"127.0.0.1:{port}", "--grpc", f"127.0.0.1:{gport}", "--chat-model", a.chat_model,
-           "--embed-model", a.model, "--max-num-seqs", str(a.concurrency)]
+           "--embed-model", a.model, "--max-num-seqs", str(a.concurrency),
+           "--replicas-per-gpu", str(a.replicas_per_gpu)]
+    if a.replicas_per_gpu > 1:
+        cmd += ["--kv-fraction", str(round(0.5 / a.replicas_per_gpu, 3))]
+    if a.cpu:
+        cmd += ["--cpu"]
     core = subprocess.Popen(cmd, env=env, start_new_session=True)
     url = f"http://127.0.0.1:{port}"
     try:
         loop = asyncio.new_event_loop()
         loop.run_until_complete(_wait_http(url, "/health"))
         # workers register once their engines are up
-        loop.run_until_complete(_wait_workers(url, len(a.gpus.split(","))))
+        n_workers = len(a.gpus.split(",")) * max(1, a.replicas_per_gpu)
+        loop.run_until_complete(_wait_workers(url, n_workers))
+        loop.run_until_complete(_wait_http(url, "/ready"))
         out = {"config": "mixed chat + embeddings jobs through the lease scheduler",
-               "gpus": a.gpus, "concurrency": a.concurrency, "chat_model": a.chat_model,
+               "gpus": a.gpus, "replicas_per_gpu": a.replicas_per_gpu,
+               "concurrency": a.concurrency, "chat_model": a.chat_model,
                "embed_model": a.model, "embed_share": round(1 / a.embed_every, 3),
-               "max_tokens": a.max_tokens}
-        out.update(loop.run_until_complete(_mixed_load(
-            url, a.chat_model, a.model, a.jobs, a.concurrency, a.embed_every, a.max_tokens,
-            a.chars)))
+               "sync_every": a.sync_every, "max_tokens": a.max_tokens,
+               "fault": a.fault, "fault_device": a.fault_device}
+        circ: dict[str, set] = {}
+
+        async def watch_circuit():
+            import aiohttp
+            async with aiohttp.ClientSession() as s:
+                while True:
+                    try:
+                        async with s.get(url + "/v1/dashboard") as r:
+                            d = await r.json()
+                        for dev in d.get("devices") or []:
+                            circ.setdefault(dev.get("id", "?"), set()).add(
+                                dev.get("circuit", "ok"))
+                    except Exception:
+                        pass
+                    await asyncio.sleep(1.0)
+
+        async def run():
+            w = asyncio.ensure_future(watch_circuit())
+            try:
+                return await _mixed_load(url, a.chat_model, a.model, a.jobs, a.concurrency,
+                                         a.embed_every, a.max_tokens, a.chars, a.sync_every)
+            finally:
+                w.cancel()
+        out.update(loop.run_until_complete(run()))
+        out["circuit_states_seen"] = {k: sorted(v) for k, v in circ.items()}
+
+        async def workers():
+            import aiohttp
+            async with aiohttp.ClientSession() as s:
+                async with s.get(url + "/v1/debug/workers") as r:
+                    return (await r.json()).get("workers")
+        out["workers"] = loop.run_until_complete(workers())
         return out
     finally:
         core.terminate()
@@ -295,6 +369,13 @@ def main(argv=None):
     ap.add_argument("--chars", type=int, default=1024)
     ap.add_argument("--embed-every", type=int, default=4)
     ap.add_argument("--max-tokens", type=int, default=128)
+    ap.add_argument("--sync-every", type=int, default=0,
+                    help="mixed: every k-th request is a sync /v1/chat/completions call")
+    ap.add_argument("--replicas-per-gpu", type=int, default=1,
+                    help="mixed: workers per GPU (1-GPU rehearsal of a multi-GPU node)")
+    ap.add_argument("--fault", default="", help="mixed: LMX_FAULT spec for the targeted worker")
+    ap.add_argument("--fault-device", default="", help="mixed: device-id suffix, e.g. gpu0.r1")
+    ap.add_argument("--cpu", action="store_true", help="mixed: CPU engines (plumbing)")
     a = ap.parse_args(argv)
     fn = {"queue": bench_queue, "embed": bench_embed, "mixed": bench_mixed}[a.what]
     print(json.dumps(fn(a)), flush=True)

@@ -136,6 +136,8 @@ void JobQueue::journal(const JobRow& j) {
     line += S;
     line += std::to_string(v);
   }
+  line += S;
+  line += esc(j.pin_device);
   line += '\n';
   fwrite(line.data(), 1, line.size(), jf_);
   fflush(jf_);
@@ -169,7 +171,7 @@ void JobQueue::replay() {
   auto apply = [&](const std::string& l) {
     if (l.empty()) return;
     std::vector<std::string> v = split(l);
-    if (v[0] == "J" && v.size() == 20) {
+    if (v[0] == "J" && (v.size() == 20 || v.size() == 21)) {
       JobRow j;
       j.id = v[1]; j.kind = v[2]; j.payload = v[3]; j.source = v[4]; j.status = v[5];
       j.result = v[6]; j.error = v[7]; j.device_id = v[8]; j.model_id = v[9];
@@ -178,6 +180,8 @@ void JobQueue::replay() {
       j.max_attempts = std::stoi(v[14]); j.lease_until = std::stoll(v[15]);
       j.deadline_at = std::stoll(v[16]); j.queued_at = std::stoll(v[17]);
       j.updated_at = std::stoll(v[18]); j.seq = std::stoll(v[19]);
+      // journals written before the pin field: a placed device counts as a pin
+      j.pin_device = v.size() == 21 ? v[20] : j.device_id;
       auto it = jobs_.find(j.id);
       if (it != jobs_.end()) index_erase(it->second);
       jobs_[j.id] = j;
@@ -235,6 +239,7 @@ std::string JobQueue::submit(const std::string& kind, const std::string& payload
   j.max_attempts = max_attempts > 0 ? max_attempts : 3;
   j.deadline_at = deadline_at;
   j.device_id = device_id;
+  j.pin_device = device_id;
   j.model_id = model_id;
   j.queued_at = now;
   j.updated_at = now;
@@ -266,11 +271,13 @@ bool JobQueue::claim(const std::string& worker_id, const ClaimFilter& f, int64_t
       continue;
     if (j.deadline_at > 0 && now > j.deadline_at) { to_error_deadline.push_back(j.id); continue; }
     if (j.attempts >= j.max_attempts) { to_error_attempts.push_back(j.id); continue; }
-    const std::string& dev = !j.device_id.empty() ? j.device_id : f.worker_device;
-    if (!j.device_id.empty() && !f.worker_device.empty() && j.device_id != f.worker_device)
+    // only the submitter's pin restricts placement: a requeued or lease-lapsed
+    // job goes to any device, not back to the one it failed on
+    const std::string& dev = !j.pin_device.empty() ? j.pin_device : f.worker_device;
+    if (!j.pin_device.empty() && !f.worker_device.empty() && j.pin_device != f.worker_device)
       continue;  // pinned to another device
     if (!dev.empty()) {
-      if (f.check_online && !j.device_id.empty() && !f.online_devices.count(dev)) continue;
+      if (f.check_online && !j.pin_device.empty() && !f.online_devices.count(dev)) continue;
       int limit = f.device_max_concurrency;
       auto li = f.device_limits.find(dev);
       if (li != f.device_limits.end()) limit = li->second;
@@ -312,7 +319,7 @@ bool JobQueue::claim(const std::string& worker_id, const ClaimFilter& f, int64_t
   j.attempts += 1;
   j.lease_until = now + lease_ms;
   j.worker_id = worker_id;
-  if (j.device_id.empty()) j.device_id = f.worker_device;  // placement
+  j.device_id = j.pin_device.empty() ? f.worker_device : j.pin_device;  // placement
   j.lease_token = new_id();
   j.updated_at = now;
   index_insert(j);
@@ -388,6 +395,7 @@ std::string JobQueue::fail(const std::string& id, const std::string& worker_id,
   j.lease_token.clear();
   j.updated_at = now;
   j.status = j.attempts < j.max_attempts ? "queued" : "error";
+  if (j.status == "queued") j.device_id = j.pin_device;   // placement dropped on requeue
   index_insert(j);
   journal(j);
   for (auto& a : attempts_[id])

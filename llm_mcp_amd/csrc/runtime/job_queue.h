@@ -39,7 +39,8 @@ namespace lmxrt {
 
 struct JobRow {
   std::string id, kind, payload, source, status, result, error;
-  std::string device_id, model_id;  // payload->>'device_id' / 'model_id' (indexed)
+  std::string device_id, model_id;  // placement (running/last device) / payload->>'model_id'
+  std::string pin_device;           // payload->>'device_id': the submitter's pin ("" = any)
   std::string worker_id, lease_token;
   int32_t priority = 0, attempts = 0, max_attempts = 3;
   int64_t lease_until = 0, deadline_at = 0, queued_at = 0, updated_at = 0;  // ms, 0 = NULL

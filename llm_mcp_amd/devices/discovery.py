@@ -92,6 +92,16 @@ class DiscoveryRunner:
                          "capacity": max([m.capacity for m in ms] or [0]) or None,
                          "models": sorted({m.model_id for m in ms})},
                 "models": [(m.model_id, m.cfg, m.max_model_len) for m in ms]})
+        # extra workers on one GPU (``serve --replicas-per-gpu``: gpuN.rk)
+        for dev, ms in served.items():
+            base, _, rep = dev.rpartition(".r")
+            if rep.isdigit() and ":gpu" in base and not any(d["id"] == dev for d in out):
+                out.append({"id": dev, "name": dev, "platform": "rocm", "arch": "gfx950",
+                            "host": host, "tags": {"engine": True, "rocm": True,
+                                                   "replica_of": base,
+                                                   "models": sorted({m.model_id for m in ms}),
+                                                   "capacity": max(m.capacity for m in ms)},
+                            "models": [(m.model_id, m.cfg, m.max_model_len) for m in ms]})
         # multi-GPU (TP) engines registered under a group id
         for dev, ms in served.items():
             if ":tp" in dev and not any(d["id"] == dev for d in out):

@@ -88,6 +88,11 @@ VARS: list[Var] = [
     Var("LMX_RESTART_BACKOFF_S", float, 1.0, "serve: first restart delay of a dead GPU worker (doubles per consecutive death)"),
     Var("LMX_RESTART_MAX_S", float, 60.0, "serve: cap of the worker restart backoff"),
     Var("LMX_SOCKET_DIR", str, "", "serve: directory of the engine sockets (default /tmp)"),
+    Var("LMX_DGEMM", str, "1", "0 disables the decode GEMM (K11) dispatch table (hipBLASLt everywhere)"),
+    Var("LMX_DGEMM_TABLE", str, "", "decode GEMM dispatch table (default llm_mcp_amd/config/dgemm_gfx950.json)"),
+    Var("LMX_FAULT_DEVICE", str, "", "apply LMX_FAULT only in the worker whose device id ends with this (e.g. gpu0.r1)"),
+    Var("LMX_WATCHDOG_S", float, 1.0, "worker: engine health check cadence; an unhealthy engine makes the worker exit for a restart"),
+    Var("LMX_WATCHDOG_GRACE_S", float, 2.0, "worker: delay between detecting a broken engine and exiting"),
     Var("LMX_PROGRESS_S", float, 2.0, "worker: cadence of job progress reports (tokens so far)"),
     Var("LMX_PEER_NODES", str, "", "other nodes' core URLs polled by discovery"),
     Var("LMX_PEER_PORTS", str, "8080", "core ports probed on mesh / subnet hosts"),

@@ -138,6 +138,7 @@ class PostgresStore:
 
     def claim_job(self, worker_id, kinds, lease_s, worker_device="", device_max_concurrency=1,
                   check_online=True):
+        PIN = "NULLIF(j.payload->>'device_id', '')"   # noqa: N806 (SQL fragment)
         # The claim transaction locks exactly one row, by SKIP LOCKED: expired
         # deadlines and attempt-capped rows are filtered out here and retired
         # by the maintenance sweep (expire_deadlines / sweep_exhausted, also
@@ -151,21 +152,24 @@ class PostgresStore:
                   WHERE status = 'running' AND lease_until >= now() AND device_id IS NOT NULL
                   GROUP BY device_id
                 ), cand AS (
-                  SELECT j.id, COALESCE(j.device_id, NULLIF($3, '')) AS place
+                  -- only the submitter's pin (payload device_id) restricts
+                  -- placement; jobs.device_id is where the job last ran, so a
+                  -- requeued / lease-lapsed job may move to any device
+                  SELECT j.id, COALESCE({PIN}, NULLIF($3, '')) AS place
                   FROM jobs j
                   LEFT JOIN running_per_device r
-                         ON r.device_id = COALESCE(j.device_id, NULLIF($3, ''))
-                  LEFT JOIN devices d ON d.id = j.device_id
+                         ON r.device_id = COALESCE({PIN}, NULLIF($3, ''))
+                  LEFT JOIN devices d ON d.id = {PIN}
                   WHERE (j.status = 'queued' OR (j.status = 'running' AND j.lease_until < now()))
                     AND j.attempts < j.max_attempts
                     AND (j.deadline_at IS NULL OR j.deadline_at >= now())
                     AND (cardinality($2::text[]) = 0 OR j.kind = ANY($2::text[]))
-                    AND (j.device_id IS NULL OR $3 = '' OR j.device_id = $3)
-                    AND (NOT $5 OR j.device_id IS NULL OR d.status = 'online')
-                    AND (COALESCE(j.device_id, NULLIF($3, '')) IS NULL
-                         OR COALESCE(($6::jsonb ->> COALESCE(j.device_id, $3))::int, $4) <= 0
+                    AND ({PIN} IS NULL OR $3 = '' OR {PIN} = $3)
+                    AND (NOT $5 OR {PIN} IS NULL OR d.status = 'online')
+                    AND (COALESCE({PIN}, NULLIF($3, '')) IS NULL
+                         OR COALESCE(($6::jsonb ->> COALESCE({PIN}, $3))::int, $4) <= 0
                          OR COALESCE(r.n, 0) <
-                            COALESCE(($6::jsonb ->> COALESCE(j.device_id, $3))::int, $4))
+                            COALESCE(($6::jsonb ->> COALESCE({PIN}, $3))::int, $4))
                   ORDER BY j.priority DESC, j.queued_at ASC
                   FOR UPDATE OF j SKIP LOCKED
                   LIMIT 1
@@ -221,9 +225,12 @@ class PostgresStore:
                         f"AND {self._OWNS} FOR UPDATE", job_id, worker_id, token or "")
             if tok is None:
                 return None
+            # a requeued job drops its placement (back to the submitter's pin)
             r = c.one("UPDATE jobs SET error = $2, lease_until = NULL, lease_token = NULL, "
                       "updated_at = now(), status = CASE WHEN attempts < max_attempts "
-                      "THEN 'queued' ELSE 'error' END WHERE id = $1::uuid "
+                      "THEN 'queued' ELSE 'error' END, device_id = CASE WHEN attempts < "
+                      "max_attempts THEN NULLIF(payload->>'device_id', '') ELSE device_id END "
+                      "WHERE id = $1::uuid "
                       "RETURNING status, $3::text AS tok", job_id, error or "", tok["tok"])
             if r is None:
                 return None

@@ -97,6 +97,14 @@ class WorkerAgent:
                 await asyncio.wait(list(self.inflight.values()),
                                    return_when=asyncio.FIRST_COMPLETED)
                 continue
+            if self.health is not None:
+                ok, why = self.health()
+                if not ok:
+                    # a broken GPU pulls no new work: the queue hands it to the
+                    # healthy devices (the worker process exits and is restarted)
+                    self.stats["unhealthy_waits"] = self.stats.get("unhealthy_waits", 0) + 1
+                    await asyncio.sleep(0.2)
+                    continue
             if self.admit is not None and self.inflight:
                 ok, _why = self.admit()
                 if not ok:

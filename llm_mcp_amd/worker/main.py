@@ -37,6 +37,9 @@ def build_parser():
     ap.add_argument("--tp", type=int, default=1)
     ap.add_argument("--cpu", action="store_true",
                     help="run the engines on the CPU (tests / plumbing; device ids stay gpuN)")
+    ap.add_argument("--replica", type=int, default=0,
+                    help="k-th worker on the same GPU (1-GPU rehearsals of multi-GPU serving): "
+                         "device id gpuN.rk")
     return ap
 
 
@@ -80,7 +83,8 @@ def main(argv=None):
         if a.embed_model:
             ecfg.kv_fraction = min(ecfg.kv_fraction, 0.5)
         engine = LLMEngine(ecfg, device=dev, model_cfg=cfg, weights=weights)
-    serve_engines(a, engine, embed, rocm_enum.device_id(a.gpu))
+    dev_id = rocm_enum.device_id(a.gpu) + (f".r{a.replica}" if a.replica else "")
+    serve_engines(a, engine, embed, dev_id)
 
 
 def serve_engines(a, engine, embed, device_id: str) -> None:
@@ -95,6 +99,10 @@ def serve_engines(a, engine, embed, device_id: str) -> None:
     from .agent import WorkerAgent, engine_admission
     from .jobs import JobRunner
 
+    fdev = os.environ.get("LMX_FAULT_DEVICE", "")
+    if fdev and not device_id.endswith(fdev):
+        from ..utils.faults import Faults, set_faults
+        set_faults(Faults(""))        # LMX_FAULT applies to the targeted device only
     reg = ModelRegistry()
     aeng = None
     if embed is not None:
@@ -152,13 +160,37 @@ def serve_engines(a, engine, embed, device_id: str) -> None:
                                 health=engine.healthy if engine is not None else None,
                                 admit=engine_admission(engine) if engine is not None else None)
             task = asyncio.create_task(agent.run())
+        fatal = {}
+
+        async def watchdog():
+            # an engine error (HIP fault) or a hung step is fatal for this GPU
+            # process: stop, let the in-flight leases lapse / requeue, exit
+            # non-zero -- the serve supervisor starts a fresh worker
+            while engine is not None and not stop.is_set():
+                await asyncio.sleep(WATCHDOG_S)
+                ok, why = engine.healthy()
+                if not ok:
+                    log.error("%s unhealthy: %s; worker exits for a restart", device_id, why)
+                    fatal["why"] = why
+                    await asyncio.sleep(WATCHDOG_GRACE_S)   # let in-flight failures report
+                    stop.set()
+
+        wd = asyncio.create_task(watchdog())
         await stop.wait()
+        wd.cancel()
         if agent is not None:
             agent.stop()
             task.cancel()
+        if fatal:
+            logging.shutdown()
+            os._exit(3)        # no teardown on a broken device (it may hang)
         server.stop()
 
     asyncio.run(run())
+
+
+WATCHDOG_S = float(os.environ.get("LMX_WATCHDOG_S", "1.0"))
+WATCHDOG_GRACE_S = float(os.environ.get("LMX_WATCHDOG_GRACE_S", "2.0"))
 
 
 if __name__ == "__main__":

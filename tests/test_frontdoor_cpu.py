@@ -210,3 +210,29 @@ async def _many(url: str, n: int, max_tokens: int) -> list[str]:
         return "ok" if fin in ("length", "stop") else (fin or "none")
     async with aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=240)) as s:
         return await asyncio.gather(*[one(s, i) for i in range(n)])
+
+
+@pytest.mark.timeout(400)
+def test_config5_mixed_load_with_a_faulty_replica():
+    """BASELINE config 5 in miniature (CPU engines): two workers on one
+    device, injected HIP faults on one of them.  Every async job completes
+    (failed attempts requeue to the healthy worker), sync chat errors stay
+    bounded, the faulty worker is restarted by the supervisor, and the
+    breaker of the faulty device trips."""
+    import json as _json
+    env = dict(ENV, LMX_FAKE_GPUS="1")
+    out = subprocess.run(
+        [sys.executable, "-m", "llm_mcp_amd.bench.serving_bench", "mixed", "--cpu", "--gpus",
+         "0", "--replicas-per-gpu", "2", "--fault", "gpu_error:0.03", "--fault-device",
+         "gpu0.r1", "--chat-model", "tiny-llama", "--model", "tiny-nomic", "--jobs", "400",
+         "--concurrency", "8", "--sync-every", "2", "--max-tokens", "16", "--chars", "64"],
+        cwd=ROOT, env=env, capture_output=True, text=True, timeout=380)
+    assert out.returncode == 0, out.stderr[-3000:]
+    r = _json.loads(out.stdout.strip().splitlines()[-1])
+    assert r["error_rate"] == 0.0, r                         # async jobs all done
+    assert r["sync_chat"]["ok"] >= 0.8 * (r["sync_chat"]["ok"] + r["sync_chat"]["error"]), r
+    faulty = next(w for w in r["workers"] if w["name"] == "gpu0.r1")
+    healthy = next(w for w in r["workers"] if w["name"] == "gpu0")
+    assert faulty["restarts"] >= 1 and healthy["restarts"] == 0, r["workers"]
+    dev = next(d for d in r["circuit_states_seen"] if d.endswith("gpu0.r1"))
+    assert "degraded" in r["circuit_states_seen"][dev], r["circuit_states_seen"]

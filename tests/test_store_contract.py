@@ -131,3 +131,33 @@ def test_deadline_filtered_and_swept(store):
     store.expire_deadlines()
     j = store.get_job(jid)
     assert j["status"] == "error" and "deadline" in (j["error"] or "")
+
+
+def test_requeued_job_is_not_stuck_on_its_failed_device(store):
+    """A claim records where the job runs (device_id), but only the
+    submitter's pin restricts placement: after a failure or a lapsed lease
+    the job goes to another device, while a pinned job stays on its pin."""
+    kind = _kind("move")
+    a_dev, b_dev = f"n{os.getpid()}:gpu0.r1", f"n{os.getpid()}:gpu0"
+    for d in (a_dev, b_dev):
+        store.upsert_device(d, status="online")
+    free = store.submit_job(kind, {})
+    a = store.claim_job("wa", [kind], 60, worker_device=a_dev)
+    assert a["id"] == free and store.get_job(free)["device_id"] == a_dev
+    assert store.fail_job(free, "wa", "HIP error", {}, token=a["attempt_id"]) == "queued"
+    b = store.claim_job("wb", [kind], 60, worker_device=b_dev)
+    assert b is not None and b["id"] == free and store.get_job(free)["device_id"] == b_dev
+    # lease lapse on b: c on a_dev takes it over
+    store.complete_job(free, "wb", {}, {}, token=b["attempt_id"])
+    lapsing = store.submit_job(kind, {})
+    assert store.claim_job("wb", [kind], 1, worker_device=b_dev)["id"] == lapsing
+    time.sleep(1.3)
+    c = store.claim_job("wa", [kind], 60, worker_device=a_dev)
+    assert c is not None and c["id"] == lapsing
+    assert store.complete_job(lapsing, "wa", {}, {}, token=c["attempt_id"])
+    # pinned: never moves
+    pinned = store.submit_job(kind, {"device_id": a_dev})
+    p = store.claim_job("wa", [kind], 60, worker_device=a_dev)
+    assert p["id"] == pinned
+    assert store.fail_job(pinned, "wa", "boom", {}, token=p["attempt_id"]) == "queued"
+    assert store.claim_job("wb", [kind], 60, worker_device=b_dev) is None

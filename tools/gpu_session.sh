@@ -73,6 +73,12 @@ for step in "$@"; do
       run dgemm70b 600 python -u -m llm_mcp_amd.bench.dgemm_bench --model llama-3-70b --tp 8 \
           --json gpurun_out/dgemm_rows_70b.json --write || exit $?
       cp llm_mcp_amd/config/dgemm_gfx950.json gpurun_out/dgemm_gfx950_70b.json ;;
+    config5)
+      # BASELINE config 5 on one GPU: two workers (chat + embed each) on cuda:0,
+      # 256 concurrent mixed jobs + sync chats, injected HIP faults on one worker
+      run config5 900 python -u -m llm_mcp_amd.bench.serving_bench mixed --gpus 0 \
+          --replicas-per-gpu 2 --fault gpu_error:0.002 --fault-device gpu0.r1 \
+          --jobs 1024 --concurrency 256 --sync-every 4 --max-tokens 64 --chars 512 || exit $? ;;
     smoke)
       run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     *)
