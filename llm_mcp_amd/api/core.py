@@ -133,6 +133,16 @@ class CoreState:
             info = m.info()
             if "kv_usage" in info:
                 self.metrics.kv_usage.labels(m.device_id).set(info["kv_usage"])
+            if info.get("running"):
+                # sampled each maintenance tick: sequences in the engine's batch
+                self.metrics.batch_size.labels(m.device_id).observe(info["running"])
+        from ..devices import rocm_enum
+        for idx, t in rocm_enum.gpu_telemetry().items():
+            dev = rocm_enum.device_id(idx)
+            if "hbm_used_bytes" in t:
+                self.metrics.hbm_used.labels(dev).set(t["hbm_used_bytes"])
+            if "busy_pct" in t:
+                self.metrics.gpu_util.labels(dev).set(t["busy_pct"])
             comm = info.get("tp_comm") or {}
             if comm and m.device_id not in self._comm_seen:
                 # the TP group's start-up all-reduce probe (parallel/tp_worker.py)

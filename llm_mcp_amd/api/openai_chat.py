@@ -19,15 +19,19 @@ Ollama's ``options.repeat_penalty`` / ``repeat_last_n``) are supported.
 from __future__ import annotations
 
 import json
+import logging
 import time
 import uuid
 
 from aiohttp import web
 
+from ..engine.async_engine import StreamItem
 from ..engine.engine import SamplingParams
 from ..models.tokenizer import IncrementalDetokenizer, apply_chat_template
 from ..utils import tracing
 from .helpers import dumps, read_json, write_error, write_json
+
+log = logging.getLogger("lmx.chat")
 
 CHAT_TIMEOUT_S = 120.0
 
@@ -134,6 +138,7 @@ class ChatHandler:
             n = 0
         if not 1 <= n <= 16:
             return write_error(400, "invalid_n", "'n' must be an integer in [1, 16]")
+        box = {"target": target}      # the replica serving the request (failover moves it)
         target.inflight += 1
         t0 = time.time()
         try:
@@ -141,11 +146,56 @@ class ChatHandler:
                 return await self._multi(request, target, model, prompt_ids, params, n, stream,
                                          include_usage, extra_headers, t0)
             if stream:
-                return await self._stream(request, target, model, prompt_ids, params,
+                return await self._stream(request, box, model, prompt_ids, params,
                                           include_usage, extra_headers, t0)
-            return await self._sync(target, model, prompt_ids, params, extra_headers, t0)
+            return await self._sync(box, model, prompt_ids, params, extra_headers, t0)
         finally:
-            target.inflight -= 1
+            box["target"].inflight -= 1
+
+    async def _failover(self, box, model, prompt_ids, params, attempts: int = 3):
+        """The engine's token stream, moved to another healthy replica when
+        the serving engine fails BEFORE its first token (worker died, HIP
+        fault): nothing reached the client yet, so the request is simply
+        resubmitted (up to ``attempts`` replicas).  After a token has been
+        streamed the error is the client's, as in the reference."""
+        st = self.state
+        circuit = getattr(st, "circuit", None)
+        tried = {box["target"].device_id}
+        while True:
+            gen = box["target"].engine.generate(prompt_ids, params)
+            emitted, failed = False, None
+            try:
+                async for it in gen:
+                    if it.token >= 0:
+                        emitted = True
+                    if (it.finish is not None and it.finish.startswith("error")
+                            and not emitted):
+                        failed = it
+                        break
+                    yield it
+                    if it.finish is not None:
+                        return
+            except ConnectionError as e:          # link already down at submit
+                if emitted:
+                    raise
+                failed = StreamItem(-1, 0.0, f"error:{e}")
+            finally:
+                await gen.aclose()
+            if failed is None:
+                return
+            if circuit is not None:
+                circuit.record(box["target"].device_id, False)
+            nxt = None if len(tried) >= attempts else \
+                st.registry.select(model, "chat", circuit, exclude=tried)
+            if nxt is None:
+                yield failed
+                return
+            log.warning("chat request failed on %s before its first token (%s); retrying on %s",
+                        box["target"].device_id, failed.finish, nxt.device_id)
+            box["target"].inflight -= 1
+            nxt.inflight += 1
+            box["target"] = nxt
+            tried.add(nxt.device_id)
 
     async def _multi(self, request, target, model, prompt_ids, params, n, stream, include_usage,
                      headers, t0):
@@ -267,11 +317,11 @@ class ChatHandler:
             self._record(target, model, status, t0, len(prompt_ids), stats["n_out"],
                          stats["ttft"], headers.get(tracing.HEADER, ""), n=n)
 
-    async def _sync(self, target, model, prompt_ids, params, headers, t0):
+    async def _sync(self, box, model, prompt_ids, params, headers, t0):
         st = self.state
-        detok = IncrementalDetokenizer(target.tokenizer, params.stop)
+        detok = IncrementalDetokenizer(box["target"].tokenizer, params.stop)
         text, n_out, finish, lps = [], 0, "stop", []
-        gen = target.engine.generate(prompt_ids, params)
+        gen = self._failover(box, model, prompt_ids, params)
         ttft = None
         try:
             async for it in gen:
@@ -291,6 +341,7 @@ class ChatHandler:
         finally:
             await gen.aclose()
         text.append(detok.flush())
+        target = box["target"]
         if finish.startswith("error"):
             self._record(target, model, "error", t0, len(prompt_ids), n_out, ttft,
                          headers.get(tracing.HEADER, ""))
@@ -310,9 +361,10 @@ class ChatHandler:
         r.headers.update(headers)
         return r
 
-    async def _stream(self, request, target, model, prompt_ids, params, include_usage, headers,
+    async def _stream(self, request, box, model, prompt_ids, params, include_usage, headers,
                       t0):
         st = self.state
+        target = box["target"]
         resp = web.StreamResponse(status=200, headers={
             "Content-Type": "text/event-stream", "Cache-Control": "no-cache",
             "Connection": "keep-alive", **headers})
@@ -324,7 +376,7 @@ class ChatHandler:
         detok = IncrementalDetokenizer(target.tokenizer, params.stop)
         n_out, finish, first = 0, "stop", True
         ttft = None
-        gen = target.engine.generate(prompt_ids, params)
+        gen = self._failover(box, model, prompt_ids, params)
         status = "ok"
         try:
             async for it in gen:
@@ -369,7 +421,7 @@ class ChatHandler:
             status = "client_gone"
         finally:
             await gen.aclose()
-            self._record(target, model, status, t0, len(prompt_ids), n_out, ttft,
+            self._record(box["target"], model, status, t0, len(prompt_ids), n_out, ttft,
                          headers.get(tracing.HEADER, ""))
         return resp
 

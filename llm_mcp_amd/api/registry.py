@@ -98,8 +98,10 @@ class ModelRegistry:
         return sorted({k for k, v in self._models.items()
                        if any(kind is None or m.kind == kind for m in v)})
 
-    def select(self, model: str, kind: str, circuit=None) -> LocalModel | None:
-        cands = [m for m in self.replicas(model) if m.kind == kind]
+    def select(self, model: str, kind: str, circuit=None,
+               exclude: set | None = None) -> LocalModel | None:
+        cands = [m for m in self.replicas(model) if m.kind == kind
+                 and (not exclude or m.device_id not in exclude)]
         if circuit is not None:
             healthy = [m for m in cands if not circuit.is_degraded(m.device_id)]
             cands = healthy or []

@@ -234,8 +234,48 @@ def table_from_rows(rows: list[dict], margin: float) -> list[dict]:
     return _consistent_bn(out)
 
 
+def encoder(ms: list[int]) -> None:
+    """Prefill / encoder shapes (nomic-bert, Llama-3-8B prefill): every K11
+    configuration (S = 1) vs the older gemm_nt kernel vs hipBLASLt, warm
+    operands (uniform [-1, 1)), TFLOP/s."""
+    shapes = {"nomic.qkv": (2304, 768), "nomic.o": (768, 768), "nomic.gate_up": (6144, 768),
+              "nomic.down": (768, 3072), "l8b.qkv": (6144, 4096), "l8b.gate_up": (28672, 4096),
+              "l8b.down": (4096, 14336)}
+    cfgs = ops.native().dgemm_configs()
+    for M in ms:
+        for name, (N, K) in shapes.items():
+            if name.startswith("l8b") and M < 8192:
+                continue
+            x = torch.rand(M, K, device="cuda", dtype=torch.bfloat16) * 2 - 1
+            w = (torch.rand(N, K, device="cuda", dtype=torch.bfloat16) * 2 - 1) * K ** -0.5
+            fl = 2.0 * M * N * K
+            iters = max(5, min(50, int(2e12 / fl)))
+            t_lib = _time(lambda i: torch.nn.functional.linear(x, w), iters)
+            t_nt = _time(lambda i: ops.gemm_nt(x, w), iters) if ops.gemm_nt_supported(N, K) \
+                else None
+            ref = torch.nn.functional.linear(x, w).float()
+            best = None
+            for cfg, (bm, bn) in enumerate(cfgs):
+                if N % bn:
+                    continue
+                out = ops.dgemm(x, w, cfg, 1)
+                if not (out.float() - ref).abs().max().item() <= 2e-2 * ref.abs().max().item():
+                    print(f"  !! {name} M={M} cfg={cfg}: mismatch", file=sys.stderr)
+                    continue
+                t = _time(lambda i: ops.dgemm(x, w, cfg, 1, out=out), iters)
+                if best is None or t < best[0]:
+                    best = (t, cfg, bm, bn)
+            line = f"{name:13s} M={M:6d} lib {fl / t_lib / 1e6:6.0f} TF"
+            if t_nt:
+                line += f" | gemm_nt {fl / t_nt / 1e6:6.0f} TF"
+            if best:
+                line += f" | K11 cfg {best[1]} ({best[2]}x{best[3]}) {fl / best[0] / 1e6:6.0f} TF"
+            print(line, flush=True)
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
+    ap.add_argument("--encoder", default="", help="comma list of M: prefill/encoder shapes")
     ap.add_argument("--model", default="llama-3-8b")
     ap.add_argument("--tp", type=int, default=1)
     ap.add_argument("--m", default=",".join(map(str, BUCKETS)))
@@ -253,6 +293,9 @@ def main(argv=None):
         return
     ops.native()
     os.environ.setdefault("LMX_DGEMM", "0")
+    if a.encoder:
+        encoder([int(v) for v in a.encoder.split(",")])
+        return
     from ..engine.engine import _load_gemm_tuning
     _load_gemm_tuning()       # the library as served: hipBLASLt with the TunableOp table
     ms = [int(v) for v in a.m.split(",") if v]

@@ -359,7 +359,7 @@ int dgemm(void* C, const void* A, const void* W, float* slabs, unsigned* tickets
   if (M <= 0) return 0;
   if (cfg < 0 || cfg >= kNumDgCfgs || splits < 1 || epi < 0 || epi > 2) return -1;
   const DgCfg c = kDgCfgs[cfg];
-  if (M > 256 || N % c.bn != 0 || K % (splits * DBK) != 0) return -1;
+  if (N % c.bn != 0 || K % (splits * DBK) != 0) return -1;
   if (epi == 2 && slabs == nullptr) return -2;
   if (splits > 1 && epi != 2) {
     if (slabs == nullptr || tickets == nullptr) return -2;

@@ -157,6 +157,50 @@ def enumerate_gpus() -> list[GpuInfo]:
     return gpus
 
 
+def gpu_telemetry(drm_root: str = "/sys/class/drm") -> dict[int, dict]:
+    """Cheap live GPU counters from the amdgpu DRM sysfs (no subprocess):
+    {gpu index: {"busy_pct", "hbm_used_bytes"}}.  Cards are matched to the
+    enumeration by PCI location (KFD location_id = bus << 8 | dev << 3 | fn),
+    falling back to card order.  Empty where the files do not exist."""
+    cards = []
+    try:
+        names = sorted((n for n in os.listdir(drm_root) if re.fullmatch(r"card\d+", n)),
+                       key=lambda n: int(n[4:]))
+    except OSError:
+        return {}
+    for n in names:
+        dev = os.path.join(drm_root, n, "device")
+        try:
+            with open(os.path.join(dev, "vendor")) as f:
+                if f.read().strip() != "0x1002":
+                    continue
+        except OSError:
+            continue
+        rec = {}
+        for key, fname in (("busy_pct", "gpu_busy_percent"), ("hbm_used_bytes", "mem_info_vram_used")):
+            try:
+                with open(os.path.join(dev, fname)) as f:
+                    rec[key] = int(f.read().strip())
+            except (OSError, ValueError):
+                pass
+        loc = None
+        m = re.search(r"([0-9a-f]{2}):([0-9a-f]{2})\.([0-7])$", os.path.realpath(dev))
+        if m:
+            loc = (int(m.group(1), 16) << 8) | (int(m.group(2), 16) << 3) | int(m.group(3))
+        if rec:
+            cards.append((loc, rec))
+    by_loc = {}
+    for g in from_kfd():
+        try:
+            by_loc[int(g.pci_bus)] = g.index
+        except ValueError:
+            pass
+    out = {}
+    for i, (loc, rec) in enumerate(cards):
+        out[by_loc.get(loc, i) if loc is not None else i] = rec
+    return out
+
+
 def host_id() -> str:
     return os.environ.get("LMX_NODE_ID") or socket.gethostname()
 

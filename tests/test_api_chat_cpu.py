@@ -146,3 +146,48 @@ def test_n_choices_sync_and_stream(engine):
             assert r.status == 400 and (await r.json())["error"] == "invalid_n"
             aeng.stop()
     _run(go())
+
+
+class _DeadEngine:
+    """A replica whose worker died: every request fails before any token."""
+
+    def __init__(self):
+        self.calls = 0
+
+    async def generate(self, prompt_ids, params, priority=0, stats=None):
+        from llm_mcp_amd.engine.async_engine import StreamItem
+        self.calls += 1
+        yield StreamItem(-1, 0.0, "error:engine_disconnected")
+
+
+def test_failover_before_first_token(engine):
+    """Sync and streamed requests that land on a replica failing before its
+    first token are resubmitted to a healthy replica (the breaker is fed);
+    the client sees a normal completion."""
+    from llm_mcp_amd.policy.circuit import CircuitBreaker
+
+    async def go():
+        st, aeng = _state(engine)
+        dead = _DeadEngine()
+        st.registry.add(LocalModel("tiny-llama", "chat", "dead0", dead, for_model(engine.cfg),
+                                   engine.cfg, max_model_len=512, capacity=8))
+        st.circuit = CircuitBreaker()
+        async with TestClient(TestServer(make_app(st))) as c:
+            aeng.start(asyncio.get_running_loop())
+            for stream in (False, True, False):
+                # make the dead replica the least loaded one so it is picked first
+                for m in st.registry.replicas("tiny-llama"):
+                    m.inflight = 0 if m.device_id == "dead0" else 1
+                r = await c.post("/v1/chat/completions", json={
+                    "model": "tiny-llama", "messages": [{"role": "user", "content": "hi"}],
+                    "max_tokens": 5, "temperature": 0, "ignore_eos": True, "stream": stream})
+                assert r.status == 200
+                body = await r.text()
+                if stream:
+                    assert '"finish_reason":"length"' in body.replace(" ", "") and \
+                        body.rstrip().endswith("[DONE]")
+                else:
+                    assert json.loads(body)["usage"]["completion_tokens"] == 5
+            assert dead.calls >= 2
+            assert st.circuit.status("dead0") in ("degraded", "probe", "ok")
+    _run(go())

@@ -261,3 +261,19 @@ def test_costs_feedback_stats_benchmarks():
             r = await c.post("/v1/knowledge/ingest", json={"text": "short", "target": "lightrag"})
             assert (await r.json())["error"] == "text_too_short"
     run(go())
+
+
+def test_gpu_telemetry_from_drm_sysfs(tmp_path):
+    """gpu_hbm_used_bytes / gpu_util come from the amdgpu DRM sysfs files."""
+    from llm_mcp_amd.devices import rocm_enum
+    for i, (busy, used, vendor) in enumerate([(37, 123456789, "0x1002"), (5, 7, "0x8086")]):
+        pci = tmp_path / f"pci0000:00/0000:0{i + 3}:00.0"
+        pci.mkdir(parents=True)
+        (pci / "vendor").write_text(vendor + "\n")
+        (pci / "gpu_busy_percent").write_text(f"{busy}\n")
+        (pci / "mem_info_vram_used").write_text(f"{used}\n")
+        card = tmp_path / "drm" / f"card{i}"
+        card.mkdir(parents=True)
+        (card / "device").symlink_to(pci)
+    t = rocm_enum.gpu_telemetry(str(tmp_path / "drm"))
+    assert t == {0: {"busy_pct": 37, "hbm_used_bytes": 123456789}}
