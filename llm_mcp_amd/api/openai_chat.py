@@ -32,6 +32,7 @@ from ..utils import tracing
 from .helpers import dumps, read_json, write_error, write_json
 
 log = logging.getLogger("lmx.chat")
+RESTART = StreamItem(-2, 0.0, None)   # _failover: generation restarted on another replica
 
 CHAT_TIMEOUT_S = 120.0
 
@@ -152,12 +153,16 @@ class ChatHandler:
         finally:
             box["target"].inflight -= 1
 
-    async def _failover(self, box, model, prompt_ids, params, attempts: int = 3):
+    async def _failover(self, box, model, prompt_ids, params, attempts: int = 3,
+                        restartable: bool = False):
         """The engine's token stream, moved to another healthy replica when
         the serving engine fails BEFORE its first token (worker died, HIP
         fault): nothing reached the client yet, so the request is simply
-        resubmitted (up to ``attempts`` replicas).  After a token has been
-        streamed the error is the client's, as in the reference."""
+        resubmitted (up to ``attempts`` replicas).  ``restartable`` (the
+        non-streaming response, buffered until the end): a failure after
+        tokens also moves the request; a ``RESTART`` item tells the caller to
+        drop what it collected.  After a streamed token the error is the
+        client's, as in the reference."""
         st = self.state
         circuit = getattr(st, "circuit", None)
         tried = {box["target"].device_id}
@@ -169,14 +174,14 @@ class ChatHandler:
                     if it.token >= 0:
                         emitted = True
                     if (it.finish is not None and it.finish.startswith("error")
-                            and not emitted):
+                            and (restartable or not emitted)):
                         failed = it
                         break
                     yield it
                     if it.finish is not None:
                         return
             except ConnectionError as e:          # link already down at submit
-                if emitted:
+                if emitted and not restartable:
                     raise
                 failed = StreamItem(-1, 0.0, f"error:{e}")
             finally:
@@ -196,6 +201,8 @@ class ChatHandler:
             nxt.inflight += 1
             box["target"] = nxt
             tried.add(nxt.device_id)
+            if emitted:
+                yield RESTART
 
     async def _multi(self, request, target, model, prompt_ids, params, n, stream, include_usage,
                      headers, t0):
@@ -321,10 +328,14 @@ class ChatHandler:
         st = self.state
         detok = IncrementalDetokenizer(box["target"].tokenizer, params.stop)
         text, n_out, finish, lps = [], 0, "stop", []
-        gen = self._failover(box, model, prompt_ids, params)
+        gen = self._failover(box, model, prompt_ids, params, restartable=True)
         ttft = None
         try:
             async for it in gen:
+                if it is RESTART:        # moved to another replica mid-generation
+                    detok = IncrementalDetokenizer(box["target"].tokenizer, params.stop)
+                    text, n_out, lps = [], 0, []
+                    continue
                 if it.token >= 0:
                     if ttft is None:
                         ttft = time.time() - t0

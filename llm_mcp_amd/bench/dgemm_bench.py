@@ -234,7 +234,7 @@ def table_from_rows(rows: list[dict], margin: float) -> list[dict]:
     return _consistent_bn(out)
 
 
-def encoder(ms: list[int]) -> None:
+def encoder(ms: list[int], write: bool = False) -> None:
     """Prefill / encoder shapes (nomic-bert, Llama-3-8B prefill): every K11
     configuration (S = 1) vs the older gemm_nt kernel vs hipBLASLt, warm
     operands (uniform [-1, 1)), TFLOP/s."""
@@ -242,6 +242,7 @@ def encoder(ms: list[int]) -> None:
               "nomic.down": (768, 3072), "l8b.qkv": (6144, 4096), "l8b.gate_up": (28672, 4096),
               "l8b.down": (4096, 14336)}
     cfgs = ops.native().dgemm_configs()
+    wins: dict = {}
     for M in ms:
         for name, (N, K) in shapes.items():
             if name.startswith("l8b") and M < 8192:
@@ -270,7 +271,22 @@ def encoder(ms: list[int]) -> None:
                 line += f" | gemm_nt {fl / t_nt / 1e6:6.0f} TF"
             if best:
                 line += f" | K11 cfg {best[1]} ({best[2]}x{best[3]}) {fl / best[0] / 1e6:6.0f} TF"
+                # vs the previous hand-written encoder GEMM (gemm_nt): keep the
+                # K11 tile that wins at the largest M measured
+                wins[(N, K)] = {"N": N, "K": K, "cfg": best[1], "bn": best[3], "M": M,
+                                "tflops": round(fl / best[0] / 1e12 * 1e6, 1),
+                                "gemm_nt_tflops": round(fl / t_nt / 1e6, 1) if t_nt else None,
+                                "lib_tflops": round(fl / t_lib / 1e6, 1)}
             print(line, flush=True)
+    if write:
+        path = os.path.join(os.path.dirname(os.path.dirname(__file__)), "config",
+                            "dgemm_gfx950.json")
+        with open(path) as f:
+            doc = json.load(f)
+        doc["encoder"] = sorted(wins.values(), key=lambda e: (e["N"], e["K"]))
+        with open(path, "w") as f:
+            json.dump(doc, f, indent=1)
+        print(f"wrote {len(wins)} encoder entries to {path}")
 
 
 def main(argv=None):
@@ -294,7 +310,7 @@ def main(argv=None):
     ops.native()
     os.environ.setdefault("LMX_DGEMM", "0")
     if a.encoder:
-        encoder([int(v) for v in a.encoder.split(",")])
+        encoder([int(v) for v in a.encoder.split(",")], a.write)
         return
     from ..engine.engine import _load_gemm_tuning
     _load_gemm_tuning()       # the library as served: hipBLASLt with the TunableOp table

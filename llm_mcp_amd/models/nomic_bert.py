@@ -42,10 +42,16 @@ class NomicBertModel:
         self.scale = 1.0 / math.sqrt(self.D)
         self.cos_sin = ref.rope_cos_sin(cfg.max_position, self.D, cfg.rope_theta, self.device)
         self.w = weights or self._random_weights(seed)
-        # gate/up rows interleaved per 64 channels for the fused SwiGLU epilogue
+        # gate/up rows interleaved for the fused SwiGLU epilogue: per BN/2
+        # channels of the K11 tile where the encoder table picks K11, else per
+        # 64 channels (gemm_nt act=3)
+        I2, d = self.w["layers"][0]["w_gate_up"].shape
+        self.gu_cfg = ops.encoder_choice(I2, d) if self.device.type == "cuda" else None
+        self.gu_block = ops.DGEMM_CONFIGS[self.gu_cfg][1] // 2 if self.gu_cfg is not None else 64
         for L in self.w["layers"]:
-            if "w_gu_il" not in L and ops.gemm_nt_supported(*L["w_gate_up"].shape):
-                L["w_gu_il"] = ops.interleave_gate_up(L["w_gate_up"])
+            L.pop("w_gu_il", None)      # always this model's own layout (never a copy's)
+            if ops.gemm_nt_supported(*L["w_gate_up"].shape) and I2 // 2 % self.gu_block == 0:
+                L["w_gu_il"] = ops.interleave_gate_up(L["w_gate_up"], self.gu_block)
 
     def _random_weights(self, seed):
         cfg, dev, dt = self.cfg, self.device, self.dtype
@@ -67,6 +73,9 @@ class NomicBertModel:
                 "emb_ln_w": ones(), "emb_ln_b": zeros(), "layers": layers}
 
     def _linear(self, x, w, residual=None):
+        cfg = ops.encoder_choice(w.shape[0], w.shape[1]) if x.is_cuda else None
+        if cfg is not None and residual is None:
+            return ops.dgemm(x, w, cfg, 1)          # K11 where it beat gemm_nt
         if ops.gemm_nt_supported(w.shape[0], w.shape[1]):
             return ops.gemm_nt(x, w, residual=residual)
         y = torch.nn.functional.linear(x, w)
@@ -119,7 +128,9 @@ class NomicBertModel:
                                         causal=False, Hq=H)
             o = self._linear(attn, L["wo"])
             h = ops.layer_norm(o, L["ln1_w"], L["ln1_b"], cfg.ln_eps, residual=x)
-            if "w_gu_il" in L:   # K8 fused into the GEMM epilogue
+            if "w_gu_il" in L and self.gu_cfg is not None and h.is_cuda:
+                g = ops.dgemm(h, L["w_gu_il"], self.gu_cfg, 1, epi=1)   # K11 + fused K8
+            elif "w_gu_il" in L and self.gu_block == 64:   # K8 fused into gemm_nt
                 g = ops.gemm_nt(h, L["w_gu_il"], act=ops.ACT_SWIGLU)
             else:
                 g = ops.silu_mul(self._linear(h, L["w_gate_up"]))

@@ -627,6 +627,30 @@ def _dg_table() -> dict:
     return DGEMM_TABLE
 
 
+_ENC_TABLE: dict | None = None
+
+
+def encoder_choice(N: int, K: int) -> int | None:
+    """K11 tile for a prefill / encoder-sized GEMM of this (N, K), where it was
+    measured faster than the older hand-written gemm_nt (config
+    dgemm_gfx950.json "encoder", bench/dgemm_bench.py --encoder); None keeps
+    gemm_nt."""
+    global _ENC_TABLE
+    if _ENC_TABLE is None:
+        _ENC_TABLE = {}
+        _dg_table()
+        import json
+        import os
+        path = os.environ.get("LMX_DGEMM_TABLE") or os.path.join(
+            os.path.dirname(os.path.dirname(__file__)), "config", "dgemm_gfx950.json")
+        if os.environ.get("LMX_DGEMM", "1") == "1" and os.path.exists(path):
+            with open(path) as f:
+                for e in json.load(f).get("encoder", []):
+                    if e.get("gemm_nt_tflops") is None or e["tflops"] > e["gemm_nt_tflops"]:
+                        _ENC_TABLE[(int(e["N"]), int(e["K"]))] = int(e["cfg"])
+    return _ENC_TABLE.get((N, K))
+
+
 def dgemm_choice(M: int, N: int, K: int, epi: int = 0) -> tuple[int, int] | None:
     """(cfg, splits) for this decode GEMM, or None (use the library)."""
     if not 0 < M <= DGEMM_MAX_M:

@@ -191,3 +191,34 @@ def test_failover_before_first_token(engine):
             assert dead.calls >= 2
             assert st.circuit.status("dead0") in ("degraded", "probe", "ok")
     _run(go())
+
+
+class _DiesMidway:
+    """A replica that streams two tokens, then loses its worker."""
+
+    async def generate(self, prompt_ids, params, priority=0, stats=None):
+        from llm_mcp_amd.engine.async_engine import StreamItem
+        yield StreamItem(7, 0.0, None)
+        yield StreamItem(8, 0.0, None)
+        yield StreamItem(-1, 0.0, "error:engine_disconnected")
+
+
+def test_sync_request_restarts_after_midway_failure(engine):
+    """A non-streaming request is buffered until the end, so a replica dying
+    mid-generation costs a restart on another replica, not an error."""
+    async def go():
+        st, aeng = _state(engine)
+        st.registry.add(LocalModel("tiny-llama", "chat", "flaky0", _DiesMidway(),
+                                   for_model(engine.cfg), engine.cfg, max_model_len=512,
+                                   capacity=8))
+        async with TestClient(TestServer(make_app(st))) as c:
+            aeng.start(asyncio.get_running_loop())
+            for m in st.registry.replicas("tiny-llama"):
+                m.inflight = 0 if m.device_id == "flaky0" else 1
+            r = await c.post("/v1/chat/completions", json={
+                "model": "tiny-llama", "messages": [{"role": "user", "content": "hi"}],
+                "max_tokens": 6, "temperature": 0, "ignore_eos": True})
+            body = await r.json()
+            assert r.status == 200, body
+            assert body["usage"]["completion_tokens"] == 6
+    _run(go())

@@ -79,6 +79,8 @@ for step in "$@"; do
       run config5 900 python -u -m llm_mcp_amd.bench.serving_bench mixed --gpus 0 \
           --replicas-per-gpu 2 --fault gpu_error:0.002 --fault-device gpu0.r1 \
           --jobs 1024 --concurrency 256 --sync-every 4 --max-tokens 64 --chars 512 || exit $? ;;
+    encoder_bench)
+      run encoder_bench 600 python -u -m llm_mcp_amd.bench.dgemm_bench --encoder 4096,32768 || exit $? ;;
     smoke)
       run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     *)
