@@ -75,10 +75,13 @@ __global__ void __launch_bounds__(256) rmsnorm_kernel(
 // residual add and the norm in one pass, so the projection needs neither a
 // reduction pass nor a bf16 output round trip.  residual += sum_s slab[s]
 // (rounded to bf16 once, as the bf16 hidden state), out = rms_norm(residual).
-template <int VPT>
+// S is a template parameter so the S x 2 slab loads of a chunk are all issued
+// before the first add (a runtime trip count serialised them: S dependent
+// memory latencies per chunk, ~8 us per 256-row call at S = 4).
+template <int VPT, int S>
 __global__ void __launch_bounds__(256) rmsnorm_slabs_kernel(
     bf16_t* __restrict__ out, bf16_t* __restrict__ residual, const float* __restrict__ slabs,
-    int S, long slab_stride, const bf16_t* __restrict__ w, int cols, long out_stride,
+    long slab_stride, const bf16_t* __restrict__ w, int cols, long out_stride,
     float eps) {
   __shared__ float scratch[16];
   const int row = blockIdx.x;
@@ -92,13 +95,19 @@ __global__ void __launch_bounds__(256) rmsnorm_slabs_kernel(
   for (int i = 0; i < VPT; ++i) {
     const int c = threadIdx.x + i * blockDim.x;
     if (c < nchunk) {
-      f32x4_t a0 = *reinterpret_cast<const f32x4_t*>(xr + c * 8);
-      f32x4_t a1 = *reinterpret_cast<const f32x4_t*>(xr + c * 8 + 4);
-      for (int s = 1; s < S; ++s) {
-        a0 += *reinterpret_cast<const f32x4_t*>(xr + s * slab_stride + c * 8);
-        a1 += *reinterpret_cast<const f32x4_t*>(xr + s * slab_stride + c * 8 + 4);
+      f32x4_t p0[S], p1[S];
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        p0[s] = *reinterpret_cast<const f32x4_t*>(xr + s * slab_stride + c * 8);
+        p1[s] = *reinterpret_cast<const f32x4_t*>(xr + s * slab_stride + c * 8 + 4);
       }
       const u16x8 b = *reinterpret_cast<const u16x8*>(rr + c * 8);
+      f32x4_t a0 = p0[0], a1 = p1[0];
+#pragma unroll
+      for (int s = 1; s < S; ++s) {
+        a0 += p0[s];
+        a1 += p1[s];
+      }
       u16x8 h;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -216,15 +225,24 @@ int rmsnorm_slabs(void* out, void* residual, const float* slabs, int S, long sla
   const int threads = pick_threads(nchunk);
   const int vpt = (nchunk + threads - 1) / threads;
   dim3 g(rows), b(threads);
-#define LMX_RMSS(V)                                                                         \
-  rmsnorm_slabs_kernel<V><<<g, b, 0, stream>>>((bf16_t*)out, (bf16_t*)residual, slabs, S,   \
-                                               slab_stride, (const bf16_t*)w, cols,         \
-                                               out_stride, eps)
-  if (vpt <= 1) LMX_RMSS(1);
-  else if (vpt <= 2) LMX_RMSS(2);
-  else if (vpt <= 4) LMX_RMSS(4);
-  else if (vpt <= 8) LMX_RMSS(8);
+#define LMX_RMSS(V, SS)                                                                     \
+  rmsnorm_slabs_kernel<V, SS><<<g, b, 0, stream>>>((bf16_t*)out, (bf16_t*)residual, slabs,  \
+                                                   slab_stride, (const bf16_t*)w, cols,     \
+                                                   out_stride, eps)
+#define LMX_RMSS_S(V)                                                                       \
+  switch (S) {                                                                              \
+    case 1: LMX_RMSS(V, 1); break;                                                          \
+    case 2: LMX_RMSS(V, 2); break;                                                          \
+    case 4: LMX_RMSS(V, 4); break;                                                          \
+    case 8: LMX_RMSS(V, 8); break;                                                          \
+    case 16: LMX_RMSS(V, 16); break;                                                        \
+    default: return -3;                                                                     \
+  }
+  if (vpt <= 1) { LMX_RMSS_S(1) }
+  else if (vpt <= 2) { LMX_RMSS_S(2) }
+  else if (vpt <= 4) { LMX_RMSS_S(4) }
   else return -2;
+#undef LMX_RMSS_S
 #undef LMX_RMSS
   return (int)hipGetLastError();
 }

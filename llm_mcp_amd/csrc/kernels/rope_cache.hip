@@ -35,6 +35,12 @@ __device__ __forceinline__ void qk_norm(float (&a)[4], float (&b)[4], const bf16
   }
 }
 
+// Decode rows: one workgroup per token.  A thread owns up to IT rotation
+// items (4 pairs of one head each); all of its q/k and cos/sin loads are
+// issued before the first use (IT is a template parameter: a runtime-bounded
+// loop re-serialised them into IT dependent memory latencies), then the V row
+// goes to the transposed page 4 elements (one 8-B load) per thread.
+template <int IT>
 __global__ void __launch_bounds__(256) rope_cache_kernel(
     bf16_t* __restrict__ qkv, long qkv_stride, const int* __restrict__ positions,
     const float* __restrict__ cos_sin, int Hq, int Hkv, int D,
@@ -49,21 +55,44 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(
   const float* cs = cos_sin + (long)pos * D;
   const int slot = slot_mapping ? slot_mapping[t] : -1;
   const int blk = slot >= 0 ? slot / BS : 0, off = slot >= 0 ? slot % BS : 0;
-
-  // rotate q (and k) heads
   const int nrot = (Hq + Hkv) * tph;
-  for (int it = threadIdx.x; it < nrot; it += blockDim.x) {
+
+  bf16x4_t x1[IT], x2[IT];
+  float4 c[IT], sn[IT];
+#pragma unroll
+  for (int k = 0; k < IT; ++k) {
+    const int it = threadIdx.x + k * 256;
+    if (it < nrot) {
+      const int h = it / tph, i = (it % tph) * 4;
+      const bf16_t* hp = row + (long)h * D;
+      x1[k] = *reinterpret_cast<const bf16x4_t*>(hp + i);
+      x2[k] = *reinterpret_cast<const bf16x4_t*>(hp + half + i);
+      c[k] = *reinterpret_cast<const float4*>(cs + i);
+      sn[k] = *reinterpret_cast<const float4*>(cs + half + i);
+    }
+  }
+  // V row loads issued with the rest (4 elements per thread per pass)
+  const bf16_t* vrow = row + (long)(Hq + Hkv) * D;
+  const int nv = Hkv * D;
+  constexpr int VP = 2;                       // V passes held in registers (nv <= 2048)
+  bf16x4_t vv[VP];
+#pragma unroll
+  for (int k = 0; k < VP; ++k) {
+    const int e = (threadIdx.x + k * 256) * 4;
+    if (slot >= 0 && v_cache && e < nv) vv[k] = *reinterpret_cast<const bf16x4_t*>(vrow + e);
+  }
+#pragma unroll
+  for (int k = 0; k < IT; ++k) {
+    const int it = threadIdx.x + k * 256;
+    if (it >= nrot) continue;
     const int h = it / tph, i = (it % tph) * 4;
     bf16_t* hp = row + (long)h * D;
-    const bf16x4_t x1 = *reinterpret_cast<const bf16x4_t*>(hp + i);
-    const bf16x4_t x2 = *reinterpret_cast<const bf16x4_t*>(hp + half + i);
-    const float4 c = *reinterpret_cast<const float4*>(cs + i);
-    const float4 s = *reinterpret_cast<const float4*>(cs + half + i);
-    const float cc[4] = {c.x, c.y, c.z, c.w}, ss[4] = {s.x, s.y, s.z, s.w};
+    const float cc[4] = {c[k].x, c[k].y, c[k].z, c[k].w};
+    const float ss[4] = {sn[k].x, sn[k].y, sn[k].z, sn[k].w};
     const bool is_k = h >= Hq;
     float a[4], b[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) a[j] = bf2f((uint16_t)x1[j]), b[j] = bf2f((uint16_t)x2[j]);
+    for (int j = 0; j < 4; ++j) a[j] = bf2f((uint16_t)x1[k][j]), b[j] = bf2f((uint16_t)x2[k][j]);
     if (q_norm) qk_norm(a, b, is_k ? k_norm : q_norm, i, half, D, eps);
     bf16x4_t o1, o2;
 #pragma unroll
@@ -84,11 +113,14 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(
   if (slot < 0 || !v_cache) return;
   // v -> transposed cache page (2-B scatter; one token per block so a page
   // row of BS tokens is completed by BS consecutive blocks, merged in L2)
-  const bf16_t* vrow = row + (long)(Hq + Hkv) * D;
-  const int nv = Hkv * D;
-  for (int it = threadIdx.x; it < nv; it += blockDim.x) {
-    const int h = it / D, d = it % D;
-    v_cache[(((long)blk * Hkv + h) * D + d) * BS + off] = vrow[it];
+#pragma unroll
+  for (int k = 0; k < VP; ++k) {
+    const int e = (threadIdx.x + k * 256) * 4;
+    if (e >= nv) continue;
+    const int h = e / D, d = e % D;
+    bf16_t* vp = v_cache + (((long)blk * Hkv + h) * D + d) * BS + off;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) vp[(long)j * BS] = (bf16_t)vv[k][j];
   }
 }
 
@@ -191,11 +223,21 @@ int rope_cache(void* qkv, long qkv_stride, const int* positions, const float* co
   if (D % 8 != 0 || D > 256) return -1;
   if ((q_norm == nullptr) != (k_norm == nullptr) || (q_norm && D != 128)) return -1;
   const int n1 = tile_from < 0 ? 0 : (tile_from > T ? T : tile_from);
-  if (n1 > 0)
-    rope_cache_kernel<<<dim3(n1), dim3(256), 0, stream>>>(
-        (bf16_t*)qkv, qkv_stride, positions, cos_sin, Hq, Hkv, D, slot_mapping,
-        (bf16_t*)k_cache, (bf16_t*)v_cache, BS, rotate_k_inplace, (const bf16_t*)q_norm,
-        (const bf16_t*)k_norm, eps);
+  if (n1 > 0) {
+    const int nrot = (Hq + Hkv) * (D / 8);
+    if (Hkv * D > 2048 || nrot > 6 * 256) return -1;
+#define LMX_RC(IT)                                                                            \
+    rope_cache_kernel<IT><<<dim3(n1), dim3(256), 0, stream>>>(                                 \
+        (bf16_t*)qkv, qkv_stride, positions, cos_sin, Hq, Hkv, D, slot_mapping,               \
+        (bf16_t*)k_cache, (bf16_t*)v_cache, BS, rotate_k_inplace, (const bf16_t*)q_norm,      \
+        (const bf16_t*)k_norm, eps)
+    if (nrot <= 256) LMX_RC(1);
+    else if (nrot <= 512) LMX_RC(2);
+    else if (nrot <= 768) LMX_RC(3);
+    else if (nrot <= 1024) LMX_RC(4);
+    else LMX_RC(6);
+#undef LMX_RC
+  }
   if (T > n1)
     rope_cache_tiled_kernel<<<dim3((T - n1 + RT - 1) / RT), dim3(256), 0, stream>>>(
         (bf16_t*)qkv, qkv_stride, positions, cos_sin, n1, T, Hq, Hkv, D, slot_mapping,
