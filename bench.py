@@ -98,7 +98,12 @@ def start_front_door(a, world: int, tag: str, socks: list[str]):
     for r, s in enumerate(socks):
         engines += ["--engine", f"{a.model}=unix:{s},device=gpu{r}"]
     env = dict(os.environ, LOG_LEVEL=os.environ.get("LMX_BENCH_API_LOG", "WARNING"))
-    apis, ready_files = [], []
+    # node-wide in-flight counts: the API processes balance on them together,
+    # so no engine receives more streams than its slots (api/shared_load.py)
+    load_file = f"/dev/shm/lmx-bench-{tag}.load"
+    if os.path.exists(load_file):
+        os.unlink(load_file)
+    apis, ready_files = [], [load_file]     # ready files + the load file: all removed at exit
     for i in range(n_api):
         rf = f"/tmp/lmx-bench-{tag}-api{i}.ready"
         if os.path.exists(rf):
@@ -106,7 +111,8 @@ def start_front_door(a, world: int, tag: str, socks: list[str]):
         ready_files.append(rf)
         apis.append(subprocess.Popen(
             [sys.executable, "-m", "llm_mcp_amd.api.serve", "--port", str(port),
-             "--reuse-port", "--ready-file", rf] + engines,
+             "--reuse-port", "--ready-file", rf, "--shared-load", load_file,
+             "--api-index", str(i), "--api-count", str(n_api)] + engines,
             cwd=HERE, env=env, stdout=subprocess.DEVNULL))
     total = a.concurrency * world
     per = [total // n_lg + (1 if i < total % n_lg else 0) for i in range(n_lg)]

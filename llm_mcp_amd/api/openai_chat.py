@@ -139,8 +139,13 @@ class ChatHandler:
             n = 0
         if not 1 <= n <= 16:
             return write_error(400, "invalid_n", "'n' must be an integer in [1, 16]")
-        box = {"target": target}      # the replica serving the request (failover moves it)
-        target.inflight += 1
+        # the replica that serves the request, counted against the node-wide
+        # load in the same step as its selection (failover moves it)
+        target = st.registry.select(model, "chat", getattr(st, "circuit", None), acquire=True)
+        if target is None:
+            st.metrics.chat_requests(model, "none", "no_device")
+            return write_error(503, "no_device", f"No online device has model '{model}'")
+        box = {"target": target}
         t0 = time.time()
         try:
             if n > 1:
@@ -151,7 +156,7 @@ class ChatHandler:
                                           include_usage, extra_headers, t0)
             return await self._sync(box, model, prompt_ids, params, extra_headers, t0)
         finally:
-            box["target"].inflight -= 1
+            st.registry.release(box["target"])
 
     async def _failover(self, box, model, prompt_ids, params, attempts: int = 3,
                         restartable: bool = False):
@@ -191,14 +196,13 @@ class ChatHandler:
             if circuit is not None:
                 circuit.record(box["target"].device_id, False)
             nxt = None if len(tried) >= attempts else \
-                st.registry.select(model, "chat", circuit, exclude=tried)
+                st.registry.select(model, "chat", circuit, exclude=tried, acquire=True)
             if nxt is None:
                 yield failed
                 return
             log.warning("chat request failed on %s before its first token (%s); retrying on %s",
                         box["target"].device_id, failed.finish, nxt.device_id)
-            box["target"].inflight -= 1
-            nxt.inflight += 1
+            st.registry.release(box["target"])
             box["target"] = nxt
             tried.add(nxt.device_id)
             if emitted:

@@ -91,12 +91,12 @@ class EmbeddingsHandler:
                 if dims and dims > target.cfg.embed_dim:
                     return write_error(400, "invalid_dimensions",
                                        f"dimensions must be <= {target.cfg.embed_dim}")
-                target.inflight += 1
+                st.registry.acquire(target)
                 try:
                     vecs = await asyncio.wait_for(target.engine.embed(seqs, dims),
                                                   EMBED_TIMEOUT_S)
                 finally:
-                    target.inflight -= 1
+                    st.registry.release(target)
             except Exception as e:  # device failure: circuit + retry elsewhere
                 last_err = e
                 st.circuit.record(target.device_id, False)

@@ -30,6 +30,7 @@ class LocalModel:
     tps: float = 0.0          # last measured decode tokens/s (benchmarks)
     inflight: int = 0
     tags: dict = field(default_factory=dict)
+    lb_slot: int = -1         # column in the front door's SharedLoad (-1: local count only)
 
     def load(self) -> float:
         return self.inflight / max(1, self.capacity)
@@ -61,6 +62,9 @@ class ModelRegistry:
     def __init__(self):
         self._lock = threading.Lock()
         self._models: dict[str, list[LocalModel]] = {}
+        # api/shared_load.SharedLoad when several API processes share the
+        # engines: selection then balances on the node-wide in-flight counts
+        self.balancer = None
 
     @staticmethod
     def canonical(name: str) -> str:
@@ -99,7 +103,11 @@ class ModelRegistry:
                        if any(kind is None or m.kind == kind for m in v)})
 
     def select(self, model: str, kind: str, circuit=None,
-               exclude: set | None = None) -> LocalModel | None:
+               exclude: set | None = None, acquire: bool = False) -> LocalModel | None:
+        """Least-loaded healthy replica with a free slot (else least loaded),
+        ties by measured tokens/s.  ``acquire``: count the request against
+        the pick in the same step (atomically across the API processes of a
+        shared front door); pair with ``release``."""
         cands = [m for m in self.replicas(model) if m.kind == kind
                  and (not exclude or m.device_id not in exclude)]
         if circuit is not None:
@@ -107,5 +115,33 @@ class ModelRegistry:
             cands = healthy or []
         if not cands:
             return None
-        free = [m for m in cands if m.inflight < m.capacity] or cands
-        return min(free, key=lambda m: (m.load(), -m.tps))
+        bal = self.balancer
+        if bal is None or all(m.lb_slot < 0 for m in cands):
+            free = [m for m in cands if m.inflight < m.capacity] or cands
+            m = min(free, key=lambda m: (m.load(), -m.tps))
+            if acquire:
+                m.inflight += 1
+            return m
+        with bal.locked():
+            tot = bal.totals()
+
+            def count(m):
+                return int(tot[m.lb_slot]) if m.lb_slot >= 0 else m.inflight
+            free = [m for m in cands if count(m) < m.capacity] or cands
+            m = min(free, key=lambda m: (count(m) / max(1, m.capacity), -m.tps))
+            if acquire:
+                m.inflight += 1
+                if m.lb_slot >= 0:
+                    bal.add(m.lb_slot, 1)
+        return m
+
+    def acquire(self, m: LocalModel) -> None:
+        m.inflight += 1
+        if self.balancer is not None and m.lb_slot >= 0:
+            with self.balancer.locked():
+                self.balancer.add(m.lb_slot, 1)
+
+    def release(self, m: LocalModel) -> None:
+        m.inflight -= 1
+        if self.balancer is not None and m.lb_slot >= 0:
+            self.balancer.release(m.lb_slot)

@@ -15,9 +15,10 @@ reference's restartable worker units (compose.yml:117,133,149
 ``restart: unless-stopped``).
 
 Several API processes can share one port (``--reuse-port``, SO_REUSEPORT):
-the kernel spreads client connections over them and every process balances
-its own streams over all engines, so one event loop does not bound the
-node's SSE rate (bench.py runs the front door this way).
+the kernel spreads client connections over them, so one event loop does not
+bound the node's SSE rate, and with ``--shared-load`` they select replicas on
+node-wide in-flight counts (api/shared_load.py) -- bench.py runs the front
+door this way.
 """
 from __future__ import annotations
 
@@ -76,7 +77,8 @@ async def _link(state, s: dict, first: asyncio.Future, supervise: bool) -> None:
             s.get("device") or minfo.get("device_id", "gpu0"), c, tok, cfg,
             max_model_len=int(minfo.get("max_model_len", 8192)),
             capacity=int(minfo.get("capacity", 256)),
-            tags={"tp_comm": minfo.get("tp_comm") or {}, "live": info})
+            tags={"tp_comm": minfo.get("tp_comm") or {}, "live": info},
+            lb_slot=int(s.get("slot", -1)))
         state.registry.add(lm)
         log.info("engine %s on %s connected (%s)", s["model"], s["path"], lm.device_id)
         if not first.done():
@@ -106,6 +108,8 @@ async def attach_engines(state, specs: list[dict], supervise: bool = True):
     ``state.engines_ready``).  The link tasks stay alive on
     ``state.engine_links`` and re-attach restarted workers."""
     loop = asyncio.get_running_loop()
+    for i, s in enumerate(specs):
+        s.setdefault("slot", i)           # column in a shared front-door load table
     firsts = [loop.create_future() for _ in specs]
     links = [asyncio.create_task(_link(state, s, f, supervise)) for s, f in zip(specs, firsts)]
     state.engine_links = getattr(state, "engine_links", []) + links
@@ -114,13 +118,20 @@ async def attach_engines(state, specs: list[dict], supervise: bool = True):
     state.engines_ready = True
 
 
-def make_serving_app(specs: list[dict], version: str | None = None, ready_file: str = ""):
+def make_serving_app(specs: list[dict], version: str | None = None, ready_file: str = "",
+                     shared_load: tuple[str, int, int] | None = None):
     """The API process's app: chat + embeddings + /ready over attached
-    engine sockets (attached on startup)."""
+    engine sockets (attached on startup).  ``shared_load`` = (path, index,
+    count): this is API process ``index`` of ``count`` sharing one port, and
+    replica selection balances on the node-wide counts (api/shared_load.py)."""
     state = ServingState(ModelRegistry(), Metrics(),
                          version=version or os.environ.get("CORE_VERSION", "0.1.0"),
                          circuit=CircuitBreaker())
     state.engines_ready = False
+    if shared_load is not None:
+        from .shared_load import SharedLoad
+        path, index, count = shared_load
+        state.registry.balancer = SharedLoad(path, index, count, max(1, len(specs)))
 
     def register(app):
         async def ready(request):
@@ -166,9 +177,16 @@ def main(argv=None):
                     help="SO_REUSEPORT: several API processes serve one port")
     ap.add_argument("--ready-file", default="",
                     help="written once every engine is attached")
+    ap.add_argument("--shared-load", default="",
+                    help="/dev/shm file of node-wide in-flight counts shared by the API "
+                         "processes of one port (with --api-index / --api-count)")
+    ap.add_argument("--api-index", type=int, default=0)
+    ap.add_argument("--api-count", type=int, default=1)
     a = ap.parse_args(argv)
     logging.basicConfig(level=os.environ.get("LOG_LEVEL", "INFO"))
-    app, _ = make_serving_app([parse_engine_spec(s) for s in a.engine], ready_file=a.ready_file)
+    shared = (a.shared_load, a.api_index, a.api_count) if a.shared_load else None
+    app, _ = make_serving_app([parse_engine_spec(s) for s in a.engine], ready_file=a.ready_file,
+                              shared_load=shared)
     web.run_app(app, host=a.host, port=a.port, access_log=None, print=None,
                 reuse_port=a.reuse_port or None)
 

@@ -7,7 +7,9 @@ weights: the weight operand rotates over enough copies (> the 256 MB
 Infinity Cache) that every call streams it from HBM, as in a decode step
 where 15 GB of other weights pass between two reads of one layer.  The
 activation operand stays warm (it was just produced).  Each configuration is
-checked against the library result before it is timed.
+checked against the library result before it is timed.  The fastest
+``NT_TOP`` configurations are timed again with the non-temporal weight stream
+(cfg id | ops.DGEMM_NT).
 
   python -m llm_mcp_amd.bench.dgemm_bench [--model llama-3-8b] [--write]
 
@@ -27,6 +29,7 @@ import torch
 from .. import ops
 
 BUCKETS = [16, 32, 48, 64, 80, 96, 112, 128, 160, 192, 224, 256]
+NT_TOP = 4      # configurations re-timed with the non-temporal weight stream (cfg | DGEMM_NT)
 
 
 def shapes(model: str, tp: int = 1) -> dict:
@@ -92,6 +95,29 @@ def run(model: str, tp: int, ms: list[int], margin: float, only: str = "") -> li
                 I = N // 2
                 ref = torch.nn.functional.silu(ref[:, :I]) * ref[:, I:]
             best = None
+            timed = []
+
+            def attempt(cfg, s, bm, bn):
+                if epi:
+                    if bn not in wil:
+                        wil[bn] = [interleave(w, bn // 2) for w in ws]
+                    wv = wil[bn]
+                else:
+                    wv = ws
+                out = ops.dgemm(x, wv[0], cfg, s, epi)
+                err = (out.float() - ref).abs().max().item()
+                tol = 2e-2 * ref.abs().max().item() + 1e-3
+                if not err <= tol:
+                    print(f"  !! {name} M={M} cfg={cfg} s={s}: max err {err:.4g} > {tol:.4g}",
+                          file=sys.stderr)
+                    rows.append({"shape": name, "M": M, "cfg": cfg, "splits": s, "error": err})
+                    return None
+                t = _time(lambda i: ops.dgemm(x, wv[i % ncopy], cfg, s, epi, out=out), iters)
+                rows.append({"shape": name, "M": M, "N": N, "K": K, "epi": epi, "cfg": cfg,
+                             "bm": bm, "bn": bn, "splits": s, "us": round(t, 2),
+                             "lib_us": round(t_lib, 2)})
+                return t
+
             for cfg, (bm, bn) in enumerate(cfgs):
                 if N % bn:
                     continue
@@ -102,27 +128,16 @@ def run(model: str, tp: int, ms: list[int], margin: float, only: str = "") -> li
                     nwg = tiles * s
                     if K % (64 * s) or nwg < 32 or nwg > 1536 or (s > 1 and K // s < 256):
                         continue
-                    if epi:
-                        if bn not in wil:
-                            wil[bn] = [interleave(w, bn // 2) for w in ws]
-                        wv = wil[bn]
-                    else:
-                        wv = ws
-                    out = ops.dgemm(x, wv[0], cfg, s, epi)
-                    err = (out.float() - ref).abs().max().item()
-                    tol = 2e-2 * ref.abs().max().item() + 1e-3
-                    if not err <= tol:
-                        print(f"  !! {name} M={M} cfg={cfg} s={s}: max err {err:.4g} > {tol:.4g}",
-                              file=sys.stderr)
-                        rows.append({"shape": name, "M": M, "cfg": cfg, "splits": s,
-                                     "error": err})
-                        continue
-                    t = _time(lambda i: ops.dgemm(x, wv[i % ncopy], cfg, s, epi, out=out), iters)
-                    rows.append({"shape": name, "M": M, "N": N, "K": K, "epi": epi, "cfg": cfg,
-                                 "bm": bm, "bn": bn, "splits": s, "us": round(t, 2),
-                                 "lib_us": round(t_lib, 2)})
-                    if best is None or t < best[0]:
-                        best = (t, cfg, s, bm, bn)
+                    t = attempt(cfg, s, bm, bn)
+                    if t is not None:
+                        timed.append((t, cfg, s, bm, bn))
+            # the fastest few again with the non-temporal weight stream
+            for t0, cfg, s, bm, bn in sorted(timed)[:NT_TOP]:
+                t = attempt(cfg | ops.DGEMM_NT, s, bm, bn)
+                if t is not None:
+                    timed.append((t, cfg | ops.DGEMM_NT, s, bm, bn))
+            if timed:
+                best = min(timed)
             line = f"{name:8s} M={M:4d} lib {t_lib:7.1f} us ({nbytes / t_lib / 1e6:5.2f} TB/s)"
             if best:
                 t, cfg, s, bm, bn = best
@@ -159,10 +174,24 @@ def deferred(name, N, K, M, x, ws, ncopy, iters, cfgs, margin, rows) -> dict:
         ops.rms_norm(torch.nn.functional.linear(x, ws[i % ncopy]), lnw, 1e-5, residual=res,
                      out=normed)
     t_lib = _time(lib, iters)
-    ch = ops.dgemm_choice(M, N, K)   # not loaded in the bench (LMX_DGEMM=0): library row
     r_ref = res0.clone()
     ref = ops.rms_norm(torch.nn.functional.linear(x, ws[0]), lnw, 1e-5, residual=r_ref)
-    best = None
+    timed = []
+
+    def attempt(cfg, s_, bm, bn):
+        r2 = res0.clone()
+        got = ops.rms_norm(ops.dgemm_partials(x, ws[0], cfg, s_), lnw, 1e-5, residual=r2)
+        err = (got.float() - ref.float()).abs().max().item()
+        if not err <= 5e-2 * ref.float().abs().max().item() + 1e-2:
+            print(f"  !! {name}+norm M={M} cfg={cfg} s={s_}: err {err:.4g}", file=sys.stderr)
+            return None
+        t = _time(lambda i: ops.rms_norm(ops.dgemm_partials(x, ws[i % ncopy], cfg, s_), lnw,
+                                         1e-5, residual=res, out=normed), iters)
+        rows.append({"shape": name + "+norm", "M": M, "N": N, "K": K, "epi": 2, "cfg": cfg,
+                     "bm": bm, "bn": bn, "splits": s_, "us": round(t, 2),
+                     "lib_us": round(t_lib, 2)})
+        return t
+
     for cfg, (bm, bn) in enumerate(cfgs):
         if N % bn or (bm > 2 * max(64, M) and bm > 64):
             continue
@@ -171,19 +200,14 @@ def deferred(name, N, K, M, x, ws, ncopy, iters, cfgs, margin, rows) -> dict:
             nwg = tiles * s_
             if K % (64 * s_) or nwg < 32 or nwg > 1536 or (s_ > 1 and K // s_ < 256):
                 continue
-            r2 = res0.clone()
-            got = ops.rms_norm(ops.dgemm_partials(x, ws[0], cfg, s_), lnw, 1e-5, residual=r2)
-            err = (got.float() - ref.float()).abs().max().item()
-            if not err <= 5e-2 * ref.float().abs().max().item() + 1e-2:
-                print(f"  !! {name}+norm M={M} cfg={cfg} s={s_}: err {err:.4g}", file=sys.stderr)
-                continue
-            t = _time(lambda i: ops.rms_norm(ops.dgemm_partials(x, ws[i % ncopy], cfg, s_), lnw,
-                                             1e-5, residual=res, out=normed), iters)
-            rows.append({"shape": name + "+norm", "M": M, "N": N, "K": K, "epi": 2, "cfg": cfg,
-                         "bm": bm, "bn": bn, "splits": s_, "us": round(t, 2),
-                         "lib_us": round(t_lib, 2)})
-            if best is None or t < best[0]:
-                best = (t, cfg, s_, bm, bn)
+            t = attempt(cfg, s_, bm, bn)
+            if t is not None:
+                timed.append((t, cfg, s_, bm, bn))
+    for t0, cfg, s_, bm, bn in sorted(timed)[:NT_TOP]:
+        t = attempt(cfg | ops.DGEMM_NT, s_, bm, bn)
+        if t is not None:
+            timed.append((t, cfg | ops.DGEMM_NT, s_, bm, bn))
+    best = min(timed) if timed else None
     line = f"{name + '+norm':12s} M={M:4d} lib+norm {t_lib:7.1f} us"
     e = {"N": N, "K": K, "epi": 2, "m_max": M, "cfg": -1, "splits": 0, "bn": 0, "us": None,
          "lib_us": round(t_lib, 2), "shape": name + "+norm"}

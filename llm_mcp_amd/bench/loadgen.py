@@ -34,9 +34,22 @@ def percentile(xs: list[float], q: float) -> float:
     return s[f] + (s[c] - s[f]) * (k - f)
 
 
+_ALPHABET = string.ascii_letters + string.digits + "     "
+
+
 def synthetic_prompt(n_chars: int, rng: random.Random) -> str:
-    alphabet = string.ascii_letters + string.digits + "     "
-    return "".join(rng.choice(alphabet) for _ in range(n_chars))
+    return "".join(rng.choices(_ALPHABET, k=n_chars))
+
+
+_PROMPTS: dict = {}     # seed -> prompts of that wave, generated ahead during the previous wave
+
+
+def wave_prompts(seed: int, concurrency: int, prompt_len: int) -> list[str]:
+    got = _PROMPTS.pop((seed, concurrency, prompt_len), None)
+    if got is not None:
+        return got
+    rng = random.Random(seed)
+    return [synthetic_prompt(prompt_len, rng) for _ in range(concurrency)]
 
 
 async def one_chat(session, url, model, prompt, max_tokens, temperature, top_p, ignore_eos=True):
@@ -71,8 +84,12 @@ async def one_chat(session, url, model, prompt, max_tokens, temperature, top_p, 
 
 
 async def wave(url, model, concurrency, prompt_len, max_tokens, temperature, top_p, seed):
-    rng = random.Random(seed)
-    prompts = [synthetic_prompt(prompt_len, rng) for _ in range(concurrency)]
+    prompts = wave_prompts(seed, concurrency, prompt_len)
+    # the next wave's prompts are generated while this one streams (the gap
+    # between two timed waves then holds no client-side prompt generation)
+    nxt = (seed + 1, concurrency, prompt_len)
+    asyncio.get_running_loop().call_later(
+        0.5, lambda: _PROMPTS.setdefault(nxt, wave_prompts(*nxt)))
     conn = aiohttp.TCPConnector(limit=0)
     timeout = aiohttp.ClientTimeout(total=3600)
     async with aiohttp.ClientSession(connector=conn, timeout=timeout) as s:

@@ -26,9 +26,15 @@
 //     one column tile on one XCD after the bijective remap (the M-tiles share
 //     the W panel in that L2, the last arriver reads its partners' slabs
 //     there);
+//   * NT (cfg id bit 5): the W stream is loaded non-temporal (LDS-DMA aux 2):
+//     a decode step reads each weight once, 15 GB apart, so keeping its lines
+//     in L2 / MALL only delays the next tile's misses (microarch guide,
+//     "nt-weights"); the activation operand keeps the default policy (every
+//     column tile re-reads it);
 //   * split-K partials go to fp32 slabs; arrival tickets (agent-scope
 //     release / acquire, guide "Projection GEMM at M = 256" item 2) elect the
-//     last slice, which sums the slabs and runs the epilogue.  Tickets are
+//     last slice, which adds the other slices' slabs into its accumulators
+//     and runs the epilogue.  Tickets are
 //     zero-initialised once and re-armed by the last arriver, so a captured
 //     decode graph needs no memset node per GEMM.
 #include "common.h"
@@ -36,18 +42,29 @@
 namespace lmx {
 namespace {
 
-constexpr int DBK = 64, DTHREADS = 512;
+constexpr int DTHREADS = 512;
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 
+template <int AUX = 0>
 __device__ __forceinline__ void dg_glds16(const void* gsrc, void* lds_base) {
-  __builtin_amdgcn_global_load_lds(gsrc, (lds_void_t*)lds_base, 16, 0, 0);
+  __builtin_amdgcn_global_load_lds(gsrc, (lds_void_t*)lds_base, 16, 0, AUX);
 }
 
-__device__ __forceinline__ int dg_swz(int r) { return (r >> 1) & 7; }
+// XOR swizzle of the 16-B chunk index in row r of a [row][BK] image, chosen
+// so that the 16-lane groups of a ds_read_b128 (lanes {0-3,12-15,20-27},
+// {4-11,16-19,28-31}, ... : 16 rows x chunk fg) hit 16 distinct 16-B slots
+// of the 256-B bank row.  BK 64 (128-B rows): chunk ^ (r/2 mod 8).  BK 32
+// (64-B rows, 4 rows per bank row): chunk ^ {0,2,3,1}[r/4 mod 4].
+template <int BK>
+__device__ __forceinline__ int dg_swz(int r) {
+  if constexpr (BK == 64) return (r >> 1) & 7;
+  else return (0x78 >> (2 * ((r >> 2) & 3))) & 3;
+}
 
+template <int BK>
 __device__ __forceinline__ bf16x8_t dg_frag(const bf16_t* tile, int r, int chunk) {
-  return *reinterpret_cast<const bf16x8_t*>(tile + r * DBK + 8 * (chunk ^ dg_swz(r)));
+  return *reinterpret_cast<const bf16x8_t*>(tile + r * BK + 8 * (chunk ^ dg_swz<BK>(r)));
 }
 
 template <int CNT>
@@ -55,27 +72,30 @@ __device__ __forceinline__ void dg_vmwait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(CNT) : "memory");
 }
 
-// One K-step (64 deep) of the A rows [m0, m0+BM) and W rows [n0, n0+BN).
-// 512 lanes x 16 B = 64 rows x 128 B per instruction; wave w fills rows
-// 8w..8w+7 of each 64-row slab (lane-linear LDS destination).
-template <int BM, int BN>
+// One K-step (BK deep) of the A rows [m0, m0+BM) and W rows [n0, n0+BN).
+// 512 lanes x 16 B per instruction = RPI rows x BK; wave w fills rows
+// (64/CPR)w .. of each RPI-row slab (lane-linear LDS destination, swizzle on
+// the global source chunk).
+template <int BM, int BN, int NT, int BK>
 __device__ __forceinline__ void dg_stage(bf16_t* lds_a, bf16_t* lds_w, const bf16_t* __restrict__ A,
                                          long lda, int m0, int M, const bf16_t* __restrict__ W,
                                          long ldw, int n0, int k0) {
+  constexpr int CPR = BK / 8, RPI = DTHREADS / CPR, RPW = 64 / CPR;
   const int t = threadIdx.x, wave = t >> 6;
-  const int rr = t >> 3, c = t & 7;
+  const int rr = t / CPR, c = t % CPR;
 #pragma unroll
-  for (int i = 0; i < BM / 64; ++i) {
-    const int r = i * 64 + rr;
+  for (int i = 0; i < BM / RPI; ++i) {
+    const int r = i * RPI + rr;
     int gr = m0 + r;
     gr = gr < M ? gr : M - 1;            // padded rows re-read row M-1; never stored
-    dg_glds16(A + (long)gr * lda + k0 + 8 * (c ^ dg_swz(r)), lds_a + (i * 64 + wave * 8) * DBK);
+    dg_glds16(A + (long)gr * lda + k0 + 8 * (c ^ dg_swz<BK>(r)),
+              lds_a + (i * RPI + wave * RPW) * BK);
   }
 #pragma unroll
-  for (int i = 0; i < BN / 64; ++i) {
-    const int r = i * 64 + rr;
-    dg_glds16(W + (long)(n0 + r) * ldw + k0 + 8 * (c ^ dg_swz(r)),
-              lds_w + (i * 64 + wave * 8) * DBK);
+  for (int i = 0; i < BN / RPI; ++i) {
+    const int r = i * RPI + rr;
+    dg_glds16<NT ? 2 : 0>(W + (long)(n0 + r) * ldw + k0 + 8 * (c ^ dg_swz<BK>(r)),
+                          lds_w + (i * RPI + wave * RPW) * BK);
   }
 }
 
@@ -83,7 +103,7 @@ __device__ __forceinline__ float dg_silu(float g) { return g / (1.f + __expf(-g)
 
 }  // namespace
 
-template <int BM, int BN, int WM, int NST, int EPI, int ROT>
+template <int BM, int BN, int WM, int NST, int EPI, int ROT, int NT, int BK>
 __global__ void __launch_bounds__(DTHREADS, 2) dgemm_kernel(
     bf16_t* __restrict__ C, const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
     float* __restrict__ slabs, unsigned* __restrict__ tickets, int M, int N, int K, long lda,
@@ -91,9 +111,11 @@ __global__ void __launch_bounds__(DTHREADS, 2) dgemm_kernel(
   constexpr int WN = 8 / WM;
   constexpr int WTM = BM / WM, WTN = BN / WN;       // wave tile
   constexpr int TM = WTM / 16, TN = WTN / 16;       // 16x16 MFMA tiles per wave
-  constexpr int LPS = (BM + BN) / 64;               // LDS-DMA instructions per thread per stage
-  constexpr int STAGE = (BM + BN) * DBK;            // bf16 elements per ring slot
+  constexpr int LPS = (BM + BN) * BK / (DTHREADS * 8);  // LDS-DMA instructions per thread per stage
+  constexpr int STAGE = (BM + BN) * BK;             // bf16 elements per ring slot
   static_assert(WM * WN == 8 && TM >= 1 && TN >= 1 && WTM % 16 == 0 && WTN % 16 == 0, "tile");
+  static_assert(BK == 32 || BK == 64, "BK");
+  static_assert(BM % (DTHREADS * 8 / BK) == 0 && BN % (DTHREADS * 8 / BK) == 0, "stage rows");
   static_assert(EPI != 1 || (WN % 2 == 0 || WN == 1), "swiglu wave split");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* const lds = reinterpret_cast<bf16_t*>(smem);
@@ -104,16 +126,16 @@ __global__ void __launch_bounds__(DTHREADS, 2) dgemm_kernel(
   const int ks = wg % splits, rest = wg / splits;
   const int tm = rest % tiles_m, tn = rest / tiles_m;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int kc = K / splits, kbeg = ks * kc, nk = kc / DBK;
+  const int kc = K / splits, kbeg = ks * kc, nk = kc / BK;
   // K-step order rotated per column tile: the workgroups of an XCD start at
   // different k-offsets, so their concurrent reads of the shared activation
   // rows (and of their W rows, all at the same 8-KB-strided offsets
-  // otherwise) spread over the L2 / HBM channels instead of camping on one
+  // otherwise) spread over the L2 / HBM channels instead of camping on one.
   // ROT 2 also staggers the M-tiles that share a W panel by 2 K-steps: the
   // leader's W reads miss to HBM, its followers re-read those lines from the
   // XCD's L2 two steps later (short latency) instead of merging into the same
   // in-flight misses -- per-CU throughput is bounded by the L1's outstanding
-  // misses x their latency (profiles/r2_pmc_dgemm.md)
+  // misses x their latency (profiles/r2_pmc_kernels.md)
   const int rot = ROT == 0 ? 0 : ((tn * 5 + (ROT == 2 ? 2 * tm : 0)) % nk);
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -130,8 +152,8 @@ __global__ void __launch_bounds__(DTHREADS, 2) dgemm_kernel(
   for (int p = 0; p < NST - 1; ++p)
     if (p < nk) {
       bf16_t* b = lds + p * STAGE;
-      dg_stage<BM, BN>(b, b + BM * DBK, A, lda, m0, M, W, ldw, n0,
-                       kbeg + ((p + rot) % nk) * DBK);
+      dg_stage<BM, BN, NT, BK>(b, b + BM * BK, A, lda, m0, M, W, ldw, n0,
+                               kbeg + ((p + rot) % nk) * BK);
     }
   for (int t = 0; t < nk; ++t) {
     if (t + NST - 2 < nk) dg_vmwait<(NST - 2) * LPS>(); else dg_vmwait<0>();
@@ -139,18 +161,18 @@ __global__ void __launch_bounds__(DTHREADS, 2) dgemm_kernel(
     __builtin_amdgcn_s_barrier();
     if (t + NST - 1 < nk) {       // refill the slot every wave finished reading at t-1
       bf16_t* b = lds + ((t + NST - 1) % NST) * STAGE;
-      dg_stage<BM, BN>(b, b + BM * DBK, A, lda, m0, M, W, ldw, n0,
-                       kbeg + ((t + NST - 1 + rot) % nk) * DBK);
+      dg_stage<BM, BN, NT, BK>(b, b + BM * BK, A, lda, m0, M, W, ldw, n0,
+                               kbeg + ((t + NST - 1 + rot) % nk) * BK);
     }
     const bf16_t* a_t = lds + (t % NST) * STAGE;
-    const bf16_t* w_t = a_t + BM * DBK;
+    const bf16_t* w_t = a_t + BM * BK;
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
+    for (int kk = 0; kk < BK / 32; ++kk) {
       bf16x8_t af[TM], bw[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = dg_frag(a_t, wr * WTM + i * 16 + fr, kk * 4 + fg);
+      for (int i = 0; i < TM; ++i) af[i] = dg_frag<BK>(a_t, wr * WTM + i * 16 + fr, kk * 4 + fg);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bw[j] = dg_frag(w_t, wc * WTN + j * 16 + fr, kk * 4 + fg);
+      for (int j = 0; j < TN; ++j) bw[j] = dg_frag<BK>(w_t, wc * WTN + j * 16 + fr, kk * 4 + fg);
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -164,161 +186,167 @@ __global__ void __launch_bounds__(DTHREADS, 2) dgemm_kernel(
   __syncthreads();
 
   // acc[i][j][r] = C[m][n]:  m = m0 + wr*WTM + 16i + fr,  n = n0 + wc*WTN + 16j + 4fg + r
-  if (splits == 1 && EPI != 2) {
-    if (EPI == 0) {
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int m = m0 + wr * WTM + 16 * i + fr;
-        if (m >= M) continue;
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int n = n0 + wc * WTN + 16 * j + 4 * fg;
-          bf16x4_t o;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) o[r] = (short)f2bf(acc[i][j][r]);
-          *reinterpret_cast<bf16x4_t*>(C + (long)m * ldc + n) = o;
-        }
-      }
-      return;
-    }
-    constexpr int HALF = BN / 2, ULD = HALF + 4;
-    if constexpr (WN == 1) {
-      // one wave column holds both halves: gate tiles j < TN/2, up tiles j + TN/2
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int m = m0 + wr * WTM + 16 * i + fr;
-        if (m >= M) continue;
-#pragma unroll
-        for (int j = 0; j < TN / 2; ++j) {
-          bf16x4_t o;
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            o[r] = (short)f2bf(dg_silu(acc[i][j][r]) * acc[i][j + TN / 2][r]);
-          *reinterpret_cast<bf16x4_t*>(C + (long)m * ldc + (n0 >> 1) + 16 * j + 4 * fg) = o;
-        }
-      }
-      return;
-    }
-    // fused SwiGLU: the up half of the tile (waves wc >= WN/2) hands its
-    // values to the gate half through the idle LDS ring
-    float* up = reinterpret_cast<float*>(smem);
-    const bool is_up = (wc * WTN) >= HALF;
-    if (is_up) {
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          *reinterpret_cast<f32x4_t*>(up + (wr * WTM + 16 * i + fr) * ULD +
-                                      (wc * WTN - HALF) + 16 * j + 4 * fg) = acc[i][j];
-    }
-    __syncthreads();
-    if (is_up) return;
+  if (splits > 1 || EPI == 2) {
+    // ---- split-K: publish this slice's fp32 partial tile ------------------
+    float* slab = slabs + (long)ks * M * N;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
-      const int ml = wr * WTM + 16 * i + fr, m = m0 + ml;
+      const int m = m0 + wr * WTM + 16 * i + fr;
       if (m >= M) continue;
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        const int nl = wc * WTN + 16 * j + 4 * fg;
-        const f32x4_t u = *reinterpret_cast<const f32x4_t*>(up + ml * ULD + nl);
+        const int n = n0 + wc * WTN + 16 * j + 4 * fg;
+        *reinterpret_cast<f32x4_t*>(slab + (long)m * N + n) = acc[i][j];
+      }
+    }
+    if (EPI == 2) return;   // partials only: the consumer kernel sums the S slabs
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(smem);       // the one LDS array (no 2nd __shared__)
+    const int tile = tn * tiles_m + tm;
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned old = __hip_atomic_fetch_add(&tickets[tile], 1u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+      *flag = (old == (unsigned)(splits - 1));
+    }
+    __syncthreads();
+    if (!*flag) return;
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      tickets[tile] = 0u;     // re-armed: every slice of this call has arrived
+    }
+    __syncthreads();
+    // last arriver: add the OTHER slices' partials into its own accumulators
+    // (its own slab is never read back), in the canonical order
+    // ((p0 + p1) + ...) + p(S-1) whichever slice arrives last, so a call's
+    // result is bitwise reproducible
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + wr * WTM + 16 * i + fr;
+      const long row = (long)(m < M ? m : M - 1) * N;   // load unconditionally (guide §5 item 4c)
+      if (ks > 0) {
+        f32x4_t pre[TN];
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          pre[j] = *reinterpret_cast<const f32x4_t*>(slabs + row + n0 + wc * WTN + 16 * j + 4 * fg);
+        for (int s2 = 1; s2 < ks; ++s2) {
+          const float* o = slabs + (long)s2 * M * N + row;
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            pre[j] += *reinterpret_cast<const f32x4_t*>(o + n0 + wc * WTN + 16 * j + 4 * fg);
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = pre[j] + acc[i][j];
+      }
+      for (int s2 = ks + 1; s2 < splits; ++s2) {
+        const float* o = slabs + (long)s2 * M * N + row;
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] += *reinterpret_cast<const f32x4_t*>(o + n0 + wc * WTN + 16 * j + 4 * fg);
+      }
+    }
+    __syncthreads();            // the SwiGLU hand-off below reuses the LDS word of the flag
+  }
+
+  if (EPI == 0) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + wr * WTM + 16 * i + fr;
+      if (m >= M) continue;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wc * WTN + 16 * j + 4 * fg;
         bf16x4_t o;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = (short)f2bf(dg_silu(acc[i][j][r]) * u[r]);
-        *reinterpret_cast<bf16x4_t*>(C + (long)m * ldc + (n0 >> 1) + nl) = o;
+        for (int r = 0; r < 4; ++r) o[r] = (short)f2bf(acc[i][j][r]);
+        *reinterpret_cast<bf16x4_t*>(C + (long)m * ldc + n) = o;
       }
     }
     return;
   }
-
-  // ---- split-K: publish this slice's fp32 partial tile --------------------
-  float* slab = slabs + (long)ks * M * N;
+  constexpr int HALF = BN / 2, ULD = HALF + 4;
+  if constexpr (WN == 1) {
+    // one wave column holds both halves: gate tiles j < TN/2, up tiles j + TN/2
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + wr * WTM + 16 * i + fr;
+      if (m >= M) continue;
+#pragma unroll
+      for (int j = 0; j < TN / 2; ++j) {
+        bf16x4_t o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          o[r] = (short)f2bf(dg_silu(acc[i][j][r]) * acc[i][j + TN / 2][r]);
+        *reinterpret_cast<bf16x4_t*>(C + (long)m * ldc + (n0 >> 1) + 16 * j + 4 * fg) = o;
+      }
+    }
+    return;
+  }
+  // fused SwiGLU: the up half of the tile (waves wc >= WN/2) hands its
+  // values to the gate half through the idle LDS ring
+  float* up = reinterpret_cast<float*>(smem);
+  const bool is_up = (wc * WTN) >= HALF;
+  if (is_up) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        *reinterpret_cast<f32x4_t*>(up + (wr * WTM + 16 * i + fr) * ULD +
+                                    (wc * WTN - HALF) + 16 * j + 4 * fg) = acc[i][j];
+  }
+  __syncthreads();
+  if (is_up) return;
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
-    const int m = m0 + wr * WTM + 16 * i + fr;
+    const int ml = wr * WTM + 16 * i + fr, m = m0 + ml;
     if (m >= M) continue;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      const int n = n0 + wc * WTN + 16 * j + 4 * fg;
-      *reinterpret_cast<f32x4_t*>(slab + (long)m * N + n) = acc[i][j];
-    }
-  }
-  if (EPI == 2) return;   // partials only: the consumer kernel sums the S slabs
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  int* flag = reinterpret_cast<int*>(smem);       // the one LDS array (no 2nd __shared__)
-  const int tile = tn * tiles_m + tm;
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned old = __hip_atomic_fetch_add(&tickets[tile], 1u, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT);
-    *flag = (old == (unsigned)(splits - 1));
-  }
-  __syncthreads();
-  if (!*flag) return;
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    tickets[tile] = 0u;     // re-armed: every slice of this call has arrived
-  }
-  __syncthreads();
-  // last arriver: reduce the S slabs of the tile (16 B per lane) + epilogue
-  const int rows = min(BM, M - m0);
-  if (EPI == 0) {
-    constexpr int C4 = BN / 4;
-    for (int e = threadIdx.x; e < rows * C4; e += DTHREADS) {
-      const int m = m0 + e / C4, n = n0 + (e % C4) * 4;
-      f32x4_t s = {0.f, 0.f, 0.f, 0.f};
-      for (int s2 = 0; s2 < splits; ++s2)
-        s += *reinterpret_cast<const f32x4_t*>(slabs + ((long)s2 * M + m) * N + n);
+      const int nl = wc * WTN + 16 * j + 4 * fg;
+      const f32x4_t u = *reinterpret_cast<const f32x4_t*>(up + ml * ULD + nl);
       bf16x4_t o;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) o[r] = (short)f2bf(s[r]);
-      *reinterpret_cast<bf16x4_t*>(C + (long)m * ldc + n) = o;
-    }
-  } else {
-    constexpr int H4 = BN / 8;          // float4 groups per half tile
-    for (int e = threadIdx.x; e < rows * H4; e += DTHREADS) {
-      const int m = m0 + e / H4, c = (e % H4) * 4;
-      f32x4_t g = {0.f, 0.f, 0.f, 0.f}, u = {0.f, 0.f, 0.f, 0.f};
-      for (int s2 = 0; s2 < splits; ++s2) {
-        const float* row = slabs + ((long)s2 * M + m) * N + n0;
-        g += *reinterpret_cast<const f32x4_t*>(row + c);
-        u += *reinterpret_cast<const f32x4_t*>(row + BN / 2 + c);
-      }
-      bf16x4_t o;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) o[r] = (short)f2bf(dg_silu(g[r]) * u[r]);
-      *reinterpret_cast<bf16x4_t*>(C + (long)m * ldc + (n0 >> 1) + c) = o;
+      for (int r = 0; r < 4; ++r) o[r] = (short)f2bf(dg_silu(acc[i][j][r]) * u[r]);
+      *reinterpret_cast<bf16x4_t*>(C + (long)m * ldc + (n0 >> 1) + nl) = o;
     }
   }
 }
 
 // ---- launcher ---------------------------------------------------------------
-// cfg ids (BM, BN, WM, NST); kept in sync with ops.DGEMM_CONFIGS
-struct DgCfg { int bm, bn, wm, nst; };
+// cfg ids (BM, BN, WM, NST, ROT, BK); kept in sync with ops.DGEMM_CONFIGS
+struct DgCfg { int bm, bn, wm, nst, rot, bk; };
 static const DgCfg kDgCfgs[] = {
-    {256, 128, 4, 3},   // 0
-    {128, 128, 2, 4},   // 1
-    {64, 128, 2, 5},    // 2
-    {256, 64, 8, 3},    // 3
-    {128, 64, 4, 4},    // 4
-    {64, 64, 2, 6},     // 5
-    {128, 256, 2, 3},   // 6
+    {256, 128, 4, 3, 0, 64},   // 0
+    {128, 128, 2, 4, 0, 64},   // 1
+    {64, 128, 2, 5, 0, 64},    // 2
+    {256, 64, 8, 3, 0, 64},    // 3
+    {128, 64, 4, 4, 0, 64},    // 4
+    {64, 64, 2, 6, 0, 64},     // 5
+    {128, 256, 2, 3, 0, 64},   // 6
     // the same tiles with the per-column-tile K rotation
-    {64, 64, 2, 6},     // 7
-    {128, 64, 4, 4},    // 8
-    {64, 128, 2, 5},    // 9
-    {128, 128, 2, 4},   // 10
-    {128, 256, 2, 3},   // 11
-    {256, 128, 4, 3},   // 12
-    {256, 256, 4, 2},   // 13
+    {64, 64, 2, 6, 1, 64},     // 7
+    {128, 64, 4, 4, 1, 64},    // 8
+    {64, 128, 2, 5, 1, 64},    // 9
+    {128, 128, 2, 4, 1, 64},   // 10
+    {128, 256, 2, 3, 1, 64},   // 11
+    {256, 128, 4, 3, 1, 64},   // 12
+    {256, 256, 4, 2, 1, 64},   // 13
     // M-tile stagger (ROT 2)
-    {64, 64, 2, 6},     // 14
-    {128, 64, 4, 4},    // 15
-    {64, 128, 2, 5},    // 16
-    {128, 128, 2, 4},   // 17
-    {128, 256, 2, 3},   // 18
+    {64, 64, 2, 6, 2, 64},     // 14
+    {128, 64, 4, 4, 2, 64},    // 15
+    {64, 128, 2, 5, 2, 64},    // 16
+    {128, 128, 2, 4, 2, 64},   // 17
+    {128, 256, 2, 3, 2, 64},   // 18
+    // 32-deep K-steps: half-size ring slots, so the 256-row tiles keep 2-3
+    // K-steps in flight across the barrier (cfg 13's 64-deep slots fit only
+    // a 2-slot ring in 160 KB and drain every step)
+    {256, 256, 4, 4, 1, 32},   // 19
+    {256, 256, 4, 5, 1, 32},   // 20
+    {256, 128, 4, 6, 1, 32},   // 21
+    {128, 256, 2, 6, 1, 32},   // 22
 };
 constexpr int kNumDgCfgs = sizeof(kDgCfgs) / sizeof(kDgCfgs[0]);
 
@@ -331,24 +359,24 @@ int dgemm_config(int cfg, int* bm, int* bn) {
   return 0;
 }
 
-template <int BM, int BN, int WM, int NST, int EPI, int ROT>
+template <int BM, int BN, int WM, int NST, int EPI, int ROT, int NT, int BK>
 static int dg_launch(bf16_t* C, const bf16_t* A, const bf16_t* W, float* slabs,
                      unsigned* tickets, int M, int N, int K, long lda, long ldw, long ldc,
                      int splits, hipStream_t stream) {
-  constexpr size_t ring = (size_t)NST * (BM + BN) * DBK * sizeof(bf16_t);
+  constexpr size_t ring = (size_t)NST * (BM + BN) * BK * sizeof(bf16_t);
   constexpr size_t xchg = EPI == 1 ? (size_t)BM * (BN / 2 + 4) * 4 : 0;   // SwiGLU hand-off
   constexpr size_t smem = ring > xchg ? ring : xchg;
   static_assert(smem <= 160 * 1024, "LDS");
   static bool attr = false;
   if (!attr) {
-    const hipError_t e = hipFuncSetAttribute((const void*)dgemm_kernel<BM, BN, WM, NST, EPI, ROT>,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             (int)smem);
+    const hipError_t e = hipFuncSetAttribute(
+        (const void*)dgemm_kernel<BM, BN, WM, NST, EPI, ROT, NT, BK>,
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return (int)e;
     attr = true;
   }
   const int nwg = ((M + BM - 1) / BM) * (N / BN) * splits;
-  dgemm_kernel<BM, BN, WM, NST, EPI, ROT><<<dim3(nwg), dim3(DTHREADS), smem, stream>>>(
+  dgemm_kernel<BM, BN, WM, NST, EPI, ROT, NT, BK><<<dim3(nwg), dim3(DTHREADS), smem, stream>>>(
       C, A, W, slabs, tickets, M, N, K, lda, ldw, ldc, splits);
   return (int)hipGetLastError();
 }
@@ -357,9 +385,11 @@ int dgemm(void* C, const void* A, const void* W, float* slabs, unsigned* tickets
           int M, int N, int K, long lda, long ldw, long ldc, int cfg, int splits, int epi,
           hipStream_t stream) {
   if (M <= 0) return 0;
+  const int nt = (cfg >> 5) & 1;      // bit 5: non-temporal weight stream
+  cfg &= 31;
   if (cfg < 0 || cfg >= kNumDgCfgs || splits < 1 || epi < 0 || epi > 2) return -1;
   const DgCfg c = kDgCfgs[cfg];
-  if (N % c.bn != 0 || K % (splits * DBK) != 0) return -1;
+  if (N % c.bn != 0 || K % (splits * c.bk) != 0) return -1;
   if (epi == 2 && slabs == nullptr) return -2;
   if (splits > 1 && epi != 2) {
     if (slabs == nullptr || tickets == nullptr) return -2;
@@ -368,38 +398,46 @@ int dgemm(void* C, const void* A, const void* W, float* slabs, unsigned* tickets
   auto C_ = (bf16_t*)C;
   auto A_ = (const bf16_t*)A;
   auto W_ = (const bf16_t*)W;
-#define LMX_DG(ID, BM, BN, WM, NST, ROT)                                                     \
-  case ID:                                                                                   \
-    if (epi == 1)                                                                            \
-      return dg_launch<BM, BN, WM, NST, 1, ROT>(C_, A_, W_, slabs, tickets, M, N, K, lda, ldw, \
-                                                ldc, splits, stream);                        \
-    if (epi == 2)                                                                            \
-      return dg_launch<BM, BN, WM, NST, 2, ROT>(C_, A_, W_, slabs, tickets, M, N, K, lda, ldw, \
-                                                ldc, splits, stream);                        \
-    return dg_launch<BM, BN, WM, NST, 0, ROT>(C_, A_, W_, slabs, tickets, M, N, K, lda, ldw,   \
-                                              ldc, splits, stream);
+#define LMX_DG_E(BM, BN, WM, NST, ROT, NT, BK)                                                 \
+  if (epi == 1)                                                                               \
+    return dg_launch<BM, BN, WM, NST, 1, ROT, NT, BK>(C_, A_, W_, slabs, tickets, M, N, K, lda, \
+                                                      ldw, ldc, splits, stream);              \
+  if (epi == 2)                                                                               \
+    return dg_launch<BM, BN, WM, NST, 2, ROT, NT, BK>(C_, A_, W_, slabs, tickets, M, N, K, lda, \
+                                                      ldw, ldc, splits, stream);              \
+  return dg_launch<BM, BN, WM, NST, 0, ROT, NT, BK>(C_, A_, W_, slabs, tickets, M, N, K, lda,   \
+                                                    ldw, ldc, splits, stream);
+#define LMX_DG(ID, BM, BN, WM, NST, ROT, BK)                                                  \
+  case ID:                                                                                    \
+    if (nt) { LMX_DG_E(BM, BN, WM, NST, ROT, 1, BK) }                                         \
+    LMX_DG_E(BM, BN, WM, NST, ROT, 0, BK)
   switch (cfg) {
-    LMX_DG(0, 256, 128, 4, 3, 0)
-    LMX_DG(1, 128, 128, 2, 4, 0)
-    LMX_DG(2, 64, 128, 2, 5, 0)
-    LMX_DG(3, 256, 64, 8, 3, 0)
-    LMX_DG(4, 128, 64, 4, 4, 0)
-    LMX_DG(5, 64, 64, 2, 6, 0)
-    LMX_DG(6, 128, 256, 2, 3, 0)
-    LMX_DG(7, 64, 64, 2, 6, 1)
-    LMX_DG(8, 128, 64, 4, 4, 1)
-    LMX_DG(9, 64, 128, 2, 5, 1)
-    LMX_DG(10, 128, 128, 2, 4, 1)
-    LMX_DG(11, 128, 256, 2, 3, 1)
-    LMX_DG(12, 256, 128, 4, 3, 1)
-    LMX_DG(13, 256, 256, 4, 2, 1)
-    LMX_DG(14, 64, 64, 2, 6, 2)
-    LMX_DG(15, 128, 64, 4, 4, 2)
-    LMX_DG(16, 64, 128, 2, 5, 2)
-    LMX_DG(17, 128, 128, 2, 4, 2)
-    LMX_DG(18, 128, 256, 2, 3, 2)
+    LMX_DG(0, 256, 128, 4, 3, 0, 64)
+    LMX_DG(1, 128, 128, 2, 4, 0, 64)
+    LMX_DG(2, 64, 128, 2, 5, 0, 64)
+    LMX_DG(3, 256, 64, 8, 3, 0, 64)
+    LMX_DG(4, 128, 64, 4, 4, 0, 64)
+    LMX_DG(5, 64, 64, 2, 6, 0, 64)
+    LMX_DG(6, 128, 256, 2, 3, 0, 64)
+    LMX_DG(7, 64, 64, 2, 6, 1, 64)
+    LMX_DG(8, 128, 64, 4, 4, 1, 64)
+    LMX_DG(9, 64, 128, 2, 5, 1, 64)
+    LMX_DG(10, 128, 128, 2, 4, 1, 64)
+    LMX_DG(11, 128, 256, 2, 3, 1, 64)
+    LMX_DG(12, 256, 128, 4, 3, 1, 64)
+    LMX_DG(13, 256, 256, 4, 2, 1, 64)
+    LMX_DG(14, 64, 64, 2, 6, 2, 64)
+    LMX_DG(15, 128, 64, 4, 4, 2, 64)
+    LMX_DG(16, 64, 128, 2, 5, 2, 64)
+    LMX_DG(17, 128, 128, 2, 4, 2, 64)
+    LMX_DG(18, 128, 256, 2, 3, 2, 64)
+    LMX_DG(19, 256, 256, 4, 4, 1, 32)
+    LMX_DG(20, 256, 256, 4, 5, 1, 32)
+    LMX_DG(21, 256, 128, 4, 6, 1, 32)
+    LMX_DG(22, 128, 256, 2, 6, 1, 32)
   }
 #undef LMX_DG
+#undef LMX_DG_E
   return -1;
 }
 

@@ -47,7 +47,7 @@ class NomicBertModel:
         # 64 channels (gemm_nt act=3)
         I2, d = self.w["layers"][0]["w_gate_up"].shape
         self.gu_cfg = ops.encoder_choice(I2, d) if self.device.type == "cuda" else None
-        self.gu_block = ops.DGEMM_CONFIGS[self.gu_cfg][1] // 2 if self.gu_cfg is not None else 64
+        self.gu_block = ops.DGEMM_CONFIGS[self.gu_cfg & ops.DGEMM_CFG_MASK][1] // 2 if self.gu_cfg is not None else 64
         for L in self.w["layers"]:
             L.pop("w_gu_il", None)      # always this model's own layout (never a copy's)
             if ops.gemm_nt_supported(*L["w_gate_up"].shape) and I2 // 2 % self.gu_block == 0:

@@ -578,7 +578,7 @@ def linear_swiglu(x: torch.Tensor, w: torch.Tensor, block: int) -> torch.Tensor:
     it (its BN must be 2 * block), else the library GEMM + the GLU kernel."""
     if x.is_cuda and x.dim() == 2:
         ch = dgemm_choice(x.shape[0], w.shape[0], w.shape[1], epi=1)
-        if ch is not None and DGEMM_CONFIGS[ch[0]][1] == 2 * block:
+        if ch is not None and DGEMM_CONFIGS[ch[0] & DGEMM_CFG_MASK][1] == 2 * block:
             return dgemm(x, w, ch[0], ch[1], epi=1)
     return silu_mul(linear(x, w), block=block)
 
@@ -586,7 +586,8 @@ def linear_swiglu(x: torch.Tensor, w: torch.Tensor, block: int) -> torch.Tensor:
 def swiglu_block(N: int, K: int) -> int:
     """Interleave block of the gate|up weights for the fused decode GEMM of
     this shape (BN/2 of the measured configurations), 0 = not fused."""
-    bns = {DGEMM_CONFIGS[cfg][1] for m, cfg, s in _dg_table().get((N, K, 1), ()) if cfg >= 0}
+    bns = {DGEMM_CONFIGS[cfg & DGEMM_CFG_MASK][1]
+           for m, cfg, s in _dg_table().get((N, K, 1), ()) if cfg >= 0}
     return min(bns) // 2 if bns else 0
 
 
@@ -596,8 +597,12 @@ def swiglu_block(N: int, K: int) -> int:
 # (BM, BN) of each kernel configuration id, in the order of kDgCfgs
 DGEMM_CONFIGS = [(256, 128), (128, 128), (64, 128), (256, 64), (128, 64), (64, 64), (128, 256),
                  (64, 64), (128, 64), (64, 128), (128, 128), (128, 256), (256, 128), (256, 256),
-                 (64, 64), (128, 64), (64, 128), (128, 128), (128, 256)]
+                 (64, 64), (128, 64), (64, 128), (128, 128), (128, 256),
+                 (256, 256), (256, 256), (256, 128), (128, 256)]     # 19-22: 32-deep K-steps
 DGEMM_MAX_M = 256
+# a configuration id with bit 5 set (cfg | DGEMM_NT) streams the weights
+# non-temporal (dgemm.hip NT): the low bits select the tile
+DGEMM_NT, DGEMM_CFG_MASK = 32, 31
 _DG_WS: dict = {}          # (device, stream) -> (slabs fp32, tickets uint32)
 _DG_TICKETS = 8192
 DGEMM_TABLE: dict | None = None
@@ -682,7 +687,7 @@ def dgemm(a: torch.Tensor, w: torch.Tensor, cfg: int, splits: int, epi: int = 0,
     with ``block=BN/2``) and the result is silu(gate) * up (N/2 columns)."""
     M, K = a.shape
     N = w.shape[0]
-    bm, bn = DGEMM_CONFIGS[cfg]
+    bm, bn = DGEMM_CONFIGS[cfg & DGEMM_CFG_MASK]
     ncols = N // 2 if epi else N
     if not a.is_cuda:
         y = a.float() @ w.float().t()
@@ -719,7 +724,7 @@ def dgemm_partials(a: torch.Tensor, w: torch.Tensor, cfg: int, splits: int) -> P
     (the consumer -- ``rms_norm`` -- sums them)."""
     M, K = a.shape
     N = w.shape[0]
-    bm, bn = DGEMM_CONFIGS[cfg]
+    bm, bn = DGEMM_CONFIGS[cfg & DGEMM_CFG_MASK]
     _bf16(a, "a"); _bf16(w, "w")
     _chk(0 < M <= DGEMM_MAX_M and N % bn == 0 and K % (64 * splits) == 0,
          f"dgemm_partials shape M={M} N={N} K={K} cfg={cfg} splits={splits}")

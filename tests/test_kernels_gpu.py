@@ -390,12 +390,13 @@ def test_apply_penalties_vs_reference():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg", list(range(19)))
+@pytest.mark.parametrize("cfg", list(range(23)) + [c | 32 for c in (1, 4, 6, 13, 19)])
 @pytest.mark.parametrize("M", [1, 37, 64, 130, 256])
 def test_dgemm_configs_vs_fp32(cfg, M):
-    """K11 decode GEMM: every tile configuration, split-K 1/2/4, both
+    """K11 decode GEMM: every tile configuration (and some with the
+    non-temporal weight stream, cfg | DGEMM_NT), split-K 1/2/4, both
     epilogues, against an fp32 PyTorch reference (rows past M masked)."""
-    bm, bn = ops.DGEMM_CONFIGS[cfg]
+    bm, bn = ops.DGEMM_CONFIGS[cfg & ops.DGEMM_CFG_MASK]
     K, N = 1024, 2 * 1024
     a = torch.randn(M, K, device=DEV).to(torch.bfloat16)
     w = (torch.randn(N, K, device=DEV) * K ** -0.5).to(torch.bfloat16)
@@ -436,7 +437,7 @@ def test_dgemm_in_graph_strided_input_long_k():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg,splits", [(0, 8), (5, 1), (1, 4), (13, 16)])
+@pytest.mark.parametrize("cfg,splits", [(0, 8), (5, 1), (1, 4), (13, 16), (1 | 32, 4), (19, 16), (21, 8)])
 def test_dgemm_partials_into_rmsnorm(cfg, splits):
     """K11 partials-only epilogue summed by the residual-add RMSNorm equals the
     fp32 reference of norm(residual + x @ w^T)."""

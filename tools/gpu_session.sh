@@ -25,7 +25,7 @@ for step in "$@"; do
     rehearse2)
       run rehearse2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
           --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus 2 --steps 2 --warmup 1 \
-          --concurrency 64 --rehearse-on-one-gpu || exit $? ;;
+          --concurrency 64 --rehearse-on-one-gpu --api-procs 2 || exit $? ;;
     dgemm_tests)
       run dgemm_tests 600 python -u -m pytest tests/test_kernels_gpu.py -k dgemm -x -q --timeout 120 \
           --timeout-method thread -p no:cacheprovider || exit $? ;;
@@ -81,6 +81,15 @@ for step in "$@"; do
           --jobs 1024 --concurrency 256 --sync-every 4 --max-tokens 64 --chars 512 || exit $? ;;
     encoder_bench)
       run encoder_bench 600 python -u -m llm_mcp_amd.bench.dgemm_bench --encoder 4096,32768 || exit $? ;;
+    prof_bench)
+      # the headline bench under a kernel trace; tools/prof_timeline.py splits it into waves/steps
+      rm -rf gpurun_out/prof_bench
+      run prof_bench 900 rocprofv3 --kernel-trace -d gpurun_out/prof_bench -o run \
+          -- python3 bench.py --steps 2 --warmup 1 || exit $?
+      python tools/prof_timeline.py gpurun_out/prof_bench/run_results.db --waves 2 \
+          > gpurun_out/prof_bench_timeline.md 2>&1 || true ;;
+    rope_probe)
+      run rope_probe 120 python -u tools/rope_probe.py || exit $? ;;
     smoke)
       run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     *)

@@ -1,0 +1,59 @@
+"""Decode rope/cache kernel cost split (1 GPU): the per-token kernel at the
+decode-graph shape (256 tokens, Llama-3-8B heads), timed whole, without the
+transposed-V scatter, and without any cache write.
+
+    python tools/rope_probe.py [--tokens 256] [--bs 32]
+"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from llm_mcp_amd import ops  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tokens", type=int, default=256)
+    ap.add_argument("--bs", type=int, default=32)
+    ap.add_argument("--iters", type=int, default=400)
+    a = ap.parse_args()
+    T, Hq, Hkv, D, BS = a.tokens, 32, 8, 128, a.bs
+    dev = torch.device("cuda", 0)
+    nb = T * 24
+    qkv = torch.randn(T, (Hq + 2 * Hkv) * D, device=dev).to(torch.bfloat16)
+    pos = torch.randint(0, 4000, (T,), device=dev, dtype=torch.int32)
+    cs = torch.randn(4096, D, device=dev)
+    pages = torch.randperm(nb, device=dev)[:T].to(torch.int32)
+    slots = pages * BS + torch.randint(0, BS, (T,), device=dev, dtype=torch.int32)
+    kc = torch.zeros(nb, Hkv, BS, D, device=dev, dtype=torch.bfloat16)
+    vc = torch.zeros(nb, Hkv, D, BS, device=dev, dtype=torch.bfloat16)
+    nat = ops.native()
+    st = torch.cuda.current_stream().cuda_stream
+
+    def call(slot_p, k_p, v_p):
+        nat.rope_cache(qkv.data_ptr(), qkv.stride(0), pos.data_ptr(), cs.data_ptr(), T, Hq, Hkv, D,
+                       slot_p, k_p, v_p, BS, 0, T, 0, 0, 1e-6, st)
+
+    variants = {
+        "full": (slots.data_ptr(), kc.data_ptr(), vc.data_ptr()),
+        "no V scatter": (slots.data_ptr(), kc.data_ptr(), 0),
+        "no cache write": (0, 0, 0),
+    }
+    for name, args in variants.items():
+        for _ in range(10):
+            call(*args)
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(a.iters):
+            call(*args)
+        e.record()
+        torch.cuda.synchronize()
+        print(f"rope_cache T={T} {name:15s} {s.elapsed_time(e) / a.iters * 1e3:7.2f} us", flush=True)
+
+
+if __name__ == "__main__":
+    main()
