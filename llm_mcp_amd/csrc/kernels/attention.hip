@@ -108,6 +108,72 @@ __device__ __forceinline__ void process_page(PageState<HD>& st, const bf16x8_t (
   }
 }
 
+// Split form of process_page for the pipelined decode loop: the page's K and
+// V^T fragments are loaded into registers one page ahead of their use.
+template <int HD>
+struct PageFrags {
+  bf16x8_t ka[HD / 32], kb[HD / 32], vf[HD / 16];
+};
+
+template <int HD>
+__device__ __forceinline__ void load_page(PageFrags<HD>& f, const bf16_t* __restrict__ kpage,
+                                          const bf16_t* __restrict__ vpage) {
+  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int s = 0; s < HD / 32; ++s) {
+    f.ka[s] = load_frag16B(kpage + c * HD + 32 * s + 8 * g);
+    f.kb[s] = load_frag16B(kpage + (16 + c) * HD + 32 * s + 8 * g);
+  }
+#pragma unroll
+  for (int i = 0; i < HD / 16; ++i) {
+    const bf16_t* vr = vpage + (16 * i + c) * BS;
+    f.vf[i] = load_frag_2x8B(vr + 4 * g, vr + 16 + 4 * g);
+  }
+}
+
+template <int HD>
+__device__ __forceinline__ void compute_page(PageState<HD>& st, const bf16x8_t (&qf)[HD / 32],
+                                             const PageFrags<HD>& f, int page_pos0, int lim,
+                                             float scale_log2) {
+  const int lane = threadIdx.x & 63, g = lane >> 4;
+  f32x4_t s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < HD / 32; ++s) {
+    s0 = mfma16(f.ka[s], qf[s], s0);
+    s1 = mfma16(f.kb[s], qf[s], s1);
+  }
+  float x[8];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int k0 = page_pos0 + 4 * g + r, k1 = k0 + 16;
+    x[r] = (k0 <= lim) ? s0[r] * scale_log2 : -INFINITY;
+    x[4 + r] = (k1 <= lim) ? s1[r] * scale_log2 : -INFINITY;
+  }
+  float mx = x[0];
+#pragma unroll
+  for (int j = 1; j < 8; ++j) mx = fmaxf(mx, x[j]);
+  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  const float m_new = fmaxf(st.m, mx);
+  const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
+  const float alpha = exp2f(st.m - m_use);
+  float p[8], rs = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { p[j] = exp2f(x[j] - m_use); rs += p[j]; }
+  rs += __shfl_xor(rs, 16, 64);
+  rs += __shfl_xor(rs, 32, 64);
+  st.l = st.l * alpha + rs;
+  st.m = m_new;
+  bf16x8_t pf;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) pf[j] = (short)f2bf(p[j]);
+#pragma unroll
+  for (int i = 0; i < HD / 16; ++i) {
+    st.acc[i] *= alpha;
+    st.acc[i] = mfma16(f.vf[i], pf, st.acc[i]);
+  }
+}
+
 // ---------------------------------------------------------------- decode ----
 // Partition length used for a sequence: the requested split-K granule, grown
 // (in 128-token steps) when the context would need more than max_parts
@@ -119,16 +185,23 @@ __device__ __forceinline__ int effective_part(int ctx, int part_tokens, int max_
 }
 
 // grid (max_parts, Hkv, B), block 256.
-template <int HD>
+// MODE 0: one page at a time (load, then compute); MODE 1: the next page's
+// block id and K/V fragments are loaded before the current page is computed
+// (two pages in flight per wave); MODE 2: loads only (diagnostic ceiling).
+template <int HD, int MODE>
 __global__ void __launch_bounds__(256) paged_decode_kernel(
     const bf16_t* __restrict__ q, long q_stride, const bf16_t* __restrict__ k_cache,
     const bf16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
-    const int* __restrict__ context_lens, bf16_t* __restrict__ out, long out_stride,
+    const int* __restrict__ context_lens, const int* __restrict__ order,
+    bf16_t* __restrict__ out, long out_stride,
     float* __restrict__ part_o, float* __restrict__ part_ml, int Hq, int Hkv, float scale,
     int part_tokens, int max_parts) {
   __shared__ float sm_ml[4][16][2];
   __shared__ float sm_o[4][16][HD + 4];
-  const int p = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
+  // order (optional): sequence of each grid z-slice, longest context first,
+  // so the workgroups dispatched last are the short ones (the batch's last
+  // round of workgroups ends together; profiles/r2_decode_attention.md)
+  const int p = blockIdx.x, kvh = blockIdx.y, b = order ? order[blockIdx.z] : blockIdx.z;
   const int ctx = context_lens[b];
   part_tokens = effective_part(ctx, part_tokens, max_parts);
   const int nparts = (ctx + part_tokens - 1) / part_tokens;
@@ -148,11 +221,39 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
   const float scale_log2 = scale * LOG2E;
   const int pg0 = t0 / BS, pg1 = (t1 + BS - 1) / BS;
   const int* bt = block_tables + (long)b * bt_stride;
-  for (int pg = pg0 + wave; pg < pg1; pg += 4) {
-    const long blk = bt[pg];
-    const bf16_t* kp = k_cache + (blk * Hkv + kvh) * (BS * HD);
-    const bf16_t* vp = v_cache + (blk * Hkv + kvh) * (BS * HD);
-    process_page(st, qf, kp, vp, pg * BS, t1 - 1, scale_log2);
+  if constexpr (MODE == 0) {
+    for (int pg = pg0 + wave; pg < pg1; pg += 4) {
+      const long blk = bt[pg];
+      const bf16_t* kp = k_cache + (blk * Hkv + kvh) * (BS * HD);
+      const bf16_t* vp = v_cache + (blk * Hkv + kvh) * (BS * HD);
+      process_page(st, qf, kp, vp, pg * BS, t1 - 1, scale_log2);
+    }
+  } else {
+    int pg = pg0 + wave;
+    PageFrags<HD> cur;
+    if (pg < pg1) {
+      const long blk = bt[pg];
+      load_page(cur, k_cache + (blk * Hkv + kvh) * (BS * HD),
+                v_cache + (blk * Hkv + kvh) * (BS * HD));
+    }
+    for (; pg < pg1; pg += 4) {
+      PageFrags<HD> nxt;
+      const bool more = pg + 4 < pg1;
+      if (more) {
+        const long blk = bt[pg + 4];
+        load_page(nxt, k_cache + (blk * Hkv + kvh) * (BS * HD),
+                  v_cache + (blk * Hkv + kvh) * (BS * HD));
+      }
+      if constexpr (MODE == 1) {
+        compute_page(st, qf, cur, pg * BS, t1 - 1, scale_log2);
+      } else {
+#pragma unroll
+        for (int s2 = 0; s2 < HD / 32; ++s2) asm volatile("" ::"v"(cur.ka[s2]), "v"(cur.kb[s2]));
+#pragma unroll
+        for (int i = 0; i < HD / 16; ++i) asm volatile("" ::"v"(cur.vf[i]));
+      }
+      if (more) cur = nxt;
+    }
   }
   // combine the 4 waves
   if (g == 0) { sm_ml[wave][c][0] = st.m; sm_ml[wave][c][1] = st.l; }
@@ -208,8 +309,12 @@ __global__ void __launch_bounds__(128) paged_decode_reduce_kernel(
   out[(long)b * out_stride + (long)head * HD + d] = f2bf(O / L);
 }
 
+static int g_decode_mode = 0;
+void set_decode_mode(int mode) { g_decode_mode = mode; }
+
 int paged_decode(const void* q, long q_stride, const void* k_cache, const void* v_cache,
-                 const int* block_tables, int bt_stride, const int* context_lens, void* out,
+                 const int* block_tables, int bt_stride, const int* context_lens,
+                 const int* order, void* out,
                  long out_stride, float* part_o, float* part_ml, int B, int Hq, int Hkv, int D,
                  int block_size, float scale, int part_tokens, int max_parts,
                  hipStream_t stream) {
@@ -218,16 +323,21 @@ int paged_decode(const void* q, long q_stride, const void* k_cache, const void* 
   if (Hq % Hkv != 0 || Hq / Hkv > 16) return -2;
   if (part_tokens % (4 * BS) != 0) return -3;
   if (max_parts > 1 && (!part_o || !part_ml)) return -4;
-#define LMX_DEC(HDV)                                                                          \
-  paged_decode_kernel<HDV><<<dim3(max_parts, Hkv, B), dim3(256), 0, stream>>>(                \
+#define LMX_DEC_K(HDV, MODE)                                                                  \
+  paged_decode_kernel<HDV, MODE><<<dim3(max_parts, Hkv, B), dim3(256), 0, stream>>>(          \
       (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, \
-      bt_stride, context_lens, (bf16_t*)out, out_stride, part_o, part_ml, Hq, Hkv, scale,      \
-      part_tokens, max_parts);                                                                \
+      bt_stride, context_lens, order, (bf16_t*)out, out_stride, part_o, part_ml, Hq, Hkv,     \
+      scale, part_tokens, max_parts);
+#define LMX_DEC(HDV)                                                                          \
+  if (g_decode_mode == 1) { LMX_DEC_K(HDV, 1) }                                               \
+  else if (g_decode_mode == 2) { LMX_DEC_K(HDV, 2) }                                          \
+  else { LMX_DEC_K(HDV, 0) }                                                                  \
   if (max_parts > 1)                                                                          \
     paged_decode_reduce_kernel<HDV><<<dim3(Hq, B), dim3(HDV), 0, stream>>>(                   \
         part_o, part_ml, context_lens, (bf16_t*)out, out_stride, Hq, part_tokens, max_parts);
   if (D == 128) { LMX_DEC(128) } else { LMX_DEC(64) }
 #undef LMX_DEC
+#undef LMX_DEC_K
   return (int)hipGetLastError();
 }
 

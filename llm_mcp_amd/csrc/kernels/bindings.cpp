@@ -20,7 +20,9 @@ int rope_cache(void*, long, const int*, const float*, int, int, int, int, const 
                int, int, int, const void*, const void*, float, hipStream_t);
 int kv_write(const void*, const void*, long, const int*, int, int, int, void*, void*, int,
              hipStream_t);
-int paged_decode(const void*, long, const void*, const void*, const int*, int, const int*, void*,
+void set_decode_mode(int);
+int paged_decode(const void*, long, const void*, const void*, const int*, int, const int*,
+                 const int*, void*,
                  long, float*, float*, int, int, int, int, int, float, int, int, hipStream_t);
 int paged_prefill(const void*, long, const void*, const void*, const int*, int, const int*,
                   const int*, const int*, int, void*, long, int, int, int, int, float, int,
@@ -99,15 +101,17 @@ PYBIND11_MODULE(_lmx_kernels, m) {
           "kv_write");
   });
   m.def("paged_decode", [](uptr q, long q_stride, uptr kc, uptr vc, uptr bt, int bt_stride,
-                           uptr ctx, uptr out, long out_stride, uptr part_o, uptr part_ml, int B,
-                           int Hq, int Hkv, int D, int BS, float scale, int part_tokens,
-                           int max_parts, uptr stream) {
+                           uptr ctx, uptr order, uptr out, long out_stride, uptr part_o,
+                           uptr part_ml, int B, int Hq, int Hkv, int D, int BS, float scale,
+                           int part_tokens, int max_parts, uptr stream) {
     check(lmx::paged_decode(P<void>(q), q_stride, P<void>(kc), P<void>(vc), P<int>(bt), bt_stride,
-                            P<int>(ctx), P<void>(out), out_stride, P<float>(part_o),
+                            P<int>(ctx), P<int>(order), P<void>(out), out_stride, P<float>(part_o),
                             P<float>(part_ml), B, Hq, Hkv, D, BS, scale, part_tokens, max_parts,
                             S(stream)),
           "paged_decode");
   });
+  m.def("set_decode_mode", [](int mode) { lmx::set_decode_mode(mode); },
+        "paged decode loop: 0 one page at a time, 1 next page prefetched, 2 loads only (probe)");
   m.def("paged_prefill", [](uptr q, long q_stride, uptr kc, uptr vc, uptr bt, int bt_stride,
                             uptr cu_q, uptr ctx, uptr tiles, int num_tiles, uptr out,
                             long out_stride, int Hq, int Hkv, int D, int BS, float scale,

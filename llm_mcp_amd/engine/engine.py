@@ -227,7 +227,8 @@ class LLMEngine:
                                              self.device)
         T = ecfg.max_batched_tokens + ecfg.max_num_seqs
         cap = 4 * (4 * T + ecfg.max_num_seqs * (self.max_blocks + 8) + 2 * T) + 16 * 64 + \
-            8 * ecfg.max_num_seqs * 4 + 4 * ecfg.max_num_seqs * (PEN_WINDOW + 4)
+            8 * ecfg.max_num_seqs * 4 + 4 * ecfg.max_num_seqs * (PEN_WINDOW + 4) + \
+            4 * ecfg.max_num_seqs + 16          # decode dispatch order
         self.packer = _Packer(cap, self.device)
         self.event_sink = event_sink
         self._intake: queue.SimpleQueue = queue.SimpleQueue()
@@ -310,7 +311,7 @@ class LLMEngine:
             ("ctx", np.int32, (Bmax,)), ("bt", np.int32, (Bmax, self.max_blocks)),
             ("temp", np.float32, (Bmax,)), ("topk", np.int32, (Bmax,)),
             ("topp", np.float32, (Bmax,)), ("seeds", np.int64, (Bmax,)),
-            ("offs", np.int32, (Bmax,))], dev)
+            ("offs", np.int32, (Bmax,)), ("order", np.int32, (Bmax,))], dev)
         # penalty inputs: uploaded only on steps with penalised rows, read by
         # the lazily captured penalty variants of the decode graphs
         pmeta = _FixedMeta([("win", np.int32, (Bmax, PEN_WINDOW)), ("ngen", np.int32, (Bmax,)),
@@ -321,6 +322,7 @@ class LLMEngine:
         h = meta.h
         h["ids"][:] = 0; h["pos"][:] = 0; h["slots"][:] = -1; h["ctx"][:] = 1; h["bt"][:] = 0
         h["temp"][:] = 0; h["topk"][:] = 0; h["topp"][:] = 1; h["seeds"][:] = 0; h["offs"][:] = 0
+        h["order"][:] = np.arange(Bmax, dtype=np.int32)
         meta.upload()
         self._gmeta = meta
         g = dict(meta.d)
@@ -348,7 +350,8 @@ class LLMEngine:
         g, dev, stream = self._gbuf, self.device, self._gstream
         pmeta = self._pmeta
         inp = StepInputs(g["ids"][:B], g["pos"][:B], g["slots"][:B], B, g["bt"][:B],
-                         g["ctx"][:B], g["cu"][:B + 1], g["tiles"], g["rows"][:B], B, B)
+                         g["ctx"][:B], g["cu"][:B + 1], g["tiles"], g["rows"][:B], B, B,
+                         decode_order=g["order"][:B])
         parts = self._graph_parts(B)
         ws = ops.DecodeWorkspace.__new__(ops.DecodeWorkspace)
         ws.max_parts, ws.part_o, ws.part_ml = parts, self.decode_ws.part_o, self.decode_ws.part_ml
@@ -651,6 +654,9 @@ class LLMEngine:
              np.zeros(2, np.int32)),
             ("rows", rows), ("temp", plan["temp"]), ("topk", plan["topk"]),
             ("topp", plan["topp"]), ("seeds", plan["seeds"]), ("offs", plan["offs"])]
+        nd = plan["num_decode"]
+        if nd > 1:
+            items.append(("order", ops.decode_order(plan["context_lens"][:nd])))
         pen = bool(plan.get("any_penalty")) and self.is_leader
         if pen:   # one pack, one upload: the pinned staging buffer is reused per call
             N = len(plan["sample_rows"])
@@ -658,7 +664,7 @@ class LLMEngine:
                       ("ngen", plan["pen_ngen"]), ("pen", plan["pen_params"].reshape(N, 3))]
         d = self.packer.pack(items)
         inp = StepInputs(d["ids"], d["pos"], d["slots"], plan["num_decode"], d["bt"], d["ctx"],
-                         d["cu"], d["tiles"], d["rows"], T, S)
+                         d["cu"], d["tiles"], d["rows"], T, S, decode_order=d.get("order"))
         ws = self.decode_ws
         logits = self.model.forward(inp, self.k_caches, self.v_caches, ws, self.ecfg.part_tokens)
         if not self.is_leader:
@@ -693,6 +699,7 @@ class LLMEngine:
         # never read (and always hold valid page ids)
         h["bt"][:n, :mb] = plan["block_tables"].reshape(n, mb)
         h["bt"][n:B, 0] = 0
+        h["order"][:B] = ops.decode_order(h["ctx"][:B])
         if pen:
             ph = self._pmeta.h
             ph["win"][:n] = plan["pen_window"].reshape(n, -1)

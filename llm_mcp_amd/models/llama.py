@@ -50,6 +50,7 @@ class StepInputs:
     sample_rows: torch.Tensor     # int64 [N] token rows whose logits are needed
     num_tokens: int
     num_seqs: int
+    decode_order: torch.Tensor | None = None   # int32 [num_decode] (ops.decode_order)
 
 
 class TPContext:
@@ -262,7 +263,7 @@ class LlamaModel:
             if nd > 0:
                 ops.paged_decode_attention(qkv[:nd], kc, vc, inp.block_tables,
                                            inp.context_lens, self.scale, attn[:nd], decode_ws,
-                                           part_tokens, Hq=Hq)
+                                           part_tokens, Hq=Hq, order=inp.decode_order)
             if T > nd:
                 ops.paged_prefill_attention(qkv, kc, vc, inp.block_tables[nd:],
                                             inp.cu_q[nd:], inp.context_lens[nd:],

@@ -221,8 +221,11 @@ class DecodeWorkspace:
 
 def paged_decode_attention(q: torch.Tensor, k_cache, v_cache, block_tables, context_lens,
                            scale: float, out: torch.Tensor, ws: DecodeWorkspace | None = None,
-                           part_tokens: int = 512, Hq: int | None = None) -> torch.Tensor:
-    """q: [B, Hq*D] rows (row stride = q.stride(0)); out: [B, Hq*D]."""
+                           part_tokens: int = 512, Hq: int | None = None,
+                           order: torch.Tensor | None = None) -> torch.Tensor:
+    """q: [B, Hq*D] rows (row stride = q.stride(0)); out: [B, Hq*D].
+    ``order`` (int32 [B], optional): a permutation of the rows, longest
+    context first -- the workgroup dispatch order (``decode_order``)."""
     B = q.shape[0]
     NB, Hkv, BS, D = k_cache.shape
     Hq = Hq or (q.shape[1] // D)
@@ -237,12 +240,24 @@ def paged_decode_attention(q: torch.Tensor, k_cache, v_cache, block_tables, cont
     _chk(block_tables.dtype == torch.int32 and context_lens.dtype == torch.int32, "int32 meta")
     _chk(block_tables.shape[0] >= B and context_lens.numel() >= B, "meta rows")
     _chk(part_tokens % 128 == 0, "part_tokens % 128")
+    if order is not None:
+        _chk(order.dtype == torch.int32 and order.numel() >= B and order.is_cuda, "order int32[B]")
     max_parts = ws.max_parts if ws is not None else 1
     native().paged_decode(_ptr(q), q.stride(0), _ptr(k_cache), _ptr(v_cache), _ptr(block_tables),
-                          block_tables.stride(0), _ptr(context_lens), _ptr(out), out.stride(0),
+                          block_tables.stride(0), _ptr(context_lens), _ptr(order), _ptr(out),
+                          out.stride(0),
                           _ptr(ws.part_o) if ws else 0, _ptr(ws.part_ml) if ws else 0, B, Hq, Hkv,
                           D, BS, float(scale), part_tokens, max_parts, _stream())
     return out
+
+
+def decode_order(context_lens) -> "np.ndarray":
+    """Dispatch order of the decode attention workgroups: rows by context
+    length, longest first (stable).  Measured at 256 rows with contexts
+    535-791: 5.2-5.4 TB/s in row order, 5.5-5.7 sorted
+    (tools/decode_attn_probe.py)."""
+    import numpy as np
+    return np.argsort(-np.asarray(context_lens, dtype=np.int64), kind="stable").astype(np.int32)
 
 
 def paged_prefill_attention(q: torch.Tensor, k_cache, v_cache, block_tables, cu_q,

@@ -162,6 +162,36 @@ def test_paged_prefill_varlen_with_prefix(Hq, Hkv, D):
     torch.testing.assert_close(out2.float().view(T, Hq, D), expect2.float(), atol=2e-2, rtol=2e-2)
 
 
+@pytest.mark.gpu
+def test_paged_decode_dispatch_order_and_loop_modes():
+    """The longest-first dispatch order (ops.decode_order) and the pipelined
+    loop form (mode 1) give bitwise the row-order result."""
+    Hq, Hkv, D = 32, 8, 128
+    ctxs = [535, 791, 1, 640, 33, 700, 64, 600] * 4
+    B = len(ctxs)
+    NB = sum(math.ceil(c / 32) for c in ctxs) + 4
+    kc, vc = _cache(NB, Hkv, D)
+    bt = _random_tables(B, ctxs, NB)
+    ctx = torch.tensor(ctxs, dtype=torch.int32, device=DEV)
+    q = _bf(B, (Hq + 2 * Hkv) * D)
+    scale = 1 / math.sqrt(D)
+    base = torch.empty(B, Hq * D, dtype=torch.bfloat16, device=DEV)
+    ops.paged_decode_attention(q, kc, vc, bt, ctx, scale, base, Hq=Hq)
+    order = torch.from_numpy(ops.decode_order(ctxs)).to(DEV)
+    assert sorted(order.tolist()) == list(range(B)) and ctxs[int(order[0])] == 791
+    got = torch.empty_like(base)
+    ops.paged_decode_attention(q, kc, vc, bt, ctx, scale, got, Hq=Hq, order=order)
+    assert torch.equal(got, base)
+    try:
+        ops.native().set_decode_mode(1)
+        ops.paged_decode_attention(q, kc, vc, bt, ctx, scale, got, Hq=Hq, order=order)
+    finally:
+        ops.native().set_decode_mode(0)
+    assert torch.equal(got, base)
+    expect = ref.paged_decode(q[:, :Hq * D].reshape(B, Hq, D), kc, vc, bt, ctx, scale)
+    torch.testing.assert_close(base.float().view(B, Hq, D), expect.float(), atol=2e-2, rtol=2e-2)
+
+
 def test_paged_decode_spike_rescale():
     """Force the online-softmax rescale: one key scores far above the rest in a
     late page (guide §5.4 rule 26)."""

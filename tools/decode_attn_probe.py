@@ -1,0 +1,66 @@
+"""Paged decode attention (K4) at the headline decode shape: 256 sequences,
+Llama-3-8B heads (32 q / 8 kv x 128), contexts 535-791 (the bench wave's
+range), random page tables over a 40 GB cache.  Times each loop form of the
+kernel (ops.native().set_decode_mode) and reports the K/V stream in TB/s.
+
+    python tools/decode_attn_probe.py [--batch 256] [--iters 50]
+"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from llm_mcp_amd import ops  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--ctx-lo", type=int, default=535)
+    ap.add_argument("--ctx-hi", type=int, default=791)
+    ap.add_argument("--order", choices=("random", "desc", "asc"), default="random",
+                    help="sequence order = workgroup dispatch order (longest-first test)")
+    a = ap.parse_args()
+    B, Hq, Hkv, D, BS = a.batch, 32, 8, 128, 32
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    ctx = torch.randint(a.ctx_lo, a.ctx_hi + 1, (B,), dtype=torch.int32)
+    if a.order != "random":
+        ctx = ctx.sort(descending=a.order == "desc").values
+    maxb = (a.ctx_hi + BS - 1) // BS
+    nb = 20000                                  # 20000 pages x 64 KB x 2 = 2.6 GB (> MALL)
+    perm = torch.randperm(nb)[:B * maxb].view(B, maxb).to(torch.int32)
+    k_cache = (torch.randn(nb, Hkv, BS, D, device=dev) * 0.5).to(torch.bfloat16)
+    v_cache = torch.randn(nb, Hkv, D, BS, device=dev).to(torch.bfloat16)
+    q = torch.randn(B, Hq * D, device=dev).to(torch.bfloat16)
+    bt, cl = perm.to(dev), ctx.to(dev)
+    out = torch.empty(B, Hq * D, device=dev, dtype=torch.bfloat16)
+    kv_bytes = int(ctx.sum()) * Hkv * D * 2 * 2
+    scale = D ** -0.5
+    ref = None
+    nat = ops.native()
+    for mode in (0, 1, 2, 0, 1):
+        nat.set_decode_mode(mode)
+        ops.paged_decode_attention(q, k_cache, v_cache, bt, cl, scale, out)
+        torch.cuda.synchronize()
+        if mode == 0 and ref is None:
+            ref = out.clone()
+        same = "-" if mode == 2 else ("bitwise" if torch.equal(out, ref) else
+                                      f"max diff {(out.float() - ref.float()).abs().max():.3g}")
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(a.iters):
+            ops.paged_decode_attention(q, k_cache, v_cache, bt, cl, scale, out)
+        e.record()
+        torch.cuda.synchronize()
+        us = s.elapsed_time(e) / a.iters * 1e3
+        print(f"decode attn B={B} {a.order} mode {mode}: {us:7.1f} us  {kv_bytes / us / 1e6:5.2f} TB/s  "
+              f"vs mode 0: {same}", flush=True)
+    nat.set_decode_mode(0)
+
+
+if __name__ == "__main__":
+    main()

@@ -88,6 +88,8 @@ for step in "$@"; do
           -- python3 bench.py --steps 2 --warmup 1 || exit $?
       python tools/prof_timeline.py gpurun_out/prof_bench/run_results.db --waves 2 \
           > gpurun_out/prof_bench_timeline.md 2>&1 || true ;;
+    attn_probe)
+      run attn_probe 180 python -u tools/decode_attn_probe.py || exit $? ;;
     rope_probe)
       run rope_probe 120 python -u tools/rope_probe.py || exit $? ;;
     smoke)
