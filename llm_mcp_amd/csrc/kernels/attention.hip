@@ -187,7 +187,8 @@ __device__ __forceinline__ int effective_part(int ctx, int part_tokens, int max_
 // grid (max_parts, Hkv, B), block 256.
 // MODE 0: one page at a time (load, then compute); MODE 1: the next page's
 // block id and K/V fragments are loaded before the current page is computed
-// (two pages in flight per wave); MODE 2: loads only (diagnostic ceiling).
+// (two pages in flight per wave); MODE 2: loads only (diagnostic ceiling);
+// MODE 3: loads only, every instruction one contiguous 1 KB (diagnostic).
 template <int HD, int MODE>
 __global__ void __launch_bounds__(256) paged_decode_kernel(
     const bf16_t* __restrict__ q, long q_stride, const bf16_t* __restrict__ k_cache,
@@ -246,6 +247,22 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
       }
       if constexpr (MODE == 1) {
         compute_page(st, qf, cur, pg * BS, t1 - 1, scale_log2);
+      } else if constexpr (MODE == 3) {
+        // probe: the same bytes as whole 1-KB contiguous pieces per instruction
+        const long blk = bt[pg];
+        const bf16_t* kp = k_cache + (blk * Hkv + kvh) * (BS * HD);
+        const bf16_t* vp = v_cache + (blk * Hkv + kvh) * (BS * HD);
+#pragma unroll
+        for (int s2 = 0; s2 < HD / 32; ++s2) {
+          cur.ka[s2] = load_frag16B(kp + (2 * s2) * 512 + lane * 8);
+          cur.kb[s2] = load_frag16B(kp + (2 * s2 + 1) * 512 + lane * 8);
+        }
+#pragma unroll
+        for (int i = 0; i < HD / 16; ++i) cur.vf[i] = load_frag16B(vp + i * 512 + lane * 8);
+#pragma unroll
+        for (int s2 = 0; s2 < HD / 32; ++s2) asm volatile("" ::"v"(cur.ka[s2]), "v"(cur.kb[s2]));
+#pragma unroll
+        for (int i = 0; i < HD / 16; ++i) asm volatile("" ::"v"(cur.vf[i]));
       } else {
 #pragma unroll
         for (int s2 = 0; s2 < HD / 32; ++s2) asm volatile("" ::"v"(cur.ka[s2]), "v"(cur.kb[s2]));
@@ -331,6 +348,7 @@ int paged_decode(const void* q, long q_stride, const void* k_cache, const void* 
 #define LMX_DEC(HDV)                                                                          \
   if (g_decode_mode == 1) { LMX_DEC_K(HDV, 1) }                                               \
   else if (g_decode_mode == 2) { LMX_DEC_K(HDV, 2) }                                          \
+  else if (g_decode_mode == 3) { LMX_DEC_K(HDV, 3) }                                          \
   else { LMX_DEC_K(HDV, 0) }                                                                  \
   if (max_parts > 1)                                                                          \
     paged_decode_reduce_kernel<HDV><<<dim3(Hq, B), dim3(HDV), 0, stream>>>(                   \

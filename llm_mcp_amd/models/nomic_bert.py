@@ -47,7 +47,8 @@ class NomicBertModel:
         # 64 channels (gemm_nt act=3)
         I2, d = self.w["layers"][0]["w_gate_up"].shape
         self.gu_cfg = ops.encoder_choice(I2, d) if self.device.type == "cuda" else None
-        self.gu_block = ops.DGEMM_CONFIGS[self.gu_cfg & ops.DGEMM_CFG_MASK][1] // 2 if self.gu_cfg is not None else 64
+        self.gu_block = (ops.DGEMM_CONFIGS[self.gu_cfg & ops.DGEMM_CFG_MASK][1] // 2
+                         if self.gu_cfg is not None else 64)
         for L in self.w["layers"]:
             L.pop("w_gu_il", None)      # always this model's own layout (never a copy's)
             if ops.gemm_nt_supported(*L["w_gate_up"].shape) and I2 // 2 % self.gu_block == 0:
@@ -73,10 +74,12 @@ class NomicBertModel:
                 "emb_ln_w": ones(), "emb_ln_b": zeros(), "layers": layers}
 
     def _linear(self, x, w, residual=None):
-        cfg = ops.encoder_choice(w.shape[0], w.shape[1]) if x.is_cuda else None
-        if cfg is not None and residual is None:
-            return ops.dgemm(x, w, cfg, 1)          # K11 where it beat gemm_nt
-        if ops.gemm_nt_supported(w.shape[0], w.shape[1]):
+        """Plain projection on the backend measured fastest for its shape
+        (ops.encoder_backend): K11, hipBLASLt or gemm_nt."""
+        kind, cfg = ops.encoder_backend(w.shape[0], w.shape[1]) if x.is_cuda else ("lib", None)
+        if kind == "k11" and residual is None:
+            return ops.dgemm(x, w, cfg, 1)
+        if kind == "gemm_nt" and ops.gemm_nt_supported(w.shape[0], w.shape[1]):
             return ops.gemm_nt(x, w, residual=residual)
         y = torch.nn.functional.linear(x, w)
         return y if residual is None else y + residual

@@ -650,15 +650,13 @@ def _dg_table() -> dict:
 _ENC_TABLE: dict | None = None
 
 
-def encoder_choice(N: int, K: int) -> int | None:
-    """K11 tile for a prefill / encoder-sized GEMM of this (N, K), where it was
-    measured faster than the older hand-written gemm_nt (config
-    dgemm_gfx950.json "encoder", bench/dgemm_bench.py --encoder); None keeps
-    gemm_nt."""
+def _enc_table() -> dict:
+    """{(N, K): encoder-table entry} (config dgemm_gfx950.json "encoder",
+    bench/dgemm_bench.py --encoder: TF/s of K11's best tile, gemm_nt and
+    hipBLASLt on prefill / encoder shapes at the largest M measured)."""
     global _ENC_TABLE
     if _ENC_TABLE is None:
         _ENC_TABLE = {}
-        _dg_table()
         import json
         import os
         path = os.environ.get("LMX_DGEMM_TABLE") or os.path.join(
@@ -666,9 +664,36 @@ def encoder_choice(N: int, K: int) -> int | None:
         if os.environ.get("LMX_DGEMM", "1") == "1" and os.path.exists(path):
             with open(path) as f:
                 for e in json.load(f).get("encoder", []):
-                    if e.get("gemm_nt_tflops") is None or e["tflops"] > e["gemm_nt_tflops"]:
-                        _ENC_TABLE[(int(e["N"]), int(e["K"]))] = int(e["cfg"])
-    return _ENC_TABLE.get((N, K))
+                    _ENC_TABLE[(int(e["N"]), int(e["K"]))] = e
+    return _ENC_TABLE
+
+
+def encoder_choice(N: int, K: int) -> int | None:
+    """K11 tile for a fused-epilogue encoder GEMM of this (N, K) (the SwiGLU
+    gate/up projection), where K11 was measured faster than the older
+    hand-written gemm_nt; None keeps gemm_nt."""
+    e = _enc_table().get((N, K))
+    if e is None:
+        return None
+    if e.get("gemm_nt_tflops") is None or e["tflops"] > e["gemm_nt_tflops"]:
+        return int(e["cfg"])
+    return None
+
+
+def encoder_backend(N: int, K: int) -> tuple[str, int | None]:
+    """Fastest measured backend for a PLAIN encoder GEMM of this (N, K):
+    ("k11", cfg), ("lib", None) -- hipBLASLt, the library is kept for plain
+    GEMMs it wins -- or ("gemm_nt", None).  Unmeasured shapes: gemm_nt."""
+    e = _enc_table().get((N, K))
+    if e is None:
+        return ("gemm_nt", None)
+    cands = [(e["tflops"], "k11")]
+    if e.get("gemm_nt_tflops") is not None:
+        cands.append((e["gemm_nt_tflops"], "gemm_nt"))
+    if e.get("lib_tflops") is not None:
+        cands.append((e["lib_tflops"], "lib"))
+    best = max(cands)[1]
+    return (best, int(e["cfg"]) if best == "k11" else None)
 
 
 def dgemm_choice(M: int, N: int, K: int, epi: int = 0) -> tuple[int, int] | None:

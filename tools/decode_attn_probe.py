@@ -42,13 +42,13 @@ def main():
     scale = D ** -0.5
     ref = None
     nat = ops.native()
-    for mode in (0, 1, 2, 0, 1):
+    for mode in (0, 1, 2, 3, 0, 1, 2, 3):
         nat.set_decode_mode(mode)
         ops.paged_decode_attention(q, k_cache, v_cache, bt, cl, scale, out)
         torch.cuda.synchronize()
         if mode == 0 and ref is None:
             ref = out.clone()
-        same = "-" if mode == 2 else ("bitwise" if torch.equal(out, ref) else
+        same = "-" if mode >= 2 else ("bitwise" if torch.equal(out, ref) else
                                       f"max diff {(out.float() - ref.float()).abs().max():.3g}")
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()

@@ -90,6 +90,8 @@ for step in "$@"; do
           > gpurun_out/prof_bench_timeline.md 2>&1 || true ;;
     attn_probe)
       run attn_probe 180 python -u tools/decode_attn_probe.py || exit $? ;;
+    embed_bench)
+      run embed_bench 300 python -u -m llm_mcp_amd.bench.embed_engine_bench || exit $? ;;
     rope_probe)
       run rope_probe 120 python -u tools/rope_probe.py || exit $? ;;
     smoke)
