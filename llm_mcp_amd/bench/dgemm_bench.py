@@ -264,7 +264,8 @@ def encoder(ms: list[int], write: bool = False) -> None:
     operands (uniform [-1, 1)), TFLOP/s."""
     shapes = {"nomic.qkv": (2304, 768), "nomic.o": (768, 768), "nomic.gate_up": (6144, 768),
               "nomic.down": (768, 3072), "l8b.qkv": (6144, 4096), "l8b.gate_up": (28672, 4096),
-              "l8b.down": (4096, 14336)}
+              "l8b.down": (4096, 14336), "bert.qkv": (3072, 1024), "bert.o": (1024, 1024),
+              "bert.w1": (4096, 1024), "bert.w2": (1024, 4096)}
     cfgs = ops.native().dgemm_configs()
     wins: dict = {}
     for M in ms:

@@ -70,10 +70,20 @@ class BertModel:
         return n
 
     def _linear(self, x, w, b=None, act=0, residual=None):
-        if x.is_cuda and ops.gemm_nt_supported(w.shape[0], w.shape[1]):
-            return ops.gemm_nt(x, w, b, act, residual=residual)
+        """Projection + bias (+ GELU) on the backend measured fastest for the
+        shape (ops.encoder_backend).  Returns (y, residual still to add): the
+        K7 epilogue fuses the residual, the library path leaves it to the
+        following LayerNorm's fused residual add."""
+        if x.is_cuda:
+            kind, _ = ops.encoder_backend(w.shape[0], w.shape[1])
+            if kind == "lib" or not ops.gemm_nt_supported(w.shape[0], w.shape[1]):
+                y = torch.nn.functional.linear(x, w, b)
+                if act == ops.ACT_GELU_ERF:
+                    y = torch.nn.functional.gelu(y)
+                return y, residual
+            return ops.gemm_nt(x, w, b, act, residual=residual), None
         from ..ops import ref
-        return ref.gemm_nt(x, w, b, act, residual)
+        return ref.gemm_nt(x, w, b, act, residual), None
 
     @torch.no_grad()
     def forward(self, ids: torch.Tensor, cu: torch.Tensor, lens: list[int],
@@ -117,17 +127,17 @@ class BertModel:
         x = ops.layer_norm(x, w["emb_ln_w"], w["emb_ln_b"], cfg.ln_eps, residual=pe)
         attn = torch.empty((T, H * D), dtype=self.dtype, device=dev)
         for L in w["layers"]:
-            qkv = self._linear(x, L["wqkv"], L["bqkv"])
+            qkv, _ = self._linear(x, L["wqkv"], L["bqkv"])
             k = qkv[:, d:2 * d].view(T, H, D)
             v = qkv[:, 2 * d:].view(T, H, D)
             ops.kv_write(k, v, slots_t, kc, vc)
             ops.paged_prefill_attention(qkv, kc, vc, bt, cu, ctx, tiles_t, self.scale, attn,
                                         causal=False, Hq=H)
-            o = self._linear(attn, L["wo"], L["bo"], residual=x)
-            h = ops.layer_norm(o, L["ln1_w"], L["ln1_b"], cfg.ln_eps)
-            f = self._linear(h, L["w1"], L["b1"], act=ops.ACT_GELU_ERF)
-            m = self._linear(f, L["w2"], L["b2"], residual=h)
-            x = ops.layer_norm(m, L["ln2_w"], L["ln2_b"], cfg.ln_eps)
+            o, r = self._linear(attn, L["wo"], L["bo"], residual=x)
+            h = ops.layer_norm(o, L["ln1_w"], L["ln1_b"], cfg.ln_eps, residual=r)
+            f, _ = self._linear(h, L["w1"], L["b1"], act=ops.ACT_GELU_ERF)
+            m, r = self._linear(f, L["w2"], L["b2"], residual=h)
+            x = ops.layer_norm(m, L["ln2_w"], L["ln2_b"], cfg.ln_eps, residual=r)
         if cfg.pooling == "cls":
             x = x.index_select(0, first_t.long()).contiguous()
             cu = torch.arange(S + 1, dtype=torch.int32, device=dev)
