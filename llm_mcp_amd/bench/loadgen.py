@@ -83,26 +83,38 @@ async def one_chat(session, url, model, prompt, max_tokens, temperature, top_p, 
             "decode_s": (last - t0 - ttft) if (last and ttft) else 0.0}
 
 
-async def wave(url, model, concurrency, prompt_len, max_tokens, temperature, top_p, seed):
+async def wave(url, model, concurrency, prompt_len, max_tokens, temperature, top_p, seed,
+               session=None):
+    """One wave of ``concurrency`` concurrent streams.  ``session``: a
+    ClientSession kept across waves (its keep-alive connections skip the
+    reconnects at the start of the next wave), else a fresh one."""
     prompts = wave_prompts(seed, concurrency, prompt_len)
     # the next wave's prompts are generated while this one streams (the gap
     # between two timed waves then holds no client-side prompt generation)
     nxt = (seed + 1, concurrency, prompt_len)
     asyncio.get_running_loop().call_later(
         0.5, lambda: _PROMPTS.setdefault(nxt, wave_prompts(*nxt)))
-    conn = aiohttp.TCPConnector(limit=0)
-    timeout = aiohttp.ClientTimeout(total=3600)
-    async with aiohttp.ClientSession(connector=conn, timeout=timeout) as s:
+    own = session is None
+    s = session or new_session()
+    try:
         t0 = time.perf_counter()
         res = await asyncio.gather(*[one_chat(s, url, model, p, max_tokens, temperature, top_p)
                                      for p in prompts])
         el = time.perf_counter() - t0
+    finally:
+        if own:
+            await s.close()
     ttfts = [r["ttft"] for r in res]
     tok = sum(r["tokens"] for r in res)
     itl = [r["decode_s"] / (r["tokens"] - 1) for r in res if r["tokens"] > 1]
     return {"elapsed": el, "tokens": tok, "requests": len(res), "ttfts": ttfts, "itls": itl,
             "ttft_p50": percentile(ttfts, 50), "ttft_p95": percentile(ttfts, 95),
             "itl_p50": percentile(itl, 50), "tok_s": tok / el if el > 0 else 0.0}
+
+
+def new_session() -> aiohttp.ClientSession:
+    return aiohttp.ClientSession(connector=aiohttp.TCPConnector(limit=0),
+                                 timeout=aiohttp.ClientTimeout(total=3600))
 
 
 async def wait_ready(url, timeout=1800):
@@ -117,6 +129,10 @@ async def wait_ready(url, timeout=1800):
                 pass
             await asyncio.sleep(0.5)
     return False
+
+
+async def _make_session() -> aiohttp.ClientSession:
+    return new_session()          # created inside the loop that will use it
 
 
 def main(argv=None):
@@ -139,6 +155,7 @@ def main(argv=None):
     if a.serve_stdin:
         ok = loop.run_until_complete(wait_ready(a.url))
         print(json.dumps({"ready": ok}), flush=True)
+        session = loop.run_until_complete(_make_session())
         i = 0
         for line in sys.stdin:
             cmd = line.strip()
@@ -147,9 +164,10 @@ def main(argv=None):
             if cmd.startswith("run"):
                 r = loop.run_until_complete(wave(a.url, a.model, a.concurrency, a.prompt_len,
                                                  a.max_tokens, a.temperature, a.top_p,
-                                                 (a.seed_base << 20) + i))
+                                                 (a.seed_base << 20) + i, session=session))
                 i += 1
                 print(json.dumps(r), flush=True)
+        loop.run_until_complete(session.close())
         return
     for i in range(a.waves):
         r = loop.run_until_complete(wave(a.url, a.model, a.concurrency, a.prompt_len,

@@ -43,15 +43,16 @@ def summarise(steps, prev_end):
 def report(db_path: str, waves: int = 2, wave_gap_ms: float = 30.0) -> str:
     db = sqlite3.connect(db_path)
     rows = db.execute("select name, start, end from kernels order by start").fetchall()
-    steps = steps_of(rows)
-    # split into waves at long idle gaps
-    groups, cur = [], [steps[0]]
-    for a, b in zip(steps, steps[1:]):
-        if (b[0][1] - a[-1][2]) / 1e6 > wave_gap_ms:
-            groups.append(cur)
+    # waves: runs of kernels separated by an idle GPU longer than wave_gap_ms
+    segs, cur = [], [rows[0]]
+    for a, b in zip(rows, rows[1:]):
+        if (b[1] - a[2]) / 1e6 > wave_gap_ms:
+            segs.append(cur)
             cur = []
         cur.append(b)
-    groups.append(cur)
+    segs.append(cur)
+    groups = [g for g in (steps_of(sg) for sg in segs) if g]
+    steps = [st for g in groups for st in g]
     out = [f"{len(steps)} engine steps in {len(groups)} waves (split at idle > {wave_gap_ms} ms)", ""]
     out += ["| wave | span ms | class | steps | wall ms | busy ms | host gaps ms | max gap ms |",
             "|---:|---:|---|---:|---:|---:|---:|---:|"]
