@@ -245,6 +245,7 @@ class LlamaModel:
             x = ops.embed_gather(w["embed"], inp.input_ids)
         residual = None
         attn = torch.empty((T, Hq * D), dtype=self.dtype, device=self.device)
+        all_rows = inp.sample_rows.numel() == T     # decode: rows 0..T-1, each sampled
         for li, L in enumerate(w["layers"]):
             if residual is None:
                 residual = x
@@ -282,7 +283,10 @@ class LlamaModel:
                 a = ops.silu_mul(ops.linear(h, L["w_gate_up"]))
             # down's partials go to the next layer's input norm (not after the
             # last layer: the final norm runs on the sampled rows only)
-            x = ops.linear(a, L["w_down"], defer=tp.size == 1 and li + 1 < len(w["layers"]))
+            # the last layer's partials go to the final norm when every row is
+            # sampled (pure decode): no gather of the sampled rows is needed
+            x = ops.linear(a, L["w_down"], defer=tp.size == 1 and
+                           (li + 1 < len(w["layers"]) or all_rows))
             if tp.size > 1:
                 x = tp.reduce_scatter_rows(x, Tp) if sp else tp.all_reduce(x)
         # final norm only on the rows we sample from
@@ -290,6 +294,8 @@ class LlamaModel:
         if sp:
             hs = tp.all_gather_rows(ops.rms_norm(x, w["norm"], cfg.rms_eps,
                                                  residual=residual))[:T].index_select(0, rows)
+        elif all_rows:
+            hs = ops.rms_norm(x, w["norm"], cfg.rms_eps, residual=residual)
         else:
             xs = x.index_select(0, rows)
             rs = residual.index_select(0, rows)

@@ -26,6 +26,10 @@ for step in "$@"; do
       run rehearse2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
           --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus 2 --steps 2 --warmup 1 \
           --concurrency 64 --rehearse-on-one-gpu --api-procs 2 || exit $? ;;
+    rehearse4)
+      run rehearse4 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 \
+          --master-addr 127.0.0.1 --master-port 29612 bench.py --gpus 4 --steps 2 --warmup 1 \
+          --concurrency 32 --rehearse-on-one-gpu || exit $? ;;
     dgemm_tests)
       run dgemm_tests 600 python -u -m pytest tests/test_kernels_gpu.py -k dgemm -x -q --timeout 120 \
           --timeout-method thread -p no:cacheprovider || exit $? ;;
