@@ -147,37 +147,56 @@ __global__ void __launch_bounds__(256) rope_cache_tiled_kernel(
   if (threadIdx.x < RT)
     sslot[threadIdx.x] = (threadIdx.x < nt && slot_mapping) ? slot_mapping[t0 + threadIdx.x] : -1;
   __syncthreads();
-  const int per_tok = (Hq + Hkv) * tph;
-  for (int it = threadIdx.x; it < nt * per_tok; it += blockDim.x) {
-    const int tt = it / per_tok, rem = it - tt * per_tok;
-    const int h = rem / tph, i = (rem % tph) * 4;
-    bf16_t* hp = qkv + (long)(t0 + tt) * qkv_stride + (long)h * D;
+  // a thread owns one (token, 4-pair chunk) and walks every q / k head of the
+  // token: the cos/sin chunk is loaded once per item instead of once per
+  // head, and HU heads' loads are issued before their arithmetic
+  const int H = Hq + Hkv;
+  constexpr int HU = 4;
+  for (int it = threadIdx.x; it < nt * tph; it += blockDim.x) {
+    const int tt = it / tph, i = (it % tph) * 4;
+    bf16_t* row = qkv + (long)(t0 + tt) * qkv_stride;
     const float* cs = cos_sin + (long)positions[t0 + tt] * D;
     const int slot = sslot[tt];
-    const bf16x4_t x1 = *reinterpret_cast<const bf16x4_t*>(hp + i);
-    const bf16x4_t x2 = *reinterpret_cast<const bf16x4_t*>(hp + half + i);
     const float4 c = *reinterpret_cast<const float4*>(cs + i);
     const float4 sn = *reinterpret_cast<const float4*>(cs + half + i);
     const float cc[4] = {c.x, c.y, c.z, c.w}, ss[4] = {sn.x, sn.y, sn.z, sn.w};
-    const bool is_k = h >= Hq;
-    float a[4], b[4];
+    for (int h0 = 0; h0 < H; h0 += HU) {
+      bf16x4_t x1[HU], x2[HU];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) a[j] = bf2f((uint16_t)x1[j]), b[j] = bf2f((uint16_t)x2[j]);
-    if (q_norm) qk_norm(a, b, is_k ? k_norm : q_norm, i, half, D, eps);
-    bf16x4_t o1, o2;
+      for (int u = 0; u < HU; ++u) {
+        if (h0 + u < H) {
+          const bf16_t* hp = row + (long)(h0 + u) * D;
+          x1[u] = *reinterpret_cast<const bf16x4_t*>(hp + i);
+          x2[u] = *reinterpret_cast<const bf16x4_t*>(hp + half + i);
+        }
+      }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      o1[j] = (short)f2bf(a[j] * cc[j] - b[j] * ss[j]);
-      o2[j] = (short)f2bf(b[j] * cc[j] + a[j] * ss[j]);
-    }
-    if (!is_k || rotate_k_inplace || slot < 0) {
-      *reinterpret_cast<bf16x4_t*>(hp + i) = o1;
-      *reinterpret_cast<bf16x4_t*>(hp + half + i) = o2;
-    }
-    if (is_k && slot >= 0 && k_cache) {
-      bf16_t* kp = k_cache + (((long)(slot / BS) * Hkv + (h - Hq)) * BS + slot % BS) * D;
-      *reinterpret_cast<bf16x4_t*>(kp + i) = o1;
-      *reinterpret_cast<bf16x4_t*>(kp + half + i) = o2;
+      for (int u = 0; u < HU; ++u) {
+        const int h = h0 + u;
+        if (h >= H) break;
+        bf16_t* hp = row + (long)h * D;
+        const bool is_k = h >= Hq;
+        float a[4], b[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          a[j] = bf2f((uint16_t)x1[u][j]), b[j] = bf2f((uint16_t)x2[u][j]);
+        if (q_norm) qk_norm(a, b, is_k ? k_norm : q_norm, i, half, D, eps);
+        bf16x4_t o1, o2;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          o1[j] = (short)f2bf(a[j] * cc[j] - b[j] * ss[j]);
+          o2[j] = (short)f2bf(b[j] * cc[j] + a[j] * ss[j]);
+        }
+        if (!is_k || rotate_k_inplace || slot < 0) {
+          *reinterpret_cast<bf16x4_t*>(hp + i) = o1;
+          *reinterpret_cast<bf16x4_t*>(hp + half + i) = o2;
+        }
+        if (is_k && slot >= 0 && k_cache) {
+          bf16_t* kp = k_cache + (((long)(slot / BS) * Hkv + (h - Hq)) * BS + slot % BS) * D;
+          *reinterpret_cast<bf16x4_t*>(kp + i) = o1;
+          *reinterpret_cast<bf16x4_t*>(kp + half + i) = o2;
+        }
+      }
     }
   }
   if (!v_cache || !slot_mapping) return;

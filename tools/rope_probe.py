@@ -42,6 +42,27 @@ def main():
         "no V scatter": (slots.data_ptr(), kc.data_ptr(), 0),
         "no cache write": (0, 0, 0),
     }
+    # prefill rows: 16,384 tokens of 32 prompts with consecutive slots (tiled kernel)
+    TP = 16384
+    qkvp = torch.randn(TP, (Hq + 2 * Hkv) * D, device=dev).to(torch.bfloat16)
+    posp = (torch.arange(TP, device=dev, dtype=torch.int32) % 512)
+    slotsp = torch.arange(TP, device=dev, dtype=torch.int32)
+    kcp = torch.zeros(TP // BS, Hkv, BS, D, device=dev, dtype=torch.bfloat16)
+    vcp = torch.zeros(TP // BS, Hkv, D, BS, device=dev, dtype=torch.bfloat16)
+    for _ in range(5):
+        nat.rope_cache(qkvp.data_ptr(), qkvp.stride(0), posp.data_ptr(), cs.data_ptr(), TP, Hq,
+                       Hkv, D, slotsp.data_ptr(), kcp.data_ptr(), vcp.data_ptr(), BS, 0, 0, 0, 0,
+                       1e-6, st)
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(50):
+        nat.rope_cache(qkvp.data_ptr(), qkvp.stride(0), posp.data_ptr(), cs.data_ptr(), TP, Hq,
+                       Hkv, D, slotsp.data_ptr(), kcp.data_ptr(), vcp.data_ptr(), BS, 0, 0, 0, 0,
+                       1e-6, st)
+    e.record()
+    torch.cuda.synchronize()
+    print(f"rope_cache tiled T={TP} {s.elapsed_time(e) / 50 * 1e3:7.2f} us", flush=True)
     for name, args in variants.items():
         for _ in range(10):
             call(*args)
