@@ -129,6 +129,8 @@ class CoreState:
             self._retention = RetentionPlanner(
                 self.store, float(os.environ.get("LMX_JOB_RETENTION_DAYS", "7")))
         self._retention.tick()
+        if not hasattr(self, "_comm_live_seq"):
+            self._comm_live_seq: dict[str, int] = {}
         for m in self.registry.all():
             info = m.info()
             if "kv_usage" in info:
@@ -136,13 +138,6 @@ class CoreState:
             if info.get("running"):
                 # sampled each maintenance tick: sequences in the engine's batch
                 self.metrics.batch_size.labels(m.device_id).observe(info["running"])
-        from ..devices import rocm_enum
-        for idx, t in rocm_enum.gpu_telemetry().items():
-            dev = rocm_enum.device_id(idx)
-            if "hbm_used_bytes" in t:
-                self.metrics.hbm_used.labels(dev).set(t["hbm_used_bytes"])
-            if "busy_pct" in t:
-                self.metrics.gpu_util.labels(dev).set(t["busy_pct"])
             comm = info.get("tp_comm") or {}
             if comm and m.device_id not in self._comm_seen:
                 # the TP group's start-up all-reduce probe (parallel/tp_worker.py)
@@ -150,6 +145,19 @@ class CoreState:
                 for path, by_size in comm.items():
                     for us in by_size.values():
                         self.metrics.allreduce.labels(path).observe(us / 1e6)
+            live = info.get("tp_comm_live") or {}
+            if live.get("seq", 0) > self._comm_live_seq.get(m.device_id, 0):
+                # the engine's latest in-service sample (engine._comm_probe)
+                self._comm_live_seq[m.device_id] = live["seq"]
+                for path, us in (live.get("us") or {}).items():
+                    self.metrics.allreduce.labels(path).observe(us / 1e6)
+        from ..devices import rocm_enum
+        for idx, t in rocm_enum.gpu_telemetry().items():
+            dev = rocm_enum.device_id(idx)
+            if "hbm_used_bytes" in t:
+                self.metrics.hbm_used.labels(dev).set(t["hbm_used_bytes"])
+            if "busy_pct" in t:
+                self.metrics.gpu_util.labels(dev).set(t["busy_pct"])
 
     async def start_background(self, app=None):
         disc = env_int("DISCOVERY_INTERVAL", 0)

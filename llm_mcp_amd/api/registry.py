@@ -55,6 +55,10 @@ class LocalModel:
         comm = getattr(eng, "tp_comm", None) or self.tags.get("tp_comm")
         if comm:
             d["tp_comm"] = comm       # TP all-reduce probe, us by message size
+        live = getattr(eng, "tp_comm_live", None) or \
+            (self.tags.get("live") or {}).get("tp_comm_live")
+        if live:
+            d["tp_comm_live"] = live  # latest in-service sample (engine._comm_probe)
         return d
 
 

@@ -215,6 +215,9 @@ class LLMEngine:
         self.tp = self.model.tp
         self.is_leader = self.tp.rank == 0
         self.chan = plan_channel
+        # live TP all-reduce samples every LMX_TP_PROBE_STEPS engine steps (0 = off)
+        self._comm_every = int(os.environ.get("LMX_TP_PROBE_STEPS", "2000"))
+        self.tp_comm_live: dict = {}
         self.Hq, self.Hkv, self.D = self.model.Hq, self.model.Hkv, self.model.D
         self.q_per_tile = ops.prefill_q_per_tile(self.Hq, self.Hkv)
         self._alloc_kv()
@@ -430,7 +433,21 @@ class LLMEngine:
                 self._run_graph(plan, bucket)
             else:
                 self._run_eager(plan)
+            if msg.get("probe"):
+                self._comm_probe()
             n += 1
+
+    def _comm_probe(self):
+        """Live all-reduce sample of the TP group (collective: the leader
+        flags it in the step's plan, every rank runs it after the step): one
+        decode-sized message (batch x hidden bf16) per path, exported as
+        rccl_allreduce_seconds{group=path} next to the start-up probe."""
+        from ..parallel.tp_worker import probe_allreduce
+        n = max(1, self.ecfg.max_num_seqs) * self.cfg.hidden_size * 2
+        res = probe_allreduce(self.tp, self.device, sizes=(n,), iters=3)
+        seq = int(self.tp_comm_live.get("seq", 0)) + 1
+        self.tp_comm_live = {"seq": seq, "bytes": n,
+                             "us": {p: next(iter(v.values())) for p, v in res.items() if v}}
 
     @property
     def num_active(self) -> int:
@@ -555,9 +572,13 @@ class LLMEngine:
         bucket = None
         if nd == S == T and self.graphs:
             bucket = next((b for b in self._bucket_list if b >= nd), None)
+        probe = (self.tp.size > 1 and self._comm_every > 0
+                 and self.stats["steps"] % self._comm_every == self._comm_every - 1)
         if self.chan is not None:
             from ..parallel.plan_channel import encode_plan
-            self.chan.publish(encode_plan(plan, bucket))
+            msg = encode_plan(plan, bucket)
+            msg["probe"] = int(probe)
+            self.chan.publish(msg)
         t1 = time.perf_counter()
         if bucket is not None:
             tok, lp = self._run_graph(plan, bucket)
@@ -570,6 +591,8 @@ class LLMEngine:
         toks, lps = self._finish_fetch(N)
         t4 = time.perf_counter()
         finished = self.sched.update(toks)
+        if probe:
+            self._comm_probe()
         t5 = time.perf_counter()
         self._pending = (plan["seq_ids"], plan["sample_seq"], toks, lps, finished)
         if not self.sched.has_work:

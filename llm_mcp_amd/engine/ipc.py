@@ -185,7 +185,8 @@ class EngineServer:
         s = e.sched
         return {"running": s.num_running, "waiting": s.num_waiting, "kv_usage": s.kv_usage,
                 "kv_free_blocks": s.kv_free_blocks, "stats": dict(e.stats),
-                "tp_comm": getattr(e, "tp_comm", {})}
+                "tp_comm": getattr(e, "tp_comm", {}),
+                "tp_comm_live": getattr(e, "tp_comm_live", {})}
 
     # engine thread: one message per connection per step
     def _sink(self, evs: list[TokenEvent]):

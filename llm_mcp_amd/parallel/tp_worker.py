@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import logging
 import os
+import time
 
 import torch
 import torch.distributed as dist
@@ -85,6 +86,12 @@ def probe_allreduce(tp: TPContext, device: torch.device, sizes=(16 << 10, 256 <<
                         tp.peer = saved
             for _ in range(3):
                 call()
+            if device.type != "cuda":          # gloo group (CPU tests / plumbing)
+                t0 = time.perf_counter()
+                for _ in range(iters):
+                    call()
+                res[n] = round((time.perf_counter() - t0) / iters * 1e6, 1)
+                continue
             torch.cuda.synchronize(device)
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()

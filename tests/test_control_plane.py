@@ -277,3 +277,28 @@ def test_gpu_telemetry_from_drm_sysfs(tmp_path):
         (card / "device").symlink_to(pci)
     t = rocm_enum.gpu_telemetry(str(tmp_path / "drm"))
     assert t == {0: {"busy_pct": 37, "hbm_used_bytes": 123456789}}
+
+
+def test_maintenance_exports_live_allreduce_samples():
+    """rccl_allreduce_seconds takes the TP engine's start-up probe once and
+    every new in-service sample (engine._comm_probe, seq-numbered) once."""
+    from llm_mcp_amd.api.registry import LocalModel
+    st = CoreState(store=MemoryStore())
+    lm = LocalModel("llama-3-70b", "chat", "tp8-0", None, None, None,
+                    tags={"tp_comm": {"rccl": {1 << 20: 40.0}},
+                          "live": {"tp_comm_live": {"seq": 1, "us": {"rccl": 35.0, "peer": 12.0}}}})
+    st.registry.add(lm)
+
+    def count(path):
+        for mf in st.metrics.allreduce.collect():
+            for s in mf.samples:
+                if s.name.endswith("_count") and s.labels.get("group") == path:
+                    return s.value
+        return 0.0
+    st._maintenance()
+    assert count("rccl") == 2 and count("peer") == 1
+    st._maintenance()                                  # same samples: not re-observed
+    assert count("rccl") == 2
+    lm.tags["live"] = {"tp_comm_live": {"seq": 2, "us": {"rccl": 33.0}}}
+    st._maintenance()
+    assert count("rccl") == 3

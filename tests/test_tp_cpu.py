@@ -35,7 +35,7 @@ def _ecfg(model="tiny-llama"):
 def _rank_main(rank, size, port, ckpt, tag, q, sp_min_tokens=0, model="tiny-llama"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(size), LOCAL_RANK=str(rank),
-                      LMX_SP_MIN_TOKENS=str(sp_min_tokens))
+                      LMX_SP_MIN_TOKENS=str(sp_min_tokens), LMX_TP_PROBE_STEPS="3")
     torch.set_num_threads(2 if size <= 2 else 1)
     import torch.distributed as dist
 
@@ -50,7 +50,7 @@ def _rank_main(rank, size, port, ckpt, tag, q, sp_min_tokens=0, model="tiny-llam
                                                                max_tokens=5, seed=7,
                                                                ignore_eos=True))
             eng.release_followers()
-            q.put(("leader", greedy, sampled, eng.num_blocks))
+            q.put(("leader", greedy, sampled, eng.num_blocks, eng.tp_comm_live))
         else:
             q.put(("follower", eng.run_follower(), eng.num_blocks))
     finally:
@@ -128,8 +128,10 @@ def test_tp2_generation_matches_single_process(full_model, sp_min_tokens):
                 p.kill()
     leader = next(r for r in res if r[0] == "leader")
     follower = next(r for r in res if r[0] == "follower")
-    _, greedy, sampled, nb = leader
+    _, greedy, sampled, nb, live = leader
     assert follower[2] == nb                     # agreed KV page count
+    # in-service all-reduce samples every 3 steps, run collectively by both ranks
+    assert live.get("seq", 0) >= 1 and live["us"].get("rccl", 0) > 0, live
     assert follower[1] > 0                       # follower executed the steps
     for p, o in zip(PROMPTS, greedy):
         assert len(o) == 6
