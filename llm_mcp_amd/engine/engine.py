@@ -218,6 +218,7 @@ class LLMEngine:
         # live TP all-reduce samples every LMX_TP_PROBE_STEPS engine steps (0 = off)
         self._comm_every = int(os.environ.get("LMX_TP_PROBE_STEPS", "2000"))
         self.tp_comm_live: dict = {}
+        self._upload_ev = None
         self.Hq, self.Hkv, self.D = self.model.Hq, self.model.Hkv, self.model.D
         self.q_per_tile = ops.prefill_q_per_tile(self.Hq, self.Hkv)
         self._alloc_kv()
@@ -424,11 +425,10 @@ class LLMEngine:
             if msg.get("cmd") != "step":
                 return n
             plan, bucket = decode_plan(msg)
-            if self.device.type == "cuda":
-                # the pinned staging buffers are reused: the previous step's
-                # uploads must have been consumed (the leader waits for its
-                # tokens every step, so this costs the followers nothing)
-                torch.cuda.current_stream(self.device).synchronize()
+            if self._upload_ev is not None:
+                # the pinned staging buffers are reused: wait for the previous
+                # step's H2D copies only (not for its kernels)
+                self._upload_ev.synchronize()
             if bucket is not None:
                 self._run_graph(plan, bucket)
             else:
@@ -436,6 +436,14 @@ class LLMEngine:
             if msg.get("probe"):
                 self._comm_probe()
             n += 1
+
+    def _mark_upload(self):
+        """Event after this step's metadata H2D copies (TP followers reuse the
+        pinned staging buffers as soon as it has completed)."""
+        if self.device.type == "cuda" and self.chan is not None and not self.is_leader:
+            if self._upload_ev is None:
+                self._upload_ev = torch.cuda.Event()
+            self._upload_ev.record()
 
     def _comm_probe(self):
         """Live all-reduce sample of the TP group (collective: the leader
@@ -686,6 +694,7 @@ class LLMEngine:
             items += [("win", plan["pen_window"].reshape(N, PEN_WINDOW)),
                       ("ngen", plan["pen_ngen"]), ("pen", plan["pen_params"].reshape(N, 3))]
         d = self.packer.pack(items)
+        self._mark_upload()
         inp = StepInputs(d["ids"], d["pos"], d["slots"], plan["num_decode"], d["bt"], d["ctx"],
                          d["cu"], d["tiles"], d["rows"], T, S, decode_order=d.get("order"))
         ws = self.decode_ws
@@ -731,6 +740,7 @@ class LLMEngine:
             ph["pen"][:n] = plan["pen_params"].reshape(n, 3)
             self._pmeta.upload()
         self._gmeta.upload()
+        self._mark_upload()
         (self.pen_graphs if pen else self.graphs)[B]["graph"].replay()
         return g["tok"][:B], g["lp"][:B]
 
