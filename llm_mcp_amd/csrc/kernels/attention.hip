@@ -379,8 +379,12 @@ int paged_decode(const void* q, long q_stride, const void* k_cache, const void* 
 //  q:  [T_total][Hq][D] rows at q_stride (tokens of seq s start at cu_q[s])
 //  context_lens[s] = total keys of seq s (cached prefix + this chunk)
 //  causal: query i of the chunk sits at absolute position ctx - qlen + i.
-constexpr int PF_NG = 2;     // column groups per wave
 constexpr int PF_TK = 64;    // keys per LDS tile (two pages)
+// column groups per wave: 4 at D = 64 (twice the MFMA work per K/V byte read
+// from LDS; the registers fit at 2 waves / SIMD), 2 at D = 128.  Must match
+// ops.prefill_q_per_tile.
+template <int HD>
+constexpr int pf_groups() { return HD == 64 ? 4 : 2; }
 
 template <int HD>
 __device__ __forceinline__ int kswz(int r) {
@@ -412,7 +416,7 @@ __device__ __forceinline__ void pf_stage_page(bf16_t* k_lds, bf16_t* v_lds,
   }
 }
 
-template <int HD>
+template <int HD, int PF_NG = pf_groups<HD>()>
 __global__ void __launch_bounds__(256, 2) paged_prefill_kernel(
     const bf16_t* __restrict__ q, long q_stride, const bf16_t* __restrict__ k_cache,
     const bf16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,

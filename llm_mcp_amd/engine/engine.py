@@ -220,7 +220,7 @@ class LLMEngine:
         self.tp_comm_live: dict = {}
         self._upload_ev = None
         self.Hq, self.Hkv, self.D = self.model.Hq, self.model.Hkv, self.model.D
-        self.q_per_tile = ops.prefill_q_per_tile(self.Hq, self.Hkv)
+        self.q_per_tile = ops.prefill_q_per_tile(self.Hq, self.Hkv, self.D)
         self._alloc_kv()
         self.sched = _runtime.Scheduler(self.num_blocks, BLOCK_SIZE, ecfg.max_num_seqs,
                                         ecfg.max_batched_tokens, self.max_model_len,

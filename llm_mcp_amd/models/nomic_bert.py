@@ -101,7 +101,7 @@ class NomicBertModel:
         cu_h = np.concatenate([[0], np.cumsum(ln)])
         within = np.arange(T, dtype=np.int64) - np.repeat(cu_h[:-1], ln)
         slots = np.repeat(page_off[:-1] * PAGE, ln) + within
-        qpt = ops.prefill_q_per_tile(H, H)
+        qpt = ops.prefill_q_per_tile(H, H, D)
         nt = -(-ln // qpt)
         tile_seq = np.repeat(np.arange(S), nt)
         tile_q0 = (np.arange(int(nt.sum())) - np.repeat(np.concatenate([[0], np.cumsum(nt)])[:-1],

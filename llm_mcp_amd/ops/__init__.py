@@ -289,9 +289,11 @@ def paged_prefill_attention(q: torch.Tensor, k_cache, v_cache, block_tables, cu_
 PREFILL_GROUPS_PER_WAVE = 2   # PF_NG in csrc/kernels/attention.hip
 
 
-def prefill_q_per_tile(Hq: int, Hkv: int) -> int:
-    """Queries per prefill workgroup: 4 waves x PF_NG column groups x 16/G."""
-    return 4 * PREFILL_GROUPS_PER_WAVE * (16 // (Hq // Hkv))
+def prefill_q_per_tile(Hq: int, Hkv: int, D: int = 128) -> int:
+    """Queries per prefill workgroup: 4 waves x column groups x 16/G (column
+    groups per wave: 4 at head dim 64, 2 at 128 -- attention.hip
+    pf_groups)."""
+    return 4 * (4 if D == 64 else PREFILL_GROUPS_PER_WAVE) * (16 // (Hq // Hkv))
 
 
 # ---------------------------------------------------------------- sampling ---

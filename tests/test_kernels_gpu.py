@@ -142,7 +142,7 @@ def test_paged_prefill_varlen_with_prefix(Hq, Hkv, D):
                       device=DEV)
     T = int(cu[-1])
     q = _bf(T, (Hq + 2 * Hkv) * D)
-    qpt = ops.prefill_q_per_tile(Hq, Hkv)
+    qpt = ops.prefill_q_per_tile(Hq, Hkv, D)
     tiles = []
     for s, ql in enumerate(qlens):
         for q0 in range(0, ql, qpt):
@@ -335,7 +335,7 @@ def test_paged_prefill_long_multi_tile(Hq, Hkv, D):
                       device=DEV)
     T = int(cu[-1])
     q = _bf(T, (Hq + 2 * Hkv) * D)
-    qpt = ops.prefill_q_per_tile(Hq, Hkv)
+    qpt = ops.prefill_q_per_tile(Hq, Hkv, D)
     tiles = [v for s, ql in enumerate(qlens) for q0 in range(0, ql, qpt) for v in (s, q0)]
     tiles = torch.tensor(tiles, dtype=torch.int32, device=DEV)
     ctx = torch.tensor(ctxs, dtype=torch.int32, device=DEV)

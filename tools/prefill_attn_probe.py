@@ -1,0 +1,68 @@
+"""Paged prefill / encoder attention (K3) at the served shapes, TFLOP/s:
+nomic-embed-text (32 x 1024 tokens, 12 heads x 64, bidirectional),
+mxbai-embed-large (64 x 512, 16 x 64, bidirectional) and a Llama-3-8B
+prefill chunk (30 prompts x 546 tokens, 32 q / 8 kv x 128, causal).
+
+    python tools/prefill_attn_probe.py [--iters 20]
+"""
+import argparse
+import math
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from llm_mcp_amd import ops  # noqa: E402
+
+SHAPES = {"nomic": (32, 1024, 12, 12, 64, False), "mxbai": (64, 512, 16, 16, 64, False),
+          "llama8b": (30, 546, 32, 8, 128, True)}
+
+
+def run(name, S, L, Hq, Hkv, D, causal, iters, ng=0):
+    dev = torch.device("cuda", 0)
+    BS = 32
+    T = S * L
+    pages = -(-L // BS)
+    NB = S * pages
+    kc = torch.randn(NB, Hkv, BS, D, device=dev).to(torch.bfloat16)
+    vc = torch.randn(NB, Hkv, D, BS, device=dev).to(torch.bfloat16)
+    bt = torch.randperm(NB, device=dev).to(torch.int32).view(S, pages)
+    q = torch.randn(T, (Hq + 2 * Hkv) * D, device=dev).to(torch.bfloat16)
+    cu = torch.arange(0, T + 1, L, dtype=torch.int32, device=dev)
+    ctx = torch.full((S,), L, dtype=torch.int32, device=dev)
+    qpt = 4 * ng * (16 // (Hq // Hkv)) if ng else ops.prefill_q_per_tile(Hq, Hkv, D)
+    tiles = torch.tensor([v for s in range(S) for q0 in range(0, L, qpt) for v in (s, q0)],
+                         dtype=torch.int32, device=dev)
+    out = torch.empty(T, Hq * D, dtype=torch.bfloat16, device=dev)
+    scale = 1 / math.sqrt(D)
+
+    def call():
+        ops.paged_prefill_attention(q, kc, vc, bt, cu, ctx, tiles, scale, out, causal=causal,
+                                    Hq=Hq)
+    for _ in range(3):
+        call()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        call()
+    e.record()
+    torch.cuda.synchronize()
+    us = s.elapsed_time(e) / iters * 1e3
+    flops = 4.0 * S * L * L * D * Hq * (0.5 if causal else 1.0)
+    print(f"prefill attn {name:8s} {us:8.1f} us  {flops / us / 1e6:6.0f} TF/s", flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--ng", type=int, default=0,
+                    help="column groups per wave of the loaded build (A/B of an older .so)")
+    a = ap.parse_args()
+    for name, shp in SHAPES.items():
+        run(name, *shp, a.iters, a.ng)
+
+
+if __name__ == "__main__":
+    main()
