@@ -21,6 +21,7 @@
 //   prefill (K3): columns = (16/G queries) x (G heads): the K/V page read is
 //                 shared by all heads of the kv group; each wave walks its own
 //                 causal key range; varlen batches via a host-built tile list.
+#include <algorithm>
 #include <climits>
 
 #include "common.h"
@@ -184,25 +185,27 @@ __device__ __forceinline__ int effective_part(int ctx, int part_tokens, int max_
   return need > part_tokens ? need : part_tokens;
 }
 
-// grid (max_parts, Hkv, B), block 256.
+// One (partition, kv head, sequence) segment of the decode attention, by one
+// 256-thread workgroup.
 // MODE 0: one page at a time (load, then compute); MODE 1: the next page's
 // block id and K/V fragments are loaded before the current page is computed
 // (two pages in flight per wave); MODE 2: loads only (diagnostic ceiling);
 // MODE 3: loads only, every instruction one contiguous 1 KB (diagnostic).
+template <int HD>
+struct DecodeSmem {
+  float ml[4][16][2];
+  float o[4][16][HD + 4];
+};
+
 template <int HD, int MODE>
-__global__ void __launch_bounds__(256) paged_decode_kernel(
-    const bf16_t* __restrict__ q, long q_stride, const bf16_t* __restrict__ k_cache,
-    const bf16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
-    const int* __restrict__ context_lens, const int* __restrict__ order,
-    bf16_t* __restrict__ out, long out_stride,
-    float* __restrict__ part_o, float* __restrict__ part_ml, int Hq, int Hkv, float scale,
-    int part_tokens, int max_parts) {
-  __shared__ float sm_ml[4][16][2];
-  __shared__ float sm_o[4][16][HD + 4];
-  // order (optional): sequence of each grid z-slice, longest context first,
-  // so the workgroups dispatched last are the short ones (the batch's last
-  // round of workgroups ends together; profiles/r2_decode_attention.md)
-  const int p = blockIdx.x, kvh = blockIdx.y, b = order ? order[blockIdx.z] : blockIdx.z;
+__device__ __forceinline__ void decode_segment(
+    DecodeSmem<HD>& sm, int p, int kvh, int b, const bf16_t* __restrict__ q, long q_stride,
+    const bf16_t* __restrict__ k_cache, const bf16_t* __restrict__ v_cache,
+    const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ context_lens,
+    bf16_t* __restrict__ out, long out_stride, float* __restrict__ part_o,
+    float* __restrict__ part_ml, int Hq, int Hkv, float scale, int part_tokens, int max_parts) {
+  float (&sm_ml)[4][16][2] = sm.ml;
+  float (&sm_o)[4][16][HD + 4] = sm.o;
   const int ctx = context_lens[b];
   part_tokens = effective_part(ctx, part_tokens, max_parts);
   const int nparts = (ctx + part_tokens - 1) / part_tokens;
@@ -303,6 +306,48 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
   }
 }
 
+
+// grid (max_parts, Hkv, B), block 256: one workgroup per segment.  order
+// (optional): sequence of each grid z-slice, longest context first, so the
+// workgroups dispatched last are the short ones (profiles/r2_decode_attention.md)
+template <int HD, int MODE>
+__global__ void __launch_bounds__(256) paged_decode_kernel(
+    const bf16_t* __restrict__ q, long q_stride, const bf16_t* __restrict__ k_cache,
+    const bf16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
+    const int* __restrict__ context_lens, const int* __restrict__ order,
+    bf16_t* __restrict__ out, long out_stride,
+    float* __restrict__ part_o, float* __restrict__ part_ml, int Hq, int Hkv, float scale,
+    int part_tokens, int max_parts) {
+  __shared__ DecodeSmem<HD> sm;
+  decode_segment<HD, MODE>(sm, blockIdx.x, blockIdx.y, order ? order[blockIdx.z] : blockIdx.z, q,
+                           q_stride, k_cache, v_cache, block_tables, bt_stride, context_lens,
+                           out, out_stride, part_o, part_ml, Hq, Hkv, scale, part_tokens,
+                           max_parts);
+}
+
+// Persistent form (one partition per sequence): a fixed grid of about the
+// resident workgroup count walks the (sequence, kv head) segments in
+// longest-first order with a grid stride, so no workgroup launches ragged
+// rounds behind the first and the per-workgroup start-up is paid once per
+// resident slot.
+template <int HD>
+__global__ void __launch_bounds__(256, 3) paged_decode_persist_kernel(
+    const bf16_t* __restrict__ q, long q_stride, const bf16_t* __restrict__ k_cache,
+    const bf16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
+    const int* __restrict__ context_lens, const int* __restrict__ order,
+    bf16_t* __restrict__ out, long out_stride, int B, int Hq, int Hkv, float scale,
+    int part_tokens) {
+  __shared__ DecodeSmem<HD> sm;
+  const int nseg = B * Hkv;
+  for (int seg = blockIdx.x; seg < nseg; seg += gridDim.x) {
+    const int r = seg / Hkv, kvh = seg - r * Hkv;
+    decode_segment<HD, 0>(sm, 0, kvh, order ? order[r] : r, q, q_stride, k_cache, v_cache,
+                          block_tables, bt_stride, context_lens, out, out_stride, nullptr,
+                          nullptr, Hq, Hkv, scale, part_tokens, 1);
+    __syncthreads();            // the segment's LDS combine is read before the next reuses it
+  }
+}
+
 // grid (Hq, B), block HD (one thread per d)
 template <int HD>
 __global__ void __launch_bounds__(128) paged_decode_reduce_kernel(
@@ -326,8 +371,25 @@ __global__ void __launch_bounds__(128) paged_decode_reduce_kernel(
   out[(long)b * out_stride + (long)head * HD + d] = f2bf(O / L);
 }
 
+// loop form (probe / A-B knob): 0 default -- the persistent grid when every
+// sequence is one partition, else one workgroup per segment; 1 pipelined
+// pages; 2, 3 load-only diagnostics; 4 one workgroup per segment always
 static int g_decode_mode = 0;
 void set_decode_mode(int mode) { g_decode_mode = mode; }
+
+// resident 256-thread decode workgroups: 3 per CU (168 VGPRs incl. AGPRs)
+static int decode_resident_wgs() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+    n = 3 * cus;
+  }
+  return n;
+}
 
 int paged_decode(const void* q, long q_stride, const void* k_cache, const void* v_cache,
                  const int* block_tables, int bt_stride, const int* context_lens,
@@ -345,8 +407,14 @@ int paged_decode(const void* q, long q_stride, const void* k_cache, const void* 
       (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, \
       bt_stride, context_lens, order, (bf16_t*)out, out_stride, part_o, part_ml, Hq, Hkv,     \
       scale, part_tokens, max_parts);
+#define LMX_DEC_P(HDV)                                                                        \
+  paged_decode_persist_kernel<HDV><<<dim3(std::min(B * Hkv, decode_resident_wgs())), dim3(256), \
+                                      0, stream>>>(                                           \
+      (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, \
+      bt_stride, context_lens, order, (bf16_t*)out, out_stride, B, Hq, Hkv, scale, part_tokens);
 #define LMX_DEC(HDV)                                                                          \
-  if (g_decode_mode == 1) { LMX_DEC_K(HDV, 1) }                                               \
+  if (g_decode_mode == 0 && max_parts == 1) { LMX_DEC_P(HDV) }                                \
+  else if (g_decode_mode == 1) { LMX_DEC_K(HDV, 1) }                                          \
   else if (g_decode_mode == 2) { LMX_DEC_K(HDV, 2) }                                          \
   else if (g_decode_mode == 3) { LMX_DEC_K(HDV, 3) }                                          \
   else { LMX_DEC_K(HDV, 0) }                                                                  \
@@ -356,6 +424,7 @@ int paged_decode(const void* q, long q_stride, const void* k_cache, const void* 
   if (D == 128) { LMX_DEC(128) } else { LMX_DEC(64) }
 #undef LMX_DEC
 #undef LMX_DEC_K
+#undef LMX_DEC_P
   return (int)hipGetLastError();
 }
 

@@ -302,9 +302,21 @@ class LLMEngine:
         return [b for b in base if b <= self.ecfg.max_num_seqs]
 
     def _graph_parts(self, B: int) -> int:
-        # enough split-K partitions to fill the chip for small batches; the
-        # kernel grows the partition length when a context needs more
-        return max(1, min(self.max_parts, 2048 // max(1, B * self.Hkv)))
+        """Split-K partitions of the decode attention for B rows: one as soon
+        as the batch has a workgroup per CU (B x Hkv >= 256); a split adds
+        the partial write, the reduce launch and per-workgroup start-up and
+        measured 20-27 % slower at 32-128 rows, context ~660
+        (profiles/r2_decode_attention.md).  Smaller batches split to fill the
+        chip; the kernel grows the partition length when a context needs
+        more."""
+        return max(1, min(self.max_parts, -(-256 // max(1, B * self.Hkv))))
+
+    def _decode_ws(self, B: int):
+        """The decode workspace seen by a B-row step (max_parts = policy)."""
+        ws = ops.DecodeWorkspace.__new__(ops.DecodeWorkspace)
+        ws.max_parts, ws.part_o, ws.part_ml = (self._graph_parts(B), self.decode_ws.part_o,
+                                               self.decode_ws.part_ml)
+        return ws
 
     def _capture_graphs(self):
         t0 = time.time()
@@ -356,9 +368,7 @@ class LLMEngine:
         inp = StepInputs(g["ids"][:B], g["pos"][:B], g["slots"][:B], B, g["bt"][:B],
                          g["ctx"][:B], g["cu"][:B + 1], g["tiles"], g["rows"][:B], B, B,
                          decode_order=g["order"][:B])
-        parts = self._graph_parts(B)
-        ws = ops.DecodeWorkspace.__new__(ops.DecodeWorkspace)
-        ws.max_parts, ws.part_o, ws.part_ml = parts, self.decode_ws.part_o, self.decode_ws.part_ml
+        ws = self._decode_ws(B)
 
         def run():
             logits = self.model.forward(inp, self.k_caches, self.v_caches, ws,
@@ -380,7 +390,7 @@ class LLMEngine:
         with torch.cuda.graph(graph, pool=self._gpool, stream=stream):
             run()
         self._gpool = graph.pool()
-        return {"graph": graph, "parts": parts}
+        return {"graph": graph, "parts": ws.max_parts}
 
     # --------------------------------------------------------- public API ---
     def submit(self, req: GenRequest) -> GenRequest:
@@ -697,7 +707,7 @@ class LLMEngine:
         self._mark_upload()
         inp = StepInputs(d["ids"], d["pos"], d["slots"], plan["num_decode"], d["bt"], d["ctx"],
                          d["cu"], d["tiles"], d["rows"], T, S, decode_order=d.get("order"))
-        ws = self.decode_ws
+        ws = self._decode_ws(plan["num_decode"]) if plan["num_decode"] else self.decode_ws
         logits = self.model.forward(inp, self.k_caches, self.v_caches, ws, self.ecfg.part_tokens)
         if not self.is_leader:
             return None, None

@@ -164,8 +164,10 @@ def test_paged_prefill_varlen_with_prefix(Hq, Hkv, D):
 
 @pytest.mark.gpu
 def test_paged_decode_dispatch_order_and_loop_modes():
-    """The longest-first dispatch order (ops.decode_order) and the pipelined
-    loop form (mode 1) give bitwise the row-order result."""
+    """The persistent grid (default, one partition per sequence), the
+    longest-first order (ops.decode_order), the pipelined loop form (mode 1)
+    and the one-workgroup-per-segment grid (mode 4) give bitwise the same
+    result."""
     Hq, Hkv, D = 32, 8, 128
     ctxs = [535, 791, 1, 640, 33, 700, 64, 600] * 4
     B = len(ctxs)
@@ -182,12 +184,13 @@ def test_paged_decode_dispatch_order_and_loop_modes():
     got = torch.empty_like(base)
     ops.paged_decode_attention(q, kc, vc, bt, ctx, scale, got, Hq=Hq, order=order)
     assert torch.equal(got, base)
-    try:
-        ops.native().set_decode_mode(1)
-        ops.paged_decode_attention(q, kc, vc, bt, ctx, scale, got, Hq=Hq, order=order)
-    finally:
-        ops.native().set_decode_mode(0)
-    assert torch.equal(got, base)
+    for mode in (1, 4):       # pipelined pages; one workgroup per segment (not persistent)
+        try:
+            ops.native().set_decode_mode(mode)
+            ops.paged_decode_attention(q, kc, vc, bt, ctx, scale, got, Hq=Hq, order=order)
+        finally:
+            ops.native().set_decode_mode(0)
+        assert torch.equal(got, base), mode
     expect = ref.paged_decode(q[:, :Hq * D].reshape(B, Hq, D), kc, vc, bt, ctx, scale)
     torch.testing.assert_close(base.float().view(B, Hq, D), expect.float(), atol=2e-2, rtol=2e-2)
 

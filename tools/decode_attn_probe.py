@@ -21,6 +21,8 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--ctx-lo", type=int, default=535)
     ap.add_argument("--ctx-hi", type=int, default=791)
+    ap.add_argument("--parts", type=int, default=1, help="split-K partitions per sequence")
+    ap.add_argument("--part-tokens", type=int, default=256)
     ap.add_argument("--order", choices=("random", "desc", "asc"), default="random",
                     help="sequence order = workgroup dispatch order (longest-first test)")
     a = ap.parse_args()
@@ -32,33 +34,43 @@ def main():
         ctx = ctx.sort(descending=a.order == "desc").values
     maxb = (a.ctx_hi + BS - 1) // BS
     nb = 20000                                  # 20000 pages x 64 KB x 2 = 2.6 GB (> MALL)
-    perm = torch.randperm(nb)[:B * maxb].view(B, maxb).to(torch.int32)
     k_cache = (torch.randn(nb, Hkv, BS, D, device=dev) * 0.5).to(torch.bfloat16)
     v_cache = torch.randn(nb, Hkv, D, BS, device=dev).to(torch.bfloat16)
     q = torch.randn(B, Hq * D, device=dev).to(torch.bfloat16)
-    bt, cl = perm.to(dev), ctx.to(dev)
+    cl = ctx.to(dev)
+    # page tables rotated per call over disjoint page sets: a call's K/V were
+    # last read >= 640 MB of other pages ago, so they come from HBM (as in a
+    # decode step, where the whole model streams between two calls of a layer)
+    nrot = max(1, min(8, nb // (B * maxb)))
+    tables = [p.view(B, maxb).to(dev) for p in
+              torch.randperm(nb)[:nrot * B * maxb].to(torch.int32).chunk(nrot)]
+    bt = tables[0]
     out = torch.empty(B, Hq * D, device=dev, dtype=torch.bfloat16)
     kv_bytes = int(ctx.sum()) * Hkv * D * 2 * 2
+    ws = ops.DecodeWorkspace(B, Hq, D, a.parts, dev) if a.parts > 1 else None
+    order = torch.from_numpy(ops.decode_order(ctx.numpy())).to(dev)
     scale = D ** -0.5
     ref = None
     nat = ops.native()
-    for mode in (0, 1, 2, 3, 0, 1, 2, 3):
+    for mode in (4, 0, 4, 0):
         nat.set_decode_mode(mode)
-        ops.paged_decode_attention(q, k_cache, v_cache, bt, cl, scale, out)
+        ops.paged_decode_attention(q, k_cache, v_cache, bt, cl, scale, out, ws, a.part_tokens,
+                                   order=order)
         torch.cuda.synchronize()
-        if mode == 0 and ref is None:
+        if mode == 4 and ref is None:
             ref = out.clone()
-        same = "-" if mode >= 2 else ("bitwise" if torch.equal(out, ref) else
+        same = "-" if mode in (2, 3) else ("bitwise" if torch.equal(out, ref) else
                                       f"max diff {(out.float() - ref.float()).abs().max():.3g}")
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
-        for _ in range(a.iters):
-            ops.paged_decode_attention(q, k_cache, v_cache, bt, cl, scale, out)
+        for i in range(a.iters):
+            ops.paged_decode_attention(q, k_cache, v_cache, tables[i % nrot], cl, scale, out, ws,
+                                       a.part_tokens, order=order)
         e.record()
         torch.cuda.synchronize()
         us = s.elapsed_time(e) / a.iters * 1e3
-        print(f"decode attn B={B} {a.order} mode {mode}: {us:7.1f} us  {kv_bytes / us / 1e6:5.2f} TB/s  "
-              f"vs mode 0: {same}", flush=True)
+        print(f"decode attn B={B} parts {a.parts}x{a.part_tokens} {a.order} mode {mode}: {us:7.1f} us  {kv_bytes / us / 1e6:5.2f} TB/s  "
+              f"vs grid (mode 4): {same}", flush=True)
     nat.set_decode_mode(0)
 
 
