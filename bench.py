@@ -254,7 +254,9 @@ def main() -> None:
     log("engine host phases (ms/step avg over all steps): " + ", ".join(
         f"{k[2:]} {st[k] / ns * 1e3:.3f}" for k in st if k.startswith("t_")) +
         f"; steps {st['steps']} graph {st['graph_steps']}, decode step "
-        f"{st['decode_step_s'] / max(1, st['graph_steps']) * 1e3:.2f} ms")
+        f"{st['decode_step_s'] / max(1, st['graph_steps']) * 1e3:.2f} ms (host: " + ", ".join(
+            f"{k[2:]} {st[k] / max(1, st['graph_steps']) * 1e3:.3f}" for k in st
+            if k.startswith("g_")) + ")")
     mine = {"rank": rank, "elapsed": elapsed, "gen_tokens": int(st["generated_tokens"]),
             "finished": int(st["finished"]), "steps": int(st["steps"]),
             "graph_steps": int(st["graph_steps"]),

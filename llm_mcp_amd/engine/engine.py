@@ -246,7 +246,9 @@ class LLMEngine:
         self.stats = {"steps": 0, "decode_steps": 0, "graph_steps": 0, "prefill_tokens": 0,
                       "generated_tokens": 0, "step_time_s": 0.0, "finished": 0,
                       "t_schedule": 0.0, "t_launch": 0.0, "t_events": 0.0, "t_wait": 0.0,
-                      "t_update": 0.0, "t_gpu": 0.0, "decode_step_s": 0.0}
+                      "t_update": 0.0, "t_gpu": 0.0, "decode_step_s": 0.0,
+                      "g_schedule": 0.0, "g_launch": 0.0, "g_update": 0.0, "g_upload": 0.0,
+                      "g_replay": 0.0}
         self._pending = None
         self._fetch_cpu = None
         # (arrival, first token) wall times of recent requests: engine-side TTFT
@@ -628,6 +630,11 @@ class LLMEngine:
         st["graph_steps"] += int(bucket is not None)
         if bucket is not None:
             st["decode_step_s"] += t5 - t0
+            # host phases of graph (pure decode) steps alone: schedule,
+            # launch (metadata + upload + replay), update
+            st["g_schedule"] += t1 - t0
+            st["g_launch"] += t2 - t1
+            st["g_update"] += t5 - t4
         st["prefill_tokens"] += plan["num_prefill_tokens"]
         st["generated_tokens"] += N
         return True
@@ -749,9 +756,14 @@ class LLMEngine:
             ph["ngen"][:n] = plan["pen_ngen"]
             ph["pen"][:n] = plan["pen_params"].reshape(n, 3)
             self._pmeta.upload()
+        ta = time.perf_counter()
         self._gmeta.upload()
         self._mark_upload()
+        tb = time.perf_counter()
         (self.pen_graphs if pen else self.graphs)[B]["graph"].replay()
+        st = self.stats
+        st["g_upload"] += tb - ta
+        st["g_replay"] += time.perf_counter() - tb
         return g["tok"][:B], g["lp"][:B]
 
     def _start_fetch(self, tok: torch.Tensor, lp: torch.Tensor, n: int):
