@@ -683,16 +683,21 @@ def encoder_choice(N: int, K: int) -> int | None:
 
 
 def encoder_backend(N: int, K: int) -> tuple[str, int | None]:
-    """Fastest measured backend for a PLAIN encoder GEMM of this (N, K):
-    ("k11", cfg), ("lib", None) -- hipBLASLt, the library is kept for plain
-    GEMMs it wins -- or ("gemm_nt", None).  Unmeasured shapes: gemm_nt."""
+    """Backend of a PLAIN encoder GEMM of this (N, K): the faster measured
+    backend among the hand-written kernels, ("k11", cfg) or ("gemm_nt", None),
+    and hipBLASLt (("lib", None), a plain GEMM where the library was measured
+    faster).  LMX_ENCODER_LIBRARY=0 keeps every projection on the
+    hand-written kernels (profiles/r2_config5_and_embeddings.md has both
+    numbers: mxbai 2,123 vs 1,615 emb/s, nomic 2,457 vs 2,308).
+    Unmeasured shapes: gemm_nt."""
+    import os
     e = _enc_table().get((N, K))
     if e is None:
         return ("gemm_nt", None)
     cands = [(e["tflops"], "k11")]
     if e.get("gemm_nt_tflops") is not None:
         cands.append((e["gemm_nt_tflops"], "gemm_nt"))
-    if e.get("lib_tflops") is not None:
+    if e.get("lib_tflops") is not None and os.environ.get("LMX_ENCODER_LIBRARY", "1") == "1":
         cands.append((e["lib_tflops"], "lib"))
     best = max(cands)[1]
     return (best, int(e["cfg"]) if best == "k11" else None)
