@@ -257,7 +257,12 @@ def main() -> None:
         f"{st['decode_step_s'] / max(1, st['graph_steps']) * 1e3:.2f} ms (host: " + ", ".join(
             f"{k[2:]} {st[k] / max(1, st['graph_steps']) * 1e3:.3f}" for k in st
             if k.startswith("g_")) + ")")
+    # engine-side TTFT: request arrival at the engine -> first token handed to
+    # the IPC link (the client-side figure adds the front door and SSE path)
+    e_ttft = sorted(now - arr for arr, now in list(engine.ttft_samples))
+    e_ttft_p50 = e_ttft[len(e_ttft) // 2] * 1e3 if e_ttft else None
     mine = {"rank": rank, "elapsed": elapsed, "gen_tokens": int(st["generated_tokens"]),
+            "engine_ttft_p50_ms": e_ttft_p50,
             "finished": int(st["finished"]), "steps": int(st["steps"]),
             "graph_steps": int(st["graph_steps"]),
             "decode_ms": st["decode_step_s"] / max(1, st["graph_steps"]) * 1e3,
@@ -294,6 +299,8 @@ def main() -> None:
             "per_gpu_tok_s": per_gpu,
             "gpu_balance_max_over_min": round(max(nz) / min(nz), 3) if nz else None,
             "decode_step_ms": [round(x["decode_ms"], 2) for x in allr],
+            "engine_ttft_p50_ms": [None if x["engine_ttft_p50_ms"] is None else
+                                   round(x["engine_ttft_p50_ms"], 1) for x in allr],
             "front_door_cpu_pct": round(cpu.get("api", 0.0), 1),
             "loadgen_cpu_pct": round(cpu.get("loadgen", 0.0), 1),
             "engine_cpu_pct": [round(x["engine_cpu_pct"], 1) for x in allr],

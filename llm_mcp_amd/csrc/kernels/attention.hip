@@ -50,7 +50,26 @@ __device__ __forceinline__ void state_init(PageState<HD>& st) {
 //  key_lo/key_hi: absolute key positions of this page; a key is visible to the
 //  lane's column iff key_pos <= lim (lim = causal limit of the column, already
 //  clipped to ctx-1).
-template <int HD>
+// K/V page loads; NTL: non-temporal (the decode step reads each page once per
+// layer, with the whole model streamed between two reads of it)
+template <bool NTL>
+__device__ __forceinline__ bf16x8_t kv_frag16B(const bf16_t* p) {
+  if constexpr (NTL) return __builtin_nontemporal_load(reinterpret_cast<const bf16x8_t*>(p));
+  else return load_frag16B(p);
+}
+
+template <bool NTL>
+__device__ __forceinline__ bf16x8_t kv_frag_2x8B(const bf16_t* p0, const bf16_t* p1) {
+  if constexpr (NTL) {
+    const bf16x4_t a = __builtin_nontemporal_load(reinterpret_cast<const bf16x4_t*>(p0));
+    const bf16x4_t b = __builtin_nontemporal_load(reinterpret_cast<const bf16x4_t*>(p1));
+    return bf16x8_t{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  } else {
+    return load_frag_2x8B(p0, p1);
+  }
+}
+
+template <int HD, bool NTL = false>
 __device__ __forceinline__ void process_page(PageState<HD>& st, const bf16x8_t (&qf)[HD / 32],
                                              const bf16_t* __restrict__ kpage,
                                              const bf16_t* __restrict__ vpage, int page_pos0,
@@ -61,15 +80,15 @@ __device__ __forceinline__ void process_page(PageState<HD>& st, const bf16x8_t (
   bf16x8_t ka[KS], kb[KS];
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
-    ka[s] = load_frag16B(kpage + c * HD + 32 * s + 8 * g);
-    kb[s] = load_frag16B(kpage + (16 + c) * HD + 32 * s + 8 * g);
+    ka[s] = kv_frag16B<NTL>(kpage + c * HD + 32 * s + 8 * g);
+    kb[s] = kv_frag16B<NTL>(kpage + (16 + c) * HD + 32 * s + 8 * g);
   }
   // V^T fragments (issued early so they overlap the QK MFMAs and softmax)
   bf16x8_t vf[NT];
 #pragma unroll
   for (int i = 0; i < NT; ++i) {
     const bf16_t* vr = vpage + (16 * i + c) * BS;
-    vf[i] = load_frag_2x8B(vr + 4 * g, vr + 16 + 4 * g);
+    vf[i] = kv_frag_2x8B<NTL>(vr + 4 * g, vr + 16 + 4 * g);
   }
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
@@ -176,6 +195,86 @@ __device__ __forceinline__ void compute_page(PageState<HD>& st, const bf16x8_t (
 }
 
 // ---------------------------------------------------------------- decode ----
+// Optional fused K2 + K5 for decode rows (cos_sin == nullptr: off).  The row's
+// q / k / v are the unrotated QKV projection output (q at the row start, k at
+// Hq*HD, v at (Hq+Hkv)*HD); positions[b] is the token's rotary position,
+// slots[b] its cache slot (-1: padding row, nothing written).
+struct RopeIn {
+  const int* positions;
+  const float* cos_sin;   // [max_pos][HD]: cos | sin (rope_cache.hip)
+  const int* slots;
+};
+
+// q fragments of one lane (column c = head, 8 elements per s-block at
+// 32s + 8g) rotated in registers: element e < HD/2 pairs with e + HD/2, which
+// sits in block s + KS/2 of the same lane.  Same fp32 expression and bf16
+// rounding as rope_cache_kernel.
+template <int HD>
+__device__ __forceinline__ void rope_q_frags(bf16x8_t (&qf)[HD / 32], const float* __restrict__ cs,
+                                             int g) {
+  constexpr int KS = HD / 32, half = HD / 2;
+#pragma unroll
+  for (int s = 0; s < KS / 2; ++s) {
+    const int e = 32 * s + 8 * g;
+    const float4 c0 = *reinterpret_cast<const float4*>(cs + e);
+    const float4 c1 = *reinterpret_cast<const float4*>(cs + e + 4);
+    const float4 s0 = *reinterpret_cast<const float4*>(cs + half + e);
+    const float4 s1 = *reinterpret_cast<const float4*>(cs + half + e + 4);
+    const float cc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+    const float ss[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float a = bf2f((uint16_t)qf[s][j]), b = bf2f((uint16_t)qf[s + KS / 2][j]);
+      qf[s][j] = (short)f2bf(a * cc[j] - b * ss[j]);
+      qf[s + KS / 2][j] = (short)f2bf(b * cc[j] + a * ss[j]);
+    }
+  }
+}
+
+// The new token's k (rotated) and v of kv head kvh into its cache slot:
+// threads [0, HD/8) rotate 4 pairs of k each, threads [64, 64 + HD/4) move 4
+// v elements each into the d-major page.  Ends with the stores retired and a
+// workgroup barrier, so every wave's page loads that follow see them.
+template <int HD>
+__device__ __forceinline__ void rope_write_kv(const bf16_t* __restrict__ krow,
+                                              const bf16_t* __restrict__ vrow,
+                                              const float* __restrict__ cs, int slot, int kvh,
+                                              int Hkv, bf16_t* __restrict__ k_cache,
+                                              bf16_t* __restrict__ v_cache) {
+  constexpr int half = HD / 2;
+  const int t = threadIdx.x;
+  if (slot >= 0) {
+    const long blk = slot / BS, off = slot % BS;
+    if (t < HD / 8) {
+      const int i = 4 * t;
+      const bf16x4_t x1 = *reinterpret_cast<const bf16x4_t*>(krow + i);
+      const bf16x4_t x2 = *reinterpret_cast<const bf16x4_t*>(krow + half + i);
+      const float4 c = *reinterpret_cast<const float4*>(cs + i);
+      const float4 sn = *reinterpret_cast<const float4*>(cs + half + i);
+      const float cc[4] = {c.x, c.y, c.z, c.w}, ss[4] = {sn.x, sn.y, sn.z, sn.w};
+      bf16x4_t o1, o2;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float a = bf2f((uint16_t)x1[j]), b = bf2f((uint16_t)x2[j]);
+        o1[j] = (short)f2bf(a * cc[j] - b * ss[j]);
+        o2[j] = (short)f2bf(b * cc[j] + a * ss[j]);
+      }
+      bf16_t* kp = k_cache + ((blk * Hkv + kvh) * BS + off) * HD;
+      *reinterpret_cast<bf16x4_t*>(kp + i) = o1;
+      *reinterpret_cast<bf16x4_t*>(kp + half + i) = o2;
+    } else if (t >= 64 && t < 64 + HD / 4) {
+      const int d = 4 * (t - 64);
+      const bf16x4_t v = *reinterpret_cast<const bf16x4_t*>(vrow + d);
+      bf16_t* vp = v_cache + ((blk * Hkv + kvh) * HD + d) * BS + off;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) vp[(long)j * BS] = (bf16_t)v[j];
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __threadfence_block();
+  __syncthreads();
+}
+
 // Partition length used for a sequence: the requested split-K granule, grown
 // (in 128-token steps) when the context would need more than max_parts
 // partitions, so the grid baked into a captured graph always covers it.
@@ -190,7 +289,8 @@ __device__ __forceinline__ int effective_part(int ctx, int part_tokens, int max_
 // MODE 0: one page at a time (load, then compute); MODE 1: the next page's
 // block id and K/V fragments are loaded before the current page is computed
 // (two pages in flight per wave); MODE 2: loads only (diagnostic ceiling);
-// MODE 3: loads only, every instruction one contiguous 1 KB (diagnostic).
+// MODE 3: loads only, every instruction one contiguous 1 KB (diagnostic);
+// MODE 5: MODE 0 with non-temporal K/V loads.
 template <int HD>
 struct DecodeSmem {
   float ml[4][16][2];
@@ -203,7 +303,8 @@ __device__ __forceinline__ void decode_segment(
     const bf16_t* __restrict__ k_cache, const bf16_t* __restrict__ v_cache,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ context_lens,
     bf16_t* __restrict__ out, long out_stride, float* __restrict__ part_o,
-    float* __restrict__ part_ml, int Hq, int Hkv, float scale, int part_tokens, int max_parts) {
+    float* __restrict__ part_ml, int Hq, int Hkv, float scale, int part_tokens, int max_parts,
+    const RopeIn rp) {
   float (&sm_ml)[4][16][2] = sm.ml;
   float (&sm_o)[4][16][HD + 4] = sm.o;
   const int ctx = context_lens[b];
@@ -219,18 +320,27 @@ __device__ __forceinline__ void decode_segment(
 #pragma unroll
   for (int s = 0; s < HD / 32; ++s)
     qf[s] = (c < G) ? load_frag16B(qrow + 32 * s + 8 * g) : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+  if (rp.cos_sin) {   // fused rotary + cache write of this step's token
+    const float* cs = rp.cos_sin + (long)rp.positions[b] * HD;
+    rope_q_frags<HD>(qf, cs, g);
+    if (p == nparts - 1) {   // the partition holding position ctx-1 reads the new k / v
+      const bf16_t* krow = q + (long)b * q_stride + (long)(Hq + kvh) * HD;
+      rope_write_kv<HD>(krow, krow + (long)Hkv * HD, cs, rp.slots[b], kvh, Hkv,
+                        const_cast<bf16_t*>(k_cache), const_cast<bf16_t*>(v_cache));
+    }
+  }
 
   PageState<HD> st;
   state_init(st);
   const float scale_log2 = scale * LOG2E;
   const int pg0 = t0 / BS, pg1 = (t1 + BS - 1) / BS;
   const int* bt = block_tables + (long)b * bt_stride;
-  if constexpr (MODE == 0) {
+  if constexpr (MODE == 0 || MODE == 5) {
     for (int pg = pg0 + wave; pg < pg1; pg += 4) {
       const long blk = bt[pg];
       const bf16_t* kp = k_cache + (blk * Hkv + kvh) * (BS * HD);
       const bf16_t* vp = v_cache + (blk * Hkv + kvh) * (BS * HD);
-      process_page(st, qf, kp, vp, pg * BS, t1 - 1, scale_log2);
+      process_page<HD, MODE == 5>(st, qf, kp, vp, pg * BS, t1 - 1, scale_log2);
     }
   } else {
     int pg = pg0 + wave;
@@ -317,12 +427,12 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
     const int* __restrict__ context_lens, const int* __restrict__ order,
     bf16_t* __restrict__ out, long out_stride,
     float* __restrict__ part_o, float* __restrict__ part_ml, int Hq, int Hkv, float scale,
-    int part_tokens, int max_parts) {
+    int part_tokens, int max_parts, RopeIn rp) {
   __shared__ DecodeSmem<HD> sm;
   decode_segment<HD, MODE>(sm, blockIdx.x, blockIdx.y, order ? order[blockIdx.z] : blockIdx.z, q,
                            q_stride, k_cache, v_cache, block_tables, bt_stride, context_lens,
                            out, out_stride, part_o, part_ml, Hq, Hkv, scale, part_tokens,
-                           max_parts);
+                           max_parts, rp);
 }
 
 // Persistent form (one partition per sequence): a fixed grid of about the
@@ -330,20 +440,20 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
 // longest-first order with a grid stride, so no workgroup launches ragged
 // rounds behind the first and the per-workgroup start-up is paid once per
 // resident slot.
-template <int HD>
+template <int HD, int MODE>
 __global__ void __launch_bounds__(256, 3) paged_decode_persist_kernel(
     const bf16_t* __restrict__ q, long q_stride, const bf16_t* __restrict__ k_cache,
     const bf16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ context_lens, const int* __restrict__ order,
     bf16_t* __restrict__ out, long out_stride, int B, int Hq, int Hkv, float scale,
-    int part_tokens) {
+    int part_tokens, RopeIn rp) {
   __shared__ DecodeSmem<HD> sm;
   const int nseg = B * Hkv;
   for (int seg = blockIdx.x; seg < nseg; seg += gridDim.x) {
     const int r = seg / Hkv, kvh = seg - r * Hkv;
-    decode_segment<HD, 0>(sm, 0, kvh, order ? order[r] : r, q, q_stride, k_cache, v_cache,
+    decode_segment<HD, MODE>(sm, 0, kvh, order ? order[r] : r, q, q_stride, k_cache, v_cache,
                           block_tables, bt_stride, context_lens, out, out_stride, nullptr,
-                          nullptr, Hq, Hkv, scale, part_tokens, 1);
+                          nullptr, Hq, Hkv, scale, part_tokens, 1, rp);
     __syncthreads();            // the segment's LDS combine is read before the next reuses it
   }
 }
@@ -373,7 +483,8 @@ __global__ void __launch_bounds__(128) paged_decode_reduce_kernel(
 
 // loop form (probe / A-B knob): 0 default -- the persistent grid when every
 // sequence is one partition, else one workgroup per segment; 1 pipelined
-// pages; 2, 3 load-only diagnostics; 4 one workgroup per segment always
+// pages; 2, 3 load-only diagnostics; 4 one workgroup per segment always; 5 the
+// default forms with non-temporal K/V loads
 static int g_decode_mode = 0;
 void set_decode_mode(int mode) { g_decode_mode = mode; }
 
@@ -396,8 +507,11 @@ int paged_decode(const void* q, long q_stride, const void* k_cache, const void* 
                  const int* order, void* out,
                  long out_stride, float* part_o, float* part_ml, int B, int Hq, int Hkv, int D,
                  int block_size, float scale, int part_tokens, int max_parts,
+                 const int* rope_positions, const float* cos_sin, const int* slots,
                  hipStream_t stream) {
   if (B <= 0) return 0;
+  if (cos_sin && (!rope_positions || !slots)) return -5;
+  const RopeIn rp{rope_positions, cos_sin, slots};
   if ((D != 128 && D != 64) || block_size != BS) return -1;
   if (Hq % Hkv != 0 || Hq / Hkv > 16) return -2;
   if (part_tokens % (4 * BS) != 0) return -3;
@@ -406,14 +520,17 @@ int paged_decode(const void* q, long q_stride, const void* k_cache, const void* 
   paged_decode_kernel<HDV, MODE><<<dim3(max_parts, Hkv, B), dim3(256), 0, stream>>>(          \
       (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, \
       bt_stride, context_lens, order, (bf16_t*)out, out_stride, part_o, part_ml, Hq, Hkv,     \
-      scale, part_tokens, max_parts);
-#define LMX_DEC_P(HDV)                                                                        \
-  paged_decode_persist_kernel<HDV><<<dim3(std::min(B * Hkv, decode_resident_wgs())), dim3(256), \
+      scale, part_tokens, max_parts, rp);
+#define LMX_DEC_P(HDV, MODE)                                                                  \
+  paged_decode_persist_kernel<HDV, MODE><<<dim3(std::min(B * Hkv, decode_resident_wgs())), dim3(256), \
                                       0, stream>>>(                                           \
       (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, \
-      bt_stride, context_lens, order, (bf16_t*)out, out_stride, B, Hq, Hkv, scale, part_tokens);
+      bt_stride, context_lens, order, (bf16_t*)out, out_stride, B, Hq, Hkv, scale, part_tokens, \
+      rp);
 #define LMX_DEC(HDV)                                                                          \
-  if (g_decode_mode == 0 && max_parts == 1) { LMX_DEC_P(HDV) }                                \
+  if (g_decode_mode == 0 && max_parts == 1) { LMX_DEC_P(HDV, 0) }                             \
+  else if (g_decode_mode == 5 && max_parts == 1) { LMX_DEC_P(HDV, 5) }                        \
+  else if (g_decode_mode == 5) { LMX_DEC_K(HDV, 5) }                                          \
   else if (g_decode_mode == 1) { LMX_DEC_K(HDV, 1) }                                          \
   else if (g_decode_mode == 2) { LMX_DEC_K(HDV, 2) }                                          \
   else if (g_decode_mode == 3) { LMX_DEC_K(HDV, 3) }                                          \

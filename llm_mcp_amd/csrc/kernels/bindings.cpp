@@ -23,7 +23,8 @@ int kv_write(const void*, const void*, long, const int*, int, int, int, void*, v
 void set_decode_mode(int);
 int paged_decode(const void*, long, const void*, const void*, const int*, int, const int*,
                  const int*, void*,
-                 long, float*, float*, int, int, int, int, int, float, int, int, hipStream_t);
+                 long, float*, float*, int, int, int, int, int, float, int, int, const int*,
+                 const float*, const int*, hipStream_t);
 int paged_prefill(const void*, long, const void*, const void*, const int*, int, const int*,
                   const int*, const int*, int, void*, long, int, int, int, int, float, int,
                   hipStream_t);
@@ -103,11 +104,12 @@ PYBIND11_MODULE(_lmx_kernels, m) {
   m.def("paged_decode", [](uptr q, long q_stride, uptr kc, uptr vc, uptr bt, int bt_stride,
                            uptr ctx, uptr order, uptr out, long out_stride, uptr part_o,
                            uptr part_ml, int B, int Hq, int Hkv, int D, int BS, float scale,
-                           int part_tokens, int max_parts, uptr stream) {
+                           int part_tokens, int max_parts, uptr positions, uptr cos_sin,
+                           uptr slots, uptr stream) {
     check(lmx::paged_decode(P<void>(q), q_stride, P<void>(kc), P<void>(vc), P<int>(bt), bt_stride,
                             P<int>(ctx), P<int>(order), P<void>(out), out_stride, P<float>(part_o),
                             P<float>(part_ml), B, Hq, Hkv, D, BS, scale, part_tokens, max_parts,
-                            S(stream)),
+                            P<int>(positions), P<float>(cos_sin), P<int>(slots), S(stream)),
           "paged_decode");
   });
   m.def("set_decode_mode", [](int mode) { lmx::set_decode_mode(mode); },

@@ -164,6 +164,8 @@ class LlamaModel:
         self.scale = 1.0 / math.sqrt(self.D)
         self.cos_sin = ref.rope_cos_sin(cfg.max_position, self.D, cfg.rope_theta, self.device,
                                         cfg.rope_scaling)
+        # K2 + K5 inside K4 for decode rows (LMX_FUSED_DECODE_ROPE=0: separate kernels)
+        self.fuse_decode_rope = os.environ.get("LMX_FUSED_DECODE_ROPE", "1") == "1"
         if weights is None:
             weights = self._random_weights(seed)
         self.w = weights
@@ -258,13 +260,23 @@ class LlamaModel:
             if "bqkv" in L:          # Qwen2: biased q/k/v
                 qkv += L["bqkv"]
             kc, vc = k_caches[li], v_caches[li]
-            ops.rope_and_cache(qkv, inp.positions, self.cos_sin, Hq, Hkv, D, inp.slots, kc, vc,
-                               tile_from=nd, q_norm=L.get("q_norm"), k_norm=L.get("k_norm"),
-                               eps=cfg.rms_eps)
+            # decode rows: rotary + cache write fused into the decode attention
+            # kernel (one launch and one boundary fewer per layer); prefill rows
+            # (and q/k-norm models) keep the rope/cache kernels
+            fuse = nd > 0 and self.fuse_decode_rope and "q_norm" not in L
+            if not fuse:
+                ops.rope_and_cache(qkv, inp.positions, self.cos_sin, Hq, Hkv, D, inp.slots, kc,
+                                   vc, tile_from=nd, q_norm=L.get("q_norm"),
+                                   k_norm=L.get("k_norm"), eps=cfg.rms_eps)
+            elif T > nd:
+                ops.rope_and_cache(qkv[nd:], inp.positions[nd:], self.cos_sin, Hq, Hkv, D,
+                                   inp.slots[nd:], kc, vc, tile_from=0, eps=cfg.rms_eps)
             if nd > 0:
                 ops.paged_decode_attention(qkv[:nd], kc, vc, inp.block_tables,
                                            inp.context_lens, self.scale, attn[:nd], decode_ws,
-                                           part_tokens, Hq=Hq, order=inp.decode_order)
+                                           part_tokens, Hq=Hq, order=inp.decode_order,
+                                           rope=(inp.positions, self.cos_sin, inp.slots)
+                                           if fuse else None)
             if T > nd:
                 ops.paged_prefill_attention(qkv, kc, vc, inp.block_tables[nd:],
                                             inp.cu_q[nd:], inp.context_lens[nd:],

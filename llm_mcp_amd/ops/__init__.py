@@ -222,13 +222,23 @@ class DecodeWorkspace:
 def paged_decode_attention(q: torch.Tensor, k_cache, v_cache, block_tables, context_lens,
                            scale: float, out: torch.Tensor, ws: DecodeWorkspace | None = None,
                            part_tokens: int = 512, Hq: int | None = None,
-                           order: torch.Tensor | None = None) -> torch.Tensor:
+                           order: torch.Tensor | None = None, rope: tuple | None = None
+                           ) -> torch.Tensor:
     """q: [B, Hq*D] rows (row stride = q.stride(0)); out: [B, Hq*D].
     ``order`` (int32 [B], optional): a permutation of the rows, longest
-    context first -- the workgroup dispatch order (``decode_order``)."""
+    context first -- the workgroup dispatch order (``decode_order``).
+    ``rope`` = (positions int32[B], cos_sin fp32[P, D], slots int32[B]): q is
+    the UNROTATED fused QKV row ([q | k | v] heads); the kernel rotates q in
+    registers and writes the step's rotated k and v into the cache at
+    ``slots`` itself (K2 + K5 fused into K4: ``rope_and_cache`` is skipped for
+    these rows; no q/k-norm models)."""
     B = q.shape[0]
     NB, Hkv, BS, D = k_cache.shape
     Hq = Hq or (q.shape[1] // D)
+    if rope is not None and not q.is_cuda:
+        positions, cos_sin, slots = rope
+        ref.rope_cache(q, positions[:B], cos_sin, Hq, Hkv, D, slots[:B], k_cache, v_cache, False)
+        rope = None
     if not q.is_cuda:
         o = ref.paged_decode(q[:, : Hq * D].reshape(B, Hq, D), k_cache, v_cache, block_tables,
                              context_lens, scale)
@@ -243,11 +253,20 @@ def paged_decode_attention(q: torch.Tensor, k_cache, v_cache, block_tables, cont
     if order is not None:
         _chk(order.dtype == torch.int32 and order.numel() >= B and order.is_cuda, "order int32[B]")
     max_parts = ws.max_parts if ws is not None else 1
+    pos = cs = slots = None
+    if rope is not None:
+        pos, cs, slots = rope
+        _chk(q.shape[1] >= (Hq + 2 * Hkv) * D, "fused rope: q rows must be whole QKV rows")
+        _chk(pos.dtype == torch.int32 and pos.numel() >= B and slots.dtype == torch.int32
+             and slots.numel() >= B, "fused rope: positions / slots int32[B]")
+        _chk(cs.dtype == torch.float32 and cs.shape[1] == D and cs.is_contiguous(),
+             "fused rope: cos_sin [P, D] fp32")
     native().paged_decode(_ptr(q), q.stride(0), _ptr(k_cache), _ptr(v_cache), _ptr(block_tables),
                           block_tables.stride(0), _ptr(context_lens), _ptr(order), _ptr(out),
                           out.stride(0),
                           _ptr(ws.part_o) if ws else 0, _ptr(ws.part_ml) if ws else 0, B, Hq, Hkv,
-                          D, BS, float(scale), part_tokens, max_parts, _stream())
+                          D, BS, float(scale), part_tokens, max_parts, _ptr(pos), _ptr(cs),
+                          _ptr(slots), _stream())
     return out
 
 

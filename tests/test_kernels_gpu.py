@@ -195,6 +195,58 @@ def test_paged_decode_dispatch_order_and_loop_modes():
     torch.testing.assert_close(base.float().view(B, Hq, D), expect.float(), atol=2e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("Hq,Hkv,D", [(32, 8, 128), (8, 1, 128), (16, 16, 64), (28, 4, 128)])
+@pytest.mark.parametrize("parts", [1, 4])
+@pytest.mark.parametrize("mode", [0, 1, 4])
+def test_paged_decode_fused_rope(Hq, Hkv, D, parts, mode):
+    """K2 + K5 fused into K4 (rope=...): the kernel rotates q in registers and
+    writes the step's rotated k / transposed v into the cache itself.  Same
+    output and cache as rope_and_cache followed by the plain decode kernel,
+    and as the fp32 reference; padding rows (slot -1, context 1) write nothing."""
+    ctxs = [535, 791, 1, 33, 32, 700, 1024, 64, 2000, 17]
+    B = len(ctxs)
+    NB = sum(math.ceil(c / 32) for c in ctxs) + 4
+    kc, vc = _cache(NB, Hkv, D)
+    bt = _random_tables(B, ctxs, NB)
+    ctx = torch.tensor(ctxs, dtype=torch.int32, device=DEV)
+    pos = (ctx - 1).to(torch.int32)
+    slots = torch.tensor([int(bt[b, (c - 1) // 32]) * 32 + (c - 1) % 32 for b, c in enumerate(ctxs)],
+                         dtype=torch.int32, device=DEV)
+    slots[2] = -1                        # a padding row of a captured bucket
+    cs = ref.rope_cos_sin(4096, D, 500000.0, DEV)
+    qkv = _bf(B, (Hq + 2 * Hkv) * D)
+    scale = 1 / math.sqrt(D)
+    ws = ops.DecodeWorkspace(B, Hq, D, parts, DEV) if parts > 1 else None
+    order = torch.from_numpy(ops.decode_order(ctxs)).to(DEV)
+    # unfused: rope/cache kernel, then the decode kernel on the rotated rows
+    q_u, kc_u, vc_u = qkv.clone(), kc.clone(), vc.clone()
+    ops.rope_and_cache(q_u, pos, cs, Hq, Hkv, D, slots, kc_u, vc_u, tile_from=B)
+    out_u = torch.empty(B, Hq * D, dtype=torch.bfloat16, device=DEV)
+    out_f = torch.empty_like(out_u)
+    q_f, kc_f, vc_f = qkv.clone(), kc.clone(), vc.clone()
+    try:
+        ops.native().set_decode_mode(mode)
+        ops.paged_decode_attention(q_u, kc_u, vc_u, bt, ctx, scale, out_u, ws, 256, Hq=Hq,
+                                   order=order)
+        ops.paged_decode_attention(q_f, kc_f, vc_f, bt, ctx, scale, out_f, ws, 256, Hq=Hq,
+                                   order=order, rope=(pos, cs, slots))
+    finally:
+        ops.native().set_decode_mode(0)
+    torch.cuda.synchronize()
+    assert torch.equal(q_f, qkv)                      # the fused kernel leaves the rows alone
+    assert torch.equal(vc_f, vc_u)
+    torch.testing.assert_close(kc_f.float(), kc_u.float(), atol=1e-2, rtol=1e-2)
+    torch.testing.assert_close(out_f.float(), out_u.float(), atol=1e-2, rtol=1e-2)
+    # fp32 reference of the whole step
+    q0, kc0, vc0 = qkv.cpu(), kc.cpu(), vc.cpu()
+    ref.rope_cache(q0, pos.cpu(), cs.cpu(), Hq, Hkv, D, slots.cpu(), kc0, vc0, False)
+    expect = ref.paged_decode(q0[:, :Hq * D].reshape(B, Hq, D), kc0, vc0, bt.cpu(), ctx.cpu(),
+                              scale)
+    live = [b for b in range(B) if b != 2]
+    torch.testing.assert_close(out_f.float().cpu().view(B, Hq, D)[live], expect.float()[live],
+                               atol=2e-2, rtol=2e-2)
+
+
 def test_paged_decode_spike_rescale():
     """Force the online-softmax rescale: one key scores far above the rest in a
     late page (guide §5.4 rule 26)."""

@@ -25,6 +25,11 @@ def main():
     ap.add_argument("--part-tokens", type=int, default=256)
     ap.add_argument("--order", choices=("random", "desc", "asc"), default="random",
                     help="sequence order = workgroup dispatch order (longest-first test)")
+    ap.add_argument("--layout", choices=("random", "contig", "engine"), default="random",
+                    help="page placement: random pages; each sequence's pages contiguous; or the "
+                         "engine's wave pattern (prompt pages contiguous per sequence, decode "
+                         "pages handed out one per sequence in turn)")
+    ap.add_argument("--pages", type=int, default=20000, help="pages in the cache")
     a = ap.parse_args()
     B, Hq, Hkv, D, BS = a.batch, 32, 8, 128, 32
     dev = torch.device("cuda", 0)
@@ -33,7 +38,7 @@ def main():
     if a.order != "random":
         ctx = ctx.sort(descending=a.order == "desc").values
     maxb = (a.ctx_hi + BS - 1) // BS
-    nb = 20000                                  # 20000 pages x 64 KB x 2 = 2.6 GB (> MALL)
+    nb = a.pages                                # 20000 pages x 64 KB x 2 = 2.6 GB (> MALL)
     k_cache = (torch.randn(nb, Hkv, BS, D, device=dev) * 0.5).to(torch.bfloat16)
     v_cache = torch.randn(nb, Hkv, D, BS, device=dev).to(torch.bfloat16)
     q = torch.randn(B, Hq * D, device=dev).to(torch.bfloat16)
@@ -42,8 +47,25 @@ def main():
     # last read >= 640 MB of other pages ago, so they come from HBM (as in a
     # decode step, where the whole model streams between two calls of a layer)
     nrot = max(1, min(8, nb // (B * maxb)))
-    tables = [p.view(B, maxb).to(dev) for p in
-              torch.randperm(nb)[:nrot * B * maxb].to(torch.int32).chunk(nrot)]
+    def table(base):
+        if a.layout == "random":
+            return torch.randperm(nb)[:B * maxb].to(torch.int32).view(B, maxb)
+        if a.layout == "contig":
+            return (base + torch.arange(B * maxb, dtype=torch.int32)).view(B, maxb)
+        # engine wave: prompt pages (ctx_lo tokens) contiguous per sequence,
+        # then one page per sequence in turn as decode crosses page boundaries
+        npr = (a.ctx_lo + BS - 1) // BS
+        t = torch.empty(B, maxb, dtype=torch.int32)
+        t[:, :npr] = (base + torch.arange(B * npr, dtype=torch.int32)).view(B, npr)
+        nxt = base + B * npr
+        for j in range(npr, maxb):
+            t[:, j] = nxt + torch.arange(B, dtype=torch.int32)
+            nxt += B
+        return t
+    tables = [table(i * B * maxb).to(dev) for i in range(nrot)]
+    if a.layout == "random":
+        tables = [p.view(B, maxb).to(dev) for p in
+                  torch.randperm(nb)[:nrot * B * maxb].to(torch.int32).chunk(nrot)]
     bt = tables[0]
     out = torch.empty(B, Hq * D, device=dev, dtype=torch.bfloat16)
     kv_bytes = int(ctx.sum()) * Hkv * D * 2 * 2
@@ -52,7 +74,7 @@ def main():
     scale = D ** -0.5
     ref = None
     nat = ops.native()
-    for mode in (4, 0, 4, 0):
+    for mode in (4, 0, 5, 4, 0, 5):
         nat.set_decode_mode(mode)
         ops.paged_decode_attention(q, k_cache, v_cache, bt, cl, scale, out, ws, a.part_tokens,
                                    order=order)
@@ -69,7 +91,7 @@ def main():
         e.record()
         torch.cuda.synchronize()
         us = s.elapsed_time(e) / a.iters * 1e3
-        print(f"decode attn B={B} parts {a.parts}x{a.part_tokens} {a.order} mode {mode}: {us:7.1f} us  {kv_bytes / us / 1e6:5.2f} TB/s  "
+        print(f"decode attn {a.layout} pages={nb} B={B} parts {a.parts}x{a.part_tokens} {a.order} mode {mode}: {us:7.1f} us  {kv_bytes / us / 1e6:5.2f} TB/s  "
               f"vs grid (mode 4): {same}", flush=True)
     nat.set_decode_mode(0)
 
