@@ -608,7 +608,7 @@ __global__ void __launch_bounds__(256, 2) paged_prefill_kernel(
     const bf16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ cu_q, const int* __restrict__ context_lens,
     const int* __restrict__ tiles, bf16_t* __restrict__ out, long out_stride, int Hq, int Hkv,
-    float scale, int causal) {
+    float scale, int causal, float rescale_thr) {
   extern __shared__ __attribute__((aligned(16))) char pf_smem[];
   constexpr int PAGE = BS * HD;
   // buffer b: K pages at b*4*PAGE + {0, PAGE}, V pages at b*4*PAGE + 2*PAGE + {0, PAGE}
@@ -706,7 +706,15 @@ __global__ void __launch_bounds__(256, 2) paged_prefill_kernel(
         for (int n = 0; n < PF_NG; ++n) s[n][kb] = mfma16(kf, qf[n][ks], s[n][kb]);
       }
     }
-    // online softmax per column group
+    // online softmax per column group.  The scores stay raw (the scale is
+    // folded into the exp argument: one FMA per score), and the running max m
+    // (log2 units) is only raised when a tile's max exceeds it by more than
+    // rescale_thr (guide T13): until then p = 2^(x - m) <= 2^thr, harmless in
+    // bf16 P / fp32 l, and the O^T accumulators are not rescaled -- the
+    // NT x 4 multiplies per column group and tile that a per-tile rescale
+    // costs are most of the softmax VALU work at this tile shape.  The wave
+    // rescales together when any of its columns needs it (exact alpha per
+    // column, 1 for the ones that did not grow).
     const bool need_mask = key0 + PF_TK - 1 > wave_lo;
     bf16x8_t pf[PF_NG][2];
 #pragma unroll
@@ -717,25 +725,29 @@ __global__ void __launch_bounds__(256, 2) paged_prefill_kernel(
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int key = key0 + kb * 16 + 4 * g + r;
-          x[4 * kb + r] = (!need_mask || key <= lim[n]) ? s[n][kb][r] * scale_log2 : -INFINITY;
+          x[4 * kb + r] = (!need_mask || key <= lim[n]) ? s[n][kb][r] : -INFINITY;
         }
       float mx = x[0];
 #pragma unroll
       for (int j = 1; j < 16; ++j) mx = fmaxf(mx, x[j]);
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float m_new = fmaxf(m[n], mx);
-      const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
-      const float alpha = exp2f(m[n] - m_use);
+      const float mx2 = mx * scale_log2;                 // -inf stays -inf (scale > 0)
+      if (__ballot(mx2 > m[n] + rescale_thr)) {
+        const float m_new = fmaxf(m[n], mx2);
+        const float alpha = (m_new == -INFINITY) ? 1.f : exp2f(m[n] - m_new);
+        l[n] *= alpha;
+#pragma unroll
+        for (int i = 0; i < NT; ++i) acc[n][i] *= alpha;
+        m[n] = m_new;
+      }
+      const float m_use = (m[n] == -INFINITY) ? 0.f : m[n];
       float rs = 0.f;
 #pragma unroll
-      for (int j = 0; j < 16; ++j) { x[j] = exp2f(x[j] - m_use); rs += x[j]; }
+      for (int j = 0; j < 16; ++j) { x[j] = exp2f(fmaf(x[j], scale_log2, -m_use)); rs += x[j]; }
       rs += __shfl_xor(rs, 16, 64);
       rs += __shfl_xor(rs, 32, 64);
-      l[n] = l[n] * alpha + rs;
-      m[n] = m_new;
-#pragma unroll
-      for (int i = 0; i < NT; ++i) acc[n][i] *= alpha;
+      l[n] += rs;
       // page p: keys 4g+r (block 2p) then 16+4g+r (block 2p+1) -> permuted-k B operand
 #pragma unroll
       for (int pp = 0; pp < 2; ++pp)
@@ -773,6 +785,11 @@ __global__ void __launch_bounds__(256, 2) paged_prefill_kernel(
   }
 }
 
+// lazy-rescale threshold of the prefill softmax, log2 units (0: rescale
+// whenever a column's max grows -- the test knob of guide §5.4 rule 26)
+static float g_prefill_rescale_thr = 8.f;
+void set_prefill_rescale_thr(float thr) { g_prefill_rescale_thr = thr; }
+
 int paged_prefill(const void* q, long q_stride, const void* k_cache, const void* v_cache,
                   const int* block_tables, int bt_stride, const int* cu_q,
                   const int* context_lens, const int* tiles, int num_tiles, void* out,
@@ -785,7 +802,8 @@ int paged_prefill(const void* q, long q_stride, const void* k_cache, const void*
   paged_prefill_kernel<HDV><<<dim3(num_tiles, Hkv), dim3(256), 2 * 4 * BS * HDV * 2,         \
                               stream>>>(                                                      \
       (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, \
-      bt_stride, cu_q, context_lens, tiles, (bf16_t*)out, out_stride, Hq, Hkv, scale, causal);
+      bt_stride, cu_q, context_lens, tiles, (bf16_t*)out, out_stride, Hq, Hkv, scale, causal, \
+      g_prefill_rescale_thr);
   if (D == 128) { LMX_PRE(128) } else { LMX_PRE(64) }
 #undef LMX_PRE
   return (int)hipGetLastError();

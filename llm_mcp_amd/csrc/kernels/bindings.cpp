@@ -21,6 +21,7 @@ int rope_cache(void*, long, const int*, const float*, int, int, int, int, const 
 int kv_write(const void*, const void*, long, const int*, int, int, int, void*, void*, int,
              hipStream_t);
 void set_decode_mode(int);
+void set_prefill_rescale_thr(float);
 int paged_decode(const void*, long, const void*, const void*, const int*, int, const int*,
                  const int*, void*,
                  long, float*, float*, int, int, int, int, int, float, int, int, const int*,
@@ -114,6 +115,8 @@ PYBIND11_MODULE(_lmx_kernels, m) {
   });
   m.def("set_decode_mode", [](int mode) { lmx::set_decode_mode(mode); },
         "paged decode loop: 0 one page at a time, 1 next page prefetched, 2 loads only (probe)");
+  m.def("set_prefill_rescale_thr", [](float thr) { lmx::set_prefill_rescale_thr(thr); },
+        "prefill softmax: raise the running max only past this many log2 units (0: always)");
   m.def("paged_prefill", [](uptr q, long q_stride, uptr kc, uptr vc, uptr bt, int bt_stride,
                             uptr cu_q, uptr ctx, uptr tiles, int num_tiles, uptr out,
                             long out_stride, int Hq, int Hkv, int D, int BS, float scale,

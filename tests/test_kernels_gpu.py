@@ -265,6 +265,47 @@ def test_paged_decode_spike_rescale():
     torch.testing.assert_close(out.float().view(1, Hq, D), expect.float(), atol=2e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("Hq,Hkv,D", [(32, 8, 128), (12, 12, 64)])
+@pytest.mark.parametrize("causal", [True, False])
+def test_paged_prefill_lazy_rescale(Hq, Hkv, D, causal):
+    """The prefill softmax raises its running max only past a threshold (guide
+    T13).  Force the rescale branch: key 700 scores far above every other key
+    for the queries after it (and, bidirectional, for all of them), in a late
+    tile.  The shipped threshold and threshold 0 (rescale on every growth)
+    agree to rounding and both match the fp32 reference (guide §5.4 rule 26)."""
+    L, S = 900, 2
+    NB = S * math.ceil(L / 32) + 2
+    kc, vc = _cache(NB, Hkv, D)
+    bt = _random_tables(S, [L] * S, NB)
+    cu = torch.tensor([0, L, 2 * L], dtype=torch.int32, device=DEV)
+    ctx = torch.tensor([L] * S, dtype=torch.int32, device=DEV)
+    q = _bf(S * L, (Hq + 2 * Hkv) * D)
+    G = Hq // Hkv
+    # key 700 of sequence 0 = 6 x (query 800's head-0 vector of each kv group)
+    qv = q[800, :Hq * D].view(Hkv, G, D)[:, 0, :]
+    blk = int(bt[0, 700 // 32])
+    kc[blk, :, 700 % 32, :] = (qv * 6).to(kc.dtype)
+    qpt = ops.prefill_q_per_tile(Hq, Hkv, D)
+    tiles = torch.tensor([v for s_ in range(S) for q0 in range(0, L, qpt) for v in (s_, q0)],
+                         dtype=torch.int32, device=DEV)
+    scale = 1 / math.sqrt(D)
+    outs = []
+    try:
+        for thr in (8.0, 0.0):
+            ops.native().set_prefill_rescale_thr(thr)
+            o = torch.zeros(S * L, Hq * D, dtype=torch.bfloat16, device=DEV)
+            ops.paged_prefill_attention(q, kc, vc, bt, cu, ctx, tiles, scale, o, causal=causal,
+                                        Hq=Hq)
+            outs.append(o)
+    finally:
+        ops.native().set_prefill_rescale_thr(8.0)
+    torch.testing.assert_close(outs[0].float(), outs[1].float(), atol=1e-2, rtol=1e-2)
+    expect = ref.paged_prefill(q[:, :Hq * D].reshape(S * L, Hq, D), kc, vc, bt, cu, ctx, scale,
+                               causal=causal)
+    torch.testing.assert_close(outs[0].float().view(S * L, Hq, D), expect.float(), atol=2e-2,
+                               rtol=2e-2)
+
+
 def _params(B, t=1.0, k=0, p=1.0):
     f = lambda v, dt: torch.full((B,), v, dtype=dt, device=DEV)
     return (f(t, torch.float32), f(k, torch.int32), f(p, torch.float32),

@@ -19,7 +19,7 @@ SHAPES = {"nomic": (32, 1024, 12, 12, 64, False), "mxbai": (64, 512, 16, 16, 64,
           "llama8b": (30, 546, 32, 8, 128, True)}
 
 
-def run(name, S, L, Hq, Hkv, D, causal, iters, ng=0):
+def run(name, S, L, Hq, Hkv, D, causal, iters, ng=0, tag=""):
     dev = torch.device("cuda", 0)
     BS = 32
     T = S * L
@@ -51,7 +51,7 @@ def run(name, S, L, Hq, Hkv, D, causal, iters, ng=0):
     torch.cuda.synchronize()
     us = s.elapsed_time(e) / iters * 1e3
     flops = 4.0 * S * L * L * D * Hq * (0.5 if causal else 1.0)
-    print(f"prefill attn {name:8s} {us:8.1f} us  {flops / us / 1e6:6.0f} TF/s", flush=True)
+    print(f"prefill attn {name:8s} {tag} {us:8.1f} us  {flops / us / 1e6:6.0f} TF/s", flush=True)
 
 
 def main():
@@ -59,9 +59,16 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--ng", type=int, default=0,
                     help="column groups per wave of the loaded build (A/B of an older .so)")
+    ap.add_argument("--thr", default="8",
+                    help="comma list of softmax lazy-rescale thresholds to interleave")
     a = ap.parse_args()
-    for name, shp in SHAPES.items():
-        run(name, *shp, a.iters, a.ng)
+    thrs = [float(t) for t in a.thr.split(",")]
+    for _ in range(2):
+        for name, shp in SHAPES.items():
+            for thr in thrs:
+                if hasattr(ops.native(), "set_prefill_rescale_thr"):
+                    ops.native().set_prefill_rescale_thr(thr)
+                run(name, *shp, a.iters, a.ng, tag=f"thr={thr:g}")
 
 
 if __name__ == "__main__":
