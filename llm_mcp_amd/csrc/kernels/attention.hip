@@ -602,7 +602,16 @@ __device__ __forceinline__ void pf_stage_page(bf16_t* k_lds, bf16_t* v_lds,
   }
 }
 
-template <int HD, int PF_NG = pf_groups<HD>()>
+template <int CNT>
+__device__ __forceinline__ void pf_vmwait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(CNT) : "memory");
+}
+
+// NST: LDS ring slots of 64-key K/V tiles.  NST = 2: the next tile's DMA is in
+// flight while the current tile computes, drained (vmcnt 0) at the next
+// barrier.  NST = 3: two tiles in flight across a raw s_barrier with a counted
+// vmcnt (cdna guide §5 "Pipelining across barriers").
+template <int HD, int NST, int PF_NG = pf_groups<HD>()>
 __global__ void __launch_bounds__(256, 2) paged_prefill_kernel(
     const bf16_t* __restrict__ q, long q_stride, const bf16_t* __restrict__ k_cache,
     const bf16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
@@ -639,12 +648,37 @@ __global__ void __launch_bounds__(256, 2) paged_prefill_kernel(
     qi[n] = q_start + (wave * PF_NG + n) * QG + c / G;
     valid[n] = c < QG * G && qi[n] < qlen;
     lim[n] = valid[n] ? (causal ? (ctx - qlen + qi[n]) : (ctx - 1)) : -1;
-    const int head = kvh * G + (c % G);
-    const bf16_t* qrow = q + (long)(qbeg + (valid[n] ? qi[n] : 0)) * q_stride + (long)head * HD;
+  }
+  // Q fragments through LDS (one image row per column: [wave][n][c][HD]) by
+  // LDS-DMA, not plain loads: an ordinary global load whose result the tile
+  // loop consumes makes hipcc drain the whole DMA ring (vmcnt 0) before the
+  // first MFMA of EVERY tile (guide §5 item 4b); the image borrows the ring
+  // slots before the prologue fills them.
+  {
+    constexpr int QROWS = 4 * PF_NG * 16, QCH = HD / 8;   // rows, 16-B chunks per row
+    static_assert(QROWS * HD <= NST * 4 * PAGE, "Q image fits the ring");
 #pragma unroll
-    for (int s = 0; s < KS; ++s)
-      qf[n][s] = valid[n] ? load_frag16B(qrow + 32 * s + 8 * g)
-                          : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+    for (int j = 0; j < QROWS * QCH / 256; ++j) {
+      const int e = j * 256 + threadIdx.x, row = e / QCH, ch = e % QCH;
+      const int rw = row / (PF_NG * 16), rn = (row / 16) % PF_NG, rc = row % 16;
+      const int rq = q_start + (rw * PF_NG + rn) * QG + rc / G;
+      const bool ok = rc < QG * G && rq < qlen;
+      const bf16_t* src = q + (long)(qbeg + (ok ? rq : 0)) * q_stride +
+                          (long)(kvh * G + (ok ? rc % G : 0)) * HD + 8 * ch;
+      pf_glds16(src, lds + j * 2048 + wave * 512);
+    }
+    pf_vmwait<0>();
+    __builtin_amdgcn_s_barrier();
+#pragma unroll
+    for (int n = 0; n < PF_NG; ++n) {
+      const bf16_t* qrow = lds + ((wave * PF_NG + n) * 16 + c) * HD;
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+        qf[n][s] = valid[n] ? load_frag16B(qrow + 32 * s + 8 * g)
+                            : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();     // every wave holds its Q before the ring reuses the slots
   }
   // smallest column limit of the wave: tiles below it need no mask
   int wave_lo = INT_MAX;
@@ -679,12 +713,19 @@ __global__ void __launch_bounds__(256, 2) paged_prefill_kernel(
     }
   };
 
-  stage(0, 0);
+  // LDS-DMA instructions per thread per tile (2 pages x K and V)
+  constexpr int LPS = 4 * (PAGE / 2048);
+#pragma unroll
+  for (int p = 0; p < NST - 1; ++p)
+    if (p < ntiles) stage(p, p);
   for (int t = 0; t < ntiles; ++t) {
-    const int buf = t & 1;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t + 1 < ntiles) stage(t + 1, buf ^ 1);
+    const int buf = t % NST;
+    // tile t landed once at most the tiles issued after it remain in flight
+    if (t + NST - 2 < ntiles) pf_vmwait<(NST - 2) * LPS>(); else pf_vmwait<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();    // raw: a __syncthreads fence would drain the ring
+    // refill the slot every wave finished reading at t - 1
+    if (t + NST - 1 < ntiles) stage(t + NST - 1, (t + NST - 1) % NST);
     if (wave_idle) continue;
     const bf16_t* kt = lds + buf * 4 * PAGE;
     const bf16_t* vt = kt + 2 * PAGE;
@@ -789,6 +830,9 @@ __global__ void __launch_bounds__(256, 2) paged_prefill_kernel(
 // whenever a column's max grows -- the test knob of guide §5.4 rule 26)
 static float g_prefill_rescale_thr = 8.f;
 void set_prefill_rescale_thr(float thr) { g_prefill_rescale_thr = thr; }
+// LDS ring slots of the prefill kernel (0: default per head dim; 2 or 3: A/B knob)
+static int g_prefill_stages = 0;
+void set_prefill_stages(int n) { g_prefill_stages = (n == 2 || n == 3) ? n : 0; }
 
 int paged_prefill(const void* q, long q_stride, const void* k_cache, const void* v_cache,
                   const int* block_tables, int bt_stride, const int* cu_q,
@@ -798,13 +842,28 @@ int paged_prefill(const void* q, long q_stride, const void* k_cache, const void*
   if (num_tiles <= 0) return 0;
   if ((D != 128 && D != 64) || block_size != BS) return -1;
   if (Hq % Hkv != 0 || Hq / Hkv > 16) return -2;
-#define LMX_PRE(HDV)                                                                          \
-  paged_prefill_kernel<HDV><<<dim3(num_tiles, Hkv), dim3(256), 2 * 4 * BS * HDV * 2,         \
-                              stream>>>(                                                      \
-      (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, \
-      bt_stride, cu_q, context_lens, tiles, (bf16_t*)out, out_stride, Hq, Hkv, scale, causal, \
-      g_prefill_rescale_thr);
-  if (D == 128) { LMX_PRE(128) } else { LMX_PRE(64) }
+#define LMX_PRE(HDV, NSTV)                                                                    \
+  {                                                                                           \
+    constexpr int smem = NSTV * 4 * BS * HDV * 2;                                             \
+    static bool attr = false;                                                                 \
+    if (smem > 65536 && !attr) {                                                              \
+      (void)hipFuncSetAttribute((const void*)paged_prefill_kernel<HDV, NSTV>,                 \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, smem);            \
+      attr = true;                                                                            \
+    }                                                                                         \
+    paged_prefill_kernel<HDV, NSTV><<<dim3(num_tiles, Hkv), dim3(256), smem, stream>>>(       \
+        (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache,           \
+        block_tables, bt_stride, cu_q, context_lens, tiles, (bf16_t*)out, out_stride, Hq, Hkv, \
+        scale, causal, g_prefill_rescale_thr);                                                \
+  }
+  // 2 slots by default: 3 measured equal at D = 64 and 1.55x slower at D = 128
+  // (96 KB of LDS leaves one workgroup per CU) -- tools/prefill_attn_probe.py
+  const int nst = g_prefill_stages ? g_prefill_stages : 2;
+  if (D == 128) {
+    if (nst == 3) LMX_PRE(128, 3) else LMX_PRE(128, 2)
+  } else {
+    if (nst == 3) LMX_PRE(64, 3) else LMX_PRE(64, 2)
+  }
 #undef LMX_PRE
   return (int)hipGetLastError();
 }

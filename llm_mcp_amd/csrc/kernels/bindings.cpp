@@ -22,6 +22,7 @@ int kv_write(const void*, const void*, long, const int*, int, int, int, void*, v
              hipStream_t);
 void set_decode_mode(int);
 void set_prefill_rescale_thr(float);
+void set_prefill_stages(int);
 int paged_decode(const void*, long, const void*, const void*, const int*, int, const int*,
                  const int*, void*,
                  long, float*, float*, int, int, int, int, int, float, int, int, const int*,
@@ -117,6 +118,8 @@ PYBIND11_MODULE(_lmx_kernels, m) {
         "paged decode loop: 0 one page at a time, 1 next page prefetched, 2 loads only (probe)");
   m.def("set_prefill_rescale_thr", [](float thr) { lmx::set_prefill_rescale_thr(thr); },
         "prefill softmax: raise the running max only past this many log2 units (0: always)");
+  m.def("set_prefill_stages", [](int n) { lmx::set_prefill_stages(n); },
+        "prefill attention LDS ring slots: 0 default per head dim, 2 or 3");
   m.def("paged_prefill", [](uptr q, long q_stride, uptr kc, uptr vc, uptr bt, int bt_stride,
                             uptr cu_q, uptr ctx, uptr tiles, int num_tiles, uptr out,
                             long out_stride, int Hq, int Hkv, int D, int BS, float scale,

@@ -128,9 +128,17 @@ def test_paged_decode(Hq, Hkv, D, ctxs):
     torch.testing.assert_close(out.float().view(B, Hq, D), expect.float(), atol=2e-2, rtol=2e-2)
 
 
+@pytest.fixture(params=[0, 2, 3], ids=["nst-default", "nst2", "nst3"])
+def prefill_ring(request):
+    """LDS ring slots of the prefill kernel: default per head dim, 2, 3."""
+    ops.native().set_prefill_stages(request.param)
+    yield request.param
+    ops.native().set_prefill_stages(0)
+
+
 @pytest.mark.parametrize("Hq,Hkv,D", [(32, 8, 128), (8, 1, 128), (12, 12, 64), (4, 4, 128),
                                      (28, 4, 128), (7, 1, 64), (24, 8, 128)])
-def test_paged_prefill_varlen_with_prefix(Hq, Hkv, D):
+def test_paged_prefill_varlen_with_prefix(Hq, Hkv, D, prefill_ring):
     qlens = [1, 70, 33, 256]
     prefix = [0, 40, 0, 100]
     ctxs = [q + p for q, p in zip(qlens, prefix)]

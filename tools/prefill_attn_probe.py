@@ -61,14 +61,22 @@ def main():
                     help="column groups per wave of the loaded build (A/B of an older .so)")
     ap.add_argument("--thr", default="8",
                     help="comma list of softmax lazy-rescale thresholds to interleave")
+    ap.add_argument("--stages", default="0",
+                    help="comma list of LDS ring slot counts to interleave (0 = default)")
     a = ap.parse_args()
     thrs = [float(t) for t in a.thr.split(",")]
+    stages = [int(t) for t in a.stages.split(",")]
+    nat = ops.native()
     for _ in range(2):
         for name, shp in SHAPES.items():
             for thr in thrs:
-                if hasattr(ops.native(), "set_prefill_rescale_thr"):
-                    ops.native().set_prefill_rescale_thr(thr)
-                run(name, *shp, a.iters, a.ng, tag=f"thr={thr:g}")
+                for st in stages:
+                    if hasattr(nat, "set_prefill_rescale_thr"):
+                        nat.set_prefill_rescale_thr(thr)
+                    if hasattr(nat, "set_prefill_stages"):
+                        nat.set_prefill_stages(st)
+                    run(name, *shp, a.iters, a.ng, tag=f"thr={thr:g} nst={st}")
+    nat.set_prefill_stages(0)
 
 
 if __name__ == "__main__":
