@@ -231,10 +231,11 @@ __device__ __forceinline__ void rope_q_frags(bf16x8_t (&qf)[HD / 32], const floa
   }
 }
 
-// The new token's k (rotated) and v of kv head kvh into its cache slot:
-// threads [0, HD/8) rotate 4 pairs of k each, threads [64, 64 + HD/4) move 4
-// v elements each into the d-major page.  Ends with the stores retired and a
-// workgroup barrier, so every wave's page loads that follow see them.
+// The new token's k (rotated) and v of kv head kvh into its cache slot, by ONE
+// wave: lanes [0, HD/8) rotate 4 pairs of k each, lanes [16, 16 + HD/4) move
+// 4 v elements each into the d-major page.  No wait here: the caller (the
+// wave that later reads the page holding the slot) retires the stores with
+// s_waitcnt vmcnt(0) before that read, so the other waves never wait on it.
 template <int HD>
 __device__ __forceinline__ void rope_write_kv(const bf16_t* __restrict__ krow,
                                               const bf16_t* __restrict__ vrow,
@@ -242,37 +243,33 @@ __device__ __forceinline__ void rope_write_kv(const bf16_t* __restrict__ krow,
                                               int Hkv, bf16_t* __restrict__ k_cache,
                                               bf16_t* __restrict__ v_cache) {
   constexpr int half = HD / 2;
-  const int t = threadIdx.x;
-  if (slot >= 0) {
-    const long blk = slot / BS, off = slot % BS;
-    if (t < HD / 8) {
-      const int i = 4 * t;
-      const bf16x4_t x1 = *reinterpret_cast<const bf16x4_t*>(krow + i);
-      const bf16x4_t x2 = *reinterpret_cast<const bf16x4_t*>(krow + half + i);
-      const float4 c = *reinterpret_cast<const float4*>(cs + i);
-      const float4 sn = *reinterpret_cast<const float4*>(cs + half + i);
-      const float cc[4] = {c.x, c.y, c.z, c.w}, ss[4] = {sn.x, sn.y, sn.z, sn.w};
-      bf16x4_t o1, o2;
+  const int lane = threadIdx.x & 63;
+  if (slot < 0) return;
+  const long blk = slot / BS, off = slot % BS;
+  if (lane < HD / 8) {
+    const int i = 4 * lane;
+    const bf16x4_t x1 = *reinterpret_cast<const bf16x4_t*>(krow + i);
+    const bf16x4_t x2 = *reinterpret_cast<const bf16x4_t*>(krow + half + i);
+    const float4 c = *reinterpret_cast<const float4*>(cs + i);
+    const float4 sn = *reinterpret_cast<const float4*>(cs + half + i);
+    const float cc[4] = {c.x, c.y, c.z, c.w}, ss[4] = {sn.x, sn.y, sn.z, sn.w};
+    bf16x4_t o1, o2;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float a = bf2f((uint16_t)x1[j]), b = bf2f((uint16_t)x2[j]);
-        o1[j] = (short)f2bf(a * cc[j] - b * ss[j]);
-        o2[j] = (short)f2bf(b * cc[j] + a * ss[j]);
-      }
-      bf16_t* kp = k_cache + ((blk * Hkv + kvh) * BS + off) * HD;
-      *reinterpret_cast<bf16x4_t*>(kp + i) = o1;
-      *reinterpret_cast<bf16x4_t*>(kp + half + i) = o2;
-    } else if (t >= 64 && t < 64 + HD / 4) {
-      const int d = 4 * (t - 64);
-      const bf16x4_t v = *reinterpret_cast<const bf16x4_t*>(vrow + d);
-      bf16_t* vp = v_cache + ((blk * Hkv + kvh) * HD + d) * BS + off;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) vp[(long)j * BS] = (bf16_t)v[j];
+    for (int j = 0; j < 4; ++j) {
+      const float a = bf2f((uint16_t)x1[j]), b = bf2f((uint16_t)x2[j]);
+      o1[j] = (short)f2bf(a * cc[j] - b * ss[j]);
+      o2[j] = (short)f2bf(b * cc[j] + a * ss[j]);
     }
+    bf16_t* kp = k_cache + ((blk * Hkv + kvh) * BS + off) * HD;
+    *reinterpret_cast<bf16x4_t*>(kp + i) = o1;
+    *reinterpret_cast<bf16x4_t*>(kp + half + i) = o2;
+  } else if (lane >= 16 && lane < 16 + HD / 4) {
+    const int d = 4 * (lane - 16);
+    const bf16x4_t v = *reinterpret_cast<const bf16x4_t*>(vrow + d);
+    bf16_t* vp = v_cache + ((blk * Hkv + kvh) * HD + d) * BS + off;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) vp[(long)j * BS] = (bf16_t)v[j];
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __threadfence_block();
-  __syncthreads();
 }
 
 // Partition length used for a sequence: the requested split-K granule, grown
@@ -320,23 +317,31 @@ __device__ __forceinline__ void decode_segment(
 #pragma unroll
   for (int s = 0; s < HD / 32; ++s)
     qf[s] = (c < G) ? load_frag16B(qrow + 32 * s + 8 * g) : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
-  if (rp.cos_sin) {   // fused rotary + cache write of this step's token
+  const int pg0 = t0 / BS, pg1 = (t1 + BS - 1) / BS;
+  // fused rotary + cache write of this step's token: every wave rotates its q
+  // fragments; the wave that will read the last page (the one holding
+  // position ctx-1, in the last partition) writes the new k / v first and
+  // retires those stores just before it loads that page
+  bool writer = false;
+  if (rp.cos_sin) {
     const float* cs = rp.cos_sin + (long)rp.positions[b] * HD;
     rope_q_frags<HD>(qf, cs, g);
-    if (p == nparts - 1) {   // the partition holding position ctx-1 reads the new k / v
+    writer = p == nparts - 1 && wave == (pg1 - 1 - pg0) % 4;
+    if (writer) {
       const bf16_t* krow = q + (long)b * q_stride + (long)(Hq + kvh) * HD;
       rope_write_kv<HD>(krow, krow + (long)Hkv * HD, cs, rp.slots[b], kvh, Hkv,
                         const_cast<bf16_t*>(k_cache), const_cast<bf16_t*>(v_cache));
+      if constexpr (MODE != 0 && MODE != 5) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
   }
 
   PageState<HD> st;
   state_init(st);
   const float scale_log2 = scale * LOG2E;
-  const int pg0 = t0 / BS, pg1 = (t1 + BS - 1) / BS;
   const int* bt = block_tables + (long)b * bt_stride;
   if constexpr (MODE == 0 || MODE == 5) {
     for (int pg = pg0 + wave; pg < pg1; pg += 4) {
+      if (writer && pg == pg1 - 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const long blk = bt[pg];
       const bf16_t* kp = k_cache + (blk * Hkv + kvh) * (BS * HD);
       const bf16_t* vp = v_cache + (blk * Hkv + kvh) * (BS * HD);
