@@ -67,7 +67,8 @@ def interleave(w: torch.Tensor, block: int) -> torch.Tensor:
     return w.view(2, I // block, block, d).transpose(0, 1).reshape(I2, d).contiguous()
 
 
-def run(model: str, tp: int, ms: list[int], margin: float, only: str = "") -> list[dict]:
+def run(model: str, tp: int, ms: list[int], margin: float, only: str = "",
+        swiglu16: bool = True) -> list[dict]:
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     cfgs = ops.native().dgemm_configs()
@@ -76,6 +77,10 @@ def run(model: str, tp: int, ms: list[int], margin: float, only: str = "") -> li
     for name, (N, K, epi) in shapes(model, tp).items():
         if only and name not in only.split(","):
             continue
+        # gate/up: the in-register SwiGLU over 16-column pairs (epi 3, one
+        # weight layout for every tile) unless --no-swiglu16 (epi 1, BN/2 blocks)
+        if epi == 1 and swiglu16:
+            epi = 3
         nbytes = N * K * 2
         ncopy = max(2, math.ceil((640 << 20) / nbytes))
         ws = [torch.randn(N, K, device=dev, dtype=torch.bfloat16) * 0.02 for _ in range(ncopy)]
@@ -83,7 +88,14 @@ def run(model: str, tp: int, ms: list[int], margin: float, only: str = "") -> li
         for M in ms:
             x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
             iters = max(ncopy, 40)
-            if epi:
+            if epi == 3:
+                if 16 not in wil:
+                    wil[16] = [interleave(w, ops.SWIGLU16) for w in ws]
+
+                def lib(i):
+                    ops.silu_mul(torch.nn.functional.linear(x, wil[16][i % ncopy]),
+                                 block=ops.SWIGLU16)
+            elif epi:
                 def lib(i):
                     ops.silu_mul(torch.nn.functional.linear(x, ws[i % ncopy]))
             else:
@@ -98,7 +110,9 @@ def run(model: str, tp: int, ms: list[int], margin: float, only: str = "") -> li
             timed = []
 
             def attempt(cfg, s, bm, bn):
-                if epi:
+                if epi == 3:
+                    wv = wil[16]
+                elif epi:
                     if bn not in wil:
                         wil[bn] = [interleave(w, bn // 2) for w in ws]
                     wv = wil[bn]
@@ -119,7 +133,7 @@ def run(model: str, tp: int, ms: list[int], margin: float, only: str = "") -> li
                 return t
 
             for cfg, (bm, bn) in enumerate(cfgs):
-                if N % bn:
+                if N % bn or (epi == 3 and not ops.swiglu16_ok(cfg)):
                     continue
                 tiles = -(-M // bm) * (N // bn)
                 if bm > 2 * max(64, M) and bm > 64:
@@ -282,7 +296,7 @@ def encoder(ms: list[int], write: bool = False) -> None:
             ref = torch.nn.functional.linear(x, w).float()
             best = None
             for cfg, (bm, bn) in enumerate(cfgs):
-                if N % bn:
+                if N % bn or (epi == 3 and not ops.swiglu16_ok(cfg)):
                     continue
                 out = ops.dgemm(x, w, cfg, 1)
                 if not (out.float() - ref).abs().max().item() <= 2e-2 * ref.abs().max().item():
@@ -322,6 +336,8 @@ def main(argv=None):
     ap.add_argument("--m", default=",".join(map(str, BUCKETS)))
     ap.add_argument("--only", default="", help="comma list of qkv,o,gate_up,down")
     ap.add_argument("--margin", type=float, default=0.03)
+    ap.add_argument("--no-swiglu16", action="store_true",
+                    help="gate/up with the LDS hand-off epilogue (epi 1) instead of epi 3")
     ap.add_argument("--write", action="store_true")
     ap.add_argument("--json", default="", help="also dump every timing row here")
     ap.add_argument("--from-rows", default="",
@@ -340,7 +356,7 @@ def main(argv=None):
     from ..engine.engine import _load_gemm_tuning
     _load_gemm_tuning()       # the library as served: hipBLASLt with the TunableOp table
     ms = [int(v) for v in a.m.split(",") if v]
-    rows, best = run(a.model, a.tp, ms, a.margin, a.only)
+    rows, best = run(a.model, a.tp, ms, a.margin, a.only, swiglu16=not a.no_swiglu16)
     if a.json:
         with open(a.json, "w") as f:
             json.dump(rows, f, indent=1)
@@ -357,10 +373,11 @@ def _write(best: list[dict], device: str) -> None:
             old = json.load(f)
     keys = {(e["N"], e["K"], e["epi"]) for e in best}
     kept = [e for e in old.get("entries", []) if (e["N"], e["K"], e.get("epi", 0)) not in keys]
-    doc = {"device": device,
-           "note": "decode GEMM dispatch measured by bench/dgemm_bench.py (cold weights); "
-                   "cfg -1 = the library keeps the bucket",
-           "entries": kept + best}
+    doc = dict(old)          # other sections (the "encoder" table) are kept
+    doc.update({"device": device,
+                "note": "decode GEMM dispatch measured by bench/dgemm_bench.py (cold weights); "
+                        "cfg -1 = the library keeps the bucket",
+                "entries": kept + best})
     with open(path, "w") as f:
         json.dump(doc, f, indent=1)
     print(f"wrote {len(doc['entries'])} entries to {path}")

@@ -97,6 +97,17 @@ __device__ __forceinline__ void dg_stage(bf16_t* lds_a, bf16_t* lds_w, const bf1
     dg_glds16<NT ? 2 : 0>(W + (long)(n0 + r) * ldw + k0 + 8 * (c ^ dg_swz<BK>(r)),
                           lds_w + (i * RPI + wave * RPW) * BK);
   }
+  if constexpr (BN % RPI != 0) {
+    // a tile width that is not a multiple of RPI rows (e.g. BN = 224): the
+    // waves below (BN % RPI) / RPW issue one more instruction (wave-uniform;
+    // the kernel's counted waits use per-wave counts)
+    constexpr int i = BN / RPI;
+    if (wave < (BN % RPI) / RPW) {
+      const int r = i * RPI + rr;
+      dg_glds16<NT ? 2 : 0>(W + (long)(n0 + r) * ldw + k0 + 8 * (c ^ dg_swz<BK>(r)),
+                            lds_w + (i * RPI + wave * RPW) * BK);
+    }
+  }
 }
 
 __device__ __forceinline__ float dg_silu(float g) { return g / (1.f + __expf(-g)); }
@@ -111,12 +122,17 @@ __global__ void __launch_bounds__(DTHREADS, 2) dgemm_kernel(
   constexpr int WN = 8 / WM;
   constexpr int WTM = BM / WM, WTN = BN / WN;       // wave tile
   constexpr int TM = WTM / 16, TN = WTN / 16;       // 16x16 MFMA tiles per wave
-  constexpr int LPS = (BM + BN) * BK / (DTHREADS * 8);  // LDS-DMA instructions per thread per stage
+  constexpr int RPI = DTHREADS * 8 / BK, RPW = RPI / 8;  // rows per glds instruction / per wave
+  // LDS-DMA instructions per thread per stage: LPS_F for the waves that stage
+  // the partial last W slab of a BN % RPI != 0 tile, LPS_P for the others
+  constexpr int LPS_P = BM / RPI + BN / RPI, LPS_F = LPS_P + (BN % RPI != 0);
+  constexpr int WFULL = BN % RPI == 0 ? 8 : (BN % RPI) / RPW;
   constexpr int STAGE = (BM + BN) * BK;             // bf16 elements per ring slot
   static_assert(WM * WN == 8 && TM >= 1 && TN >= 1 && WTM % 16 == 0 && WTN % 16 == 0, "tile");
   static_assert(BK == 32 || BK == 64, "BK");
-  static_assert(BM % (DTHREADS * 8 / BK) == 0 && BN % (DTHREADS * 8 / BK) == 0, "stage rows");
+  static_assert(BM % RPI == 0 && BN % RPW == 0, "stage rows");
   static_assert(EPI != 1 || (WN % 2 == 0 || WN == 1), "swiglu wave split");
+  static_assert(EPI != 3 || WTN % 32 == 0, "swiglu16: gate/up 16-column pairs inside a wave");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* const lds = reinterpret_cast<bf16_t*>(smem);
 
@@ -156,7 +172,11 @@ __global__ void __launch_bounds__(DTHREADS, 2) dgemm_kernel(
                                kbeg + ((p + rot) % nk) * BK);
     }
   for (int t = 0; t < nk; ++t) {
-    if (t + NST - 2 < nk) dg_vmwait<(NST - 2) * LPS>(); else dg_vmwait<0>();
+    if (t + NST - 2 < nk) {
+      if (wave < WFULL) dg_vmwait<(NST - 2) * LPS_F>(); else dg_vmwait<(NST - 2) * LPS_P>();
+    } else {
+      dg_vmwait<0>();
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (t + NST - 1 < nk) {       // refill the slot every wave finished reading at t-1
@@ -267,6 +287,27 @@ __global__ void __launch_bounds__(DTHREADS, 2) dgemm_kernel(
     }
     return;
   }
+  if constexpr (EPI == 3) {
+    // SwiGLU on 16-column pairs (ops.interleave_gate_up(w, 16): W rows
+    // [16 gate | 16 up] per 16 channels): tiles 2j and 2j+1 of a wave are the
+    // gate and up values of the same 16 channels in the same lane registers,
+    // so the epilogue needs no LDS hand-off and any BN with WTN % 32 == 0 works
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + wr * WTM + 16 * i + fr;
+      if (m >= M) continue;
+#pragma unroll
+      for (int j = 0; j < TN / 2; ++j) {
+        bf16x4_t o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          o[r] = (short)f2bf(dg_silu(acc[i][2 * j][r]) * acc[i][2 * j + 1][r]);
+        *reinterpret_cast<bf16x4_t*>(C + (long)m * ldc + ((n0 + wc * WTN) >> 1) + 16 * j +
+                                     4 * fg) = o;
+      }
+    }
+    return;
+  }
   constexpr int HALF = BN / 2, ULD = HALF + 4;
   if constexpr (WN == 1) {
     // one wave column holds both halves: gate tiles j < TN/2, up tiles j + TN/2
@@ -347,6 +388,12 @@ static const DgCfg kDgCfgs[] = {
     {256, 256, 4, 5, 1, 32},   // 20
     {256, 128, 4, 6, 1, 32},   // 21
     {128, 256, 2, 6, 1, 32},   // 22
+    // 224-column tiles (28672 = 128 x 224: one workgroup per CU at M = 256 with
+    // 128-row tiles), 8 x 1 waves; the W slab's last 32 rows are staged by
+    // waves 0-3 only
+    {128, 224, 8, 3, 1, 64},   // 23
+    {256, 224, 8, 2, 1, 64},   // 24
+    {256, 224, 8, 4, 1, 32},   // 25
 };
 constexpr int kNumDgCfgs = sizeof(kDgCfgs) / sizeof(kDgCfgs[0]);
 
@@ -387,7 +434,7 @@ int dgemm(void* C, const void* A, const void* W, float* slabs, unsigned* tickets
   if (M <= 0) return 0;
   const int nt = (cfg >> 5) & 1;      // bit 5: non-temporal weight stream
   cfg &= 31;
-  if (cfg < 0 || cfg >= kNumDgCfgs || splits < 1 || epi < 0 || epi > 2) return -1;
+  if (cfg < 0 || cfg >= kNumDgCfgs || splits < 1 || epi < 0 || epi > 3) return -1;
   const DgCfg c = kDgCfgs[cfg];
   if (N % c.bn != 0 || K % (splits * c.bk) != 0) return -1;
   if (epi == 2 && slabs == nullptr) return -2;
@@ -399,6 +446,12 @@ int dgemm(void* C, const void* A, const void* W, float* slabs, unsigned* tickets
   auto A_ = (const bf16_t*)A;
   auto W_ = (const bf16_t*)W;
 #define LMX_DG_E(BM, BN, WM, NST, ROT, NT, BK)                                                 \
+  if (epi == 3) {                                                                             \
+    if constexpr ((BN / (8 / WM)) % 32 == 0)                                                  \
+      return dg_launch<BM, BN, WM, NST, 3, ROT, NT, BK>(C_, A_, W_, slabs, tickets, M, N, K, \
+                                                        lda, ldw, ldc, splits, stream);       \
+    return -1;                                                                                \
+  }                                                                                           \
   if (epi == 1)                                                                               \
     return dg_launch<BM, BN, WM, NST, 1, ROT, NT, BK>(C_, A_, W_, slabs, tickets, M, N, K, lda, \
                                                       ldw, ldc, splits, stream);              \
@@ -435,6 +488,9 @@ int dgemm(void* C, const void* A, const void* W, float* slabs, unsigned* tickets
     LMX_DG(20, 256, 256, 4, 5, 1, 32)
     LMX_DG(21, 256, 128, 4, 6, 1, 32)
     LMX_DG(22, 128, 256, 2, 6, 1, 32)
+    LMX_DG(23, 128, 224, 8, 3, 1, 64)
+    LMX_DG(24, 256, 224, 8, 2, 1, 64)
+    LMX_DG(25, 256, 224, 8, 4, 1, 32)
   }
 #undef LMX_DG
 #undef LMX_DG_E

@@ -611,20 +611,36 @@ def linear(x: torch.Tensor, w: torch.Tensor, defer: bool = False):
 def linear_swiglu(x: torch.Tensor, w: torch.Tensor, block: int) -> torch.Tensor:
     """silu(gate) * up of x @ w^T for gate|up weights interleaved per
     ``block`` channels: the fused-epilogue decode GEMM where the table picks
-    it (its BN must be 2 * block), else the library GEMM + the GLU kernel."""
+    it, else the library GEMM + the GLU kernel.  block 16: the in-register
+    epilogue over 16-column gate/up pairs (epi 3, any tile width); otherwise
+    the LDS hand-off form (epi 1, tile BN = 2 * block)."""
     if x.is_cuda and x.dim() == 2:
-        ch = dgemm_choice(x.shape[0], w.shape[0], w.shape[1], epi=1)
-        if ch is not None and DGEMM_CONFIGS[ch[0] & DGEMM_CFG_MASK][1] == 2 * block:
-            return dgemm(x, w, ch[0], ch[1], epi=1)
+        if block == SWIGLU16:
+            ch = dgemm_choice(x.shape[0], w.shape[0], w.shape[1], epi=3)
+            if ch is not None:
+                return dgemm(x, w, ch[0], ch[1], epi=3)
+        else:
+            ch = dgemm_choice(x.shape[0], w.shape[0], w.shape[1], epi=1)
+            if ch is not None and DGEMM_CONFIGS[ch[0] & DGEMM_CFG_MASK][1] == 2 * block:
+                return dgemm(x, w, ch[0], ch[1], epi=1)
     return silu_mul(linear(x, w), block=block)
 
 
 def swiglu_block(N: int, K: int) -> int:
     """Interleave block of the gate|up weights for the fused decode GEMM of
-    this shape (BN/2 of the measured configurations), 0 = not fused."""
+    this shape: 16 when the table has in-register-epilogue (epi 3) entries,
+    else BN/2 of the measured epi-1 configurations; 0 = not fused."""
+    if any(cfg >= 0 for m, cfg, s in _dg_table().get((N, K, 3), ())):
+        return SWIGLU16
     bns = {DGEMM_CONFIGS[cfg & DGEMM_CFG_MASK][1]
            for m, cfg, s in _dg_table().get((N, K, 1), ()) if cfg >= 0}
     return min(bns) // 2 if bns else 0
+
+
+def swiglu16_ok(cfg: int) -> bool:
+    """Configuration can run the epi-3 (16-column pair) SwiGLU epilogue."""
+    c = cfg & DGEMM_CFG_MASK
+    return (DGEMM_CONFIGS[c][1] * DGEMM_WM[c] // 8) % 32 == 0
 
 
 # ---------------------------------------------------------------------------
@@ -634,7 +650,12 @@ def swiglu_block(N: int, K: int) -> int:
 DGEMM_CONFIGS = [(256, 128), (128, 128), (64, 128), (256, 64), (128, 64), (64, 64), (128, 256),
                  (64, 64), (128, 64), (64, 128), (128, 128), (128, 256), (256, 128), (256, 256),
                  (64, 64), (128, 64), (64, 128), (128, 128), (128, 256),
-                 (256, 256), (256, 256), (256, 128), (128, 256)]     # 19-22: 32-deep K-steps
+                 (256, 256), (256, 256), (256, 128), (128, 256),     # 19-22: 32-deep K-steps
+                 (128, 224), (256, 224), (256, 224)]                 # 23-25: 224-column tiles
+# waves along M of each configuration (dgemm.hip kDgCfgs): the fused SwiGLU on
+# 16-column gate/up pairs (epi 3) needs a wave tile width BN*WM/8 divisible by 32
+DGEMM_WM = [4, 2, 2, 8, 4, 2, 2, 2, 4, 2, 2, 2, 4, 4, 2, 4, 2, 2, 2, 4, 4, 4, 2, 8, 8, 8]
+SWIGLU16 = 16              # gate/up interleave block of the epi-3 form
 DGEMM_MAX_M = 256
 # a configuration id with bit 5 set (cfg | DGEMM_NT) streams the weights
 # non-temporal (dgemm.hip NT): the low bits select the tile
@@ -750,15 +771,19 @@ def dgemm(a: torch.Tensor, w: torch.Tensor, cfg: int, splits: int, epi: int = 0,
           out: torch.Tensor | None = None) -> torch.Tensor:
     """a @ w^T for decode-sized M on the K11 kernel; epi=1: ``w`` interleaved
     per BN-column tile as [BN/2 gate | BN/2 up] rows (``interleave_gate_up``
-    with ``block=BN/2``) and the result is silu(gate) * up (N/2 columns)."""
+    with ``block=BN/2``) and the result is silu(gate) * up (N/2 columns);
+    epi=3: the same with ``w`` interleaved per 16 rows (block 16, any tile
+    whose wave tile width is a multiple of 32, ``swiglu16_ok``)."""
     M, K = a.shape
     N = w.shape[0]
     bm, bn = DGEMM_CONFIGS[cfg & DGEMM_CFG_MASK]
-    ncols = N // 2 if epi else N
+    ncols = N // 2 if epi in (1, 3) else N
+    _chk(epi != 3 or swiglu16_ok(cfg), f"dgemm cfg {cfg} cannot run the epi-3 epilogue")
     if not a.is_cuda:
         y = a.float() @ w.float().t()
-        if epi:
-            y = y.view(M, N // bn, 2, bn // 2)
+        if epi in (1, 3):
+            blk = SWIGLU16 if epi == 3 else bn // 2
+            y = y.view(M, N // (2 * blk), 2, blk)
             y = (torch.nn.functional.silu(y[:, :, 0]) * y[:, :, 1]).reshape(M, ncols)
         y = y.to(a.dtype)
         if out is not None:

@@ -164,7 +164,10 @@ def test_llama3_8b_shapes_on_decode_gemm_match_dense(graphs):
     e = LLMEngine(EngineConfig(model="llama-3-8b", max_num_seqs=64, max_batched_tokens=512,
                                max_model_len=512, use_graphs=graphs, kv_cache_gb=1),
                   device="cuda", model_cfg=cfg)
-    assert e.model.gu_block == 64, "fused SwiGLU layout not selected from the table"
+    # 16: the in-register epilogue over 16-column gate/up pairs (epi 3 table
+    # entries); BN/2 of the LDS hand-off form (epi 1) when only those exist
+    assert e.model.gu_block == ops.swiglu_block(2 * cfg.intermediate_size, cfg.hidden_size) > 0, \
+        "fused SwiGLU layout not selected from the table"
     prompts = [[(17 * i + 3 * j) % 120000 + 100 for j in range(4)] for i in range(48)]
     outs = e.generate(prompts, SamplingParams(temperature=0, max_tokens=3, ignore_eos=True))
     assert ops.DGEMM_CALLS[0] > n0

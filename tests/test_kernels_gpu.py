@@ -524,14 +524,18 @@ def test_apply_penalties_vs_reference():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg", list(range(23)) + [c | 32 for c in (1, 4, 6, 13, 19)])
+@pytest.mark.parametrize("cfg", list(range(len(ops.DGEMM_CONFIGS))) +
+                         [c | 32 for c in (1, 4, 6, 13, 19, 23)])
 @pytest.mark.parametrize("M", [1, 37, 64, 130, 256])
 def test_dgemm_configs_vs_fp32(cfg, M):
     """K11 decode GEMM: every tile configuration (and some with the
-    non-temporal weight stream, cfg | DGEMM_NT), split-K 1/2/4, both
-    epilogues, against an fp32 PyTorch reference (rows past M masked)."""
+    non-temporal weight stream, cfg | DGEMM_NT), split-K 1/2/4, every
+    epilogue (plain; SwiGLU with the LDS hand-off, epi 1; SwiGLU on 16-column
+    pairs, epi 3, where the wave tile allows), against an fp32 PyTorch
+    reference (rows past M masked).  224-column tiles stage their last W slab
+    from half the waves (per-wave counted waits)."""
     bm, bn = ops.DGEMM_CONFIGS[cfg & ops.DGEMM_CFG_MASK]
-    K, N = 1024, 2 * 1024
+    K, N = 1024, (1792 if bn == 224 else 2 * 1024)
     a = torch.randn(M, K, device=DEV).to(torch.bfloat16)
     w = (torch.randn(N, K, device=DEV) * K ** -0.5).to(torch.bfloat16)
     y = a.float() @ w.float().t()
@@ -546,6 +550,9 @@ def test_dgemm_configs_vs_fp32(cfg, M):
         g = torch.nn.functional.silu(y[:, :I]) * y[:, I:]
         out3 = ops.dgemm(a, wil, cfg, s, epi=1)
         torch.testing.assert_close(out3.float(), g, atol=2e-2, rtol=2e-2)
+        if ops.swiglu16_ok(cfg):
+            out4 = ops.dgemm(a, ops.interleave_gate_up(w, ops.SWIGLU16), cfg, s, epi=3)
+            torch.testing.assert_close(out4.float(), g, atol=2e-2, rtol=2e-2)
 
 
 @pytest.mark.gpu
