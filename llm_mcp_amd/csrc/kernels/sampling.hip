@@ -3,8 +3,9 @@
 // log-probability (for OpenAI `logprobs` / usage accounting).
 //
 // One 1024-thread workgroup per row; the row (128256 logits for Llama-3) is
-// streamed from L2 once per pass, no sort.  Sampling is Gumbel-max
-// (argmax z_i + G_i == a draw from softmax(z)); truncation uses rejection
+// streamed from L2 once per pass, no sort.  Sampling is inverse-CDF in a
+// fixed element order (one uniform per row and round, see the pass structure
+// below); truncation uses rejection
 // with a pivot: draw j from the distribution restricted to {z > pivot}; accept
 // iff j is inside both the nucleus (mass strictly above j < top_p) and the
 // top-k set (count strictly above j < k); otherwise pivot = z_j.  Every
@@ -34,21 +35,12 @@ __device__ __forceinline__ uint32_t lowbias32(uint32_t x) {
   return x;
 }
 
-// Per element: a 32-bit counter hash keyed by a 64-bit (seed, offset, round)
-// key mixed once per row-round (the 64-bit mixing stays off the per-element
-// path: 64-bit multiplies are multi-instruction on CDNA).
+// A 64-bit (seed, offset, round) key mixed once per row-round.
 struct RowKey { uint32_t k0, k1; };
 
 __device__ __forceinline__ RowKey row_key(uint64_t seed, uint64_t off, int round) {
   const uint64_t h = mix64(seed ^ mix64(off * 0x9E3779B97F4A7C15ULL + (uint64_t)round));
   return RowKey{(uint32_t)h, (uint32_t)(h >> 32)};
-}
-
-// Gumbel(0,1) noise for element i
-__device__ __forceinline__ float gumbel(RowKey k, int i) {
-  const uint32_t h = lowbias32(lowbias32((uint32_t)i * 0x9E3779B9u ^ k.k0) ^ k.k1);
-  const float u = ((float)(h >> 8) + 0.5f) * (1.0f / 16777216.0f);
-  return -__logf(-__logf(u));
 }
 
 template <typename T>
@@ -76,6 +68,13 @@ __device__ __forceinline__ void scan_row(const T* __restrict__ x, int V, F&& f) 
     done = nv * VEC;
   }
   for (int i = done + threadIdx.x; i < V; i += blockDim.x) f(i, ld<T>(x, i));
+}
+
+// scan_row already visits only the calling thread's elements, in a fixed
+// order; the inverse-CDF walk re-reads them in that same order
+template <typename T, typename F>
+__device__ __forceinline__ void scan_row_own(const T* __restrict__ x, int V, F&& f) {
+  scan_row(x, V, static_cast<F&&>(f));
 }
 
 struct ArgMax { float v; int i; };
@@ -131,11 +130,80 @@ __device__ __forceinline__ MaxSum block_maxsum(MaxSum a, float inv_t, float* sv,
 }
 
 // Pass structure (the row is 128256 logits = 256 KB in bf16; B rows do not
-// fit the L2s, so passes are the cost):
-//   pass 1: online max + softmax normaliser + the first Gumbel-max draw,
-//           all from one read of the row;
-//   pass 2 (only with top-k/top-p): mass and count strictly above the
-//           draw -> accept (~1 - top_p rejections) or pivot and redraw.
+// fit the L2s, so passes are the cost, and per-element VALU work decides each
+// pass's time -- the round-1 Gumbel-max draw spent two logs and a 64-bit-free
+// hash per element):
+//   pass 1: online max + softmax normaliser S (one exp per element);
+//   draw:   inverse CDF in the threads' element order: every thread sums the
+//           p_i = exp((x_i - xmax) / T) of its own elements (the scan_row
+//           order: coalesced), a block scan of the 1024 sums places one
+//           uniform u * total in one thread, which walks its own elements
+//           again to the index (exact sampling from the restricted
+//           distribution for any fixed element order);
+//   check:  (top-k / top-p only) mass and count strictly above the draw ->
+//           accept (~1 - top_p rejections) or pivot on it and redraw.
+// Seeded per (seed, offset, round): batch-composition independent.
+__device__ __forceinline__ float row_uniform(uint64_t seed, uint64_t off, int round) {
+  const RowKey k = row_key(seed, off, round);
+  return ((float)(k.k0 >> 8) + 0.5f) * (1.0f / 16777216.0f);   // (0, 1)
+}
+
+// exclusive block scan of one float per thread (1024 threads); also the total
+__device__ __forceinline__ float block_excl_scan(float v, float* sv, float* total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  float inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float t = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += t;
+  }
+  __syncthreads();
+  if (lane == 63) sv[wid] = inc;
+  __syncthreads();
+  float wbase = 0.f, tot = 0.f;
+  for (int w2 = 0; w2 < nw; ++w2) {
+    const float t = sv[w2];
+    if (w2 < wid) wbase += t;
+    tot += t;
+  }
+  *total = tot;
+  return wbase + inc - v;
+}
+
+// One draw restricted to {x > pivot_x} (pivot_x = -inf: the full row).
+// Returns the index (every thread), or -1 when rounding left the target past
+// the total (probability ~2^-24; the caller falls back to the argmax).
+template <typename T>
+__device__ __forceinline__ int icdf_draw(const T* __restrict__ x, int V, float xmax, float inv_t,
+                                         float pivot_x, float u, float* sv, int* sel) {
+  float loc = 0.f;
+  scan_row(x, V, [&](int i, float v) {
+    if (v > pivot_x) loc += __expf((v - xmax) * inv_t);
+  });
+  float tot;
+  const float pre = block_excl_scan(loc, sv, &tot);
+  const float target = u * tot;
+  if (threadIdx.x == 0) *sel = -1;
+  __syncthreads();
+  if (loc > 0.f && target >= pre && target < pre + loc) {
+    // this thread's elements hold the target: walk them in the same order
+    float acc = pre;
+    int j = -1, last = -1;
+    scan_row_own(x, V, [&](int i, float v) {
+      if (j < 0 && v > pivot_x) {
+        acc += __expf((v - xmax) * inv_t);
+        last = i;
+        if (acc > target) j = i;
+      }
+    });
+    *sel = j >= 0 ? j : last;
+  }
+  __syncthreads();
+  const int r = *sel;
+  __syncthreads();   // sel is rewritten by the next draw
+  return r;
+}
+
 template <typename T>
 __global__ void __launch_bounds__(1024) sample_kernel(
     const T* __restrict__ logits, long stride, int V, const float* __restrict__ temperature,
@@ -144,6 +212,7 @@ __global__ void __launch_bounds__(1024) sample_kernel(
     float* __restrict__ out_logprob, int max_rounds) {
   __shared__ float sv[16], sv2[16];
   __shared__ int si[16];
+  __shared__ int sel;
   const int row = blockIdx.x;
   const T* x = logits + (long)row * stride;
   const float temp = temperature ? temperature[row] : 0.f;
@@ -171,60 +240,41 @@ __global__ void __launch_bounds__(1024) sample_kernel(
   const float inv_t = 1.f / temp;
   const uint64_t seed = seeds ? seeds[row] : 0x1234ULL;
   const uint64_t off = offsets ? (uint64_t)offsets[row] : 0ULL;
-  // pass 1
-  RowKey key = row_key(seed, off, 0);
-  ArgMax g{-INFINITY, 0x7fffffff};
+  // pass 1: max and normaliser
   MaxSum ms{-INFINITY, 0.f};
   scan_row(x, V, [&](int i, float v) {
     if (v > ms.m) { ms.s = ms.s * __expf((ms.m - v) * inv_t) + 1.f; ms.m = v; }
     else ms.s += __expf((v - ms.m) * inv_t);
-    const float k = v * inv_t + gumbel(key, i);
-    if (k > g.v) { g.v = k; g.i = i; }
   });
-  g = block_argmax(g, sv, si);
   ms = block_maxsum(ms, inv_t, sv, sv2);
   const float xmax = ms.m, S = ms.s;        // z_i = (x_i - xmax) / T, S = sum exp(z)
   const float tp = top_p ? top_p[row] : 1.f;
   const bool truncate = (tp < 1.f) || (kk > 0 && kk < V);
-  int chosen = g.i;
-  if (truncate) {
-    float pivot = -INFINITY;
-    chosen = -1;
-    int j = g.i;
-    for (int round = 0; round < max_rounds; ++round) {
-      if (round > 0) {
-        // redraw restricted to z > pivot
-        key = row_key(seed, off, round);
-        ArgMax h{-INFINITY, 0x7fffffff};
-        scan_row(x, V, [&](int i, float v) {
-          const float z = (v - xmax) * inv_t;
-          if (z > pivot) {
-            const float k = z + gumbel(key, i);
-            if (k > h.v) { h.v = k; h.i = i; }
-          }
-        });
-        j = block_argmax(h, sv, si).i;
-      }
-      float mass = 0.f, cnt = 0.f;
-      // z > zj  <=>  x > xj (T > 0): compare raw logits, exp only above
-      const float xj = ld<T>(x, j);
-      scan_row(x, V, [&](int i, float v) {
-        if (v > xj) { mass += __expf((v - xmax) * inv_t); cnt += 1.f; }
-      });
-      mass = block_sum(mass, sv) / S;
-      cnt = block_sum(cnt, sv);
-      const bool in_p = mass < tp;
-      const bool in_k = (kk <= 0) || (cnt < (float)kk);
-      if (in_p && in_k) { chosen = j; break; }
-      pivot = (xj - xmax) * inv_t;
-    }
-    if (chosen < 0) {   // fallback: the argmax is inside every truncation
-      ArgMax am{-INFINITY, 0x7fffffff};
-      scan_row(x, V, [&](int i, float v) {
-        if (v > am.v) { am.v = v; am.i = i; }
-      });
-      chosen = block_argmax(am, sv, si).i;
-    }
+  int chosen = -1;
+  float pivot_x = -INFINITY;
+  for (int round = 0; round < (truncate ? max_rounds : 1); ++round) {
+    const int j = icdf_draw(x, V, xmax, inv_t, pivot_x, row_uniform(seed, off, round), sv, &sel);
+    if (j < 0) break;
+    if (!truncate) { chosen = j; break; }
+    float mass = 0.f, cnt = 0.f;
+    // z > zj  <=>  x > xj (T > 0): compare raw logits, exp only above
+    const float xj = ld<T>(x, j);
+    scan_row(x, V, [&](int i, float v) {
+      if (v > xj) { mass += __expf((v - xmax) * inv_t); cnt += 1.f; }
+    });
+    mass = block_sum(mass, sv) / S;
+    cnt = block_sum(cnt, sv);
+    const bool in_p = mass < tp;
+    const bool in_k = (kk <= 0) || (cnt < (float)kk);
+    if (in_p && in_k) { chosen = j; break; }
+    pivot_x = xj;
+  }
+  if (chosen < 0) {   // fallback: the argmax is inside every truncation
+    ArgMax am{-INFINITY, 0x7fffffff};
+    scan_row(x, V, [&](int i, float v) {
+      if (v > am.v) { am.v = v; am.i = i; }
+    });
+    chosen = block_argmax(am, sv, si).i;
   }
   if (threadIdx.x == 0) {
     out_tok[row] = chosen;

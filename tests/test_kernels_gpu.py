@@ -342,6 +342,31 @@ def test_sample_distribution_matches_softmax():
     assert torch.allclose(freq, expect, atol=0.03), (freq, expect)
 
 
+def test_sample_distribution_full_vocab():
+    """Inverse-CDF draw over the whole 128k vocabulary: five hot tokens placed
+    in different threads' element sets (a flat tail carries the remaining
+    ~0.7 % of the mass) are drawn at their softmax frequencies; with top_p
+    0.8 only the nucleus (mass strictly above < 0.8) is ever drawn."""
+    V, B = 128256, 4096
+    hot = torch.tensor([3, 40001, 77777, 100000, 128255], device=DEV)
+    lg = torch.zeros(V, device=DEV)
+    lg[hot] = torch.tensor([16.0, 15.5, 15.0, 14.0, 13.0], device=DEV)
+    lg = lg.repeat(B, 1).to(torch.bfloat16)
+    seeds = torch.arange(B, dtype=torch.int64, device=DEV) * 131 + 7
+    t, k, p, _, off = _params(B, t=1.0)
+    tok, _ = ops.sample(lg, t, k, p, seeds, off)
+    probs = torch.softmax(lg[0].float(), -1)
+    cnt = torch.bincount(tok.long(), minlength=V).float() / B
+    torch.testing.assert_close(cnt[hot], probs[hot], atol=0.03, rtol=0)
+    t, k, p, _, off = _params(B, t=1.0, p=0.8)
+    tok, _ = ops.sample(lg, t, k, p, seeds, off)
+    order = probs.argsort(descending=True)
+    above = torch.cumsum(probs[order], 0) - probs[order]
+    nucleus = set(order[above < 0.8].tolist())
+    assert nucleus == set(hot[:3].tolist())
+    assert set(tok.tolist()) == nucleus
+
+
 def test_sample_top_k_top_p_support():
     V, B = 1000, 2048
     lg = torch.randn(V, device=DEV).repeat(B, 1) * 2
