@@ -134,9 +134,11 @@ __device__ __forceinline__ MaxSum block_maxsum(MaxSum a, float inv_t, float* sv,
 // pass's time -- the round-1 Gumbel-max draw spent two logs and a 64-bit-free
 // hash per element):
 //   pass 1: online max + softmax normaliser S (one exp per element);
-//   draw:   inverse CDF in the threads' element order: every thread sums the
-//           p_i = exp((x_i - xmax) / T) of its own elements (the scan_row
-//           order: coalesced), a block scan of the 1024 sums places one
+//   draw:   inverse CDF in the threads' element order: every thread's sum of
+//           the p_i = exp((x_i - xmax) / T) of its own elements (the scan_row
+//           order: coalesced; for the first draw it is the thread's pass-1
+//           online normaliser rescaled to the row max, so no extra pass), a
+//           block scan of the 1024 sums places one
 //           uniform u * total in one thread, which walks its own elements
 //           again to the index (exact sampling from the restricted
 //           distribution for any fixed element order);
@@ -173,13 +175,19 @@ __device__ __forceinline__ float block_excl_scan(float v, float* sv, float* tota
 // One draw restricted to {x > pivot_x} (pivot_x = -inf: the full row).
 // Returns the index (every thread), or -1 when rounding left the target past
 // the total (probability ~2^-24; the caller falls back to the argmax).
+// loc_in >= 0: this thread's sum is already known (the first draw reuses the
+// thread's pass-1 online normaliser, rescaled to the row max: no extra pass).
 template <typename T>
 __device__ __forceinline__ int icdf_draw(const T* __restrict__ x, int V, float xmax, float inv_t,
-                                         float pivot_x, float u, float* sv, int* sel) {
-  float loc = 0.f;
-  scan_row(x, V, [&](int i, float v) {
-    if (v > pivot_x) loc += __expf((v - xmax) * inv_t);
-  });
+                                         float pivot_x, float u, float* sv, int* sel,
+                                         float loc_in = -1.f) {
+  float loc = loc_in;
+  if (loc < 0.f) {
+    loc = 0.f;
+    scan_row(x, V, [&](int i, float v) {
+      if (v > pivot_x) loc += __expf((v - xmax) * inv_t);
+    });
+  }
   float tot;
   const float pre = block_excl_scan(loc, sv, &tot);
   const float target = u * tot;
@@ -246,14 +254,19 @@ __global__ void __launch_bounds__(1024) sample_kernel(
     if (v > ms.m) { ms.s = ms.s * __expf((ms.m - v) * inv_t) + 1.f; ms.m = v; }
     else ms.s += __expf((v - ms.m) * inv_t);
   });
+  const MaxSum mine = ms;
   ms = block_maxsum(ms, inv_t, sv, sv2);
   const float xmax = ms.m, S = ms.s;        // z_i = (x_i - xmax) / T, S = sum exp(z)
+  // this thread's share of S: the first (unrestricted) draw needs no pass
+  const float loc0 = mine.m == -INFINITY ? 0.f : mine.s * __expf((mine.m - xmax) * inv_t);
   const float tp = top_p ? top_p[row] : 1.f;
   const bool truncate = (tp < 1.f) || (kk > 0 && kk < V);
   int chosen = -1;
   float pivot_x = -INFINITY;
+  float loc = loc0;       // this thread's mass above the pivot, for the next draw
   for (int round = 0; round < (truncate ? max_rounds : 1); ++round) {
-    const int j = icdf_draw(x, V, xmax, inv_t, pivot_x, row_uniform(seed, off, round), sv, &sel);
+    const int j = icdf_draw(x, V, xmax, inv_t, pivot_x, row_uniform(seed, off, round), sv, &sel,
+                            loc);
     if (j < 0) break;
     if (!truncate) { chosen = j; break; }
     float mass = 0.f, cnt = 0.f;
@@ -262,6 +275,10 @@ __global__ void __launch_bounds__(1024) sample_kernel(
     scan_row(x, V, [&](int i, float v) {
       if (v > xj) { mass += __expf((v - xmax) * inv_t); cnt += 1.f; }
     });
+    // on rejection the pivot becomes xj, and this thread's mass above xj is
+    // exactly its share of the restricted distribution: the redraw needs no
+    // pass of its own (one pass per rejection round)
+    loc = mass;
     mass = block_sum(mass, sv) / S;
     cnt = block_sum(cnt, sv);
     const bool in_p = mass < tp;
