@@ -323,9 +323,11 @@ __device__ __forceinline__ void decode_segment(
   // position ctx-1, in the last partition) writes the new k / v first and
   // retires those stores just before it loads that page
   bool writer = false;
+  const float* cs = nullptr;
   if (rp.cos_sin) {
-    const float* cs = rp.cos_sin + (long)rp.positions[b] * HD;
-    rope_q_frags<HD>(qf, cs, g);
+    cs = rp.cos_sin + (long)rp.positions[b] * HD;
+    // the one-page-at-a-time loops rotate q under their first page's loads
+    if constexpr (MODE != 0 && MODE != 5) rope_q_frags<HD>(qf, cs, g);
     writer = p == nparts - 1 && wave == (pg1 - 1 - pg0) % 4;
     if (writer) {
       const bf16_t* krow = q + (long)b * q_stride + (long)(Hq + kvh) * HD;
@@ -340,7 +342,23 @@ __device__ __forceinline__ void decode_segment(
   const float scale_log2 = scale * LOG2E;
   const int* bt = block_tables + (long)b * bt_stride;
   if constexpr (MODE == 0 || MODE == 5) {
-    for (int pg = pg0 + wave; pg < pg1; pg += 4) {
+    int pg = pg0 + wave;
+    if (cs) {
+      if (pg < pg1 && !(writer && pg == pg1 - 1)) {
+        // first page: its K/V fragments are in flight while q rotates (the
+        // rotation's cos/sin round trip no longer serialises the segment)
+        const long blk = bt[pg];
+        PageFrags<HD> f;
+        load_page(f, k_cache + (blk * Hkv + kvh) * (BS * HD),
+                  v_cache + (blk * Hkv + kvh) * (BS * HD));
+        rope_q_frags<HD>(qf, cs, g);
+        compute_page(st, qf, f, pg * BS, t1 - 1, scale_log2);
+        pg += 4;
+      } else {
+        rope_q_frags<HD>(qf, cs, g);
+      }
+    }
+    for (; pg < pg1; pg += 4) {
       if (writer && pg == pg1 - 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const long blk = bt[pg];
       const bf16_t* kp = k_cache + (blk * Hkv + kvh) * (BS * HD);
