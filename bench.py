@@ -65,6 +65,13 @@ def parse(argv=None):
     ap.add_argument("--loadgen-procs", type=int, default=0,
                     help="load-generator processes (0: N)")
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--load", choices=("waves", "closed"), default="waves",
+                    help="waves (the headline: K synchronized waves of C streams per GPU) or "
+                         "closed (C streams per GPU at constant concurrency, each client sending "
+                         "its next request when its stream ends, for --duration seconds after "
+                         "--closed-warmup seconds; a separate record, never the headline)")
+    ap.add_argument("--duration", type=float, default=30.0)
+    ap.add_argument("--closed-warmup", type=float, default=10.0)
     ap.add_argument("--rehearse-on-one-gpu", action="store_true",
                     help="multi-rank rehearsal on a 1-GPU box: every rank uses device 0 with a "
                          "fixed KV budget (never used for reported numbers)")
@@ -238,6 +245,11 @@ def main() -> None:
         return sum(sum(p.cpu_times()[:2]) for p in ps)
     cpu0 = {k: cpu_s(v) for k, v in procs.items()}
 
+    if a.load == "closed":
+        closed(a, rank, world, lgs, barrier)
+        shutdown(a, world, lgs, apis, server, ready_files)
+        return
+
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -321,6 +333,10 @@ def main() -> None:
                                             f"{world}-GPU number)"
         print(json.dumps(out), flush=True)
     barrier()
+    shutdown(a, world, lgs, apis, server, ready_files)
+
+
+def shutdown(a, world, lgs, apis, server, ready_files) -> None:
     for p in lgs:
         try:
             p.wait(timeout=30)
@@ -338,7 +354,50 @@ def main() -> None:
         if os.path.exists(f):
             os.unlink(f)
     if world > 1:
+        import torch.distributed as dist
         dist.destroy_process_group()
+
+
+def closed(a, rank, world, lgs, barrier) -> None:
+    """--load closed: one constant-concurrency window through the same front
+    door; prints its own JSON line (metric tagged "closed loop")."""
+    import torch
+    from llm_mcp_amd.bench.loadgen import percentile
+    barrier()
+    torch.cuda.synchronize()
+    parts = []
+    if rank == 0:
+        for p in lgs:
+            p.stdin.write(f"closed {a.closed_warmup} {a.duration}\n")
+            p.stdin.flush()
+        for p in lgs:
+            parts.append(json.loads(p.stdout.readline()))
+    barrier()
+    if rank == 0:
+        tok = sum(x["tokens"] for x in parts)
+        ttfts = [t for x in parts for t in x["ttfts"]]
+        itls = [t for x in parts for t in x["itls"]]
+        out = {"metric": METRIC + " [closed loop]", "value": round(tok / a.duration, 1),
+               "unit": "tokens/s", "n_gpus": world, "duration_s": a.duration,
+               "requests": sum(x["requests"] for x in parts), "dtype": "bf16",
+               "data": "synthetic prompts, random-init weights",
+               "ttft_p50_ms": round(percentile(ttfts, 50) * 1e3, 1),
+               "ttft_p95_ms": round(percentile(ttfts, 95) * 1e3, 1),
+               "itl_p50_ms": round(percentile(itls, 50) * 1e3, 2),
+               "itl_p95_ms": round(percentile(itls, 95) * 1e3, 2),
+               "config": {"model": a.model, "concurrency": a.concurrency * world,
+                          "prompt_len": a.prompt_len, "max_tokens": a.max_tokens,
+                          "load": f"closed loop: {a.concurrency} streams per GPU, next request "
+                                  f"on stream end, {a.closed_warmup:g} s warm-up, "
+                                  f"{a.duration:g} s window",
+                          "sampling": {"temperature": a.temperature, "top_p": a.top_p}}}
+        if a.rehearse_on_one_gpu:
+            out["rehearsal_one_gpu"] = True
+        print(json.dumps(out), flush=True)
+        for p in lgs:
+            p.stdin.write("quit\n")
+            p.stdin.flush()
+    barrier()
 
 
 if __name__ == "__main__":

@@ -8,7 +8,8 @@ interpolation.
 
 Runs standalone (``python -m llm_mcp_amd.bench.loadgen --url ...``) or as the
 client subprocess of bench.py: then it reads one command per line on stdin
-("run" / "quit") and answers one JSON line per wave on stdout.
+("run" = one wave, "closed WARMUP_S DURATION_S" = a constant-concurrency
+window, "quit") and answers one JSON line per command on stdout.
 """
 from __future__ import annotations
 
@@ -112,6 +113,49 @@ async def wave(url, model, concurrency, prompt_len, max_tokens, temperature, top
             "itl_p50": percentile(itl, 50), "tok_s": tok / el if el > 0 else 0.0}
 
 
+async def closed_loop(url, model, concurrency, prompt_len, max_tokens, temperature, top_p, seed,
+                      warmup_s: float, duration_s: float, session=None):
+    """Constant concurrency: ``concurrency`` client loops, each sending its
+    next request as soon as the previous stream ends, for ``warmup_s`` +
+    ``duration_s`` seconds.  Throughput over the window counts every
+    request's tokens in proportion to its overlap with the window (tokens
+    spread over the stream's decode time); TTFT / ITL over the requests that
+    START inside the window."""
+    rng = random.Random(seed)
+    t_start = time.perf_counter()
+    w0, w1 = t_start + warmup_s, t_start + warmup_s + duration_s
+    recs = []
+    s = session or new_session()
+
+    async def client(k):
+        while time.perf_counter() < w1:
+            p = synthetic_prompt(prompt_len, rng)
+            t0 = time.perf_counter()
+            r = await one_chat(s, url, model, p, max_tokens, temperature, top_p)
+            r["t0"] = t0
+            recs.append(r)
+
+    try:
+        await asyncio.gather(*[client(k) for k in range(concurrency)])
+    finally:
+        if session is None:
+            await s.close()
+    tok = 0.0
+    for r in recs:
+        a, b = r["t0"] + r["ttft"], r["t0"] + r["latency"]     # token-producing span
+        if b <= a:
+            tok += r["tokens"] if w0 <= a < w1 else 0
+            continue
+        tok += r["tokens"] * max(0.0, min(b, w1) - max(a, w0)) / (b - a)
+    inside = [r for r in recs if w0 <= r["t0"] < w1]
+    ttfts = [r["ttft"] for r in inside]
+    itl = [r["decode_s"] / (r["tokens"] - 1) for r in inside if r["tokens"] > 1]
+    return {"elapsed": duration_s, "tokens": tok, "requests": len(inside), "ttfts": ttfts,
+            "itls": itl, "ttft_p50": percentile(ttfts, 50), "ttft_p95": percentile(ttfts, 95),
+            "itl_p50": percentile(itl, 50), "itl_p95": percentile(itl, 95),
+            "tok_s": tok / duration_s}
+
+
 def new_session() -> aiohttp.ClientSession:
     return aiohttp.ClientSession(connector=aiohttp.TCPConnector(limit=0),
                                  timeout=aiohttp.ClientTimeout(total=3600))
@@ -161,6 +205,13 @@ def main(argv=None):
             cmd = line.strip()
             if cmd == "quit":
                 break
+            if cmd.startswith("closed"):
+                _, warm, dur = cmd.split()
+                r = loop.run_until_complete(closed_loop(
+                    a.url, a.model, a.concurrency, a.prompt_len, a.max_tokens, a.temperature,
+                    a.top_p, (a.seed_base << 20) + 999, float(warm), float(dur), session=session))
+                print(json.dumps(r), flush=True)
+                continue
             if cmd.startswith("run"):
                 r = loop.run_until_complete(wave(a.url, a.model, a.concurrency, a.prompt_len,
                                                  a.max_tokens, a.temperature, a.top_p,
