@@ -36,6 +36,7 @@ int glu(void*, const void*, long, int, int, int, hipStream_t);
 int apply_penalties(void*, long, int, int, const int*, const int*, const float*, const int*, int,
                     hipStream_t);
 int embed_gather(void*, const void*, const int*, int, int, int, int, hipStream_t);
+int ids_from_prev(int*, const int*, const int*, int, hipStream_t);
 int mean_pool_l2(float*, float*, const void*, const int*, int, int, int, int, int, hipStream_t);
 int bias_act(void*, const void*, long, int, int, hipStream_t);
 int gemm_splitk(void*, const void*, const void*, float*, int*, int, int, int, long, long, long,
@@ -139,6 +140,10 @@ PYBIND11_MODULE(_lmx_kernels, m) {
   });
   m.def("glu", [](uptr out, uptr x, long rows, int I, int act, int block, uptr stream) {
     check(lmx::glu(P<void>(out), P<void>(x), rows, I, act, block, S(stream)), "glu");
+  });
+  m.def("ids_from_prev", [](uptr ids, uptr src, uptr prev, int n, uptr stream) {
+    check(lmx::ids_from_prev(P<int>(ids), P<int>(src), P<int>(prev), n, S(stream)),
+          "ids_from_prev");
   });
   m.def("embed_gather", [](uptr out, uptr table, uptr ids, int T, int d, int vs, int vr,
                            uptr stream) {

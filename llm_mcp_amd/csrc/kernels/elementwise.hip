@@ -90,6 +90,26 @@ int embed_gather(void* out, const void* table, const int* ids, int T, int d, int
   return (int)hipGetLastError();
 }
 
+// Lookahead decode (engine "async" stepping): step n+1 is launched before the
+// host has read step n's sampled tokens, so the rows whose input token is still
+// on the device name it by its sample index (src >= 0) and take it from the
+// previous step's token buffer here, in stream order ahead of the embedding.
+__global__ void __launch_bounds__(256) ids_from_prev_kernel(int* __restrict__ ids,
+                                                            const int* __restrict__ src,
+                                                            const int* __restrict__ prev, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    const int s = src[i];
+    if (s >= 0) ids[i] = prev[s];
+  }
+}
+
+int ids_from_prev(int* ids, const int* src, const int* prev, int n, hipStream_t stream) {
+  if (n <= 0) return 0;
+  ids_from_prev_kernel<<<dim3((n + 255) / 256), dim3(256), 0, stream>>>(ids, src, prev, n);
+  return (int)hipGetLastError();
+}
+
 // grid (nseq), block 256; d <= 256 * 8
 __global__ void __launch_bounds__(256) mean_pool_l2_kernel(float* __restrict__ out,
                                                            const bf16_t* __restrict__ h,

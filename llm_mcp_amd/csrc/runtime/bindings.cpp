@@ -74,6 +74,8 @@ PYBIND11_MODULE(_lmx_runtime, m) {
         d["input_ids"] = to_np(p.input_ids);
         d["positions"] = to_np(p.positions);
         d["slots"] = to_np(p.slots);
+        d["input_src"] = to_np(p.input_src);
+        d["num_pending_inputs"] = p.num_pending_inputs;
         d["seq_ids"] = to_np(p.seq_ids);
         d["qlens"] = to_np(p.qlens);
         d["context_lens"] = to_np(p.context_lens);
@@ -105,6 +107,12 @@ PYBIND11_MODULE(_lmx_runtime, m) {
       .def("update", [](Scheduler& s, py::array_t<int32_t, py::array::c_style | py::array::forcecast> a) {
         return s.update(a.data(), (int)a.size());
       })
+      .def("update_lookahead", &Scheduler::update_lookahead)
+      .def("patch", [](Scheduler& s, py::array_t<int32_t, py::array::c_style | py::array::forcecast> a) {
+        return s.patch(a.data(), (int)a.size());
+      })
+      .def_property_readonly("num_inflight_samples", &Scheduler::num_inflight_samples)
+      .def("discard_lookahead", &Scheduler::discard_lookahead)
       .def_property_readonly("num_waiting", &Scheduler::num_waiting)
       .def_property_readonly("num_running", &Scheduler::num_running)
       .def_property_readonly("has_work", &Scheduler::has_work)

@@ -68,13 +68,34 @@ bool Scheduler::abort(int64_t id) {
   auto it = seqs_.find(id);
   if (it == seqs_.end()) return false;
   Seq* s = it->second.get();
+  if (s->zombie) return false;    // already finished, awaiting its plan's consumption
   auto w = std::find(waiting_.begin(), waiting_.end(), s);
   if (w != waiting_.end()) waiting_.erase(w);
   auto r = std::find(running_.begin(), running_.end(), s);
   if (r != running_.end()) running_.erase(r);
   bm_.free_seq(id);
+  // lookahead: a sample of it awaiting patch() is dropped; a row of it in the
+  // plan in flight keeps the object alive until update_lookahead() consumes it
+  for (Seq*& q : inflight_)
+    if (q == s) q = nullptr;
+  if (in_plan(s)) {
+    s->status = FINISHED;
+    s->finish = FR_ABORT;
+    s->zombie = true;
+    return true;
+  }
   seqs_.erase(it);
   return true;
+}
+
+bool Scheduler::in_plan(const Seq* s) const {
+  return std::find(plan_seqs_.begin(), plan_seqs_.end(), s) != plan_seqs_.end();
+}
+
+bool Scheduler::length_done(const Seq* s) const {
+  return s->num_generated >= s->max_new || (int)s->tokens.size() >= max_model_len_ ||
+         // a sequence longer than the whole KV cache could never be re-admitted
+         (int)s->tokens.size() >= bm_.num_blocks() * bm_.block_size();
 }
 
 void Scheduler::preempt(Seq* s) {
@@ -100,7 +121,8 @@ void Scheduler::finish(Seq* s, int reason) {
 const StepPlan& Scheduler::schedule(int q_per_tile) {
   if (q_per_tile <= 0) q_per_tile = 16;
   StepPlan& p = plan_;
-  p.input_ids.clear(); p.positions.clear(); p.slots.clear();
+  p.input_ids.clear(); p.positions.clear(); p.slots.clear(); p.input_src.clear();
+  p.num_pending_inputs = 0;
   p.seq_ids.clear(); p.qlens.clear(); p.context_lens.clear(); p.cu_q.clear();
   p.block_tables.clear(); p.sample_rows.clear(); p.sample_seq.clear();
   p.sample_temp.clear(); p.sample_topp.clear(); p.sample_topk.clear(); p.sample_off.clear();
@@ -168,8 +190,16 @@ const StepPlan& Scheduler::schedule(int q_per_tile) {
     const int n = s->scheduled;
     const std::vector<int32_t>& tab = bm_.table(s->id);
     const int row0 = p.num_tokens;
+    const int pend_t = s->pend >= 0 ? (int)s->tokens.size() - 1 : -1;
     for (int t = s->num_computed; t < s->num_computed + n; ++t) {
-      p.input_ids.push_back(s->tokens[t]);
+      if (t == pend_t) {          // the in-flight plan's sample: filled on the device
+        p.input_ids.push_back(0);
+        p.input_src.push_back(s->pend);
+        ++p.num_pending_inputs;
+      } else {
+        p.input_ids.push_back(s->tokens[t]);
+        p.input_src.push_back(-1);
+      }
       p.positions.push_back(t);
       p.slots.push_back(tab[t / bs] * bs + t % bs);
     }
@@ -244,9 +274,7 @@ std::vector<std::pair<int64_t, int>> Scheduler::update(const int32_t* sampled, i
     if (!s->ignore_eos &&
         std::find(s->stop_ids.begin(), s->stop_ids.end(), tok) != s->stop_ids.end())
       reason = FR_STOP;
-    else if (s->num_generated >= s->max_new || (int)s->tokens.size() >= max_model_len_ ||
-             // a sequence longer than the whole KV cache could never be re-admitted
-             (int)s->tokens.size() >= bm_.num_blocks() * bm_.block_size())
+    else if (length_done(s))
       reason = FR_LENGTH;
     if (reason != FR_NONE) {
       finish(s, reason);
@@ -256,6 +284,73 @@ std::vector<std::pair<int64_t, int>> Scheduler::update(const int32_t* sampled, i
   for (auto& d : done) seqs_.erase(d.first);
   plan_seqs_.clear();
   return done;
+}
+
+void Scheduler::update_lookahead() {
+  if (!inflight_.empty()) throw std::logic_error("update_lookahead before patch of the last plan");
+  for (Seq* s : plan_seqs_) {
+    if (s->zombie) continue;
+    s->num_computed += s->scheduled;
+    s->scheduled = 0;
+    bm_.commit(s->id, s->tokens.data(), s->num_computed);
+  }
+  const int n = (int)plan_.sample_rows.size();
+  inflight_.assign(n, nullptr);
+  for (int i = 0; i < n; ++i) {
+    Seq* s = plan_seqs_[plan_.sample_seq[i]];
+    if (s->zombie) continue;     // finished after this plan was launched: sample dropped
+    s->tokens.push_back(0);      // placeholder until patch()
+    s->num_generated++;
+    s->pend = i;
+    inflight_[i] = s;
+    // its last token: pages freed now (no further row), reason (stop or
+    // length, stop first as in update()) reported by patch()
+    if (length_done(s)) finish(s, FR_LENGTH);
+  }
+  for (Seq* s : plan_seqs_)
+    if (s->zombie) seqs_.erase(s->id);
+  plan_seqs_.clear();
+}
+
+std::vector<std::pair<int64_t, int>> Scheduler::patch(const int32_t* sampled, int n) {
+  if (n != (int)inflight_.size()) throw std::invalid_argument("sample count mismatch");
+  std::vector<std::pair<int64_t, int>> done;
+  for (int i = 0; i < n; ++i) {
+    Seq* s = inflight_[i];
+    if (s == nullptr) continue;
+    const int32_t tok = sampled[i];
+    s->tokens.back() = tok;
+    s->pend = -1;
+    const bool stop = !s->ignore_eos &&
+        std::find(s->stop_ids.begin(), s->stop_ids.end(), tok) != s->stop_ids.end();
+    if (s->status == FINISHED) {  // its last token (update_lookahead freed it)
+      done.emplace_back(s->id, stop ? FR_STOP : FR_LENGTH);
+      seqs_.erase(s->id);
+      continue;
+    }
+    if (stop) {
+      finish(s, FR_STOP);
+      done.emplace_back(s->id, FR_STOP);
+      if (in_plan(s)) s->zombie = true;
+      else seqs_.erase(s->id);
+    }
+  }
+  inflight_.clear();
+  return done;
+}
+
+void Scheduler::discard_lookahead() {
+  for (Seq* s : inflight_) {
+    if (s == nullptr) continue;
+    s->pend = -1;
+    if (s->status == FINISHED) seqs_.erase(s->id);
+  }
+  inflight_.clear();
+  for (Seq* s : plan_seqs_) {
+    s->scheduled = 0;
+    if (s->zombie) seqs_.erase(s->id);
+  }
+  plan_seqs_.clear();
 }
 
 }  // namespace lmxrt

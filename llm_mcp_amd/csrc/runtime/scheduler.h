@@ -54,6 +54,12 @@ struct Seq {
   int status = WAITING;
   int finish = FR_NONE;
   int scheduled = 0;            // tokens scheduled in the current plan
+  // lookahead stepping: tokens.back() is the sample `pend` of the plan in
+  // flight, not yet read back (-1: every token is known)
+  int pend = -1;
+  // finished (stop token / abort) while the plan in flight still holds a row
+  // of it: the object lives until that plan is consumed
+  bool zombie = false;
 };
 
 constexpr int kPenWindow = 64;   // token window of the penalty kernel (one wave per row)
@@ -61,6 +67,10 @@ constexpr int kPenWindow = 64;   // token window of the penalty kernel (one wave
 struct StepPlan {
   // per token rows (T)
   std::vector<int32_t> input_ids, positions, slots;
+  // lookahead stepping: -1, or the previous plan's sample index whose token
+  // (still on the device) is this row's input; input_ids holds 0 there
+  std::vector<int32_t> input_src;
+  int num_pending_inputs = 0;
   // per scheduled sequence (S), decode sequences first
   std::vector<int64_t> seq_ids;
   std::vector<int32_t> qlens, context_lens, cu_q;  // cu_q has S+1 entries
@@ -99,6 +109,26 @@ class Scheduler {
   const StepPlan& schedule(int q_per_tile);
   // sampled[i] is the token for plan.sample_rows[i]; returns finished (id, reason)
   std::vector<std::pair<int64_t, int>> update(const int32_t* sampled, int n);
+  // Lookahead stepping (the engine launches plan n+1 before it has read plan
+  // n's tokens):
+  //   update_lookahead()  consume the plan just launched with its sampled
+  //                       tokens still unknown: a placeholder is appended per
+  //                       sample and the next schedule() points the rows that
+  //                       read it at the sample (plan.input_src); a sequence
+  //                       at its length limit is finished here (no next row);
+  //   patch(sampled, n)   the tokens of the plan consumed by the last
+  //                       update_lookahead(): placeholders filled, that plan's
+  //                       finishes returned (stop before length, as update()).  A sequence that stops while the
+  //                       next plan (already launched) holds a row of it is
+  //                       finished at once (pages freed: the in-flight write
+  //                       lands before any later step in stream order) and its
+  //                       extra sample is dropped by the next update_lookahead.
+  void update_lookahead();
+  std::vector<std::pair<int64_t, int>> patch(const int32_t* sampled, int n);
+  int num_inflight_samples() const { return (int)inflight_.size(); }
+  // drop the lookahead state (engine failure): pending samples and the plan
+  // in flight are forgotten, finished objects released
+  void discard_lookahead();
 
   int num_waiting() const { return (int)waiting_.size(); }
   int num_running() const { return (int)running_.size(); }
@@ -110,6 +140,8 @@ class Scheduler {
  private:
   void preempt(Seq* s);
   void finish(Seq* s, int reason);
+  bool in_plan(const Seq* s) const;
+  bool length_done(const Seq* s) const;
 
   BlockManager bm_;
   int max_num_seqs_, max_batched_tokens_, max_model_len_, max_blocks_;
@@ -117,6 +149,7 @@ class Scheduler {
   std::deque<Seq*> waiting_;
   std::vector<Seq*> running_;
   std::vector<Seq*> plan_seqs_;
+  std::vector<Seq*> inflight_;   // samples awaiting patch() (nullptr: dropped)
   StepPlan plan_;
   int64_t arrival_ = 0;
   int64_t preemptions_ = 0;

@@ -250,7 +250,7 @@ class LLMEngine:
                       "g_schedule": 0.0, "g_launch": 0.0, "g_update": 0.0, "g_upload": 0.0,
                       "g_replay": 0.0}
         self._pending = None
-        self._fetch_cpu = None
+        self._fetch_cpu = [None, None]
         # (arrival, first token) wall times of recent requests: engine-side TTFT
         import collections
         self.ttft_samples: collections.deque = collections.deque(maxlen=65536)
@@ -260,9 +260,23 @@ class LLMEngine:
         self._prof = None
         self._prof_spec = os.environ.get("LMX_TORCH_PROFILE", "")
         if self.device.type == "cuda":
-            self._hout = torch.zeros((2, ecfg.max_num_seqs), dtype=torch.int32, pin_memory=True)
+            # two slots: under lookahead stepping step n+1's copy is queued
+            # while step n's is still being read
+            self._hout = torch.zeros((2, 2, ecfg.max_num_seqs), dtype=torch.int32,
+                                     pin_memory=True)
             self._hout_np = self._hout.numpy()
-            self._out_ev = torch.cuda.Event()
+            self._out_evs = [torch.cuda.Event(), torch.cuda.Event()]
+        self._slot = 0
+        # lookahead stepping (step n+1 scheduled and launched before step n's
+        # tokens are read back): the leader of a GPU engine without a TP plan
+        # channel; LMX_LOOKAHEAD=0 turns it off
+        # (a TP group's plan channel is attached after construction: step()
+        # checks it again)
+        la_env = os.environ.get("LMX_LOOKAHEAD", "")
+        self.lookahead = plan_channel is None and self.tp.size == 1 and (
+            la_env == "1" or (la_env != "0" and self.device.type == "cuda"))
+        self._la = None                    # the launched step not yet read back
+        self._penalized: set[int] = set()  # active requests with penalty windows
         if ecfg.use_graphs and self.device.type == "cuda" and not ops.debug_sync():
             self._capture_graphs()
         self._bucket_list = sorted(self.graphs)
@@ -329,7 +343,8 @@ class LLMEngine:
             ("ctx", np.int32, (Bmax,)), ("bt", np.int32, (Bmax, self.max_blocks)),
             ("temp", np.float32, (Bmax,)), ("topk", np.int32, (Bmax,)),
             ("topp", np.float32, (Bmax,)), ("seeds", np.int64, (Bmax,)),
-            ("offs", np.int32, (Bmax,)), ("order", np.int32, (Bmax,))], dev)
+            ("offs", np.int32, (Bmax,)), ("order", np.int32, (Bmax,)),
+            ("src", np.int32, (Bmax,))], dev)
         # penalty inputs: uploaded only on steps with penalised rows, read by
         # the lazily captured penalty variants of the decode graphs
         pmeta = _FixedMeta([("win", np.int32, (Bmax, PEN_WINDOW)), ("ngen", np.int32, (Bmax,)),
@@ -341,6 +356,7 @@ class LLMEngine:
         h["ids"][:] = 0; h["pos"][:] = 0; h["slots"][:] = -1; h["ctx"][:] = 1; h["bt"][:] = 0
         h["temp"][:] = 0; h["topk"][:] = 0; h["topp"][:] = 1; h["seeds"][:] = 0; h["offs"][:] = 0
         h["order"][:] = np.arange(Bmax, dtype=np.int32)
+        h["src"][:] = -1
         meta.upload()
         self._gmeta = meta
         g = dict(meta.d)
@@ -348,7 +364,10 @@ class LLMEngine:
             "cu": torch.arange(Bmax + 1, dtype=torch.int32, device=dev),
             "tiles": torch.zeros(2, dtype=torch.int32, device=dev),
             "rows": torch.arange(Bmax, dtype=torch.int64, device=dev),
-            "tok": torch.zeros(Bmax, dtype=torch.int32, device=dev),
+            # every sample of a step (an eager step may sample more rows than
+            # the largest bucket): the next graph step's ids_from_prev source
+            "tok": torch.zeros(max(Bmax, self.ecfg.max_num_seqs), dtype=torch.int32,
+                               device=dev),
             "lp": torch.zeros(Bmax, dtype=torch.float32, device=dev),
         })
         self._gbuf = g
@@ -373,6 +392,8 @@ class LLMEngine:
         ws = self._decode_ws(B)
 
         def run():
+            # lookahead rows: input tokens still on the device (previous step's samples)
+            ops.ids_from_prev(g["ids"][:B], g["src"][:B], g["tok"])
             logits = self.model.forward(inp, self.k_caches, self.v_caches, ws,
                                         self.ecfg.part_tokens)
             if self.is_leader:
@@ -494,6 +515,10 @@ class LLMEngine:
 
     def _fail_all(self, why: str):
         self._pending = None
+        if self._la is not None:
+            self._la = None
+            self.sched.discard_lookahead()
+        self._penalized.clear()
         evs = []
         for rid, req in list(self._reqs.items()):
             self.sched.abort(rid)
@@ -512,6 +537,7 @@ class LLMEngine:
                 break
             req = self._reqs.pop(rid, None)
             if req is not None:
+                self._penalized.discard(rid)
                 self.sched.abort(rid)
                 req.finished = True
                 evs.append(TokenEvent(req, -1, 0.0, "abort"))
@@ -531,6 +557,7 @@ class LLMEngine:
                     self.sched.set_penalties(req.id, float(p.repetition_penalty),
                                              float(p.presence_penalty),
                                              float(p.frequency_penalty), int(p.penalty_last_n))
+                    self._penalized.add(req.id)
                 self._reqs[req.id] = req
             except Exception as e:
                 req.finished = True
@@ -563,12 +590,12 @@ class LLMEngine:
         only schedule + upload + launch + update (all native / array code;
         sampling parameters come out of the native plan as flat arrays)."""
         self._drain()
-        if not self.sched.has_work:
+        if not self.sched.has_work and self._la is None:
             self._flush_pending()
             return False
         self._step_started = time.monotonic()
         try:
-            return self._step()
+            return self._step_la() if self.lookahead and self.chan is None else self._step()
         finally:
             self._step_started = 0.0
 
@@ -639,6 +666,105 @@ class LLMEngine:
         st["generated_tokens"] += N
         return True
 
+    def _step_la(self) -> bool:
+        """Lookahead step (one-step asynchronous scheduling):
+
+            consume step n (tokens unknown) -> schedule(n+1) -> launch(n+1)
+            -> wait for step n's tokens (n+1 queued behind it) -> patch(n)
+            -> emit step n's events
+
+        so the GPU always has the next step queued and the host's schedule /
+        metadata / launch work runs under the previous step's kernels.  Rows
+        whose input is step n's sample carry its index (plan input_src); the
+        decode graphs gather those tokens on the device (ops.ids_from_prev),
+        an eager (prefill / mixed) step waits for them first.  Sequences that
+        stop on a sampled stop token one step late cost one dropped row
+        (native Scheduler::patch)."""
+        fl = faults()
+        if fl:
+            if fl.hit("step_hang"):
+                time.sleep(float(os.environ.get("LMX_FAULT_HANG_S", "5")))
+            fl.maybe_raise("gpu_error", "HIP error: injected device fault")
+        if self._prof is not None:
+            self._prof_tick()
+        t0 = time.perf_counter()
+        la = self._la
+        if la is not None:
+            self.sched.update_lookahead()
+            if self._penalized:     # penalty windows are built from the real tokens
+                self._la_resolve()
+                la = None
+        plan = self.sched.schedule(self.q_per_tile)
+        T = plan["num_tokens"]
+        if T == 0:
+            if la is not None:
+                self._la_resolve()
+            self._flush_pending()
+            return la is not None
+        S = len(plan["seq_ids"])
+        nd = plan["num_decode"]
+        N = len(plan["sample_seq"])
+        bucket = None
+        if nd == S == T and self.graphs:
+            bucket = next((b for b in self._bucket_list if b >= nd), None)
+        t1 = time.perf_counter()
+        tw = 0.0
+        if bucket is not None:
+            tok, lp = self._run_graph(plan, bucket)
+        else:
+            if la is not None:      # this step's inputs need step n's tokens on the host
+                tw = time.perf_counter()
+                prev = self._la_resolve()
+                tw = time.perf_counter() - tw
+                la = None
+                if plan["num_pending_inputs"]:
+                    src = plan["input_src"]
+                    m = src >= 0
+                    plan["input_ids"][m] = prev[src[m]]
+            elif plan["num_pending_inputs"]:
+                raise RuntimeError("lookahead plan references an unread step")
+            tok, lp = self._run_eager(plan)
+            if self.graphs and N:
+                # the next (graph) step gathers its input tokens from here
+                self._gbuf["tok"][:N].copy_(tok[:N], non_blocking=True)
+        k = self._start_fetch(tok, lp, N)
+        t2 = time.perf_counter()
+        if la is not None:
+            self._la_resolve()
+        t3 = time.perf_counter()
+        self._la = {"seq_ids": plan["seq_ids"], "sample_seq": plan["sample_seq"], "N": N,
+                    "slot": k}
+        st = self.stats
+        st["t_schedule"] += t1 - t0
+        st["t_launch"] += t2 - t1 - tw
+        st["t_wait"] += t3 - t2 + tw
+        st["t_gpu"] += t3 - t1
+        st["steps"] += 1
+        st["step_time_s"] += t3 - t0
+        st["decode_steps"] += int(nd == S)
+        st["graph_steps"] += int(bucket is not None)
+        if bucket is not None:
+            st["decode_step_s"] += t3 - t0
+            st["g_schedule"] += t1 - t0
+            st["g_launch"] += t2 - t1
+        st["prefill_tokens"] += plan["num_prefill_tokens"]
+        st["generated_tokens"] += N
+        return True
+
+    def _la_resolve(self) -> np.ndarray:
+        """Read back the launched step's tokens, fill the scheduler's
+        placeholders and emit that step's events; returns its tokens."""
+        la, self._la = self._la, None
+        t = time.perf_counter()
+        toks, lps = self._finish_fetch(la["N"], la["slot"])
+        t2 = time.perf_counter()
+        fin = self.sched.patch(toks)
+        self.stats["t_update"] += time.perf_counter() - t2
+        self.stats["t_events"] += t2 - t
+        self._pending = (la["seq_ids"], la["sample_seq"], toks, lps, fin)
+        self._flush_pending()
+        return toks
+
     def start_profile(self, out_dir: str, steps: int = 20):
         """Record a torch.profiler (ROCm/roctracer) timeline of the next
         ``steps`` engine steps into ``out_dir`` (chrome trace)."""
@@ -684,6 +810,7 @@ class LLMEngine:
             if reason is not None:
                 req.finished = True
                 del reqs[rid]
+                self._penalized.discard(rid)
                 self.stats["finished"] += 1
             evs.append(TokenEvent(req, tl[i], ll[i], reason))
         if evs and self.event_sink:
@@ -744,6 +871,12 @@ class LLMEngine:
             a = h[k]
             a[:n] = plan[_PLAN_KEY.get(k, k)]
             a[n:B] = fill
+        src = plan.get("input_src")
+        if src is not None and plan.get("num_pending_inputs"):
+            h["src"][:n] = src
+        else:
+            h["src"][:n] = -1
+        h["src"][n:B] = -1
         # only the live columns: stale entries beyond a row's context are
         # never read (and always hold valid page ids)
         h["bt"][:n, :mb] = plan["block_tables"].reshape(n, mb)
@@ -766,21 +899,24 @@ class LLMEngine:
         st["g_replay"] += time.perf_counter() - tb
         return g["tok"][:B], g["lp"][:B]
 
-    def _start_fetch(self, tok: torch.Tensor, lp: torch.Tensor, n: int):
+    def _start_fetch(self, tok: torch.Tensor, lp: torch.Tensor, n: int) -> int:
         """Queue the D2H copy of the sampled tokens/logprobs into pinned
-        memory behind the step's kernels (no sync here)."""
+        memory behind the step's kernels (no sync here); returns the slot."""
+        k = self._slot = self._slot ^ 1
         if not tok.is_cuda:
-            self._fetch_cpu = (tok[:n].numpy().copy(), lp[:n].numpy().copy())
-            return
-        self._hout[0, :n].copy_(tok[:n], non_blocking=True)
-        self._hout[1, :n].copy_(lp[:n].view(torch.int32), non_blocking=True)
-        self._out_ev.record()
+            self._fetch_cpu[k] = (tok[:n].numpy().copy(), lp[:n].numpy().copy())
+            return k
+        self._hout[k, 0, :n].copy_(tok[:n], non_blocking=True)
+        self._hout[k, 1, :n].copy_(lp[:n].view(torch.int32), non_blocking=True)
+        self._out_evs[k].record()
+        return k
 
-    def _finish_fetch(self, n: int):
+    def _finish_fetch(self, n: int, k: int | None = None):
+        k = self._slot if k is None else k
         if self.device.type != "cuda":
-            return self._fetch_cpu
-        self._out_ev.synchronize()
-        h = self._hout_np
+            return self._fetch_cpu[k]
+        self._out_evs[k].synchronize()
+        h = self._hout_np[k]
         return h[0, :n].copy(), h[1, :n].view(np.float32).copy()
 
     # ----------------------------------------------------- offline helper ---

@@ -419,6 +419,20 @@ def embed_gather(table: torch.Tensor, ids: torch.Tensor, vocab_start: int = 0,
     return out
 
 
+def ids_from_prev(ids: torch.Tensor, src: torch.Tensor, prev: torch.Tensor) -> torch.Tensor:
+    """In place: ids[i] = prev[src[i]] where src[i] >= 0 (lookahead decode: the
+    input token of a row is the previous step's sample src[i], still on the
+    device when the step is launched)."""
+    if not ids.is_cuda:
+        m = src >= 0
+        ids[m] = prev[src[m].long()]
+        return ids
+    _chk(ids.dtype == src.dtype == prev.dtype == torch.int32 and ids.numel() == src.numel()
+         and ids.is_contiguous() and src.is_contiguous(), "ids_from_prev")
+    native().ids_from_prev(_ptr(ids), _ptr(src), _ptr(prev), ids.numel(), _stream())
+    return ids
+
+
 def mean_pool_l2(h: torch.Tensor, cu: torch.Tensor, dims: int | None = None,
                  normalize: bool = True) -> torch.Tensor:
     T, d = h.shape

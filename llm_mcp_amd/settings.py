@@ -83,6 +83,7 @@ VARS: list[Var] = [
     Var("LMX_MAINTENANCE_INTERVAL", int, 60, "seconds between store maintenance ticks"),
     Var("LMX_JOB_STREAM_MAX_S", int, 3600, "max duration of one /v1/jobs/{id}/stream"),
     Var("LMX_SP_MIN_TOKENS", int, 0, "TP: steps with at least this many tokens run sequence-parallel (reduce-scatter/all-gather residual stream); 0 disables (default until the RCCL branch is measured on a multi-GPU node)"),
+    Var("LMX_LOOKAHEAD", str, "", "engine lookahead stepping (step n+1 scheduled and launched before step n's tokens are read back; input tokens gathered on the device): default on for a single-GPU engine, 1 forces it (also on CPU), 0 off; TP groups step synchronously"),
     Var("LMX_FUSED_DECODE_ROPE", str, "1", "1: decode rows' rotary embedding and KV-cache write run inside the paged decode attention kernel; 0: separate rope/cache kernel"),
     Var("LMX_ENCODER_LIBRARY", str, "1", "encoder (embedding-model) plain projections may run on hipBLASLt where it was measured faster than the hand-written kernels; 0 keeps them on the hand-written kernels"),
     Var("LMX_TP_PROBE_STEPS", int, 2000, "TP engines: every N steps all ranks time one decode-sized all-reduce (rccl_allreduce_seconds live samples; 0 = off)"),

@@ -57,9 +57,12 @@ def _rank(rank, size, port, ckpt, tag, q, model="tiny-llama"):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("size,model", [(2, "tiny-llama"), (4, "tiny-llama-tp8")])
+@pytest.mark.parametrize("size,model", [(2, "tiny-llama"), (4, "tiny-llama-tp8"),
+                                        (8, "tiny-llama-tp8")])
 def test_tp_group_on_gpu_kernels(tmp_path, size, model):
-    """TP=2, and TP=4 of the 70B-shaped tiny model (4 q / 2 kv heads per rank)."""
+    """TP=2, and TP=4 / TP=8 of the 70B-shaped tiny model (4 q / 2 kv and 2 q / 1 kv
+    heads per rank): the TP=8 leader/follower group and its world-8 peer
+    all-reduce, eight processes on the one GPU."""
     from llm_mcp_amd.models import config as mc
     from llm_mcp_amd.models.llama import LlamaModel
     from llm_mcp_amd.models.weights import save_hf_llama

@@ -112,3 +112,35 @@ def test_waiting_sequences_do_not_pin_prefix_pages():
     assert not t.is_alive(), (e.sched.num_running, e.sched.num_waiting, e.sched.kv_usage)
     assert [len(o) for o in out["o"]] == [300] * 8
     assert e.sched.preemptions > 0
+
+
+def test_lookahead_stepping_matches_synchronous(monkeypatch):
+    """Lookahead stepping (engine._step_la: step n+1 scheduled before step n's
+    tokens are read; forced on here, the GPU default) gives the synchronous
+    engine's tokens: seeded sampling, stop tokens seen one step late,
+    preemption by a 16-page KV cache, ragged prompt lengths."""
+    monkeypatch.setenv("LMX_LOOKAHEAD", "0")
+    base = _engine()
+    kv = 16 * 2 * 2 * 2 * 32 * 128 * 2 / (1 << 30)
+    prompts = [list(range(i, i + 20 + 17 * i)) for i in range(6)]
+
+    def run(la, stops):
+        monkeypatch.setenv("LMX_LOOKAHEAD", la)
+        e = LLMEngine(EngineConfig(model="tiny-llama", max_num_seqs=8, max_batched_tokens=96,
+                                   max_model_len=512, use_graphs=False, kv_cache_gb=kv),
+                      device="cpu", weights=base.model.w)
+        assert e.lookahead == (la == "1")
+        sp = SamplingParams(temperature=0.9, top_p=0.9, max_tokens=24, seed=5,
+                            stop_token_ids=stops)
+        out = e.generate(prompts, sp)
+        assert not e.sched.has_work
+        return out, e.sched.preemptions
+
+    free, pre0 = run("0", [])
+    free_la, pre1 = run("1", [])
+    assert free_la == free and pre0 > 0 and pre1 > 0   # through preemption
+    stops = [free[0][4], free[3][9]]           # tokens the streams do sample
+    sync, _ = run("0", stops)
+    ahead, _ = run("1", stops)
+    assert ahead == sync
+    assert any(len(o) < 24 for o in ahead)     # streams ended on a stop token

@@ -173,3 +173,41 @@ def test_llama3_8b_shapes_on_decode_gemm_match_dense(graphs):
     assert ops.DGEMM_CALLS[0] > n0
     for p, o in list(zip(prompts, outs))[::7]:
         assert_greedy_consistent(e.model, p, o, tol=0.08)
+
+
+def test_lookahead_graph_steps_match_synchronous(monkeypatch):
+    """Lookahead stepping on the captured decode graphs (input tokens gathered
+    on the device by ops.ids_from_prev from the previous step's samples) gives
+    the synchronous engine's tokens: seeded top-p sampling, stop tokens, rows
+    joining while others decode, and the greedy streams stay consistent with
+    the dense fp32 forward."""
+    ops.native()
+    base = None
+    prompts = [list(range(10, 50)), list(range(5, 300)), [7] * 33, [3], list(range(40, 41 + 70))]
+
+    def run(la, sp):
+        nonlocal base
+        monkeypatch.setenv("LMX_LOOKAHEAD", la)
+        e = LLMEngine(EngineConfig(model="tiny-llama", max_num_seqs=16, max_batched_tokens=96,
+                                   max_model_len=1024, use_graphs=True, kv_cache_gb=0.05),
+                      device="cuda", weights=None if base is None else base.model.w)
+        base = base or e
+        assert e.lookahead == (la == "1")
+        out = e.generate(prompts, sp)
+        torch.cuda.synchronize()
+        assert e.stats["graph_steps"] > 0
+        return out, e
+
+    greedy = SamplingParams(temperature=0, max_tokens=16, ignore_eos=True)
+    g0, _ = run("0", greedy)
+    g1, e1 = run("1", greedy)
+    assert g1 == g0
+    for p, o in zip(prompts, g1):
+        assert_greedy_consistent(e1.model, p, o)
+    free, _ = run("0", SamplingParams(temperature=0.8, top_p=0.9, max_tokens=16, seed=3))
+    stops = [free[0][3], free[2][7]]
+    sp = SamplingParams(temperature=0.8, top_p=0.9, max_tokens=16, seed=3, stop_token_ids=stops)
+    s0, _ = run("0", sp)
+    s1, _ = run("1", sp)
+    assert s1 == s0
+    assert any(len(o) < 16 for o in s1)
