@@ -256,9 +256,7 @@ class LlamaModel:
                 h = ops.rms_norm(x, L["ln1"], cfg.rms_eps, residual=residual)
             if sp:
                 h = tp.all_gather_rows(h)[:T]
-            qkv = ops.linear(h, L["wqkv"])
-            if "bqkv" in L:          # Qwen2: biased q/k/v
-                qkv += L["bqkv"]
+            qkv = ops.linear(h, L["wqkv"], bias=L.get("bqkv"))   # Qwen2: biased q/k/v
             kc, vc = k_caches[li], v_caches[li]
             # decode rows: rotary + cache write fused into the decode attention
             # kernel (one launch and one boundary fewer per layer); prefill rows

@@ -602,24 +602,30 @@ def splitk_preferred(M: int, N: int, K: int) -> bool:
     return False
 
 
-def linear(x: torch.Tensor, w: torch.Tensor, defer: bool = False):
-    """x @ w^T: the decode GEMM (K11) where the measured table picks it, the
-    older split-K kernel where it was measured faster, else hipBLASLt.
-    ``defer``: the caller feeds the result to ``rms_norm(..., residual=)``,
-    so a table entry for the partials-only form (epi 2) may return
-    ``Partials`` and leave the K reduction to the norm."""
+def linear(x: torch.Tensor, w: torch.Tensor, defer: bool = False,
+           bias: torch.Tensor | None = None):
+    """x @ w^T (+ bias): the decode GEMM (K11) where the measured table picks
+    it, the older split-K kernel where it was measured faster, else hipBLASLt
+    (bias in its epilogue).  ``defer``: the caller feeds the result to
+    ``rms_norm(..., residual=)``, so a table entry for the partials-only form
+    (epi 2) may return ``Partials`` and leave the K reduction to the norm."""
     if x.is_cuda and x.dim() == 2:
         M, N, K = x.shape[0], w.shape[0], w.shape[1]
-        if defer:
+        if defer and bias is None:
             ch = dgemm_choice(M, N, K, epi=2)
             if ch is not None:
                 return dgemm_partials(x, w, ch[0], ch[1])
         ch = dgemm_choice(M, N, K)
+        y = None
         if ch is not None:
-            return dgemm(x, w, ch[0], ch[1])
-        if splitk_preferred(M, N, K):
-            return gemm_splitk(x, w)
-    return torch.nn.functional.linear(x, w)
+            y = dgemm(x, w, ch[0], ch[1])
+        elif splitk_preferred(M, N, K):
+            y = gemm_splitk(x, w)
+        if y is not None:
+            if bias is not None:
+                y += bias
+            return y
+    return torch.nn.functional.linear(x, w, bias)
 
 
 def linear_swiglu(x: torch.Tensor, w: torch.Tensor, block: int) -> torch.Tensor:
