@@ -14,11 +14,15 @@ from __future__ import annotations
 
 import asyncio
 import base64
+import json
 import os
-import struct
 import time
 
-from .helpers import read_json, write_error, write_json
+import numpy as np
+from aiohttp import web
+
+from ..native import runtime
+from .helpers import read_json, write_error
 
 EMBED_TIMEOUT_S = 120.0
 
@@ -33,6 +37,24 @@ def _texts(inp):
             return None, [[int(t) for t in x] for x in inp]
         return [x for x in inp if isinstance(x, str)], None
     return None, None
+
+
+def _response(vecs, fmt: str, model: str, ntok: int) -> web.Response:
+    """OpenAI list response.  The float form is spliced from rows formatted
+    natively (``_lmx_runtime.f32_json_rows``: shortest float32 round-trip
+    text); json.dumps over Python floats costs ~7 ms per 16 x 768 response
+    and bounded the API process."""
+    arr = np.asarray(vecs, dtype=np.float32).reshape(len(vecs), -1)
+    if fmt == "base64":
+        rows = ['"' + base64.b64encode(arr[i].astype("<f4").tobytes()).decode() + '"'
+                for i in range(len(arr))]
+    else:
+        rows = runtime().f32_json_rows(arr)
+    data = ",".join('{"object":"embedding","embedding":%s,"index":%d}' % (r, i)
+                    for i, r in enumerate(rows))
+    body = '{"object":"list","data":[%s],"model":%s,"usage":{"prompt_tokens":%d,' \
+           '"total_tokens":%d}}\n' % (data, json.dumps(model, ensure_ascii=False), ntok, ntok)
+    return web.Response(status=200, text=body, content_type="application/json")
 
 
 class EmbeddingsHandler:
@@ -108,13 +130,7 @@ class EmbeddingsHandler:
             m.embedding_requests.labels(model, target.device_id, "ok").inc()
             m.embedding_duration.labels(model, target.device_id).observe(el)
             m.embedding_tokens.labels(model, target.device_id).inc(ntok)
-            data = []
-            for i, v in enumerate(vecs):
-                emb = base64.b64encode(struct.pack(f"<{len(v)}f", *v)).decode() \
-                    if fmt == "base64" else v
-                data.append({"object": "embedding", "embedding": emb, "index": i})
-            return write_json(200, {"object": "list", "data": data, "model": model,
-                                    "usage": {"prompt_tokens": ntok, "total_tokens": ntok}})
+            return _response(vecs, fmt, model, ntok)
         st.metrics.embedding_requests.labels(model, "all", "error").inc()
         return write_error(502, "embed_failed", str(last_err) if last_err else
                            "All devices failed")

@@ -87,3 +87,25 @@ def test_embeddings_over_ipc_api_process_app():
         asyncio.new_event_loop().run_until_complete(go())
     finally:
         srv.stop()
+
+
+def test_embedding_response_rows_are_exact_float32():
+    """/v1/embeddings bodies are spliced from natively formatted rows
+    (shortest float32 round trip): parsing them back gives the float32
+    values bit for bit; non-finite values become null."""
+    import json
+
+    import numpy as np
+
+    from llm_mcp_amd.api.openai_embed import _response
+    from llm_mcp_amd.native import runtime
+    v = (np.random.default_rng(0).standard_normal((5, 96)) * 10.0 ** np.arange(-6, 6, 0.125)[:96]
+         ).astype(np.float32)
+    body = json.loads(_response(v.tolist(), "float", "m", 7).text)
+    assert [d["index"] for d in body["data"]] == list(range(5))
+    back = np.asarray([d["embedding"] for d in body["data"]], np.float32)
+    assert np.array_equal(back, v)
+    assert body["usage"] == {"prompt_tokens": 7, "total_tokens": 7}
+    row = json.loads(runtime().f32_json_rows(np.asarray([[1.5, np.nan, -np.inf, 0.0]],
+                                                        np.float32))[0])
+    assert row == [1.5, None, None, 0.0]
