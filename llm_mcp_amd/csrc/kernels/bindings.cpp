@@ -21,6 +21,7 @@ int rope_cache(void*, long, const int*, const float*, int, int, int, int, const 
 int kv_write(const void*, const void*, long, const int*, int, int, int, void*, void*, int,
              hipStream_t);
 void set_decode_mode(int);
+void set_slab_norm_threads(int);
 void set_prefill_rescale_thr(float);
 void set_prefill_stages(int);
 int paged_decode(const void*, long, const void*, const void*, const int*, int, const int*,
@@ -115,6 +116,8 @@ PYBIND11_MODULE(_lmx_kernels, m) {
                             P<int>(positions), P<float>(cos_sin), P<int>(slots), S(stream)),
           "paged_decode");
   });
+  m.def("set_slab_norm_threads", [](int t) { lmx::set_slab_norm_threads(t); },
+        "probe knob: workgroup size cap of the slab RMSNorm (default 512)");
   m.def("set_decode_mode", [](int mode) { lmx::set_decode_mode(mode); },
         "paged decode loop: 0 one page at a time, 1 next page prefetched, 2 loads only (probe)");
   m.def("set_prefill_rescale_thr", [](float thr) { lmx::set_prefill_rescale_thr(thr); },

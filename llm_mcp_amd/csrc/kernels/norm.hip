@@ -79,7 +79,7 @@ __global__ void __launch_bounds__(256) rmsnorm_kernel(
 // before the first add (a runtime trip count serialised them: S dependent
 // memory latencies per chunk, ~8 us per 256-row call at S = 4).
 template <int VPT, int S>
-__global__ void __launch_bounds__(256) rmsnorm_slabs_kernel(
+__global__ void __launch_bounds__(512) rmsnorm_slabs_kernel(
     bf16_t* __restrict__ out, bf16_t* __restrict__ residual, const float* __restrict__ slabs,
     long slab_stride, const bf16_t* __restrict__ w, int cols, long out_stride,
     float eps) {
@@ -217,12 +217,20 @@ int rmsnorm(void* out, void* residual, const void* x, const void* w, int rows, i
   return (int)hipGetLastError();
 }
 
+// workgroup cap of the slab norm (probe knob: tools/slab_norm_probe.py)
+static int g_slab_threads = 512;
+void set_slab_norm_threads(int t) { g_slab_threads = t < 64 ? 64 : (t > 512 ? 512 : t); }
+
 int rmsnorm_slabs(void* out, void* residual, const float* slabs, int S, long slab_stride,
                   const void* w, int rows, int cols, long out_stride, float eps,
                   hipStream_t stream) {
   if (cols % 8 != 0 || rows <= 0 || S < 1 || residual == nullptr) return -1;
   const int nchunk = cols / 8;
-  const int threads = pick_threads(nchunk);
+  // up to 512 threads (one 8-column chunk per thread at hidden 4096): a
+  // decode step has one workgroup per row (~one per CU), so the S slabs'
+  // loads of a row are spread over twice the waves of the plain norm
+  int threads = ((nchunk + 63) / 64) * 64;
+  threads = threads > g_slab_threads ? g_slab_threads : (threads < 64 ? 64 : threads);
   const int vpt = (nchunk + threads - 1) / threads;
   dim3 g(rows), b(threads);
 #define LMX_RMSS(V, SS)                                                                     \
