@@ -30,6 +30,10 @@ def main():
                          "engine's wave pattern (prompt pages contiguous per sequence, decode "
                          "pages handed out one per sequence in turn)")
     ap.add_argument("--pages", type=int, default=20000, help="pages in the cache")
+    ap.add_argument("--rope", action="store_true",
+                    help="the engine's fused form: q rows are whole unrotated QKV rows, the "
+                         "kernel rotates q and writes the step's k/v at ctx-1")
+    ap.add_argument("--modes", default="4,0,5,4,0,5")
     a = ap.parse_args()
     B, Hq, Hkv, D, BS = a.batch, 32, 8, 128, 32
     dev = torch.device("cuda", 0)
@@ -41,7 +45,7 @@ def main():
     nb = a.pages                                # 20000 pages x 64 KB x 2 = 2.6 GB (> MALL)
     k_cache = (torch.randn(nb, Hkv, BS, D, device=dev) * 0.5).to(torch.bfloat16)
     v_cache = torch.randn(nb, Hkv, D, BS, device=dev).to(torch.bfloat16)
-    q = torch.randn(B, Hq * D, device=dev).to(torch.bfloat16)
+    q = torch.randn(B, (Hq + 2 * Hkv if a.rope else Hq) * D, device=dev).to(torch.bfloat16)
     cl = ctx.to(dev)
     # page tables rotated per call over disjoint page sets: a call's K/V were
     # last read >= 640 MB of other pages ago, so they come from HBM (as in a
@@ -74,12 +78,19 @@ def main():
     scale = D ** -0.5
     ref = None
     nat = ops.native()
-    for mode in (4, 0, 5, 4, 0, 5):
+    ropes = [None] * len(tables)
+    if a.rope:
+        from llm_mcp_amd.ops import ref as opsref
+        cs = opsref.rope_cos_sin(8192, D, 500000.0, dev)
+        pos = (cl - 1).to(torch.int32)
+        ropes = [(pos, cs, (t[torch.arange(B, device=dev), (pos // BS).long()] * BS + pos % BS)
+                  .to(torch.int32)) for t in tables]
+    for mode in map(int, a.modes.split(",")):
         nat.set_decode_mode(mode)
         ops.paged_decode_attention(q, k_cache, v_cache, bt, cl, scale, out, ws, a.part_tokens,
-                                   order=order)
+                                   order=order, Hq=Hq, rope=ropes[0])
         torch.cuda.synchronize()
-        if mode == 4 and ref is None:
+        if ref is None:
             ref = out.clone()
         same = "-" if mode in (2, 3) else ("bitwise" if torch.equal(out, ref) else
                                       f"max diff {(out.float() - ref.float()).abs().max():.3g}")
@@ -87,13 +98,28 @@ def main():
         s.record()
         for i in range(a.iters):
             ops.paged_decode_attention(q, k_cache, v_cache, tables[i % nrot], cl, scale, out, ws,
-                                       a.part_tokens, order=order)
+                                       a.part_tokens, order=order, Hq=Hq, rope=ropes[i % nrot])
         e.record()
         torch.cuda.synchronize()
         us = s.elapsed_time(e) / a.iters * 1e3
-        print(f"decode attn {a.layout} pages={nb} B={B} parts {a.parts}x{a.part_tokens} {a.order} mode {mode}: {us:7.1f} us  {kv_bytes / us / 1e6:5.2f} TB/s  "
-              f"vs grid (mode 4): {same}", flush=True)
+        print(f"decode attn {'rope ' if a.rope else ''}{a.layout} pages={nb} B={B} parts {a.parts}x{a.part_tokens} {a.order} mode {mode}: {us:7.1f} us  {kv_bytes / us / 1e6:5.2f} TB/s  "
+              f"vs first mode: {same}", flush=True)
     nat.set_decode_mode(0)
+    if a.rope:
+        # the unfused form: the per-token rope / cache kernel, then attention without rope
+        pos_, cs_, _ = ropes[0]
+        for rep in range(2):
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for i in range(a.iters):
+                _, _, sl = ropes[i % nrot]
+                ops.rope_and_cache(q, pos_, cs_, Hq, Hkv, D, sl, k_cache, v_cache, tile_from=B)
+                ops.paged_decode_attention(q, k_cache, v_cache, tables[i % nrot], cl, scale,
+                                           out, ws, a.part_tokens, order=order, Hq=Hq)
+            e.record()
+            torch.cuda.synchronize()
+            print(f"decode attn rope split (rope_cache kernel + attention): "
+                  f"{s.elapsed_time(e) / a.iters * 1e3:7.1f} us", flush=True)
 
 
 if __name__ == "__main__":
