@@ -35,16 +35,27 @@ def test_lease_queue_matches_model(ops):
             def live_on(dev, but):
                 return sum(1 for k2, m2 in model.items() if k2 != but and m2["dev"] == dev
                            and m2["status"] == "running" and m2["lease"] >= now[0])
-            # per-device concurrency (DEVICE_MAX_CONCURRENCY = 1) for pinned jobs
-            claimable = [k for k, m in model.items()
-                         if m["attempts"] < m["max"] and (m["status"] == "queued" or
-                                                         (m["status"] == "running" and
-                                                          m["lease"] < now[0]))
-                         and (not m["dev"] or live_on(m["dev"], k) < 1)]
-            if not claimable:
+            # the claim walks queued / lease-lapsed rows by (priority, FIFO):
+            # rows that exhausted max_attempts are retired ('attempts_exhausted')
+            # as the walk passes them (the Postgres store retires them in its
+            # maintenance sweep instead); per-device concurrency
+            # (DEVICE_MAX_CONCURRENCY = 1) for pinned jobs
+            best = None
+            for k in sorted((k for k, m in model.items() if m["status"] in ("queued", "running")),
+                            key=lambda k: (-model[k]["prio"], model[k]["seq"])):
+                m = model[k]
+                if m["status"] == "running" and m["lease"] >= now[0]:
+                    continue
+                if m["attempts"] >= m["max"]:
+                    m.update(status="error", lease=0.0, token=None)
+                    continue
+                if m["dev"] and live_on(m["dev"], k) >= 1:
+                    continue
+                best = k
+                break
+            if best is None:
                 assert j is None
                 continue
-            best = max(claimable, key=lambda k: (model[k]["prio"], -model[k]["seq"]))
             assert j is not None and j["id"] == best
             m = model[best]
             m.update(status="running", attempts=m["attempts"] + 1, lease=now[0] + 10,
