@@ -12,7 +12,7 @@
 // k index of the PV product is permuted so that B element j of lane group g is
 // key 4g+j (j<4) or 16+4g+j-4 (j>=4), exactly where S^T left it; the V^T
 // operand is read with the same permutation as two 8-byte loads from the
-// d-major V page, see rope_cache.hip for the cache layout).
+// key-quad V page [BS/4][D][4], see rope_cache.hip for the cache layout).
 //
 //   decode  (K4): columns = the G query heads of one token (G = Hq/Hkv <= 16);
 //                 the 4 waves split the page range, combined through LDS, and
@@ -86,10 +86,9 @@ __device__ __forceinline__ void process_page(PageState<HD>& st, const bf16x8_t (
   // V^T fragments (issued early so they overlap the QK MFMAs and softmax)
   bf16x8_t vf[NT];
 #pragma unroll
-  for (int i = 0; i < NT; ++i) {
-    const bf16_t* vr = vpage + (16 * i + c) * BS;
-    vf[i] = kv_frag_2x8B<NTL>(vr + 4 * g, vr + 16 + 4 * g);
-  }
+  for (int i = 0; i < NT; ++i)
+    vf[i] = kv_frag_2x8B<NTL>(vpage + vq_off(16 * i + c, 4 * g, HD),
+                              vpage + vq_off(16 * i + c, 16 + 4 * g, HD));
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
     s0 = mfma16(ka[s], qf[s], s0);
@@ -145,10 +144,9 @@ __device__ __forceinline__ void load_page(PageFrags<HD>& f, const bf16_t* __rest
     f.kb[s] = load_frag16B(kpage + (16 + c) * HD + 32 * s + 8 * g);
   }
 #pragma unroll
-  for (int i = 0; i < HD / 16; ++i) {
-    const bf16_t* vr = vpage + (16 * i + c) * BS;
-    f.vf[i] = load_frag_2x8B(vr + 4 * g, vr + 16 + 4 * g);
-  }
+  for (int i = 0; i < HD / 16; ++i)
+    f.vf[i] = load_frag_2x8B(vpage + vq_off(16 * i + c, 4 * g, HD),
+                             vpage + vq_off(16 * i + c, 16 + 4 * g, HD));
 }
 
 template <int HD>
@@ -233,7 +231,7 @@ __device__ __forceinline__ void rope_q_frags(bf16x8_t (&qf)[HD / 32], const floa
 
 // The new token's k (rotated) and v of kv head kvh into its cache slot, by ONE
 // wave: lanes [0, HD/8) rotate 4 pairs of k each, lanes [16, 16 + HD/4) move
-// 4 v elements each into the d-major page.  No wait here: the caller (the
+// 4 v elements each into the key-quad page.  No wait here: the caller (the
 // wave that later reads the page holding the slot) retires the stores with
 // s_waitcnt vmcnt(0) before that read, so the other waves never wait on it.
 template <int HD>
@@ -266,9 +264,9 @@ __device__ __forceinline__ void rope_write_kv(const bf16_t* __restrict__ krow,
   } else if (lane >= 16 && lane < 16 + HD / 4) {
     const int d = 4 * (lane - 16);
     const bf16x4_t v = *reinterpret_cast<const bf16x4_t*>(vrow + d);
-    bf16_t* vp = v_cache + ((blk * Hkv + kvh) * HD + d) * BS + off;
+    bf16_t* vp = v_cache + (blk * Hkv + kvh) * (BS * HD) + vq_off(d, off, HD);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) vp[(long)j * BS] = (bf16_t)v[j];
+    for (int j = 0; j < 4; ++j) vp[4 * j] = (bf16_t)v[j];
   }
 }
 
@@ -606,6 +604,19 @@ __device__ __forceinline__ void pf_glds16(const void* g, void* lds) {
   __builtin_amdgcn_global_load_lds(g, (lds_void_t*)lds, 16, 0, 0);
 }
 
+// LDS V image: 16-B chunk slot of (quad q, d pair p) is p ^ pf_vswz(q), so
+// the four key quads a ds_read_b64 lane group touches land 32 banks apart
+__device__ __forceinline__ int pf_vswz(int q) { return (q & 3) * 8; }
+
+// V^T fragment (keys 4g..4g+3 and 16+4g..16+4g+3 of row d) from the LDS page image
+template <int HD>
+__device__ __forceinline__ bf16x8_t pf_vfrag(const bf16_t* vpg, int d, int g) {
+  const int q0 = g, q1 = 4 + g;
+  const bf16_t* p0 = vpg + ((q0 * (HD / 2) + ((d >> 1) ^ pf_vswz(q0))) * 8 + (d & 1) * 4);
+  const bf16_t* p1 = vpg + ((q1 * (HD / 2) + ((d >> 1) ^ pf_vswz(q1))) * 8 + (d & 1) * 4);
+  return load_frag_2x8B(p0, p1);
+}
+
 // DMA one 32-token page of K and of V into the LDS tile slot `pslot`.
 template <int HD>
 __device__ __forceinline__ void pf_stage_page(bf16_t* k_lds, bf16_t* v_lds,
@@ -619,9 +630,11 @@ __device__ __forceinline__ void pf_stage_page(bf16_t* k_lds, bf16_t* v_lds,
     // K: row = key, 16-B chunk position swizzled by the row
     const int kr = off / HD, kpos = (off % HD) / 8;
     pf_glds16(kp + kr * HD + 8 * (kpos ^ kswz<HD>(kr)), k_lds + j * 2048 + wave * 512);
-    // V: row = d (32 keys = 64 B), 16-B pair position swizzled by d/4
-    const int vd = off / BS, vq = (off % BS) / 8;
-    pf_glds16(vp + vd * BS + 8 * (vq ^ ((vd >> 2) & 3)), v_lds + j * 2048 + wave * 512);
+    // V: key-quad page [BS/4][HD][4]; LDS chunk (quad q, slot pp) holds the
+    // global chunk d = 2p, 2p+1 with p = pp ^ vswz(q) (conflict-free 8-B
+    // fragment reads, pf_vfrag)
+    const int ch = off / 8, q = ch / (HD / 2), pp = ch % (HD / 2);
+    pf_glds16(vp + ((long)q * HD + 2 * (pp ^ pf_vswz(q))) * 4, v_lds + j * 2048 + wave * 512);
   }
 }
 
@@ -824,10 +837,7 @@ __global__ void __launch_bounds__(256, 2) paged_prefill_kernel(
       const bf16_t* vpg = vt + pp * PAGE;
 #pragma unroll
       for (int i = 0; i < NT; ++i) {
-        const int d = 16 * i + c;
-        const int sw = 2 * ((d >> 2) & 3);
-        const bf16_t* vr = vpg + d * BS;
-        const bf16x8_t vf = load_frag_2x8B(vr + 4 * (g ^ sw), vr + 4 * ((4 + g) ^ sw));
+        const bf16x8_t vf = pf_vfrag<HD>(vpg, 16 * i + c, g);
 #pragma unroll
         for (int n = 0; n < PF_NG; ++n) acc[n][i] = mfma16(vf, pf[n][pp], acc[n][i]);
       }

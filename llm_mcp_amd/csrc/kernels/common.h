@@ -85,6 +85,14 @@ __device__ __forceinline__ bf16x8_t load_frag16B(const bf16_t* p) {
 }
 
 // Two 8-byte halves -> one fragment (used for permuted-k operands).
+// V-cache page layout [BS/4][D][4] ("key-quad"): the 4 consecutive keys of
+// one d are 8 contiguous bytes (the 8-B V^T fragment run of the PV MFMA), and
+// one token's D values lie in one D x 8-B span, so a decode step's per-token
+// write touches D/16 128-B lines instead of D/2 (profiles/r2_decode_attention.md)
+__device__ __forceinline__ long vq_off(int d, int key, int D) {
+  return ((long)(key >> 2) * D + d) * 4 + (key & 3);
+}
+
 __device__ __forceinline__ bf16x8_t load_frag_2x8B(const bf16_t* p0, const bf16_t* p1) {
   bf16x4_t a = *reinterpret_cast<const bf16x4_t*>(p0);
   bf16x4_t b = *reinterpret_cast<const bf16x4_t*>(p1);

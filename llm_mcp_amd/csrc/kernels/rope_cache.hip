@@ -6,9 +6,13 @@
 // attention kernels, see decode_attn.hip):
 //   k_cache [num_blocks][Hkv][BS][D]   token-major: a K row is the 16-B A/B
 //                                      fragment source of S = K.Q^T
-//   v_cache [num_blocks][Hkv][D][BS]   d-major (transposed): 8 consecutive
-//                                      tokens of one d are the contiguous
-//                                      fragment of O^T = V^T.P^T
+//   v_cache [num_blocks][Hkv][BS/4][D][4]   key-quad: the 4 consecutive
+//                                      tokens of one d are the contiguous 8-B
+//                                      fragment run of O^T = V^T.P^T, and one
+//                                      token's D values share D/16 128-B lines
+//                                      (a d-major page [D][BS] spread a token
+//                                      over D/2 lines: 17-20 us per decode
+//                                      call of partial-line writes)
 // cos/sin come from a host-precomputed fp32 table [max_pos][D] (cos | sin),
 // so no transcendental runs on the device (guide App. B, element-wise).
 #include "common.h"
@@ -111,25 +115,25 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(
     }
   }
   if (slot < 0 || !v_cache) return;
-  // v -> transposed cache page (2-B scatter; one token per block so a page
-  // row of BS tokens is completed by BS consecutive blocks, merged in L2)
+  // v -> key-quad cache page (2-B stores 8 B apart: one token's D values
+  // share D/16 lines of its page)
 #pragma unroll
   for (int k = 0; k < VP; ++k) {
     const int e = (threadIdx.x + k * 256) * 4;
     if (e >= nv) continue;
     const int h = e / D, d = e % D;
-    bf16_t* vp = v_cache + (((long)blk * Hkv + h) * D + d) * BS + off;
+    bf16_t* vp = v_cache + ((long)blk * Hkv + h) * BS * D + vq_off(d, off, D);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) vp[(long)j * BS] = (bf16_t)vv[k][j];
+    for (int j = 0; j < 4; ++j) vp[4 * j] = (bf16_t)vv[k][j];
   }
 }
 
 // Prefill rows: 32 consecutive tokens per workgroup.  Rotation and the K
-// write as above; V goes through an LDS tile so that the transposed cache page
-// ([D][BS]) is written in whole rows -- a thread stores 8 consecutive tokens
-// of one d (16 B) whenever their slots are consecutive and 8-aligned (always
-// true inside a prefill chunk), and a wave covers 16 full 64-B page rows.
-// The per-token kernel's 2-B scatter remains for decode rows (one token per
+// write as above; V goes through an LDS tile so that the key-quad cache page
+// ([BS/4][D][4]) is written in 16-B pieces -- a thread stores 4 consecutive
+// tokens of 2 d whenever their slots are consecutive and 4-aligned (always
+// true inside a prefill chunk), and a wave covers 8 whole 128-B lines.
+// The per-token kernel's 2-B stores remain for decode rows (one token per
 // page per step, nothing to coalesce).
 constexpr int RT = 32;
 
@@ -208,25 +212,32 @@ __global__ void __launch_bounds__(256) rope_cache_tiled_kernel(
       *reinterpret_cast<u16x8*>(&vt[tt * LD + 8 * c]) = *reinterpret_cast<const u16x8*>(src);
     }
     __syncthreads();
-    for (int it = threadIdx.x; it < D * (RT / 8); it += blockDim.x) {
-      const int d = it / (RT / 8), tt0 = (it % (RT / 8)) * 8;
+    // one 16-B store per (key quad, d pair): 4 tokens x 2 d of the
+    // key-quad page, whenever the quad's 4 slots are consecutive and
+    // 4-aligned (always, inside a prefill chunk's whole pages)
+    for (int it = threadIdx.x; it < (D / 2) * (RT / 4); it += blockDim.x) {
+      const int d = 2 * (it % (D / 2)), tt0 = (it / (D / 2)) * 4;
       if (tt0 >= nt) continue;
       const int s0 = sslot[tt0];
-      bool vec = tt0 + 8 <= nt && s0 >= 0 && (s0 % 8) == 0 && BS % 8 == 0;
+      bool vec = tt0 + 4 <= nt && s0 >= 0 && (s0 % 4) == 0;
 #pragma unroll
-      for (int j = 1; j < 8; ++j) vec = vec && sslot[tt0 + j] == s0 + j;
+      for (int j = 1; j < 4; ++j) vec = vec && sslot[tt0 + j] == s0 + j;
       if (vec) {
         u16x8 w;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) w.v[j] = vt[(tt0 + j) * LD + d];
-        *reinterpret_cast<u16x8*>(v_cache + (((long)(s0 / BS) * Hkv + h) * D + d) * BS +
-                                  s0 % BS) = w;
+        for (int j = 0; j < 4; ++j) {
+          w.v[j] = vt[(tt0 + j) * LD + d];
+          w.v[4 + j] = vt[(tt0 + j) * LD + d + 1];
+        }
+        *reinterpret_cast<u16x8*>(v_cache + ((long)(s0 / BS) * Hkv + h) * BS * D +
+                                  vq_off(d, s0 % BS, D)) = w;
       } else {
-        for (int j = 0; j < 8 && tt0 + j < nt; ++j) {
+        for (int j = 0; j < 4 && tt0 + j < nt; ++j) {
           const int sl = sslot[tt0 + j];
-          if (sl >= 0)
-            v_cache[(((long)(sl / BS) * Hkv + h) * D + d) * BS + sl % BS] =
-                vt[(tt0 + j) * LD + d];
+          if (sl < 0) continue;
+          bf16_t* vp = v_cache + ((long)(sl / BS) * Hkv + h) * BS * D + vq_off(d, sl % BS, D);
+          vp[0] = vt[(tt0 + j) * LD + d];
+          vp[4] = vt[(tt0 + j) * LD + d + 1];
         }
       }
     }
@@ -278,7 +289,7 @@ __global__ void kv_write_kernel(const bf16_t* __restrict__ k, const bf16_t* __re
   for (int it = threadIdx.x; it < Hkv * D; it += blockDim.x) {
     const int h = it / D, d = it % D;
     k_cache[(((long)blk * Hkv + h) * BS + off) * D + d] = k[(long)t * kv_stride + it];
-    v_cache[(((long)blk * Hkv + h) * D + d) * BS + off] = v[(long)t * kv_stride + it];
+    v_cache[((long)blk * Hkv + h) * BS * D + vq_off(d, off, D)] = v[(long)t * kv_stride + it];
   }
 }
 

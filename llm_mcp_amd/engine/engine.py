@@ -306,7 +306,7 @@ class LLMEngine:
                               dtype=torch.bfloat16, device=self.device)
         self.k_caches = [self.kv[l, 0].view(self.num_blocks, self.Hkv, BLOCK_SIZE, self.D)
                          for l in range(cfg.num_layers)]
-        self.v_caches = [self.kv[l, 1].view(self.num_blocks, self.Hkv, self.D, BLOCK_SIZE)
+        self.v_caches = [self.kv[l, 1].view(self.num_blocks, self.Hkv, BLOCK_SIZE // 4, self.D, 4)
                          for l in range(cfg.num_layers)]
         log.info("KV cache: %d blocks x %d tokens (%.1f GB)", self.num_blocks, BLOCK_SIZE,
                  self.kv.numel() * 2 / 1e9)

@@ -119,7 +119,7 @@ class BertModel:
         bt = torch.from_numpy(bt_np).to(dev, non_blocking=True)
         ctx = torch.tensor(lens, dtype=torch.int32).to(dev, non_blocking=True)
         kc = torch.zeros((NB, H, PAGE, D), dtype=self.dtype, device=dev)
-        vc = torch.zeros((NB, H, D, PAGE), dtype=self.dtype, device=dev)
+        vc = torch.zeros((NB, H, PAGE // 4, D, 4), dtype=self.dtype, device=dev)   # key-quad
 
         x = ops.embed_gather(w["word"], ids)
         # absolute position + token-type rows enter as the LayerNorm's fused residual

@@ -118,7 +118,7 @@ class NomicBertModel:
         bt = torch.from_numpy(bt_np).to(dev, non_blocking=True)
         ctx = torch.tensor(lens, dtype=torch.int32).to(dev, non_blocking=True)
         kc = torch.zeros((NB, H, PAGE, D), dtype=self.dtype, device=dev)
-        vc = torch.zeros((NB, H, D, PAGE), dtype=self.dtype, device=dev)
+        vc = torch.zeros((NB, H, PAGE // 4, D, 4), dtype=self.dtype, device=dev)   # key-quad
 
         x = ops.embed_gather(w["word"], ids)
         x = ops.layer_norm(x, w["emb_ln_w"], w["emb_ln_b"], cfg.ln_eps,

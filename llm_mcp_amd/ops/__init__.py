@@ -188,8 +188,9 @@ def rope_and_cache(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Te
     BS = 0
     if k_cache is not None:
         _chk(slots is not None and slots.dtype == torch.int32, "slots int32")
-        _chk(k_cache.shape[1] == Hkv and k_cache.shape[3] == D and v_cache.shape[2] == D,
-             "cache layout [NB,Hkv,BS,D] / [NB,Hkv,D,BS]")
+        _chk(k_cache.shape[1] == Hkv and k_cache.shape[3] == D and v_cache.dim() == 5
+             and v_cache.shape[3] == D and v_cache.shape[4] == 4,
+             "cache layout [NB,Hkv,BS,D] / [NB,Hkv,BS/4,D,4]")
         BS = k_cache.shape[2]
     native().rope_cache(_ptr(qkv), qkv.stride(0), _ptr(positions), _ptr(cos_sin), T, Hq, Hkv, D,
                         _ptr(slots), _ptr(k_cache), _ptr(v_cache), BS,

@@ -7,7 +7,8 @@ They serve two purposes:
   CUDA/HIP tensor never takes this path: ``ops.kernels`` dispatches device
   tensors to the native kernels and raises if the extension is missing.
 
-Cache layouts match the kernels: k_cache [NB, Hkv, BS, D], v_cache [NB, Hkv, D, BS].
+Cache layouts match the kernels: k_cache [NB, Hkv, BS, D], v_cache [NB, Hkv, BS/4, D, 4]
+(key-quad: v_cache[blk, h, key // 4, d, key % 4]).
 """
 from __future__ import annotations
 
@@ -94,7 +95,7 @@ def write_cache(k, v, slots, k_cache, v_cache):
     s, k, v = s[keep], k[keep], v[keep]
     blk, off = s // BS, s % BS
     k_cache[blk, :, off, :] = k.to(k_cache.dtype)
-    v_cache[blk, :, :, off] = v.to(v_cache.dtype)
+    v_cache[blk, :, off // 4, :, off % 4] = v.to(v_cache.dtype)
 
 
 def gather_kv(k_cache, v_cache, block_table, n):
@@ -104,7 +105,7 @@ def gather_kv(k_cache, v_cache, block_table, n):
     blk = block_table.long()[idx // BS]
     off = idx % BS
     k = k_cache[blk, :, off, :]           # [n, Hkv, D]
-    v = v_cache[blk, :, :, off]           # [n, Hkv, D]
+    v = v_cache[blk, :, off // 4, :, off % 4]   # [n, Hkv, D]
     return k, v
 
 

@@ -50,7 +50,7 @@ def test_layer_norm():
 
 def _cache(NB, Hkv, D, BS=32):
     k = _bf(NB, Hkv, BS, D)
-    v = _bf(NB, Hkv, D, BS)
+    v = _bf(NB, Hkv, BS // 4, D, 4)      # key-quad V pages
     return k, v
 
 
@@ -80,7 +80,7 @@ def _rope_case(Hq, Hkv, D, layout, tile_from, qk_norm):
             torch.int32).to(DEV)
     slots[3] = -1
     kc, vc = torch.zeros(NB, Hkv, 32, D, device=DEV, dtype=torch.bfloat16), \
-        torch.zeros(NB, Hkv, D, 32, device=DEV, dtype=torch.bfloat16)
+        torch.zeros(NB, Hkv, 8, D, 4, device=DEV, dtype=torch.bfloat16)
     qkv0, kc0, vc0 = qkv.cpu(), kc.cpu(), vc.cpu()
     qn = kn = None
     if qk_norm:

@@ -44,7 +44,7 @@ def main():
     maxb = (a.ctx_hi + BS - 1) // BS
     nb = a.pages                                # 20000 pages x 64 KB x 2 = 2.6 GB (> MALL)
     k_cache = (torch.randn(nb, Hkv, BS, D, device=dev) * 0.5).to(torch.bfloat16)
-    v_cache = torch.randn(nb, Hkv, D, BS, device=dev).to(torch.bfloat16)
+    v_cache = torch.randn(nb, Hkv, BS // 4, D, 4, device=dev).to(torch.bfloat16)
     q = torch.randn(B, (Hq + 2 * Hkv if a.rope else Hq) * D, device=dev).to(torch.bfloat16)
     cl = ctx.to(dev)
     # page tables rotated per call over disjoint page sets: a call's K/V were

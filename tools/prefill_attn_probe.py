@@ -26,7 +26,7 @@ def run(name, S, L, Hq, Hkv, D, causal, iters, ng=0, tag=""):
     pages = -(-L // BS)
     NB = S * pages
     kc = torch.randn(NB, Hkv, BS, D, device=dev).to(torch.bfloat16)
-    vc = torch.randn(NB, Hkv, D, BS, device=dev).to(torch.bfloat16)
+    vc = torch.randn(NB, Hkv, BS // 4, D, 4, device=dev).to(torch.bfloat16)   # key-quad V pages
     bt = torch.randperm(NB, device=dev).to(torch.int32).view(S, pages)
     q = torch.randn(T, (Hq + 2 * Hkv) * D, device=dev).to(torch.bfloat16)
     cu = torch.arange(0, T + 1, L, dtype=torch.int32, device=dev)

@@ -29,7 +29,7 @@ def main():
     pages = torch.randperm(nb, device=dev)[:T].to(torch.int32)
     slots = pages * BS + torch.randint(0, BS, (T,), device=dev, dtype=torch.int32)
     kc = torch.zeros(nb, Hkv, BS, D, device=dev, dtype=torch.bfloat16)
-    vc = torch.zeros(nb, Hkv, D, BS, device=dev, dtype=torch.bfloat16)
+    vc = torch.zeros(nb, Hkv, BS // 4, D, 4, device=dev, dtype=torch.bfloat16)
     nat = ops.native()
     st = torch.cuda.current_stream().cuda_stream
 
@@ -48,7 +48,7 @@ def main():
     posp = (torch.arange(TP, device=dev, dtype=torch.int32) % 512)
     slotsp = torch.arange(TP, device=dev, dtype=torch.int32)
     kcp = torch.zeros(TP // BS, Hkv, BS, D, device=dev, dtype=torch.bfloat16)
-    vcp = torch.zeros(TP // BS, Hkv, D, BS, device=dev, dtype=torch.bfloat16)
+    vcp = torch.zeros(TP // BS, Hkv, BS // 4, D, 4, device=dev, dtype=torch.bfloat16)
     for _ in range(5):
         nat.rope_cache(qkvp.data_ptr(), qkvp.stride(0), posp.data_ptr(), cs.data_ptr(), TP, Hq,
                        Hkv, D, slotsp.data_ptr(), kcp.data_ptr(), vcp.data_ptr(), BS, 0, 0, 0, 0,
