@@ -285,7 +285,10 @@ __device__ __forceinline__ int effective_part(int ctx, int part_tokens, int max_
 // block id and K/V fragments are loaded before the current page is computed
 // (two pages in flight per wave); MODE 2: loads only (diagnostic ceiling);
 // MODE 3: loads only, every instruction one contiguous 1 KB (diagnostic);
-// MODE 5: MODE 0 with non-temporal K/V loads.
+// MODE 5: MODE 0 with non-temporal K/V loads; MODE 6: MODE 0 with a
+// block-table load per page.  MODE 0 / 5 read the segment's block ids once
+// into a VGPR (lane i: page pg0 + i) and take them by readlane, so a page's
+// K/V loads do not wait on its block-table load.
 template <int HD>
 struct DecodeSmem {
   float ml[4][16][2];
@@ -309,6 +312,7 @@ __device__ __forceinline__ void decode_segment(
   const int G = Hq / Hkv;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
   const int t0 = p * part_tokens, t1 = min(t0 + part_tokens, ctx);
+  constexpr bool kOnePage = MODE == 0 || MODE == 5 || MODE == 6;
 
   bf16x8_t qf[HD / 32];
   const bf16_t* qrow = q + (long)b * q_stride + (long)(kvh * G + c) * HD;
@@ -325,13 +329,13 @@ __device__ __forceinline__ void decode_segment(
   if (rp.cos_sin) {
     cs = rp.cos_sin + (long)rp.positions[b] * HD;
     // the one-page-at-a-time loops rotate q under their first page's loads
-    if constexpr (MODE != 0 && MODE != 5) rope_q_frags<HD>(qf, cs, g);
+    if constexpr (!kOnePage) rope_q_frags<HD>(qf, cs, g);
     writer = p == nparts - 1 && wave == (pg1 - 1 - pg0) % 4;
     if (writer) {
       const bf16_t* krow = q + (long)b * q_stride + (long)(Hq + kvh) * HD;
       rope_write_kv<HD>(krow, krow + (long)Hkv * HD, cs, rp.slots[b], kvh, Hkv,
                         const_cast<bf16_t*>(k_cache), const_cast<bf16_t*>(v_cache));
-      if constexpr (MODE != 0 && MODE != 5) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if constexpr (!kOnePage) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
   }
 
@@ -339,13 +343,21 @@ __device__ __forceinline__ void decode_segment(
   state_init(st);
   const float scale_log2 = scale * LOG2E;
   const int* bt = block_tables + (long)b * bt_stride;
-  if constexpr (MODE == 0 || MODE == 5) {
+  if constexpr (kOnePage) {
+    int btv = 0;
+    if constexpr (MODE != 6) btv = pg0 + lane < pg1 ? bt[pg0 + lane] : 0;
+    auto blk_of = [&](int pg) -> long {
+      if constexpr (MODE != 6) {
+        if (pg - pg0 < 64) return __builtin_amdgcn_readlane(btv, pg - pg0);
+      }
+      return bt[pg];
+    };
     int pg = pg0 + wave;
     if (cs) {
       if (pg < pg1 && !(writer && pg == pg1 - 1)) {
         // first page: its K/V fragments are in flight while q rotates (the
         // rotation's cos/sin round trip no longer serialises the segment)
-        const long blk = bt[pg];
+        const long blk = blk_of(pg);
         PageFrags<HD> f;
         load_page(f, k_cache + (blk * Hkv + kvh) * (BS * HD),
                   v_cache + (blk * Hkv + kvh) * (BS * HD));
@@ -358,7 +370,7 @@ __device__ __forceinline__ void decode_segment(
     }
     for (; pg < pg1; pg += 4) {
       if (writer && pg == pg1 - 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const long blk = bt[pg];
+      const long blk = blk_of(pg);
       const bf16_t* kp = k_cache + (blk * Hkv + kvh) * (BS * HD);
       const bf16_t* vp = v_cache + (blk * Hkv + kvh) * (BS * HD);
       process_page<HD, MODE == 5>(st, qf, kp, vp, pg * BS, t1 - 1, scale_log2);
@@ -551,6 +563,8 @@ int paged_decode(const void* q, long q_stride, const void* k_cache, const void* 
 #define LMX_DEC(HDV)                                                                          \
   if (g_decode_mode == 0 && max_parts == 1) { LMX_DEC_P(HDV, 0) }                             \
   else if (g_decode_mode == 5 && max_parts == 1) { LMX_DEC_P(HDV, 5) }                        \
+  else if (g_decode_mode == 6 && max_parts == 1) { LMX_DEC_P(HDV, 6) }                        \
+  else if (g_decode_mode == 6) { LMX_DEC_K(HDV, 6) }                                          \
   else if (g_decode_mode == 5) { LMX_DEC_K(HDV, 5) }                                          \
   else if (g_decode_mode == 1) { LMX_DEC_K(HDV, 1) }                                          \
   else if (g_decode_mode == 2) { LMX_DEC_K(HDV, 2) }                                          \
