@@ -65,7 +65,7 @@ class EmbeddingEngine:
             self._thread = None
 
     def _truncate(self, seqs):
-        return [s[: self.max_seq_len] if s else [0] for s in seqs]
+        return [s[: self.max_seq_len] if len(s) else [0] for s in seqs]
 
     # synchronous API (worker jobs, tests)
     def embed_sync(self, seqs: list[list[int]], dims: int | None = None) -> list[list[float]]:
@@ -189,7 +189,9 @@ class EmbeddingEngine:
             if not fused:
                 e = e[:, :r.dims or self.cfg.embed_dim]
                 e = e / e.norm(dim=-1, keepdim=True).clamp_min(1e-12)
-            outs.append(e.float().tolist())
+            # float32 rows (consumers needing JSON lists call .tolist(); the
+            # engine socket ships the bytes)
+            outs.append(e.float().numpy())
         self.stats["batches"] += 1
         self.stats["sequences"] += sum(len(r.seqs) for r in batch)
         self.stats["tokens"] += ntok

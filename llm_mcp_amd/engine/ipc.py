@@ -8,9 +8,11 @@ core -> Ollama ``/api/chat`` NDJSON hop (core/internal/api/handlers.go:2427):
 
   API -> engine   {"op": "submit", "rid", "prompt", "params", "priority"}
                   {"op": "abort", "rid"}        {"op": "info", "tag"}
+                  {"op": "embed", "tag", "ids": int32 bytes, "lens", "dims"}
   engine -> API   {"op": "ev", "ev": [[rid, token, logprob, finish], ...]}
                   (ONE message per engine step per connection)
                   {"op": "info", "tag", "info": {...}}
+                  {"op": "emb", "tag", "vec": float32 bytes, "shape", "error"}
 
 ``EngineClient`` exposes the same ``generate()`` async-iterator interface as
 ``AsyncEngine``, so the API layer does not care where the engine lives.
@@ -27,6 +29,7 @@ import struct
 import threading
 
 import msgpack
+import numpy as np
 
 from .async_engine import RequestStats, StreamItem
 from .engine import GenRequest, SamplingParams, TokenEvent
@@ -169,13 +172,27 @@ class EngineServer:
             c.send({"op": "emb", "tag": msg.get("tag"), "error": "no embedding model"})
             return
         from .embed_engine import EmbedRequest
-        req = EmbedRequest(self.embed_engine._truncate(msg["seqs"]), msg.get("dims"))
+        if "ids" in msg:
+            # binary form: one int32 buffer + lengths in, float32 rows out (no
+            # per-token Python objects on either side of the socket)
+            flat = np.frombuffer(msg["ids"], dtype=np.int32)
+            seqs = np.split(flat, np.cumsum(msg["lens"])[:-1]) if msg["lens"] else []
+        else:
+            seqs = msg["seqs"]
+        binary = "ids" in msg
+        req = EmbedRequest(self.embed_engine._truncate(seqs), msg.get("dims"))
         self.embed_engine._q.put(req)
 
         def reply():
             req.done.wait()
-            c.send({"op": "emb", "tag": msg.get("tag"), "vectors": req.result,
-                    "error": req.error})
+            out = {"op": "emb", "tag": msg.get("tag"), "error": req.error}
+            if req.error is None:
+                v = np.ascontiguousarray(np.asarray(req.result, dtype=np.float32))
+                if binary:
+                    out.update(vec=v.tobytes(), shape=list(v.shape))
+                else:
+                    out["vectors"] = v.tolist()
+            c.send(out)
         threading.Thread(target=reply, daemon=True).start()
 
     def engine_info(self) -> dict:
@@ -257,6 +274,9 @@ class EngineClient:
                     if f is not None and not f.done():
                         if msg.get("error"):
                             f.set_exception(RuntimeError(msg["error"]))
+                        elif "vec" in msg:
+                            f.set_result(np.frombuffer(msg["vec"], dtype=np.float32)
+                                         .reshape(msg["shape"]))
                         else:
                             f.set_result(msg["vectors"])
         except (asyncio.IncompleteReadError, ConnectionError):
@@ -288,11 +308,14 @@ class EngineClient:
         self._send({"op": "info", "tag": tag})
         return await asyncio.wait_for(f, timeout)
 
-    async def embed(self, seqs, dims=None) -> list[list[float]]:
+    async def embed(self, seqs, dims=None) -> np.ndarray:
         tag = next(self._ids)
         f = asyncio.get_running_loop().create_future()
         self._info_waiters[tag] = f
-        self._send({"op": "embed", "tag": tag, "seqs": [list(s) for s in seqs], "dims": dims})
+        lens = [len(s) for s in seqs]
+        flat = np.concatenate([np.asarray(s, dtype=np.int32) for s in seqs]) if seqs else \
+            np.zeros(0, np.int32)
+        self._send({"op": "embed", "tag": tag, "ids": flat.tobytes(), "lens": lens, "dims": dims})
         return await f
 
     async def complete(self, prompt_ids, params, priority=0):

@@ -183,6 +183,7 @@ class JobRunner:
                 for t in texts]
         t0 = time.time()
         vecs = await m.engine.embed(seqs, payload.get("dimensions"))
+        vecs = [list(map(float, v)) for v in vecs]      # JSON job result
         ms = int((time.time() - t0) * 1000)
         data = {"embedding": vecs[0]} if isinstance(inp, str) else {"embeddings": vecs}
         return ({"ok": True, "provider": "local", "model": m.model_id, "device_id": m.device_id,
