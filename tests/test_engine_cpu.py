@@ -144,3 +144,32 @@ def test_lookahead_stepping_matches_synchronous(monkeypatch):
     ahead, _ = run("1", stops)
     assert ahead == sync
     assert any(len(o) < 24 for o in ahead)     # streams ended on a stop token
+
+
+def test_lookahead_abort_and_late_arrivals(monkeypatch):
+    """Lookahead stepping with an abort of a running request (its in-flight
+    row becomes a dropped sample), a request arriving while a step is in
+    flight, and the engine draining to idle: every other stream completes
+    with its full token count and exactly one finish event."""
+    from llm_mcp_amd.engine.engine import GenRequest
+    monkeypatch.setenv("LMX_LOOKAHEAD", "1")
+    e = _engine()
+    assert e.lookahead
+    evs = {}
+    e.event_sink = lambda batch: [evs.setdefault(x.req.id, []).append(x) for x in batch]
+    sp = SamplingParams(temperature=0, max_tokens=10, ignore_eos=True)
+    reqs = [e.submit(GenRequest(list(range(i, i + 30)), sp)) for i in range(3)]
+    for _ in range(4):
+        e.step()
+    e.abort(reqs[1].id)
+    late = e.submit(GenRequest(list(range(100, 140)), sp))
+    for _ in range(200):
+        if not e.step() and e._la is None:
+            break
+    assert not e.sched.has_work and e._la is None
+    for r in (reqs[0], reqs[2], late):
+        toks = [x for x in evs[r.id] if x.token >= 0]
+        fins = [x for x in evs[r.id] if x.finish is not None]
+        assert len(toks) == 10 and len(fins) == 1 and fins[0].finish == "length"
+    assert [x.finish for x in evs[reqs[1].id] if x.finish is not None] == ["abort"]
+    assert e.num_active == 0

@@ -4,9 +4,8 @@
 set -o pipefail
 rounds=$1; shift
 mkdir -p gpurun_out
+args=("$@")
 for r in $(seq 1 $rounds); do
-  set -- "$@"
-  args=("$@")
   for ((i = 0; i < ${#args[@]}; i += 2)); do
     n=${args[i]}; e=${args[i+1]}
     [ "$e" = "-" ] && e=""
