@@ -173,3 +173,25 @@ def test_lookahead_abort_and_late_arrivals(monkeypatch):
         assert len(toks) == 10 and len(fins) == 1 and fins[0].finish == "length"
     assert [x.finish for x in evs[reqs[1].id] if x.finish is not None] == ["abort"]
     assert e.num_active == 0
+
+
+def test_kv_page_layouts_roundtrip():
+    """The CPU reference writes / gathers the kernels' page layouts: K pages
+    token-major [NB, Hkv, BS, D]; V pages key-quad [NB, Hkv, BS/4, D, 4]
+    (v_cache[blk, h, key // 4, d, key % 4]), the layout that keeps one
+    token's V inside D/16 128-B lines of its page."""
+    from llm_mcp_amd.ops import ref
+    NB, Hkv, BS, D, n = 6, 2, 32, 64, 70
+    kc = torch.zeros(NB, Hkv, BS, D)
+    vc = torch.zeros(NB, Hkv, BS // 4, D, 4)
+    k, v = torch.randn(n, Hkv, D), torch.randn(n, Hkv, D)
+    table = torch.tensor([4, 1, 5], dtype=torch.int32)
+    slots = torch.tensor([int(table[i // BS]) * BS + i % BS for i in range(n)],
+                         dtype=torch.int32)
+    ref.write_cache(k, v, slots, kc, vc)
+    k2, v2 = ref.gather_kv(kc, vc, table, n)
+    assert torch.equal(k2, k) and torch.equal(v2, v)
+    # flat offset of (block, head, key, d) in the V page = ((key // 4) * D + d) * 4 + key % 4
+    blk, h, key, d = 1, 1, 37 - 32, 9
+    flat = vc.reshape(NB, Hkv, BS * D)[blk, h, ((key // 4) * D + d) * 4 + key % 4]
+    assert flat == v[37, h, d]
