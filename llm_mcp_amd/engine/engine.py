@@ -515,7 +515,7 @@ class LLMEngine:
 
     def _fail_all(self, why: str):
         self._pending = None
-        if self._la is not None:
+        if self.lookahead:       # whatever step was in flight or half read back
             self._la = None
             self.sched.discard_lookahead()
         self._penalized.clear()
