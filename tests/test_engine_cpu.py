@@ -195,3 +195,34 @@ def test_kv_page_layouts_roundtrip():
     blk, h, key, d = 1, 1, 37 - 32, 9
     flat = vc.reshape(NB, Hkv, BS * D)[blk, h, ((key // 4) * D + d) * 4 + key % 4]
     assert flat == v[37, h, d]
+
+
+def test_lookahead_recovers_after_a_step_failure(monkeypatch):
+    """A step that raises while a lookahead step is in flight (as a HIP error
+    would): the engine fails the in-flight requests (the _loop path) and
+    serves new ones afterwards."""
+    from llm_mcp_amd.engine.engine import GenRequest
+    monkeypatch.setenv("LMX_LOOKAHEAD", "1")
+    e = _engine()
+    evs = []
+    e.event_sink = evs.extend
+    sp = SamplingParams(temperature=0, max_tokens=8, ignore_eos=True)
+    for i in range(3):
+        e.submit(GenRequest(list(range(i, i + 20)), sp))
+    real, calls = e._run_eager, [0]
+
+    def flaky(plan):
+        calls[0] += 1
+        if calls[0] == 4:
+            raise RuntimeError("HIP error: injected")
+        return real(plan)
+    monkeypatch.setattr(e, "_run_eager", flaky)
+    for _ in range(50):
+        try:
+            e.step()
+        except RuntimeError:
+            e._fail_all("engine_error")
+            break
+    assert sum(1 for x in evs if x.finish == "error") == 3 and e.num_active == 0
+    outs = e.generate([list(range(50, 80))], sp)
+    assert len(outs[0]) == 8
