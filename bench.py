@@ -324,6 +324,10 @@ def main() -> None:
                                   f"API process(es) on one SO_REUSEPORT port, replica "
                                   f"selection per stream; {len(lgs)} load generator(s)",
                        "sampling": {"temperature": a.temperature, "top_p": a.top_p},
+                       "engine": {"lookahead_stepping": bool(engine.lookahead),
+                                  "decode_graph_buckets": len(engine.graphs),
+                                  "kv_pages": "K [BS][D] token-major, V [BS/4][D][4] key-quad",
+                                  "max_batched_tokens": a.max_batched_tokens},
                        "engine_steps": sum(x["steps"] for x in allr),
                        "graph_steps": sum(x["graph_steps"] for x in allr)},
         }
