@@ -116,6 +116,11 @@ void Scheduler::finish(Seq* s, int reason) {
   bm_.free_seq(s->id);
   auto r = std::find(running_.begin(), running_.end(), s);
   if (r != running_.end()) running_.erase(r);
+  // lookahead: a sequence preempted by the plan after the one that sampled
+  // its stop token sits in waiting_ when patch() finishes it; it must leave
+  // that queue before its Seq is erased
+  auto w = std::find(waiting_.begin(), waiting_.end(), s);
+  if (w != waiting_.end()) waiting_.erase(w);
 }
 
 const StepPlan& Scheduler::schedule(int q_per_tile) {

@@ -139,10 +139,61 @@ static int scheduler_stress(int steps) {
   return 0;
 }
 
+
+// Lookahead protocol (update_lookahead / schedule / patch) under KV pressure:
+// stop tokens are frequent, so in-flight samples of sequences the next plan
+// preempted or already carries turn out to be STOP (a preempted
+// sequence finished by patch() used to stay in the waiting queue after its
+// Seq was freed).  Run under ASan this reports any such use-after-free.
+static int lookahead_stress(int steps) {
+  Scheduler s(12, 16, 16, 128, 512, true);
+  std::mt19937 rng(11);
+  int64_t next = 1;
+  int finished = 0;
+  std::set<int64_t> live;
+  std::vector<int32_t> prev;     // samples of the plan in flight, read back one step late
+  bool inflight = false;
+  for (int it = 0; it < steps; ++it) {
+    if (live.size() < 20 && rng() % 2 == 0) {
+      std::vector<int32_t> prompt(1 + rng() % 60);
+      for (auto& t : prompt) t = (int32_t)(10 + rng() % 1000);
+      s.add(next, prompt, 1 + rng() % 80, {7}, false, 0);
+      live.insert(next++);
+    }
+    if (!live.empty() && rng() % 23 == 0) {
+      auto it2 = live.begin();
+      std::advance(it2, rng() % live.size());
+      if (s.abort(*it2)) live.erase(it2);
+    }
+    if (inflight) s.update_lookahead();
+    const StepPlan& p = s.schedule(16);
+    std::vector<int32_t> toks(p.sample_rows.size());
+    for (auto& t : toks) t = rng() % 9 == 0 ? 7 : (int32_t)(10 + rng() % 1000);
+    if (inflight) {
+      for (auto& d : s.patch(prev.data(), (int)prev.size())) {
+        live.erase(d.first);
+        ++finished;
+      }
+    }
+    inflight = p.num_tokens > 0;
+    prev = toks;
+    if (!inflight) continue;
+    std::set<int32_t> slots;
+    for (int32_t sl : p.slots) {
+      CHECK(sl >= 0 && sl < 12 * 16);
+      CHECK(slots.insert(sl).second);
+    }
+  }
+  if (inflight) s.discard_lookahead();
+  std::printf("lookahead: %d finished, %lld preemptions\n", finished, (long long)s.preemptions());
+  return 0;
+}
+
 int main(int argc, char** argv) {
   const int jobs = argc > 1 ? std::atoi(argv[1]) : 3000;
   queue_stress(jobs, 8);
   scheduler_stress(argc > 2 ? std::atoi(argv[2]) : 4000);
+  lookahead_stress(argc > 2 ? std::atoi(argv[2]) : 4000);
   std::printf("ok\n");
   return 0;
 }

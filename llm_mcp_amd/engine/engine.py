@@ -141,9 +141,17 @@ _TORCH_DT = {np.dtype(np.int32): torch.int32, np.dtype(np.int64): torch.int64,
 
 
 class _FixedMeta:
-    """Fixed-layout metadata block (pinned host mirror + device buffer): the
+    """Fixed-layout metadata block (pinned host mirrors + device buffer): the
     static inputs of the captured decode graphs are device views into it, so
-    a replay needs exactly one host->device copy."""
+    a replay needs exactly one host->device copy.
+
+    Two host mirrors, alternated per step (``next()``): under lookahead
+    stepping step n's non-blocking upload is queued behind step n-1's
+    kernels, and the host writes step n+1's metadata after waiting only for
+    step n-1's tokens, i.e. possibly before step n's copy has read the
+    mirror.  Step n+1 writes the other mirror; ``next()`` also waits for the
+    event recorded after that mirror's last copy (already complete in the
+    steady state: it precedes the output event the host waited for)."""
 
     def __init__(self, fields: list[tuple[str, type, tuple]], device):
         off, spans = 0, []
@@ -152,16 +160,39 @@ class _FixedMeta:
             spans.append((name, off, dt, shape, n))
             off += (n + 15) & ~15
         self.nbytes = off
-        self.host_t = torch.empty(off, dtype=torch.uint8, pin_memory=device.type == "cuda")
+        self._cuda = device.type == "cuda"
+        self.host_ts = [torch.empty(off, dtype=torch.uint8, pin_memory=self._cuda)
+                        for _ in range(2)]
         self.dev_t = torch.empty(off, dtype=torch.uint8, device=device)
-        hnp = self.host_t.numpy()
-        self.h, self.d = {}, {}
-        for name, o, dt, shape, n in spans:
-            self.h[name] = hnp[o:o + n].view(dt).reshape(shape)
-            self.d[name] = self.dev_t[o:o + n].view(_TORCH_DT[np.dtype(dt)]).view(shape)
+        self._hs = []
+        for host_t in self.host_ts:
+            hnp = host_t.numpy()
+            self._hs.append({name: hnp[o:o + n].view(dt).reshape(shape)
+                             for name, o, dt, shape, n in spans})
+        self.d = {name: self.dev_t[o:o + n].view(_TORCH_DT[np.dtype(dt)]).view(shape)
+                  for name, o, dt, shape, n in spans}
+        self._evs = [None, None]
+        self._k = 0
+        self.h = self._hs[0]
+
+    def mirror_all(self):
+        """Copy the current host mirror into the other one (initial fill)."""
+        self.host_ts[self._k ^ 1].numpy()[:] = self.host_ts[self._k].numpy()
+
+    def next(self):
+        """Switch to the other host mirror before writing a step's fields."""
+        self._k ^= 1
+        ev = self._evs[self._k]
+        if ev is not None:
+            ev.synchronize()
+        self.h = self._hs[self._k]
 
     def upload(self):
-        self.dev_t.copy_(self.host_t, non_blocking=True)
+        self.dev_t.copy_(self.host_ts[self._k], non_blocking=True)
+        if self._cuda:
+            if self._evs[self._k] is None:
+                self._evs[self._k] = torch.cuda.Event()
+            self._evs[self._k].record()
 
 
 _TUNING_LOADED = False
@@ -350,6 +381,7 @@ class LLMEngine:
         pmeta = _FixedMeta([("win", np.int32, (Bmax, PEN_WINDOW)), ("ngen", np.int32, (Bmax,)),
                             ("pen", np.float32, (Bmax, 3))], dev)
         pmeta.h["win"][:] = -1; pmeta.h["ngen"][:] = 0; pmeta.h["pen"][:] = 0
+        pmeta.mirror_all()
         pmeta.upload()
         self._pmeta = pmeta
         h = meta.h
@@ -357,6 +389,7 @@ class LLMEngine:
         h["temp"][:] = 0; h["topk"][:] = 0; h["topp"][:] = 1; h["seeds"][:] = 0; h["offs"][:] = 0
         h["order"][:] = np.arange(Bmax, dtype=np.int32)
         h["src"][:] = -1
+        meta.mirror_all()
         meta.upload()
         self._gmeta = meta
         g = dict(meta.d)
@@ -663,7 +696,6 @@ class LLMEngine:
             st["g_launch"] += t2 - t1
             st["g_update"] += t5 - t4
         st["prefill_tokens"] += plan["num_prefill_tokens"]
-        st["generated_tokens"] += N
         return True
 
     def _step_la(self) -> bool:
@@ -748,7 +780,6 @@ class LLMEngine:
             st["g_schedule"] += t1 - t0
             st["g_launch"] += t2 - t1
         st["prefill_tokens"] += plan["num_prefill_tokens"]
-        st["generated_tokens"] += N
         return True
 
     def _la_resolve(self) -> np.ndarray:
@@ -813,6 +844,9 @@ class LLMEngine:
                 self._penalized.discard(rid)
                 self.stats["finished"] += 1
             evs.append(TokenEvent(req, tl[i], ll[i], reason))
+        # counted where the tokens are delivered: lookahead's dropped rows
+        # (a stopped or aborted sequence's extra sample) never reach here
+        self.stats["generated_tokens"] += len(evs)
         if evs and self.event_sink:
             self.event_sink(evs)
 
@@ -850,6 +884,7 @@ class LLMEngine:
         return ops.sample(logits, d["temp"], d["topk"], d["topp"], d["seeds"], d["offs"])
 
     def _run_graph(self, plan, B):
+        self._gmeta.next()
         g, h = self._gbuf, self._gmeta.h
         n = len(plan["seq_ids"])
         mb = plan["max_blocks"]
@@ -865,6 +900,8 @@ class LLMEngine:
             self.pen_graphs[B] = self._capture_bucket(B, penalties=True)
             log.info("captured the penalty decode graph of bucket %d in %.2fs", B,
                      time.time() - t0)
+            self._gmeta.next()
+            h = self._gmeta.h
         # rows n..B-1 are padding: no cache write (slot -1), a 1-token context
         for k, fill in (("ids", 0), ("pos", 0), ("slots", -1), ("ctx", 1), ("temp", 0),
                         ("topk", 0), ("topp", 1), ("seeds", 0), ("offs", 0)):
@@ -883,6 +920,7 @@ class LLMEngine:
         h["bt"][n:B, 0] = 0
         h["order"][:B] = ops.decode_order(h["ctx"][:B])
         if pen:
+            self._pmeta.next()
             ph = self._pmeta.h
             ph["win"][:n] = plan["pen_window"].reshape(n, -1)
             ph["win"][n:B] = -1

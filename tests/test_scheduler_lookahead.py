@@ -177,3 +177,30 @@ def test_stop_in_flight_makes_a_zombie_row():
     assert list(p2["seq_ids"]) == [2] and list(p2["input_src"]) == [1]
     assert s.patch(np.asarray([0, 60], np.int32)) == []
     assert p0["num_tokens"] == 6
+
+
+def test_stop_of_a_preempted_sequence_leaves_the_waiting_queue():
+    """the plan after a sampled step can preempt a sequence
+    whose in-flight sample turns out to be STOP.  patch() must take it out of
+    the waiting queue before freeing it, or the next schedule() reads a freed
+    Seq.  3 pages of 16: both 16-token prompts fill a page each, the decode
+    step needs a second page for each and only one is free, so sequence 2
+    (running_.back()) preempts itself."""
+    s = make(3)
+    s.add(1, list(range(100, 116)), 10, [STOP], False, 0)
+    s.add(2, list(range(200, 216)), 10, [STOP], False, 0)
+    p0 = s.schedule(16)
+    assert p0["num_tokens"] == 32
+    s.update_lookahead()
+    p1 = s.schedule(16)
+    assert list(p1["seq_ids"]) == [1] and list(p1["preempted"]) == [2]
+    fin = s.patch(np.asarray([50, STOP], np.int32))
+    assert fin == [(2, 1)]
+    s.update_lookahead()                  # consumes p1 (sequence 1 only)
+    p2 = s.schedule(16)
+    assert list(p2["seq_ids"]) == [1]     # the freed sequence 2 is gone from every queue
+    assert s.patch(np.asarray([60], np.int32)) == []
+    s.discard_lookahead()
+    assert s.abort(1)
+    assert not s.has_work
+    assert s.kv_usage == 0.0
