@@ -23,6 +23,12 @@ a barrier + ``torch.cuda.synchronize()`` on both sides on every rank; the
 elapsed time is the max over ranks and the value is all completion tokens
 streamed to the clients divided by it (weak scaling: C streams per GPU).
 
+``--tp T`` (BASELINE config 4, e.g. Llama-3-70B at T = 8): the N ranks form
+N / T tensor-parallel groups of T consecutive ranks (RCCL subgroups); each
+group's rank 0 is the engine behind the front door, its followers execute
+the leader's plans on their weight shards (parallel/tp_worker.py), and
+``--concurrency`` counts streams per engine.
+
 Prints ONE JSON line on rank 0 (driver contract).  ``--gpus`` must equal the
 launcher's WORLD_SIZE (a mismatch exits non-zero).  ``--rehearse-on-one-gpu``
 runs every rank on cuda:0 (a plumbing rehearsal on a 1-GPU box; its line is
@@ -54,7 +60,10 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--model", default="llama-3-8b")
-    ap.add_argument("--concurrency", type=int, default=256, help="concurrent streams per GPU")
+    ap.add_argument("--concurrency", type=int, default=256,
+                    help="concurrent streams per engine (per GPU at --tp 1)")
+    ap.add_argument("--tp", type=int, default=1,
+                    help="tensor-parallel degree: N/T engines of T GPUs each")
     ap.add_argument("--prompt-len", type=int, default=512)
     ap.add_argument("--max-tokens", type=int, default=256)
     ap.add_argument("--temperature", type=float, default=0.8)
@@ -96,14 +105,17 @@ def self_launch(a) -> None:
 
 def start_front_door(a, world: int, tag: str, socks: list[str]):
     """Rank 0, before any HIP call: the API processes (one shared port) and
-    the load generators.  Returns (api procs, loadgen procs, url, ready files)."""
+    the load generators.  Returns (api procs, loadgen procs, url, ready files).
+    ``socks``: one engine socket per engine (per TP group)."""
     port = free_port()
     url = f"http://127.0.0.1:{port}"
-    n_api = a.api_procs or max(1, math.ceil(world / 2))
-    n_lg = a.loadgen_procs or world
+    n_eng = len(socks)
+    n_api = a.api_procs or max(1, math.ceil(n_eng / 2))
+    n_lg = a.loadgen_procs or n_eng
     engines = []
-    for r, s in enumerate(socks):
-        engines += ["--engine", f"{a.model}=unix:{s},device=gpu{r}"]
+    for g, s in enumerate(socks):
+        dev = f"gpu{g}" if a.tp == 1 else f"tp{a.tp}:gpu{g * a.tp}-{(g + 1) * a.tp - 1}"
+        engines += ["--engine", f"{a.model}=unix:{s},device={dev}"]
     env = dict(os.environ, LOG_LEVEL=os.environ.get("LMX_BENCH_API_LOG", "WARNING"))
     # node-wide in-flight counts: the API processes balance on them together,
     # so no engine receives more streams than its slots (api/shared_load.py)
@@ -121,7 +133,7 @@ def start_front_door(a, world: int, tag: str, socks: list[str]):
              "--reuse-port", "--ready-file", rf, "--shared-load", load_file,
              "--api-index", str(i), "--api-count", str(n_api)] + engines,
             cwd=HERE, env=env, stdout=subprocess.DEVNULL))
-    total = a.concurrency * world
+    total = a.concurrency * n_eng
     per = [total // n_lg + (1 if i < total % n_lg else 0) for i in range(n_lg)]
     lgs = []
     for i, c in enumerate(per):
@@ -141,11 +153,14 @@ def main() -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != a.gpus:
         sys.exit(f"bench.py: --gpus {a.gpus} but the launcher started WORLD_SIZE={world} ranks")
+    if a.tp < 1 or world % a.tp:
+        sys.exit(f"bench.py: --tp {a.tp} does not divide --gpus {world}")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    n_eng, grp, grank = world // a.tp, rank // a.tp, rank % a.tp
     # all ranks of one launch share their parent (the torchrun agent)
     tag = str(os.getppid() if "WORLD_SIZE" in os.environ and world > 1 else os.getpid())
-    socks = [f"/tmp/lmx-bench-{tag}-{r}.sock" for r in range(world)]
+    socks = [f"/tmp/lmx-bench-{tag}-{g}.sock" for g in range(n_eng)]
 
     apis, lgs, ready_files = [], [], []
     if rank == 0:
@@ -169,6 +184,19 @@ def main() -> None:
         os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
         dist.init_process_group("gloo", timeout=datetime.timedelta(minutes=60))
     ops.native()  # fail loudly if the HIP kernels are missing
+    tpctx = None
+    if a.tp > 1:
+        # every rank creates every group's subgroups, in the same order
+        from llm_mcp_amd.models.llama import TPContext
+        for g in range(n_eng):
+            ranks = list(range(g * a.tp, (g + 1) * a.tp))
+            # one GPU per rank: RCCL over xGMI; a one-GPU rehearsal cannot put
+            # several ranks of one communicator on one device: gloo + the
+            # peer-memory all-reduce kernel (decode sizes)
+            tg = dist.new_group(ranks, backend="gloo" if a.rehearse_on_one_gpu else "nccl")
+            cg = dist.new_group(ranks, backend="gloo")
+            if g == grp:
+                tpctx = TPContext(grank, a.tp, tg, cpu_group=cg)
 
     t_init = time.time()
     ecfg = EngineConfig(model=a.model, max_num_seqs=max(a.concurrency, 1),
@@ -176,14 +204,30 @@ def main() -> None:
                         max_model_len=min(8192, a.prompt_len + a.max_tokens + 64),
                         use_graphs=not a.no_graphs, seed=rank,
                         kv_cache_gb=24 if a.rehearse_on_one_gpu else None)
-    engine = LLMEngine(ecfg, device=dev)
+    follower = None
+    if tpctx is None:
+        engine = LLMEngine(ecfg, device=dev)
+    else:
+        import threading
+
+        from llm_mcp_amd.parallel.tp_worker import build_tp_engine
+        engine = build_tp_engine(ecfg, dev, tpctx, f"bench-{tag}-g{grp}")
+        if grank:
+            # followers execute the leader's plans until it releases them
+            follower = threading.Thread(target=engine.run_follower, name="tp-follower",
+                                        daemon=True)
+            follower.start()
     log(f"engine ready on cuda:{gpu} in {time.time() - t_init:.1f}s: {engine.num_blocks} KV "
         f"blocks, {len(engine.graphs)} decode graphs, "
-        f"weights {engine.model.weight_bytes() / 1e9:.1f} GB")
-    server = EngineServer(engine, socks[rank], info={
-        "kind": "chat", "model": a.model, "device_id": f"gpu{rank}",
-        "max_model_len": engine.max_model_len, "capacity": ecfg.max_num_seqs})
-    server.start()
+        f"weights {engine.model.weight_bytes() / 1e9:.1f} GB"
+        + (f" (TP rank {grank}/{a.tp} of engine {grp})" if a.tp > 1 else ""))
+    server = None
+    if grank == 0:
+        server = EngineServer(engine, socks[grp], info={
+            "kind": "chat", "model": a.model,
+            "device_id": f"gpu{rank}" if a.tp == 1 else f"tp{a.tp}:gpu{rank}-{rank + a.tp - 1}",
+            "max_model_len": engine.max_model_len, "capacity": ecfg.max_num_seqs})
+        server.start()
 
     def barrier():
         if world > 1:
@@ -227,7 +271,7 @@ def main() -> None:
             if not ready.get("ready"):
                 raise RuntimeError("load generator could not reach the front door")
         log(f"front door up: {len(apis)} API processes on {url}, {len(lgs)} load generators, "
-            f"{a.concurrency * world} streams per wave over {world} engines")
+            f"{a.concurrency * n_eng} streams per wave over {n_eng} engines")
     barrier()
     if rank == 0:
         waves(a.warmup, "warmup")
@@ -246,8 +290,8 @@ def main() -> None:
     cpu0 = {k: cpu_s(v) for k, v in procs.items()}
 
     if a.load == "closed":
-        closed(a, rank, world, lgs, barrier)
-        shutdown(a, world, lgs, apis, server, ready_files)
+        closed(a, rank, world, n_eng, lgs, barrier)
+        shutdown(a, world, lgs, apis, server, ready_files, engine, follower)
         return
 
     barrier()
@@ -295,7 +339,8 @@ def main() -> None:
         ttfts = [t for r in results for t in r["ttfts"]]
         itls = [t for r in results for t in r["itls"]]
         value = tokens / slow
-        per_gpu = [round(x["gen_tokens"] / slow, 1) for x in allr]
+        # tokens are generated by the engines (TP leaders): one entry per engine
+        per_gpu = [round(x["gen_tokens"] / slow, 1) for x in allr if x["rank"] % a.tp == 0]
         nz = [v for v in per_gpu if v > 0]
         out = {
             "metric": METRIC,
@@ -316,11 +361,14 @@ def main() -> None:
             "front_door_cpu_pct": round(cpu.get("api", 0.0), 1),
             "loadgen_cpu_pct": round(cpu.get("loadgen", 0.0), 1),
             "engine_cpu_pct": [round(x["engine_cpu_pct"], 1) for x in allr],
-            "config": {"model": a.model, "global_batch": a.concurrency * world,
+            "config": {"model": a.model, "global_batch": a.concurrency * n_eng,
                        "seq_len": a.prompt_len + a.max_tokens, "prompt_len": a.prompt_len,
-                       "max_tokens": a.max_tokens, "parallelism": f"dp{world}",
+                       "max_tokens": a.max_tokens,
+                       "parallelism": f"dp{world}" if a.tp == 1 else
+                       (f"tp{a.tp}" if n_eng == 1 else f"dp{n_eng}xtp{a.tp}"),
                        "endpoint": "/v1/chat/completions stream=true",
-                       "serving": f"{world} engine rank(s) behind one front door: {len(apis)} "
+                       "serving": f"{n_eng} engine(s) of {a.tp} GPU(s) behind one front door: "
+                                  f"{len(apis)} "
                                   f"API process(es) on one SO_REUSEPORT port, replica "
                                   f"selection per stream; {len(lgs)} load generator(s)",
                        "sampling": {"temperature": a.temperature, "top_p": a.top_p},
@@ -337,16 +385,24 @@ def main() -> None:
                                             f"{world}-GPU number)"
         print(json.dumps(out), flush=True)
     barrier()
-    shutdown(a, world, lgs, apis, server, ready_files)
+    shutdown(a, world, lgs, apis, server, ready_files, engine, follower)
 
 
-def shutdown(a, world, lgs, apis, server, ready_files) -> None:
+def shutdown(a, world, lgs, apis, server, ready_files, engine=None, follower=None) -> None:
     for p in lgs:
         try:
             p.wait(timeout=30)
         except subprocess.TimeoutExpired:
             p.kill()
-    server.stop()
+    if server is not None:
+        server.stop()
+    if engine is not None and a.tp > 1:
+        if follower is None:
+            engine.release_followers()
+        else:
+            follower.join(timeout=60)
+        if engine.chan is not None:
+            engine.chan.close()
     for p in apis:
         p.terminate()
     for p in apis:
@@ -362,7 +418,7 @@ def shutdown(a, world, lgs, apis, server, ready_files) -> None:
         dist.destroy_process_group()
 
 
-def closed(a, rank, world, lgs, barrier) -> None:
+def closed(a, rank, world, n_eng, lgs, barrier) -> None:
     """--load closed: one constant-concurrency window through the same front
     door; prints its own JSON line (metric tagged "closed loop")."""
     import torch
@@ -389,7 +445,7 @@ def closed(a, rank, world, lgs, barrier) -> None:
                "ttft_p95_ms": round(percentile(ttfts, 95) * 1e3, 1),
                "itl_p50_ms": round(percentile(itls, 50) * 1e3, 2),
                "itl_p95_ms": round(percentile(itls, 95) * 1e3, 2),
-               "config": {"model": a.model, "concurrency": a.concurrency * world,
+               "config": {"model": a.model, "concurrency": a.concurrency * n_eng,
                           "prompt_len": a.prompt_len, "max_tokens": a.max_tokens,
                           "load": f"closed loop: {a.concurrency} streams per GPU, next request "
                                   f"on stream end, {a.closed_warmup:g} s warm-up, "

@@ -271,6 +271,8 @@ def cmd_serve(args):
     env.setdefault("CORE_HTTP_URL", "http://127.0.0.1" + args.http[args.http.rfind(":"):])
     sock_dir = args.socket_dir or "/tmp"
     extra = ["--cpu"] if args.cpu else []
+    if args.weights:       # real checkpoint for the chat model (each TP rank loads its shard)
+        extra += ["--weights", args.weights]
     plan = [dict(w, replica=k) for w in plan for k in range(max(1, args.replicas_per_gpu))
             if k == 0 or w["tp"] == 1]
     for w in plan:
@@ -330,6 +332,8 @@ def main(argv=None):
             p.add_argument("--embed-model", default=os.environ.get("LMX_EMBED_MODEL", ""))
             p.add_argument("--embed-gpus", default="")
             p.add_argument("--tp", type=int, default=int(os.environ.get("LMX_TP", "1")))
+            p.add_argument("--weights", default=os.environ.get("LMX_WEIGHTS", ""),
+                           help="safetensors dir of the chat model's real weights")
             p.add_argument("--max-num-seqs", type=int,
                            default=int(os.environ.get("LMX_MAX_BATCH", "256")))
             p.add_argument("--registry", default=os.environ.get("LMX_MODEL_REGISTRY", ""),

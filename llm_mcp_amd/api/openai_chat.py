@@ -73,6 +73,16 @@ def penalty_window(n) -> int:
     return 64 if n < 0 else min(n, 64)
 
 
+def logprob_item(tok, token: int, logprob: float, as_ids: bool = False) -> dict:
+    """One OpenAI ``logprobs.content`` entry: the token's text (or
+    ``token_id:<id>`` with ``return_tokens_as_token_ids``), its logprob and
+    its UTF-8 bytes (the sampler reports the chosen token only: no
+    top_logprobs alternatives)."""
+    b = tok.token_bytes(token)
+    return {"token": f"token_id:{token}" if as_ids else b.decode("utf-8", errors="replace"),
+            "logprob": logprob, "bytes": list(b), "top_logprobs": []}
+
+
 class ChatHandler:
     def __init__(self, state):
         self.state = state
@@ -145,12 +155,13 @@ class ChatHandler:
         if target is None:
             st.metrics.chat_requests(model, "none", "no_device")
             return write_error(503, "no_device", f"No online device has model '{model}'")
-        box = {"target": target}
+        # vLLM's extension: logprobs entries name their token as "token_id:<id>"
+        box = {"target": target, "ids": bool(body.get("return_tokens_as_token_ids", False))}
         t0 = time.time()
         try:
             if n > 1:
                 return await self._multi(request, target, model, prompt_ids, params, n, stream,
-                                         include_usage, extra_headers, t0)
+                                         include_usage, extra_headers, t0, box["ids"])
             if stream:
                 return await self._stream(request, box, model, prompt_ids, params,
                                           include_usage, extra_headers, t0)
@@ -209,7 +220,7 @@ class ChatHandler:
                 yield RESTART
 
     async def _multi(self, request, target, model, prompt_ids, params, n, stream, include_usage,
-                     headers, t0):
+                     headers, t0, as_ids=False):
         """``n`` choices: n engine requests of the same prompt (seeds seed+i, or
         distinct per-request seeds), batched by the engine like any other
         concurrent requests; streamed chunks carry their choice ``index``."""
@@ -231,9 +242,9 @@ class ChatHandler:
                         if stats["ttft"] is None:
                             stats["ttft"] = time.time() - t0
                         piece = detok.push(it.token)
-                        if sp.logprobs:
-                            lps.append(it.logprob)
-                        await q.put((i, piece, None, it.logprob))
+                        lp = logprob_item(target.tokenizer, it.token, it.logprob, as_ids) \
+                            if sp.logprobs else None
+                        await q.put((i, piece, None, lp))
                         if detok.stopped:
                             break
                     if it.finish is not None:
@@ -273,7 +284,7 @@ class ChatHandler:
                     c = {"index": i, "message": {"role": "assistant", "content": "".join(texts[i])},
                          "finish_reason": fins[i]}
                     if params.logprobs:
-                        c["logprobs"] = {"content": [{"logprob": v} for v in lps[i]]}
+                        c["logprobs"] = {"content": lps[i]}
                     choices.append(c)
                 resp = {"id": chat_id, "object": "chat.completion", "created": created,
                         "model": model, "choices": choices,
@@ -290,20 +301,22 @@ class ChatHandler:
             started = [False] * n
             left = n
 
-            def chunk(i, delta, fin=None):
+            def chunk(i, delta, fin=None, lp=None):
+                c = {"index": i, "delta": delta, "finish_reason": fin}
+                if lp is not None:
+                    c["logprobs"] = {"content": [lp]}
                 return b"data: " + dumps({"id": chat_id, "object": "chat.completion.chunk",
                                           "created": created, "model": model,
-                                          "choices": [{"index": i, "delta": delta,
-                                                       "finish_reason": fin}]}).encode() + b"\n\n"
+                                          "choices": [c]}).encode() + b"\n\n"
             try:
                 while left:
-                    i, piece, fin, _ = await q.get()
-                    if piece or not started[i]:
+                    i, piece, fin, lp = await q.get()
+                    if piece or not started[i] or lp is not None:
                         delta = {"content": piece}
                         if not started[i]:
                             delta["role"] = "assistant"
                             started[i] = True
-                        await resp.write(chunk(i, delta))
+                        await resp.write(chunk(i, delta, lp=lp))
                     if fin is not None:
                         left -= 1
                         await resp.write(chunk(i, {}, fin))
@@ -346,7 +359,8 @@ class ChatHandler:
                     n_out += 1
                     text.append(detok.push(it.token))
                     if params.logprobs:
-                        lps.append(it.logprob)
+                        lps.append(logprob_item(box["target"].tokenizer, it.token, it.logprob,
+                                                box.get("ids", False)))
                     if detok.stopped:
                         finish = "stop"
                         break
@@ -366,7 +380,7 @@ class ChatHandler:
         choice = {"index": 0, "message": {"role": "assistant", "content": "".join(text)},
                   "finish_reason": finish if finish in ("stop", "length") else "stop"}
         if params.logprobs:
-            choice["logprobs"] = {"content": [{"logprob": lp} for lp in lps]}
+            choice["logprobs"] = {"content": lps}
         resp = {
             "id": "chatcmpl-" + uuid.uuid4().hex[:24], "object": "chat.completion",
             "created": int(time.time()), "model": model, "choices": [choice],
@@ -398,13 +412,16 @@ class ChatHandler:
                 if it.token >= 0:
                     n_out += 1
                     piece = detok.push(it.token)
-                    if piece or first:
+                    # with logprobs every token gets its chunk (a partial UTF-8
+                    # character streams as "" content next to its logprob)
+                    if piece or first or params.logprobs:
                         if ttft is None:
                             ttft = time.time() - t0
                         role = '"role":"assistant",' if first else ""
                         first = False
-                        lp = (',"logprobs":{"content":[{"logprob":%.6f}]}' % it.logprob
-                              if params.logprobs else "")
+                        lp = (',"logprobs":{"content":[%s]}' % dumps(logprob_item(
+                            box["target"].tokenizer, it.token, it.logprob, box.get("ids", False)))
+                            if params.logprobs else "")
                         await resp.write((head + '{%s"content":%s}%s}]}\n\n'
                                           % (role, json.dumps(piece, ensure_ascii=False), lp)
                                           ).encode())

@@ -376,8 +376,21 @@ def main(argv=None):
     ap.add_argument("--fault", default="", help="mixed: LMX_FAULT spec for the targeted worker")
     ap.add_argument("--fault-device", default="", help="mixed: device-id suffix, e.g. gpu0.r1")
     ap.add_argument("--cpu", action="store_true", help="mixed: CPU engines (plumbing)")
+    ap.add_argument("--runs", type=int, default=1,
+                    help="mixed: repeat the whole run (fresh serve each time) and report the "
+                         "median jobs/s with the spread; pair with a fixed fault schedule "
+                         "(--fault gpu_error@N) so runs differ only in performance")
     a = ap.parse_args(argv)
     fn = {"queue": bench_queue, "embed": bench_embed, "mixed": bench_mixed}[a.what]
+    if a.what == "mixed" and a.runs > 1:
+        runs = [fn(a) for _ in range(a.runs)]
+        rates = sorted(r["jobs_per_s"] for r in runs)
+        med = sorted(runs, key=lambda r: r["jobs_per_s"])[len(runs) // 2]
+        out = dict(med, runs=a.runs, jobs_per_s_runs=[r["jobs_per_s"] for r in runs],
+                   jobs_per_s_median=med["jobs_per_s"],
+                   spread_pct=round((rates[-1] - rates[0]) / med["jobs_per_s"] * 100, 1))
+        print(json.dumps(out), flush=True)
+        return
     print(json.dumps(fn(a)), flush=True)
 
 

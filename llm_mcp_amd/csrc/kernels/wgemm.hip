@@ -27,8 +27,8 @@
 //
 // Split-K combine (S > 1) without a second launch and without every slice
 // writing a slab: each slice takes an arrival ticket when its main loop ends;
-// the first S-1 arrivals publish their fp32 partial tile (agent release,
-// publish counter) and leave, the last arrival waits for the S-1 publishes
+// the first S-1 arrivals publish their fp32 partial tile (write-through sc1
+// stores, publish counter) and leave, the last arrival waits for the S-1 publishes
 // (it only waits for workgroups that are already running: no residency
 // assumption), acquires, and adds the partials in slice order, so a call's
 // result does not depend on which slice arrived last.  Counters are re-armed
@@ -95,7 +95,8 @@ __device__ __forceinline__ float wg_silu(float g) { return g / (1.f + __expf(-g)
 
 // BN: column tile; WM x WN waves over the 256 x BN tile; BK: K-step;
 // NX / NW: A / W ring slots; EPI: 0 bf16, 2 partial slabs, 3 SwiGLU;
-// NT: non-temporal weight stream; MMA: 0 = data movement only (lab probe)
+// NT: non-temporal weight stream; MMA: 1 = compute, 0 = data movement only,
+// 2 / 3 = data movement without the A / W loads (lab probes)
 template <int BN, int WM, int WN, int BK, int NX, int NW, int EPI, int NT, int MMA, int PK>
 __global__ void __launch_bounds__(WM * WN * 64, 1)
 wgemm_kernel(bf16_t* __restrict__ C, const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
@@ -186,20 +187,28 @@ wgemm_kernel(bf16_t* __restrict__ C, const bf16_t* __restrict__ A, const bf16_t*
 #pragma unroll
   for (int v = -(NW - 1); v < 0; ++v) {
     const int tx = v + NX - 1, tw = v + NW - 1;
-    if (tx >= 0 && tx < nk) stage_x(tx % NX, kb + tx);
-    if (tw < nk) stage_w(tw % NW, kb + tw);
+    if (MMA != 2 && tx >= 0 && tx < nk) stage_x(tx % NX, kb + tx);
+    if (MMA != 3 && tw < nk) stage_w(tw % NW, kb + tw);
   }
   const int wi = WIF + (wextra ? 1 : 0);
   for (int t = 0; t < nk; ++t) {
     // A(t) was issued at v = t-NX+1; behind it: W(t+NW-NX) and the loads of
     // iterations t-NX+2 .. t-1.  W(t) is older than A(t).
-    if (t + NW - 2 < nk) {
-      if (wextra) wg_vmwait_c<(WIF + 1) + (NX - 2) * (XI + WIF + 1)>();
-      else wg_vmwait_c<WIF + (NX - 2) * (XI + WIF)>();
+    if constexpr (MMA >= 2) {
+      // probes: one operand only; wait for the oldest outstanding stage of it
+      constexpr int D = MMA == 2 ? NW : NX;
+      const int per = MMA == 2 ? wi : XI;
+      wg_vmwait(t + D - 2 < nk ? (D - 2) * per : 0);
+    } else if (t + NW - 2 < nk) {
+      // W(t+NW-NX), issued right after A(t), may stay in flight only when it
+      // is a later K-step than t (NW > NX; with NW == NX it is W(t) itself)
+      constexpr int LAG = NW > NX ? 1 : 0;
+      if (wextra) wg_vmwait_c<LAG * (WIF + 1) + (NX - 2) * (XI + WIF + 1)>();
+      else wg_vmwait_c<LAG * WIF + (NX - 2) * (XI + WIF)>();
     } else {
       int n = 0;
       for (int v = t - NX + 1; v <= t - 1; ++v) {
-        if (v + NW - 1 < nk) n += wi;
+        if (v + NW - 1 < nk && (v > t - NX + 1 || NW > NX)) n += wi;
         if (v > t - NX + 1 && v + NX - 1 < nk) n += XI;
       }
       wg_vmwait(n);
@@ -208,8 +217,8 @@ wgemm_kernel(bf16_t* __restrict__ C, const bf16_t* __restrict__ A, const bf16_t*
     __builtin_amdgcn_s_barrier();
     {
       const int tx = t + NX - 1, tw = t + NW - 1;
-      if (tx < nk) stage_x(tx % NX, kb + tx);
-      if (tw < nk) stage_w(tw % NW, kb + tw);
+      if (MMA != 2 && tx < nk) stage_x(tx % NX, kb + tx);
+      if (MMA != 3 && tw < nk) stage_w(tw % NW, kb + tw);
     }
     const bf16_t* xt = xs + (t % NX) * XSLOT;
     const bf16_t* wt = wsm + (t % NW) * WSLOT;
@@ -220,7 +229,7 @@ wgemm_kernel(bf16_t* __restrict__ C, const bf16_t* __restrict__ A, const bf16_t*
       for (int i = 0; i < TM; ++i) af[i] = wg_frag<BK>(xt, wr * WTM + 16 * i + fr, kk * 4 + fg);
 #pragma unroll
       for (int j = 0; j < TN; ++j) bw[j] = wg_frag<BK>(wt, wc * WTN + 16 * j + fr, kk * 4 + fg);
-      if constexpr (MMA) {
+      if constexpr (MMA == 1) {
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -261,23 +270,29 @@ wgemm_kernel(bf16_t* __restrict__ C, const bf16_t* __restrict__ A, const bf16_t*
       // slab of slice s of this tile: [256][BN] fp32, tile-major
       float* tslab = slabs + (long)tile * splits * BM * BN;
       if (order + 1 < (unsigned)splits) {
-        float* mine = tslab + (long)ks * BM * BN;
+        // publish write-through (sc1 stores: no L2 write-back fence), every
+        // storing wave drains, then one lane counts the publish (guide
+        // Guideline 16 R1; a release fence here flushes the XCD's whole dirty
+        // L2 and cost more than the main loop's tail)
+        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
+            tslab + (long)ks * BM * BN, 0, BM * BN * (int)sizeof(float), 0x00020000);
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
           const int m = wr * WTM + 16 * i + fr;
           if (m >= M) continue;
 #pragma unroll
-          for (int j = 0; j < TN; ++j)
-            *reinterpret_cast<f32x4_t*>(mine + m * BN + wc * WTN + 16 * j + 4 * fg) = acc[i][j];
+          for (int j = 0; j < TN; ++j) {
+            typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+            __builtin_amdgcn_raw_buffer_store_b128(
+                __builtin_bit_cast(u32x4_t, acc[i][j]), rsrc,
+                (m * BN + wc * WTN + 16 * j + 4 * fg) * (int)sizeof(float), 0, 16);
+          }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (threadIdx.x == 0) {
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (threadIdx.x == 0)
           __hip_atomic_fetch_add(&cnt[2 * tile + 1], 1u, __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT);
-        }
         return;
       }
       if (threadIdx.x == 0) {
@@ -395,7 +410,10 @@ struct WgCfg { int bn, wm, wn, bk, nx, nw; };
   X(9, 192, 2, 2, 64, 2, 3)         \
   X(10, 256, 2, 2, 64, 2, 2)        \
   X(11, 224, 4, 1, 64, 2, 3)        \
-  X(12, 128, 4, 1, 64, 2, 4)
+  X(12, 128, 4, 1, 64, 2, 4)        \
+  X(13, 112, 4, 1, 64, 3, 4)        \
+  X(14, 112, 4, 1, 32, 4, 12)       \
+  X(15, 128, 4, 1, 64, 3, 3)
 
 static const WgCfg kWgCfgs[] = {
 #define LMX_WG_ROW(ID, BN, WM, WN, BK, NX, NW) {BN, WM, WN, BK, NX, NW},
@@ -440,7 +458,10 @@ int wgemm(void* C, const void* A, const void* W, float* slabs, unsigned* cnt, in
           int N, int K, long lda, long ldw, long ldc, int cfg, int splits, int epi,
           hipStream_t stream) {
   if (M <= 0) return 0;
-  const int nt = (cfg >> 5) & 1, probe = (cfg >> 6) & 1, pk = (cfg >> 7) & 1;
+  const int nt = (cfg >> 5) & 1, pk = (cfg >> 7) & 1;
+  // bit 6: no MFMA; bit 8 / 9 (with bit 6): also skip the A / W loads
+  const int probe = (cfg >> 6) & 1 ? ((cfg >> 8) & 1 ? 2 : (cfg >> 9) & 1 ? 3 : 1) : 0;
+  constexpr int nt_probe = 0;
   cfg &= 31;
   if (cfg >= kNumWgCfgs || splits < 1 || M > 256) return -1;
   const WgCfg c = kWgCfgs[cfg];
@@ -470,6 +491,8 @@ int wgemm(void* C, const void* A, const void* W, float* slabs, unsigned* cnt, in
 #ifdef LMX_WGEMM_LAB
 #define LMX_WG_CASE(ID, BN, WM, WN, BK, NX, NW)                                               \
   case ID:                                                                                    \
+    if (probe == 2) { LMX_WG_E(BN, WM, WN, BK, NX, NW, nt_probe, 2) }                         \
+    if (probe == 3) { LMX_WG_E(BN, WM, WN, BK, NX, NW, nt_probe, 3) }                         \
     if (probe) { LMX_WG_E(BN, WM, WN, BK, NX, NW, 0, 0) }                                     \
     if (nt) { LMX_WG_E(BN, WM, WN, BK, NX, NW, 1, 1) }                                        \
     LMX_WG_E(BN, WM, WN, BK, NX, NW, 0, 1)

@@ -242,10 +242,21 @@ ALIASES = {
 
 
 def resolve(name: str):
-    key = ALIASES.get(name, name)
+    """Preset by name or alias.  ``<name>@L<n>`` keeps the preset's shapes
+    with only n layers (e.g. ``llama-3-70b@L8``: one-GPU rehearsals of the
+    70B TP layout; never a number for the full model)."""
+    base, _, layers = name.partition("@L")
+    key = ALIASES.get(base, base)
     if key not in PRESETS:
         raise KeyError(f"unknown model {name!r}; known: {sorted(PRESETS)}")
-    return PRESETS[key]
+    cfg = PRESETS[key]
+    if layers:
+        import dataclasses
+        n = int(layers)
+        if n < 1 or n > cfg.num_layers:
+            raise KeyError(f"{name!r}: layer count must be 1..{cfg.num_layers}")
+        cfg = dataclasses.replace(cfg, name=name, num_layers=n)
+    return cfg
 
 
 def from_hf_config(path: str | Path):

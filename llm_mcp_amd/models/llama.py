@@ -57,8 +57,13 @@ class TPContext:
     """Tensor-parallel placement of this rank (size 1 = no TP)."""
 
     def __init__(self, rank: int = 0, size: int = 1, group=None,
-                 sp_min_tokens: int | None = None):
+                 sp_min_tokens: int | None = None, cpu_group=None):
+        """``group``: the TP process group (RCCL on GPUs); ``cpu_group``: a
+        gloo group over the same ranks for host-side control values (built
+        by the caller when several TP groups share one world, where a
+        subgroup cannot be created lazily by one group alone)."""
         self.rank, self.size, self.group = rank, size, group
+        self.cpu_group = cpu_group
         self.peer = None      # parallel.peer_allreduce.PeerAllReduce when enabled
         # Sequence parallelism (SURVEY.md §2.4 "SP" row): steps with at least
         # this many tokens keep the residual stream row-sharded across the TP
@@ -103,6 +108,13 @@ class TPContext:
         torch.distributed.all_gather_into_tensor(out, src, group=self.group)
         return out
 
+    def global_rank(self, group_rank: int) -> int:
+        """World rank of a rank of this TP group (collectives that name a
+        root take world ranks)."""
+        if self.group is None or self.group == torch.distributed.group.WORLD:
+            return group_rank
+        return torch.distributed.get_global_rank(self.group, group_rank)
+
     def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
         if self.size > 1:
             if self.peer is not None and self.peer.supports(t):
@@ -131,7 +143,7 @@ class TPContext:
         if not src.is_cuda or self._host_staged(src):
             h = src.cpu()
             parts = [torch.empty_like(h) for _ in range(self.size)] if self.rank == 0 else None
-            torch.distributed.gather(h, parts, dst=0, group=self.group)
+            torch.distributed.gather(h, parts, dst=self.global_rank(0), group=self.group)
             if self.rank:
                 return None
             return torch.cat(parts, dim=-1).to(t.device, non_blocking=True)

@@ -150,9 +150,10 @@ def _cpu_group(group):
     return _CPU_GROUPS[key]
 
 
-def _agree(ok: bool, group) -> bool:
+def _agree(ok: bool, tp) -> bool:
     flag = torch.tensor([int(ok)], dtype=torch.int32)
-    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=_cpu_group(group))
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN,
+                    group=getattr(tp, "cpu_group", None) or _cpu_group(tp.group))
     return bool(flag.item())
 
 
@@ -167,11 +168,11 @@ def setup(tp, device: torch.device) -> PeerAllReduce | None:
     except Exception as ex:   # IPC unavailable (no peer access, old driver ...)
         log.warning("peer all-reduce unavailable: %s", ex)
         ok = False
-    if not _agree(ok, tp.group):          # symmetric: everyone built it, or nobody uses it
+    if not _agree(ok, tp):          # symmetric: everyone built it, or nobody uses it
         if ar is not None:
             ar.close()
         return None
-    if not _agree(ar.self_test(tp.all_reduce), tp.group):
+    if not _agree(ar.self_test(tp.all_reduce), tp):
         ar.close()
         return None
     tp.peer = ar

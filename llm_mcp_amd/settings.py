@@ -75,6 +75,7 @@ VARS: list[Var] = [
     Var("LMX_CHAT_MODEL", str, "llama-3-8b", "chat model preset / alias"),
     Var("LMX_EMBED_MODEL", str, "", "embedding model preset (e.g. nomic-embed-text)"),
     Var("LMX_TP", int, 1, "tensor-parallel degree of a chat-model group"),
+    Var("LMX_WEIGHTS", str, "", "safetensors dir of the chat model's real weights (`serve`)"),
     Var("LMX_MODEL_REGISTRY", str, "", "per-GPU placement 'GPUS:[tpN:|embed:]MODEL;...' "
         "(overrides LMX_CHAT_MODEL / LMX_TP for `serve`)"),
     Var("LMX_MAX_BATCH", int, 256, "max concurrent sequences per engine"),

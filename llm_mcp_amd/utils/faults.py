@@ -1,7 +1,10 @@
 """Deterministic fault injection for failure-path tests.
 
 ``LMX_FAULT="job_crash:0.2,gpu_error:0.05,claim_drop:0.1,step_hang:0.01"``
-(probabilities) with ``LMX_FAULT_SEED``.  The reference has no fault
+(probabilities) with ``LMX_FAULT_SEED``, or a fixed schedule
+``LMX_FAULT="gpu_error@40/200"``: the fault fires on the 40th and 200th call
+of its hook in this process (1-based; e.g. engine steps), so repeated runs of
+a benchmark fail at the same points and differ only in performance.  The reference has no fault
 injection; its failure paths (lease expiry, requeue, device offline) were
 only exercised by real outages.
 
@@ -29,8 +32,13 @@ class Faults:
     def __init__(self, spec: str | None = None, seed: int | None = None):
         spec = os.environ.get("LMX_FAULT", "") if spec is None else spec
         self.p: dict[str, float] = {}
+        self.at: dict[str, set[int]] = {}     # name -> call indices that fire
+        self.calls: dict[str, int] = {}
         for part in spec.split(","):
-            if ":" in part:
+            if "@" in part:
+                k, v = part.split("@", 1)
+                self.at[k.strip()] = {int(x) for x in v.split("/") if x.strip()}
+            elif ":" in part:
                 k, v = part.split(":", 1)
                 self.p[k.strip()] = float(v)
         seed = int(os.environ.get("LMX_FAULT_SEED", "0")) if seed is None else seed
@@ -39,9 +47,17 @@ class Faults:
         self.fired: dict[str, int] = {}
 
     def __bool__(self) -> bool:
-        return bool(self.p)
+        return bool(self.p) or bool(self.at)
 
     def hit(self, name: str) -> bool:
+        sched = self.at.get(name)
+        if sched is not None:
+            with self._lock:
+                n = self.calls[name] = self.calls.get(name, 0) + 1
+                fire = n in sched
+                if fire:
+                    self.fired[name] = self.fired.get(name, 0) + 1
+            return fire
         p = self.p.get(name, 0.0)
         if p <= 0.0:
             return False

@@ -129,3 +129,13 @@ def test_injected_gpu_error_fails_requests_engine_survives():
     finally:
         set_faults(None)
         e.stop()
+
+
+def test_fault_schedule_fires_at_fixed_calls():
+    from llm_mcp_amd.utils.faults import Faults
+    f = Faults("gpu_error@3/5,job_crash:0.0")
+    fired = [f.hit("gpu_error") for _ in range(7)]
+    assert fired == [False, False, True, False, True, False, False]
+    assert f.fired["gpu_error"] == 2 and not f.hit("job_crash") and bool(f)
+    g = Faults("gpu_error@3/5")
+    assert [g.hit("gpu_error") for _ in range(7)] == fired     # same schedule every process
