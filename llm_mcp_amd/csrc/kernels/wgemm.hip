@@ -150,8 +150,11 @@ wgemm_kernel(bf16_t* __restrict__ C, const bf16_t* __restrict__ A, const bf16_t*
     bf16_t* dst = wsm + slot * WSLOT;
     if constexpr (PK) {
       // packed weights (wgemm_pack): the [BN][BK] LDS image of (tile, kstep)
-      // is one contiguous run, read lane-linearly
-      const bf16_t* src = W + ((long)tile * nk_all + kstep) * WSLOT + lane * 8;
+      // is one contiguous run, read lane-linearly; PK 1: tiles outermost
+      // (a workgroup streams one contiguous region), PK 2: K-steps outermost
+      // (the workgroups of a K-step read adjacent images)
+      const long blk = PK == 1 ? (long)tile * nk_all + kstep : (long)kstep * tiles_n + tile;
+      const bf16_t* src = W + blk * WSLOT + lane * 8;
 #pragma unroll
       for (int i = 0; i < WIF; ++i)
         wg_glds16<NT ? 2 : 0>(src + (i * RPR + wave * RPW) * BK, dst + (i * RPR + wave * RPW) * BK);
@@ -378,7 +381,7 @@ wgemm_kernel(bf16_t* __restrict__ C, const bf16_t* __restrict__ A, const bf16_t*
 //       W[tile*BN + r][kstep*BK + 8 (p ^ swz(r)) .. +8]
 template <int BK>
 __global__ void wgemm_pack_kernel(bf16_t* __restrict__ P, const bf16_t* __restrict__ W, int N,
-                                  int K, long ldw, int BN) {
+                                  int K, long ldw, int BN, int kmajor) {
   constexpr int CPR = BK / 8;
   const long chunks = (long)N * K / 8;
   const int nk = K / BK;
@@ -388,7 +391,9 @@ __global__ void wgemm_pack_kernel(bf16_t* __restrict__ P, const bf16_t* __restri
     const long rowblk = c / CPR;                 // (tile * nk + kstep) * BN + r
     const int r = (int)(rowblk % BN);
     const long tk = rowblk / BN;
-    const int kstep = (int)(tk % nk), tile = (int)(tk / nk);
+    const int tiles = N / BN;
+    const int kstep = kmajor ? (int)(tk / tiles) : (int)(tk % nk);
+    const int tile = kmajor ? (int)(tk % tiles) : (int)(tk / nk);
     const long src = (long)(tile * BN + r) * ldw + (long)kstep * BK + 8 * (p ^ wg_swz<BK>(r));
     *reinterpret_cast<u16x8*>(P + c * 8) = *reinterpret_cast<const u16x8*>(W + src);
   }
@@ -413,7 +418,8 @@ struct WgCfg { int bn, wm, wn, bk, nx, nw; };
   X(12, 128, 4, 1, 64, 2, 4)        \
   X(13, 112, 4, 1, 64, 3, 4)        \
   X(14, 112, 4, 1, 32, 4, 12)       \
-  X(15, 128, 4, 1, 64, 3, 3)
+  X(15, 128, 4, 1, 64, 3, 3)        \
+  X(16, 112, 4, 1, 32, 2, 18)
 
 static const WgCfg kWgCfgs[] = {
 #define LMX_WG_ROW(ID, BN, WM, WN, BK, NX, NW) {BN, WM, WN, BK, NX, NW},
@@ -453,12 +459,13 @@ static int wg_launch(bf16_t* C, const bf16_t* A, const bf16_t* W, float* slabs, 
 
 // epi: 0 bf16, 2 partial slabs, 3 SwiGLU (4-row gate/up blocks); cfg bit 5:
 // non-temporal weight stream; cfg bit 6: no MFMA (data-movement probe);
-// cfg bit 7: W is in the packed layout of this configuration (wgemm_pack)
+// cfg bit 7: W is in the packed layout of this configuration (wgemm_pack);
+// bit 10 (with bit 7): the K-step-major packed layout
 int wgemm(void* C, const void* A, const void* W, float* slabs, unsigned* cnt, int n_cnt, int M,
           int N, int K, long lda, long ldw, long ldc, int cfg, int splits, int epi,
           hipStream_t stream) {
   if (M <= 0) return 0;
-  const int nt = (cfg >> 5) & 1, pk = (cfg >> 7) & 1;
+  const int nt = (cfg >> 5) & 1, pk = (cfg >> 7) & 1 ? ((cfg >> 10) & 1 ? 2 : 1) : 0;
   // bit 6: no MFMA; bit 8 / 9 (with bit 6): also skip the A / W loads
   const int probe = (cfg >> 6) & 1 ? ((cfg >> 8) & 1 ? 2 : (cfg >> 9) & 1 ? 3 : 1) : 0;
   constexpr int nt_probe = 0;
@@ -486,6 +493,7 @@ int wgemm(void* C, const void* A, const void* W, float* slabs, unsigned* cnt, in
   return wg_launch<BN, WM, WN, BK, NX, NW, 0, NT, MMA, PK>(C_, A_, W_, slabs, cnt, M, N, K,    \
                                                            lda, ldw, ldc, splits, stream);
 #define LMX_WG_E(BN, WM, WN, BK, NX, NW, NT, MMA)                                               \
+  if (pk == 2) { LMX_WG_P(BN, WM, WN, BK, NX, NW, NT, MMA, 2) }                               \
   if (pk) { LMX_WG_P(BN, WM, WN, BK, NX, NW, NT, MMA, 1) }                                    \
   LMX_WG_P(BN, WM, WN, BK, NX, NW, NT, MMA, 0)
 #ifdef LMX_WGEMM_LAB
@@ -512,16 +520,20 @@ int wgemm(void* C, const void* A, const void* W, float* slabs, unsigned* cnt, in
 
 // Packs W [N][K] (row stride ldw) into P for configuration cfg (N*K elements)
 int wgemm_pack(void* P, const void* W, int N, int K, long ldw, int cfg, hipStream_t stream) {
+  const bool kmajor = (cfg >> 10) & 1;
   cfg &= 31;
   if (cfg >= kNumWgCfgs) return -1;
   const WgCfg c = kWgCfgs[cfg];
   if (N % c.bn != 0 || K % c.bk != 0 || ldw % 8 != 0) return -1;
   const long chunks = (long)N * K / 8;
   const int grid = (int)std::min<long>(8192, (chunks + 255) / 256);
+  const int km = kmajor ? 1 : 0;
   if (c.bk == 64)
-    wgemm_pack_kernel<64><<<grid, 256, 0, stream>>>((bf16_t*)P, (const bf16_t*)W, N, K, ldw, c.bn);
+    wgemm_pack_kernel<64><<<grid, 256, 0, stream>>>((bf16_t*)P, (const bf16_t*)W, N, K, ldw, c.bn,
+                                                    km);
   else
-    wgemm_pack_kernel<32><<<grid, 256, 0, stream>>>((bf16_t*)P, (const bf16_t*)W, N, K, ldw, c.bn);
+    wgemm_pack_kernel<32><<<grid, 256, 0, stream>>>((bf16_t*)P, (const bf16_t*)W, N, K, ldw, c.bn,
+                                                    km);
   return (int)hipGetLastError();
 }
 

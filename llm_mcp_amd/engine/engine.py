@@ -304,8 +304,14 @@ class LLMEngine:
         # (a TP group's plan channel is attached after construction: step()
         # checks it again)
         la_env = os.environ.get("LMX_LOOKAHEAD", "")
-        self.lookahead = plan_channel is None and self.tp.size == 1 and (
-            la_env == "1" or (la_env != "0" and self.device.type == "cuda"))
+        self.lookahead = la_env == "1" or (la_env != "0" and self.device.type == "cuda")
+        # lookahead in a TP group: the followers sample the step too (the
+        # logits are all-gathered to every rank, the sampler is seeded and
+        # deterministic), so every rank holds step n's tokens on its device
+        # for step n+1's ids_from_prev gather and the leader never has to
+        # ship tokens to them
+        self.sample_all = self.tp.size > 1 and self.lookahead
+        self.tp.logits_to_all = self.sample_all
         self._la = None                    # the launched step not yet read back
         self._penalized: set[int] = set()  # active requests with penalty windows
         if ecfg.use_graphs and self.device.type == "cuda" and not ops.debug_sync():
@@ -429,7 +435,7 @@ class LLMEngine:
             ops.ids_from_prev(g["ids"][:B], g["src"][:B], g["tok"])
             logits = self.model.forward(inp, self.k_caches, self.v_caches, ws,
                                         self.ecfg.part_tokens)
-            if self.is_leader:
+            if self.is_leader or self.sample_all:
                 if penalties:
                     pd = pmeta.d
                     ops.apply_penalties(logits, pd["win"][:B], pd["ngen"][:B], pd["pen"][:B])
@@ -498,7 +504,11 @@ class LLMEngine:
             if bucket is not None:
                 self._run_graph(plan, bucket)
             else:
-                self._run_eager(plan)
+                tok, _ = self._run_eager(plan)
+                N = len(plan["sample_rows"])
+                if self.sample_all and self.graphs and N:
+                    # the next (graph) step gathers its inputs from here
+                    self._gbuf["tok"][:N].copy_(tok[:N], non_blocking=True)
             if msg.get("probe"):
                 self._comm_probe()
             n += 1
@@ -628,7 +638,7 @@ class LLMEngine:
             return False
         self._step_started = time.monotonic()
         try:
-            return self._step_la() if self.lookahead and self.chan is None else self._step()
+            return self._step_la() if self.lookahead else self._step()
         finally:
             self._step_started = 0.0
 
@@ -654,11 +664,7 @@ class LLMEngine:
             bucket = next((b for b in self._bucket_list if b >= nd), None)
         probe = (self.tp.size > 1 and self._comm_every > 0
                  and self.stats["steps"] % self._comm_every == self._comm_every - 1)
-        if self.chan is not None:
-            from ..parallel.plan_channel import encode_plan
-            msg = encode_plan(plan, bucket)
-            msg["probe"] = int(probe)
-            self.chan.publish(msg)
+        self._publish(plan, bucket, probe)
         t1 = time.perf_counter()
         if bucket is not None:
             tok, lp = self._run_graph(plan, bucket)
@@ -697,6 +703,15 @@ class LLMEngine:
             st["g_update"] += t5 - t4
         st["prefill_tokens"] += plan["num_prefill_tokens"]
         return True
+
+    def _publish(self, plan, bucket, probe: bool) -> None:
+        """TP leader: hand the step's plan to the followers (no-op alone)."""
+        if self.chan is None:
+            return
+        from ..parallel.plan_channel import encode_plan
+        msg = encode_plan(plan, bucket, full=self.sample_all)
+        msg["probe"] = int(probe)
+        self.chan.publish(msg)
 
     def _step_la(self) -> bool:
         """Lookahead step (one-step asynchronous scheduling):
@@ -739,9 +754,12 @@ class LLMEngine:
         bucket = None
         if nd == S == T and self.graphs:
             bucket = next((b for b in self._bucket_list if b >= nd), None)
+        probe = (self.tp.size > 1 and self._comm_every > 0
+                 and self.stats["steps"] % self._comm_every == self._comm_every - 1)
         t1 = time.perf_counter()
         tw = 0.0
         if bucket is not None:
+            self._publish(plan, bucket, probe)
             tok, lp = self._run_graph(plan, bucket)
         else:
             if la is not None:      # this step's inputs need step n's tokens on the host
@@ -755,6 +773,7 @@ class LLMEngine:
                     plan["input_ids"][m] = prev[src[m]]
             elif plan["num_pending_inputs"]:
                 raise RuntimeError("lookahead plan references an unread step")
+            self._publish(plan, None, probe)
             tok, lp = self._run_eager(plan)
             if self.graphs and N:
                 # the next (graph) step gathers its input tokens from here
@@ -766,6 +785,8 @@ class LLMEngine:
         t3 = time.perf_counter()
         self._la = {"seq_ids": plan["seq_ids"], "sample_seq": plan["sample_seq"], "N": N,
                     "slot": k}
+        if probe:
+            self._comm_probe()
         st = self.stats
         st["t_schedule"] += t1 - t0
         st["t_launch"] += t2 - t1 - tw
@@ -866,7 +887,8 @@ class LLMEngine:
         nd = plan["num_decode"]
         if nd > 1:
             items.append(("order", ops.decode_order(plan["context_lens"][:nd])))
-        pen = bool(plan.get("any_penalty")) and self.is_leader
+        samples = self.is_leader or self.sample_all
+        pen = bool(plan.get("any_penalty")) and samples
         if pen:   # one pack, one upload: the pinned staging buffer is reused per call
             N = len(plan["sample_rows"])
             items += [("win", plan["pen_window"].reshape(N, PEN_WINDOW)),
@@ -877,7 +899,7 @@ class LLMEngine:
                          d["cu"], d["tiles"], d["rows"], T, S, decode_order=d.get("order"))
         ws = self._decode_ws(plan["num_decode"]) if plan["num_decode"] else self.decode_ws
         logits = self.model.forward(inp, self.k_caches, self.v_caches, ws, self.ecfg.part_tokens)
-        if not self.is_leader:
+        if not samples:
             return None, None
         if pen:
             ops.apply_penalties(logits, d["win"], d["ngen"], d["pen"])
@@ -888,7 +910,7 @@ class LLMEngine:
         g, h = self._gbuf, self._gmeta.h
         n = len(plan["seq_ids"])
         mb = plan["max_blocks"]
-        pen = bool(plan.get("any_penalty")) and self.is_leader
+        pen = bool(plan.get("any_penalty")) and (self.is_leader or self.sample_all)
         if pen and B not in self.pen_graphs:
             # one-time capture of this bucket's penalty variant; its warm-up
             # run must not write the KV cache: no slots, 1-token contexts

@@ -64,6 +64,10 @@ class TPContext:
         subgroup cannot be created lazily by one group alone)."""
         self.rank, self.size, self.group = rank, size, group
         self.cpu_group = cpu_group
+        # lookahead TP (engine.sample_all): every rank keeps the full logits
+        # and samples them itself, so each rank holds the step's tokens on
+        # its device for the next step's ids_from_prev gather
+        self.logits_to_all = False
         self.peer = None      # parallel.peer_allreduce.PeerAllReduce when enabled
         # Sequence parallelism (SURVEY.md §2.4 "SP" row): steps with at least
         # this many tokens keep the residual stream row-sharded across the TP
@@ -142,6 +146,10 @@ class TPContext:
         B, Vs = src.shape
         if not src.is_cuda or self._host_staged(src):
             h = src.cpu()
+            if self.logits_to_all:
+                parts = [torch.empty_like(h) for _ in range(self.size)]
+                torch.distributed.all_gather(parts, h, group=self.group)
+                return torch.cat(parts, dim=-1).to(t.device, non_blocking=True)
             parts = [torch.empty_like(h) for _ in range(self.size)] if self.rank == 0 else None
             torch.distributed.gather(h, parts, dst=self.global_rank(0), group=self.group)
             if self.rank:
@@ -149,7 +157,7 @@ class TPContext:
             return torch.cat(parts, dim=-1).to(t.device, non_blocking=True)
         out = torch.empty((self.size * B, Vs), dtype=src.dtype, device=src.device)
         torch.distributed.all_gather_into_tensor(out, src, group=self.group)
-        if self.rank:
+        if self.rank and not self.logits_to_all:
             return None
         return out.view(self.size, B, Vs).permute(1, 0, 2).reshape(B, self.size * Vs)
 

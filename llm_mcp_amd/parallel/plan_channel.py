@@ -34,6 +34,10 @@ _HDR = 4096
 PLAN_KEYS = ("input_ids", "positions", "slots", "context_lens", "cu_q", "block_tables",
              "prefill_tiles", "sample_rows", "seq_ids", "temp", "topk", "topp", "seeds", "offs")
 PLAN_INTS = ("num_decode", "max_blocks", "num_tokens", "num_prefill_tokens", "max_context")
+# present when the followers sample too (lookahead TP): pending-input rows and
+# the penalty windows of the step
+PLAN_OPT_KEYS = ("input_src", "pen_window", "pen_ngen", "pen_params")
+PLAN_OPT_INTS = ("num_pending_inputs", "any_penalty")
 BEAT_S = 1.0
 
 
@@ -62,23 +66,31 @@ def leader_timeout_s() -> float:
     return float(os.environ.get("LMX_TP_LEADER_TIMEOUT_S", "30"))
 
 
-def encode_plan(plan: dict, bucket: int | None) -> dict:
+def encode_plan(plan: dict, bucket: int | None, full: bool = False) -> dict:
+    """``full``: also the keys the followers need to sample (lookahead TP)."""
     msg = {"cmd": "step", "bucket": bucket or 0}
-    for k in PLAN_KEYS:
-        a = np.ascontiguousarray(plan[k])
+    keys = PLAN_KEYS + (PLAN_OPT_KEYS if full else ())
+    for k in keys:
+        if k not in plan:
+            continue
+        a = np.ascontiguousarray(plan[k]).reshape(-1)
         msg[k] = (a.dtype.str, a.shape[0], a.tobytes())
-    for k in PLAN_INTS:
-        msg[k] = int(plan[k])
+    for k in PLAN_INTS + (PLAN_OPT_INTS if full else ()):
+        if k in plan:
+            msg[k] = int(plan[k])
     return msg
 
 
 def decode_plan(msg: dict) -> tuple[dict, int | None]:
     plan = {}
-    for k in PLAN_KEYS:
+    for k in PLAN_KEYS + PLAN_OPT_KEYS:
+        if k not in msg:
+            continue
         dt, n, b = msg[k]
         plan[k] = np.frombuffer(b, dtype=np.dtype(dt), count=n)
-    for k in PLAN_INTS:
-        plan[k] = msg[k]
+    for k in PLAN_INTS + PLAN_OPT_INTS:
+        if k in msg:
+            plan[k] = msg[k]
     plan["sample_seq"] = np.arange(len(plan["sample_rows"]), dtype=np.int32)
     return plan, (msg["bucket"] or None)
 

@@ -32,10 +32,12 @@ def _ecfg(model="tiny-llama"):
                         max_model_len=512, use_graphs=False)
 
 
-def _rank_main(rank, size, port, ckpt, tag, q, sp_min_tokens=0, model="tiny-llama"):
+def _rank_main(rank, size, port, ckpt, tag, q, sp_min_tokens=0, model="tiny-llama",
+               lookahead="0"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(size), LOCAL_RANK=str(rank),
-                      LMX_SP_MIN_TOKENS=str(sp_min_tokens), LMX_TP_PROBE_STEPS="3")
+                      LMX_SP_MIN_TOKENS=str(sp_min_tokens), LMX_TP_PROBE_STEPS="3",
+                      LMX_LOOKAHEAD=lookahead)
     torch.set_num_threads(2 if size <= 2 else 1)
     import torch.distributed as dist
 
@@ -99,12 +101,14 @@ def test_plan_roundtrip(tmp_path):
     leader.close()
 
 
-@pytest.mark.parametrize("sp_min_tokens", [0, 7])
-def test_tp2_generation_matches_single_process(full_model, sp_min_tokens):
+@pytest.mark.parametrize("sp_min_tokens,lookahead", [(0, "0"), (7, "0"), (0, "1")])
+def test_tp2_generation_matches_single_process(full_model, sp_min_tokens, lookahead):
     """sp_min_tokens=7: every prefill / mixed step of >= 7 tokens runs
     sequence-parallel (reduce-scatter + row-sharded RMSNorm + all-gather),
     odd token counts included (padded rows); pure decode steps stay on the
-    all-reduce path."""
+    all-reduce path.  lookahead=1: the leader launches step n+1 before it
+    reads step n back; every rank samples the all-gathered logits itself
+    (engine.sample_all) and gathers its inputs from its own samples."""
     m, path = full_model
     single = LLMEngine(_ecfg(), device="cpu", model_cfg=m.cfg, weights=m.w)
     ref_sampled = single.generate(PROMPTS[:2], SamplingParams(temperature=0.8, top_p=0.9,
@@ -113,7 +117,9 @@ def test_tp2_generation_matches_single_process(full_model, sp_min_tokens):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port, tag = _free_port(), f"test-{os.getpid()}-{_free_port()}"
-    procs = [ctx.Process(target=_rank_main, args=(r, 2, port, path, tag, q, sp_min_tokens), daemon=True)
+    procs = [ctx.Process(target=_rank_main,
+                         args=(r, 2, port, path, tag, q, sp_min_tokens, "tiny-llama", lookahead),
+                         daemon=True)
              for r in range(2)]
     for p in procs:
         p.start()

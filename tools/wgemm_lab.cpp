@@ -139,14 +139,14 @@ int main(int argc, char** argv) {
   for (char* tok = std::strtok(list, ","); tok; tok = std::strtok(nullptr, ",")) {
     int cfg = 0, S = 1;
     std::sscanf(tok, "%i:%d", &cfg, &S);
-    if ((cfg & 128) && packed_for != (cfg & 31)) {
+    if ((cfg & 128) && packed_for != (cfg & 1055)) {
       for (int c = 0; c < copies; ++c)
         if (lmx::wgemm_pack(Wpk + (long)c * N * K, Wall + (long)c * N * K, N, K, K, cfg, nullptr)) {
           std::printf("  pack failed for cfg %#x\n", cfg);
           break;
         }
       CK(hipDeviceSynchronize());
-      packed_for = cfg & 31;
+      packed_for = cfg & 1055;
     }
     bf16_t* Wsrc = (cfg & 128) ? Wpk : Wall;
     auto launch = [&](int i) {
