@@ -50,6 +50,11 @@ int dgemm_num_configs();
 int rmsnorm_slabs(void*, void*, const float*, int, long, const void*, int, int, long, float,
                   hipStream_t);
 int dgemm_config(int, int*, int*);
+int wgemm(void*, const void*, const void*, float*, unsigned*, int, int, int, int, long, long, long,
+          int, int, int, hipStream_t);
+int wgemm_pack(void*, const void*, int, int, long, int, hipStream_t);
+int wgemm_num_configs();
+int wgemm_config(int, int*, int*);
 long ar_region_bytes(long);
 int ar_alloc(void**, long);
 int ar_free(void*);
@@ -187,6 +192,25 @@ PYBIND11_MODULE(_lmx_kernels, m) {
       int bm = 0, bn = 0;
       lmx::dgemm_config(i, &bm, &bn);
       out.emplace_back(bm, bn);
+    }
+    return out;
+  });
+  // ---- K12 weight-streaming GEMM (wgemm.hip) ----
+  m.def("wgemm", [](uptr C, uptr A, uptr W, uptr slabs, uptr cnt, int n_cnt, int M, int N, int K,
+                    long lda, long ldw, long ldc, int cfg, int splits, int epi, uptr stream) {
+    check(lmx::wgemm(P<void>(C), P<void>(A), P<void>(W), P<float>(slabs), P<unsigned>(cnt), n_cnt,
+                     M, N, K, lda, ldw, ldc, cfg, splits, epi, S(stream)),
+          "wgemm");
+  });
+  m.def("wgemm_pack", [](uptr P_, uptr W, int N, int K, long ldw, int cfg, uptr stream) {
+    check(lmx::wgemm_pack(P<void>(P_), P<void>(W), N, K, ldw, cfg, S(stream)), "wgemm_pack");
+  });
+  m.def("wgemm_configs", []() {
+    std::vector<std::pair<int, int>> out;
+    for (int i = 0; i < lmx::wgemm_num_configs(); ++i) {
+      int bn = 0, bk = 0;
+      lmx::wgemm_config(i, &bn, &bk);
+      out.emplace_back(bn, bk);
     }
     return out;
   });

@@ -505,11 +505,17 @@ int wgemm(void* C, const void* A, const void* W, float* slabs, unsigned* cnt, in
     if (nt) { LMX_WG_E(BN, WM, WN, BK, NX, NW, 1, 1) }                                        \
     LMX_WG_E(BN, WM, WN, BK, NX, NW, 0, 1)
 #else
+  // the library keeps the configurations the measurements left standing
+  // (profiles/r3_decode_gemm_study.md): the 4x1 / 2x2 single-workgroup tiles
+  // and the partials form; packed layouts row-major or K-step-major
 #define LMX_WG_CASE(ID, BN, WM, WN, BK, NX, NW)                                               \
   case ID:                                                                                    \
-    if (probe) return -1;                                                                     \
-    if (nt) { LMX_WG_E(BN, WM, WN, BK, NX, NW, 1, 1) }                                        \
-    LMX_WG_E(BN, WM, WN, BK, NX, NW, 0, 1)
+    if constexpr (ID == 3 || ID == 6 || ID == 8 || ID == 12 || ID == 13) {                    \
+      if (probe || pk == 1) return -1;                                                        \
+      if (nt) { LMX_WG_E(BN, WM, WN, BK, NX, NW, 1, 1) }                                      \
+      LMX_WG_E(BN, WM, WN, BK, NX, NW, 0, 1)                                                  \
+    }                                                                                         \
+    return -1;
 #endif
   switch (cfg) { LMX_WG_CONFIGS(LMX_WG_CASE) }
 #undef LMX_WG_CASE

@@ -848,3 +848,79 @@ def dgemm_partials(a: torch.Tensor, w: torch.Tensor, cfg: int, splits: int) -> P
                    a.stride(0), w.stride(0), N, cfg, splits, 2, _stream())
     DGEMM_CALLS[0] += 1
     return Partials(slabs[:splits * M * N].view(splits, M, N), splits, M, N)
+
+
+# ---------------------------------------------------------------------------
+# K12: weight-streaming GEMM for 129..256-row decode batches (csrc/kernels/wgemm.hip)
+# ---------------------------------------------------------------------------
+# configuration ids the library builds (wgemm.hip LMX_WG_CONFIGS):
+# id -> (BN, BK); 4 waves, one workgroup per CU, all 256 rows per tile
+WGEMM_CONFIGS = {3: (112, 64), 6: (128, 64), 8: (96, 64), 12: (128, 64), 13: (112, 64)}
+WGEMM_NT, WGEMM_PACKED, WGEMM_KMAJOR = 32, 128, 1024
+WGEMM_SWIGLU_BLOCK = 4         # gate/up interleave of the epi-3 form
+_WG_WS: dict = {}
+_WG_CNT = 4096
+
+
+def wgemm_pack(w: torch.Tensor, cfg: int, kmajor: bool = True) -> torch.Tensor:
+    """``w`` [N, K] rearranged into the packed layout of K12 configuration
+    ``cfg`` (every (column tile, K-step) LDS image contiguous; K-steps
+    outermost with ``kmajor``).  Same element count, opaque layout."""
+    _bf16(w, "w")
+    N, K = w.shape
+    bn, bk = WGEMM_CONFIGS[cfg & 31]
+    _chk(N % bn == 0 and K % bk == 0 and w.stride(1) == 1 and w.stride(0) % 8 == 0,
+         f"wgemm_pack shape N={N} K={K} cfg={cfg}")
+    out = torch.empty_like(w, memory_format=torch.contiguous_format)
+    native().wgemm_pack(_ptr(out), _ptr(w), N, K, w.stride(0),
+                        cfg | (WGEMM_KMAJOR if kmajor else 0), _stream())
+    return out
+
+
+def _wg_workspace(dev: torch.device, n_floats: int):
+    key = (dev.index, _stream())
+    ws = _WG_WS.get(key)
+    if ws is None or ws[0].numel() < n_floats:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("wgemm workspace must be allocated before graph capture")
+        n_floats = max(n_floats, ws[0].numel() if ws else 0, 1 << 20)
+        cnt = ws[1] if ws else torch.zeros(_WG_CNT, dtype=torch.int32, device=dev)
+        ws = (torch.empty(n_floats, dtype=torch.float32, device=dev), cnt)
+        _WG_WS[key] = ws
+    return ws
+
+
+def wgemm(a: torch.Tensor, w: torch.Tensor, cfg: int, splits: int = 1, epi: int = 0,
+          packed: int = 0, out: torch.Tensor | None = None):
+    """a @ w^T on K12 for M <= 256 rows.  ``epi``: 0 bf16 [M, N]; 2 fp32
+    partials (``Partials``, summed by ``rms_norm``); 3 SwiGLU over gate/up
+    weights interleaved per 4 rows (``interleave_gate_up(w, 4)``), [M, N/2].
+    ``packed``: 0 row-major ``w``; 1 / 2 ``w`` from ``wgemm_pack`` (tile- /
+    K-step-major)."""
+    M, K = a.shape
+    N = w.shape[0]
+    bn, bk = WGEMM_CONFIGS[cfg & 31]
+    _bf16(a, "a"); _bf16(w, "w")
+    _chk(0 < M <= 256 and N % bn == 0 and K % bk == 0 and K // bk >= splits >= 1,
+         f"wgemm shape M={M} N={N} K={K} cfg={cfg} splits={splits}")
+    _chk(w.shape[1] == K and a.stride(1) == 1 and w.stride(1) == 1 and a.stride(0) % 8 == 0
+         and w.stride(0) % 8 == 0 and a.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0,
+         "wgemm operands need 16-B aligned rows")
+    code = cfg | (WGEMM_PACKED if packed else 0) | (WGEMM_KMAJOR if packed == 2 else 0)
+    slabs = cnt = None
+    if epi == 2:
+        slabs, cnt = _wg_workspace(a.device, splits * M * N)
+        native().wgemm(0, _ptr(a), _ptr(w), _ptr(slabs), _ptr(cnt), _WG_CNT, M, N, K,
+                       a.stride(0), w.stride(0), N, code, splits, 2, _stream())
+        return Partials(slabs[:splits * M * N].view(splits, M, N), splits, M, N)
+    ncols = N // 2 if epi == 3 else N
+    if out is None:
+        out = torch.empty((M, ncols), dtype=a.dtype, device=a.device)
+    _chk(out.shape == (M, ncols) and out.stride(1) == 1 and out.stride(0) % 4 == 0,
+         "wgemm output layout")
+    if splits > 1:
+        _chk(2 * (N // bn) <= _WG_CNT, "wgemm tile count")
+        slabs, cnt = _wg_workspace(a.device, splits * 256 * N)
+    native().wgemm(_ptr(out), _ptr(a), _ptr(w), _ptr(slabs), _ptr(cnt), _WG_CNT, M, N, K,
+                   a.stride(0), w.stride(0), out.stride(0), code, splits, epi, _stream())
+    return out

@@ -621,3 +621,37 @@ def test_dgemm_partials_into_rmsnorm(cfg, splits):
     out = ops.rms_norm(p, g, 1e-5, residual=r2)
     torch.testing.assert_close(r2.float(), r_ref.float(), atol=3e-2, rtol=2e-2)
     torch.testing.assert_close(out.float(), expect.float(), atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", sorted(ops.WGEMM_CONFIGS))
+@pytest.mark.parametrize("M", [129, 200, 256])
+def test_wgemm_vs_fp32(cfg, M):
+    """K12 weight-streaming GEMM (csrc/kernels/wgemm.hip): plain, in-kernel
+    split-K (ticketed write-through combine, re-armed counters), SwiGLU on
+    4-row gate/up blocks (permlane16 pairing), partials for the norm, and
+    both packed weight layouts, against an fp32 PyTorch reference (padded
+    rows past M never stored)."""
+    bn, bk = ops.WGEMM_CONFIGS[cfg]
+    K, N = 2048, bn * 8
+    a = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) * K ** -0.5).to(torch.bfloat16)
+    y = a.float() @ w.float().t()
+    I = N // 2
+    g = torch.nn.functional.silu(y[:, :I]) * y[:, I:]
+    wil = ops.interleave_gate_up(w, ops.WGEMM_SWIGLU_BLOCK)
+    for s in (1, 2, 4):
+        out = ops.wgemm(a, w, cfg, s)
+        torch.testing.assert_close(out.float(), y, atol=2e-2, rtol=2e-2)
+        assert torch.equal(out, ops.wgemm(a, w, cfg, s))      # deterministic, counters re-armed
+        out3 = ops.wgemm(a, wil, cfg, s, epi=3)
+        torch.testing.assert_close(out3.float(), g, atol=2e-2, rtol=2e-2)
+        p = ops.wgemm(a, w, cfg, s, epi=2)
+        torch.testing.assert_close(p.sum(), y, atol=2e-2, rtol=2e-2)
+    for kmajor, code in ((False, 1), (True, 2)):
+        wp = ops.wgemm_pack(w, cfg, kmajor=kmajor)
+        out = ops.wgemm(a, wp, cfg, 2, packed=code)
+        torch.testing.assert_close(out.float(), y, atol=2e-2, rtol=2e-2)
+        wpil = ops.wgemm_pack(wil, cfg, kmajor=kmajor)
+        torch.testing.assert_close(ops.wgemm(a, wpil, cfg, 1, epi=3, packed=code).float(), g,
+                                   atol=2e-2, rtol=2e-2)

@@ -70,6 +70,31 @@ __global__ void stream_kernel(const f32x4_t* p, long n, float* sink) {
   if (acc[0] == 1234.5f) sink[0] = acc[1];
 }
 
+// W-stream probe: one 256-thread workgroup per CU (as K12), each wave streams
+// its own contiguous share with plain 16-B vector loads, R loads in flight per
+// lane (software-pipelined register ring): can register staging beat the
+// LDS-DMA ring's 5.1-5.4 TB/s?
+template <int R>
+__global__ void __launch_bounds__(256, 1) wstream_kernel(const f32x4_t* __restrict__ p, long vecs_per_wave,
+                                                       float* sink) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const f32x4_t* q = p + ((long)blockIdx.x * 4 + wave) * vecs_per_wave + lane;
+  f32x4_t r[R], acc = {0, 0, 0, 0};
+#pragma unroll
+  for (int j = 0; j < R; ++j) r[j] = __builtin_nontemporal_load(q + 64 * j);
+  const long n = vecs_per_wave / 64;
+  for (long i = R; i < n; i += R) {
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      acc += r[j];
+      r[j] = __builtin_nontemporal_load(q + 64 * (i + j));
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < R; ++j) acc += r[j];
+  if (acc[0] == 1234.5f) sink[0] = acc[1];
+}
+
 int main(int argc, char** argv) {
   if (argc < 6) {
     std::fprintf(stderr, "usage: %s N K M epi cfg:splits[,...] [iters]\n", argv[0]);
@@ -133,6 +158,31 @@ int main(int argc, char** argv) {
     CK(hipEventElapsedTime(&ms, e0, e1));
     const double us = ms * 1e3 / iters;
     std::printf("  stream-read W: %.2f us  %.2f TB/s\n", us, wbytes / us / 1e6);
+  }
+
+  {
+    const long vpw = wbytes / 16 / 1024;     // 256 workgroups x 4 waves
+    auto runR = [&](auto kern, int R) {
+      auto run = [&](int i) {
+        kern<<<256, 256>>>((const f32x4_t*)(Wall + (long)(i % copies) * N * K), vpw, sink);
+      };
+      for (int i = 0; i < 3; ++i) run(i);
+      CK(hipEventRecord(e0));
+      for (int i = 0; i < iters; ++i) run(i);
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      const double us = ms * 1e3 / iters;
+      std::printf("  wstream R=%-2d (1 WG/CU, 4 waves): %.2f us  %.2f TB/s\n", R, us,
+                  vpw * 16.0 * 1024 / us / 1e6);
+    };
+    if (std::getenv("LMX_LAB_WSTREAM")) {
+      runR(wstream_kernel<4>, 4);
+      runR(wstream_kernel<8>, 8);
+      runR(wstream_kernel<16>, 16);
+      runR(wstream_kernel<24>, 24);
+    }
   }
 
   char* list = argv[5];
