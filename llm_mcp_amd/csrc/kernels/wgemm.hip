@@ -399,6 +399,338 @@ __global__ void wgemm_pack_kernel(bf16_t* __restrict__ P, const bf16_t* __restri
   }
 }
 
+// ---- K12-RS: register-streamed weights ------------------------------------
+// The LDS-DMA weight ring above tops out at 5.1-5.4 TB/s (44-46 us for the
+// 235 MB gate/up stream), while a plain 16-B vector-load stream from the same
+// one-workgroup-per-CU grid reaches 6.4-6.7 TB/s
+// (profiles/r3_decode_gemm_study.md).  So here the weights never touch LDS:
+// each of the 4 waves owns all 256 rows x BN/4 columns of the tile, loads its
+// W fragments (the MFMA A operand of D = W . X^T) straight into a DW-deep
+// register ring from a packed layout in which every wave-instruction's 1 KB
+// is exactly one fragment, and only the activation panel -- shared by the 4
+// waves, an L2 hit -- is staged through LDS (register-staged, issue early /
+// write late, two slots).  Every load is an ordinary vector load, so the
+// compiler counts the waits; the K loop is unrolled by DW so the register
+// ring is statically indexed.
+template <int BN, int DW, int EPI, int NT>
+__global__ void __launch_bounds__(256, 1)
+wgemm_rs_kernel(bf16_t* __restrict__ C, const bf16_t* __restrict__ A,
+                const bf16_t* __restrict__ Wp, float* __restrict__ slabs,
+                unsigned* __restrict__ cnt, int M, int N, int K, long lda, long ldc, int splits) {
+  constexpr int BM = 256, BK = 64, KK = BK / 32, NWAVE = 4;
+  constexpr int WTN = BN / NWAVE, TN = WTN / 16, TM = BM / 16;
+  constexpr int XI = BM * BK / (NWAVE * 64 * 8);   // 16-B activation loads per lane per K-step
+  constexpr int XSLOT = BM * BK;
+  constexpr int WFR = TN * KK;                     // W fragments per wave per K-step
+  static_assert(WTN % 16 == 0 && DW % 2 == 0 && DW >= 2, "rs geometry");
+  static_assert(EPI != 3 || TM % 2 == 0, "SwiGLU pairs tiles (i, i+1)");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* const xs = reinterpret_cast<bf16_t*>(smem);
+
+  const int tiles_n = N / BN, nwg = tiles_n * splits;
+  const int wg = xcd_remap(blockIdx.x, nwg);
+  const int tile = wg / splits, ks = wg % splits;
+  const int n0 = tile * BN;
+  const int nk_all = K / BK;
+  const int kb = (int)((long)ks * nk_all / splits);
+  const int nk = (int)((long)(ks + 1) * nk_all / splits) - kb;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int fr = lane & 15, fg = lane >> 4;
+  // activation staging: instruction i of wave w covers rows w*64 + 8i .. +8
+  const int xrow = wave * (BM / NWAVE) + (lane >> 3), xc = lane & 7;
+  const bf16_t* xsrc[XI];
+  int xdst[XI];
+#pragma unroll
+  for (int i = 0; i < XI; ++i) {
+    const int r = xrow + 8 * i;
+    xsrc[i] = A + (long)(r < M ? r : M - 1) * lda + 8 * xc;
+    xdst[i] = r * BK + 8 * (xc ^ wg_swz<BK>(r));
+  }
+  // W fragments of (tile, kstep, wave): WFR x 1 KB, lane-linear
+  const bf16_t* wsrc = Wp + (((long)tile * nk_all + kb) * NWAVE + wave) * (WFR * 512) + lane * 8;
+  constexpr long WSTEP = (long)NWAVE * WFR * 512;   // elements per K-step of one tile
+
+  f32x4_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8_t wq[DW][WFR];
+  bf16x8_t xg[XI];
+  auto load_w = [&](bf16x8_t (&dst)[WFR], int t) {
+    const bf16_t* p = wsrc + (long)t * WSTEP;
+#pragma unroll
+    for (int f = 0; f < WFR; ++f) {
+      if constexpr (NT)
+        dst[f] = __builtin_nontemporal_load(reinterpret_cast<const bf16x8_t*>(p + f * 512));
+      else
+        dst[f] = *reinterpret_cast<const bf16x8_t*>(p + f * 512);
+    }
+  };
+  auto load_x = [&](int t) {
+    const long k0 = (long)(kb + t) * BK;
+#pragma unroll
+    for (int i = 0; i < XI; ++i) xg[i] = *reinterpret_cast<const bf16x8_t*>(xsrc[i] + k0);
+  };
+  auto store_x = [&](int slot) {
+    bf16_t* d = xs + slot * XSLOT;
+#pragma unroll
+    for (int i = 0; i < XI; ++i) *reinterpret_cast<bf16x8_t*>(d + xdst[i]) = xg[i];
+  };
+
+  // prologue: activation K-step 0 into slot 0, weights of K-steps 0 .. DW-2
+  load_x(0);
+#pragma unroll
+  for (int u = 0; u < DW - 1; ++u)
+    if (u < nk) load_w(wq[u], u);
+  store_x(0);
+  __syncthreads();
+  for (int t0 = 0; t0 < nk; t0 += DW) {
+#pragma unroll
+    for (int u = 0; u < DW; ++u) {
+      const int t = t0 + u;
+      if (t < nk) {
+        if (t + 1 < nk) load_x(t + 1);            // issued before this step's W load
+        if (t + DW - 1 < nk) load_w(wq[(u + DW - 1) % DW], t + DW - 1);
+        const bf16_t* xt = xs + (u & 1) * XSLOT;
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk) {
+#pragma unroll
+          for (int i = 0; i < TM; ++i) {
+            const bf16x8_t xf = wg_frag<BK>(xt, 16 * i + fr, kk * 4 + fg);
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              acc[i][j] = mfma16(wq[u][j * KK + kk], xf, acc[i][j]);
+          }
+        }
+        if (t + 1 < nk) store_x((u + 1) & 1);
+        __syncthreads();
+      }
+    }
+  }
+
+  // acc[i][j][r] = C[m][n]: m = 16i + fr, n = n0 + wave*WTN + 16j + 4fg + r
+  constexpr int WM = 1, WTM = BM, wr = 0;
+  const int wc = wave;
+  (void)WM;
+  if constexpr (EPI == 2) {
+    float* slab = slabs + (long)ks * M * N;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = wr * WTM + 16 * i + fr;
+      if (m >= M) continue;
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        *reinterpret_cast<f32x4_t*>(slab + (long)m * N + n0 + wc * WTN + 16 * j + 4 * fg) =
+            acc[i][j];
+    }
+    return;
+  } else {
+    if (splits > 1) {
+      unsigned* word = reinterpret_cast<unsigned*>(smem);
+      __syncthreads();
+      if (threadIdx.x == 0)
+        word[0] = __hip_atomic_fetch_add(&cnt[2 * tile], 1u, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      const unsigned order = word[0];
+      float* tslab = slabs + (long)tile * splits * BM * BN;
+      if (order + 1 < (unsigned)splits) {
+        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
+            tslab + (long)ks * BM * BN, 0, BM * BN * (int)sizeof(float), 0x00020000);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int m = wr * WTM + 16 * i + fr;
+          if (m >= M) continue;
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+            __builtin_amdgcn_raw_buffer_store_b128(
+                __builtin_bit_cast(u32x4_t, acc[i][j]), rsrc,
+                (m * BN + wc * WTN + 16 * j + 4 * fg) * (int)sizeof(float), 0, 16);
+          }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0)
+          __hip_atomic_fetch_add(&cnt[2 * tile + 1], 1u, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+        return;
+      }
+      if (threadIdx.x == 0) {
+        while (__hip_atomic_load(&cnt[2 * tile + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+               (unsigned)(splits - 1))
+          __builtin_amdgcn_s_sleep(2);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(&cnt[2 * tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&cnt[2 * tile + 1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        int m = wr * WTM + 16 * i + fr;
+        m = m < M ? m : M - 1;
+        if (ks > 0) {
+          f32x4_t pre[TN];
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            pre[j] = *reinterpret_cast<const f32x4_t*>(tslab + m * BN + wc * WTN + 16 * j + 4 * fg);
+          for (int s2 = 1; s2 < ks; ++s2) {
+            const float* o = tslab + (long)s2 * BM * BN + m * BN + wc * WTN + 4 * fg;
+#pragma unroll
+            for (int j = 0; j < TN; ++j) pre[j] += *reinterpret_cast<const f32x4_t*>(o + 16 * j);
+          }
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = pre[j] + acc[i][j];
+        }
+        for (int s2 = ks + 1; s2 < splits; ++s2) {
+          const float* o = tslab + (long)s2 * BM * BN + m * BN + wc * WTN + 4 * fg;
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] += *reinterpret_cast<const f32x4_t*>(o + 16 * j);
+        }
+      }
+    }
+    if constexpr (EPI == 0) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int m = wr * WTM + 16 * i + fr;
+        if (m >= M) continue;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          bf16x4_t o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = (short)f2bf(acc[i][j][r]);
+          *reinterpret_cast<bf16x4_t*>(C + (long)m * ldc + n0 + wc * WTN + 16 * j + 4 * fg) = o;
+        }
+      }
+    } else {
+      const int sub = fg & 1, set = fg >> 1;
+#pragma unroll
+      for (int i = 0; i < TM; i += 2) {
+        const int m = wr * WTM + 16 * (i + sub) + fr;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          bf16x4_t o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const auto p = __builtin_amdgcn_permlane16_swap(
+                __float_as_uint(acc[i][j][r]), __float_as_uint(acc[i + 1][j][r]), false, false);
+            const float g = __uint_as_float(p[0]), u = __uint_as_float(p[1]);
+            o[r] = (short)f2bf(wg_silu(g) * u);
+          }
+          if (m < M)
+            *reinterpret_cast<bf16x4_t*>(C + (long)m * ldc + ((n0 + wc * WTN + 16 * j) >> 1) +
+                                         4 * set) = o;
+        }
+      }
+    }
+  }
+}
+
+// packed weights of K12-RS (BN columns per tile): for tile, K-step, wave w,
+// fragment f = j*2 + kk, lane l = (fg << 4) | fr:
+//   P[((((tile*nk + kstep)*4 + w)*WFR + f)*64 + l)*8 .. +8] =
+//       W[tile*BN + w*BN/4 + 16j + fr][kstep*64 + 32kk + 8fg .. +8]
+__global__ void wgemm_rs_pack_kernel(bf16_t* __restrict__ P, const bf16_t* __restrict__ W, int N,
+                                     int K, long ldw, int BN) {
+  const int TN = BN / 64, WFR = TN * 2, nk = K / 64;
+  const long chunks = (long)N * K / 8;
+  for (long c = blockIdx.x * (long)blockDim.x + threadIdx.x; c < chunks;
+       c += (long)gridDim.x * blockDim.x) {
+    const int l = (int)(c & 63);
+    long q = c >> 6;
+    const int f = (int)(q % WFR);
+    q /= WFR;
+    const int w = (int)(q & 3);
+    q >>= 2;
+    const int kstep = (int)(q % nk), tile = (int)(q / nk);
+    const int j = f >> 1, kk = f & 1, fr = l & 15, fg = l >> 4;
+    const long row = (long)tile * BN + w * (BN / 4) + 16 * j + fr;
+    const long col = (long)kstep * 64 + 32 * kk + 8 * fg;
+    *reinterpret_cast<u16x8*>(P + c * 8) = *reinterpret_cast<const u16x8*>(W + row * ldw + col);
+  }
+}
+
+struct WgRsCfg { int bn, dw; };
+static const WgRsCfg kWgRsCfgs[] = {{128, 6}, {128, 4}, {128, 8}, {64, 6}, {64, 8}, {128, 2}};
+constexpr int kNumWgRsCfgs = sizeof(kWgRsCfgs) / sizeof(kWgRsCfgs[0]);
+
+int wgemm_rs_config(int cfg, int* bn) {
+  if (cfg < 0 || cfg >= kNumWgRsCfgs) return -1;
+  *bn = kWgRsCfgs[cfg].bn;
+  return 0;
+}
+
+template <int BN, int DW, int EPI, int NT>
+static int wg_rs_launch(bf16_t* C, const bf16_t* A, const bf16_t* Wp, float* slabs, unsigned* cnt,
+                        int M, int N, int K, long lda, long ldc, int splits, hipStream_t stream) {
+  constexpr size_t smem = 2 * 256 * 64 * sizeof(bf16_t);
+  auto kern = wgemm_rs_kernel<BN, DW, EPI, NT>;
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e = hipFuncSetAttribute((const void*)kern,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    if (e != hipSuccess) return (int)e;
+    attr = true;
+  }
+  kern<<<dim3((N / BN) * splits), dim3(256), smem, stream>>>(C, A, Wp, slabs, cnt, M, N, K, lda,
+                                                            ldc, splits);
+  return (int)hipGetLastError();
+}
+
+// cfg: K12-RS configuration (kWgRsCfgs) | 32 for non-temporal weight loads;
+// Wp in the wgemm_rs_pack layout of the configuration's BN
+int wgemm_rs(void* C, const void* A, const void* Wp, float* slabs, unsigned* cnt, int n_cnt, int M,
+             int N, int K, long lda, long ldc, int cfg, int splits, int epi, hipStream_t stream) {
+  if (M <= 0) return 0;
+  const int nt = (cfg >> 5) & 1;
+  cfg &= 31;
+  if (cfg >= kNumWgRsCfgs || splits < 1 || M > 256) return -1;
+  const WgRsCfg c = kWgRsCfgs[cfg];
+  if (N % c.bn != 0 || K % 64 != 0 || K / 64 < splits) return -1;
+  if (epi != 0 && epi != 2 && epi != 3) return -1;
+  if ((epi == 2 || splits > 1) && slabs == nullptr) return -2;
+  if (epi != 2 && splits > 1 && (cnt == nullptr || 2 * (N / c.bn) > n_cnt)) return -3;
+  auto C_ = (bf16_t*)C;
+  auto A_ = (const bf16_t*)A;
+  auto W_ = (const bf16_t*)Wp;
+#define LMX_WGRS_E(BN, DW, NT)                                                                   \
+  if (epi == 3) return wg_rs_launch<BN, DW, 3, NT>(C_, A_, W_, slabs, cnt, M, N, K, lda, ldc,      \
+                                                   splits, stream);                              \
+  if (epi == 2) return wg_rs_launch<BN, DW, 2, NT>(C_, A_, W_, slabs, cnt, M, N, K, lda, ldc,      \
+                                                   splits, stream);                              \
+  return wg_rs_launch<BN, DW, 0, NT>(C_, A_, W_, slabs, cnt, M, N, K, lda, ldc, splits, stream);
+#define LMX_WGRS_CASE(ID, BN, DW)                                                                \
+  case ID:                                                                                       \
+    if (nt) { LMX_WGRS_E(BN, DW, 1) }                                                            \
+    LMX_WGRS_E(BN, DW, 0)
+  switch (cfg) {
+    LMX_WGRS_CASE(0, 128, 6)
+    LMX_WGRS_CASE(1, 128, 4)
+    LMX_WGRS_CASE(2, 128, 8)
+    LMX_WGRS_CASE(3, 64, 6)
+    LMX_WGRS_CASE(4, 64, 8)
+    LMX_WGRS_CASE(5, 128, 2)
+  }
+#undef LMX_WGRS_CASE
+#undef LMX_WGRS_E
+  return -1;
+}
+
+int wgemm_rs_pack(void* P, const void* W, int N, int K, long ldw, int cfg, hipStream_t stream) {
+  cfg &= 31;
+  if (cfg >= kNumWgRsCfgs) return -1;
+  const int bn = kWgRsCfgs[cfg].bn;
+  if (N % bn != 0 || K % 64 != 0 || ldw % 8 != 0) return -1;
+  const long chunks = (long)N * K / 8;
+  const int grid = (int)std::min<long>(8192, (chunks + 255) / 256);
+  wgemm_rs_pack_kernel<<<grid, 256, 0, stream>>>((bf16_t*)P, (const bf16_t*)W, N, K, ldw, bn);
+  return (int)hipGetLastError();
+}
+
 // ---- launcher ---------------------------------------------------------------
 // cfg ids (BN, WM, WN, BK, NX, NW); kept in sync with ops.WGEMM_CONFIGS
 struct WgCfg { int bn, wm, wn, bk, nx, nw; };

@@ -189,7 +189,17 @@ int main(int argc, char** argv) {
   for (char* tok = std::strtok(list, ","); tok; tok = std::strtok(nullptr, ",")) {
     int cfg = 0, S = 1;
     std::sscanf(tok, "%i:%d", &cfg, &S);
-    if ((cfg & 128) && packed_for != (cfg & 1055)) {
+    if ((cfg & 0x800) && packed_for != (cfg & 0x81f)) {
+      for (int c = 0; c < copies; ++c)
+        if (lmx::wgemm_rs_pack(Wpk + (long)c * N * K, Wall + (long)c * N * K, N, K, K, cfg & 31,
+                               nullptr)) {
+          std::printf("  rs pack failed for cfg %#x\n", cfg);
+          break;
+        }
+      CK(hipDeviceSynchronize());
+      packed_for = cfg & 0x81f;
+    }
+    if (!(cfg & 0x800) && (cfg & 128) && packed_for != (cfg & 1055)) {
       for (int c = 0; c < copies; ++c)
         if (lmx::wgemm_pack(Wpk + (long)c * N * K, Wall + (long)c * N * K, N, K, K, cfg, nullptr)) {
           std::printf("  pack failed for cfg %#x\n", cfg);
@@ -198,8 +208,11 @@ int main(int argc, char** argv) {
       CK(hipDeviceSynchronize());
       packed_for = cfg & 1055;
     }
-    bf16_t* Wsrc = (cfg & 128) ? Wpk : Wall;
+    bf16_t* Wsrc = (cfg & (128 | 0x800)) ? Wpk : Wall;
     auto launch = [&](int i) {
+      if (cfg & 0x800)
+        return lmx::wgemm_rs(C, A, Wsrc + (long)(i % copies) * N * K, slabs, cnt, 65536, M, N, K,
+                             K, ncol, cfg & 63, S, epi, nullptr);
       return lmx::wgemm(C, A, Wsrc + (long)(i % copies) * N * K, slabs, cnt, 65536, M, N, K, K, K,
                         ncol, cfg, S, epi, nullptr);
     };
@@ -210,7 +223,7 @@ int main(int argc, char** argv) {
     }
     CK(hipDeviceSynchronize());
     double maxerr = 0, maxref = 0;
-    if (!(cfg & 64)) {
+    if (!(cfg & 64) || (cfg & 0x800)) {
       if (epi == 2) {
         slab_sum_kernel<<<(int)(((long)M * N + 255) / 256), 256>>>(C, slabs, S, M, N);
         CK(hipDeviceSynchronize());
