@@ -412,13 +412,15 @@ __global__ void wgemm_pack_kernel(bf16_t* __restrict__ P, const bf16_t* __restri
 // write late, two slots).  Every load is an ordinary vector load, so the
 // compiler counts the waits; the K loop is unrolled by DW so the register
 // ring is statically indexed.
-template <int BN, int DW, int EPI, int NT>
+template <int BN, int DW, int EPI, int NT, int WMR>
 __global__ void __launch_bounds__(256, 1)
 wgemm_rs_kernel(bf16_t* __restrict__ C, const bf16_t* __restrict__ A,
                 const bf16_t* __restrict__ Wp, float* __restrict__ slabs,
                 unsigned* __restrict__ cnt, int M, int N, int K, long lda, long ldc, int splits) {
-  constexpr int BM = 256, BK = 64, KK = BK / 32, NWAVE = 4;
-  constexpr int WTN = BN / NWAVE, TN = WTN / 16, TM = BM / 16;
+  // WMR waves along M share each W fragment (loaded by each of them: the
+  // second request of a line hits the CU's L1), 4 / WMR along N
+  constexpr int BM = 256, BK = 64, KK = BK / 32, NWAVE = 4, WNR = NWAVE / WMR;
+  constexpr int WTM = BM / WMR, WTN = BN / WNR, TN = WTN / 16, TM = WTM / 16;
   constexpr int XI = BM * BK / (NWAVE * 64 * 8);   // 16-B activation loads per lane per K-step
   constexpr int XSLOT = BM * BK;
   constexpr int WFR = TN * KK;                     // W fragments per wave per K-step
@@ -447,9 +449,10 @@ wgemm_rs_kernel(bf16_t* __restrict__ C, const bf16_t* __restrict__ A,
     xsrc[i] = A + (long)(r < M ? r : M - 1) * lda + 8 * xc;
     xdst[i] = r * BK + 8 * (xc ^ wg_swz<BK>(r));
   }
-  // W fragments of (tile, kstep, wave): WFR x 1 KB, lane-linear
-  const bf16_t* wsrc = Wp + (((long)tile * nk_all + kb) * NWAVE + wave) * (WFR * 512) + lane * 8;
-  constexpr long WSTEP = (long)NWAVE * WFR * 512;   // elements per K-step of one tile
+  const int wr = wave % WMR, wc = wave / WMR;
+  // W fragments of (tile, kstep, wave column): WFR x 1 KB, lane-linear
+  const bf16_t* wsrc = Wp + (((long)tile * nk_all + kb) * WNR + wc) * (WFR * 512) + lane * 8;
+  constexpr long WSTEP = (long)WNR * WFR * 512;     // elements per K-step of one tile
 
   f32x4_t acc[TM][TN];
 #pragma unroll
@@ -499,7 +502,7 @@ wgemm_rs_kernel(bf16_t* __restrict__ C, const bf16_t* __restrict__ A,
         for (int kk = 0; kk < KK; ++kk) {
 #pragma unroll
           for (int i = 0; i < TM; ++i) {
-            const bf16x8_t xf = wg_frag<BK>(xt, 16 * i + fr, kk * 4 + fg);
+            const bf16x8_t xf = wg_frag<BK>(xt, wr * WTM + 16 * i + fr, kk * 4 + fg);
 #pragma unroll
             for (int j = 0; j < TN; ++j)
               acc[i][j] = mfma16(wq[u][j * KK + kk], xf, acc[i][j]);
@@ -511,10 +514,7 @@ wgemm_rs_kernel(bf16_t* __restrict__ C, const bf16_t* __restrict__ A,
     }
   }
 
-  // acc[i][j][r] = C[m][n]: m = 16i + fr, n = n0 + wave*WTN + 16j + 4fg + r
-  constexpr int WM = 1, WTM = BM, wr = 0;
-  const int wc = wave;
-  (void)WM;
+  // acc[i][j][r] = C[m][n]: m = wr*WTM + 16i + fr, n = n0 + wc*WTN + 16j + 4fg + r
   if constexpr (EPI == 2) {
     float* slab = slabs + (long)ks * M * N;
 #pragma unroll
@@ -635,8 +635,8 @@ wgemm_rs_kernel(bf16_t* __restrict__ C, const bf16_t* __restrict__ A,
 //   P[((((tile*nk + kstep)*4 + w)*WFR + f)*64 + l)*8 .. +8] =
 //       W[tile*BN + w*BN/4 + 16j + fr][kstep*64 + 32kk + 8fg .. +8]
 __global__ void wgemm_rs_pack_kernel(bf16_t* __restrict__ P, const bf16_t* __restrict__ W, int N,
-                                     int K, long ldw, int BN) {
-  const int TN = BN / 64, WFR = TN * 2, nk = K / 64;
+                                     int K, long ldw, int BN, int WNR) {
+  const int TN = BN / WNR / 16, WFR = TN * 2, nk = K / 64;
   const long chunks = (long)N * K / 8;
   for (long c = blockIdx.x * (long)blockDim.x + threadIdx.x; c < chunks;
        c += (long)gridDim.x * blockDim.x) {
@@ -644,18 +644,20 @@ __global__ void wgemm_rs_pack_kernel(bf16_t* __restrict__ P, const bf16_t* __res
     long q = c >> 6;
     const int f = (int)(q % WFR);
     q /= WFR;
-    const int w = (int)(q & 3);
-    q >>= 2;
+    const int w = (int)(q % WNR);
+    q /= WNR;
     const int kstep = (int)(q % nk), tile = (int)(q / nk);
     const int j = f >> 1, kk = f & 1, fr = l & 15, fg = l >> 4;
-    const long row = (long)tile * BN + w * (BN / 4) + 16 * j + fr;
+    const long row = (long)tile * BN + w * (BN / WNR) + 16 * j + fr;
     const long col = (long)kstep * 64 + 32 * kk + 8 * fg;
     *reinterpret_cast<u16x8*>(P + c * 8) = *reinterpret_cast<const u16x8*>(W + row * ldw + col);
   }
 }
 
-struct WgRsCfg { int bn, dw; };
-static const WgRsCfg kWgRsCfgs[] = {{128, 6}, {128, 4}, {128, 8}, {64, 6}, {64, 8}, {128, 2}};
+struct WgRsCfg { int bn, dw, wmr; };
+static const WgRsCfg kWgRsCfgs[] = {{128, 6, 1}, {128, 4, 1}, {128, 8, 1}, {64, 6, 1},
+                                    {64, 8, 1},  {128, 2, 1}, {128, 6, 2}, {128, 8, 2},
+                                    {112, 2, 4}, {112, 4, 4}, {224, 2, 2}, {128, 4, 2}};
 constexpr int kNumWgRsCfgs = sizeof(kWgRsCfgs) / sizeof(kWgRsCfgs[0]);
 
 int wgemm_rs_config(int cfg, int* bn) {
@@ -664,11 +666,11 @@ int wgemm_rs_config(int cfg, int* bn) {
   return 0;
 }
 
-template <int BN, int DW, int EPI, int NT>
+template <int BN, int DW, int EPI, int NT, int WMR>
 static int wg_rs_launch(bf16_t* C, const bf16_t* A, const bf16_t* Wp, float* slabs, unsigned* cnt,
                         int M, int N, int K, long lda, long ldc, int splits, hipStream_t stream) {
   constexpr size_t smem = 2 * 256 * 64 * sizeof(bf16_t);
-  auto kern = wgemm_rs_kernel<BN, DW, EPI, NT>;
+  auto kern = wgemm_rs_kernel<BN, DW, EPI, NT, WMR>;
   static bool attr = false;
   if (!attr) {
     const hipError_t e = hipFuncSetAttribute((const void*)kern,
@@ -697,23 +699,30 @@ int wgemm_rs(void* C, const void* A, const void* Wp, float* slabs, unsigned* cnt
   auto C_ = (bf16_t*)C;
   auto A_ = (const bf16_t*)A;
   auto W_ = (const bf16_t*)Wp;
-#define LMX_WGRS_E(BN, DW, NT)                                                                   \
-  if (epi == 3) return wg_rs_launch<BN, DW, 3, NT>(C_, A_, W_, slabs, cnt, M, N, K, lda, ldc,      \
-                                                   splits, stream);                              \
-  if (epi == 2) return wg_rs_launch<BN, DW, 2, NT>(C_, A_, W_, slabs, cnt, M, N, K, lda, ldc,      \
-                                                   splits, stream);                              \
-  return wg_rs_launch<BN, DW, 0, NT>(C_, A_, W_, slabs, cnt, M, N, K, lda, ldc, splits, stream);
-#define LMX_WGRS_CASE(ID, BN, DW)                                                                \
+#define LMX_WGRS_E(BN, DW, NT, WMR)                                                              \
+  if (epi == 3) return wg_rs_launch<BN, DW, 3, NT, WMR>(C_, A_, W_, slabs, cnt, M, N, K, lda, ldc, \
+                                                        splits, stream);                         \
+  if (epi == 2) return wg_rs_launch<BN, DW, 2, NT, WMR>(C_, A_, W_, slabs, cnt, M, N, K, lda, ldc, \
+                                                        splits, stream);                         \
+  return wg_rs_launch<BN, DW, 0, NT, WMR>(C_, A_, W_, slabs, cnt, M, N, K, lda, ldc, splits,       \
+                                          stream);
+#define LMX_WGRS_CASE(ID, BN, DW, WMR)                                                           \
   case ID:                                                                                       \
-    if (nt) { LMX_WGRS_E(BN, DW, 1) }                                                            \
-    LMX_WGRS_E(BN, DW, 0)
+    if (nt) { LMX_WGRS_E(BN, DW, 1, WMR) }                                                       \
+    LMX_WGRS_E(BN, DW, 0, WMR)
   switch (cfg) {
-    LMX_WGRS_CASE(0, 128, 6)
-    LMX_WGRS_CASE(1, 128, 4)
-    LMX_WGRS_CASE(2, 128, 8)
-    LMX_WGRS_CASE(3, 64, 6)
-    LMX_WGRS_CASE(4, 64, 8)
-    LMX_WGRS_CASE(5, 128, 2)
+    LMX_WGRS_CASE(0, 128, 6, 1)
+    LMX_WGRS_CASE(1, 128, 4, 1)
+    LMX_WGRS_CASE(2, 128, 8, 1)
+    LMX_WGRS_CASE(3, 64, 6, 1)
+    LMX_WGRS_CASE(4, 64, 8, 1)
+    LMX_WGRS_CASE(5, 128, 2, 1)
+    LMX_WGRS_CASE(6, 128, 6, 2)
+    LMX_WGRS_CASE(7, 128, 8, 2)
+    LMX_WGRS_CASE(8, 112, 2, 4)
+    LMX_WGRS_CASE(9, 112, 4, 4)
+    LMX_WGRS_CASE(10, 224, 2, 2)
+    LMX_WGRS_CASE(11, 128, 4, 2)
   }
 #undef LMX_WGRS_CASE
 #undef LMX_WGRS_E
@@ -723,11 +732,12 @@ int wgemm_rs(void* C, const void* A, const void* Wp, float* slabs, unsigned* cnt
 int wgemm_rs_pack(void* P, const void* W, int N, int K, long ldw, int cfg, hipStream_t stream) {
   cfg &= 31;
   if (cfg >= kNumWgRsCfgs) return -1;
-  const int bn = kWgRsCfgs[cfg].bn;
+  const int bn = kWgRsCfgs[cfg].bn, wnr = 4 / kWgRsCfgs[cfg].wmr;
   if (N % bn != 0 || K % 64 != 0 || ldw % 8 != 0) return -1;
   const long chunks = (long)N * K / 8;
   const int grid = (int)std::min<long>(8192, (chunks + 255) / 256);
-  wgemm_rs_pack_kernel<<<grid, 256, 0, stream>>>((bf16_t*)P, (const bf16_t*)W, N, K, ldw, bn);
+  wgemm_rs_pack_kernel<<<grid, 256, 0, stream>>>((bf16_t*)P, (const bf16_t*)W, N, K, ldw, bn,
+                                                 wnr);
   return (int)hipGetLastError();
 }
 
