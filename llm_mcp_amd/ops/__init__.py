@@ -895,8 +895,8 @@ def wgemm(a: torch.Tensor, w: torch.Tensor, cfg: int, splits: int = 1, epi: int 
     """a @ w^T on K12 for M <= 256 rows.  ``epi``: 0 bf16 [M, N]; 2 fp32
     partials (``Partials``, summed by ``rms_norm``); 3 SwiGLU over gate/up
     weights interleaved per 4 rows (``interleave_gate_up(w, 4)``), [M, N/2].
-    ``packed``: 0 row-major ``w``; 1 / 2 ``w`` from ``wgemm_pack`` (tile- /
-    K-step-major)."""
+    ``packed``: 0 row-major ``w``; 2 ``w`` from ``wgemm_pack`` (K-step-major;
+    the tile-major layout 1 is a lab-only build)."""
     M, K = a.shape
     N = w.shape[0]
     bn, bk = WGEMM_CONFIGS[cfg & 31]
