@@ -314,7 +314,11 @@ class LLMEngine:
         self.tp.logits_to_all = self.sample_all
         self._la = None                    # the launched step not yet read back
         self._penalized: set[int] = set()  # active requests with penalty windows
-        if ecfg.use_graphs and self.device.type == "cuda" and not ops.debug_sync():
+        # a gloo TP group (one-GPU rehearsals, CPU-hosted collectives) cannot be
+        # captured: its host-staged collectives synchronise inside the step
+        host_tp = self.tp.size > 1 and self.tp.group is not None and \
+            torch.distributed.get_backend(self.tp.group) == "gloo"
+        if ecfg.use_graphs and self.device.type == "cuda" and not ops.debug_sync() and not host_tp:
             self._capture_graphs()
         self._bucket_list = sorted(self.graphs)
 

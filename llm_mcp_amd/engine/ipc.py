@@ -200,10 +200,14 @@ class EngineServer:
         if e is None:
             return {"stats": dict(self.embed_engine.stats) if self.embed_engine else {}}
         s = e.sched
+
+        def skeys(d):
+            # msgpack peers unpack with strict_map_key: message-size keys as str
+            return {str(k): skeys(v) if isinstance(v, dict) else v for k, v in d.items()}
         return {"running": s.num_running, "waiting": s.num_waiting, "kv_usage": s.kv_usage,
                 "kv_free_blocks": s.kv_free_blocks, "stats": dict(e.stats),
-                "tp_comm": getattr(e, "tp_comm", {}),
-                "tp_comm_live": getattr(e, "tp_comm_live", {})}
+                "tp_comm": skeys(getattr(e, "tp_comm", {}) or {}),
+                "tp_comm_live": skeys(getattr(e, "tp_comm_live", {}) or {})}
 
     # engine thread: one message per connection per step
     def _sink(self, evs: list[TokenEvent]):

@@ -109,3 +109,24 @@ def test_embedding_response_rows_are_exact_float32():
     row = json.loads(runtime().f32_json_rows(np.asarray([[1.5, np.nan, -np.inf, 0.0]],
                                                         np.float32))[0])
     assert row == [1.5, None, None, 0.0]
+
+
+def test_engine_info_survives_strict_msgpack_with_tp_probe_sizes():
+    """A TP leader's start-up all-reduce probe is keyed by message size
+    (ints): the engine socket's peer unpacks with msgpack's strict_map_key,
+    so the info reply must carry those keys as strings (a GPU TP group's
+    info request used to drop the connection)."""
+    import types
+
+    import msgpack
+
+    from llm_mcp_amd.engine.ipc import EngineServer
+    sched = types.SimpleNamespace(num_running=1, num_waiting=0, kv_usage=0.5, kv_free_blocks=7)
+    eng = types.SimpleNamespace(sched=sched, stats={"steps": 3},
+                                tp_comm={"rccl": {16384: 21.5, 1048576: 80.0}, "peer": {16384: 9.1}},
+                                tp_comm_live={"seq": 2, "bytes": 1 << 20, "us": {"rccl": 75.0}})
+    srv = EngineServer.__new__(EngineServer)
+    srv.engine = eng
+    info = srv.engine_info()
+    back = msgpack.unpackb(msgpack.packb(info), raw=False)
+    assert back["tp_comm"]["rccl"]["16384"] == 21.5 and back["tp_comm_live"]["us"]["rccl"] == 75.0

@@ -83,6 +83,19 @@ for step in "$@"; do
       run config5 900 python -u -m llm_mcp_amd.bench.serving_bench mixed --gpus 0 \
           --replicas-per-gpu 2 --fault gpu_error:0.002 --fault-device gpu0.r1 \
           --jobs 1024 --concurrency 256 --sync-every 4 --max-tokens 64 --chars 512 || exit $? ;;
+    config5det)
+      # config 5 with a FIXED fault schedule (the faulty worker fails at its
+      # 300th engine step, every life) and the median of 3 runs
+      run config5det 1100 python -u -m llm_mcp_amd.bench.serving_bench mixed --gpus 0 \
+          --replicas-per-gpu 2 --fault gpu_error@300 --fault-device gpu0.r1 --runs 3 \
+          --jobs 1024 --concurrency 256 --sync-every 4 --max-tokens 64 --chars 512 || exit $? ;;
+    tp_rehearse)
+      # BASELINE config 4's launcher on one GPU: bench.py --tp 2 with the 70B
+      # layer shapes cut to 8 layers (a plumbing rehearsal, never an N-GPU number)
+      run tp_rehearse 480 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+          --master-addr 127.0.0.1 --master-port 29613 bench.py --gpus 2 --tp 2 \
+          --rehearse-on-one-gpu --model llama-3-70b@L8 --concurrency 64 --max-tokens 128 \
+          --steps 2 --warmup 1 || exit $? ;;
     encoder_bench)
       run encoder_bench 600 python -u -m llm_mcp_amd.bench.dgemm_bench --encoder 4096,32768 || exit $? ;;
     prof_bench)
