@@ -6,16 +6,20 @@ runs in-process on the GPU:
 
   embed_gather(word) + token_type row -> LayerNorm
   per layer (post-norm BERT with rotary and SwiGLU):
-      QKV = gemm_nt (K7, hand-written MFMA GEMM)            [T, 3d]
+      QKV = x . Wqkv^T                                      [T, 3d]
       rope + scatter K/V into a per-batch paged scratch cache (K2/K5)
       bidirectional varlen attention on the paged kernel (K3, causal=0)
-      h = LayerNorm(x + gemm_nt(attn, Wo))                  (fused residual LN)
-      g = silu_mul(gemm_nt(h, [fc12; fc11]))                (K8)
-      x = LayerNorm(h + gemm_nt(g, fc2))
+      h = LayerNorm(x + attn . Wo^T)                        (fused residual LN)
+      g = silu(h . Wgate^T) * (h . Wup^T)                   (SwiGLU in the GEMM epilogue)
+      x = LayerNorm(h + g . Wfc2^T)
   masked mean pool + Matryoshka truncation + L2 normalise (K9)
 
-All projections run on the hand-written gfx950 GEMM (``ops.gemm_nt``); the
-sequences of a batch are packed (cu_seqlens), never padded.
+Each projection runs on the backend ``ops.encoder_backend`` picks for its
+(N, K) from the measured encoder table (config/dgemm_gfx950.json
+"encoder", bench/dgemm_bench.py --encoder): the hand-written large-M GEMM
+where it was measured fastest, else hipBLASLt; the gate/up projection runs
+hand-written with the fused SwiGLU epilogue.  The sequences of a batch are
+packed (cu_seqlens), never padded.
 """
 from __future__ import annotations
 

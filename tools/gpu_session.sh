@@ -85,10 +85,12 @@ for step in "$@"; do
           --jobs 1024 --concurrency 256 --sync-every 4 --max-tokens 64 --chars 512 || exit $? ;;
     config5det)
       # config 5 with a FIXED fault schedule (the faulty worker fails at its
-      # 300th engine step, every life) and the median of 3 runs
+      # 300th engine step, every life) and the median of 3 runs; 4096 jobs per
+      # run so each run spans several fault/restart cycles (1024-job runs: one
+      # fault per ~10 s run, 84-112 jobs/s spread from where it lands)
       run config5det 1100 python -u -m llm_mcp_amd.bench.serving_bench mixed --gpus 0 \
           --replicas-per-gpu 2 --fault gpu_error@300 --fault-device gpu0.r1 --runs 3 \
-          --jobs 1024 --concurrency 256 --sync-every 4 --max-tokens 64 --chars 512 || exit $? ;;
+          --jobs 4096 --concurrency 256 --sync-every 4 --max-tokens 64 --chars 512 || exit $? ;;
     tp_rehearse)
       # BASELINE config 4's launcher on one GPU: bench.py --tp 2 with the 70B
       # layer shapes cut to 8 layers (a plumbing rehearsal, never an N-GPU number)
