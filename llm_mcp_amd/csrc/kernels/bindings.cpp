@@ -53,6 +53,8 @@ int dgemm_config(int, int*, int*);
 int wgemm(void*, const void*, const void*, float*, unsigned*, int, int, int, int, long, long, long,
           int, int, int, hipStream_t);
 int wgemm_pack(void*, const void*, int, int, long, int, hipStream_t);
+int pgemm(void*, const void*, const void*, const void*, int, int, int, long, long, long, int, int,
+          hipStream_t);
 int wgemm_num_configs();
 int wgemm_config(int, int*, int*);
 long ar_region_bytes(long);
@@ -201,6 +203,13 @@ PYBIND11_MODULE(_lmx_kernels, m) {
     check(lmx::wgemm(P<void>(C), P<void>(A), P<void>(W), P<float>(slabs), P<unsigned>(cnt), n_cnt,
                      M, N, K, lda, ldw, ldc, cfg, splits, epi, S(stream)),
           "wgemm");
+  });
+  // ---- K13 large-M GEMM (pgemm.hip) ----
+  m.def("pgemm", [](uptr C, uptr A, uptr W, uptr bias, int M, int N, int K, long lda, long ldw,
+                    long ldc, int act, int grid, uptr stream) {
+    check(lmx::pgemm(P<void>(C), P<void>(A), P<void>(W), P<void>(bias), M, N, K, lda, ldw, ldc,
+                     act, grid, S(stream)),
+          "pgemm");
   });
   m.def("wgemm_pack", [](uptr P_, uptr W, int N, int K, long ldw, int cfg, uptr stream) {
     check(lmx::wgemm_pack(P<void>(P_), P<void>(W), N, K, ldw, cfg, S(stream)), "wgemm_pack");

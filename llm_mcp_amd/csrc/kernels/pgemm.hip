@@ -1,0 +1,513 @@
+// K13: large-M projection GEMM (prefill chunks, embedding-model batches):
+//     C[M, N] = epi(A[M, K] . W[N, K]^T)     bf16 in, fp32 accumulate, bf16 out
+// epi: optional bias (staged in LDS), then none / GELU(tanh) / SiLU / GELU(erf),
+// or SwiGLU over 16-row gate/up pairs (W from ops.interleave_gate_up(w, 16);
+// C then has N/2 columns).
+//
+// The structure is chosen for one 512-thread workgroup per CU holding a
+// 256 x 256 output tile (cdna guide §5 "the 256² 8-phase template", MI355X
+// microarch guide §LDS / MFMA):
+//   * persistent: gridDim = min(tiles, CUs); a workgroup walks its tiles
+//     (linear id i * grid + xcd_remap(block), grouped 8 M-tiles x N so one XCD's
+//     32 concurrent tiles share 8 A panels and 4 W panels in its L2) and the
+//     k-steps of consecutive tiles form ONE load stream: the next tile's first
+//     K-steps are already in LDS when the current tile's last MFMA retires, so
+//     there is no per-tile prologue bubble (what a fresh workgroup per tile
+//     pays: the short-K encoder shapes, K = 768-1024, run 12-16 K-steps a tile);
+//   * 8 waves: 2 (M) x 4 (N), wave tile 128 x 64 = 2 x 2 quadrants of 64 x 32
+//     (16x16x32 bf16 MFMA, operands swapped so each lane's 4 accumulators are
+//     4 consecutive output columns); one K-step (64 deep) is 4 phases, one
+//     quadrant (16 MFMAs) per phase in the order (0,0) (0,1) (1,1) (1,0);
+//   * ping-pong: waves 4-7 run one barrier behind waves 0-3, so on every SIMD
+//     one wave issues its 16 MFMAs while the other reads its next fragments
+//     and issues its LDS-DMA (two barriers per phase, s_setprio(1) around the
+//     MFMA cluster);
+//   * LDS: two K-step stages of four 16-KB half-tile images (A rows of M-half
+//     0/1 of every wave, W columns of N-half 0/1 of every wave) filled by
+//     buffer_load ... lds (16 B per lane, XOR-swizzled on the global source
+//     chunk, undone on the ds_read_b128), ONE half-tile per phase, two K-steps
+//     ahead; a half is refilled in the phase after its last ds_read, so every
+//     DMA has 4-5 phases (~2k cycles) to land and each phase ends in a
+//     counted vmcnt (10, or 8 before a K-step's first phase) -- never 0 in the
+//     loop;
+//   * fragments: A M-half 1 and W N-half 0 of K-step s are read in phases 0-1
+//     of s, A M-half 0 and W N-half 1 of K-step s+1 in phases 2-3 of s (their
+//     registers are free by then): 8 / 4 / 4 / 8 ds_read_b128 per phase;
+//   * epilogue: the previous tile's quadrant q is converted and stored (raw
+//     buffer stores: rows >= M fall outside the buffer and are dropped, so the
+//     instruction count per wave is fixed) in the read half of phase q of the
+//     next tile's first K-step, just before that quadrant's first MFMA
+//     (zero accumulator input); the stores sit in the vmcnt window of the
+//     next 8 phases and the counted waits include them.
+//
+// Requirements (checked by the launcher): N % 256 == 0, K % 64 == 0, K >= 192,
+// lda / ldw / ldc multiples of 8 elements, 16-B aligned operands; bias (if
+// any) N <= 8192.
+#include "common.h"
+
+namespace lmx {
+namespace {
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+
+constexpr int PG_THREADS = 512;
+constexpr int PG_HALF_B = 128 * 64 * 2;       // one half-tile image: 128 rows x 64 bf16
+constexpr int PG_STAGE_B = 4 * PG_HALF_B;     // A0 A1 W0 W1
+constexpr int PG_RING_B = 2 * PG_STAGE_B;     // 128 KB
+constexpr int PG_MAX_BIAS = 8192;
+constexpr int PG_GROUP_M = 8;                 // M-tiles per tile group (L2 reuse)
+constexpr int HA0 = 0, HA1 = 1, HW0 = 2, HW1 = 3;
+
+// step modes: plain K-step / first K-step of a tile after another tile (stores
+// the previous tile's quadrants) / the two K-steps after that (their vmcnt
+// windows still hold some of those stores) / first K-step of the first tile
+constexpr int MODE_PLAIN = 0, MODE_K0 = 1, MODE_K1 = 2, MODE_K2 = 3, MODE_FIRST = 4;
+
+template <int CNT>
+__device__ __forceinline__ void pg_vmwait() {
+  static_assert(CNT >= 0 && CNT < 64, "vmcnt");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(CNT) : "memory");
+}
+
+__device__ __forceinline__ void pg_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int ACT>
+__device__ __forceinline__ float pg_act(float v) {
+  if constexpr (ACT == 1) {
+    const float u = 0.7978845608f * (v + 0.044715f * v * v * v);
+    return 0.5f * v * (1.f + tanhf(u));
+  } else if constexpr (ACT == 2) {
+    return v / (1.f + __expf(-v));
+  } else if constexpr (ACT == 4) {
+    return 0.5f * v * (1.f + erff(v * 0.70710678118f));
+  } else {
+    return v;
+  }
+}
+
+struct PgRegs {
+  f32x4_t acc[2][2][4][2];       // [quadrant m][quadrant n][16-row tile][16-col tile]
+  bf16x8_t a[4][2];              // A fragments of the current M-half: [16-row tile][k32]
+  bf16x8_t w[2][2];              // W fragments of the current N-half: [16-col tile][k32]
+};
+
+// load cursor: the K-step whose half-tiles the current K-step's phases issue
+struct PgLoad {
+  __amdgpu_buffer_rsrc_t ra;     // A rows [m0, M) of the cursor's tile
+  __amdgpu_buffer_rsrc_t rw;     // W rows [n0, N)
+  int kbyte;                     // k * 128
+  int k, tile;                   // K-step in the tile, tile index of this workgroup
+  bool done;                     // past the last step: re-issue the last one (free halves)
+};
+
+// output side of the tile whose quadrants are stored
+struct PgOut {
+  __amdgpu_buffer_rsrc_t rc;     // C rows [m0, M)
+  int n0;
+};
+
+// thread constants
+struct PgThr {
+  int a_voff[2][2];              // [half][instr]: A source offset (bytes, from the tile's row 0)
+  int w_voff;                    // W source offset of this thread (instr / half parts uniform)
+  int w_uoff[2][2];              // [half][instr]: uniform W row offset (bytes)
+  int ra_off, rw_off;            // fragment row offsets in a half image (bytes)
+  int co[2];                     // fragment chunk offsets for k32 step 0 / 1 (bytes)
+  int wave, wm, wn, fr, fg;
+  int ldc;
+};
+
+__device__ __forceinline__ void pg_tile_coords(int lin, int tiles_m, int tiles_n, int& tm,
+                                               int& tn) {
+  const int per_group = PG_GROUP_M * tiles_n;
+  const int g = lin / per_group, r = lin % per_group;
+  const int first = g * PG_GROUP_M;
+  const int gsize = min(PG_GROUP_M, tiles_m - first);
+  tm = first + r % gsize;
+  tn = r / gsize;
+}
+
+template <int H>
+__device__ __forceinline__ void pg_issue(char* smem, int stage, const PgLoad& L, const PgThr& T) {
+  char* dst = smem + stage * PG_STAGE_B + H * PG_HALF_B + T.wave * 1024;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    if constexpr (H == HA0 || H == HA1) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(L.ra, (lds_void_t*)(dst + i * 8192), 16,
+                                               T.a_voff[H][i], L.kbyte, 0, 0);
+    } else {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(L.rw, (lds_void_t*)(dst + i * 8192), 16,
+                                               T.w_voff, L.kbyte + T.w_uoff[H - HW0][i], 0, 0);
+    }
+  }
+}
+
+__device__ __forceinline__ bf16x8_t pg_frag(const char* p) {
+  return *reinterpret_cast<const bf16x8_t*>(p);
+}
+
+// A fragments of M-half H from stage `stage`
+template <int H>
+__device__ __forceinline__ void pg_read_a(bf16x8_t (&a)[4][2], const char* smem, int stage,
+                                          const PgThr& T) {
+  const char* b = smem + stage * PG_STAGE_B + H * PG_HALF_B + T.ra_off;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) a[i][kk] = pg_frag(b + i * 2048 + T.co[kk]);
+}
+
+template <int H>
+__device__ __forceinline__ void pg_read_w(bf16x8_t (&w)[2][2], const char* smem, int stage,
+                                          const PgThr& T) {
+  const char* b = smem + stage * PG_STAGE_B + (HW0 + H) * PG_HALF_B + T.rw_off;
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) w[j][kk] = pg_frag(b + j * 2048 + T.co[kk]);
+}
+
+template <int QM, int QN, bool ZERO>
+__device__ __forceinline__ void pg_mma(PgRegs& R) {
+  const bf16x8_t(&a)[4][2] = R.a;
+  const bf16x8_t(&w)[2][2] = R.w;
+  const f32x4_t z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        R.acc[QM][QN][i][j] =
+            mfma16(w[j][kk], a[i][kk], (ZERO && kk == 0) ? z : R.acc[QM][QN][i][j]);
+}
+
+// quadrant (QM, QN) of the tile described by O: NS stores per wave, always
+// issued (rows >= M are out of the buffer range and dropped)
+template <int QM, int QN, int ACT, int BIAS>
+__device__ __forceinline__ void pg_store(const PgRegs& R, const PgOut& O, const PgThr& T,
+                                         const char* smem) {
+  if constexpr (ACT == 3) {
+    // SwiGLU: 16-col tiles 0 (gate) and 1 (up) of the quadrant are one pair
+    const int col = (O.n0 >> 1) + T.wn * 32 + QN * 16 + 4 * T.fg;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = T.wm * 128 + QM * 64 + 16 * i + T.fr;
+      const f32x4_t g = R.acc[QM][QN][i][0], u = R.acc[QM][QN][i][1];
+      bf16x4_t o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = (short)f2bf(g[r] / (1.f + __expf(-g[r])) * u[r]);
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, o), O.rc,
+                                            (row * T.ldc + col) * 2, 0, 0);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = O.n0 + T.wn * 64 + QN * 32 + 16 * j + 4 * T.fg;
+      f32x4_t b = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (BIAS) {
+        const bf16x4_t bb = *reinterpret_cast<const bf16x4_t*>(smem + PG_RING_B + col * 2);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) b[r] = bf2f((uint16_t)bb[r]);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = T.wm * 128 + QM * 64 + 16 * i + T.fr;
+        const f32x4_t v = R.acc[QM][QN][i][j];
+        bf16x4_t o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = (short)f2bf(pg_act<ACT>(v[r] + b[r]));
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, o), O.rc,
+                                              (row * T.ldc + col) * 2, 0, 0);
+      }
+    }
+  }
+}
+
+// stores per quadrant per wave
+template <int ACT>
+constexpr int pg_ns() { return ACT == 3 ? 4 : 8; }
+
+// DMA issue schedule (one half-tile per phase; a half is refilled in the
+// phase after its last ds_read): phase 0 of K-step s issues W N-half 0 of
+// s+1, phases 1-3 A M-half 0, W N-half 1, A M-half 1 of s+2.  Fragment reads
+// (same phase as their MFMAs): phase 0 A0 + W0, 1 W1, 2 A1, 3 W0 again.
+//
+// vmcnt at the end of phase Q's read half: the youngest DMA the next phase
+// reads was issued D phases back (Q 0/1: 6 -- W1 / A1 of this K-step; Q 3: 3 --
+// W0 of the next K-step; Q 2: the next phase reads nothing new, no wait);
+// every vector-memory op issued after it counts -- 2 DMA per phase plus the
+// epilogue stores of the window (NS per store phase; the store phases are the
+// 4 phases of a tile's first K-step S, so the windows of K-steps S, S+1 and
+// S+2 hold some of them).  Returns -1 for "no wait".
+template <int Q, int MODE, int ACT>
+constexpr int pg_vmcnt() {
+  if constexpr (Q == 2) return -1;
+  constexpr int base = Q == 3 ? 6 : 12;
+  constexpr int ns = pg_ns<ACT>();
+  if constexpr (MODE == MODE_K0) return base + ns * (Q == 0 ? 1 : Q == 1 ? 2 : 3);
+  else if constexpr (MODE == MODE_K1) return base + ns * (Q == 3 ? 0 : 4);
+  else if constexpr (MODE == MODE_K2) return base + ns * (Q == 0 ? 1 : 0);
+  else return base;
+}
+
+template <int Q, int MODE, int ACT, int BIAS>
+__device__ __forceinline__ void pg_phase(PgRegs& R, char* smem, int stage, const PgLoad& L1,
+                                         const PgLoad& L2, const PgOut& O, const PgThr& T) {
+  constexpr int QM = (Q == 2 || Q == 3) ? 1 : 0;
+  constexpr int QN = (Q == 1 || Q == 2) ? 1 : 0;
+  // ---- read half: epilogue of the previous tile's quadrant, fragments, DMA
+  if constexpr (MODE == MODE_K0) pg_store<QM, QN, ACT, BIAS>(R, O, T, smem);
+  if constexpr (Q == 0) {
+    pg_read_a<HA0>(R.a, smem, stage, T);
+    pg_read_w<0>(R.w, smem, stage, T);
+    pg_issue<HW0>(smem, stage ^ 1, L1, T);
+  } else if constexpr (Q == 1) {
+    pg_read_w<1>(R.w, smem, stage, T);
+    pg_issue<HA0>(smem, stage, L2, T);
+  } else if constexpr (Q == 2) {
+    pg_read_a<HA1>(R.a, smem, stage, T);
+    pg_issue<HW1>(smem, stage, L2, T);
+  } else {
+    pg_read_w<0>(R.w, smem, stage, T);
+    pg_issue<HA1>(smem, stage, L2, T);
+  }
+  constexpr int vm = pg_vmcnt<Q, MODE, ACT>();
+  if constexpr (vm >= 0) pg_vmwait<vm>();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  pg_barrier();
+  // ---- MFMA half
+  __builtin_amdgcn_s_setprio(1);
+  pg_mma<QM, QN, MODE == MODE_K0 || MODE == MODE_FIRST>(R);
+  __builtin_amdgcn_s_setprio(0);
+  pg_barrier();
+}
+
+template <int MODE, int ACT, int BIAS>
+__device__ __forceinline__ void pg_step(PgRegs& R, char* smem, int stage, const PgLoad& L1,
+                                        const PgLoad& L2, const PgOut& O, const PgThr& T) {
+  pg_phase<0, MODE, ACT, BIAS>(R, smem, stage, L1, L2, O, T);
+  pg_phase<1, MODE, ACT, BIAS>(R, smem, stage, L1, L2, O, T);
+  pg_phase<2, MODE, ACT, BIAS>(R, smem, stage, L1, L2, O, T);
+  pg_phase<3, MODE, ACT, BIAS>(R, smem, stage, L1, L2, O, T);
+}
+
+}  // namespace
+
+template <int ACT, int BIAS>
+__global__ void __launch_bounds__(PG_THREADS, 1) pgemm_kernel(
+    bf16_t* __restrict__ C, const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
+    const bf16_t* __restrict__ bias, int M, int N, int K, int lda, int ldw, int ldc) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tiles_m = (M + 255) / 256, tiles_n = N / 256, ntiles = tiles_m * tiles_n;
+  const int G = gridDim.x;
+  const int r = xcd_remap(blockIdx.x, G);
+  const int my_tiles = (ntiles - r + G - 1) / G;
+  const int nk = K / 64;
+
+  PgThr T;
+  const int lane = threadIdx.x & 63;
+  T.wave = threadIdx.x >> 6;
+  T.wm = T.wave >> 2;
+  T.wn = T.wave & 3;
+  T.fr = lane & 15;
+  T.fg = lane >> 4;
+  T.ldc = ldc;
+  {
+    // DMA: instr i of a half covers image rows [64i, 64i+64); this lane's row
+    // 64i + 8 wave + lane/8, chunk lane%8 read from source chunk ^ swizzle
+    const int sc = (lane & 7) ^ ((4 * T.wave + (lane >> 4)) & 7);
+    const int rr = 8 * T.wave + (lane >> 3);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) T.a_voff[h][i] = (128 * i + 64 * h + rr) * lda * 2 + sc * 16;
+    // W image row lr = 64i + rr -> tile column (2i + wave/4) * 64 + 32h + 8 (wave%4) + lane/8
+    T.w_voff = ((T.wave >> 2) * 64 + 8 * (T.wave & 3) + (lane >> 3)) * ldw * 2 + sc * 16;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) T.w_uoff[h][i] = (128 * i + 32 * h) * ldw * 2;
+    T.ra_off = (T.wm * 64 + T.fr) * 128;
+    T.rw_off = (T.wn * 32 + T.fr) * 128;
+    const int s = (T.fr >> 1) & 7;
+    T.co[0] = 16 * (T.fg ^ s);
+    T.co[1] = 16 * ((4 + T.fg) ^ s);
+  }
+
+  if constexpr (BIAS) {
+    // bias row staged once (no DMA in flight yet)
+    for (int c = threadIdx.x * 8; c < N; c += PG_THREADS * 8)
+      *reinterpret_cast<bf16x8_t*>(smem + PG_RING_B + c * 2) =
+          *reinterpret_cast<const bf16x8_t*>(bias + c);
+    __syncthreads();
+  }
+
+  auto set_tile = [&](PgLoad& L, int t) {
+    int tm, tn;
+    pg_tile_coords(t * G + r, tiles_m, tiles_n, tm, tn);
+    const int m0 = tm * 256, n0 = tn * 256;
+    const long rows = M - m0;
+    const long abytes = rows * (long)lda * 2;
+    L.ra = __builtin_amdgcn_make_buffer_rsrc((void*)(A + (long)m0 * lda), (short)0,
+                                             (int)(abytes < 0x7fffffffL ? abytes : 0x7fffffffL),
+                                             0x00020000);
+    const long wbytes = 256L * ldw * 2;
+    L.rw = __builtin_amdgcn_make_buffer_rsrc((void*)(W + (long)n0 * ldw), (short)0, (int)wbytes,
+                                             0x00020000);
+  };
+  auto set_out = [&](PgOut& O, int t) {
+    int tm, tn;
+    pg_tile_coords(t * G + r, tiles_m, tiles_n, tm, tn);
+    const int m0 = tm * 256;
+    const long cbytes = (long)(M - m0) * ldc * 2;
+    O.rc = __builtin_amdgcn_make_buffer_rsrc((void*)(C + (long)m0 * ldc), (short)0,
+                                             (int)(cbytes < 0x7fffffffL ? cbytes : 0x7fffffffL),
+                                             0x00020000);
+    O.n0 = tn * 256;
+  };
+  auto advance = [&](PgLoad& L) {
+    if (L.done) return;
+    if (++L.k == nk) {
+      if (L.tile + 1 >= my_tiles) {
+        L.done = true;            // keep re-issuing the last K-step into free halves
+        L.k = nk - 1;
+        return;
+      }
+      L.k = 0;
+      ++L.tile;
+      set_tile(L, L.tile);
+    }
+    L.kbyte = L.k * 128;
+  };
+
+  PgRegs R;
+  PgLoad L1, L2;                    // K-steps s+1 and s+2 of the running K-step s
+  L2.k = 0;
+  L2.tile = 0;
+  L2.kbyte = 0;
+  L2.done = false;
+  set_tile(L2, 0);
+  PgOut O;
+  set_out(O, 0);
+
+  // ---- prologue: the DMA of the phases before K-step 0, in loop order
+  pg_issue<HA0>(smem, 0, L2, T);
+  pg_issue<HW1>(smem, 0, L2, T);
+  pg_issue<HA1>(smem, 0, L2, T);
+  pg_issue<HW0>(smem, 0, L2, T);
+  advance(L2);
+  pg_issue<HA0>(smem, 1, L2, T);
+  pg_issue<HW1>(smem, 1, L2, T);
+  pg_issue<HA1>(smem, 1, L2, T);
+  L1 = L2;
+  advance(L2);
+  pg_vmwait<6>();                   // A0, W0 of K-step 0
+  pg_barrier();
+  if (T.wm == 1) pg_barrier();      // waves 4-7 run one barrier behind
+
+  int stage = 0;
+  auto next = [&]() {
+    L1 = L2;
+    advance(L2);
+    stage ^= 1;
+  };
+  for (int t = 0; t < my_tiles; ++t) {
+    if (t == 0) {
+      pg_step<MODE_FIRST, ACT, BIAS>(R, smem, stage, L1, L2, O, T);
+      next();
+      pg_step<MODE_PLAIN, ACT, BIAS>(R, smem, stage, L1, L2, O, T);
+      next();
+      pg_step<MODE_PLAIN, ACT, BIAS>(R, smem, stage, L1, L2, O, T);
+    } else {
+      pg_step<MODE_K0, ACT, BIAS>(R, smem, stage, L1, L2, O, T);   // stores tile t-1
+      next();
+      set_out(O, t);
+      pg_step<MODE_K1, ACT, BIAS>(R, smem, stage, L1, L2, O, T);
+      next();
+      pg_step<MODE_K2, ACT, BIAS>(R, smem, stage, L1, L2, O, T);
+    }
+    next();
+    for (int k = 3; k < nk; ++k) {
+      pg_step<MODE_PLAIN, ACT, BIAS>(R, smem, stage, L1, L2, O, T);
+      next();
+    }
+  }
+  if (T.wm == 0) pg_barrier();
+  pg_vmwait<0>();                   // trailing (re-issued) DMA lands before the LDS is released
+  pg_store<0, 0, ACT, BIAS>(R, O, T, smem);
+  pg_store<0, 1, ACT, BIAS>(R, O, T, smem);
+  pg_store<1, 1, ACT, BIAS>(R, O, T, smem);
+  pg_store<1, 0, ACT, BIAS>(R, O, T, smem);
+}
+
+// ---- launcher ---------------------------------------------------------------
+static int g_pg_cus = 0;
+
+template <int ACT, int BIAS>
+static int pg_launch(bf16_t* C, const bf16_t* A, const bf16_t* W, const bf16_t* bias, int M,
+                     int N, int K, int lda, int ldw, int ldc, int grid, hipStream_t stream) {
+  constexpr size_t smem = PG_RING_B + (BIAS ? PG_MAX_BIAS * 2 : 0);
+  static_assert(smem <= 160 * 1024, "LDS");
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e = hipFuncSetAttribute((const void*)pgemm_kernel<ACT, BIAS>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    if (e != hipSuccess) return (int)e;
+    attr = true;
+  }
+  pgemm_kernel<ACT, BIAS><<<dim3(grid), dim3(PG_THREADS), smem, stream>>>(C, A, W, bias, M, N, K,
+                                                                        lda, ldw, ldc);
+  return (int)hipGetLastError();
+}
+
+int pgemm(void* C, const void* A, const void* W, const void* bias, int M, int N, int K, long lda,
+          long ldw, long ldc, int act, int grid, hipStream_t stream) {
+  if (M <= 0) return 0;
+  if (N % 256 != 0 || K % 64 != 0 || K < 192) return -1;
+  if (lda % 8 || ldw % 8 || ldc % 4) return -1;
+  if (act < 0 || act > 4 || (act == 3 && bias != nullptr)) return -1;
+  if (bias != nullptr && N > PG_MAX_BIAS) return -1;
+  // byte offsets of one tile's rows are 32-bit
+  if (256L * lda * 2 > 0x7fffffffL || 256L * ldw * 2 > 0x7fffffffL || 256L * ldc * 2 > 0x7fffffffL)
+    return -1;
+  if (g_pg_cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return -2;
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, dev) != hipSuccess) return -2;
+    g_pg_cus = p.multiProcessorCount;
+  }
+  const long tiles = (long)((M + 255) / 256) * (N / 256);
+  if (grid <= 0) grid = g_pg_cus;
+  if (grid > tiles) grid = (int)tiles;
+  auto C_ = (bf16_t*)C;
+  auto A_ = (const bf16_t*)A;
+  auto W_ = (const bf16_t*)W;
+  auto b_ = (const bf16_t*)bias;
+  const int ia = (int)lda, iw = (int)ldw, ic = (int)ldc;
+  if (bias != nullptr) {
+    switch (act) {
+      case 0: return pg_launch<0, 1>(C_, A_, W_, b_, M, N, K, ia, iw, ic, grid, stream);
+      case 1: return pg_launch<1, 1>(C_, A_, W_, b_, M, N, K, ia, iw, ic, grid, stream);
+      case 2: return pg_launch<2, 1>(C_, A_, W_, b_, M, N, K, ia, iw, ic, grid, stream);
+      case 4: return pg_launch<4, 1>(C_, A_, W_, b_, M, N, K, ia, iw, ic, grid, stream);
+    }
+    return -1;
+  }
+  switch (act) {
+    case 0: return pg_launch<0, 0>(C_, A_, W_, b_, M, N, K, ia, iw, ic, grid, stream);
+    case 1: return pg_launch<1, 0>(C_, A_, W_, b_, M, N, K, ia, iw, ic, grid, stream);
+    case 2: return pg_launch<2, 0>(C_, A_, W_, b_, M, N, K, ia, iw, ic, grid, stream);
+    case 3: return pg_launch<3, 0>(C_, A_, W_, b_, M, N, K, ia, iw, ic, grid, stream);
+    case 4: return pg_launch<4, 0>(C_, A_, W_, b_, M, N, K, ia, iw, ic, grid, stream);
+  }
+  return -1;
+}
+
+}  // namespace lmx

@@ -924,3 +924,56 @@ def wgemm(a: torch.Tensor, w: torch.Tensor, cfg: int, splits: int = 1, epi: int 
     native().wgemm(_ptr(out), _ptr(a), _ptr(w), _ptr(slabs), _ptr(cnt), _WG_CNT, M, N, K,
                    a.stride(0), w.stride(0), out.stride(0), code, splits, epi, _stream())
     return out
+
+
+# ---------------------------------------------------------------------------
+# K13: large-M GEMM (csrc/kernels/pgemm.hip): prefill chunks, encoder batches
+# ---------------------------------------------------------------------------
+PGEMM_MAX_BIAS = 8192
+PGEMM_CALLS = [0]          # host-side launch count (tests: the K13 path really ran)
+
+
+def pgemm_supported(N: int, K: int, act: int = 0, bias: bool = False) -> bool:
+    """Shapes K13 takes: 256-column tiles, 64-deep K-steps, >= 3 of them;
+    a bias row fits its LDS slot; the SwiGLU form takes no bias."""
+    return (N % 256 == 0 and K % 64 == 0 and K >= 192 and act in (0, 1, 2, 3, 4)
+            and not (bias and (N > PGEMM_MAX_BIAS or act == ACT_SWIGLU)))
+
+
+def pgemm(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, act: int = 0,
+          out: torch.Tensor | None = None, grid: int = 0) -> torch.Tensor:
+    """act(a @ w^T + bias) on the persistent 256x256 MFMA GEMM (any M).
+    act: ACT_NONE / ACT_GELU (tanh) / ACT_SILU / ACT_GELU_ERF, or ACT_SWIGLU
+    with ``w`` from ``interleave_gate_up(w, 16)`` (result [M, N/2]).
+    ``grid``: workgroups (0 = one per CU)."""
+    M, K = a.shape
+    N = w.shape[0]
+    ncols = N // 2 if act == ACT_SWIGLU else N
+    if not a.is_cuda:
+        if act == ACT_SWIGLU:
+            y = (a.float() @ w.float().t()).view(M, N // 32, 2, 16)
+            y = (torch.nn.functional.silu(y[:, :, 0]) * y[:, :, 1]).reshape(M, ncols).to(a.dtype)
+        else:
+            y = ref.gemm_nt(a, w, bias, act, None)
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
+    _bf16(a, "a"); _bf16(w, "w")
+    _chk(pgemm_supported(N, K, act, bias is not None),
+         f"pgemm shape N={N} K={K} act={act} bias={bias is not None}")
+    _chk(w.shape[1] == K and a.stride(1) == 1 and w.stride(1) == 1 and a.stride(0) % 8 == 0
+         and w.stride(0) % 8 == 0 and a.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0,
+         "pgemm operands need 16-B aligned rows")
+    if bias is not None:
+        _bf16(bias, "bias")
+        _chk(bias.numel() == N and bias.is_contiguous() and bias.data_ptr() % 16 == 0,
+             "pgemm bias")
+    if out is None:
+        out = torch.empty((M, ncols), dtype=a.dtype, device=a.device)
+    _chk(out.shape == (M, ncols) and out.stride(1) == 1 and out.stride(0) % 4 == 0
+         and out.data_ptr() % 8 == 0, "pgemm output layout")
+    PGEMM_CALLS[0] += 1
+    native().pgemm(_ptr(out), _ptr(a), _ptr(w), _ptr(bias), M, N, K, a.stride(0), w.stride(0),
+                   out.stride(0), act, grid, _stream())
+    return out
