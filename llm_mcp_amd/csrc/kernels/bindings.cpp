@@ -54,7 +54,7 @@ int wgemm(void*, const void*, const void*, float*, unsigned*, int, int, int, int
           int, int, int, hipStream_t);
 int wgemm_pack(void*, const void*, int, int, long, int, hipStream_t);
 int pgemm(void*, const void*, const void*, const void*, int, int, int, long, long, long, int, int,
-          hipStream_t);
+          int, hipStream_t);
 int wgemm_num_configs();
 int wgemm_config(int, int*, int*);
 long ar_region_bytes(long);
@@ -206,9 +206,9 @@ PYBIND11_MODULE(_lmx_kernels, m) {
   });
   // ---- K13 large-M GEMM (pgemm.hip) ----
   m.def("pgemm", [](uptr C, uptr A, uptr W, uptr bias, int M, int N, int K, long lda, long ldw,
-                    long ldc, int act, int grid, uptr stream) {
+                    long ldc, int act, int grid, int variant, uptr stream) {
     check(lmx::pgemm(P<void>(C), P<void>(A), P<void>(W), P<void>(bias), M, N, K, lda, ldw, ldc,
-                     act, grid, S(stream)),
+                     act, grid, variant, S(stream)),
           "pgemm");
   });
   m.def("wgemm_pack", [](uptr P_, uptr W, int N, int K, long ldw, int cfg, uptr stream) {

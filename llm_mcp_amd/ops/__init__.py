@@ -941,11 +941,12 @@ def pgemm_supported(N: int, K: int, act: int = 0, bias: bool = False) -> bool:
 
 
 def pgemm(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, act: int = 0,
-          out: torch.Tensor | None = None, grid: int = 0) -> torch.Tensor:
+          out: torch.Tensor | None = None, grid: int = 0, variant: int = 0) -> torch.Tensor:
     """act(a @ w^T + bias) on the persistent 256x256 MFMA GEMM (any M).
     act: ACT_NONE / ACT_GELU (tanh) / ACT_SILU / ACT_GELU_ERF, or ACT_SWIGLU
     with ``w`` from ``interleave_gate_up(w, 16)`` (result [M, N/2]).
-    ``grid``: workgroups (0 = one per CU)."""
+    ``grid``: workgroups (0 = one per CU); ``variant``: 0 four waves with
+    128x128 wave tiles (default), 1 the eight-wave ping-pong form."""
     M, K = a.shape
     N = w.shape[0]
     ncols = N // 2 if act == ACT_SWIGLU else N
@@ -975,5 +976,5 @@ def pgemm(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, ac
          and out.data_ptr() % 8 == 0, "pgemm output layout")
     PGEMM_CALLS[0] += 1
     native().pgemm(_ptr(out), _ptr(a), _ptr(w), _ptr(bias), M, N, K, a.stride(0), w.stride(0),
-                   out.stride(0), act, grid, _stream())
+                   out.stride(0), act, grid, variant, _stream())
     return out

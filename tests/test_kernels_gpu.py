@@ -660,7 +660,8 @@ def test_wgemm_vs_fp32(cfg, M):
 @pytest.mark.parametrize("M,N,K", [(256, 512, 192), (300, 768, 768), (1000, 2304, 768),
                                    (4096, 1024, 1024), (77, 256, 4096)])
 @pytest.mark.parametrize("grid", [0, 3])
-def test_pgemm_vs_fp32(M, N, K, grid):
+@pytest.mark.parametrize("variant", [0, 1, 2])
+def test_pgemm_vs_fp32(M, N, K, grid, variant):
     """K13 persistent large-M GEMM (csrc/kernels/pgemm.hip): plain, bias +
     GELU(erf) (BERT FFN), bias only, SwiGLU on 16-row gate/up pairs, against
     an fp32 PyTorch reference; ragged M (rows >= M dropped by the buffer
@@ -671,22 +672,22 @@ def test_pgemm_vs_fp32(M, N, K, grid):
     b = _bf(N)
     y = a.float() @ w.float().t()
     before = ops.PGEMM_CALLS[0]
-    out = ops.pgemm(a, w, grid=grid)
+    out = ops.pgemm(a, w, grid=grid, variant=variant)
     torch.testing.assert_close(out.float(), y, atol=2e-2, rtol=2e-2)
-    assert torch.equal(out, ops.pgemm(a, w, grid=grid))            # deterministic
+    assert torch.equal(out, ops.pgemm(a, w, grid=grid, variant=variant))            # deterministic
     yb = y + b.float()
-    torch.testing.assert_close(ops.pgemm(a, w, bias=b, grid=grid).float(), yb, atol=2e-2,
+    torch.testing.assert_close(ops.pgemm(a, w, bias=b, grid=grid, variant=variant).float(), yb, atol=2e-2,
                                rtol=2e-2)
-    torch.testing.assert_close(ops.pgemm(a, w, bias=b, act=ops.ACT_GELU_ERF, grid=grid).float(),
+    torch.testing.assert_close(ops.pgemm(a, w, bias=b, act=ops.ACT_GELU_ERF, grid=grid, variant=variant).float(),
                                torch.nn.functional.gelu(yb), atol=2e-2, rtol=2e-2)
     wil = ops.interleave_gate_up(w, 16)
     I = N // 2
     g = torch.nn.functional.silu(y[:, :I]) * y[:, I:]
-    torch.testing.assert_close(ops.pgemm(a, wil, act=ops.ACT_SWIGLU, grid=grid).float(), g,
+    torch.testing.assert_close(ops.pgemm(a, wil, act=ops.ACT_SWIGLU, grid=grid, variant=variant).float(), g,
                                atol=2e-2, rtol=2e-2)
     # strided output rows (a view into a wider buffer)
     big = torch.zeros(M, N + 64, dtype=torch.bfloat16, device=DEV)
-    ops.pgemm(a, w, out=big[:, 32:32 + N], grid=grid)
+    ops.pgemm(a, w, out=big[:, 32:32 + N], grid=grid, variant=variant)
     torch.testing.assert_close(big[:, 32:32 + N].float(), y, atol=2e-2, rtol=2e-2)
     assert big[:, :32].abs().sum().item() == 0 and big[:, 32 + N:].abs().sum().item() == 0
     assert ops.PGEMM_CALLS[0] - before == 6
