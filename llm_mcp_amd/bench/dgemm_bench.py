@@ -272,16 +272,26 @@ def table_from_rows(rows: list[dict], margin: float) -> list[dict]:
     return _consistent_bn(out)
 
 
-def encoder(ms: list[int], write: bool = False) -> None:
-    """Prefill / encoder shapes (nomic-bert, Llama-3-8B prefill): every K11
-    configuration (S = 1) vs the older gemm_nt kernel vs hipBLASLt, warm
-    operands (uniform [-1, 1)), TFLOP/s."""
+SWIGLU_SHAPES = ("nomic.gate_up", "l8b.gate_up")
+
+
+def encoder(ms: list[int], write: bool = False, k11: bool = False) -> None:
+    """Prefill / encoder shapes (nomic-bert, BERT-large, Llama-3-8B prefill):
+    hipBLASLt vs K13 (the large-M GEMM, ops.pgemm), warm operands (uniform
+    [-1, 1)), TFLOP/s; the gate/up shapes also as the fused SwiGLU forms
+    (library GEMM + GLU kernel vs K13's SwiGLU epilogue, FLOPs of the GEMM).
+    ``k11``: also sweep every K11 configuration and gemm_nt (the round-2 table).
+    ``write`` merges the numbers of the largest M into config/dgemm_gfx950.json
+    "encoder" (read by ops.encoder_backend / ops.large_gemm_backend)."""
     shapes = {"nomic.qkv": (2304, 768), "nomic.o": (768, 768), "nomic.gate_up": (6144, 768),
-              "nomic.down": (768, 3072), "l8b.qkv": (6144, 4096), "l8b.gate_up": (28672, 4096),
-              "l8b.down": (4096, 14336), "bert.qkv": (3072, 1024), "bert.o": (1024, 1024),
-              "bert.w1": (4096, 1024), "bert.w2": (1024, 4096)}
+              "nomic.down": (768, 3072), "l8b.qkv": (6144, 4096), "l8b.o": (4096, 4096),
+              "l8b.gate_up": (28672, 4096), "l8b.down": (4096, 14336), "bert.qkv": (3072, 1024),
+              "bert.o": (1024, 1024), "bert.w1": (4096, 1024), "bert.w2": (1024, 4096)}
     cfgs = ops.native().dgemm_configs()
-    wins: dict = {}
+    path = os.path.join(os.path.dirname(os.path.dirname(__file__)), "config", "dgemm_gfx950.json")
+    with open(path) as f:
+        doc = json.load(f)
+    table = {(e["N"], e["K"]): e for e in doc.get("encoder", [])}
     for M in ms:
         for name, (N, K) in shapes.items():
             if name.startswith("l8b") and M < 8192:
@@ -290,47 +300,58 @@ def encoder(ms: list[int], write: bool = False) -> None:
             w = (torch.rand(N, K, device="cuda", dtype=torch.bfloat16) * 2 - 1) * K ** -0.5
             fl = 2.0 * M * N * K
             iters = max(5, min(50, int(2e12 / fl)))
-            t_lib = _time(lambda i: torch.nn.functional.linear(x, w), iters)
-            t_nt = _time(lambda i: ops.gemm_nt(x, w), iters) if ops.gemm_nt_supported(N, K) \
-                else None
             ref = torch.nn.functional.linear(x, w).float()
-            best = None
-            for cfg, (bm, bn) in enumerate(cfgs):
-                if N % bn or (epi == 3 and not ops.swiglu16_ok(cfg)):
-                    continue
-                out = ops.dgemm(x, w, cfg, 1)
-                if not (out.float() - ref).abs().max().item() <= 2e-2 * ref.abs().max().item():
-                    print(f"  !! {name} M={M} cfg={cfg}: mismatch", file=sys.stderr)
-                    continue
-                t = _time(lambda i: ops.dgemm(x, w, cfg, 1, out=out), iters)
-                if best is None or t < best[0]:
-                    best = (t, cfg, bm, bn)
-            line = f"{name:13s} M={M:6d} lib {fl / t_lib / 1e6:6.0f} TF"
-            if t_nt:
-                line += f" | gemm_nt {fl / t_nt / 1e6:6.0f} TF"
-            if best:
-                line += f" | K11 cfg {best[1]} ({best[2]}x{best[3]}) {fl / best[0] / 1e6:6.0f} TF"
-                # vs the previous hand-written encoder GEMM (gemm_nt): keep the
-                # K11 tile that wins at the largest M measured
-                wins[(N, K)] = {"N": N, "K": K, "cfg": best[1], "bn": best[3], "M": M,
-                                "tflops": round(fl / best[0] / 1e12 * 1e6, 1),
-                                "gemm_nt_tflops": round(fl / t_nt / 1e6, 1) if t_nt else None,
-                                "lib_tflops": round(fl / t_lib / 1e6, 1)}
+            t_lib = _time(lambda i: torch.nn.functional.linear(x, w), iters)
+            out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+            ops.pgemm(x, w, out=out)
+            assert (out.float() - ref).abs().max().item() <= 2e-2 * ref.abs().max().item(), name
+            t_k13 = _time(lambda i: ops.pgemm(x, w, out=out), iters)
+            e = table.setdefault((N, K), {"N": N, "K": K})
+            e.update({"M": M, "lib_tflops": round(fl / t_lib / 1e6, 1),
+                      "k13_tflops": round(fl / t_k13 / 1e6, 1)})
+            line = (f"{name:13s} M={M:6d} lib {fl / t_lib / 1e6:6.0f} TF | "
+                    f"K13 {fl / t_k13 / 1e6:6.0f} TF ({t_lib / t_k13:.3f}x)")
+            if name in SWIGLU_SHAPES:
+                wil = ops.interleave_gate_up(w, ops.SWIGLU16)
+                g = torch.empty(M, N // 2, device="cuda", dtype=torch.bfloat16)
+                t_lg = _time(lambda i: ops.silu_mul(torch.nn.functional.linear(x, wil),
+                                                    block=ops.SWIGLU16), iters)
+                t_ks = _time(lambda i: ops.pgemm(x, wil, act=ops.ACT_SWIGLU, out=g), iters)
+                e.update({"lib_glu_tflops": round(fl / t_lg / 1e6, 1),
+                          "k13_swiglu_tflops": round(fl / t_ks / 1e6, 1)})
+                line += (f" | SwiGLU: lib+glu {fl / t_lg / 1e6:6.0f} TF, K13 "
+                         f"{fl / t_ks / 1e6:6.0f} TF ({t_lg / t_ks:.3f}x)")
+            if k11:
+                t_nt = _time(lambda i: ops.gemm_nt(x, w), iters) \
+                    if ops.gemm_nt_supported(N, K) else None
+                best = None
+                for cfg, (bm, bn) in enumerate(cfgs):
+                    if N % bn:
+                        continue
+                    o11 = ops.dgemm(x, w, cfg, 1)
+                    if not (o11.float() - ref).abs().max().item() <= 2e-2 * ref.abs().max().item():
+                        continue
+                    t = _time(lambda i: ops.dgemm(x, w, cfg, 1, out=o11), iters)
+                    if best is None or t < best[0]:
+                        best = (t, cfg, bm, bn)
+                if best:
+                    e.update({"cfg": best[1], "bn": best[3],
+                              "tflops": round(fl / best[0] / 1e6, 1)})
+                    line += f" | K11 cfg {best[1]} {fl / best[0] / 1e6:6.0f} TF"
+                if t_nt:
+                    e["gemm_nt_tflops"] = round(fl / t_nt / 1e6, 1)
             print(line, flush=True)
     if write:
-        path = os.path.join(os.path.dirname(os.path.dirname(__file__)), "config",
-                            "dgemm_gfx950.json")
-        with open(path) as f:
-            doc = json.load(f)
-        doc["encoder"] = sorted(wins.values(), key=lambda e: (e["N"], e["K"]))
+        doc["encoder"] = sorted(table.values(), key=lambda e: (e["N"], e["K"]))
         with open(path, "w") as f:
             json.dump(doc, f, indent=1)
-        print(f"wrote {len(wins)} encoder entries to {path}")
+        print(f"wrote {len(table)} encoder entries to {path}")
 
 
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--encoder", default="", help="comma list of M: prefill/encoder shapes")
+    ap.add_argument("--k11", action="store_true", help="--encoder: also sweep K11 and gemm_nt")
     ap.add_argument("--model", default="llama-3-8b")
     ap.add_argument("--tp", type=int, default=1)
     ap.add_argument("--m", default=",".join(map(str, BUCKETS)))
@@ -351,7 +372,7 @@ def main(argv=None):
     ops.native()
     os.environ.setdefault("LMX_DGEMM", "0")
     if a.encoder:
-        encoder([int(v) for v in a.encoder.split(",")], a.write)
+        encoder([int(v) for v in a.encoder.split(",")], a.write, a.k11)
         return
     from ..engine.engine import _load_gemm_tuning
     _load_gemm_tuning()       # the library as served: hipBLASLt with the TunableOp table

@@ -206,32 +206,50 @@ __device__ __forceinline__ void pg_store(const RT& R, const PgOut& O, const PgTh
                                             (row * T.ldc + col) * 2, 0, 0);
     }
   } else {
+    // the quadrant's two 16-column tiles as one 16-B store per lane: lanes of
+    // 16-lane rows 0/2 keep tile 0 and take its columns 4-7 from the row
+    // above, rows 1/3 take tile 1's columns 0-3 from the row below
+    // (v_permlane16_swap), so 4 stores per quadrant instead of 8
+    f32x4_t b[2];
+    if constexpr (BIAS) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int col = O.n0 + T.wn * 64 + QN * 32 + 16 * j + 4 * T.fg;
-      f32x4_t b = {0.f, 0.f, 0.f, 0.f};
-      if constexpr (BIAS) {
-        const bf16x4_t bb = *reinterpret_cast<const bf16x4_t*>(smem + PG_RING_B + col * 2);
+      for (int j = 0; j < 2; ++j) {
+        const int bc = O.n0 + T.wn * 64 + QN * 32 + 16 * j + 4 * T.fg;
+        const bf16x4_t bb = *reinterpret_cast<const bf16x4_t*>(smem + PG_RING_B + bc * 2);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) b[r] = bf2f((uint16_t)bb[r]);
+        for (int r = 0; r < 4; ++r) b[j][r] = bf2f((uint16_t)bb[r]);
       }
+    }
+    const int col = O.n0 + T.wn * 64 + QN * 32 + 16 * (T.fg & 1) + 8 * (T.fg >> 1);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = T.wm * 128 + QM * 64 + 16 * i + T.fr;
+    for (int i = 0; i < 4; ++i) {
+      const int row = T.wm * 128 + QM * 64 + 16 * i + T.fr;
+      unsigned d[2][2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
         const f32x4_t v = R.acc[QM][QN][i][j];
-        bf16x4_t o;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = (short)f2bf(pg_act<ACT>(v[r] + b[r]));
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, o), O.rc,
-                                              (row * T.ldc + col) * 2, 0, 0);
+        for (int q = 0; q < 2; ++q) {
+          float x0 = v[2 * q], x1 = v[2 * q + 1];
+          if constexpr (BIAS) {
+            x0 += b[j][2 * q];
+            x1 += b[j][2 * q + 1];
+          }
+          d[j][q] = pack_bf16x2(pg_act<ACT>(x0), pg_act<ACT>(x1));
+        }
       }
+      const auto p = __builtin_amdgcn_permlane16_swap(d[0][0], d[1][0], false, false);
+      const auto q = __builtin_amdgcn_permlane16_swap(d[0][1], d[1][1], false, false);
+      typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+      const u32x4_t o = {p[0], q[0], p[1], q[1]};
+      __builtin_amdgcn_raw_buffer_store_b128(o, O.rc, (row * T.ldc + col) * 2, 0, 0);
     }
   }
 }
 
 // stores per quadrant per wave
 template <int ACT>
-constexpr int pg_ns() { return ACT == 3 ? 4 : 8; }
+constexpr int pg_ns() { return 4; }   // 16-B (8-B SwiGLU) stores of 16 rows each
 
 // DMA issue schedule (one half-tile per phase; a half is refilled in the
 // phase after its last ds_read): phase 0 of K-step s issues W N-half 0 of
@@ -475,12 +493,16 @@ struct PpRegs {
 template <int ACT>
 constexpr int pp_nsp() { return 2 * pg_ns<ACT>(); }   // stores per phase (two quadrants)
 
-template <int Q, int MODE, int ACT>
+// SCHED 0: phase 0 issues A1 of s+1, phase 1 A0 W0 W1 of s+2 (2 / 6 DMA per
+// wave); SCHED 1: phase 0 A1 and W1 of s+1, phase 1 A0 W0 of s+2 (4 / 4; W1 then
+// has one phase less to land)
+template <int Q, int MODE, int ACT, int SCHED>
 constexpr int pp_vmcnt() {
   constexpr int ns = pp_nsp<ACT>();
-  if constexpr (MODE == MODE_K0) return Q == 0 ? 8 + ns : 8 + 2 * ns;
-  else if constexpr (MODE == MODE_K1) return Q == 0 ? 8 + ns : 8;
-  else return 8;
+  constexpr int b0 = SCHED == 0 ? 8 : 10, b1 = SCHED == 0 ? 8 : 4;
+  if constexpr (MODE == MODE_K0) return Q == 0 ? b0 + ns : (SCHED == 0 ? b1 + 2 * ns : b1 + ns);
+  else if constexpr (MODE == MODE_K1) return Q == 0 ? b0 + ns : b1;
+  else return Q == 0 ? b0 : b1;
 }
 
 template <int QM, bool ZERO>
@@ -500,7 +522,7 @@ __device__ __forceinline__ void pp_mma(PpRegs& R) {
   }
 }
 
-template <int Q, int MODE, int ACT, int BIAS>
+template <int Q, int MODE, int ACT, int BIAS, int SCHED>
 __device__ __forceinline__ void pp_phase(PpRegs& R, char* smem, int stage, const PgLoad& L1,
                                          const PgLoad& L2, const PgOut& O, const PgThr& T) {
   if constexpr (MODE == MODE_K0) {
@@ -514,13 +536,14 @@ __device__ __forceinline__ void pp_phase(PpRegs& R, char* smem, int stage, const
     pg_read_w<0>(R.w0, smem, stage, T);
     pg_read_w<1>(R.w1, smem, stage, T);
     pg_issue<HA1>(smem, stage ^ 1, L1, T);
+    if constexpr (SCHED == 1) pg_issue<HW1>(smem, stage ^ 1, L1, T);
   } else {
     pg_read_a<HA1>(R.a, smem, stage, T);
     pg_issue<HA0>(smem, stage, L2, T);
     pg_issue<HW0>(smem, stage, L2, T);
-    pg_issue<HW1>(smem, stage, L2, T);
+    if constexpr (SCHED == 0) pg_issue<HW1>(smem, stage, L2, T);
   }
-  pg_vmwait<pp_vmcnt<Q, MODE, ACT>()>();
+  pg_vmwait<pp_vmcnt<Q, MODE, ACT, SCHED>()>();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   pg_barrier();
   __builtin_amdgcn_s_setprio(1);
@@ -529,16 +552,16 @@ __device__ __forceinline__ void pp_phase(PpRegs& R, char* smem, int stage, const
   pg_barrier();
 }
 
-template <int MODE, int ACT, int BIAS>
+template <int MODE, int ACT, int BIAS, int SCHED>
 __device__ __forceinline__ void pp_step(PpRegs& R, char* smem, int stage, const PgLoad& L1,
                                         const PgLoad& L2, const PgOut& O, const PgThr& T) {
-  pp_phase<0, MODE, ACT, BIAS>(R, smem, stage, L1, L2, O, T);
-  pp_phase<1, MODE, ACT, BIAS>(R, smem, stage, L1, L2, O, T);
+  pp_phase<0, MODE, ACT, BIAS, SCHED>(R, smem, stage, L1, L2, O, T);
+  pp_phase<1, MODE, ACT, BIAS, SCHED>(R, smem, stage, L1, L2, O, T);
 }
 
 }  // namespace
 
-template <int ACT, int BIAS>
+template <int ACT, int BIAS, int SCHED>
 __global__ void __launch_bounds__(PG_THREADS, 1) pgemm_pp2_kernel(
     bf16_t* __restrict__ C, const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
     const bf16_t* __restrict__ bias, int M, int N, int K, int lda, int ldw, int ldc) {
@@ -630,17 +653,30 @@ __global__ void __launch_bounds__(PG_THREADS, 1) pgemm_pp2_kernel(
   set_out(O, 0);
 
   // ---- prologue: the DMA of the phases before K-step 0, in loop order
-  pg_issue<HA0>(smem, 0, L2, T);
-  pg_issue<HW0>(smem, 0, L2, T);
-  pg_issue<HW1>(smem, 0, L2, T);
-  pg_issue<HA1>(smem, 0, L2, T);
-  advance(L2);
-  pg_issue<HA0>(smem, 1, L2, T);
-  pg_issue<HW0>(smem, 1, L2, T);
-  pg_issue<HW1>(smem, 1, L2, T);
-  L1 = L2;
-  advance(L2);
-  pg_vmwait<8>();                   // A0, W0, W1 of K-step 0
+  if constexpr (SCHED == 0) {
+    pg_issue<HA0>(smem, 0, L2, T);
+    pg_issue<HW0>(smem, 0, L2, T);
+    pg_issue<HW1>(smem, 0, L2, T);
+    pg_issue<HA1>(smem, 0, L2, T);
+    advance(L2);
+    pg_issue<HA0>(smem, 1, L2, T);
+    pg_issue<HW0>(smem, 1, L2, T);
+    pg_issue<HW1>(smem, 1, L2, T);
+    L1 = L2;
+    advance(L2);
+    pg_vmwait<8>();                 // A0, W0, W1 of K-step 0
+  } else {
+    pg_issue<HA0>(smem, 0, L2, T);
+    pg_issue<HW0>(smem, 0, L2, T);
+    pg_issue<HA1>(smem, 0, L2, T);
+    pg_issue<HW1>(smem, 0, L2, T);
+    advance(L2);
+    pg_issue<HA0>(smem, 1, L2, T);
+    pg_issue<HW0>(smem, 1, L2, T);
+    L1 = L2;
+    advance(L2);
+    pg_vmwait<4>();                 // A0, W0, W1 of K-step 0
+  }
   pg_barrier();
   if (T.wm == 1) pg_barrier();      // waves 4-7 run one barrier behind
 
@@ -652,18 +688,18 @@ __global__ void __launch_bounds__(PG_THREADS, 1) pgemm_pp2_kernel(
   };
   for (int t = 0; t < my_tiles; ++t) {
     if (t == 0) {
-      pp_step<MODE_FIRST, ACT, BIAS>(R, smem, stage, L1, L2, O, T);
+      pp_step<MODE_FIRST, ACT, BIAS, SCHED>(R, smem, stage, L1, L2, O, T);
       next();
-      pp_step<MODE_PLAIN, ACT, BIAS>(R, smem, stage, L1, L2, O, T);
+      pp_step<MODE_PLAIN, ACT, BIAS, SCHED>(R, smem, stage, L1, L2, O, T);
     } else {
-      pp_step<MODE_K0, ACT, BIAS>(R, smem, stage, L1, L2, O, T);   // stores tile t-1
+      pp_step<MODE_K0, ACT, BIAS, SCHED>(R, smem, stage, L1, L2, O, T);   // stores tile t-1
       next();
       set_out(O, t);
-      pp_step<MODE_K1, ACT, BIAS>(R, smem, stage, L1, L2, O, T);
+      pp_step<MODE_K1, ACT, BIAS, SCHED>(R, smem, stage, L1, L2, O, T);
     }
     next();
     for (int k = 2; k < nk; ++k) {
-      pp_step<MODE_PLAIN, ACT, BIAS>(R, smem, stage, L1, L2, O, T);
+      pp_step<MODE_PLAIN, ACT, BIAS, SCHED>(R, smem, stage, L1, L2, O, T);
       next();
     }
   }
@@ -1066,9 +1102,10 @@ static int pg_launch(bf16_t* C, const bf16_t* A, const bf16_t* W, const bf16_t* 
   constexpr size_t ring = P4Geo<P4_TM>::RING > PG_RING_B ? P4Geo<P4_TM>::RING : PG_RING_B;
   constexpr size_t smem = ring + (BIAS ? PG_MAX_BIAS * 2 : 0);
   static_assert(smem <= 160 * 1024, "LDS");
-  static bool attr[3] = {false, false, false};
+  static bool attr[4] = {false, false, false, false};
   const void* fn = variant == 1   ? (const void*)pgemm_kernel<ACT, BIAS>
-                   : variant == 2 ? (const void*)pgemm_pp2_kernel<ACT, BIAS>
+                   : variant == 2 ? (const void*)pgemm_pp2_kernel<ACT, BIAS, 0>
+                   : variant == 3 ? (const void*)pgemm_pp2_kernel<ACT, BIAS, 1>
                                   : (const void*)pgemm4_kernel<P4_TM, ACT, BIAS>;
   if (!attr[variant]) {
     const hipError_t e =
@@ -1080,8 +1117,11 @@ static int pg_launch(bf16_t* C, const bf16_t* A, const bf16_t* W, const bf16_t* 
     pgemm_kernel<ACT, BIAS><<<dim3(grid), dim3(PG_THREADS), smem, stream>>>(C, A, W, bias, M, N,
                                                                           K, lda, ldw, ldc);
   else if (variant == 2)
-    pgemm_pp2_kernel<ACT, BIAS><<<dim3(grid), dim3(PG_THREADS), smem, stream>>>(C, A, W, bias, M,
-                                                                              N, K, lda, ldw, ldc);
+    pgemm_pp2_kernel<ACT, BIAS, 0><<<dim3(grid), dim3(PG_THREADS), smem, stream>>>(
+        C, A, W, bias, M, N, K, lda, ldw, ldc);
+  else if (variant == 3)
+    pgemm_pp2_kernel<ACT, BIAS, 1><<<dim3(grid), dim3(PG_THREADS), smem, stream>>>(
+        C, A, W, bias, M, N, K, lda, ldw, ldc);
   else
     pgemm4_kernel<P4_TM, ACT, BIAS><<<dim3(grid), dim3(P4_THREADS), smem, stream>>>(C, A, W, bias, M, N,
                                                                            K, lda, ldw, ldc);
@@ -1091,7 +1131,7 @@ static int pg_launch(bf16_t* C, const bf16_t* A, const bf16_t* W, const bf16_t* 
 int pgemm(void* C, const void* A, const void* W, const void* bias, int M, int N, int K, long lda,
           long ldw, long ldc, int act, int grid, int variant, hipStream_t stream) {
   if (M <= 0) return 0;
-  if (variant < 0 || variant > 2) return -1;
+  if (variant < 0 || variant > 3) return -1;
   if (N % 256 != 0 || K % 64 != 0 || K < 192) return -1;
   if (lda % 8 || ldw % 8 || ldc % 4) return -1;
   if (act < 0 || act > 4 || (act == 3 && bias != nullptr)) return -1;

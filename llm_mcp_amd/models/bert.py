@@ -70,12 +70,15 @@ class BertModel:
         return n
 
     def _linear(self, x, w, b=None, act=0, residual=None):
-        """Projection + bias (+ GELU) on the backend measured fastest for the
-        shape (ops.encoder_backend).  Returns (y, residual still to add): the
-        K7 epilogue fuses the residual, the library path leaves it to the
-        following LayerNorm's fused residual add."""
+        """Projection + bias (+ GELU) on the backend ops.encoder_backend picks
+        for the shape (K13 by default).  Returns (y, residual still to add):
+        the K7 epilogue fuses the residual, K13 and the library leave it to
+        the following LayerNorm's fused residual add."""
         if x.is_cuda:
-            kind, _ = ops.encoder_backend(w.shape[0], w.shape[1])
+            kind, _ = ops.encoder_backend(w.shape[0], w.shape[1], act, b is not None)
+            if kind == "k13" and ops.pgemm_operands_ok(x, w):
+                # bias + GELU in K13's epilogue; the residual goes to the next LayerNorm
+                return ops.pgemm(x, w, bias=b, act=act), residual
             if kind == "lib" or not ops.gemm_nt_supported(w.shape[0], w.shape[1]):
                 y = torch.nn.functional.linear(x, w, b)
                 if act == ops.ACT_GELU_ERF:

@@ -14,12 +14,13 @@ runs in-process on the GPU:
       x = LayerNorm(h + g . Wfc2^T)
   masked mean pool + Matryoshka truncation + L2 normalise (K9)
 
-Each projection runs on the backend ``ops.encoder_backend`` picks for its
-(N, K) from the measured encoder table (config/dgemm_gfx950.json
-"encoder", bench/dgemm_bench.py --encoder): the hand-written large-M GEMM
-where it was measured fastest, else hipBLASLt; the gate/up projection runs
-hand-written with the fused SwiGLU epilogue.  The sequences of a batch are
-packed (cu_seqlens), never padded.
+Every projection runs on the hand-written large-M GEMM (K13,
+csrc/kernels/pgemm.hip) by default -- ``ops.encoder_backend``; with
+LMX_ENCODER_LIBRARY=1 hipBLASLt takes the shapes where the encoder table
+(config/dgemm_gfx950.json "encoder", bench/dgemm_bench.py --encoder)
+measured it faster -- and the gate/up projection carries the SwiGLU in
+K13's epilogue (gate/up rows interleaved per 16 channels).  The sequences of
+a batch are packed (cu_seqlens), never padded.
 """
 from __future__ import annotations
 
@@ -46,12 +47,16 @@ class NomicBertModel:
         self.scale = 1.0 / math.sqrt(self.D)
         self.cos_sin = ref.rope_cos_sin(cfg.max_position, self.D, cfg.rope_theta, self.device)
         self.w = weights or self._random_weights(seed)
-        # gate/up rows interleaved for the fused SwiGLU epilogue: per BN/2
-        # channels of the K11 tile where the encoder table picks K11, else per
-        # 64 channels (gemm_nt act=3)
+        # gate/up rows interleaved for the fused SwiGLU epilogue: per 16
+        # channels for K13 (the large-M GEMM; the default), per BN/2 channels
+        # of the K11 tile where the encoder table picks K11, else per 64
+        # channels (gemm_nt act=3)
         I2, d = self.w["layers"][0]["w_gate_up"].shape
-        self.gu_cfg = ops.encoder_choice(I2, d) if self.device.type == "cuda" else None
-        self.gu_block = (ops.DGEMM_CONFIGS[self.gu_cfg & ops.DGEMM_CFG_MASK][1] // 2
+        cuda = self.device.type == "cuda"
+        self.gu_k13 = cuda and ops.encoder_backend(I2, d, ops.ACT_SWIGLU)[0] == "k13"
+        self.gu_cfg = ops.encoder_choice(I2, d) if cuda and not self.gu_k13 else None
+        self.gu_block = (ops.SWIGLU16 if self.gu_k13 else
+                         ops.DGEMM_CONFIGS[self.gu_cfg & ops.DGEMM_CFG_MASK][1] // 2
                          if self.gu_cfg is not None else 64)
         for L in self.w["layers"]:
             L.pop("w_gu_il", None)      # always this model's own layout (never a copy's)
@@ -78,9 +83,12 @@ class NomicBertModel:
                 "emb_ln_w": ones(), "emb_ln_b": zeros(), "layers": layers}
 
     def _linear(self, x, w, residual=None):
-        """Plain projection on the backend measured fastest for its shape
-        (ops.encoder_backend): K11, hipBLASLt or gemm_nt."""
+        """Plain projection on the backend ops.encoder_backend picks for its
+        shape: K13 (default), K11, gemm_nt, or hipBLASLt (LMX_ENCODER_LIBRARY=1
+        where measured faster)."""
         kind, cfg = ops.encoder_backend(w.shape[0], w.shape[1]) if x.is_cuda else ("lib", None)
+        if kind == "k13" and residual is None and ops.pgemm_operands_ok(x, w):
+            return ops.pgemm(x, w)
         if kind == "k11" and residual is None:
             return ops.dgemm(x, w, cfg, 1)
         if kind == "gemm_nt" and ops.gemm_nt_supported(w.shape[0], w.shape[1]):
@@ -135,7 +143,9 @@ class NomicBertModel:
                                         causal=False, Hq=H)
             o = self._linear(attn, L["wo"])
             h = ops.layer_norm(o, L["ln1_w"], L["ln1_b"], cfg.ln_eps, residual=x)
-            if "w_gu_il" in L and self.gu_cfg is not None and h.is_cuda:
+            if "w_gu_il" in L and self.gu_k13 and h.is_cuda:
+                g = ops.pgemm(h, L["w_gu_il"], act=ops.ACT_SWIGLU)          # K13 + fused SwiGLU
+            elif "w_gu_il" in L and self.gu_cfg is not None and h.is_cuda:
                 g = ops.dgemm(h, L["w_gu_il"], self.gu_cfg, 1, epi=1)   # K11 + fused K8
             elif "w_gu_il" in L and self.gu_block == 64:   # K8 fused into gemm_nt
                 g = ops.gemm_nt(h, L["w_gu_il"], act=ops.ACT_SWIGLU)

@@ -606,8 +606,9 @@ def splitk_preferred(M: int, N: int, K: int) -> bool:
 def linear(x: torch.Tensor, w: torch.Tensor, defer: bool = False,
            bias: torch.Tensor | None = None):
     """x @ w^T (+ bias): the decode GEMM (K11) where the measured table picks
-    it, the older split-K kernel where it was measured faster, else hipBLASLt
-    (bias in its epilogue).  ``defer``: the caller feeds the result to
+    it, the older split-K kernel where it was measured faster, the large-M
+    GEMM (K13) for prefill-sized M where ``large_gemm_backend`` picks it, else
+    hipBLASLt (bias in its epilogue).  ``defer``: the caller feeds the result to
     ``rms_norm(..., residual=)``, so a table entry for the partials-only form
     (epi 2) may return ``Partials`` and leave the K reduction to the norm."""
     if x.is_cuda and x.dim() == 2:
@@ -626,13 +627,17 @@ def linear(x: torch.Tensor, w: torch.Tensor, defer: bool = False,
             if bias is not None:
                 y += bias
             return y
+        if (large_gemm_backend(M, N, K, 0, bias is not None) == "k13"
+                and pgemm_operands_ok(x, w)):
+            return pgemm(x, w, bias=bias)
     return torch.nn.functional.linear(x, w, bias)
 
 
 def linear_swiglu(x: torch.Tensor, w: torch.Tensor, block: int) -> torch.Tensor:
     """silu(gate) * up of x @ w^T for gate|up weights interleaved per
     ``block`` channels: the fused-epilogue decode GEMM where the table picks
-    it, else the library GEMM + the GLU kernel.  block 16: the in-register
+    it, K13 with its SwiGLU epilogue for prefill-sized M (block 16), else the
+    library GEMM + the GLU kernel.  block 16: the in-register
     epilogue over 16-column gate/up pairs (epi 3, any tile width); otherwise
     the LDS hand-off form (epi 1, tile BN = 2 * block)."""
     if x.is_cuda and x.dim() == 2:
@@ -640,6 +645,9 @@ def linear_swiglu(x: torch.Tensor, w: torch.Tensor, block: int) -> torch.Tensor:
             ch = dgemm_choice(x.shape[0], w.shape[0], w.shape[1], epi=3)
             if ch is not None:
                 return dgemm(x, w, ch[0], ch[1], epi=3)
+            if (large_gemm_backend(x.shape[0], w.shape[0], w.shape[1], ACT_SWIGLU) == "k13"
+                    and pgemm_operands_ok(x, w)):
+                return pgemm(x, w, act=ACT_SWIGLU)     # K13 with the SwiGLU epilogue
         else:
             ch = dgemm_choice(x.shape[0], w.shape[0], w.shape[1], epi=1)
             if ch is not None and DGEMM_CONFIGS[ch[0] & DGEMM_CFG_MASK][1] == 2 * block:
@@ -736,32 +744,63 @@ def encoder_choice(N: int, K: int) -> int | None:
     gate/up projection), where K11 was measured faster than the older
     hand-written gemm_nt; None keeps gemm_nt."""
     e = _enc_table().get((N, K))
-    if e is None:
+    if e is None or e.get("tflops") is None or e.get("cfg") is None:
         return None
     if e.get("gemm_nt_tflops") is None or e["tflops"] > e["gemm_nt_tflops"]:
         return int(e["cfg"])
     return None
 
 
-def encoder_backend(N: int, K: int) -> tuple[str, int | None]:
-    """Backend of a PLAIN encoder GEMM of this (N, K): the faster measured
-    backend among the hand-written kernels, ("k11", cfg) or ("gemm_nt", None),
-    and hipBLASLt (("lib", None), a plain GEMM where the library was measured
-    faster).  LMX_ENCODER_LIBRARY=0 keeps every projection on the
-    hand-written kernels (profiles/r2_config5_and_embeddings.md has both
-    numbers: mxbai 2,123 vs 1,615 emb/s, nomic 2,457 vs 2,308).
-    Unmeasured shapes: gemm_nt."""
+def encoder_backend(N: int, K: int, act: int = 0,
+                    bias: bool = False) -> tuple[str, int | None]:
+    """Backend of an encoder projection of this (N, K) (+ bias / activation
+    epilogue): the large-M hand-written GEMM K13 (("k13", None)) for every
+    shape it takes.  LMX_ENCODER_LIBRARY=1 lets hipBLASLt (("lib", None))
+    take the shapes where the encoder table (bench/dgemm_bench.py --encoder)
+    measured it faster than K13.  Shapes K13 does not take: the faster
+    measured of K11 (("k11", cfg)) and gemm_nt, gemm_nt when unmeasured."""
     import os
     e = _enc_table().get((N, K))
-    if e is None:
+    if pgemm_supported(N, K, act, bias):
+        if (os.environ.get("LMX_ENCODER_LIBRARY", "0") == "1" and e is not None
+                and e.get("lib_tflops") and e.get("k13_tflops")
+                and e["lib_tflops"] > e["k13_tflops"]):
+            return ("lib", None)
+        return ("k13", None)
+    if e is None or e.get("tflops") is None or e.get("cfg") is None:
         return ("gemm_nt", None)
     cands = [(e["tflops"], "k11")]
     if e.get("gemm_nt_tflops") is not None:
         cands.append((e["gemm_nt_tflops"], "gemm_nt"))
-    if e.get("lib_tflops") is not None and os.environ.get("LMX_ENCODER_LIBRARY", "1") == "1":
+    if e.get("lib_tflops") is not None and os.environ.get("LMX_ENCODER_LIBRARY", "0") == "1":
         cands.append((e["lib_tflops"], "lib"))
     best = max(cands)[1]
     return (best, int(e["cfg"]) if best == "k11" else None)
+
+
+PGEMM_MIN_M = 512          # below: the decode-sized paths (K11 / split-K / library)
+
+
+def large_gemm_backend(M: int, N: int, K: int, act: int = 0, bias: bool = False) -> str:
+    """"k13" or "lib" for a large-M (prefill) projection.  LMX_LARGE_GEMM:
+    "k13" / "lib" force one; "auto" (default) takes the faster of the two in
+    the encoder table (config/dgemm_gfx950.json "encoder": k13_tflops vs
+    lib_tflops, or k13_swiglu_tflops vs lib_glu_tflops for the fused SwiGLU
+    form) and K13 for unmeasured shapes."""
+    import os
+    if M < PGEMM_MIN_M or not pgemm_supported(N, K, act, bias):
+        return "lib"
+    mode = os.environ.get("LMX_LARGE_GEMM", "auto")
+    if mode in ("k13", "lib"):
+        return mode
+    e = _enc_table().get((N, K))
+    if e is None:
+        return "k13"
+    mine, lib = (("k13_swiglu_tflops", "lib_glu_tflops") if act == ACT_SWIGLU
+                 else ("k13_tflops", "lib_tflops"))
+    if e.get(mine) is None or e.get(lib) is None:
+        return "k13"
+    return "k13" if e[mine] >= e[lib] else "lib"
 
 
 def dgemm_choice(M: int, N: int, K: int, epi: int = 0) -> tuple[int, int] | None:
@@ -930,6 +969,7 @@ def wgemm(a: torch.Tensor, w: torch.Tensor, cfg: int, splits: int = 1, epi: int 
 # K13: large-M GEMM (csrc/kernels/pgemm.hip): prefill chunks, encoder batches
 # ---------------------------------------------------------------------------
 PGEMM_MAX_BIAS = 8192
+PGEMM_VARIANT = 2
 PGEMM_CALLS = [0]          # host-side launch count (tests: the K13 path really ran)
 
 
@@ -940,13 +980,24 @@ def pgemm_supported(N: int, K: int, act: int = 0, bias: bool = False) -> bool:
             and not (bias and (N > PGEMM_MAX_BIAS or act == ACT_SWIGLU)))
 
 
+def pgemm_operands_ok(a: torch.Tensor, w: torch.Tensor) -> bool:
+    """Layouts K13 reads directly: unit-stride 16-B aligned rows."""
+    return (a.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and a.stride(1) == 1
+            and w.stride(1) == 1 and a.stride(0) % 8 == 0 and w.stride(0) % 8 == 0
+            and a.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0)
+
+
 def pgemm(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, act: int = 0,
-          out: torch.Tensor | None = None, grid: int = 0, variant: int = 0) -> torch.Tensor:
+          out: torch.Tensor | None = None, grid: int = 0,
+          variant: int | None = None) -> torch.Tensor:
     """act(a @ w^T + bias) on the persistent 256x256 MFMA GEMM (any M).
     act: ACT_NONE / ACT_GELU (tanh) / ACT_SILU / ACT_GELU_ERF, or ACT_SWIGLU
     with ``w`` from ``interleave_gate_up(w, 16)`` (result [M, N/2]).
-    ``grid``: workgroups (0 = one per CU); ``variant``: 0 four waves with
-    128x128 wave tiles (default), 1 the eight-wave ping-pong form."""
+    ``grid``: workgroups (0 = one per CU); ``variant`` (default
+    PGEMM_VARIANT): 2 eight-wave ping-pong, 2 phases per K-step; 3 the same
+    with the DMA split 4/4 over the phases; 1 ping-pong with 4 phases per
+    K-step; 0 four waves (one per SIMD), 192x256 tiles -- the measured
+    design points of csrc/kernels/pgemm.hip."""
     M, K = a.shape
     N = w.shape[0]
     ncols = N // 2 if act == ACT_SWIGLU else N
@@ -976,5 +1027,6 @@ def pgemm(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, ac
          and out.data_ptr() % 8 == 0, "pgemm output layout")
     PGEMM_CALLS[0] += 1
     native().pgemm(_ptr(out), _ptr(a), _ptr(w), _ptr(bias), M, N, K, a.stride(0), w.stride(0),
-                   out.stride(0), act, grid, variant, _stream())
+                   out.stride(0), act, grid, PGEMM_VARIANT if variant is None else variant,
+                   _stream())
     return out

@@ -42,9 +42,10 @@ def test_llama3_8b_decode_step_runs():
 @pytest.mark.gpu
 @pytest.mark.parametrize("preset", ["tiny-nomic", "nomic-2layer"])
 def test_nomic_bert_gpu_matches_cpu_reference(preset):
-    """Encoder on the HIP kernels (gemm_nt incl. the fused SwiGLU epilogue,
-    tiled rope/cache, bidirectional paged prefill, LayerNorm, mean-pool) vs
-    the same weights on the fp32-reference CPU path."""
+    """Encoder on the HIP kernels (K13 large-M GEMM incl. the fused SwiGLU
+    epilogue -- gemm_nt for the tiny shapes K13 does not take -- tiled
+    rope/cache, bidirectional paged prefill, LayerNorm, mean-pool) vs the same
+    weights on the fp32-reference CPU path."""
     import dataclasses
 
     from llm_mcp_amd.models import config as mc
@@ -58,7 +59,10 @@ def test_nomic_bert_gpu_matches_cpu_reference(preset):
     lens = [30, 1, 39, 70]
     ids = torch.randint(0, 500, (sum(lens),), dtype=torch.int32)
     cu = torch.tensor([0] + list(torch.cumsum(torch.tensor(lens), 0)), dtype=torch.int32)
+    before = ops.PGEMM_CALLS[0]
     a = g.forward(ids.cuda(), cu.cuda(), lens).cpu()
+    if preset == "nomic-2layer":
+        assert ops.PGEMM_CALLS[0] - before == 2 * 4     # every projection on K13
     b = c.forward(ids, cu, lens)
     cos = torch.nn.functional.cosine_similarity(a, b, dim=-1)
     assert float(cos.min()) > 0.999, cos
@@ -68,9 +72,10 @@ def test_nomic_bert_gpu_matches_cpu_reference(preset):
 @pytest.mark.gpu
 @pytest.mark.parametrize("preset", ["tiny-bert", "tiny-bert-mean", "mxbai-2layer"])
 def test_bert_gpu_matches_cpu_reference(preset):
-    """BERT encoder on the HIP kernels (gemm_nt with fused bias / exact GELU /
-    residual, kv_write, bidirectional paged prefill, LayerNorm, CLS or mean
-    pooling) vs the same weights on the fp32-reference CPU path."""
+    """BERT encoder on the HIP kernels (K13 with fused bias / exact GELU --
+    gemm_nt with the residual for the tiny shapes -- kv_write, bidirectional
+    paged prefill, LayerNorm, CLS or mean pooling) vs the same weights on the
+    fp32-reference CPU path."""
     import dataclasses
 
     from llm_mcp_amd.models import config as mc
@@ -84,7 +89,10 @@ def test_bert_gpu_matches_cpu_reference(preset):
     lens = [30, 1, 39, 70]
     ids = torch.randint(0, 500, (sum(lens),), dtype=torch.int32)
     cu = torch.tensor([0] + list(torch.cumsum(torch.tensor(lens), 0)), dtype=torch.int32)
+    before = ops.PGEMM_CALLS[0]
     a = g.forward(ids.cuda(), cu.cuda(), lens).cpu()
+    if preset == "mxbai-2layer":
+        assert ops.PGEMM_CALLS[0] - before == 2 * 4     # every projection on K13
     b = c.forward(ids, cu, lens)
     cos = torch.nn.functional.cosine_similarity(a, b, dim=-1)
     assert float(cos.min()) > 0.999, cos

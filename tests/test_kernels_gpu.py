@@ -660,7 +660,7 @@ def test_wgemm_vs_fp32(cfg, M):
 @pytest.mark.parametrize("M,N,K", [(256, 512, 192), (300, 768, 768), (1000, 2304, 768),
                                    (4096, 1024, 1024), (77, 256, 4096)])
 @pytest.mark.parametrize("grid", [0, 3])
-@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
 def test_pgemm_vs_fp32(M, N, K, grid, variant):
     """K13 persistent large-M GEMM (csrc/kernels/pgemm.hip): plain, bias +
     GELU(erf) (BERT FFN), bias only, SwiGLU on 16-row gate/up pairs, against
@@ -691,3 +691,26 @@ def test_pgemm_vs_fp32(M, N, K, grid, variant):
     torch.testing.assert_close(big[:, 32:32 + N].float(), y, atol=2e-2, rtol=2e-2)
     assert big[:, :32].abs().sum().item() == 0 and big[:, 32 + N:].abs().sum().item() == 0
     assert ops.PGEMM_CALLS[0] - before == 6
+
+
+def test_linear_large_m_runs_k13(monkeypatch):
+    """Prefill-sized projections: ops.linear / linear_swiglu route M >= 512 to
+    K13 (LMX_LARGE_GEMM=k13), bias and the 16-row gate/up SwiGLU included,
+    and match the library / GLU-kernel path."""
+    monkeypatch.setenv("LMX_LARGE_GEMM", "k13")
+    M, K, N = 700, 1024, 2048
+    x = _bf(M, K)
+    w = _bf(N, K, scale=K ** -0.5)
+    b = _bf(N)
+    before = ops.PGEMM_CALLS[0]
+    y = ops.linear(x, w, bias=b)
+    torch.testing.assert_close(y.float(), torch.nn.functional.linear(x, w, b).float(),
+                               atol=2e-2, rtol=2e-2)
+    wil = ops.interleave_gate_up(w, ops.SWIGLU16)
+    g = ops.linear_swiglu(x, wil, ops.SWIGLU16)
+    ref_g = ops.silu_mul(torch.nn.functional.linear(x, wil), block=ops.SWIGLU16)
+    torch.testing.assert_close(g.float(), ref_g.float(), atol=2e-2, rtol=2e-2)
+    assert ops.PGEMM_CALLS[0] - before == 2
+    monkeypatch.setenv("LMX_LARGE_GEMM", "lib")
+    ops.linear(x, w)
+    assert ops.PGEMM_CALLS[0] - before == 2
