@@ -86,7 +86,8 @@ VARS: list[Var] = [
     Var("LMX_SP_MIN_TOKENS", int, 0, "TP: steps with at least this many tokens run sequence-parallel (reduce-scatter/all-gather residual stream); 0 disables (default until the RCCL branch is measured on a multi-GPU node)"),
     Var("LMX_LOOKAHEAD", str, "", "engine lookahead stepping (step n+1 scheduled and launched before step n's tokens are read back; input tokens gathered on the device): default on for a single-GPU engine, 1 forces it (also on CPU), 0 off; TP groups step synchronously"),
     Var("LMX_FUSED_DECODE_ROPE", str, "1", "1: decode rows' rotary embedding and KV-cache write run inside the paged decode attention kernel; 0: separate rope/cache kernel"),
-    Var("LMX_ENCODER_LIBRARY", str, "1", "encoder (embedding-model) plain projections may run on hipBLASLt where it was measured faster than the hand-written kernels; 0 keeps them on the hand-written kernels"),
+    Var("LMX_ENCODER_LIBRARY", str, "0", "1: encoder (embedding-model) projections may run on hipBLASLt where the encoder table measured it faster than K13; 0 (default) keeps them on the hand-written kernels"),
+    Var("LMX_LARGE_GEMM", str, "auto", "large-M (prefill) projections: k13 = the hand-written persistent GEMM, lib = hipBLASLt, auto = the faster of the two per the encoder table (K13 where unmeasured)"),
     Var("LMX_TP_PROBE_STEPS", int, 2000, "TP engines: every N steps all ranks time one decode-sized all-reduce (rccl_allreduce_seconds live samples; 0 = off)"),
     Var("LMX_TP_LEADER_TIMEOUT_S", float, 30.0, "TP follower: exit when the leader's mailbox heartbeat is older than this (or its pid is gone)"),
     Var("LMX_ENGINE_INFO_S", float, 5.0, "API process: cadence of live engine info polls (KV usage, running, waiting)"),
