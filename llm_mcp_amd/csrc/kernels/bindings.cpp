@@ -55,6 +55,8 @@ int wgemm(void*, const void*, const void*, float*, unsigned*, int, int, int, int
 int wgemm_pack(void*, const void*, int, int, long, int, hipStream_t);
 int pgemm(void*, const void*, const void*, const void*, int, int, int, long, long, long, int, int,
           int, hipStream_t);
+int pgemm_sk(void*, const void*, const void*, void*, void*, int, int, int, int, long, long, long,
+             int, int, int, hipStream_t);
 int wgemm_num_configs();
 int wgemm_config(int, int*, int*);
 long ar_region_bytes(long);
@@ -210,6 +212,13 @@ PYBIND11_MODULE(_lmx_kernels, m) {
     check(lmx::pgemm(P<void>(C), P<void>(A), P<void>(W), P<void>(bias), M, N, K, lda, ldw, ldc,
                      act, grid, variant, S(stream)),
           "pgemm");
+  });
+  m.def("pgemm_sk", [](uptr C, uptr A, uptr W, uptr slabs, uptr cnt, int n_cnt, int M, int N,
+                       int K, long lda, long ldw, long ldc, int act, int splits, int epi,
+                       uptr stream) {
+    check(lmx::pgemm_sk(P<void>(C), P<void>(A), P<void>(W), P<void>(slabs), P<void>(cnt), n_cnt,
+                        M, N, K, lda, ldw, ldc, act, splits, epi, S(stream)),
+          "pgemm_sk");
   });
   m.def("wgemm_pack", [](uptr P_, uptr W, int N, int K, long ldw, int cfg, uptr stream) {
     check(lmx::wgemm_pack(P<void>(P_), P<void>(W), N, K, ldw, cfg, S(stream)), "wgemm_pack");

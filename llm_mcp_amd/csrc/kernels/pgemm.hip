@@ -712,6 +712,222 @@ __global__ void __launch_bounds__(PG_THREADS, 1) pgemm_pp2_kernel(
 }
 
 // ============================================================================
+// K13-SK: the 2-phase ping-pong 256 x 256 tile with split-K, for decode batches
+// ============================================================================
+// At decode batch sizes (M <= 256) one 256-row tile covers the batch, and every
+// column tile re-reads the whole 256 x K activation panel from L2: at the
+// 128-column tiles of K11 / hipBLASLt each CU moves 2 bytes of activations
+// through its vector L1 per byte of weights, and the L1's outstanding-miss
+// capacity bounds those kernels (profiles/r3_decode_gemm_study.md).  A
+// 256-column tile halves that ratio; split-K over S slices gives the N / 256
+// tiles enough workgroups to fill the CUs (Llama-3-8B gate/up: 112 tiles x 2).
+// One workgroup per (slice, tile), slice-major (the workgroups of one XCD read
+// the same K-slice of the activations from its L2); the main loop is the
+// pgemm_pp2 one with a single tile.  Combine:
+//   EPI 0: ticketed, in-kernel -- the first S-1 arrivals publish their fp32
+//          accumulators write-through (sc1) in the lane-native order (32
+//          coalesced 16-B stores per lane, no index math) and leave; the last
+//          adds them in slice order (deterministic) and runs the bf16 epilogue
+//          of pg_store, incl. the SwiGLU form;  counters re-armed by the last;
+//   EPI 2: every slice writes its fp32 partial tile to slab [S][M][N] and the
+//          residual-add RMSNorm that consumes the result sums the slabs
+//          (rmsnorm_slabs), so no combine at all.
+template <int ACT, int EPI>
+__global__ void __launch_bounds__(PG_THREADS, 1) pgemm_sk_kernel(
+    bf16_t* __restrict__ C, const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
+    float* __restrict__ slabs, unsigned* __restrict__ cnt, int M, int N, int K, int lda, int ldw,
+    int ldc, int splits) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tiles_m = (M + 255) / 256, tiles_n = N / 256, ntiles = tiles_m * tiles_n;
+  const int wid = xcd_remap(blockIdx.x, gridDim.x);
+  const int ks = wid / ntiles, tile = wid - ks * ntiles;
+  const int nk = K / 64 / splits;
+  const int k0 = ks * nk * 64;
+
+  PgThr T;
+  const int lane = threadIdx.x & 63;
+  T.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  T.wm = T.wave >> 2;
+  T.wn = T.wave & 3;
+  T.fr = lane & 15;
+  T.fg = lane >> 4;
+  T.ldc = ldc;
+  {
+    const int sc = (lane & 7) ^ ((4 * T.wave + (lane >> 4)) & 7);
+    const int rr = 8 * T.wave + (lane >> 3);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) T.a_voff[h][i] = (128 * i + 64 * h + rr) * lda * 2 + sc * 16;
+    T.w_voff = ((T.wave >> 2) * 64 + 8 * (T.wave & 3) + (lane >> 3)) * ldw * 2 + sc * 16;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) T.w_uoff[h][i] = (128 * i + 32 * h) * ldw * 2;
+    T.ra_off = (T.wm * 64 + T.fr) * 128;
+    T.rw_off = (T.wn * 32 + T.fr) * 128;
+    const int s = (T.fr >> 1) & 7;
+    T.co[0] = 16 * (T.fg ^ s);
+    T.co[1] = 16 * ((4 + T.fg) ^ s);
+  }
+
+  int tm, tn;
+  pg_tile_coords(tile, tiles_m, tiles_n, tm, tn);
+  const int m0 = tm * 256, n0 = tn * 256;
+  PgLoad L1, L2;
+  {
+    // the slice's K range starts at k0: base pointers moved there, byte
+    // ranges shortened by as much (rows >= M still fall outside the range)
+    const long abytes = (long)(M - m0) * lda * 2 - (long)k0 * 2;
+    L2.ra = __builtin_amdgcn_make_buffer_rsrc((void*)(A + (long)m0 * lda + k0), (short)0,
+                                              (int)(abytes < 0x7fffffffL ? abytes : 0x7fffffffL),
+                                              0x00020000);
+    L2.rw = __builtin_amdgcn_make_buffer_rsrc((void*)(W + (long)n0 * ldw + k0), (short)0,
+                                              (int)(256L * ldw * 2 - (long)k0 * 2), 0x00020000);
+  }
+  L2.k = 0;
+  L2.tile = 0;
+  L2.kbyte = 0;
+  L2.done = false;
+  PgOut O;
+  {
+    const long cbytes = (long)(M - m0) * ldc * 2;
+    O.rc = __builtin_amdgcn_make_buffer_rsrc((void*)(C + (long)m0 * ldc), (short)0,
+                                             (int)(cbytes < 0x7fffffffL ? cbytes : 0x7fffffffL),
+                                             0x00020000);
+    O.n0 = n0;
+  }
+  auto advance = [&](PgLoad& L) {
+    if (L.done) return;
+    if (++L.k == nk) {
+      L.done = true;                // re-issue the last K-step into free halves
+      L.k = nk - 1;
+      return;
+    }
+    L.kbyte = L.k * 128;
+  };
+
+  PpRegs R;
+  pg_issue<HA0>(smem, 0, L2, T);
+  pg_issue<HW0>(smem, 0, L2, T);
+  pg_issue<HW1>(smem, 0, L2, T);
+  pg_issue<HA1>(smem, 0, L2, T);
+  advance(L2);
+  pg_issue<HA0>(smem, 1, L2, T);
+  pg_issue<HW0>(smem, 1, L2, T);
+  pg_issue<HW1>(smem, 1, L2, T);
+  L1 = L2;
+  advance(L2);
+  pg_vmwait<8>();                   // A0, W0, W1 of K-step 0
+  pg_barrier();
+  if (T.wm == 1) pg_barrier();      // waves 4-7 run one barrier behind
+
+  int stage = 0;
+  auto next = [&]() {
+    L1 = L2;
+    advance(L2);
+    stage ^= 1;
+  };
+  pp_step<MODE_FIRST, ACT, 0, 0>(R, smem, stage, L1, L2, O, T);
+  next();
+  for (int k = 1; k < nk; ++k) {
+    pp_step<MODE_PLAIN, ACT, 0, 0>(R, smem, stage, L1, L2, O, T);
+    next();
+  }
+  if (T.wm == 0) pg_barrier();
+  pg_vmwait<0>();
+
+  if constexpr (EPI == 2) {
+    // fp32 partial tile -> slab ks [M][N]; rows >= M fall outside the range
+    const long sbytes = (long)M * N * 4;
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(
+        slabs + (long)ks * M * N, (short)0, (int)(sbytes < 0x7fffffffL ? sbytes : 0x7fffffffL),
+        0x00020000);
+    typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+      for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int row = m0 + T.wm * 128 + qm * 64 + 16 * i + T.fr;
+            const int col = n0 + T.wn * 64 + qn * 32 + 16 * j + 4 * T.fg;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, R.acc[qm][qn][i][j]),
+                                                   rs, (row * N + col) * 4, 0, 0);
+          }
+    return;
+  } else {
+    if (splits > 1) {
+      typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+      constexpr int TSLAB = PG_THREADS * 128;        // floats of one slice's tile
+      unsigned* word = reinterpret_cast<unsigned*>(smem + PG_RING_B);
+      __syncthreads();                               // every wave's DMA has landed
+      if (threadIdx.x == 0)
+        word[0] = __hip_atomic_fetch_add(&cnt[2 * tile], 1u, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      const unsigned order = word[0];
+      float* tslab = slabs + (long)tile * splits * TSLAB;
+      // accumulator r = ((qm * 2 + qn) * 4 + i) * 2 + j of every lane is float4
+      // r * PG_THREADS + tid of a slice's slab
+#define PG_FOR_ACC(BODY)                                   \
+  _Pragma("unroll") for (int qm = 0; qm < 2; ++qm)         \
+  _Pragma("unroll") for (int qn = 0; qn < 2; ++qn)         \
+  _Pragma("unroll") for (int i = 0; i < 4; ++i)            \
+  _Pragma("unroll") for (int j = 0; j < 2; ++j) {          \
+    const int r = ((qm * 2 + qn) * 4 + i) * 2 + j;         \
+    f32x4_t& a = R.acc[qm][qn][i][j];                      \
+    BODY                                                   \
+  }
+      if (order + 1 < (unsigned)splits) {
+        // publish write-through (sc1): no L2 write-back fence (wgemm.hip)
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc(tslab + (long)ks * TSLAB, (short)0,
+                                                          TSLAB * 4, 0x00020000);
+        PG_FOR_ACC(__builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(u32x4_t, a), rs, (r * PG_THREADS + (int)threadIdx.x) * 16, 0, 16);)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0)
+          __hip_atomic_fetch_add(&cnt[2 * tile + 1], 1u, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+        return;
+      }
+      if (threadIdx.x == 0) {
+        while (__hip_atomic_load(&cnt[2 * tile + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+               (unsigned)(splits - 1))
+          __builtin_amdgcn_s_sleep(2);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(&cnt[2 * tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&cnt[2 * tile + 1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __syncthreads();
+      // ((p0 + p1) + ...) + p(S-1), own partial at its slice position
+      const f32x4_t* tin = reinterpret_cast<const f32x4_t*>(tslab) + threadIdx.x;
+      PG_FOR_ACC({
+        f32x4_t v;
+        if (ks > 0) {
+          v = tin[r * PG_THREADS];
+          for (int s = 1; s < ks; ++s) v += tin[(long)s * (TSLAB / 4) + r * PG_THREADS];
+          v += a;
+        } else {
+          v = a;
+        }
+        for (int s = ks + 1; s < splits; ++s) v += tin[(long)s * (TSLAB / 4) + r * PG_THREADS];
+        a = v;
+      })
+#undef PG_FOR_ACC
+    }
+    pg_store<0, 0, ACT, 0>(R, O, T, smem);
+    pg_store<0, 1, ACT, 0>(R, O, T, smem);
+    pg_store<1, 0, ACT, 0>(R, O, T, smem);
+    pg_store<1, 1, ACT, 0>(R, O, T, smem);
+  }
+}
+
+// ============================================================================
 // K13 variant 0 (default): 4 waves, one per SIMD, (16 TM) x 128 wave tiles
 // ============================================================================
 // The ping-pong form above keeps a quadrant's 16 MFMAs (256 cycles) per
@@ -1169,6 +1385,59 @@ int pgemm(void* C, const void* A, const void* W, const void* bias, int M, int N,
     case 2: return pg_launch<2, 0>(C_, A_, W_, b_, M, N, K, ia, iw, ic, grid, variant, stream);
     case 3: return pg_launch<3, 0>(C_, A_, W_, b_, M, N, K, ia, iw, ic, grid, variant, stream);
     case 4: return pg_launch<4, 0>(C_, A_, W_, b_, M, N, K, ia, iw, ic, grid, variant, stream);
+  }
+  return -1;
+}
+
+// ---- K13-SK launcher --------------------------------------------------------
+template <int ACT, int EPI>
+static int pg_sk_launch(bf16_t* C, const bf16_t* A, const bf16_t* W, float* slabs, unsigned* cnt,
+                        int M, int N, int K, int lda, int ldw, int ldc, int splits, int grid,
+                        hipStream_t stream) {
+  constexpr size_t smem = PG_RING_B + 16;
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e = hipFuncSetAttribute((const void*)pgemm_sk_kernel<ACT, EPI>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    if (e != hipSuccess) return (int)e;
+    attr = true;
+  }
+  pgemm_sk_kernel<ACT, EPI><<<dim3(grid), dim3(PG_THREADS), smem, stream>>>(
+      C, A, W, slabs, cnt, M, N, K, lda, ldw, ldc, splits);
+  return (int)hipGetLastError();
+}
+
+// epi 0: C = act(A . W^T) bf16 ([M, N/2] for the SwiGLU act 3); splits > 1
+// needs `slabs` >= tiles * splits * 65536 floats and `cnt` >= 2 * tiles zeroed
+// counters (re-armed by the kernel).  epi 2: fp32 partials [splits][M][N] in
+// `slabs` (C unused).
+int pgemm_sk(void* C, const void* A, const void* W, void* slabs, void* cnt, int ncnt, int M,
+             int N, int K, long lda, long ldw, long ldc, int act, int splits, int epi,
+             hipStream_t stream) {
+  if (M <= 0) return 0;
+  if (splits < 1 || N % 256 != 0 || K % (64 * splits) != 0 || K / (64 * splits) < 2) return -1;
+  if (lda % 8 || ldw % 8 || ldc % 4) return -1;
+  if (epi != 0 && epi != 2) return -1;
+  if (act < 0 || act > 4) return -1;
+  if (256L * lda * 2 > 0x7fffffffL || 256L * ldw * 2 > 0x7fffffffL || 256L * ldc * 2 > 0x7fffffffL)
+    return -1;
+  const long tiles = (long)((M + 255) / 256) * (N / 256);
+  if (epi == 2 && (slabs == nullptr || (long)M * N * 4 > 0x7fffffffL)) return -1;
+  if (epi == 0 && splits > 1 && (slabs == nullptr || cnt == nullptr || 2 * tiles > ncnt)) return -1;
+  const int grid = (int)(tiles * splits);
+  auto C_ = (bf16_t*)C;
+  auto A_ = (const bf16_t*)A;
+  auto W_ = (const bf16_t*)W;
+  auto s_ = (float*)slabs;
+  auto c_ = (unsigned*)cnt;
+  const int ia = (int)lda, iw = (int)ldw, ic = (int)ldc;
+  if (epi == 2) return pg_sk_launch<0, 2>(C_, A_, W_, s_, c_, M, N, K, ia, iw, ic, splits, grid, stream);
+  switch (act) {
+    case 0: return pg_sk_launch<0, 0>(C_, A_, W_, s_, c_, M, N, K, ia, iw, ic, splits, grid, stream);
+    case 1: return pg_sk_launch<1, 0>(C_, A_, W_, s_, c_, M, N, K, ia, iw, ic, splits, grid, stream);
+    case 2: return pg_sk_launch<2, 0>(C_, A_, W_, s_, c_, M, N, K, ia, iw, ic, splits, grid, stream);
+    case 3: return pg_sk_launch<3, 0>(C_, A_, W_, s_, c_, M, N, K, ia, iw, ic, splits, grid, stream);
+    case 4: return pg_sk_launch<4, 0>(C_, A_, W_, s_, c_, M, N, K, ia, iw, ic, splits, grid, stream);
   }
   return -1;
 }

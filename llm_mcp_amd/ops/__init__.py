@@ -614,9 +614,15 @@ def linear(x: torch.Tensor, w: torch.Tensor, defer: bool = False,
     if x.is_cuda and x.dim() == 2:
         M, N, K = x.shape[0], w.shape[0], w.shape[1]
         if defer and bias is None:
+            s = sk_choice(M, N, K, epi=2)
+            if s is not None and pgemm_operands_ok(x, w):
+                return pgemm_sk(x, w, s, epi=2)
             ch = dgemm_choice(M, N, K, epi=2)
             if ch is not None:
                 return dgemm_partials(x, w, ch[0], ch[1])
+        s = sk_choice(M, N, K) if bias is None else None
+        if s is not None and pgemm_operands_ok(x, w):
+            return pgemm_sk(x, w, s)
         ch = dgemm_choice(M, N, K)
         y = None
         if ch is not None:
@@ -642,6 +648,9 @@ def linear_swiglu(x: torch.Tensor, w: torch.Tensor, block: int) -> torch.Tensor:
     the LDS hand-off form (epi 1, tile BN = 2 * block)."""
     if x.is_cuda and x.dim() == 2:
         if block == SWIGLU16:
+            s = sk_choice(x.shape[0], w.shape[0], w.shape[1], epi=3)
+            if s is not None and pgemm_operands_ok(x, w):
+                return pgemm_sk(x, w, s, act=ACT_SWIGLU)   # K13-SK, SwiGLU epilogue
             ch = dgemm_choice(x.shape[0], w.shape[0], w.shape[1], epi=3)
             if ch is not None:
                 return dgemm(x, w, ch[0], ch[1], epi=3)
@@ -659,7 +668,7 @@ def swiglu_block(N: int, K: int) -> int:
     """Interleave block of the gate|up weights for the fused decode GEMM of
     this shape: 16 when the table has in-register-epilogue (epi 3) entries,
     else BN/2 of the measured epi-1 configurations; 0 = not fused."""
-    if any(cfg >= 0 for m, cfg, s in _dg_table().get((N, K, 3), ())):
+    if any(cfg >= 0 for m, cfg, s in _dg_table().get((N, K, 3), ())) or _sk_table().get((N, K, 3)):
         return SWIGLU16
     bns = {DGEMM_CONFIGS[cfg & DGEMM_CFG_MASK][1]
            for m, cfg, s in _dg_table().get((N, K, 1), ()) if cfg >= 0}
@@ -801,6 +810,39 @@ def large_gemm_backend(M: int, N: int, K: int, act: int = 0, bias: bool = False)
     if e.get(mine) is None or e.get(lib) is None:
         return "k13"
     return "k13" if e[mine] >= e[lib] else "lib"
+
+
+_SK_TABLE: dict | None = None
+
+
+def _sk_table() -> dict:
+    """Measured K13-SK dispatch: {(N, K, epi): [(m_min, m_max, splits), ...]}
+    from config/dgemm_gfx950.json "sk" (tools/pgemm_sk_probe.py: shapes and
+    batch ranges where the split-K 256x256 tile beat K11 / hipBLASLt).  epi 0
+    plain, 2 partials for the residual-add RMSNorm, 3 SwiGLU (16-row gate/up
+    interleave).  LMX_DGEMM=0 or LMX_SK=0 disables."""
+    global _SK_TABLE
+    if _SK_TABLE is None:
+        import json
+        import os
+        _SK_TABLE = {}
+        path = os.environ.get("LMX_DGEMM_TABLE") or os.path.join(
+            os.path.dirname(os.path.dirname(__file__)), "config", "dgemm_gfx950.json")
+        if (os.environ.get("LMX_DGEMM", "1") == "1" and os.environ.get("LMX_SK", "1") == "1"
+                and os.path.exists(path)):
+            with open(path) as f:
+                for e in json.load(f).get("sk", []):
+                    _SK_TABLE.setdefault((int(e["N"]), int(e["K"]), int(e.get("epi", 0))), []).append(
+                        (int(e["m_min"]), int(e["m_max"]), int(e["splits"])))
+    return _SK_TABLE
+
+
+def sk_choice(M: int, N: int, K: int, epi: int = 0) -> int | None:
+    """Split count of K13-SK for this decode GEMM, or None."""
+    for m_min, m_max, s in _sk_table().get((N, K, epi), ()):
+        if m_min <= M <= m_max and pgemm_sk_supported(M, N, K, s):
+            return s
+    return None
 
 
 def dgemm_choice(M: int, N: int, K: int, epi: int = 0) -> tuple[int, int] | None:
@@ -1029,4 +1071,66 @@ def pgemm(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, ac
     native().pgemm(_ptr(out), _ptr(a), _ptr(w), _ptr(bias), M, N, K, a.stride(0), w.stride(0),
                    out.stride(0), act, grid, PGEMM_VARIANT if variant is None else variant,
                    _stream())
+    return out
+
+
+_PG_WS: dict = {}
+_PG_CNT = 4096
+
+
+def _pg_workspace(dev: torch.device, n_floats: int):
+    key = (dev.index, _stream())
+    ws = _PG_WS.get(key)
+    if ws is None or ws[0].numel() < n_floats:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("pgemm_sk workspace must be allocated before graph capture "
+                               "(run the shape once eagerly)")
+        n_floats = max(n_floats, ws[0].numel() if ws else 0, 1 << 20)
+        cnt = ws[1] if ws else torch.zeros(_PG_CNT, dtype=torch.int32, device=dev)
+        ws = (torch.empty(n_floats, dtype=torch.float32, device=dev), cnt)
+        _PG_WS[key] = ws
+    return ws
+
+
+def pgemm_sk_supported(M: int, N: int, K: int, splits: int) -> bool:
+    """Shapes K13-SK takes: 256-column tiles, >= 2 64-deep K-steps per slice."""
+    return (0 < M and N % 256 == 0 and splits >= 1 and K % (64 * splits) == 0
+            and K // (64 * splits) >= 2 and 2 * (-(-M // 256)) * (N // 256) <= _PG_CNT)
+
+
+def pgemm_sk(a: torch.Tensor, w: torch.Tensor, splits: int, act: int = 0, epi: int = 0,
+             out: torch.Tensor | None = None):
+    """act(a @ w^T) on K13-SK (the 256x256 ping-pong tile, split-K over
+    ``splits`` slices, one workgroup per (slice, tile)): the decode-batch form
+    (M <= 256).  epi 0: bf16 [M, N] ([M, N/2] for ACT_SWIGLU with ``w`` from
+    ``interleave_gate_up(w, 16)``), slices combined in-kernel; epi 2: fp32
+    ``Partials`` [splits, M, N] summed by ``rms_norm(..., residual=)``."""
+    M, K = a.shape
+    N = w.shape[0]
+    _chk(pgemm_sk_supported(M, N, K, splits), f"pgemm_sk shape M={M} N={N} K={K} S={splits}")
+    if not a.is_cuda:
+        if epi == 2:
+            y = (a.float() @ w.float().t()).unsqueeze(0)
+            p = torch.cat([y] + [torch.zeros_like(y)] * (splits - 1))
+            return Partials(p, splits, M, N)
+        return pgemm(a, w, act=act, out=out)
+    _bf16(a, "a"); _bf16(w, "w")
+    _chk(w.shape[1] == K and pgemm_operands_ok(a, w), "pgemm_sk operands need 16-B aligned rows")
+    tiles = -(-M // 256) * (N // 256)
+    PGEMM_CALLS[0] += 1
+    if epi == 2:
+        slabs, cnt = _pg_workspace(a.device, splits * M * N)
+        native().pgemm_sk(0, _ptr(a), _ptr(w), _ptr(slabs), _ptr(cnt), _PG_CNT, M, N, K,
+                          a.stride(0), w.stride(0), N, 0, splits, 2, _stream())
+        return Partials(slabs[:splits * M * N].view(splits, M, N), splits, M, N)
+    ncols = N // 2 if act == ACT_SWIGLU else N
+    if out is None:
+        out = torch.empty((M, ncols), dtype=a.dtype, device=a.device)
+    _chk(out.shape == (M, ncols) and out.stride(1) == 1 and out.stride(0) % 8 == 0
+         and out.data_ptr() % 16 == 0, "pgemm_sk output layout")
+    slabs = cnt = None
+    if splits > 1:
+        slabs, cnt = _pg_workspace(a.device, tiles * splits * 65536)
+    native().pgemm_sk(_ptr(out), _ptr(a), _ptr(w), _ptr(slabs), _ptr(cnt), _PG_CNT, M, N, K,
+                      a.stride(0), w.stride(0), out.stride(0), act, splits, 0, _stream())
     return out

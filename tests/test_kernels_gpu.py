@@ -693,6 +693,41 @@ def test_pgemm_vs_fp32(M, N, K, grid, variant):
     assert ops.PGEMM_CALLS[0] - before == 6
 
 
+@pytest.mark.parametrize("M,N,K", [(256, 1024, 4096), (200, 768, 1536), (37, 512, 512),
+                                   (300, 512, 1024)])
+@pytest.mark.parametrize("splits", [1, 2, 3, 4])
+def test_pgemm_sk_vs_fp32(M, N, K, splits):
+    """K13-SK (split-K 256x256 decode tile): in-kernel ticketed combine (plain,
+    GELU, 16-row SwiGLU), the fp32 partials form summed by the norm, ragged M,
+    repeated calls (counters re-armed), bitwise deterministic."""
+    if not ops.pgemm_sk_supported(M, N, K, splits):
+        pytest.skip("shape outside K13-SK")
+    a = _bf(M, K)
+    w = _bf(N, K, scale=K ** -0.5)
+    y = a.float() @ w.float().t()
+    out = ops.pgemm_sk(a, w, splits)
+    torch.testing.assert_close(out.float(), y, atol=2e-2, rtol=2e-2)
+    for _ in range(3):
+        assert torch.equal(out, ops.pgemm_sk(a, w, splits))
+    torch.testing.assert_close(ops.pgemm_sk(a, w, splits, act=ops.ACT_GELU).float(),
+                               torch.nn.functional.gelu(y, approximate="tanh"), atol=2e-2, rtol=2e-2)
+    wil = ops.interleave_gate_up(w, 16)
+    g = torch.nn.functional.silu(y[:, :N // 2]) * y[:, N // 2:]
+    torch.testing.assert_close(ops.pgemm_sk(a, wil, splits, act=ops.ACT_SWIGLU).float(), g,
+                               atol=2e-2, rtol=2e-2)
+    p = ops.pgemm_sk(a, w, splits, epi=2)
+    assert p.slabs.shape == (splits, M, N)
+    torch.testing.assert_close(p.sum(), y, atol=2e-3, rtol=2e-3)
+    # through the residual-add RMSNorm that consumes partials
+    res = _bf(M, N)
+    nw = _bf(N)
+    ref_res = res.float() + y
+    ref_out = ref_res * torch.rsqrt(ref_res.pow(2).mean(-1, keepdim=True) + 1e-5) * nw.float()
+    got = ops.rms_norm(p, nw, 1e-5, residual=res)
+    torch.testing.assert_close(res.float(), ref_res, atol=3e-2, rtol=2e-2)
+    torch.testing.assert_close(got.float(), ref_out, atol=5e-2, rtol=3e-2)
+
+
 def test_linear_large_m_runs_k13(monkeypatch):
     """Prefill-sized projections: ops.linear / linear_swiglu route M >= 512 to
     K13 (LMX_LARGE_GEMM=k13), bias and the 16-row gate/up SwiGLU included,
