@@ -788,6 +788,7 @@ def encoder_backend(N: int, K: int, act: int = 0,
 
 
 PGEMM_MIN_M = 512          # below: the decode-sized paths (K11 / split-K / library)
+PGEMM_LIB_MARGIN = 0.05    # "auto": hipBLASLt only where measured > 5 % faster than K13
 
 
 def large_gemm_backend(M: int, N: int, K: int, act: int = 0, bias: bool = False) -> str:
@@ -795,7 +796,11 @@ def large_gemm_backend(M: int, N: int, K: int, act: int = 0, bias: bool = False)
     "k13" / "lib" force one; "auto" (default) takes the faster of the two in
     the encoder table (config/dgemm_gfx950.json "encoder": k13_tflops vs
     lib_tflops, or k13_swiglu_tflops vs lib_glu_tflops for the fused SwiGLU
-    form) and K13 for unmeasured shapes."""
+    form) -- the library only where it is more than PGEMM_LIB_MARGIN faster,
+    since K13 also removes the neighbouring elementwise passes (a whole
+    headline bench with every prefill projection on K13 measured 16,142 vs
+    15,995 tok/s all-library, profiles/r3_k13_and_decode_sk.md) -- and K13 for
+    unmeasured shapes."""
     import os
     if M < PGEMM_MIN_M or not pgemm_supported(N, K, act, bias):
         return "lib"
@@ -809,7 +814,7 @@ def large_gemm_backend(M: int, N: int, K: int, act: int = 0, bias: bool = False)
                  else ("k13_tflops", "lib_tflops"))
     if e.get(mine) is None or e.get(lib) is None:
         return "k13"
-    return "k13" if e[mine] >= e[lib] else "lib"
+    return "k13" if e[mine] >= (1.0 - PGEMM_LIB_MARGIN) * e[lib] else "lib"
 
 
 _SK_TABLE: dict | None = None
@@ -840,7 +845,8 @@ def _sk_table() -> dict:
 def sk_choice(M: int, N: int, K: int, epi: int = 0) -> int | None:
     """Split count of K13-SK for this decode GEMM, or None."""
     for m_min, m_max, s in _sk_table().get((N, K, epi), ()):
-        if m_min <= M <= m_max and pgemm_sk_supported(M, N, K, s):
+        if (m_min <= M <= m_max and pgemm_sk_supported(M, N, K, s)
+                and (epi != 2 or s in (1, 2, 4, 8, 16))):     # rmsnorm_slabs' S
             return s
     return None
 

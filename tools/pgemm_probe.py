@@ -25,7 +25,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--only", default="")
     ap.add_argument("--grid", type=int, default=0)
-    ap.add_argument("--variant", type=int, default=0)
+    ap.add_argument("--variant", type=int, default=None, help="default: ops.PGEMM_VARIANT")
     a = ap.parse_args()
     ops.native()
     torch.manual_seed(0)
