@@ -109,10 +109,10 @@ __device__ __forceinline__ void process_page(PageState<HD>& st, const bf16x8_t (
   const float m_new = fmaxf(st.m, mx);
   // a column may see no visible key in this page (causal tail): keep its state
   const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
-  const float alpha = exp2f(st.m - m_use);
+  const float alpha = fast_exp2(st.m - m_use);
   float p[8], rs = 0.f;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) { p[j] = exp2f(x[j] - m_use); rs += p[j]; }
+  for (int j = 0; j < 8; ++j) { p[j] = fast_exp2(x[j] - m_use); rs += p[j]; }
   rs += __shfl_xor(rs, 16, 64);
   rs += __shfl_xor(rs, 32, 64);
   st.l = st.l * alpha + rs;
@@ -174,10 +174,10 @@ __device__ __forceinline__ void compute_page(PageState<HD>& st, const bf16x8_t (
   mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
   const float m_new = fmaxf(st.m, mx);
   const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
-  const float alpha = exp2f(st.m - m_use);
+  const float alpha = fast_exp2(st.m - m_use);
   float p[8], rs = 0.f;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) { p[j] = exp2f(x[j] - m_use); rs += p[j]; }
+  for (int j = 0; j < 8; ++j) { p[j] = fast_exp2(x[j] - m_use); rs += p[j]; }
   rs += __shfl_xor(rs, 16, 64);
   rs += __shfl_xor(rs, 32, 64);
   st.l = st.l * alpha + rs;
@@ -434,7 +434,7 @@ __device__ __forceinline__ void decode_segment(
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
       const float mw = sm_ml[w][h][0];
-      const float f = (mw == -INFINITY) ? 0.f : exp2f(mw - M);
+      const float f = (mw == -INFINITY) ? 0.f : fast_exp2(mw - M);
       L += sm_ml[w][h][1] * f;
       O += sm_o[w][h][d] * f;
     }
@@ -507,7 +507,7 @@ __global__ void __launch_bounds__(128) paged_decode_reduce_kernel(
   for (int p = 0; p < nparts; ++p) M = fmaxf(M, part_ml[(base + p) * 2]);
   float L = 0.f, O = 0.f;
   for (int p = 0; p < nparts; ++p) {
-    const float f = exp2f(part_ml[(base + p) * 2] - M);
+    const float f = fast_exp2(part_ml[(base + p) * 2] - M);
     L += part_ml[(base + p) * 2 + 1] * f;
     O += part_o[(base + p) * HD + d] * f;
   }
@@ -631,24 +631,27 @@ __device__ __forceinline__ bf16x8_t pf_vfrag(const bf16_t* vpg, int d, int g) {
   return load_frag_2x8B(p0, p1);
 }
 
-// DMA one 32-token page of K and of V into the LDS tile slot `pslot`.
-template <int HD>
+// DMA one 32-token page of K and of V into the LDS tile slot `pslot`
+// (PW waves: 64 PW x 8 elements per instruction).
+template <int HD, int PW>
 __device__ __forceinline__ void pf_stage_page(bf16_t* k_lds, bf16_t* v_lds,
                                               const bf16_t* __restrict__ kp,
                                               const bf16_t* __restrict__ vp) {
   const int tid = threadIdx.x, wave = tid >> 6;
   constexpr int PAGE = BS * HD;            // elements per page
+  constexpr int PER = 512 * PW;            // elements per instruction of the workgroup
+  static_assert(PAGE % PER == 0, "a page is whole DMA instructions");
 #pragma unroll
-  for (int j = 0; j < PAGE / 2048; ++j) {  // 2048 elements = 4 KB per instruction
-    const int off = j * 2048 + tid * 8;
+  for (int j = 0; j < PAGE / PER; ++j) {
+    const int off = j * PER + tid * 8;
     // K: row = key, 16-B chunk position swizzled by the row
     const int kr = off / HD, kpos = (off % HD) / 8;
-    pf_glds16(kp + kr * HD + 8 * (kpos ^ kswz<HD>(kr)), k_lds + j * 2048 + wave * 512);
+    pf_glds16(kp + kr * HD + 8 * (kpos ^ kswz<HD>(kr)), k_lds + j * PER + wave * 512);
     // V: key-quad page [BS/4][HD][4]; LDS chunk (quad q, slot pp) holds the
     // global chunk d = 2p, 2p+1 with p = pp ^ vswz(q) (conflict-free 8-B
     // fragment reads, pf_vfrag)
     const int ch = off / 8, q = ch / (HD / 2), pp = ch % (HD / 2);
-    pf_glds16(vp + ((long)q * HD + 2 * (pp ^ pf_vswz(q))) * 4, v_lds + j * 2048 + wave * 512);
+    pf_glds16(vp + ((long)q * HD + 2 * (pp ^ pf_vswz(q))) * 4, v_lds + j * PER + wave * 512);
   }
 }
 
@@ -661,20 +664,34 @@ __device__ __forceinline__ void pf_vmwait() {
 // flight while the current tile computes, drained (vmcnt 0) at the next
 // barrier.  NST = 3: two tiles in flight across a raw s_barrier with a counted
 // vmcnt (cdna guide §5 "Pipelining across barriers").
-template <int HD, int NST, int PF_NG = pf_groups<HD>()>
-__global__ void __launch_bounds__(256, 2) paged_prefill_kernel(
+// PW: waves per workgroup.  4 (two workgroups per CU) or 8 (one workgroup per
+// CU, same waves per SIMD and registers per wave): 8 waves serve twice the
+// queries from one K/V tile, so the tiles a (sequence, kv head) streams from
+// L2 / HBM into LDS are moved half as often -- the short causal walks of a
+// GQA prefill chunk (32 queries per 4-wave workgroup at G = 4) are bound by
+// that tile latency, not by the MFMAs.
+template <int HD, int NST, int PW = 4, int PF_NG = pf_groups<HD>()>
+__global__ void __launch_bounds__(64 * PW, 8 / PW) paged_prefill_kernel(
     const bf16_t* __restrict__ q, long q_stride, const bf16_t* __restrict__ k_cache,
     const bf16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ cu_q, const int* __restrict__ context_lens,
     const int* __restrict__ tiles, bf16_t* __restrict__ out, long out_stride, int Hq, int Hkv,
-    float scale, int causal, float rescale_thr) {
+    float scale, int causal, float rescale_thr, int xcd) {
   extern __shared__ __attribute__((aligned(16))) char pf_smem[];
   constexpr int PAGE = BS * HD;
   // buffer b: K pages at b*4*PAGE + {0, PAGE}, V pages at b*4*PAGE + 2*PAGE + {0, PAGE}
   bf16_t* const lds = reinterpret_cast<bf16_t*>(pf_smem);
   constexpr int KS = HD / 32, NT = HD / 16;
 
-  const int tile = blockIdx.x, kvh = blockIdx.y;
+  // XCD-aware order: the workgroups of one (kv head, sequence) -- its query
+  // tiles, which all stream the same K/V pages -- are consecutive logical ids
+  // and xcd_remap puts consecutive ids on one XCD, so the pages are read from
+  // HBM into that XCD's L2 once instead of once per XCD (hardware hands
+  // linear workgroup b to XCD b % 8)
+  const int nwg = gridDim.x * gridDim.y;
+  const int lin0 = blockIdx.x + blockIdx.y * gridDim.x;
+  const int lin = xcd ? xcd_remap(lin0, nwg) : lin0;
+  const int tile = lin % gridDim.x, kvh = lin / gridDim.x;
   const int seq = tiles[2 * tile], q_start = tiles[2 * tile + 1];
   // queries per 16-lane column group; with G not dividing 16 (e.g. Qwen2.5's
   // 7) the last 16 - QG*G lanes of a group are idle
@@ -682,7 +699,7 @@ __global__ void __launch_bounds__(256, 2) paged_prefill_kernel(
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, c = lane & 15, g = lane >> 4;
   const int qbeg = cu_q[seq], qlen = cu_q[seq + 1] - qbeg;
   const int ctx = context_lens[seq];
-  const int wg_q1 = min(q_start + 4 * PF_NG * QG, qlen);   // one past the WG's last query
+  const int wg_q1 = min(q_start + PW * PF_NG * QG, qlen);  // one past the WG's last query
   const int wg_lim = causal ? (ctx - qlen + wg_q1 - 1) : (ctx - 1);
   const int ntiles = wg_lim / PF_TK + 1;
   const int last_page = (ctx - 1) / BS;
@@ -699,25 +716,55 @@ __global__ void __launch_bounds__(256, 2) paged_prefill_kernel(
     valid[n] = c < QG * G && qi[n] < qlen;
     lim[n] = valid[n] ? (causal ? (ctx - qlen + qi[n]) : (ctx - 1)) : -1;
   }
+  auto stage = [&](int t, int buf) {
+#pragma unroll
+    for (int pp = 0; pp < 2; ++pp) {
+      const int pg = min(2 * t + pp, last_page);
+      const long blk = bt[pg];
+      const bf16_t* kp = k_cache + (blk * Hkv + kvh) * PAGE;
+      const bf16_t* vp = v_cache + (blk * Hkv + kvh) * PAGE;
+      bf16_t* base = lds + buf * 4 * PAGE;
+      pf_stage_page<HD, PW>(base + pp * PAGE, base + 2 * PAGE + pp * PAGE, kp, vp);
+    }
+  };
+  // LDS-DMA instructions per thread per tile (2 pages x K and V)
+  constexpr int LPS = 4 * (PAGE / (512 * PW));
+
   // Q fragments through LDS (one image row per column: [wave][n][c][HD]) by
   // LDS-DMA, not plain loads: an ordinary global load whose result the tile
   // loop consumes makes hipcc drain the whole DMA ring (vmcnt 0) before the
-  // first MFMA of EVERY tile (guide §5 item 4b); the image borrows the ring
-  // slots before the prologue fills them.
+  // first MFMA of EVERY tile (guide §5 item 4b).  The image borrows the first
+  // QSL ring slots; K/V tile t lives in slot (t + QSL) % NST, so the first
+  // NST - QSL tiles are staged into the other slots while Q is still in
+  // flight (the Q and tile-0 latencies overlap instead of adding up at the
+  // start of every workgroup: ~5 tiles per workgroup on a 546-token causal
+  // chunk).
+  constexpr int QROWS = PW * PF_NG * 16, QCH = HD / 8;  // rows, 16-B chunks per row
+  constexpr int QSL = (QROWS * HD + 4 * PAGE - 1) / (4 * PAGE);
+  constexpr int EARLY = NST - QSL;                       // tiles staged under the Q load
+  static_assert(QSL <= NST, "Q image fits the ring");
   {
-    constexpr int QROWS = 4 * PF_NG * 16, QCH = HD / 8;   // rows, 16-B chunks per row
-    static_assert(QROWS * HD <= NST * 4 * PAGE, "Q image fits the ring");
 #pragma unroll
-    for (int j = 0; j < QROWS * QCH / 256; ++j) {
-      const int e = j * 256 + threadIdx.x, row = e / QCH, ch = e % QCH;
+    for (int j = 0; j < QROWS * QCH / (64 * PW); ++j) {
+      const int e = j * 64 * PW + threadIdx.x, row = e / QCH, ch = e % QCH;
       const int rw = row / (PF_NG * 16), rn = (row / 16) % PF_NG, rc = row % 16;
       const int rq = q_start + (rw * PF_NG + rn) * QG + rc / G;
       const bool ok = rc < QG * G && rq < qlen;
       const bf16_t* src = q + (long)(qbeg + (ok ? rq : 0)) * q_stride +
                           (long)(kvh * G + (ok ? rc % G : 0)) * HD + 8 * ch;
-      pf_glds16(src, lds + j * 2048 + wave * 512);
+      pf_glds16(src, lds + j * 512 * PW + wave * 512);
     }
-    pf_vmwait<0>();
+#pragma unroll
+    for (int p = 0; p < EARLY && p < NST - 1; ++p)
+      if (p < ntiles) stage(p, (p + QSL) % NST);
+    // Q landed: only the early tiles' DMA (issued after it) may remain
+    if constexpr (EARLY >= 2) {
+      if (ntiles >= 2) pf_vmwait<2 * LPS>(); else pf_vmwait<LPS>();
+    } else if constexpr (EARLY == 1) {
+      pf_vmwait<LPS>();
+    } else {
+      pf_vmwait<0>();
+    }
     __builtin_amdgcn_s_barrier();
 #pragma unroll
     for (int n = 0; n < PF_NG; ++n) {
@@ -751,31 +798,17 @@ __global__ void __launch_bounds__(256, 2) paged_prefill_kernel(
   }
   const float scale_log2 = scale * LOG2E;
 
-  auto stage = [&](int t, int buf) {
 #pragma unroll
-    for (int pp = 0; pp < 2; ++pp) {
-      const int pg = min(2 * t + pp, last_page);
-      const long blk = bt[pg];
-      const bf16_t* kp = k_cache + (blk * Hkv + kvh) * PAGE;
-      const bf16_t* vp = v_cache + (blk * Hkv + kvh) * PAGE;
-      bf16_t* base = lds + buf * 4 * PAGE;
-      pf_stage_page<HD>(base + pp * PAGE, base + 2 * PAGE + pp * PAGE, kp, vp);
-    }
-  };
-
-  // LDS-DMA instructions per thread per tile (2 pages x K and V)
-  constexpr int LPS = 4 * (PAGE / 2048);
-#pragma unroll
-  for (int p = 0; p < NST - 1; ++p)
-    if (p < ntiles) stage(p, p);
+  for (int p = EARLY; p < NST - 1; ++p)    // the rest of the prologue, into the Q slots
+    if (p < ntiles) stage(p, (p + QSL) % NST);
   for (int t = 0; t < ntiles; ++t) {
-    const int buf = t % NST;
+    const int buf = (t + QSL) % NST;
     // tile t landed once at most the tiles issued after it remain in flight
     if (t + NST - 2 < ntiles) pf_vmwait<(NST - 2) * LPS>(); else pf_vmwait<0>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();    // raw: a __syncthreads fence would drain the ring
     // refill the slot every wave finished reading at t - 1
-    if (t + NST - 1 < ntiles) stage(t + NST - 1, (t + NST - 1) % NST);
+    if (t + NST - 1 < ntiles) stage(t + NST - 1, (t + NST - 1 + QSL) % NST);
     if (wave_idle) continue;
     const bf16_t* kt = lds + buf * 4 * PAGE;
     const bf16_t* vt = kt + 2 * PAGE;
@@ -808,34 +841,52 @@ __global__ void __launch_bounds__(256, 2) paged_prefill_kernel(
     // column, 1 for the ones that did not grow).
     const bool need_mask = key0 + PF_TK - 1 > wave_lo;
     bf16x8_t pf[PF_NG][2];
+    // fp32 pairs (v_pk_fma_f32 / v_pk_add_f32 on the exp argument and the row
+    // sum, half the VALU issue of the scalar form); the causal mask only on
+    // the tiles that cross a column limit (wave-uniform branch)
+    typedef float f32x2_t __attribute__((ext_vector_type(2)));
 #pragma unroll
     for (int n = 0; n < PF_NG; ++n) {
-      float x[16];
+      f32x2_t x[8];                                      // x[2 kb + h] = keys 16 kb + 4 g + 2 h + {0, 1}
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = key0 + kb * 16 + 4 * g + r;
-          x[4 * kb + r] = (!need_mask || key <= lim[n]) ? s[n][kb][r] : -INFINITY;
-        }
-      float mx = x[0];
+        for (int h = 0; h < 2; ++h) x[2 * kb + h] = f32x2_t{s[n][kb][2 * h], s[n][kb][2 * h + 1]};
+      if (need_mask) {
 #pragma unroll
-      for (int j = 1; j < 16; ++j) mx = fmaxf(mx, x[j]);
+        for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int key = key0 + kb * 16 + 4 * g + r;
+            if (key > lim[n]) x[2 * kb + (r >> 1)][r & 1] = -INFINITY;
+          }
+      }
+      float mx = fmaxf(x[0].x, x[0].y);
+#pragma unroll
+      for (int j = 1; j < 8; ++j) mx = fmaxf(mx, fmaxf(x[j].x, x[j].y));
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float mx2 = mx * scale_log2;                 // -inf stays -inf (scale > 0)
       if (__ballot(mx2 > m[n] + rescale_thr)) {
         const float m_new = fmaxf(m[n], mx2);
-        const float alpha = (m_new == -INFINITY) ? 1.f : exp2f(m[n] - m_new);
+        const float alpha = (m_new == -INFINITY) ? 1.f : fast_exp2(m[n] - m_new);
         l[n] *= alpha;
 #pragma unroll
         for (int i = 0; i < NT; ++i) acc[n][i] *= alpha;
         m[n] = m_new;
       }
       const float m_use = (m[n] == -INFINITY) ? 0.f : m[n];
-      float rs = 0.f;
+      const f32x2_t sc2 = {scale_log2, scale_log2}, nm2 = {-m_use, -m_use};
+      f32x2_t rs2 = {0.f, 0.f};
 #pragma unroll
-      for (int j = 0; j < 16; ++j) { x[j] = exp2f(fmaf(x[j], scale_log2, -m_use)); rs += x[j]; }
+      for (int j = 0; j < 8; ++j) {
+        f32x2_t y = x[j] * sc2 + nm2;
+        y.x = fast_exp2(y.x);
+        y.y = fast_exp2(y.y);
+        x[j] = y;
+        rs2 += y;
+      }
+      float rs = rs2.x + rs2.y;
       rs += __shfl_xor(rs, 16, 64);
       rs += __shfl_xor(rs, 32, 64);
       l[n] += rs;
@@ -843,7 +894,11 @@ __global__ void __launch_bounds__(256, 2) paged_prefill_kernel(
 #pragma unroll
       for (int pp = 0; pp < 2; ++pp)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) pf[n][pp][j] = (short)f2bf(x[8 * pp + j]);
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t w = pack_bf16x2(x[4 * pp + j].x, x[4 * pp + j].y);
+          pf[n][pp][2 * j] = (short)(w & 0xffff);
+          pf[n][pp][2 * j + 1] = (short)(w >> 16);
+        }
     }
     // O^T += V^T . P^T
 #pragma unroll
@@ -880,36 +935,51 @@ void set_prefill_rescale_thr(float thr) { g_prefill_rescale_thr = thr; }
 // LDS ring slots of the prefill kernel (0: default per head dim; 2 or 3: A/B knob)
 static int g_prefill_stages = 0;
 void set_prefill_stages(int n) { g_prefill_stages = (n == 2 || n == 3) ? n : 0; }
+// XCD-aware workgroup order of the prefill kernel (1, default) or hardware order (0: A/B knob)
+static int g_prefill_xcd = 1;
+void set_prefill_xcd(int on) { g_prefill_xcd = on ? 1 : 0; }
 
+// q_per_tile: the tile list's queries per workgroup (ops.prefill_q_per_tile);
+// it selects the workgroup width PW = q_per_tile / (column groups x 16/G):
+// 4 or 8 waves (8 only at head dim 128)
 int paged_prefill(const void* q, long q_stride, const void* k_cache, const void* v_cache,
                   const int* block_tables, int bt_stride, const int* cu_q,
                   const int* context_lens, const int* tiles, int num_tiles, void* out,
                   long out_stride, int Hq, int Hkv, int D, int block_size, float scale,
-                  int causal, hipStream_t stream) {
+                  int causal, int q_per_tile, hipStream_t stream) {
   if (num_tiles <= 0) return 0;
   if ((D != 128 && D != 64) || block_size != BS) return -1;
   if (Hq % Hkv != 0 || Hq / Hkv > 16) return -2;
-#define LMX_PRE(HDV, NSTV)                                                                    \
+  const int per_wave = (D == 128 ? pf_groups<128>() : pf_groups<64>()) * (16 / (Hq / Hkv));
+  const int pw = q_per_tile / per_wave;
+  if (q_per_tile % per_wave != 0 || (pw != 4 && pw != 8) || (pw == 8 && D != 128)) return -3;
+#define LMX_PRE(HDV, NSTV, PWV)                                                               \
   {                                                                                           \
     constexpr int smem = NSTV * 4 * BS * HDV * 2;                                             \
     static bool attr = false;                                                                 \
     if (smem > 65536 && !attr) {                                                              \
-      (void)hipFuncSetAttribute((const void*)paged_prefill_kernel<HDV, NSTV>,                 \
+      (void)hipFuncSetAttribute((const void*)paged_prefill_kernel<HDV, NSTV, PWV>,            \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, smem);            \
       attr = true;                                                                            \
     }                                                                                         \
-    paged_prefill_kernel<HDV, NSTV><<<dim3(num_tiles, Hkv), dim3(256), smem, stream>>>(       \
+    paged_prefill_kernel<HDV, NSTV, PWV><<<dim3(num_tiles, Hkv), dim3(64 * PWV), smem,        \
+                                           stream>>>(                                         \
         (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache,           \
         block_tables, bt_stride, cu_q, context_lens, tiles, (bf16_t*)out, out_stride, Hq, Hkv, \
-        scale, causal, g_prefill_rescale_thr);                                                \
+        scale, causal, g_prefill_rescale_thr, g_prefill_xcd);                                 \
   }
   // 2 slots by default: 3 measured equal at D = 64 and 1.55x slower at D = 128
-  // (96 KB of LDS leaves one workgroup per CU) -- tools/prefill_attn_probe.py
+  // with 4-wave workgroups (96 KB of LDS leaves one workgroup per CU) --
+  // tools/prefill_attn_probe.py; the 8-wave form is one workgroup per CU anyway
   const int nst = g_prefill_stages ? g_prefill_stages : 2;
   if (D == 128) {
-    if (nst == 3) LMX_PRE(128, 3) else LMX_PRE(128, 2)
+    if (pw == 8) {
+      if (nst == 3) LMX_PRE(128, 3, 8) else LMX_PRE(128, 2, 8)
+    } else {
+      if (nst == 3) LMX_PRE(128, 3, 4) else LMX_PRE(128, 2, 4)
+    }
   } else {
-    if (nst == 3) LMX_PRE(64, 3) else LMX_PRE(64, 2)
+    if (nst == 3) LMX_PRE(64, 3, 4) else LMX_PRE(64, 2, 4)
   }
 #undef LMX_PRE
   return (int)hipGetLastError();

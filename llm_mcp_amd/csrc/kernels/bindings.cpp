@@ -24,12 +24,13 @@ void set_decode_mode(int);
 void set_slab_norm_threads(int);
 void set_prefill_rescale_thr(float);
 void set_prefill_stages(int);
+void set_prefill_xcd(int);
 int paged_decode(const void*, long, const void*, const void*, const int*, int, const int*,
                  const int*, void*,
                  long, float*, float*, int, int, int, int, int, float, int, int, const int*,
                  const float*, const int*, hipStream_t);
 int paged_prefill(const void*, long, const void*, const void*, const int*, int, const int*,
-                  const int*, const int*, int, void*, long, int, int, int, int, float, int,
+                  const int*, const int*, int, void*, long, int, int, int, int, float, int, int,
                   hipStream_t);
 int sample(const void*, int, long, int, int, const float*, const int*, const float*,
            const uint64_t*, const int*, int*, float*, int, hipStream_t);
@@ -133,13 +134,16 @@ PYBIND11_MODULE(_lmx_kernels, m) {
         "prefill softmax: raise the running max only past this many log2 units (0: always)");
   m.def("set_prefill_stages", [](int n) { lmx::set_prefill_stages(n); },
         "prefill attention LDS ring slots: 0 default per head dim, 2 or 3");
+  m.def("set_prefill_xcd", [](int on) { lmx::set_prefill_xcd(on); },
+        "prefill attention workgroup order: 1 XCD-aware (default), 0 hardware order");
   m.def("paged_prefill", [](uptr q, long q_stride, uptr kc, uptr vc, uptr bt, int bt_stride,
                             uptr cu_q, uptr ctx, uptr tiles, int num_tiles, uptr out,
                             long out_stride, int Hq, int Hkv, int D, int BS, float scale,
-                            int causal, uptr stream) {
+                            int causal, int q_per_tile, uptr stream) {
     check(lmx::paged_prefill(P<void>(q), q_stride, P<void>(kc), P<void>(vc), P<int>(bt),
                              bt_stride, P<int>(cu_q), P<int>(ctx), P<int>(tiles), num_tiles,
-                             P<void>(out), out_stride, Hq, Hkv, D, BS, scale, causal, S(stream)),
+                             P<void>(out), out_stride, Hq, Hkv, D, BS, scale, causal, q_per_tile,
+                             S(stream)),
           "paged_prefill");
   });
   m.def("sample", [](uptr logits, int is_bf16, long stride, int B, int V, uptr temp, uptr topk,

@@ -30,6 +30,12 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
   return *reinterpret_cast<uint16_t*>(&b);
 }
 
+// 2^x as the bare v_exp_f32 (exp2f adds a denormal range fix-up -- v_cmp,
+// two v_cndmask and a v_ldexp per call, 4 of the ~7 VALU per softmax element
+// of the attention kernels).  Results below 2^-126 flush to 0, -inf -> 0:
+// what a softmax weight needs.
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
   return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
 }

@@ -282,9 +282,12 @@ def decode_order(context_lens) -> "np.ndarray":
 
 def paged_prefill_attention(q: torch.Tensor, k_cache, v_cache, block_tables, cu_q,
                             context_lens, tiles, scale: float, out: torch.Tensor,
-                            causal: bool = True, Hq: int | None = None) -> torch.Tensor:
+                            causal: bool = True, Hq: int | None = None,
+                            q_per_tile: int | None = None) -> torch.Tensor:
     """Varlen prefill. q/out: [T, Hq*D] rows; tiles: int32 [(seq, q_start)]
-    built with q_per_tile = 128 / G (see ``prefill_q_per_tile``)."""
+    built with ``q_per_tile`` queries per tile (default
+    ``prefill_q_per_tile(Hq, Hkv, D)``; the kernel's workgroup width follows
+    from it)."""
     NB, Hkv, BS, D = k_cache.shape
     T = q.shape[0]
     Hq = Hq or (q.shape[1] // D)
@@ -302,18 +305,29 @@ def paged_prefill_attention(q: torch.Tensor, k_cache, v_cache, block_tables, cu_
     native().paged_prefill(_ptr(q), q.stride(0), _ptr(k_cache), _ptr(v_cache),
                            _ptr(block_tables), block_tables.stride(0), _ptr(cu_q),
                            _ptr(context_lens), _ptr(tiles), num_tiles, _ptr(out), out.stride(0),
-                           Hq, Hkv, D, BS, float(scale), int(causal), _stream())
+                           Hq, Hkv, D, BS, float(scale), int(causal),
+                           q_per_tile or prefill_q_per_tile(Hq, Hkv, D), _stream())
     return out
 
 
 PREFILL_GROUPS_PER_WAVE = 2   # PF_NG in csrc/kernels/attention.hip
+# waves per prefill workgroup at head dim 128 (4 or 8; head dim 64: 4).
+# LMX_PREFILL_WAVES overrides (A/B).
+PREFILL_WAVES_D128 = 4
+
+
+def prefill_waves(D: int) -> int:
+    import os
+    if D != 128:
+        return 4
+    return int(os.environ.get("LMX_PREFILL_WAVES", PREFILL_WAVES_D128))
 
 
 def prefill_q_per_tile(Hq: int, Hkv: int, D: int = 128) -> int:
-    """Queries per prefill workgroup: 4 waves x column groups x 16/G (column
-    groups per wave: 4 at head dim 64, 2 at 128 -- attention.hip
-    pf_groups)."""
-    return 4 * (4 if D == 64 else PREFILL_GROUPS_PER_WAVE) * (16 // (Hq // Hkv))
+    """Queries per prefill workgroup: waves (prefill_waves) x column groups
+    x 16/G (column groups per wave: 4 at head dim 64, 2 at 128 --
+    attention.hip pf_groups)."""
+    return prefill_waves(D) * (4 if D == 64 else PREFILL_GROUPS_PER_WAVE) * (16 // (Hq // Hkv))
 
 
 # ---------------------------------------------------------------- sampling ---

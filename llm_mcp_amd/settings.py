@@ -95,6 +95,7 @@ VARS: list[Var] = [
     Var("LMX_RESTART_MAX_S", float, 60.0, "serve: cap of the worker restart backoff"),
     Var("LMX_SOCKET_DIR", str, "", "serve: directory of the engine sockets (default /tmp)"),
     Var("LMX_DGEMM", str, "1", "0 disables the decode GEMM (K11) dispatch table (hipBLASLt everywhere)"),
+    Var("LMX_PREFILL_WAVES", int, 4, "waves per prefill-attention workgroup at head dim 128 (4 or 8)"),
     Var("LMX_SK", str, "1", "0 disables the K13-SK (split-K 256x256 tile) entries of the decode GEMM table"),
     Var("LMX_DGEMM_TABLE", str, "", "decode GEMM dispatch table (default llm_mcp_amd/config/dgemm_gfx950.json)"),
     Var("LMX_FAULT_DEVICE", str, "", "apply LMX_FAULT only in the worker whose device id ends with this (e.g. gpu0.r1)"),

@@ -136,9 +136,16 @@ def prefill_ring(request):
     ops.native().set_prefill_stages(0)
 
 
+@pytest.fixture(params=[4, 8], ids=["w4", "w8"])
+def prefill_waves(request, monkeypatch):
+    """Waves per prefill workgroup at head dim 128 (the tile list follows)."""
+    monkeypatch.setenv("LMX_PREFILL_WAVES", str(request.param))
+    yield request.param
+
+
 @pytest.mark.parametrize("Hq,Hkv,D", [(32, 8, 128), (8, 1, 128), (12, 12, 64), (4, 4, 128),
                                      (28, 4, 128), (7, 1, 64), (24, 8, 128)])
-def test_paged_prefill_varlen_with_prefix(Hq, Hkv, D, prefill_ring):
+def test_paged_prefill_varlen_with_prefix(Hq, Hkv, D, prefill_ring, prefill_waves):
     qlens = [1, 70, 33, 256]
     prefix = [0, 40, 0, 100]
     ctxs = [q + p for q, p in zip(qlens, prefix)]

@@ -19,7 +19,7 @@ SHAPES = {"nomic": (32, 1024, 12, 12, 64, False), "mxbai": (64, 512, 16, 16, 64,
           "llama8b": (30, 546, 32, 8, 128, True)}
 
 
-def run(name, S, L, Hq, Hkv, D, causal, iters, ng=0, tag=""):
+def run(name, S, L, Hq, Hkv, D, causal, iters, ng=0, tag="", waves=4):
     dev = torch.device("cuda", 0)
     BS = 32
     T = S * L
@@ -31,6 +31,9 @@ def run(name, S, L, Hq, Hkv, D, causal, iters, ng=0, tag=""):
     q = torch.randn(T, (Hq + 2 * Hkv) * D, device=dev).to(torch.bfloat16)
     cu = torch.arange(0, T + 1, L, dtype=torch.int32, device=dev)
     ctx = torch.full((S,), L, dtype=torch.int32, device=dev)
+    if D != 128:
+        waves = 4
+    os.environ["LMX_PREFILL_WAVES"] = str(waves)
     qpt = 4 * ng * (16 // (Hq // Hkv)) if ng else ops.prefill_q_per_tile(Hq, Hkv, D)
     tiles = torch.tensor([v for s in range(S) for q0 in range(0, L, qpt) for v in (s, q0)],
                          dtype=torch.int32, device=dev)
@@ -39,7 +42,7 @@ def run(name, S, L, Hq, Hkv, D, causal, iters, ng=0, tag=""):
 
     def call():
         ops.paged_prefill_attention(q, kc, vc, bt, cu, ctx, tiles, scale, out, causal=causal,
-                                    Hq=Hq)
+                                    Hq=Hq, q_per_tile=qpt)
     for _ in range(3):
         call()
     torch.cuda.synchronize()
@@ -61,22 +64,31 @@ def main():
                     help="column groups per wave of the loaded build (A/B of an older .so)")
     ap.add_argument("--thr", default="8",
                     help="comma list of softmax lazy-rescale thresholds to interleave")
+    ap.add_argument("--waves", default="4,8", help="comma list of waves per workgroup (head dim 128)")
+    ap.add_argument("--xcd", default="1", help="comma list of workgroup orders (1 XCD-aware, 0 hardware)")
     ap.add_argument("--stages", default="0",
                     help="comma list of LDS ring slot counts to interleave (0 = default)")
     a = ap.parse_args()
     thrs = [float(t) for t in a.thr.split(",")]
     stages = [int(t) for t in a.stages.split(",")]
+    xcds = [int(t) for t in a.xcd.split(",")]
+    wl = [int(t) for t in a.waves.split(",")]
     nat = ops.native()
     for _ in range(2):
         for name, shp in SHAPES.items():
             for thr in thrs:
-                for st in stages:
+                for st, xo, w in [(st, xo, w) for st in stages for xo in xcds for w in wl]:
+                    if shp[4] != 128 and w != wl[0]:
+                        continue
+                    if hasattr(nat, "set_prefill_xcd"):
+                        nat.set_prefill_xcd(xo)
                     if hasattr(nat, "set_prefill_rescale_thr"):
                         nat.set_prefill_rescale_thr(thr)
                     if hasattr(nat, "set_prefill_stages"):
                         nat.set_prefill_stages(st)
-                    run(name, *shp, a.iters, a.ng, tag=f"thr={thr:g} nst={st}")
+                    run(name, *shp, a.iters, a.ng, tag=f"thr={thr:g} nst={st} xcd={xo} w={w}", waves=w)
     nat.set_prefill_stages(0)
+    nat.set_prefill_xcd(1)
 
 
 if __name__ == "__main__":
