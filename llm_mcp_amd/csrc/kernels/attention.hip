@@ -23,6 +23,7 @@
 //                 causal key range; varlen batches via a host-built tile list.
 #include <algorithm>
 #include <climits>
+#include <type_traits>
 
 #include "common.h"
 
@@ -813,104 +814,144 @@ __global__ void __launch_bounds__(64 * PW, 8 / PW) paged_prefill_kernel(
     const bf16_t* kt = lds + buf * 4 * PAGE;
     const bf16_t* vt = kt + 2 * PAGE;
     const int key0 = t * PF_TK;
-    // S^T = K . Q^T for 4 key blocks of 16
-    f32x4_t s[PF_NG][4];
+    // One 64-key tile, software-pipelined over the wave's column groups so the
+    // softmax VALU of group n-1 issues between the S MFMAs of group n, and the
+    // softmax of the last group between the PV MFMAs of group 0 (the MFMA and
+    // VALU pipes of a SIMD run concurrently; in the plain S -> softmax -> PV
+    // order a wave idles one while it feeds the other):
+    //   S(0) | S(1) + sm(0) | ... | PV(0) + sm(NG-1) | PV(1) ... PV(NG-1)
+    // K fragments are read once and kept for every group, V fragments too.
+    // The softmax is branch-free inside a region (the lazy rescale decision
+    // is a wave-uniform select; the O^T rescale of group n -- rare -- runs
+    // between regions, before PV(n)); the causal mask is a tile-level variant.
+    auto tile_body = [&](auto mask_tag) {
+      constexpr bool MASK = decltype(mask_tag)::value;
+      f32x4_t s[PF_NG][4];
+      bf16x8_t pf[PF_NG][2];
+      bool need[PF_NG];
+      float alpha[PF_NG];
+      bf16x8_t kf[4][KS];
 #pragma unroll
-    for (int n = 0; n < PF_NG; ++n)
+      for (int kb = 0; kb < 4; ++kb) {
+        const int row = (kb & 1) * 16 + c;               // key row inside its page
+        const bf16_t* krow = kt + (kb >> 1) * PAGE + row * HD;
 #pragma unroll
-      for (int kb = 0; kb < 4; ++kb) s[n][kb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int kb = 0; kb < 4; ++kb) {
-      const int row = (kb & 1) * 16 + c;                 // key row inside its page
-      const bf16_t* krow = kt + (kb >> 1) * PAGE + row * HD;
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        const bf16x8_t kf = load_frag16B(krow + 8 * ((ks * 4 + g) ^ kswz<HD>(row)));
-#pragma unroll
-        for (int n = 0; n < PF_NG; ++n) s[n][kb] = mfma16(kf, qf[n][ks], s[n][kb]);
+        for (int ks = 0; ks < KS; ++ks)
+          kf[kb][ks] = load_frag16B(krow + 8 * ((ks * 4 + g) ^ kswz<HD>(row)));
       }
-    }
-    // online softmax per column group.  The scores stay raw (the scale is
-    // folded into the exp argument: one FMA per score), and the running max m
-    // (log2 units) is only raised when a tile's max exceeds it by more than
-    // rescale_thr (guide T13): until then p = 2^(x - m) <= 2^thr, harmless in
-    // bf16 P / fp32 l, and the O^T accumulators are not rescaled -- the
-    // NT x 4 multiplies per column group and tile that a per-tile rescale
-    // costs are most of the softmax VALU work at this tile shape.  The wave
-    // rescales together when any of its columns needs it (exact alpha per
-    // column, 1 for the ones that did not grow).
-    const bool need_mask = key0 + PF_TK - 1 > wave_lo;
-    bf16x8_t pf[PF_NG][2];
-    // fp32 pairs (v_pk_fma_f32 / v_pk_add_f32 on the exp argument and the row
-    // sum, half the VALU issue of the scalar form); the causal mask only on
-    // the tiles that cross a column limit (wave-uniform branch)
-    typedef float f32x2_t __attribute__((ext_vector_type(2)));
-#pragma unroll
-    for (int n = 0; n < PF_NG; ++n) {
-      f32x2_t x[8];                                      // x[2 kb + h] = keys 16 kb + 4 g + 2 h + {0, 1}
-#pragma unroll
-      for (int kb = 0; kb < 4; ++kb)
-#pragma unroll
-        for (int h = 0; h < 2; ++h) x[2 * kb + h] = f32x2_t{s[n][kb][2 * h], s[n][kb][2 * h + 1]};
-      if (need_mask) {
+      const f32x4_t z4 = {0.f, 0.f, 0.f, 0.f};
+      auto s_mma = [&](int n) {
 #pragma unroll
         for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int key = key0 + kb * 16 + 4 * g + r;
-            if (key > lim[n]) x[2 * kb + (r >> 1)][r & 1] = -INFINITY;
-          }
-      }
-      float mx = fmaxf(x[0].x, x[0].y);
+          for (int ks = 0; ks < KS; ++ks)
+            s[n][kb] = mfma16(kf[kb][ks], qf[n][ks], ks == 0 ? z4 : s[n][kb]);
+      };
+      typedef float f32x2_t __attribute__((ext_vector_type(2)));
+      auto softmax = [&](int n) {
+        f32x2_t x[8];                                    // x[2 kb + h] = keys 16 kb + 4 g + 2 h + {0, 1}
 #pragma unroll
-      for (int j = 1; j < 8; ++j) mx = fmaxf(mx, fmaxf(x[j].x, x[j].y));
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mx2 = mx * scale_log2;                 // -inf stays -inf (scale > 0)
-      if (__ballot(mx2 > m[n] + rescale_thr)) {
-        const float m_new = fmaxf(m[n], mx2);
-        const float alpha = (m_new == -INFINITY) ? 1.f : fast_exp2(m[n] - m_new);
-        l[n] *= alpha;
+        for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
-        for (int i = 0; i < NT; ++i) acc[n][i] *= alpha;
+          for (int h = 0; h < 2; ++h) x[2 * kb + h] = f32x2_t{s[n][kb][2 * h], s[n][kb][2 * h + 1]};
+        if constexpr (MASK) {
+#pragma unroll
+          for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int key = key0 + kb * 16 + 4 * g + r;
+              x[2 * kb + (r >> 1)][r & 1] = key <= lim[n] ? x[2 * kb + (r >> 1)][r & 1] : -INFINITY;
+            }
+        }
+        float mx = fmaxf(x[0].x, x[0].y);
+#pragma unroll
+        for (int j = 1; j < 8; ++j) mx = fmaxf(mx, fmaxf(x[j].x, x[j].y));
+        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const float mx2 = mx * scale_log2;               // -inf stays -inf (scale > 0)
+        // lazy rescale (guide T13): the running max m (log2 units) is raised
+        // only when a tile's max exceeds it by more than rescale_thr; until then
+        // p = 2^(x - m) <= 2^thr.  The wave rescales together (exact alpha per
+        // column, 1 where it did not grow).
+        const bool nd = __ballot(mx2 > m[n] + rescale_thr) != 0;
+        const float m_new = nd ? fmaxf(m[n], mx2) : m[n];
+        const float al = (nd && m_new != -INFINITY) ? fast_exp2(m[n] - m_new) : 1.f;
+        l[n] *= al;
         m[n] = m_new;
-      }
-      const float m_use = (m[n] == -INFINITY) ? 0.f : m[n];
-      const f32x2_t sc2 = {scale_log2, scale_log2}, nm2 = {-m_use, -m_use};
-      f32x2_t rs2 = {0.f, 0.f};
+        need[n] = nd;
+        alpha[n] = al;
+        const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
+        const f32x2_t sc2 = {scale_log2, scale_log2}, nm2 = {-m_use, -m_use};
+        f32x2_t rs2 = {0.f, 0.f};
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        f32x2_t y = x[j] * sc2 + nm2;
-        y.x = fast_exp2(y.x);
-        y.y = fast_exp2(y.y);
-        x[j] = y;
-        rs2 += y;
+        for (int j = 0; j < 8; ++j) {
+          f32x2_t y = x[j] * sc2 + nm2;
+          y.x = fast_exp2(y.x);
+          y.y = fast_exp2(y.y);
+          x[j] = y;
+          rs2 += y;
+        }
+        float rs = rs2.x + rs2.y;
+        rs += __shfl_xor(rs, 16, 64);
+        rs += __shfl_xor(rs, 32, 64);
+        l[n] += rs;
+        // page p: keys 4g+r (block 2p) then 16+4g+r (block 2p+1) -> permuted-k B operand
+#pragma unroll
+        for (int pp = 0; pp < 2; ++pp)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const uint32_t w = pack_bf16x2(x[4 * pp + j].x, x[4 * pp + j].y);
+            pf[n][pp][2 * j] = (short)(w & 0xffff);
+            pf[n][pp][2 * j + 1] = (short)(w >> 16);
+          }
+      };
+      auto rescale = [&](int n) {
+        if (need[n]) {
+#pragma unroll
+          for (int i = 0; i < NT; ++i) acc[n][i] *= alpha[n];
+        }
+      };
+      // interleave hint for one region: MFMAs spread through the VALU stream
+      auto interleave = [&](int nmfma) {
+        for (int i = 0; i < nmfma; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
+          __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);   // 5 VALU
+        }
+      };
+      s_mma(0);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int n = 1; n < PF_NG; ++n) {
+        s_mma(n);
+        softmax(n - 1);
+        interleave(4 * KS);
+        __builtin_amdgcn_sched_barrier(0);
+        rescale(n - 1);
+        __builtin_amdgcn_sched_barrier(0);
       }
-      float rs = rs2.x + rs2.y;
-      rs += __shfl_xor(rs, 16, 64);
-      rs += __shfl_xor(rs, 32, 64);
-      l[n] += rs;
-      // page p: keys 4g+r (block 2p) then 16+4g+r (block 2p+1) -> permuted-k B operand
+      // V^T fragments of both pages (kept for every group)
+      bf16x8_t vf[2][NT];
 #pragma unroll
       for (int pp = 0; pp < 2; ++pp)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t w = pack_bf16x2(x[4 * pp + j].x, x[4 * pp + j].y);
-          pf[n][pp][2 * j] = (short)(w & 0xffff);
-          pf[n][pp][2 * j + 1] = (short)(w >> 16);
-        }
-    }
-    // O^T += V^T . P^T
+        for (int i = 0; i < NT; ++i) vf[pp][i] = pf_vfrag<HD>(vt + pp * PAGE, 16 * i + c, g);
+      auto pv = [&](int n) {
 #pragma unroll
-    for (int pp = 0; pp < 2; ++pp) {
-      const bf16_t* vpg = vt + pp * PAGE;
+        for (int pp = 0; pp < 2; ++pp)
 #pragma unroll
-      for (int i = 0; i < NT; ++i) {
-        const bf16x8_t vf = pf_vfrag<HD>(vpg, 16 * i + c, g);
+          for (int i = 0; i < NT; ++i) acc[n][i] = mfma16(vf[pp][i], pf[n][pp], acc[n][i]);
+      };
+      pv(0);
+      softmax(PF_NG - 1);
+      interleave(2 * NT);
+      __builtin_amdgcn_sched_barrier(0);
+      rescale(PF_NG - 1);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int n = 0; n < PF_NG; ++n) acc[n][i] = mfma16(vf, pf[n][pp], acc[n][i]);
-      }
-    }
+      for (int n = 1; n < PF_NG; ++n) pv(n);
+    };
+    const bool need_mask = key0 + PF_TK - 1 > wave_lo;
+    if (need_mask) tile_body(std::true_type{}); else tile_body(std::false_type{});
   }
 #pragma unroll
   for (int n = 0; n < PF_NG; ++n) {
