@@ -758,3 +758,17 @@ def test_linear_large_m_runs_k13(monkeypatch):
     monkeypatch.setenv("LMX_LARGE_GEMM", "lib")
     ops.linear(x, w)
     assert ops.PGEMM_CALLS[0] - before == 2
+
+
+def test_linear_decode_lm_head_runs_k13_sk():
+    """The decode table's K13-SK entry (config "sk": Llama-3-8B LM head at
+    M 176..256) is what ops.linear runs there, and it matches the library."""
+    N, K = 128256, 4096
+    assert ops.sk_choice(256, N, K) == 1 and ops.sk_choice(128, N, K) is None
+    x = _bf(256, K)
+    w = _bf(N, K, scale=K ** -0.5)
+    before = ops.PGEMM_CALLS[0]
+    y = ops.linear(x, w)
+    assert ops.PGEMM_CALLS[0] - before == 1
+    torch.testing.assert_close(y.float(), torch.nn.functional.linear(x, w).float(),
+                               atol=2e-2, rtol=2e-2)
