@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--splits", default="1,2,3,4")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--only", default="")
+    ap.add_argument("--warm", action="store_true", help="one weight copy (re-read from the Infinity Cache)")
     a = ap.parse_args()
     ops.native()
     torch.manual_seed(0)
@@ -49,7 +50,7 @@ def main():
         for name, (N, K, act, epi) in SHAPES.items():
             if a.only and not any(o in name for o in a.only.split(",")):
                 continue
-            ncopy = max(2, int(6e8 // (N * K * 2)) + 1)
+            ncopy = 1 if a.warm else max(2, int(6e8 // (N * K * 2)) + 1)
             x = (torch.rand(M, K, device="cuda", dtype=torch.bfloat16) * 2 - 1)
             ws = [(torch.rand(N, K, device="cuda", dtype=torch.bfloat16) * 2 - 1) * K ** -0.5
                   for _ in range(ncopy)]
