@@ -684,9 +684,14 @@ def swiglu_block(N: int, K: int) -> int:
     else BN/2 of the measured epi-1 configurations; 0 = not fused."""
     if any(cfg >= 0 for m, cfg, s in _dg_table().get((N, K, 3), ())) or _sk_table().get((N, K, 3)):
         return SWIGLU16
-    bns = {DGEMM_CONFIGS[cfg & DGEMM_CFG_MASK][1]
-           for m, cfg, s in _dg_table().get((N, K, 1), ()) if cfg >= 0}
-    return min(bns) // 2 if bns else 0
+    # one interleave serves every batch size, so take the tile width of the
+    # largest-batch bucket the fused kernel won: buckets measured with another
+    # width fall back to library + GLU (Llama-3-70B TP=1: 64-row buckets at BN
+    # 128, the 128-row bucket at BN 256 -- the old smallest-width pick sent the
+    # 128-row decode steps to the library + GLU, 228 vs 160 us per layer)
+    best = max(((m, cfg) for m, cfg, s in _dg_table().get((N, K, 1), ()) if cfg >= 0),
+               default=None)
+    return DGEMM_CONFIGS[best[1] & DGEMM_CFG_MASK][1] // 2 if best else 0
 
 
 def swiglu16_ok(cfg: int) -> bool:

@@ -1,0 +1,35 @@
+"""CPU tests of the measured GEMM dispatch tables (config/dgemm_gfx950.json):
+the gate/up interleave block, the K13-SK entries and the large-M backend pick."""
+from llm_mcp_amd import ops
+
+
+def test_swiglu_block_follows_the_largest_batch_bucket(monkeypatch):
+    # 64-row buckets won at BN 128 (cfg 16 -> (64, 128)), the 128-row bucket at
+    # BN 256 (cfg 11 -> (128, 256)): one interleave for all, the big batch wins
+    table = {(57344, 8192, 1): [(64, 16 | ops.DGEMM_NT, 1), (128, 11, 1), (256, -1, 0)]}
+    monkeypatch.setattr(ops, "DGEMM_TABLE", table)
+    monkeypatch.setattr(ops, "_SK_TABLE", {})
+    assert ops.swiglu_block(57344, 8192) == 128
+    assert ops.dgemm_choice(128, 57344, 8192, epi=1) == (11, 1)
+    assert ops.dgemm_choice(200, 57344, 8192, epi=1) is None     # library bucket
+    # epi-3 entries (16-row pairs, any tile width) take precedence
+    table[(57344, 8192, 3)] = [(128, 17, 1)]
+    assert ops.swiglu_block(57344, 8192) == ops.SWIGLU16
+    assert ops.swiglu_block(1000, 1000) == 0
+
+
+def test_sk_choice_and_large_gemm_backend(monkeypatch):
+    monkeypatch.setattr(ops, "_SK_TABLE", {(128256, 4096, 0): [(176, 256, 1)],
+                                           (4096, 4096, 2): [(129, 256, 3)]})
+    assert ops.sk_choice(256, 128256, 4096) == 1
+    assert ops.sk_choice(175, 128256, 4096) is None
+    assert ops.sk_choice(200, 4096, 4096, epi=2) is None      # S 3: no rmsnorm_slabs instance
+    monkeypatch.setattr(ops, "_ENC_TABLE", {(6144, 4096): {"k13_tflops": 1560.0, "lib_tflops": 1600.0},
+                                            (768, 3072): {"k13_tflops": 1100.0, "lib_tflops": 1300.0}})
+    monkeypatch.delenv("LMX_LARGE_GEMM", raising=False)
+    assert ops.large_gemm_backend(16384, 6144, 4096) == "k13"   # within the 5 % margin
+    assert ops.large_gemm_backend(16384, 768, 3072) == "lib"
+    assert ops.large_gemm_backend(100, 6144, 4096) == "lib"     # decode-sized M
+    assert ops.large_gemm_backend(16384, 4096, 4096) == "k13"   # unmeasured
+    monkeypatch.setenv("LMX_LARGE_GEMM", "lib")
+    assert ops.large_gemm_backend(16384, 6144, 4096) == "lib"
