@@ -16,7 +16,9 @@ from llm_mcp_amd import ops  # noqa: E402
 SHAPES = {"nomic.qkv": (2304, 768), "nomic.o": (768, 768), "nomic.gate_up": (6144, 768),
           "nomic.down": (768, 3072), "l8b.qkv": (6144, 4096), "l8b.o": (4096, 4096),
           "l8b.gate_up": (28672, 4096), "l8b.down": (4096, 14336), "bert.qkv": (3072, 1024),
-          "bert.o": (1024, 1024), "bert.w1": (4096, 1024), "bert.w2": (1024, 4096)}
+          "bert.o": (1024, 1024), "bert.w1": (4096, 1024), "bert.w2": (1024, 4096),
+          "l70b.qkv": (10240, 8192), "l70b.o": (8192, 8192), "l70b.gate_up": (57344, 8192),
+          "l70b.down": (8192, 28672)}
 
 
 def main():
