@@ -183,6 +183,32 @@ def test_llama3_8b_shapes_on_decode_gemm_match_dense(graphs):
         assert_greedy_consistent(e.model, p, o, tol=0.08)
 
 
+@pytest.mark.parametrize("graphs", [False, True])
+def test_llama3_8b_shapes_k13_prefill_and_sk_lm_head(graphs):
+    """Two layers of Llama-3-8B at a 200-row batch: the one-step prefill of
+    200 x 4 tokens (M = 800) runs the projections on K13 (fused SwiGLU gate/up)
+    and the 200-row decode steps run the LM head on K13-SK (config "sk"), in
+    captured graphs too (bucket 224); greedy tokens stay (near-)argmax of the dense fp32
+    forward."""
+    import dataclasses
+
+    from llm_mcp_amd.models import config as mc
+    ops.native()
+    cfg = dataclasses.replace(mc.resolve("llama-3-8b"), num_layers=2)
+    assert ops.sk_choice(200, cfg.vocab_size, cfg.hidden_size) is not None
+    n0 = ops.PGEMM_CALLS[0]
+    e = LLMEngine(EngineConfig(model="llama-3-8b", max_num_seqs=224, max_batched_tokens=1024,
+                               max_model_len=256, use_graphs=graphs, kv_cache_gb=1),
+                  device="cuda", model_cfg=cfg)
+    prompts = [[(13 * i + 5 * j) % 120000 + 100 for j in range(4)] for i in range(200)]
+    outs = e.generate(prompts, SamplingParams(temperature=0, max_tokens=3, ignore_eos=True))
+    assert ops.PGEMM_CALLS[0] > n0
+    if graphs:
+        assert e.stats["graph_steps"] > 0
+    for p, o in list(zip(prompts, outs))[::37]:
+        assert_greedy_consistent(e.model, p, o, tol=0.08)
+
+
 def test_lookahead_graph_steps_match_synchronous(monkeypatch):
     """Lookahead stepping on the captured decode graphs (input tokens gathered
     on the device by ops.ids_from_prev from the previous step's samples) gives
