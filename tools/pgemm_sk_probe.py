@@ -1,6 +1,6 @@
 """K13-SK (ops.pgemm_sk: 256x256 ping-pong tile, split-K) vs the paths that
 serve the decode projections now (hipBLASLt via F.linear, K11 table entries)
-at decode batch sizes; warm weights as in a decode graph replay (the whole
+at decode batch sizes; cold weights by default, as in a decode graph replay (the whole
 model's weights cycle through HBM between two uses, so the tested weight is
 rotated over copies > 512 MB); us per call, median of interleaved rounds.
 
