@@ -1,4 +1,7 @@
-// K13: large-M projection GEMM (prefill chunks, embedding-model batches):
+// K13: large-M projection GEMM (prefill chunks, embedding-model batches) --
+// the projections behind the chat and embedding requests that the reference
+// proxies to Ollama (reference core/internal/api/handlers.go:1942 proxyOllamaEmbed,
+// :2427 streamOllamaChat); K13-SK below serves decode batches:
 //     C[M, N] = epi(A[M, K] . W[N, K]^T)     bf16 in, fp32 accumulate, bf16 out
 // epi: optional bias (staged in LDS), then none / GELU(tanh) / SiLU / GELU(erf),
 // or SwiGLU over 16-row gate/up pairs (W from ops.interleave_gate_up(w, 16);
