@@ -762,7 +762,7 @@ def test_linear_large_m_runs_k13(monkeypatch):
 
 def test_linear_decode_lm_head_runs_k13_sk():
     """The decode table's K13-SK entry (config "sk": Llama-3-8B LM head at
-    M 176..256) is what ops.linear runs there, and it matches the library."""
+    M 129..256) is what ops.linear runs there, and it matches the library."""
     N, K = 128256, 4096
     assert ops.sk_choice(256, N, K) == 1 and ops.sk_choice(128, N, K) is None
     x = _bf(256, K)
