@@ -692,7 +692,11 @@ __global__ void __launch_bounds__(64 * PW, 8 / PW) paged_prefill_kernel(
   const int nwg = gridDim.x * gridDim.y;
   const int lin0 = blockIdx.x + blockIdx.y * gridDim.x;
   const int lin = xcd ? xcd_remap(lin0, nwg) : lin0;
-  const int tile = lin % gridDim.x, kvh = lin / gridDim.x;
+  // xcd 2: the tile list walked backwards -- the host lists a sequence's query
+  // tiles in ascending order, so causal chunks then start their longest
+  // key walks first and the short ones fill the tail
+  const int tile = xcd == 2 ? (int)gridDim.x - 1 - lin % (int)gridDim.x : lin % (int)gridDim.x;
+  const int kvh = lin / gridDim.x;
   const int seq = tiles[2 * tile], q_start = tiles[2 * tile + 1];
   // queries per 16-lane column group; with G not dividing 16 (e.g. Qwen2.5's
   // 7) the last 16 - QG*G lanes of a group are idle
@@ -976,9 +980,10 @@ void set_prefill_rescale_thr(float thr) { g_prefill_rescale_thr = thr; }
 // LDS ring slots of the prefill kernel (0: default per head dim; 2 or 3: A/B knob)
 static int g_prefill_stages = 0;
 void set_prefill_stages(int n) { g_prefill_stages = (n == 2 || n == 3) ? n : 0; }
-// XCD-aware workgroup order of the prefill kernel (1, default) or hardware order (0: A/B knob)
-static int g_prefill_xcd = 1;
-void set_prefill_xcd(int on) { g_prefill_xcd = on ? 1 : 0; }
+// prefill workgroup order: 2 (default) XCD-aware with the tile list walked backwards, 1
+// XCD-aware, 0 hardware order (A/B knob)
+static int g_prefill_xcd = 2;
+void set_prefill_xcd(int on) { g_prefill_xcd = on < 0 ? 0 : (on > 2 ? 2 : on); }
 
 // q_per_tile: the tile list's queries per workgroup (ops.prefill_q_per_tile);
 // it selects the workgroup width PW = q_per_tile / (column groups x 16/G):

@@ -135,7 +135,7 @@ PYBIND11_MODULE(_lmx_kernels, m) {
   m.def("set_prefill_stages", [](int n) { lmx::set_prefill_stages(n); },
         "prefill attention LDS ring slots: 0 default per head dim, 2 or 3");
   m.def("set_prefill_xcd", [](int on) { lmx::set_prefill_xcd(on); },
-        "prefill attention workgroup order: 1 XCD-aware (default), 0 hardware order");
+        "prefill attention workgroup order: 2 XCD-aware, tile list reversed (default), 1 XCD-aware, 0 hardware order");
   m.def("paged_prefill", [](uptr q, long q_stride, uptr kc, uptr vc, uptr bt, int bt_stride,
                             uptr cu_q, uptr ctx, uptr tiles, int num_tiles, uptr out,
                             long out_stride, int Hq, int Hkv, int D, int BS, float scale,

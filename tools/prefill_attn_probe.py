@@ -65,7 +65,7 @@ def main():
     ap.add_argument("--thr", default="8",
                     help="comma list of softmax lazy-rescale thresholds to interleave")
     ap.add_argument("--waves", default="4,8", help="comma list of waves per workgroup (head dim 128)")
-    ap.add_argument("--xcd", default="1", help="comma list of workgroup orders (1 XCD-aware, 0 hardware)")
+    ap.add_argument("--xcd", default="2", help="comma list of workgroup orders (2 XCD-aware + reversed tile list, 1 XCD-aware, 0 hardware)")
     ap.add_argument("--stages", default="0",
                     help="comma list of LDS ring slot counts to interleave (0 = default)")
     a = ap.parse_args()
@@ -88,7 +88,7 @@ def main():
                         nat.set_prefill_stages(st)
                     run(name, *shp, a.iters, a.ng, tag=f"thr={thr:g} nst={st} xcd={xo} w={w}", waves=w)
     nat.set_prefill_stages(0)
-    nat.set_prefill_xcd(1)
+    nat.set_prefill_xcd(2)
 
 
 if __name__ == "__main__":
