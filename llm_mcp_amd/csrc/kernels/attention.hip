@@ -32,6 +32,30 @@ namespace lmx {
 constexpr int BS = 32;   // KV page (block) size in tokens
 constexpr float LOG2E = 1.4426950408889634f;
 
+// max / sum over the 4 lanes c, c+16, c+32, c+48 (one MFMA column's 4 row
+// groups) with v_permlane16_swap / v_permlane32_swap: VALU lane exchanges
+// instead of two ds_bpermute round trips through the LDS unit on the softmax's
+// serial chain.  permlane16_swap(x, x) yields {rows 0,0,2,2 ; rows 1,1,3,3} of
+// x (16-lane rows), so op(first, second) is the xor-16 reduction; the 32-lane
+// form does the same across halves.
+__device__ __forceinline__ float col4_max(float x) {
+  const unsigned u = __float_as_uint(x);
+  const auto a = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  x = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  const unsigned v = __float_as_uint(x);
+  const auto b = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+
+__device__ __forceinline__ float col4_sum(float x) {
+  const unsigned u = __float_as_uint(x);
+  const auto a = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  x = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const unsigned v = __float_as_uint(x);
+  const auto b = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
 template <int HD>
 struct PageState {
   float m;                // running max (log2 domain) of this lane's column
@@ -870,8 +894,7 @@ __global__ void __launch_bounds__(64 * PW, 8 / PW) paged_prefill_kernel(
         float mx = fmaxf(x[0].x, x[0].y);
 #pragma unroll
         for (int j = 1; j < 8; ++j) mx = fmaxf(mx, fmaxf(x[j].x, x[j].y));
-        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        mx = col4_max(mx);
         const float mx2 = mx * scale_log2;               // -inf stays -inf (scale > 0)
         // lazy rescale (guide T13): the running max m (log2 units) is raised
         // only when a tile's max exceeds it by more than rescale_thr; until then
@@ -895,10 +918,7 @@ __global__ void __launch_bounds__(64 * PW, 8 / PW) paged_prefill_kernel(
           x[j] = y;
           rs2 += y;
         }
-        float rs = rs2.x + rs2.y;
-        rs += __shfl_xor(rs, 16, 64);
-        rs += __shfl_xor(rs, 32, 64);
-        l[n] += rs;
+        l[n] += col4_sum(rs2.x + rs2.y);
         // page p: keys 4g+r (block 2p) then 16+4g+r (block 2p+1) -> permuted-k B operand
 #pragma unroll
         for (int pp = 0; pp < 2; ++pp)
