@@ -33,3 +33,23 @@ def test_sk_choice_and_large_gemm_backend(monkeypatch):
     assert ops.large_gemm_backend(16384, 4096, 4096) == "k13"   # unmeasured
     monkeypatch.setenv("LMX_LARGE_GEMM", "lib")
     assert ops.large_gemm_backend(16384, 6144, 4096) == "lib"
+
+
+def test_pgemm_sk_cpu_reference_forms():
+    """ops.pgemm_sk on CPU tensors (the fp32 reference of the K13-SK forms):
+    plain, 16-row SwiGLU pairs, fp32 partials summed by the consumer."""
+    import torch
+    torch.manual_seed(0)
+    a = torch.randn(37, 512).to(torch.bfloat16)
+    w = (torch.randn(512, 512) * 512 ** -0.5).to(torch.bfloat16)
+    y = a.float() @ w.float().t()
+    torch.testing.assert_close(ops.pgemm_sk(a, w, 2).float(), y, atol=2e-2, rtol=2e-2)
+    p = ops.pgemm_sk(a, w, 4, epi=2)
+    assert isinstance(p, ops.Partials) and p.slabs.shape == (4, 37, 512)
+    torch.testing.assert_close(p.sum(), y, atol=1e-4, rtol=1e-4)
+    wil = ops.interleave_gate_up(w, ops.SWIGLU16)
+    g = torch.nn.functional.silu(y[:, :256]) * y[:, 256:]
+    torch.testing.assert_close(ops.pgemm_sk(a, wil, 2, act=ops.ACT_SWIGLU).float(), g,
+                               atol=2e-2, rtol=2e-2)
+    assert not ops.pgemm_sk_supported(37, 500, 512, 2)          # N not a 256 multiple
+    assert not ops.pgemm_sk_supported(37, 512, 512, 8)          # one K-step per slice
