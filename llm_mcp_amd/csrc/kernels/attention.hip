@@ -701,7 +701,8 @@ __global__ void __launch_bounds__(64 * PW, 8 / PW) paged_prefill_kernel(
     const bf16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ cu_q, const int* __restrict__ context_lens,
     const int* __restrict__ tiles, bf16_t* __restrict__ out, long out_stride, int Hq, int Hkv,
-    float scale, int causal, float rescale_thr, int xcd) {
+    float scale, int causal, float rescale_thr, int xcd, const int* __restrict__ rope_pos,
+    const float* __restrict__ rope_cs) {
   extern __shared__ __attribute__((aligned(16))) char pf_smem[];
   constexpr int PAGE = BS * HD;
   // buffer b: K pages at b*4*PAGE + {0, PAGE}, V pages at b*4*PAGE + 2*PAGE + {0, PAGE}
@@ -805,6 +806,15 @@ __global__ void __launch_bounds__(64 * PW, 8 / PW) paged_prefill_kernel(
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();     // every wave holds its Q before the ring reuses the slots
+    // fused rotary embedding of q (rope_cs != nullptr): the rope/cache kernel
+    // then leaves q untouched and skips its read-modify-write of the q rows
+    // (3/4 of that kernel's traffic at G = 4); same fp32 expression and bf16
+    // rounding as the cache kernel (rope_q_frags, shared with decode)
+    if (rope_cs) {
+#pragma unroll
+      for (int n = 0; n < PF_NG; ++n)
+        if (valid[n]) rope_q_frags<HD>(qf[n], rope_cs + (long)rope_pos[qbeg + qi[n]] * HD, g);
+    }
   }
   // smallest column limit of the wave: tiles below it need no mask
   int wave_lo = INT_MAX;
@@ -1008,11 +1018,15 @@ void set_prefill_xcd(int on) { g_prefill_xcd = on < 0 ? 0 : (on > 2 ? 2 : on); }
 // q_per_tile: the tile list's queries per workgroup (ops.prefill_q_per_tile);
 // it selects the workgroup width PW = q_per_tile / (column groups x 16/G):
 // 4 or 8 waves (8 only at head dim 128)
+// rope_pos / rope_cs (both or neither): rotate q in the kernel (q rows of qkv
+// unrotated; positions per row, cos_sin [max_pos][D] as rope_cache.hip)
 int paged_prefill(const void* q, long q_stride, const void* k_cache, const void* v_cache,
                   const int* block_tables, int bt_stride, const int* cu_q,
                   const int* context_lens, const int* tiles, int num_tiles, void* out,
                   long out_stride, int Hq, int Hkv, int D, int block_size, float scale,
-                  int causal, int q_per_tile, hipStream_t stream) {
+                  int causal, int q_per_tile, const int* rope_pos, const float* rope_cs,
+                  hipStream_t stream) {
+  if ((rope_pos == nullptr) != (rope_cs == nullptr)) return -4;
   if (num_tiles <= 0) return 0;
   if ((D != 128 && D != 64) || block_size != BS) return -1;
   if (Hq % Hkv != 0 || Hq / Hkv > 16) return -2;
@@ -1032,7 +1046,7 @@ int paged_prefill(const void* q, long q_stride, const void* k_cache, const void*
                                            stream>>>(                                         \
         (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache,           \
         block_tables, bt_stride, cu_q, context_lens, tiles, (bf16_t*)out, out_stride, Hq, Hkv, \
-        scale, causal, g_prefill_rescale_thr, g_prefill_xcd);                                 \
+        scale, causal, g_prefill_rescale_thr, g_prefill_xcd, rope_pos, rope_cs);              \
   }
   // 2 slots by default: 3 measured equal at D = 64 and 1.55x slower at D = 128
   // with 4-wave workgroups (96 KB of LDS leaves one workgroup per CU) --

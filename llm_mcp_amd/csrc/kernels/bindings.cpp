@@ -17,7 +17,7 @@ int rmsnorm(void*, void*, const void*, const void*, int, int, long, long, float,
 int layernorm(void*, const void*, const void*, const void*, const void*, int, int, float,
               hipStream_t);
 int rope_cache(void*, long, const int*, const float*, int, int, int, int, const int*, void*, void*,
-               int, int, int, const void*, const void*, float, hipStream_t);
+               int, int, int, const void*, const void*, float, int, hipStream_t);
 int kv_write(const void*, const void*, long, const int*, int, int, int, void*, void*, int,
              hipStream_t);
 void set_decode_mode(int);
@@ -31,7 +31,7 @@ int paged_decode(const void*, long, const void*, const void*, const int*, int, c
                  const float*, const int*, hipStream_t);
 int paged_prefill(const void*, long, const void*, const void*, const int*, int, const int*,
                   const int*, const int*, int, void*, long, int, int, int, int, float, int, int,
-                  hipStream_t);
+                  const int*, const float*, hipStream_t);
 int sample(const void*, int, long, int, int, const float*, const int*, const float*,
            const uint64_t*, const int*, int*, float*, int, hipStream_t);
 int glu(void*, const void*, long, int, int, int, hipStream_t);
@@ -103,10 +103,11 @@ PYBIND11_MODULE(_lmx_kernels, m) {
   });
   m.def("rope_cache", [](uptr qkv, long qkv_stride, uptr positions, uptr cos_sin, int T, int Hq,
                          int Hkv, int D, uptr slots, uptr kc, uptr vc, int BS, int rot_k,
-                         int tile_from, uptr q_norm, uptr k_norm, float eps, uptr stream) {
+                         int tile_from, uptr q_norm, uptr k_norm, float eps, int skip_q,
+                         uptr stream) {
     check(lmx::rope_cache(P<void>(qkv), qkv_stride, P<int>(positions), P<float>(cos_sin), T, Hq, Hkv,
                           D, P<int>(slots), P<void>(kc), P<void>(vc), BS, rot_k, tile_from,
-                          P<void>(q_norm), P<void>(k_norm), eps, S(stream)),
+                          P<void>(q_norm), P<void>(k_norm), eps, skip_q, S(stream)),
           "rope_cache");
   });
   m.def("kv_write", [](uptr k, uptr v, long stride, uptr slots, int T, int Hkv, int D, uptr kc,
@@ -139,11 +140,12 @@ PYBIND11_MODULE(_lmx_kernels, m) {
   m.def("paged_prefill", [](uptr q, long q_stride, uptr kc, uptr vc, uptr bt, int bt_stride,
                             uptr cu_q, uptr ctx, uptr tiles, int num_tiles, uptr out,
                             long out_stride, int Hq, int Hkv, int D, int BS, float scale,
-                            int causal, int q_per_tile, uptr stream) {
+                            int causal, int q_per_tile, uptr rope_pos, uptr rope_cs,
+                            uptr stream) {
     check(lmx::paged_prefill(P<void>(q), q_stride, P<void>(kc), P<void>(vc), P<int>(bt),
                              bt_stride, P<int>(cu_q), P<int>(ctx), P<int>(tiles), num_tiles,
                              P<void>(out), out_stride, Hq, Hkv, D, BS, scale, causal, q_per_tile,
-                             S(stream)),
+                             P<int>(rope_pos), P<float>(rope_cs), S(stream)),
           "paged_prefill");
   });
   m.def("sample", [](uptr logits, int is_bf16, long stride, int B, int V, uptr temp, uptr topk,

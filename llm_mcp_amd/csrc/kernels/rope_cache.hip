@@ -142,7 +142,7 @@ __global__ void __launch_bounds__(256) rope_cache_tiled_kernel(
     const float* __restrict__ cos_sin, int row0, int T, int Hq, int Hkv, int D,
     const int* __restrict__ slot_mapping, bf16_t* __restrict__ k_cache,
     bf16_t* __restrict__ v_cache, int BS, int rotate_k_inplace,
-    const bf16_t* __restrict__ q_norm, const bf16_t* __restrict__ k_norm, float eps) {
+    const bf16_t* __restrict__ q_norm, const bf16_t* __restrict__ k_norm, float eps, int skip_q) {
   __shared__ __attribute__((aligned(16))) bf16_t vt[RT * (256 + 8)];
   __shared__ int sslot[RT];
   const int t0 = row0 + blockIdx.x * RT;
@@ -164,7 +164,8 @@ __global__ void __launch_bounds__(256) rope_cache_tiled_kernel(
     const float4 c = *reinterpret_cast<const float4*>(cs + i);
     const float4 sn = *reinterpret_cast<const float4*>(cs + half + i);
     const float cc[4] = {c.x, c.y, c.z, c.w}, ss[4] = {sn.x, sn.y, sn.z, sn.w};
-    for (int h0 = 0; h0 < H; h0 += HU) {
+    // skip_q: the prefill attention rotates q itself (paged_prefill rope_cs)
+    for (int h0 = skip_q ? Hq : 0; h0 < H; h0 += HU) {
       bf16x4_t x1[HU], x2[HU];
 #pragma unroll
       for (int u = 0; u < HU; ++u) {
@@ -248,8 +249,10 @@ __global__ void __launch_bounds__(256) rope_cache_tiled_kernel(
 int rope_cache(void* qkv, long qkv_stride, const int* positions, const float* cos_sin, int T,
                int Hq, int Hkv, int D, const int* slot_mapping, void* k_cache, void* v_cache,
                int BS, int rotate_k_inplace, int tile_from, const void* q_norm,
-               const void* k_norm, float eps, hipStream_t stream) {
+               const void* k_norm, float eps, int skip_q, hipStream_t stream) {
   if (T <= 0) return 0;
+  // skip_q only for the tiled (prefill) rows and without q/k norms
+  if (skip_q && (tile_from > 0 || q_norm != nullptr)) return -1;
   if (D % 8 != 0 || D > 256) return -1;
   if ((q_norm == nullptr) != (k_norm == nullptr) || (q_norm && D != 128)) return -1;
   const int n1 = tile_from < 0 ? 0 : (tile_from > T ? T : tile_from);
@@ -272,7 +275,7 @@ int rope_cache(void* qkv, long qkv_stride, const int* positions, const float* co
     rope_cache_tiled_kernel<<<dim3((T - n1 + RT - 1) / RT), dim3(256), 0, stream>>>(
         (bf16_t*)qkv, qkv_stride, positions, cos_sin, n1, T, Hq, Hkv, D, slot_mapping,
         (bf16_t*)k_cache, (bf16_t*)v_cache, BS, rotate_k_inplace, (const bf16_t*)q_norm,
-        (const bf16_t*)k_norm, eps);
+        (const bf16_t*)k_norm, eps, skip_q);
   return (int)hipGetLastError();
 }
 

@@ -186,6 +186,7 @@ class LlamaModel:
                                         cfg.rope_scaling)
         # K2 + K5 inside K4 for decode rows (LMX_FUSED_DECODE_ROPE=0: separate kernels)
         self.fuse_decode_rope = os.environ.get("LMX_FUSED_DECODE_ROPE", "1") == "1"
+        self.fuse_prefill_rope = os.environ.get("LMX_FUSED_PREFILL_ROPE", "0") == "1"
         if weights is None:
             weights = self._random_weights(seed)
         self.w = weights
@@ -282,7 +283,17 @@ class LlamaModel:
             # kernel (one launch and one boundary fewer per layer); prefill rows
             # (and q/k-norm models) keep the rope/cache kernels
             fuse = nd > 0 and self.fuse_decode_rope and "q_norm" not in L
-            if not fuse:
+            # prefill rows: q rotated inside the prefill attention kernel (the
+            # rope/cache kernel then only rotates k and writes the cache)
+            fuse_pf = T > nd and self.fuse_prefill_rope and "q_norm" not in L and qkv.is_cuda
+            if fuse_pf:
+                if nd > 0 and not fuse:
+                    ops.rope_and_cache(qkv[:nd], inp.positions[:nd], self.cos_sin, Hq, Hkv, D,
+                                       inp.slots[:nd], kc, vc, tile_from=nd, eps=cfg.rms_eps)
+                ops.rope_and_cache(qkv[nd:], inp.positions[nd:], self.cos_sin, Hq, Hkv, D,
+                                   inp.slots[nd:], kc, vc, tile_from=0, eps=cfg.rms_eps,
+                                   skip_q=True)
+            elif not fuse:
                 ops.rope_and_cache(qkv, inp.positions, self.cos_sin, Hq, Hkv, D, inp.slots, kc,
                                    vc, tile_from=nd, q_norm=L.get("q_norm"),
                                    k_norm=L.get("k_norm"), eps=cfg.rms_eps)
@@ -298,7 +309,9 @@ class LlamaModel:
             if T > nd:
                 ops.paged_prefill_attention(qkv, kc, vc, inp.block_tables[nd:],
                                             inp.cu_q[nd:], inp.context_lens[nd:],
-                                            inp.prefill_tiles, self.scale, attn, Hq=Hq)
+                                            inp.prefill_tiles, self.scale, attn, Hq=Hq,
+                                            rope=(inp.positions, self.cos_sin) if fuse_pf
+                                            else None)
             # TP = 1: the O projection may hand its split-K partials straight
             # to the residual-add RMSNorm (ops.Partials; K11 epi 2)
             o = ops.linear(attn, L["wo"], defer=tp.size == 1)

@@ -164,18 +164,24 @@ def rope_and_cache(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Te
                    k_cache: torch.Tensor | None, v_cache: torch.Tensor | None,
                    rotate_k_inplace: bool = False, tile_from: int | None = None,
                    q_norm: torch.Tensor | None = None, k_norm: torch.Tensor | None = None,
-                   eps: float = 1e-6) -> None:
+                   eps: float = 1e-6, skip_q: bool = False) -> None:
     """In-place rotary on q (and k) heads of the fused QKV rows; k and v are
     scattered into the paged cache at ``slots`` (-1 = skip).  Rows from
     ``tile_from`` on (prefill chunks: consecutive slots) use the 32-token
     tiled kernel with coalesced transposed-V page writes; rows before it
     (decode: one token per page) the per-token kernel.  Default: all tiled.
     ``q_norm`` / ``k_norm`` ([D] weights, D = 128): per-head RMSNorm of q and
-    k before the rotation (Qwen3), fused into the same pass."""
+    k before the rotation (Qwen3), fused into the same pass.  ``skip_q``
+    (tiled rows only, no norms): leave the q heads unrotated -- the prefill
+    attention rotates q itself (``paged_prefill_attention(rope=...)``)."""
     if not qkv.is_cuda:
+        q_keep = qkv[:, :Hq * D].clone() if skip_q else None
         ref.rope_cache(qkv, positions, cos_sin, Hq, Hkv, D, slots, k_cache, v_cache,
                        rotate_k_inplace, q_norm, k_norm, eps)
+        if skip_q:
+            qkv[:, :Hq * D] = q_keep
         return
+    _chk(not skip_q or (q_norm is None and not tile_from), "skip_q: tiled rows without q/k norms")
     if q_norm is not None:
         _chk(k_norm is not None and D == 128 and q_norm.numel() == D and k_norm.numel() == D
              and q_norm.dtype == torch.bfloat16 and k_norm.dtype == torch.bfloat16,
@@ -195,7 +201,7 @@ def rope_and_cache(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Te
     native().rope_cache(_ptr(qkv), qkv.stride(0), _ptr(positions), _ptr(cos_sin), T, Hq, Hkv, D,
                         _ptr(slots), _ptr(k_cache), _ptr(v_cache), BS,
                         int(rotate_k_inplace), 0 if tile_from is None else int(tile_from),
-                        _ptr(q_norm), _ptr(k_norm), float(eps), _stream())
+                        _ptr(q_norm), _ptr(k_norm), float(eps), int(skip_q), _stream())
 
 
 def kv_write(k, v, slots, k_cache, v_cache):
@@ -283,14 +289,20 @@ def decode_order(context_lens) -> "np.ndarray":
 def paged_prefill_attention(q: torch.Tensor, k_cache, v_cache, block_tables, cu_q,
                             context_lens, tiles, scale: float, out: torch.Tensor,
                             causal: bool = True, Hq: int | None = None,
-                            q_per_tile: int | None = None) -> torch.Tensor:
+                            q_per_tile: int | None = None, rope=None) -> torch.Tensor:
     """Varlen prefill. q/out: [T, Hq*D] rows; tiles: int32 [(seq, q_start)]
     built with ``q_per_tile`` queries per tile (default
     ``prefill_q_per_tile(Hq, Hkv, D)``; the kernel's workgroup width follows
-    from it)."""
+    from it).  ``rope`` = (positions int32 [rows], cos_sin fp32 [P, D]): q is
+    unrotated and the kernel applies the rotary embedding (the rope/cache
+    kernel ran with ``skip_q``)."""
     NB, Hkv, BS, D = k_cache.shape
     T = q.shape[0]
     Hq = Hq or (q.shape[1] // D)
+    if rope is not None and not q.is_cuda:
+        qr = q[:, :Hq * D].clone()
+        ref.rope_cache(qr, rope[0], rope[1], Hq, 0, D, None, None, None, False, None, None, 1e-6)
+        q = qr
     if not q.is_cuda:
         o = ref.paged_prefill(q[:, : Hq * D].reshape(T, Hq, D), k_cache, v_cache, block_tables,
                               cu_q, context_lens, scale, causal)
@@ -306,7 +318,9 @@ def paged_prefill_attention(q: torch.Tensor, k_cache, v_cache, block_tables, cu_
                            _ptr(block_tables), block_tables.stride(0), _ptr(cu_q),
                            _ptr(context_lens), _ptr(tiles), num_tiles, _ptr(out), out.stride(0),
                            Hq, Hkv, D, BS, float(scale), int(causal),
-                           q_per_tile or prefill_q_per_tile(Hq, Hkv, D), _stream())
+                           q_per_tile or prefill_q_per_tile(Hq, Hkv, D),
+                           _ptr(rope[0]) if rope is not None else 0,
+                           _ptr(rope[1]) if rope is not None else 0, _stream())
     return out
 
 

@@ -772,3 +772,48 @@ def test_linear_decode_lm_head_runs_k13_sk():
     assert ops.PGEMM_CALLS[0] - before == 1
     torch.testing.assert_close(y.float(), torch.nn.functional.linear(x, w).float(),
                                atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("Hq,Hkv,D", [(32, 8, 128), (12, 12, 64), (28, 4, 128)])
+def test_prefill_fused_q_rope(Hq, Hkv, D):
+    """Prefill rows with the q rotation inside the attention kernel: the
+    rope/cache kernel with skip_q leaves q untouched and writes the same K/V
+    cache; the attention over the unrotated q with rope=(positions, cos_sin)
+    matches the fp32 reference over the rotated q."""
+    qlens, prefix = [70, 33, 256], [40, 0, 100]
+    ctxs = [q + p for q, p in zip(qlens, prefix)]
+    S = len(qlens)
+    NB = sum(math.ceil(c / 32) for c in ctxs) + 2
+    kc, vc = _cache(NB, Hkv, D)
+    bt = _random_tables(S, ctxs, NB)
+    T = sum(qlens)
+    qkv = _bf(T, (Hq + 2 * Hkv) * D)
+    pos = torch.cat([torch.arange(p, p + q) for q, p in zip(qlens, prefix)]).to(torch.int32).to(DEV)
+    # slot of the token at position p of sequence s: page bt[s][p // 32], offset p % 32
+    slots = torch.cat([bt[s].long()[torch.arange(p, p + q, device=DEV) // 32] * 32 +
+                       torch.arange(p, p + q, device=DEV) % 32
+                       for s, (q, p) in enumerate(zip(qlens, prefix))]).to(torch.int32)
+    cs = ref.rope_cos_sin(4096, D, 500000.0, DEV)
+    kc2, vc2, qkv2 = kc.clone(), vc.clone(), qkv.clone()
+    q0 = qkv[:, :Hq * D].clone()
+    ops.rope_and_cache(qkv, pos, cs, Hq, Hkv, D, slots, kc, vc, tile_from=0, skip_q=True)
+    ops.rope_and_cache(qkv2, pos, cs, Hq, Hkv, D, slots, kc2, vc2, tile_from=0)
+    assert torch.equal(qkv[:, :Hq * D], q0)              # q left unrotated
+    assert torch.equal(kc, kc2) and torch.equal(vc, vc2)
+    cu = torch.tensor([0] + list(torch.cumsum(torch.tensor(qlens), 0)), dtype=torch.int32,
+                      device=DEV)
+    qpt = ops.prefill_q_per_tile(Hq, Hkv, D)
+    tiles = torch.tensor([v for s, ql in enumerate(qlens) for q0 in range(0, ql, qpt)
+                          for v in (s, q0)], dtype=torch.int32, device=DEV)
+    ctx = torch.tensor(ctxs, dtype=torch.int32, device=DEV)
+    scale = 1 / math.sqrt(D)
+    out = torch.zeros(T, Hq * D, dtype=torch.bfloat16, device=DEV)
+    ops.paged_prefill_attention(qkv, kc, vc, bt, cu, ctx, tiles, scale, out, causal=True, Hq=Hq,
+                                rope=(pos, cs))
+    out2 = torch.zeros_like(out)
+    ops.paged_prefill_attention(qkv2, kc2, vc2, bt, cu, ctx, tiles, scale, out2, causal=True,
+                                Hq=Hq)
+    # same bf16 rounding of the rotated q in both paths
+    torch.testing.assert_close(out.float(), out2.float(), atol=1e-2, rtol=1e-2)
+    expect = ref.paged_prefill(qkv2[:, :Hq * D].reshape(T, Hq, D), kc2, vc2, bt, cu, ctx, scale)
+    torch.testing.assert_close(out.float().view(T, Hq, D), expect.float(), atol=2e-2, rtol=2e-2)

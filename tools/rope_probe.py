@@ -35,7 +35,7 @@ def main():
 
     def call(slot_p, k_p, v_p):
         nat.rope_cache(qkv.data_ptr(), qkv.stride(0), pos.data_ptr(), cs.data_ptr(), T, Hq, Hkv, D,
-                       slot_p, k_p, v_p, BS, 0, T, 0, 0, 1e-6, st)
+                       slot_p, k_p, v_p, BS, 0, T, 0, 0, 1e-6, 0, st)
 
     variants = {
         "full": (slots.data_ptr(), kc.data_ptr(), vc.data_ptr()),
@@ -52,14 +52,14 @@ def main():
     for _ in range(5):
         nat.rope_cache(qkvp.data_ptr(), qkvp.stride(0), posp.data_ptr(), cs.data_ptr(), TP, Hq,
                        Hkv, D, slotsp.data_ptr(), kcp.data_ptr(), vcp.data_ptr(), BS, 0, 0, 0, 0,
-                       1e-6, st)
+                       1e-6, 0, st)
     torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
     for _ in range(50):
         nat.rope_cache(qkvp.data_ptr(), qkvp.stride(0), posp.data_ptr(), cs.data_ptr(), TP, Hq,
                        Hkv, D, slotsp.data_ptr(), kcp.data_ptr(), vcp.data_ptr(), BS, 0, 0, 0, 0,
-                       1e-6, st)
+                       1e-6, 0, st)
     e.record()
     torch.cuda.synchronize()
     print(f"rope_cache tiled T={TP} {s.elapsed_time(e) / 50 * 1e3:7.2f} us", flush=True)
