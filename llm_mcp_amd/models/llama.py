@@ -186,7 +186,7 @@ class LlamaModel:
                                         cfg.rope_scaling)
         # K2 + K5 inside K4 for decode rows (LMX_FUSED_DECODE_ROPE=0: separate kernels)
         self.fuse_decode_rope = os.environ.get("LMX_FUSED_DECODE_ROPE", "1") == "1"
-        self.fuse_prefill_rope = os.environ.get("LMX_FUSED_PREFILL_ROPE", "0") == "1"
+        self.fuse_prefill_rope = os.environ.get("LMX_FUSED_PREFILL_ROPE", "1") == "1"
         if weights is None:
             weights = self._random_weights(seed)
         self.w = weights
