@@ -25,9 +25,9 @@ a batch are packed (cu_seqlens), never padded.
 from __future__ import annotations
 
 import math
+import os
 
 import numpy as np
-
 import torch
 
 from .. import ops
@@ -46,6 +46,9 @@ class NomicBertModel:
         self.H, self.D = cfg.num_heads, cfg.head_dim
         self.scale = 1.0 / math.sqrt(self.D)
         self.cos_sin = ref.rope_cos_sin(cfg.max_position, self.D, cfg.rope_theta, self.device)
+        # q rotation inside the attention kernel: off by default for the
+        # encoder (one A/B: 2,674 fused vs 2,760 emb/s unfused on nomic)
+        self.fuse_q_rope = os.environ.get("LMX_FUSED_ENCODER_ROPE", "0") == "1"
         self.w = weights or self._random_weights(seed)
         # gate/up rows interleaved for the fused SwiGLU epilogue: per 16
         # channels for K13 (the large-M GEMM; the default), per BN/2 channels
@@ -138,9 +141,12 @@ class NomicBertModel:
         attn = torch.empty((T, H * D), dtype=self.dtype, device=dev)
         for L in w["layers"]:
             qkv = self._linear(x, L["wqkv"])
-            ops.rope_and_cache(qkv, pos_t, self.cos_sin, H, H, D, slots_t, kc, vc)
+            # q rotated inside the attention kernel when LMX_FUSED_ENCODER_ROPE=1
+            fq = self.fuse_q_rope and qkv.is_cuda
+            ops.rope_and_cache(qkv, pos_t, self.cos_sin, H, H, D, slots_t, kc, vc, skip_q=fq)
             ops.paged_prefill_attention(qkv, kc, vc, bt, cu, ctx, tiles_t, self.scale, attn,
-                                        causal=False, Hq=H)
+                                        causal=False, Hq=H,
+                                        rope=(pos_t, self.cos_sin) if fq else None)
             o = self._linear(attn, L["wo"])
             h = ops.layer_norm(o, L["ln1_w"], L["ln1_b"], cfg.ln_eps, residual=x)
             if "w_gu_il" in L and self.gu_k13 and h.is_cuda:
