@@ -81,6 +81,9 @@ def parse(argv=None):
                          "--closed-warmup seconds; a separate record, never the headline)")
     ap.add_argument("--duration", type=float, default=30.0)
     ap.add_argument("--closed-warmup", type=float, default=10.0)
+    ap.add_argument("--cpu", action="store_true",
+                    help="plumbing mode for tests: every rank runs its engine on the CPU (gloo; "
+                         "use a tiny model such as tiny-llama); never a reported number")
     ap.add_argument("--rehearse-on-one-gpu", action="store_true",
                     help="multi-rank rehearsal on a 1-GPU box: every rank uses device 0 with a "
                          "fixed KV budget (never used for reported numbers)")
@@ -175,15 +178,23 @@ def main() -> None:
     from llm_mcp_amd.engine.ipc import EngineServer
 
     gpu = 0 if a.rehearse_on_one_gpu else local_rank
-    torch.cuda.set_device(gpu)
-    dev = torch.device("cuda", gpu)
+    if a.cpu:
+        dev = torch.device("cpu")
+    else:
+        torch.cuda.set_device(gpu)
+        dev = torch.device("cuda", gpu)
+
+    def sync():
+        if not a.cpu:
+            torch.cuda.synchronize()
     if world > 1:
         # control plane only (barriers, timing, per-GPU stats): data-parallel
         # serving exchanges no tensors between GPUs
         import datetime
         os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
         dist.init_process_group("gloo", timeout=datetime.timedelta(minutes=60))
-    ops.native()  # fail loudly if the HIP kernels are missing
+    if not a.cpu:
+        ops.native()  # fail loudly if the HIP kernels are missing
     tpctx = None
     if a.tp > 1:
         # every rank creates every group's subgroups, in the same order
@@ -193,7 +204,8 @@ def main() -> None:
             # one GPU per rank: RCCL over xGMI; a one-GPU rehearsal cannot put
             # several ranks of one communicator on one device: gloo + the
             # peer-memory all-reduce kernel (decode sizes)
-            tg = dist.new_group(ranks, backend="gloo" if a.rehearse_on_one_gpu else "nccl")
+            tg = dist.new_group(ranks, backend="gloo" if (a.rehearse_on_one_gpu or a.cpu)
+                                else "nccl")
             cg = dist.new_group(ranks, backend="gloo")
             if g == grp:
                 tpctx = TPContext(grank, a.tp, tg, cpu_group=cg)
@@ -203,7 +215,9 @@ def main() -> None:
                         max_batched_tokens=a.max_batched_tokens,
                         max_model_len=min(8192, a.prompt_len + a.max_tokens + 64),
                         use_graphs=not a.no_graphs, seed=rank,
-                        kv_cache_gb=24 if a.rehearse_on_one_gpu else None)
+                        # rehearsal: every rank shares cuda:0's 288 GB
+                        kv_cache_gb=(max(4, min(24, 160 // world)) if a.rehearse_on_one_gpu
+                                     else None) if not a.cpu else 0.05)
     follower = None
     if tpctx is None:
         engine = LLMEngine(ecfg, device=dev)
@@ -217,7 +231,7 @@ def main() -> None:
             follower = threading.Thread(target=engine.run_follower, name="tp-follower",
                                         daemon=True)
             follower.start()
-    log(f"engine ready on cuda:{gpu} in {time.time() - t_init:.1f}s: {engine.num_blocks} KV "
+    log(f"engine ready on {dev} in {time.time() - t_init:.1f}s: {engine.num_blocks} KV "
         f"blocks, {len(engine.graphs)} decode graphs, "
         f"weights {engine.model.weight_bytes() / 1e9:.1f} GB"
         + (f" (TP rank {grank}/{a.tp} of engine {grp})" if a.tp > 1 else ""))
@@ -290,16 +304,16 @@ def main() -> None:
     cpu0 = {k: cpu_s(v) for k, v in procs.items()}
 
     if a.load == "closed":
-        closed(a, rank, world, n_eng, lgs, barrier)
+        closed(a, rank, world, n_eng, lgs, barrier, sync)
         shutdown(a, world, lgs, apis, server, ready_files, engine, follower)
         return
 
     barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     results = waves(a.steps, "step") if rank == 0 else []
     barrier()           # the other ranks serve until rank 0's waves are done
-    torch.cuda.synchronize()
+    sync()
     barrier()
     elapsed = time.perf_counter() - t0
 
@@ -383,6 +397,9 @@ def main() -> None:
             out["rehearsal_one_gpu"] = True
             out["config"]["parallelism"] += " (rehearsal: every rank on cuda:0, NOT an "\
                                             f"{world}-GPU number)"
+        if a.cpu:
+            out["cpu_plumbing"] = True
+            out["config"]["parallelism"] += " (CPU plumbing test, NOT a GPU number)"
         print(json.dumps(out), flush=True)
     barrier()
     shutdown(a, world, lgs, apis, server, ready_files, engine, follower)
@@ -418,13 +435,12 @@ def shutdown(a, world, lgs, apis, server, ready_files, engine=None, follower=Non
         dist.destroy_process_group()
 
 
-def closed(a, rank, world, n_eng, lgs, barrier) -> None:
+def closed(a, rank, world, n_eng, lgs, barrier, sync) -> None:
     """--load closed: one constant-concurrency window through the same front
     door; prints its own JSON line (metric tagged "closed loop")."""
-    import torch
     from llm_mcp_amd.bench.loadgen import percentile
     barrier()
-    torch.cuda.synchronize()
+    sync()
     parts = []
     if rank == 0:
         for p in lgs:

@@ -362,8 +362,14 @@ class ControlPlane:
             return write_error(400, "device_id_required", "Field device_id is required")
         await self.db(self.store.set_device_status, dev, "offline",
                       {"last_error": body.get("reason", ""), "last_error_at": iso(time.time())})
-        await self.db(self.store.release_device_leases, dev)
-        return write_json(200, {"ok": True})
+        n = await self.db(self.store.release_device_leases, dev)
+        # every job still leased on the device failed there: feed the breaker
+        # once per released lease (at least once for the report itself) -- the
+        # workers' own fail reports for those jobs race this release and may
+        # come back lease_lost, so they cannot be relied on to trip it
+        for _ in range(max(1, int(n or 0))):
+            self.st.circuit.record(dev, False)
+        return write_json(200, {"ok": True, "released": int(n or 0)})
 
     # ----------------------------------------------------------- discovery --
     async def discovery_run(self, request):
@@ -529,7 +535,8 @@ class ControlPlane:
                         "latency_ms": tags.get("latency_ms"),
                         "last_seen": iso(d.get("last_seen")), "_last_seen": d.get("last_seen"),
                         "tags": tags, "stats": self.store.device_stats_7d(d["id"]),
-                        "circuit": self.st.circuit.status(d["id"])})
+                        "circuit": self.st.circuit.status(d["id"]),
+                        "circuit_trips": self.st.circuit.trips.get(d["id"], 0)})
         out.sort(key=lambda x: (x["status"] != "online", x["name"]))
         return out
 

@@ -295,20 +295,27 @@ def bench_mixed(a) -> dict:
                "sync_every": a.sync_every, "max_tokens": a.max_tokens,
                "fault": a.fault, "fault_device": a.fault_device}
         circ: dict[str, set] = {}
+        trips: dict[str, int] = {}
+        status_seen: dict[str, set] = {}
+
+        async def poll_dashboard(s):
+            async with s.get(url + "/v1/dashboard") as r:
+                d = await r.json()
+            for dev in d.get("devices") or []:
+                k = dev.get("id", "?")
+                circ.setdefault(k, set()).add(dev.get("circuit", "ok"))
+                status_seen.setdefault(k, set()).add(dev.get("status", "?"))
+                trips[k] = max(trips.get(k, 0), int(dev.get("circuit_trips") or 0))
 
         async def watch_circuit():
             import aiohttp
             async with aiohttp.ClientSession() as s:
                 while True:
                     try:
-                        async with s.get(url + "/v1/dashboard") as r:
-                            d = await r.json()
-                        for dev in d.get("devices") or []:
-                            circ.setdefault(dev.get("id", "?"), set()).add(
-                                dev.get("circuit", "ok"))
+                        await poll_dashboard(s)
                     except Exception:
                         pass
-                    await asyncio.sleep(1.0)
+                    await asyncio.sleep(0.25)
 
         async def run():
             w = asyncio.ensure_future(watch_circuit())
@@ -318,7 +325,16 @@ def bench_mixed(a) -> dict:
             finally:
                 w.cancel()
         out.update(loop.run_until_complete(run()))
+
+        async def final_poll():
+            import aiohttp
+            async with aiohttp.ClientSession() as s:
+                await poll_dashboard(s)
+        loop.run_until_complete(final_poll())
         out["circuit_states_seen"] = {k: sorted(v) for k, v in circ.items()}
+        # breaker trips (ok -> degraded transitions) counted by the core itself
+        out["circuit_trips"] = trips
+        out["device_status_seen"] = {k: sorted(v) for k, v in status_seen.items()}
 
         async def workers():
             import aiohttp

@@ -26,6 +26,9 @@
 // their reads of parity e) completed, so no trailing barrier is needed.
 // Every wait is bounded (spin_max polls): a missing peer sets the error word
 // and the kernel still exits, so the grid always drains.
+// The same regions also carry the decode step's logits all-gather (mode 2/3
+// of the kernel), so a TP group's captured decode graph holds no RCCL
+// collective at all.
 #include <cstring>
 
 #include "common.h"
@@ -93,7 +96,26 @@ __global__ void __launch_bounds__(AR_THREADS) allreduce_kernel(
   auto in_slot = [&](int q) { return reinterpret_cast<u16x8*>(peers.p[q] + par_off); };
   auto res_slot = [&](int q) { return reinterpret_cast<u16x8*>(peers.p[q] + par_off + slot_bytes); };
 
-  if (!two_shot) {
+  if (two_shot >= 2) {
+    // all-gather (X3, the vocab-parallel logits of a decode step): every rank
+    // publishes its n8-chunk input in its own slot; mode 2: every rank reads
+    // all W chunks into out[q * n8 + i]; mode 3: only rank 0 reads (the
+    // others only publish -- a gather to the sampling leader).  Same parity
+    // / epoch protocol as the reductions: a rank reaches call e + 2 only
+    // after every peer signalled in call e + 1, i.e. after the readers'
+    // call-e kernels completed.
+    const long per = (n8 + nb - 1) / nb, lo = b * per, hi = min(n8, lo + per);
+    u16x8* mine = in_slot(rank);
+    for (long i = lo + t; i < hi; i += AR_THREADS) mine[i] = inp[i];
+    ar_barrier<W>(peers, rank, 0, b, e, spin_max);
+    if (two_shot == 2 || rank == 0) {
+#pragma unroll
+      for (int q = 0; q < W; ++q) {
+        const u16x8* src = q == rank ? inp : in_slot(q);
+        for (long i = lo + t; i < hi; i += AR_THREADS) out[q * n8 + i] = src[i];
+      }
+    }
+  } else if (!two_shot) {
     const long per = (n8 + nb - 1) / nb, lo = b * per, hi = min(n8, lo + per);
     u16x8* mine = in_slot(rank);
     for (long i = lo + t; i < hi; i += AR_THREADS) mine[i] = inp[i];
@@ -194,7 +216,8 @@ int allreduce(void* out, const void* inp, long nbytes, int rank, int world,
   if (world < 2 || world > AR_MAX_W || rank < 0 || rank >= world) return -1;
   if (nbytes % 16 != 0 || nbytes > slot_bytes) return -2;
   const long n8 = nbytes / 16;
-  if (two_shot && n8 % world != 0) return -3;
+  if (two_shot == 1 && n8 % world != 0) return -3;
+  if (two_shot < 0 || two_shot > 3) return -7;
   if (blocks < 1 || blocks > AR_MAX_BLOCKS) return -4;
   if (((uintptr_t)out | (uintptr_t)inp) % 16 != 0) return -5;
   ArPeers p;

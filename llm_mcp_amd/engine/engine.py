@@ -299,12 +299,14 @@ class LLMEngine:
             self._out_evs = [torch.cuda.Event(), torch.cuda.Event()]
         self._slot = 0
         # lookahead stepping (step n+1 scheduled and launched before step n's
-        # tokens are read back): the leader of a GPU engine without a TP plan
-        # channel; LMX_LOOKAHEAD=0 turns it off
-        # (a TP group's plan channel is attached after construction: step()
-        # checks it again)
+        # tokens are read back): on by default for a single-GPU engine;
+        # LMX_LOOKAHEAD=0 turns it off.  In a TP group it is opt-in
+        # (LMX_LOOKAHEAD=1, the sample_all mode below) until an RCCL run with
+        # captured graphs has covered the followers' sampling path; by default
+        # a TP group steps synchronously and the leader ships the tokens.
         la_env = os.environ.get("LMX_LOOKAHEAD", "")
-        self.lookahead = la_env == "1" or (la_env != "0" and self.device.type == "cuda")
+        self.lookahead = la_env == "1" or (la_env != "0" and self.device.type == "cuda"
+                                           and self.tp.size == 1)
         # lookahead in a TP group: the followers sample the step too (the
         # logits are all-gathered to every rank, the sampler is seeded and
         # deterministic), so every rank holds step n's tokens on its device

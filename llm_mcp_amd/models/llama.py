@@ -155,10 +155,18 @@ class TPContext:
             if self.rank:
                 return None
             return torch.cat(parts, dim=-1).to(t.device, non_blocking=True)
-        out = torch.empty((self.size * B, Vs), dtype=src.dtype, device=src.device)
-        torch.distributed.all_gather_into_tensor(out, src, group=self.group)
-        if self.rank and not self.logits_to_all:
-            return None
+        if self.peer is not None and self.peer.gather_supports(src):
+            # one kernel over the peer-memory slots: no RCCL collective in the
+            # captured decode graph (followers only publish unless every rank
+            # samples)
+            out = self.peer.all_gather(src, None, to_all=self.logits_to_all)
+            if out is None:
+                return None
+        else:
+            out = torch.empty((self.size * B, Vs), dtype=src.dtype, device=src.device)
+            torch.distributed.all_gather_into_tensor(out, src, group=self.group)
+            if self.rank and not self.logits_to_all:
+                return None
         return out.view(self.size, B, Vs).permute(1, 0, 2).reshape(B, self.size * Vs)
 
 

@@ -566,6 +566,18 @@ def gemm_splitk_supported(M: int, N: int, K: int) -> bool:
     return 0 < M <= SPLITK_MAX_M and N % 64 == 0 and K % 64 == 0
 
 
+# workspaces a larger request replaced: kept alive for the process lifetime,
+# because decode graphs captured earlier have their addresses baked in (a
+# freed buffer could be handed to another tensor while a graph still writes
+# its slabs there)
+_RETIRED_WS: list = []
+
+
+def _retire_ws(ws) -> None:
+    if ws is not None:
+        _RETIRED_WS.append(ws)
+
+
 def _sk_workspace(dev: torch.device, n_floats: int, n_tickets: int):
     key = (dev.index, _stream())
     ws = _SK_WS.get(key)
@@ -577,6 +589,7 @@ def _sk_workspace(dev: torch.device, n_floats: int, n_tickets: int):
         n_tickets = max(n_tickets, 4096, ws[1].numel() if ws else 0)
         ws = (torch.empty(n_floats, dtype=torch.float32, device=dev),
               torch.zeros(n_tickets, dtype=torch.int32, device=dev))
+        _retire_ws(_SK_WS.get(key))
         _SK_WS[key] = ws
     return ws
 
@@ -662,7 +675,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, defer: bool = False,
                 y += bias
             return y
         if (large_gemm_backend(M, N, K, 0, bias is not None) == "k13"
-                and pgemm_operands_ok(x, w)):
+                and pgemm_operands_ok(x, w) and pgemm_bias_ok(bias, N)):
             return pgemm(x, w, bias=bias)
     return torch.nn.functional.linear(x, w, bias)
 
@@ -904,6 +917,7 @@ def _dg_workspace(dev: torch.device, n_floats: int):
         n_floats = max(n_floats, ws[0].numel() if ws else 0, 1 << 20)
         tickets = ws[1] if ws else torch.zeros(_DG_TICKETS, dtype=torch.int32, device=dev)
         ws = (torch.empty(n_floats, dtype=torch.float32, device=dev), tickets)
+        _retire_ws(_DG_WS.get(key))
         _DG_WS[key] = ws
     return ws
 
@@ -1006,6 +1020,7 @@ def _wg_workspace(dev: torch.device, n_floats: int):
         n_floats = max(n_floats, ws[0].numel() if ws else 0, 1 << 20)
         cnt = ws[1] if ws else torch.zeros(_WG_CNT, dtype=torch.int32, device=dev)
         ws = (torch.empty(n_floats, dtype=torch.float32, device=dev), cnt)
+        _retire_ws(_WG_WS.get(key))
         _WG_WS[key] = ws
     return ws
 
@@ -1068,6 +1083,12 @@ def pgemm_operands_ok(a: torch.Tensor, w: torch.Tensor) -> bool:
             and a.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0)
 
 
+def pgemm_bias_ok(bias: torch.Tensor | None, N: int) -> bool:
+    """A bias K13 reads directly (else the caller keeps the library path)."""
+    return bias is None or (bias.dtype == torch.bfloat16 and bias.numel() == N
+                            and bias.is_contiguous() and bias.data_ptr() % 16 == 0)
+
+
 def pgemm(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, act: int = 0,
           out: torch.Tensor | None = None, grid: int = 0,
           variant: int | None = None) -> torch.Tensor:
@@ -1127,6 +1148,7 @@ def _pg_workspace(dev: torch.device, n_floats: int):
         n_floats = max(n_floats, ws[0].numel() if ws else 0, 1 << 20)
         cnt = ws[1] if ws else torch.zeros(_PG_CNT, dtype=torch.int32, device=dev)
         ws = (torch.empty(n_floats, dtype=torch.float32, device=dev), cnt)
+        _retire_ws(_PG_WS.get(key))
         _PG_WS[key] = ws
     return ws
 

@@ -92,6 +92,26 @@ class PeerAllReduce:
         self.calls += 1
         return out
 
+    def gather_supports(self, t: torch.Tensor) -> bool:
+        """``t`` can be all-gathered through the slots (bf16, 16-B rows)."""
+        return self.supports(t)
+
+    def all_gather(self, t: torch.Tensor, out: torch.Tensor | None,
+                   to_all: bool = True) -> torch.Tensor | None:
+        """Concatenation of every rank's ``t`` (flattened) in rank order:
+        ``out`` [world * t.numel()] elements.  ``to_all`` False: only rank 0
+        receives (``out`` may be None elsewhere); the others only publish."""
+        n = t.numel() * t.element_size()
+        if out is None:
+            out = torch.empty(self.world * t.numel(), dtype=t.dtype, device=t.device) \
+                if (to_all or self.rank == 0) else t
+        blocks = max(1, min(MAX_BLOCKS, n // (16 << 10)))
+        self.k.allreduce(out.data_ptr(), t.data_ptr(), n, self.rank, self.world, self.peers,
+                         self.slot, 2 if to_all else 3, blocks, self.spin_max,
+                         torch.cuda.current_stream(t.device).cuda_stream)
+        self.calls += 1
+        return out if (to_all or self.rank == 0) else None
+
     def error(self, clear: bool = False) -> int:
         """Non-zero when a kernel gave up waiting for a peer (synchronous)."""
         return self.k.ar_error(self.own, int(clear))
@@ -112,9 +132,11 @@ class PeerAllReduce:
         self.own = None
 
     # ------------------------------------------------------------ self-test --
-    def self_test(self, reference_all_reduce, sizes=(4096, 64 << 10, 1 << 20)) -> bool:
+    def self_test(self, reference_all_reduce, sizes=(4096, 64 << 10, 1 << 20),
+                  reference_all_gather=None) -> bool:
         """Compare against ``reference_all_reduce`` (the group's RCCL / gloo
-        path) on seeded data; every rank must agree on the verdict."""
+        path) -- and the all-gather against ``reference_all_gather`` when
+        given -- on seeded data; every rank must agree on the verdict."""
         ok = True
         g = torch.Generator(device="cpu").manual_seed(1234 + self.rank)
         for n in sizes:
@@ -134,6 +156,19 @@ class PeerAllReduce:
                 log.warning("peer all-reduce self-test failed at %d B (max err %.3g, %s)", n,
                             err, timed_out or "no timeout")
                 ok = False
+            if reference_all_gather is not None:
+                want_g = reference_all_gather(x.clone())
+                try:
+                    got_g = self.all_gather(x.clone(), None)
+                    torch.cuda.synchronize(self.device)
+                    same = bool(torch.equal(got_g.view(-1), want_g.view(-1)))
+                    timed_out = self.error(clear=True)
+                except RuntimeError as ex:
+                    same, timed_out = False, str(ex)
+                if not same or timed_out:
+                    log.warning("peer all-gather self-test failed at %d B (%s)", n,
+                                timed_out or "mismatch")
+                    ok = False
         return ok
 
 
@@ -172,7 +207,13 @@ def setup(tp, device: torch.device) -> PeerAllReduce | None:
         if ar is not None:
             ar.close()
         return None
-    if not _agree(ar.self_test(tp.all_reduce), tp):
+    def ref_gather(x):
+        saved, tp.peer = tp.peer, None
+        try:
+            return tp.all_gather_rows(x.view(1, -1)).view(-1)
+        finally:
+            tp.peer = saved
+    if not _agree(ar.self_test(tp.all_reduce, reference_all_gather=ref_gather), tp):
         ar.close()
         return None
     tp.peer = ar

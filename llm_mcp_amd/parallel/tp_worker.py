@@ -44,6 +44,60 @@ def init_group(device: torch.device | str | None = None) -> TPContext:
     return TPContext(rank, size, dist.group.WORLD)
 
 
+class GroupSelfTestError(RuntimeError):
+    pass
+
+
+def group_self_test(tp: TPContext, device: torch.device, timeout_s: float | None = None) -> dict:
+    """Startup check of the TP group's device collectives (RCCL on GPUs):
+    an all-reduce and an all-gather of seeded values, compared exactly with
+    what every rank can compute on the host.  A wrong result raises
+    ``GroupSelfTestError``; a collective that does not return within
+    ``timeout_s`` (LMX_TP_SELFTEST_S, default 180) ends the process with a
+    clear message and exit code 3 instead of hanging the whole launch (a
+    stuck RCCL call cannot be interrupted from Python)."""
+    if tp.size < 2:
+        return {}
+    import threading
+    timeout_s = float(os.environ.get("LMX_TP_SELFTEST_S", "180")) if timeout_s is None \
+        else timeout_s
+    done = threading.Event()
+
+    def watchdog():
+        if not done.wait(timeout_s):
+            msg = (f"TP group self-test: rank {tp.rank}/{tp.size} waited {timeout_s:.0f} s for "
+                   f"the {dist.get_backend(tp.group)} collectives on {device}; a rank is missing "
+                   "or the interconnect is down -- exiting instead of hanging")
+            log.error(msg)
+            print(msg, flush=True)
+            os._exit(3)
+    threading.Thread(target=watchdog, name="tp-selftest-watchdog", daemon=True).start()
+    t0 = time.perf_counter()
+    try:
+        n = 4096
+        x = torch.full((n,), float(tp.rank + 1), dtype=torch.float32, device=device)
+        saved, tp.peer = tp.peer, None          # the group's own collectives only
+        try:
+            tp.all_reduce(x)
+            g = tp.all_gather_rows(torch.full((1, 8), float(tp.rank), device=device))
+        finally:
+            tp.peer = saved
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+        want = tp.size * (tp.size + 1) / 2
+        ok_ar = bool((x.cpu() == want).all())
+        ok_ag = bool((g.cpu() == torch.arange(tp.size, dtype=torch.float32).view(-1, 1)).all())
+    finally:
+        done.set()
+    if not (ok_ar and ok_ag):
+        raise GroupSelfTestError(f"TP group self-test: wrong collective result on rank {tp.rank} "
+                                 f"(all_reduce ok={ok_ar}, all_gather ok={ok_ag})")
+    dt = time.perf_counter() - t0
+    log.info("TP group self-test ok (%s, %d ranks) in %.2f s", dist.get_backend(tp.group),
+             tp.size, dt)
+    return {"backend": dist.get_backend(tp.group), "seconds": round(dt, 3)}
+
+
 def attach_channel(engine, tp: TPContext, tag: str) -> PlanChannel | None:
     """Leader creates the plan mailbox, followers attach after a barrier."""
     if tp.size == 1:
@@ -115,6 +169,7 @@ def build_tp_engine(ecfg, device, tp: TPContext, tag: str, weights_path: str = "
         weights = load_llama_weights(weights_path, cfg, device, tp.rank, tp.size)
     dev = torch.device(device)
     comm = {}
+    selftest = group_self_test(tp, dev) if tp.size > 1 else {}
     if dev.type == "cuda" and tp.size > 1:
         from .peer_allreduce import setup as setup_peer_ar
         setup_peer_ar(tp, dev)
@@ -122,6 +177,7 @@ def build_tp_engine(ecfg, device, tp: TPContext, tag: str, weights_path: str = "
         log.info("TP all-reduce us by message size: %s", comm)
     eng = LLMEngine(ecfg, device=device, model_cfg=cfg, tp=tp, weights=weights)
     eng.tp_comm = comm
+    eng.tp_selftest = selftest
     attach_channel(eng, tp, tag)
     return eng
 

@@ -21,6 +21,10 @@ class CircuitBreaker:
         self.degraded_s = degraded_s
         self._lock = threading.RLock()
         self._c: dict[str, dict] = {}
+        # ok -> degraded transitions per device since start (observability:
+        # a trip can be shorter than any dashboard poll, e.g. a restarted
+        # worker's first success closes it again)
+        self.trips: dict[str, int] = {}
 
     def record(self, device_id: str, success: bool) -> None:
         if not device_id:
@@ -32,6 +36,8 @@ class CircuitBreaker:
             c = self._c.setdefault(device_id, {"failures": 0, "degraded_at": 0.0})
             c["failures"] += 1
             if c["failures"] >= self.threshold:
+                if c["failures"] == self.threshold:
+                    self.trips[device_id] = self.trips.get(device_id, 0) + 1
                 c["degraded_at"] = self.clock()
 
     # reference name

@@ -1,10 +1,11 @@
-"""Peer-memory all-reduce kernel (csrc/kernels/allreduce.hip) on the GPU.
+"""Peer-memory all-reduce and all-gather kernel (csrc/kernels/allreduce.hip) on the GPU.
 
 The 1-GPU box maps every rank's IPC region into the other ranks' processes on
 the same device, so the full protocol runs for real: IPC export/open, the
 flag rendezvous, one-shot and two-shot, in place and out of place, and
 hipGraph replay (device-side epochs).  Each rank checks its result against
-the fp32 sum of every rank's seeded input computed on the host.  Runs before
+the fp32 sum of every rank's seeded input computed on the host; the
+all-gather (the TP logits path) against torch.cat of the shards.  Runs before
 anything in this pytest process touches the GPU (ranks are spawned)."""
 import os
 import socket
@@ -82,6 +83,48 @@ def _rank(rank, world, port, q):
             if not err <= 1e-2 * max(1.0, want.abs().max().item()):
                 errs.append(f"graph replay {salt}: err={err}")
         errs += ["graph: error word set"] if ar.error(clear=True) else []
+        # all-gather (the TP logits path): to every rank and to rank 0 only,
+        # eagerly and interleaved with all-reduces inside one captured graph
+        for salt, (n, to_all) in enumerate([(8, True), (4096, False), (16032 * 4, True),
+                                            (300000, False)], start=200):
+            xs = _inputs(world, n, salt)
+            want = torch.cat(xs)
+            got = ar.all_gather(xs[rank].to(dev), None, to_all=to_all)
+            torch.cuda.synchronize()
+            if to_all or rank == 0:
+                if got is None or not torch.equal(got.cpu(), want):
+                    errs.append(f"all_gather n={n} to_all={to_all} mismatch")
+            elif got is not None:
+                errs.append("all_gather: a follower received the gather")
+        errs += ["all_gather: error word set"] if ar.error(clear=True) else []
+        n = 16032
+        src = torch.zeros(n, dtype=torch.bfloat16, device=dev)
+        red = torch.zeros(4096, dtype=torch.bfloat16, device=dev)
+        gout = torch.zeros(world * n, dtype=torch.bfloat16, device=dev)
+        with torch.cuda.stream(s):
+            ar(red)
+            ar.all_gather(src, gout)
+        torch.cuda.synchronize()
+        dist.barrier()
+        g2 = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g2, stream=s):
+            ar(red)
+            ar.all_gather(src, gout)
+        for salt in range(300, 303):
+            xs, rs = _inputs(world, n, salt), _inputs(world, 4096, salt + 50)
+            src.copy_(xs[rank].to(dev))
+            red.copy_(rs[rank].to(dev))
+            torch.cuda.synchronize()
+            dist.barrier()
+            g2.replay()
+            torch.cuda.synchronize()
+            if not torch.equal(gout.cpu(), torch.cat(xs)):
+                errs.append(f"graph all_gather {salt} mismatch")
+            want = torch.stack([x.float() for x in rs]).sum(0)
+            if not (red.float().cpu() - want).abs().max().item() <= 1e-2 * max(
+                    1.0, want.abs().max().item()):
+                errs.append(f"graph all_reduce after gather {salt}")
+        errs += ["graph all_gather: error word set"] if ar.error(clear=True) else []
         q.put(("done", rank, errs))
     except Exception as ex:   # report instead of hanging the parent
         q.put(("done", rank, [f"{type(ex).__name__}: {ex}"]))

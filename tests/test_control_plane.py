@@ -202,6 +202,18 @@ def test_discovery_devices_dashboard_capacity():
             await c.post("/v1/devices/offline", json={"device_id": "node1:gpu0", "reason": "x"})
             assert st.store.get_device("node1:gpu0")["status"] == "offline"
             assert st.store.get_job(jid)["lease_until"] is None
+            # the offline report fed the breaker once per released lease (>= 1);
+            # three jobs lost on one device trip it (config 5's fault path)
+            assert st.circuit.snapshot()["node1:gpu0"]["failures"] == 1
+            for _ in range(3):
+                st.store.submit_job("k", {"device_id": "node1:gpu1"})
+                assert st.store.claim_job("w", [], 60, "node1:gpu1", 8) is not None
+            r = await (await c.post("/v1/devices/offline",
+                                    json={"device_id": "node1:gpu1", "reason": "hip"})).json()
+            assert r["released"] == 3 and st.circuit.status("node1:gpu1") == "degraded"
+            d = await (await c.get("/v1/dashboard")).json()
+            trips = {x["id"]: x["circuit_trips"] for x in d["devices"]}
+            assert trips.get("node1:gpu1") == 1
     run(go())
 
 

@@ -774,12 +774,16 @@ def test_linear_decode_lm_head_runs_k13_sk():
                                atol=2e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("lead", [0, 5])
 @pytest.mark.parametrize("Hq,Hkv,D", [(32, 8, 128), (12, 12, 64), (28, 4, 128)])
-def test_prefill_fused_q_rope(Hq, Hkv, D):
+def test_prefill_fused_q_rope(Hq, Hkv, D, lead, prefill_waves):
     """Prefill rows with the q rotation inside the attention kernel: the
     rope/cache kernel with skip_q leaves q untouched and writes the same K/V
     cache; the attention over the unrotated q with rope=(positions, cos_sin)
-    matches the fp32 reference over the rotated q."""
+    matches the fp32 reference over the rotated q.  ``lead`` > 0: the batch
+    starts with decode-style rows (the Llama mixed-step call: the whole qkv,
+    every row's position, cu_q starting at ``lead``), so the kernel must take
+    each query's position by its absolute row."""
     qlens, prefix = [70, 33, 256], [40, 0, 100]
     ctxs = [q + p for q, p in zip(qlens, prefix)]
     S = len(qlens)
@@ -808,8 +812,19 @@ def test_prefill_fused_q_rope(Hq, Hkv, D):
     ctx = torch.tensor(ctxs, dtype=torch.int32, device=DEV)
     scale = 1 / math.sqrt(D)
     out = torch.zeros(T, Hq * D, dtype=torch.bfloat16, device=DEV)
-    ops.paged_prefill_attention(qkv, kc, vc, bt, cu, ctx, tiles, scale, out, causal=True, Hq=Hq,
-                                rope=(pos, cs))
+    if lead:
+        # leading rows with their own (unrelated) positions; the prefill
+        # kernel must neither read their positions for its rows nor write them
+        qkv_l = torch.cat([_bf(lead, qkv.shape[1]), qkv])
+        pos_l = torch.cat([torch.randint(0, 4000, (lead,), dtype=torch.int32, device=DEV), pos])
+        out_l = torch.zeros(T + lead, Hq * D, dtype=torch.bfloat16, device=DEV)
+        ops.paged_prefill_attention(qkv_l, kc, vc, bt, cu + lead, ctx, tiles, scale, out_l,
+                                    causal=True, Hq=Hq, rope=(pos_l, cs))
+        assert torch.count_nonzero(out_l[:lead]) == 0
+        out.copy_(out_l[lead:])
+    else:
+        ops.paged_prefill_attention(qkv, kc, vc, bt, cu, ctx, tiles, scale, out, causal=True,
+                                    Hq=Hq, rope=(pos, cs))
     out2 = torch.zeros_like(out)
     ops.paged_prefill_attention(qkv2, kc2, vc2, bt, cu, ctx, tiles, scale, out2, causal=True,
                                 Hq=Hq)

@@ -80,6 +80,17 @@ def test_circuit_three_failures_degrade_success_resets():
     assert not cb.is_degraded("gpu0") and "gpu0" not in cb.snapshot()
 
 
+def test_circuit_trips_count_transitions():
+    cb = CircuitBreaker(clock=Clock())
+    for _ in range(5):
+        cb.record("gpu0", False)
+    assert cb.trips == {"gpu0": 1}          # one ok -> degraded transition
+    cb.record("gpu0", True)
+    for _ in range(3):
+        cb.record("gpu0", False)
+    assert cb.trips == {"gpu0": 2}
+
+
 def test_circuit_probe_after_five_minutes():
     clk = Clock()
     cb = CircuitBreaker(clock=clk)

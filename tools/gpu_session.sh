@@ -30,6 +30,17 @@ for step in "$@"; do
       run rehearse4 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 \
           --master-addr 127.0.0.1 --master-port 29612 bench.py --gpus 4 --steps 2 --warmup 1 \
           --concurrency 32 --rehearse-on-one-gpu || exit $? ;;
+    rehearse4s)
+      # the driver's own command path (no launcher: bench.self_launch) at 4 ranks
+      run rehearse4s 600 python3 bench.py --gpus 4 --rehearse-on-one-gpu --model llama-3-8b@L8 \
+          --steps 2 --warmup 1 --concurrency 64 || exit $? ;;
+    rehearse8s)
+      run rehearse8s 900 python3 bench.py --gpus 8 --rehearse-on-one-gpu --model llama-3-8b@L8 \
+          --steps 2 --warmup 1 --concurrency 32 || exit $? ;;
+    tp8s)
+      # config 4's launcher shape: one TP-8 engine of the 70B layer shapes (8 layers)
+      run tp8s 900 python3 bench.py --gpus 8 --tp 8 --rehearse-on-one-gpu \
+          --model llama-3-70b@L8 --steps 2 --warmup 1 --concurrency 32 --max-tokens 64 || exit $? ;;
     dgemm_tests)
       run dgemm_tests 600 python -u -m pytest tests/test_kernels_gpu.py -k dgemm -x -q --timeout 120 \
           --timeout-method thread -p no:cacheprovider || exit $? ;;
