@@ -199,7 +199,7 @@ class Supervisor:
 
     def spawn(self, cmd: list[str], env: dict, name: str) -> subprocess.Popen:
         import time
-        p = subprocess.Popen(cmd, env=env)
+        p = subprocess.Popen(cmd, env=dict(env, LMX_WORKER_LIFE="1"))
         self.entries.append({"cmd": cmd, "env": env, "name": name, "proc": p,
                              "started": time.time(), "backoff": self.base,
                              "restart_at": None, "restarts": 0})
@@ -221,7 +221,10 @@ class Supervisor:
                 e["restart_at"] = now + e["backoff"] if self.restart else None
                 e["backoff"] = min(self.cap, e["backoff"] * 2)
             if e["proc"] is None and e["restart_at"] is not None and now >= e["restart_at"]:
-                e["proc"] = subprocess.Popen(e["cmd"], env=e["env"])
+                # LMX_WORKER_LIFE: 1-based life of this worker slot (fault
+                # schedules may target the first lives only: LMX_FAULT_LIVES)
+                e["proc"] = subprocess.Popen(e["cmd"], env=dict(
+                    e["env"], LMX_WORKER_LIFE=str(e["restarts"] + 2)))
                 e["started"], e["restart_at"] = now, None
                 e["restarts"] += 1
                 log.warning("worker %s restarted (pid %d, restart #%d)", e["name"],

@@ -27,6 +27,22 @@ UUID_RE = re.compile(r"^[0-9a-f]{8}-[0-9a-f]{4}-[0-9a-f]{4}-[0-9a-f]{4}-[0-9a-f]
 WORKER_PREFIX = "worker-"
 
 
+
+def revive_engine_device(store, tags: dict) -> bool:
+    """A worker (re-)registering for an engine device brings that device back
+    online: it registers only once its engine is up, so after a crash and a
+    supervisor restart this is the recovery signal (the device was taken
+    offline by the old worker's report or by lease expiry)."""
+    dev = str((tags or {}).get("device_id") or "").strip()
+    if not dev:
+        return False
+    d = store.get_device(dev)
+    if d is None or d.get("status") == "online":
+        return False
+    store.set_device_status(dev, "online", {"recovered_at": time.time()})
+    return True
+
+
 def job_json(j: dict) -> dict:
     """models.Job (core/internal/models/types.go:135-149), RFC3339 times,
     omitempty on lease_until / deadline_at / result / error."""
@@ -241,6 +257,7 @@ class ControlPlane:
                 tags = {}
         await self.db(self.store.upsert_device, wid, w.get("name", ""), w.get("platform", ""),
                       w.get("arch", ""), w.get("host", ""), tags, "online")
+        await self.db(revive_engine_device, self.store, tags)
         return write_json(200, {"worker_id": wid})
 
     async def worker_claim(self, request):

@@ -270,7 +270,8 @@ def bench_mixed(a) -> dict:
     port, gport = _port(), _port()
     env = dict(os.environ, LMX_STORE=a.store)
     if a.fault:
-        env.update(LMX_FAULT=a.fault, LMX_FAULT_DEVICE=a.fault_device)
+        env.update(LMX_FAULT=a.fault, LMX_FAULT_DEVICE=a.fault_device,
+                   LMX_FAULT_LIVES=str(a.fault_lives))
     cmd = [sys.executable, "-m", "llm_mcp_amd", "serve", "--gpus", a.gpus, "--http",
            f"127.0.0.1:{port}", "--grpc", f"127.0.0.1:{gport}", "--chat-model", a.chat_model,
            "--embed-model", a.model, "--max-num-seqs", str(a.concurrency),
@@ -342,6 +343,26 @@ def bench_mixed(a) -> dict:
                 async with s.get(url + "/v1/debug/workers") as r:
                     return (await r.json()).get("workers")
         out["workers"] = loop.run_until_complete(workers())
+        if a.await_recovery > 0:
+            # after the load: how long until every supervised worker is alive
+            # again and its device back online (the restarted worker
+            # re-registered) -- reported, never part of the timed window
+            t_rec = time.perf_counter()
+            rec = None
+            run_status = {k: sorted(v) for k, v in status_seen.items()}
+            while time.perf_counter() - t_rec < a.await_recovery:
+                ws = loop.run_until_complete(workers()) or []
+                status_seen.clear()                 # current statuses only
+                loop.run_until_complete(final_poll())
+                online = all(v == {"online"} for v in status_seen.values())
+                if ws and all(w.get("alive") for w in ws) and online:
+                    rec = round(time.perf_counter() - t_rec, 1)
+                    break
+                time.sleep(1.0)
+            out["device_status_seen"] = run_status
+            out["recovered_after_s"] = rec
+            out["workers_after_recovery"] = loop.run_until_complete(workers())
+            out["device_status_after_recovery"] = {k: sorted(v) for k, v in status_seen.items()}
         return out
     finally:
         core.terminate()
@@ -391,6 +412,11 @@ def main(argv=None):
                     help="mixed: workers per GPU (1-GPU rehearsal of a multi-GPU node)")
     ap.add_argument("--fault", default="", help="mixed: LMX_FAULT spec for the targeted worker")
     ap.add_argument("--fault-device", default="", help="mixed: device-id suffix, e.g. gpu0.r1")
+    ap.add_argument("--fault-lives", type=int, default=0,
+                    help="mixed: inject only in the first N lives of the faulty worker (0 = all)")
+    ap.add_argument("--await-recovery", type=float, default=0.0,
+                    help="mixed: after the load, wait up to S seconds for every worker to be "
+                         "alive and its device online again; reports recovered_after_s")
     ap.add_argument("--cpu", action="store_true", help="mixed: CPU engines (plumbing)")
     ap.add_argument("--runs", type=int, default=1,
                     help="mixed: repeat the whole run (fresh serve each time) and report the "

@@ -114,8 +114,12 @@ class CoreService:
     async def RegisterWorker(self, req, ctx):
         w = req.worker
         wid = w.id.strip() or f"worker-{time.time_ns()}"
+        tags = sanitize_json(w.tags_json)
         await self._db(self.store.upsert_device, wid, w.name, w.platform, w.arch, w.host,
-                       sanitize_json(w.tags_json), "online")
+                       tags, "online")
+        from ..api.routes import revive_engine_device
+        await self._db(revive_engine_device, self.store,
+                       tags if isinstance(tags, dict) else {})
         return pb.RegisterWorkerResponse(worker_id=wid)
 
     async def ClaimJob(self, req, ctx):

@@ -100,6 +100,8 @@ VARS: list[Var] = [
     Var("LMX_PREFILL_WAVES", int, 4, "waves per prefill-attention workgroup at head dim 128 (4 or 8)"),
     Var("LMX_SK", str, "1", "0 disables the K13-SK (split-K 256x256 tile) entries of the decode GEMM table"),
     Var("LMX_DGEMM_TABLE", str, "", "decode GEMM dispatch table (default llm_mcp_amd/config/dgemm_gfx950.json)"),
+    Var("LMX_FAULT_LIVES", int, 0, "apply LMX_FAULT only in the first N lives of a supervised worker (0 = every life); the serve supervisor numbers lives in LMX_WORKER_LIFE"),
+    Var("LMX_WORKER_LIFE", int, 1, "set by the serve supervisor: 1-based life of this worker slot (restarts + 1)"),
     Var("LMX_FAULT_DEVICE", str, "", "apply LMX_FAULT only in the worker whose device id ends with this (e.g. gpu0.r1)"),
     Var("LMX_WATCHDOG_S", float, 1.0, "worker: engine health check cadence; an unhealthy engine makes the worker exit for a restart"),
     Var("LMX_WATCHDOG_GRACE_S", float, 2.0, "worker: delay between detecting a broken engine and exiting"),

@@ -100,9 +100,13 @@ def serve_engines(a, engine, embed, device_id: str) -> None:
     from .jobs import JobRunner
 
     fdev = os.environ.get("LMX_FAULT_DEVICE", "")
-    if fdev and not device_id.endswith(fdev):
+    lives = int(os.environ.get("LMX_FAULT_LIVES", "0") or 0)
+    life = int(os.environ.get("LMX_WORKER_LIFE", "1") or 1)
+    if (fdev and not device_id.endswith(fdev)) or (lives > 0 and life > lives):
         from ..utils.faults import Faults, set_faults
-        set_faults(Faults(""))        # LMX_FAULT applies to the targeted device only
+        # LMX_FAULT applies to the targeted device only, and (LMX_FAULT_LIVES)
+        # only to the first N lives of its worker (the supervisor numbers them)
+        set_faults(Faults(""))
     reg = ModelRegistry()
     aeng = None
     if embed is not None:

@@ -102,6 +102,15 @@ for step in "$@"; do
       run config5det 1100 python -u -m llm_mcp_amd.bench.serving_bench mixed --gpus 0 \
           --replicas-per-gpu 2 --fault gpu_error@300 --fault-device gpu0.r1 --runs 3 \
           --jobs 4096 --concurrency 256 --sync-every 4 --max-tokens 64 --chars 512 || exit $? ;;
+    config5b)
+      # config 5, round 4: the faulty worker's first life fails at its 300th
+      # engine step (LMX_FAULT_LIVES=1), the breaker trips from the released
+      # leases, the supervisor restarts the worker; after each 4096-job run
+      # the bench waits for the restarted worker to be alive and online again
+      run config5b 1150 python -u -m llm_mcp_amd.bench.serving_bench mixed --gpus 0 \
+          --replicas-per-gpu 2 --fault gpu_error@300 --fault-device gpu0.r1 --fault-lives 1 \
+          --runs 3 --jobs 4096 --concurrency 256 --sync-every 4 --max-tokens 64 --chars 512 \
+          --await-recovery 150 || exit $? ;;
     tp_rehearse)
       # BASELINE config 4's launcher on one GPU: bench.py --tp 2 with the 70B
       # layer shapes cut to 8 layers (a plumbing rehearsal, never an N-GPU number)
