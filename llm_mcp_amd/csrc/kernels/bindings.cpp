@@ -48,6 +48,9 @@ int gemm_nt(void*, const void*, const void*, const void*, const void*, int, int,
 int dgemm(void*, const void*, const void*, float*, unsigned*, int, int, int, int, long, long, long,
           int, int, int, hipStream_t);
 int dgemm_num_configs();
+int rsgemm(void*, const void*, const void*, float*, unsigned*, int, int, int, int, long, long, long,
+           int, int, int, hipStream_t);
+int rsgemm_pack(void*, const void*, int, int, long, hipStream_t);
 int rmsnorm_slabs(void*, void*, const float*, int, long, const void*, int, int, long, float,
                   hipStream_t);
 int dgemm_config(int, int*, int*);
@@ -204,6 +207,17 @@ PYBIND11_MODULE(_lmx_kernels, m) {
       out.emplace_back(bm, bn);
     }
     return out;
+  });
+  // ---- K14 register-streamed decode GEMM (rsgemm.hip) ----
+  m.def("rsgemm", [](uptr C, uptr A, uptr Wp, uptr slabs, uptr tickets, int n_tickets, int M, int N,
+                     int K, long lda, long ldw, long ldc, int cfg, int splits, int epi,
+                     uptr stream) {
+    check(lmx::rsgemm(P<void>(C), P<void>(A), P<void>(Wp), P<float>(slabs), P<unsigned>(tickets),
+                      n_tickets, M, N, K, lda, ldw, ldc, cfg, splits, epi, S(stream)),
+          "rsgemm");
+  });
+  m.def("rsgemm_pack", [](uptr out, uptr W, int N, int K, long ldw, uptr stream) {
+    check(lmx::rsgemm_pack(P<void>(out), P<void>(W), N, K, ldw, S(stream)), "rsgemm_pack");
   });
   // ---- K12 weight-streaming GEMM (wgemm.hip) ----
   m.def("wgemm", [](uptr C, uptr A, uptr W, uptr slabs, uptr cnt, int n_cnt, int M, int N, int K,

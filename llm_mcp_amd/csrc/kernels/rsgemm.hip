@@ -1,0 +1,411 @@
+// K14: register-streamed weight GEMM for 129..256-row decode batches
+//     C[M, N] = A[M, K] . W[N, K]^T        (bf16 in, fp32 accumulate)
+//
+// Why (profiles/r3_decode_gemm_study.md, r3_k13_and_decode_sk.md): at M = 256
+// a decode projection is a weight stream that every CU must also feed with
+// the whole activation panel; the LDS-DMA designs (K11, K12, K13-SK) reach
+// 5.1-5.4 TB/s on the weight stream alone, while plain 16-B register loads of
+// a linear stream reach 6.4-6.7 TB/s.  K12-RS moved the weights to registers
+// but with one wave per SIMD and every wave owning 128 columns it exposed the
+// ds_read -> MFMA chain.  K14 keeps the weights register-streamed and shapes
+// the rest around the CDNA4 numbers:
+//   * one 512-thread workgroup per CU: 8 waves, 2 per SIMD, so one wave's LDS
+//     reads and waits overlap its partner's MFMAs;
+//   * a workgroup owns ALL rows (<= 256) x a 256-column tile over a K slice
+//     (split-K over S workgroups); wave w owns columns [32w, 32w + 32): two
+//     16-column MFMA tiles (16x16x32 bf16, weights as the A operand), so each
+//     activation fragment read from LDS feeds 2 MFMAs and a K32 step is 1024
+//     MFMA cycles per SIMD against 512 LDS cycles per CU;
+//   * weights pre-packed (rsgemm_pack): each (tile, wave, K32 block, 16-column
+//     half) is one 1-KB run in MFMA fragment order, so a wave's whole K slice
+//     is ONE linear stream of global_load_dwordx4 (1 KB per instruction, 8
+//     full lines), D K32 steps (2 x D loads) in flight in a register ring;
+//   * activations move L2 -> LDS by LDS-DMA (global_load_lds_dwordx4) into an
+//     NA-slot ring of 256 x 64 XOR-swizzled images (conflict-free
+//     ds_read_b128), one raw s_barrier per K64 step;
+//   * the weight loads are inline asm and every vmcnt wait is hand-counted:
+//     beside an LDS-DMA hipcc waits vmcnt(0) for any ordinary register load
+//     (cdna guide §5 "Projection GEMM at M = 256" item 4b), which would drain
+//     the ring every step.  Issue order per K64 step t:
+//        [4 LDS-DMA: A(t + NA - 1)] [2 loads: W(2t + D)] [2 loads: W(2t + 1 + D)]
+//     so A(t) is complete at vmcnt(4 + 8 (NA - 2)) and W(2t + 1) at
+//     vmcnt(8 (U - 1) + 6) with U = D / 2 (the prologue issues the same
+//     pattern for the virtual steps -U .. -1);
+//   * split-K: fp32 slabs + arrival ticket (K11's recipe); epilogues: bf16,
+//     fp32 partials for the residual-add RMSNorm, SwiGLU over [16 gate | 16 up]
+//     weight rows (interleave_gate_up(w, 16): a wave's two 16-column tiles are
+//     the gate and up values of the same 16 channels, in the same lanes).
+#include "common.h"
+
+namespace lmx {
+namespace {
+
+constexpr int RS_THREADS = 512, RS_BN = 256, RS_BK = 64;
+constexpr int RS_SLOT = 256 * RS_BK;   // bf16 elements of one A ring slot (32 KB)
+
+typedef __attribute__((address_space(3))) void rs_lds_t;
+
+__device__ __forceinline__ int rs_swz(int r) { return (r >> 1) & 7; }
+
+// one K64 step of the activation panel (256 rows, padded rows re-read row
+// M-1) into an LDS slot: 4 LDS-DMA instructions per thread
+__device__ __forceinline__ void rs_stage_a(bf16_t* slot, const bf16_t* __restrict__ A, long lda,
+                                           int M, int k0) {
+  const int t = threadIdx.x, wave = t >> 6;
+  const int rr = t >> 3, c = t & 7;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = i * 64 + rr;
+    const int gr = r < M ? r : M - 1;
+    __builtin_amdgcn_global_load_lds(A + (long)gr * lda + k0 + 8 * (c ^ rs_swz(r)),
+                                     (rs_lds_t*)(slot + (i * 64 + wave * 8) * RS_BK), 16, 0, 0);
+  }
+}
+
+__device__ __forceinline__ bf16x8_t rs_afrag(const bf16_t* slot, int r, int chunk) {
+  return *reinterpret_cast<const bf16x8_t*>(slot + r * RS_BK + 8 * (chunk ^ rs_swz(r)));
+}
+
+// weight fragment load (hand-counted: see the header): wave-uniform SGPR base
+// + the lane's 16-B offset + an immediate (< 4 KB), so the ring costs no
+// 64-bit address VGPRs
+template <int NT, int IMM>
+__device__ __forceinline__ void rs_ldw(bf16x8_t& r, const void* sbase, unsigned voff) {
+  if constexpr (NT)
+    asm volatile("global_load_dwordx4 %0, %1, %2 offset:%3 nt"
+                 : "=v"(r) : "v"(voff), "s"(sbase), "i"(IMM) : "memory");
+  else
+    asm volatile("global_load_dwordx4 %0, %1, %2 offset:%3"
+                 : "=v"(r) : "v"(voff), "s"(sbase), "i"(IMM) : "memory");
+}
+
+// the loop's ring refill overwrites registers the MFMAs just before it read
+// as their A operand; hipcc pads no hazard for an asm instruction, so the
+// first refill after a compute phase starts behind 20 wait states
+__device__ __forceinline__ void rs_mfma_war_pad() {
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
+}
+
+template <int CNT>
+__device__ __forceinline__ void rs_wait(bf16x8_t& a, bf16x8_t& b) {
+  asm volatile("s_waitcnt vmcnt(%2)" : "+v"(a), "+v"(b) : "n"(CNT) : "memory");
+}
+
+__device__ __forceinline__ void rs_wait0(bf16x8_t& a, bf16x8_t& b) {
+  asm volatile("s_waitcnt vmcnt(0)" : "+v"(a), "+v"(b) :: "memory");
+}
+
+__device__ __forceinline__ float rs_silu(float g) { return g / (1.f + __expf(-g)); }
+
+}  // namespace
+
+// W packed: [N/256][8 waves][K/32][2 halves][64 lanes][8]: lane l of (wave w,
+// half j, block kb) holds W[256 T + 32 w + 16 j + (l & 15)][32 kb + 8 (l >> 4) .. +8]
+__global__ void rsgemm_pack_kernel(bf16_t* __restrict__ out, const bf16_t* __restrict__ W,
+                                   int N, int K, long ldw) {
+  const long c = blockIdx.x * 256L + threadIdx.x;
+  if (c >= (long)N * K / 8) return;
+  const int KB = K / 32;
+  const int lane = (int)(c & 63);
+  long q = c >> 6;
+  const int j = (int)(q & 1);
+  q >>= 1;
+  const int kb = (int)(q % KB);
+  q /= KB;
+  const int w = (int)(q & 7), T = (int)(q >> 3);
+  const long n = (long)T * 256 + w * 32 + j * 16 + (lane & 15);
+  const int k = kb * 32 + (lane >> 4) * 8;
+  *reinterpret_cast<u16x8*>(out + c * 8) = *reinterpret_cast<const u16x8*>(W + n * ldw + k);
+}
+
+// EPI: 0 bf16 [M, N]; 2 fp32 partial slabs [S][M][N] (no combine); 3 SwiGLU16
+// -> bf16 [M, N/2].  D: weight ring depth in K32 steps (even); NA: A slots.
+// RM: 0 packed weights (rsgemm_pack); 1 the plain row-major [N][ldw] weights,
+// read as fragment-shaped loads (16 rows x 64 B per instruction; a row's two
+// 64-B halves of a 128-B line are read by consecutive K32 steps)
+template <int EPI, int D, int NA, int NT, int RM>
+__global__ void __launch_bounds__(RS_THREADS, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) rsgemm_kernel(
+    bf16_t* __restrict__ C, const bf16_t* __restrict__ A, const bf16_t* __restrict__ Wp,
+    float* __restrict__ slabs, unsigned* __restrict__ tickets, int M, int N, int K, long lda,
+    long ldw, long ldc, int splits) {
+  constexpr int U = D / 2;
+  // NA = U + 1: the prologue then issues every A slot it counts on (with
+  // fewer slots the early steps would see fewer ops behind a load than the
+  // steady-state counts assume)
+  static_assert(D % 2 == 0 && U >= 2 && NA == U + 1, "ring shape");
+  constexpr int WAIT_A = 4 + 8 * (NA - 2);          // A(t) landed, at the top of step t
+  constexpr int WAIT_W0 = 2 + 8 * (U - 1);          // W(2t) landed
+  constexpr int WAIT_TOP = WAIT_A < WAIT_W0 ? WAIT_A : WAIT_W0;
+  constexpr int WAIT_W1 = 8 * (U - 1) + 6;          // W(2t + 1) landed, mid step
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* const lds = reinterpret_cast<bf16_t*>(smem);
+
+  const int tiles = N / RS_BN, nwg = tiles * splits;
+  const int wg = xcd_remap(blockIdx.x, nwg);
+  const int ks = wg % splits, tn = wg / splits;
+  const int kc = K / splits, k0 = ks * kc, nk64 = kc / RS_BK;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int fr = lane & 15, fg = lane >> 4;
+
+  // this wave's weight stream.  Packed: 2 x 1 KB per K32 step, contiguous
+  // over the slice (K32 step k at wstream + 2 KB k, + 1 KB for the second
+  // half).  Row-major: rows 256 tn + 32 wave + 16 j + (lane & 15), 64 B per
+  // row and K32 step (K32 step k at wstream + 64 k).
+  const char* wstream =
+      RM ? reinterpret_cast<const char*>(Wp) + ((long)(tn * RS_BN + 32 * wave) * ldw + k0) * 2
+         : reinterpret_cast<const char*>(Wp) +
+               ((long)(tn * 8 + wave) * (K / 32) + k0 / 32) * 2048;
+  constexpr long KSTEP = RM ? 64 : 2048;
+  const unsigned voff0 = RM ? (unsigned)((lane & 15) * ldw * 2 + (lane >> 4) * 16) : lane * 16;
+  const unsigned voff1 = RM ? (unsigned)(((lane & 15) + 16) * ldw * 2 + (lane >> 4) * 16)
+                            : lane * 16;
+  constexpr int I0 = 0, I1 = RM ? 0 : 1024, I2 = RM ? 64 : 2048, I3 = RM ? 64 : 3072;
+  auto wsb = [&](int k) -> const void* {   // wave-uniform base of K32 step k
+    return (const void*)(wstream + (long)k * KSTEP);
+  };
+
+  f32x4_t acc[2][16];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int g = 0; g < 16; ++g) acc[j][g] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  bf16x8_t wr[D][2];
+
+  // prologue: the steady-state issue pattern of the virtual steps -U .. -1
+#pragma unroll
+  for (int s = -U; s < 0; ++s) {
+    if (s + NA - 1 >= 0) rs_stage_a(lds + ((s + NA - 1) % NA) * RS_SLOT, A, lda, M,
+                                    k0 + (s + NA - 1) * RS_BK);
+    {
+      const int k = 2 * (s + U);                     // K32 steps 2s + D, 2s + D + 1
+      const void* b = wsb(k);
+      rs_ldw<NT, I0>(wr[k][0], b, voff0);
+      rs_ldw<NT, I1>(wr[k][1], b, voff1);
+      rs_ldw<NT, I2>(wr[k + 1][0], b, voff0);
+      rs_ldw<NT, I3>(wr[k + 1][1], b, voff1);
+    }
+  }
+
+  // one K32 sub-step: the 16 row-group fragments read in pairs, the next
+  // pair in flight while the current pair's 4 MFMAs run
+  auto compute = [&](const bf16_t* slot, int kk, const bf16x8_t& w0, const bf16x8_t& w1) {
+    bf16x8_t cur0 = rs_afrag(slot, fr, kk * 4 + fg);
+    bf16x8_t cur1 = rs_afrag(slot, 16 + fr, kk * 4 + fg);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      bf16x8_t nx0 = cur0, nx1 = cur1;
+      if (p < 7) {
+        nx0 = rs_afrag(slot, 32 * (p + 1) + fr, kk * 4 + fg);
+        nx1 = rs_afrag(slot, 32 * (p + 1) + 16 + fr, kk * 4 + fg);
+      }
+      acc[0][2 * p] = mfma16(w0, cur0, acc[0][2 * p]);
+      acc[1][2 * p] = mfma16(w1, cur0, acc[1][2 * p]);
+      acc[0][2 * p + 1] = mfma16(w0, cur1, acc[0][2 * p + 1]);
+      acc[1][2 * p + 1] = mfma16(w1, cur1, acc[1][2 * p + 1]);
+      cur0 = nx0;
+      cur1 = nx1;
+    }
+    // hold that order against the scheduler's register-pressure heuristic
+    // (it otherwise reuses one fragment pair and waits lgkmcnt(0) per pair)
+    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+#pragma unroll
+    for (int p = 0; p < 7; ++p) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // steady state: steps [0, nk64 - U), in blocks of U (the ring index of a
+  // K32 step is static inside the block)
+  int t0 = 0;
+  for (; t0 + U <= nk64 - U; t0 += U) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int t = t0 + u;
+      rs_wait<WAIT_TOP>(wr[2 * u][0], wr[2 * u][1]);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      rs_stage_a(lds + ((t + NA - 1) % NA) * RS_SLOT, A, lda, M, k0 + (t + NA - 1) * RS_BK);
+      const bf16_t* slot = lds + (t % NA) * RS_SLOT;
+      const void* b = wsb(2 * t + D);
+      compute(slot, 0, wr[2 * u][0], wr[2 * u][1]);
+      __builtin_amdgcn_sched_barrier(0);
+      rs_mfma_war_pad();
+      rs_ldw<NT, I0>(wr[2 * u][0], b, voff0);
+      rs_ldw<NT, I1>(wr[2 * u][1], b, voff1);
+      rs_wait<WAIT_W1>(wr[2 * u + 1][0], wr[2 * u + 1][1]);
+      compute(slot, 1, wr[2 * u + 1][0], wr[2 * u + 1][1]);
+      __builtin_amdgcn_sched_barrier(0);
+      rs_mfma_war_pad();
+      rs_ldw<NT, I2>(wr[2 * u + 1][0], b, voff0);
+      rs_ldw<NT, I3>(wr[2 * u + 1][1], b, voff1);
+    }
+  }
+  // tail: the last U steps (no weight loads left to issue), conservative waits
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int t = t0 + u;
+    if (t >= nk64) break;
+    rs_wait0(wr[2 * u][0], wr[2 * u][1]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (t + NA - 1 < nk64)
+      rs_stage_a(lds + ((t + NA - 1) % NA) * RS_SLOT, A, lda, M, k0 + (t + NA - 1) * RS_BK);
+    const bf16_t* slot = lds + (t % NA) * RS_SLOT;
+    compute(slot, 0, wr[2 * u][0], wr[2 * u][1]);
+    rs_wait0(wr[2 * u + 1][0], wr[2 * u + 1][1]);
+    compute(slot, 1, wr[2 * u + 1][0], wr[2 * u + 1][1]);
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // acc[j][g][r] = C[m][n]: m = 16 g + fr, n = 256 tn + 32 wave + 16 j + 4 fg + r
+  const int nb = tn * RS_BN + 32 * wave + 4 * fg;
+  if (splits > 1 || EPI == 2) {
+    float* slab = slabs + (long)ks * M * N;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const int m = 16 * g + fr;
+      if (m >= M) continue;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        *reinterpret_cast<f32x4_t*>(slab + (long)m * N + nb + 16 * j) = acc[j][g];
+    }
+    if (EPI == 2) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(smem);
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned old = __hip_atomic_fetch_add(&tickets[tn], 1u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+      *flag = (old == (unsigned)(splits - 1));
+    }
+    __syncthreads();
+    if (!*flag) return;
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      tickets[tn] = 0u;       // re-armed: every slice of this call has arrived
+    }
+    __syncthreads();
+    // canonical order ((p0 + p1) + ...) whichever slice arrives last
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const int m = 16 * g + fr;
+      const long row = (long)(m < M ? m : M - 1) * N + nb;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        f32x4_t pre = {0.f, 0.f, 0.f, 0.f};
+        for (int s2 = 0; s2 < ks; ++s2)
+          pre += *reinterpret_cast<const f32x4_t*>(slabs + (long)s2 * M * N + row + 16 * j);
+        f32x4_t v = ks > 0 ? pre + acc[j][g] : acc[j][g];
+        for (int s2 = ks + 1; s2 < splits; ++s2)
+          v += *reinterpret_cast<const f32x4_t*>(slabs + (long)s2 * M * N + row + 16 * j);
+        acc[j][g] = v;
+      }
+    }
+  }
+  if constexpr (EPI == 0) {
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const int m = 16 * g + fr;
+      if (m >= M) continue;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        bf16x4_t o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = (short)f2bf(acc[j][g][r]);
+        *reinterpret_cast<bf16x4_t*>(C + (long)m * ldc + nb + 16 * j) = o;
+      }
+    }
+  } else if constexpr (EPI == 3) {
+    const int ob = (tn * RS_BN + 32 * wave) / 2 + 4 * fg;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const int m = 16 * g + fr;
+      if (m >= M) continue;
+      bf16x4_t o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = (short)f2bf(rs_silu(acc[0][g][r]) * acc[1][g][r]);
+      *reinterpret_cast<bf16x4_t*>(C + (long)m * ldc + ob) = o;
+    }
+  }
+}
+
+// ---- host -------------------------------------------------------------------
+int rsgemm_pack(void* out, const void* W, int N, int K, long ldw, hipStream_t stream) {
+  if (N % RS_BN != 0 || K % 32 != 0) return -1;
+  const long chunks = (long)N * K / 8;
+  rsgemm_pack_kernel<<<dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0, stream>>>(
+      (bf16_t*)out, (const bf16_t*)W, N, K, ldw);
+  return (int)hipGetLastError();
+}
+
+template <int EPI, int D, int NA, int NT, int RM>
+static int rs_launch(bf16_t* C, const bf16_t* A, const bf16_t* Wp, float* slabs,
+                     unsigned* tickets, int M, int N, int K, long lda, long ldw, long ldc,
+                     int splits, hipStream_t stream) {
+  constexpr size_t smem = (size_t)NA * RS_SLOT * sizeof(bf16_t);
+  static_assert(smem <= 160 * 1024, "LDS");
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e = hipFuncSetAttribute((const void*)rsgemm_kernel<EPI, D, NA, NT, RM>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    if (e != hipSuccess) return (int)e;
+    attr = true;
+  }
+  rsgemm_kernel<EPI, D, NA, NT, RM><<<dim3((N / RS_BN) * splits), dim3(RS_THREADS), smem,
+                                      stream>>>(C, A, Wp, slabs, tickets, M, N, K, lda, ldw, ldc,
+                                                splits);
+  return (int)hipGetLastError();
+}
+
+// cfg: bits 0-1 ring shape (0: D 6 / NA 4 = 128 KB LDS, 1: D 8 / NA 5 = 160 KB,
+// 2: D 4 / NA 3 = 96 KB), bit 5 non-temporal weight loads, bit 6 row-major
+// weights (W [N][ldw] as stored; else W is rsgemm_pack's layout).  The K
+// slice must be a multiple of U = D / 2 K64 steps.
+int rsgemm(void* C, const void* A, const void* W, float* slabs, unsigned* tickets,
+           int n_tickets, int M, int N, int K, long lda, long ldw, long ldc, int cfg, int splits,
+           int epi, hipStream_t stream) {
+  if (M <= 0) return 0;
+  if (M > 256 || N % RS_BN != 0 || splits < 1 || K % (splits * RS_BK) != 0) return -1;
+  const int shape = cfg & 3, nt = (cfg >> 5) & 1, rm = (cfg >> 6) & 1;
+  if (shape == 3) return -1;
+  const int U = shape == 1 ? 4 : shape == 2 ? 2 : 3;
+  const int nk64 = (K / splits) / RS_BK;
+  if (nk64 < U || nk64 % U != 0) return -1;
+  if (epi != 0 && epi != 2 && epi != 3) return -1;
+  if (rm && (ldw < K || ldw % 8 != 0 || 32L * ldw * 2 > (1L << 31))) return -1;
+  if ((splits > 1 || epi == 2) && slabs == nullptr) return -2;
+  if (splits > 1 && epi != 2 && (tickets == nullptr || N / RS_BN > n_tickets)) return -3;
+  auto C_ = (bf16_t*)C;
+  auto A_ = (const bf16_t*)A;
+  auto W_ = (const bf16_t*)W;
+#define LMX_RS_E(D, NA, NT, RM)                                                              \
+  if (epi == 3) return rs_launch<3, D, NA, NT, RM>(C_, A_, W_, slabs, tickets, M, N, K, lda, \
+                                                   ldw, ldc, splits, stream);                \
+  if (epi == 2) return rs_launch<2, D, NA, NT, RM>(C_, A_, W_, slabs, tickets, M, N, K, lda, \
+                                                   ldw, ldc, splits, stream);                \
+  return rs_launch<0, D, NA, NT, RM>(C_, A_, W_, slabs, tickets, M, N, K, lda, ldw, ldc,      \
+                                     splits, stream);
+#define LMX_RS(D, NA)                                  \
+  if (nt && rm) { LMX_RS_E(D, NA, 1, 1) }              \
+  if (nt) { LMX_RS_E(D, NA, 1, 0) }                    \
+  if (rm) { LMX_RS_E(D, NA, 0, 1) }                    \
+  LMX_RS_E(D, NA, 0, 0)
+  switch (shape) {
+    case 1: { LMX_RS(8, 5) }
+    case 2: { LMX_RS(4, 3) }
+    default: { LMX_RS(6, 4) }
+  }
+#undef LMX_RS
+#undef LMX_RS_E
+}
+
+}  // namespace lmx

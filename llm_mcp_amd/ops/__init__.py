@@ -654,6 +654,10 @@ def linear(x: torch.Tensor, w: torch.Tensor, defer: bool = False,
     (epi 2) may return ``Partials`` and leave the K reduction to the norm."""
     if x.is_cuda and x.dim() == 2:
         M, N, K = x.shape[0], w.shape[0], w.shape[1]
+        if bias is None:
+            rc = rs_choice(M, N, K, epi=2 if defer else 0)
+            if rc is not None and rsgemm_operands_ok(x, w):
+                return rsgemm(x, w, rc[0], rc[1], epi=2 if defer else 0)
         if defer and bias is None:
             s = sk_choice(M, N, K, epi=2)
             if s is not None and pgemm_operands_ok(x, w):
@@ -689,6 +693,9 @@ def linear_swiglu(x: torch.Tensor, w: torch.Tensor, block: int) -> torch.Tensor:
     the LDS hand-off form (epi 1, tile BN = 2 * block)."""
     if x.is_cuda and x.dim() == 2:
         if block == SWIGLU16:
+            rc = rs_choice(x.shape[0], w.shape[0], w.shape[1], epi=3)
+            if rc is not None and rsgemm_operands_ok(x, w):
+                return rsgemm(x, w, rc[0], rc[1], epi=3)     # K14, SwiGLU epilogue
             s = sk_choice(x.shape[0], w.shape[0], w.shape[1], epi=3)
             if s is not None and pgemm_operands_ok(x, w):
                 return pgemm_sk(x, w, s, act=ACT_SWIGLU)   # K13-SK, SwiGLU epilogue
@@ -982,6 +989,140 @@ def dgemm_partials(a: torch.Tensor, w: torch.Tensor, cfg: int, splits: int) -> P
                    a.stride(0), w.stride(0), N, cfg, splits, 2, _stream())
     DGEMM_CALLS[0] += 1
     return Partials(slabs[:splits * M * N].view(splits, M, N), splits, M, N)
+
+
+# ---------------------------------------------------------------------------
+# K14: register-streamed decode GEMM, 129..256 rows (csrc/kernels/rsgemm.hip)
+# ---------------------------------------------------------------------------
+RS_BN = 256
+RS_ROWMAJOR, RS_NT = 64, 32       # cfg bits: row-major weights, non-temporal stream
+RS_U = {0: 3, 1: 4, 2: 2}         # cfg & 3 -> K64 steps per ring block
+RSGEMM_CALLS = [0]                # host-side launch count (tests: the K14 path ran)
+_RS_TABLE: dict | None = None
+_RS_WS: dict = {}
+_RS_CNT = 4096
+
+
+def _rs_table() -> dict:
+    """Measured K14 dispatch: {(N, K, epi): [(m_min, m_max, cfg, splits)]} from
+    config/dgemm_gfx950.json "rs" (tools/rsgemm_lab.cpp, cold weights, against
+    K11 and the in-bench hipBLASLt times).  LMX_DGEMM=0 or LMX_RS=0 disables."""
+    global _RS_TABLE
+    if _RS_TABLE is None:
+        import json
+        import os
+        _RS_TABLE = {}
+        path = os.environ.get("LMX_DGEMM_TABLE") or os.path.join(
+            os.path.dirname(os.path.dirname(__file__)), "config", "dgemm_gfx950.json")
+        if (os.environ.get("LMX_DGEMM", "1") == "1" and os.environ.get("LMX_RS", "1") == "1"
+                and os.path.exists(path)):
+            with open(path) as f:
+                for e in json.load(f).get("rs", []):
+                    _RS_TABLE.setdefault((int(e["N"]), int(e["K"]), int(e.get("epi", 0))),
+                                         []).append((int(e["m_min"]), int(e["m_max"]),
+                                                     int(e["cfg"]), int(e["splits"])))
+    return _RS_TABLE
+
+
+def rsgemm_supported(M: int, N: int, K: int, cfg: int, splits: int) -> bool:
+    """Shapes K14 takes: <= 256 rows, 256-column tiles, a K slice that is a
+    whole number of the configuration's ring blocks."""
+    u = RS_U.get(cfg & 3)
+    if u is None or not (0 < M <= 256 and N % RS_BN == 0 and splits >= 1
+                         and K % (64 * splits) == 0):
+        return False
+    nk = K // splits // 64
+    return nk >= u and nk % u == 0
+
+
+def rs_choice(M: int, N: int, K: int, epi: int = 0) -> tuple[int, int] | None:
+    """(cfg, splits) of K14 for this decode GEMM, or None."""
+    for m_min, m_max, cfg, s in _rs_table().get((N, K, epi), ()):
+        if (m_min <= M <= m_max and rsgemm_supported(M, N, K, cfg, s)
+                and (epi != 2 or s in (1, 2, 4, 8, 16))):     # rmsnorm_slabs' S
+            return cfg, s
+    return None
+
+
+def rsgemm_operands_ok(a: torch.Tensor, w: torch.Tensor) -> bool:
+    """Row-major layouts K14 reads directly (16-B aligned unit-stride rows)."""
+    return (a.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and a.stride(1) == 1
+            and w.stride(1) == 1 and a.stride(0) % 8 == 0 and w.stride(0) % 8 == 0
+            and a.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0)
+
+
+def _rs_workspace(dev: torch.device, n_floats: int):
+    key = (dev.index, _stream())
+    ws = _RS_WS.get(key)
+    if ws is None or ws[0].numel() < n_floats:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("rsgemm workspace must be allocated before graph capture "
+                               "(run the shape once eagerly)")
+        n_floats = max(n_floats, ws[0].numel() if ws else 0, 1 << 20)
+        cnt = ws[1] if ws else torch.zeros(_RS_CNT, dtype=torch.int32, device=dev)
+        ws = (torch.empty(n_floats, dtype=torch.float32, device=dev), cnt)
+        _retire_ws(_RS_WS.get(key))
+        _RS_WS[key] = ws
+    return ws
+
+
+def rsgemm_pack(w: torch.Tensor) -> torch.Tensor:
+    """``w`` [N, K] in K14's packed layout (each (tile, wave, K32 block,
+    16-row half) one 1-KB run in MFMA fragment order).  Same element count."""
+    _bf16(w, "w")
+    N, K = w.shape
+    _chk(N % RS_BN == 0 and K % 32 == 0 and w.stride(1) == 1 and w.stride(0) % 8 == 0,
+         f"rsgemm_pack shape N={N} K={K}")
+    out = torch.empty((N, K), dtype=w.dtype, device=w.device)
+    native().rsgemm_pack(_ptr(out), _ptr(w), N, K, w.stride(0), _stream())
+    return out
+
+
+def rsgemm(a: torch.Tensor, w: torch.Tensor, cfg: int, splits: int, epi: int = 0,
+           out: torch.Tensor | None = None, packed: bool = False):
+    """a @ w^T on K14 (M <= 256).  epi 0: bf16 [M, N]; 2: fp32 ``Partials``
+    [splits, M, N] for ``rms_norm(..., residual=)``; 3: SwiGLU over gate/up
+    rows interleaved per 16 (``interleave_gate_up(w, 16)``), bf16 [M, N/2].
+    ``w`` row-major (cfg | RS_ROWMAJOR) or from ``rsgemm_pack`` (``packed``)."""
+    M, K = a.shape
+    N = w.shape[0]
+    cfg = (cfg & ~RS_ROWMAJOR) | (0 if packed else RS_ROWMAJOR)
+    _chk(rsgemm_supported(M, N, K, cfg, splits), f"rsgemm shape M={M} N={N} K={K} "
+                                                 f"cfg={cfg} S={splits}")
+    if not a.is_cuda:
+        _chk(not packed, "rsgemm: the CPU reference takes row-major weights")
+        y = a.float() @ w.float().t()
+        if epi == 2:
+            p = torch.cat([y.unsqueeze(0)] + [torch.zeros_like(y).unsqueeze(0)] * (splits - 1))
+            return Partials(p, splits, M, N)
+        if epi == 3:
+            y = y.view(M, N // 32, 2, 16)
+            y = (torch.nn.functional.silu(y[:, :, 0]) * y[:, :, 1]).reshape(M, N // 2)
+        y = y.to(a.dtype)
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
+    _bf16(a, "a"); _bf16(w, "w")
+    _chk(w.shape[1] == K and rsgemm_operands_ok(a, w), "rsgemm operands need 16-B aligned rows")
+    RSGEMM_CALLS[0] += 1
+    if epi == 2:
+        slabs, cnt = _rs_workspace(a.device, splits * M * N)
+        native().rsgemm(0, _ptr(a), _ptr(w), _ptr(slabs), _ptr(cnt), _RS_CNT, M, N, K,
+                        a.stride(0), w.stride(0), N, cfg, splits, 2, _stream())
+        return Partials(slabs[:splits * M * N].view(splits, M, N), splits, M, N)
+    ncols = N // 2 if epi == 3 else N
+    if out is None:
+        out = torch.empty((M, ncols), dtype=a.dtype, device=a.device)
+    _chk(out.shape == (M, ncols) and out.stride(1) == 1 and out.stride(0) % 4 == 0
+         and out.data_ptr() % 8 == 0, "rsgemm output layout")
+    slabs = cnt = None
+    if splits > 1:
+        _chk(N // RS_BN <= _RS_CNT, "rsgemm tile count")
+        slabs, cnt = _rs_workspace(a.device, splits * M * N)
+    native().rsgemm(_ptr(out), _ptr(a), _ptr(w), _ptr(slabs), _ptr(cnt), _RS_CNT, M, N, K,
+                    a.stride(0), w.stride(0), out.stride(0), cfg, splits, epi, _stream())
+    return out
 
 
 # ---------------------------------------------------------------------------

@@ -214,6 +214,12 @@ def test_discovery_devices_dashboard_capacity():
             d = await (await c.get("/v1/dashboard")).json()
             trips = {x["id"]: x["circuit_trips"] for x in d["devices"]}
             assert trips.get("node1:gpu1") == 1
+            # a worker re-registering for the engine device (after a
+            # supervisor restart) brings it back online
+            r = await c.post("/v1/workers/register", json={"worker": {
+                "id": "worker-x", "tags": {"device_id": "node1:gpu1", "engine": True}}})
+            assert r.status == 200
+            assert st.store.get_device("node1:gpu1")["status"] == "online"
     run(go())
 
 

@@ -53,3 +53,41 @@ def test_pgemm_sk_cpu_reference_forms():
                                atol=2e-2, rtol=2e-2)
     assert not ops.pgemm_sk_supported(37, 500, 512, 2)          # N not a 256 multiple
     assert not ops.pgemm_sk_supported(37, 512, 512, 8)          # one K-step per slice
+
+
+def test_rsgemm_shape_rules_and_cpu_reference(monkeypatch, tmp_path):
+    """K14 (csrc/kernels/rsgemm.hip) shape rules, its measured-table dispatch
+    ("rs" entries) and the CPU reference forms of its three epilogues."""
+    import json
+    import torch
+    from llm_mcp_amd import ops
+    # ring blocks: D4 (cfg 2) takes K slices of 2 K64 steps, D6 (cfg 0) of 3
+    assert ops.rsgemm_supported(256, 28672, 4096, 2, 2)
+    assert not ops.rsgemm_supported(256, 28672, 4096, 0, 2)        # 32 K64 steps % 3
+    assert ops.rsgemm_supported(256, 4096, 14336, 2 | 32, 16)      # 14 K64 steps
+    assert not ops.rsgemm_supported(257, 4096, 4096, 2, 1)
+    assert not ops.rsgemm_supported(256, 4000, 4096, 2, 1)
+    table = {"entries": [], "rs": [{"N": 28672, "K": 4096, "epi": 3, "m_min": 129,
+                                    "m_max": 256, "cfg": 34, "splits": 2},
+                                   {"N": 4096, "K": 4096, "epi": 2, "m_min": 129,
+                                    "m_max": 256, "cfg": 34, "splits": 16}]}
+    p = tmp_path / "t.json"
+    p.write_text(json.dumps(table))
+    monkeypatch.setenv("LMX_DGEMM_TABLE", str(p))
+    monkeypatch.setattr(ops, "_RS_TABLE", None)
+    assert ops.rs_choice(256, 28672, 4096, 3) == (34, 2)
+    assert ops.rs_choice(128, 28672, 4096, 3) is None
+    assert ops.rs_choice(200, 4096, 4096, 2) == (34, 16)
+    assert ops.rs_choice(200, 4096, 4096, 0) is None
+    monkeypatch.setattr(ops, "_RS_TABLE", None)
+    a = torch.randn(5, 2048).to(torch.bfloat16)
+    w = (torch.randn(512, 2048) * 0.02).to(torch.bfloat16)
+    y = a.float() @ w.float().t()
+    torch.testing.assert_close(ops.rsgemm(a, w, 2, 2).float(), y, atol=2e-2, rtol=2e-2)
+    part = ops.rsgemm(a, w, 2, 4, epi=2)
+    assert part.slabs.shape == (4, 5, 512)
+    torch.testing.assert_close(part.slabs.sum(0), y, atol=1e-3, rtol=1e-3)
+    g = ops.rsgemm(a, w, 2, 1, epi=3)
+    yy = y.view(5, 16, 2, 16)
+    torch.testing.assert_close(g.float(), (torch.nn.functional.silu(yy[:, :, 0]) * yy[:, :, 1])
+                               .reshape(5, 256), atol=2e-2, rtol=2e-2)

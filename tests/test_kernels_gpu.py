@@ -832,3 +832,74 @@ def test_prefill_fused_q_rope(Hq, Hkv, D, lead, prefill_waves):
     torch.testing.assert_close(out.float(), out2.float(), atol=1e-2, rtol=1e-2)
     expect = ref.paged_prefill(qkv2[:, :Hq * D].reshape(T, Hq, D), kc2, vc2, bt, cu, ctx, scale)
     torch.testing.assert_close(out.float().view(T, Hq, D), expect.float(), atol=2e-2, rtol=2e-2)
+
+
+# ---- K14: register-streamed decode GEMM (csrc/kernels/rsgemm.hip) ----
+@pytest.mark.parametrize("cfg", [2, 2 | 32, 0, 1 | 32])
+@pytest.mark.parametrize("M", [256, 200, 129, 17])
+def test_rsgemm_vs_fp32(cfg, M):
+    """K14 against the fp32 reference: row-major and packed weights, every
+    epilogue (bf16 with the in-kernel split-K combine, SwiGLU over 16-row
+    gate/up pairs, fp32 partials), split-K 1/2/4, ring shapes D4/D6/D8 with and
+    without the non-temporal stream; padded rows (M < 256) never stored."""
+    K, N = {3: 3072, 4: 4096, 2: 2048}[ops.RS_U[cfg & 3]], 1024   # K slices = whole ring blocks
+    a = _bf(M, K)
+    w = _bf(N, K, scale=K ** -0.5)
+    wp = ops.rsgemm_pack(w)
+    y = a.float() @ w.float().t()
+    wil = ops.interleave_gate_up(w, ops.SWIGLU16)
+    yil = a.float() @ wil.float().t()
+    g = (torch.nn.functional.silu(yil.view(M, N // 32, 2, 16)[:, :, 0]) *
+         yil.view(M, N // 32, 2, 16)[:, :, 1]).reshape(M, N // 2)
+    for s in (1, 2, 4):
+        if not ops.rsgemm_supported(M, N, K, cfg, s):
+            continue
+        for packed in (False, True):
+            out = ops.rsgemm(a, wp if packed else w, cfg, s, packed=packed)
+            torch.testing.assert_close(out.float(), y, atol=2e-2, rtol=2e-2)
+            assert torch.equal(out, ops.rsgemm(a, wp if packed else w, cfg, s, packed=packed))
+        out3 = ops.rsgemm(a, wil, cfg, s, epi=3)
+        torch.testing.assert_close(out3.float(), g, atol=2e-2, rtol=2e-2)
+        p = ops.rsgemm(a, w, cfg, s, epi=2)
+        torch.testing.assert_close(p.slabs.sum(0), y, atol=2e-2, rtol=2e-2)
+
+
+def test_rsgemm_llama_shapes_and_graph():
+    """The Llama-3-8B decode shapes at 256 rows (gate/up + SwiGLU S 2, QKV S 8,
+    O / down partials S 16) vs fp32, then replayed in a captured graph with new
+    activations (tickets re-armed in-kernel, no memset node)."""
+    M = 256
+    for N, K, epi, s in [(28672, 4096, 3, 2), (6144, 4096, 0, 8), (4096, 4096, 2, 16),
+                         (4096, 14336, 2, 16)]:
+        cfg = 2 | 32
+        if not ops.rsgemm_supported(M, N, K, cfg, s):
+            continue
+        a = _bf(M, K)
+        w = _bf(N, K, scale=K ** -0.5)
+        y = a.float() @ w.float().t()
+        if epi == 3:
+            y = (torch.nn.functional.silu(y.view(M, N // 32, 2, 16)[:, :, 0]) *
+                 y.view(M, N // 32, 2, 16)[:, :, 1]).reshape(M, N // 2)
+        r = ops.rsgemm(a, w, cfg, s, epi=epi)
+        got = r.slabs.sum(0) if epi == 2 else r.float()
+        torch.testing.assert_close(got, y, atol=3e-2, rtol=3e-2)
+        if epi == 2:
+            continue
+        out = torch.empty_like(r)
+        st = torch.cuda.Stream()
+        st.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(st):
+            ops.rsgemm(a, w, cfg, s, epi=epi, out=out)
+        torch.cuda.current_stream().wait_stream(st)
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr, stream=st):
+            ops.rsgemm(a, w, cfg, s, epi=epi, out=out)
+        for _ in range(2):
+            a.copy_(_bf(M, K))
+            gr.replay()
+            torch.cuda.synchronize()
+            y = a.float() @ w.float().t()
+            if epi == 3:
+                y = (torch.nn.functional.silu(y.view(M, N // 32, 2, 16)[:, :, 0]) *
+                     y.view(M, N // 32, 2, 16)[:, :, 1]).reshape(M, N // 2)
+            torch.testing.assert_close(out.float(), y, atol=3e-2, rtol=3e-2)
