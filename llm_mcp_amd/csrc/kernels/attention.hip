@@ -129,8 +129,7 @@ __device__ __forceinline__ void process_page(PageState<HD>& st, const bf16x8_t (
   float mx = x[0];
 #pragma unroll
   for (int j = 1; j < 8; ++j) mx = fmaxf(mx, x[j]);
-  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  mx = col4_max(mx);        // VALU lane swaps: no LDS traffic in the page loop
   const float m_new = fmaxf(st.m, mx);
   // a column may see no visible key in this page (causal tail): keep its state
   const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
@@ -138,8 +137,7 @@ __device__ __forceinline__ void process_page(PageState<HD>& st, const bf16x8_t (
   float p[8], rs = 0.f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) { p[j] = fast_exp2(x[j] - m_use); rs += p[j]; }
-  rs += __shfl_xor(rs, 16, 64);
-  rs += __shfl_xor(rs, 32, 64);
+  rs = col4_sum(rs);
   st.l = st.l * alpha + rs;
   st.m = m_new;
   bf16x8_t pf;
@@ -195,16 +193,14 @@ __device__ __forceinline__ void compute_page(PageState<HD>& st, const bf16x8_t (
   float mx = x[0];
 #pragma unroll
   for (int j = 1; j < 8; ++j) mx = fmaxf(mx, x[j]);
-  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  mx = col4_max(mx);        // VALU lane swaps: no LDS traffic in the page loop
   const float m_new = fmaxf(st.m, mx);
   const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
   const float alpha = fast_exp2(st.m - m_use);
   float p[8], rs = 0.f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) { p[j] = fast_exp2(x[j] - m_use); rs += p[j]; }
-  rs += __shfl_xor(rs, 16, 64);
-  rs += __shfl_xor(rs, 32, 64);
+  rs = col4_sum(rs);
   st.l = st.l * alpha + rs;
   st.m = m_new;
   bf16x8_t pf;

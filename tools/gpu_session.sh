@@ -76,6 +76,23 @@ for step in "$@"; do
             -o run --output-format csv -- python3 -m llm_mcp_amd.bench.engine_bench --batch 128 \
             --prompt-len 512 --max-tokens 8 --no-graphs --max-batched-tokens 16384 || exit $?
       done ;;
+    pmc_attn)
+      # decode attention at the headline shape (fused rope form, the persistent
+      # default and the grid form): LDS share and conflicts, waits, and the
+      # HBM read rate, one counter pass each
+      n=0
+      for pass in \
+        "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS GRBM_GUI_ACTIVE" \
+        "FETCH_SIZE TCC_HIT_sum GRBM_GUI_ACTIVE" \
+        "TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_READ_REQ_sum TCP_PENDING_STALL_CYCLES_sum TCP_UTCL1_TRANSLATION_MISS_sum TCC_MISS_sum TCC_HIT_sum GRBM_GUI_ACTIVE" ; do
+        n=$(( n + 1 ))
+        rm -rf gpurun_out/pmc_attn_$n
+        run pmc_attn_$n 120 timeout -s KILL 100 rocprofv3 --pmc $pass --kernel-trace -d gpurun_out/pmc_attn_$n \
+            -o run --output-format csv -- python3 tools/decode_attn_probe.py --layout engine --rope \
+            --modes 0,4 --iters 20 || exit $?
+      done
+      python tools/pmc_table.py gpurun_out/pmc_attn_1 gpurun_out/pmc_attn_2 gpurun_out/pmc_attn_3 \
+          --match paged_decode > gpurun_out/pmc_attn_table.md 2>&1 || true ;;
     list_counters)
       run list_counters 120 rocprofv3 -L || exit $? ;;
     tp_tests)

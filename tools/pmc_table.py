@@ -7,6 +7,9 @@ Derived columns (gfx950 conventions of MI355X_MICROARCH.md):
   HBM wr TB/s   WRITE_SIZE / time
   MFMA util     SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)
   LDS confl.    SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE (extra cycles per LDS cycle)
+  LDS busy      SQ_LDS_IDX_ACTIVE / (256 CUs x GRBM_GUI_ACTIVE / 8): the share of CU-cycles
+                the LDS array was active at all (a high conflict rate on an LDS that is
+                almost idle costs nothing)
   L2 hit        TCC_HIT / (TCC_HIT + TCC_MISS)
   L2 lat        TCP_TCC_READ_REQ_LATENCY / TCP_TCC_READ_REQ (cycles per L1->L2 read)
   wait / busy   SQ_WAIT_ANY, SQ_ACTIVE_INST_ANY as fractions of SQ_WAVE_CYCLES
@@ -32,6 +35,8 @@ def row(name, cs, dur):
                  if f("SQ_VALU_MFMA_BUSY_CYCLES") is not None and g else "-")
     cells.append(f"{f('SQ_LDS_BANK_CONFLICT') / f('SQ_LDS_IDX_ACTIVE'):.3f}"
                  if f("SQ_LDS_IDX_ACTIVE") else "-")
+    cells.append(f"{f('SQ_LDS_IDX_ACTIVE') / (256 * g / 8):.4f}"
+                 if f("SQ_LDS_IDX_ACTIVE") is not None and g else "-")
     h, m = f("TCC_HIT_sum"), f("TCC_MISS_sum")
     cells.append(f"{h / (h + m):.2f}" if h is not None and m is not None and h + m else "-")
     cells.append(f"{f('TCP_TCC_READ_REQ_LATENCY_sum') / f('TCP_TCC_READ_REQ_sum'):.0f}"
@@ -48,9 +53,9 @@ def main():
     a = ap.parse_args()
     per, dur = load(a.dirs)
     pats = [p for p in a.match.split(",") if p]
-    print("| kernel | us | HBM rd TB/s | HBM wr TB/s | MFMA util | LDS confl. | L2 hit | "
+    print("| kernel | us | HBM rd TB/s | HBM wr TB/s | MFMA util | LDS confl. | LDS busy | L2 hit | "
           "L2 lat (cyc) | wait / active |")
-    print("|---|---:|---:|---:|---:|---:|---:|---:|---|")
+    print("|---|---:|---:|---:|---:|---:|---:|---:|---:|---|")
     for name, cs in sorted(per.items(), key=lambda kv: -sum(dur.get(kv[0], [0]))):
         if pats and not any(p in name for p in pats):
             continue
