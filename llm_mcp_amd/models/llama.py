@@ -207,6 +207,12 @@ class LlamaModel:
                 for L in self.w["layers"]:
                     L["w_gate_up"] = ops.interleave_gate_up(L["w_gate_up"], blk)
                 self.gu_block = blk
+            # K14 decode shapes the table runs on packed weights get their
+            # packed copies now (row-major entries need nothing)
+            for L in self.w["layers"]:
+                for k in ("wqkv", "wo", "w_gate_up", "w_down"):
+                    if k in L:
+                        ops.rs_prepare(L[k])
 
     # ----------------------------------------------------------- weights ----
     def _random_weights(self, seed: int) -> dict:

@@ -716,7 +716,8 @@ def swiglu_block(N: int, K: int) -> int:
     """Interleave block of the gate|up weights for the fused decode GEMM of
     this shape: 16 when the table has in-register-epilogue (epi 3) entries,
     else BN/2 of the measured epi-1 configurations; 0 = not fused."""
-    if any(cfg >= 0 for m, cfg, s in _dg_table().get((N, K, 3), ())) or _sk_table().get((N, K, 3)):
+    if (any(cfg >= 0 for m, cfg, s in _dg_table().get((N, K, 3), ())) or _sk_table().get((N, K, 3))
+            or _rs_table().get((N, K, 3))):
         return SWIGLU16
     # one interleave serves every batch size, so take the tile width of the
     # largest-batch bucket the fused kernel won: buckets measured with another
@@ -1066,6 +1067,27 @@ def _rs_workspace(dev: torch.device, n_floats: int):
     return ws
 
 
+_RS_PACKED: dict = {}              # (data_ptr, N, K) of a weight -> its packed copy
+
+
+def rs_prepare(w: torch.Tensor) -> bool:
+    """Called once per decode weight at model load: when the K14 table runs
+    this weight's shape on PACKED weights (an entry whose cfg lacks
+    RS_ROWMAJOR), build and keep the packed copy (rsgemm_pack) that
+    ``rsgemm`` then finds by the weight's address.  Returns True if packed."""
+    if not w.is_cuda or w.dim() != 2:
+        return False
+    N, K = w.shape
+    wants = any(not (cfg & RS_ROWMAJOR) for ep in (0, 2, 3)
+                for _, _, cfg, _ in _rs_table().get((N, K, ep), ()))
+    if not wants or N % RS_BN or K % 32:
+        return False
+    key = (w.data_ptr(), N, K)
+    if key not in _RS_PACKED:
+        _RS_PACKED[key] = rsgemm_pack(w)
+    return True
+
+
 def rsgemm_pack(w: torch.Tensor) -> torch.Tensor:
     """``w`` [N, K] in K14's packed layout (each (tile, wave, K32 block,
     16-row half) one 1-KB run in MFMA fragment order).  Same element count."""
@@ -1086,6 +1108,12 @@ def rsgemm(a: torch.Tensor, w: torch.Tensor, cfg: int, splits: int, epi: int = 0
     ``w`` row-major (cfg | RS_ROWMAJOR) or from ``rsgemm_pack`` (``packed``)."""
     M, K = a.shape
     N = w.shape[0]
+    if not packed and not (cfg & RS_ROWMAJOR) and a.is_cuda:
+        # a table entry on packed weights: the copy rs_prepare built, else
+        # the row-major form of the same ring shape
+        wp = _RS_PACKED.get((w.data_ptr(), N, K))
+        if wp is not None:
+            w, packed = wp, True
     cfg = (cfg & ~RS_ROWMAJOR) | (0 if packed else RS_ROWMAJOR)
     _chk(rsgemm_supported(M, N, K, cfg, splits), f"rsgemm shape M={M} N={N} K={K} "
                                                  f"cfg={cfg} S={splits}")

@@ -99,6 +99,8 @@ VARS: list[Var] = [
     Var("LMX_DGEMM", str, "1", "0 disables the decode GEMM (K11) dispatch table (hipBLASLt everywhere)"),
     Var("LMX_PREFILL_WAVES", int, 4, "waves per prefill-attention workgroup at head dim 128 (4 or 8)"),
     Var("LMX_SK", str, "1", "0 disables the K13-SK (split-K 256x256 tile) entries of the decode GEMM table"),
+    Var("LMX_RS", str, "1", "0 disables the K14 (register-streamed weights, csrc/kernels/rsgemm.hip) entries of the decode GEMM table"),
+    Var("LMX_TP_SELFTEST_S", float, 180.0, "TP engines: seconds the start-up collective self-test may wait before the rank exits (code 3) instead of hanging"),
     Var("LMX_DGEMM_TABLE", str, "", "decode GEMM dispatch table (default llm_mcp_amd/config/dgemm_gfx950.json)"),
     Var("LMX_FAULT_LIVES", int, 0, "apply LMX_FAULT only in the first N lives of a supervised worker (0 = every life); the serve supervisor numbers lives in LMX_WORKER_LIFE"),
     Var("LMX_WORKER_LIFE", int, 1, "set by the serve supervisor: 1-based life of this worker slot (restarts + 1)"),
