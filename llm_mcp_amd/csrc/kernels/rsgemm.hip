@@ -97,6 +97,41 @@ __device__ __forceinline__ void rs_wait0(bf16x8_t& a, bf16x8_t& b) {
 
 __device__ __forceinline__ float rs_silu(float g) { return g / (1.f + __expf(-g)); }
 
+// split-K combine of the last arriving slice: acc[j][g] = sum over the S
+// slabs in slice order, with at most 8 loads (32 VGPRs) in flight at a time
+// beside the 128 accumulator registers
+template <int S>
+__device__ __forceinline__ void rs_combine(f32x4_t (&acc)[2][16], const float* __restrict__ slabs,
+                                           long MN, int M, int N, int nb, int fr) {
+  constexpr int SB = S < 8 ? S : 8;              // slabs per batch
+  constexpr int UN = 8 / SB;                     // (row group, half) units per batch
+#pragma unroll
+  for (int u0 = 0; u0 < 32; u0 += UN) {
+    long off[UN];
+#pragma unroll
+    for (int u = 0; u < UN; ++u) {
+      const int m = 16 * ((u0 + u) >> 1) + fr;
+      off[u] = (long)(m < M ? m : M - 1) * N + nb + 16 * ((u0 + u) & 1);
+    }
+    f32x4_t t[UN];
+#pragma unroll
+    for (int sb = 0; sb < S; sb += SB) {
+      f32x4_t v[UN][SB];
+#pragma unroll
+      for (int u = 0; u < UN; ++u)
+#pragma unroll
+        for (int s = 0; s < SB; ++s)
+          v[u][s] = *reinterpret_cast<const f32x4_t*>(slabs + (sb + s) * MN + off[u]);
+#pragma unroll
+      for (int u = 0; u < UN; ++u)
+#pragma unroll
+        for (int s = 0; s < SB; ++s) t[u] = (sb + s == 0) ? v[u][0] : t[u] + v[u][s];
+    }
+#pragma unroll
+    for (int u = 0; u < UN; ++u) acc[(u0 + u) & 1][(u0 + u) >> 1] = t[u];
+  }
+}
+
 }  // namespace
 
 // W packed: [N/256][8 waves][K/32][2 halves][64 lanes][8]: lane l of (wave w,
@@ -294,21 +329,15 @@ __global__ void __launch_bounds__(RS_THREADS, 2) __attribute__((amdgpu_waves_per
       tickets[tn] = 0u;       // re-armed: every slice of this call has arrived
     }
     __syncthreads();
-    // canonical order ((p0 + p1) + ...) whichever slice arrives last
-#pragma unroll
-    for (int g = 0; g < 16; ++g) {
-      const int m = 16 * g + fr;
-      const long row = (long)(m < M ? m : M - 1) * N + nb;
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        f32x4_t pre = {0.f, 0.f, 0.f, 0.f};
-        for (int s2 = 0; s2 < ks; ++s2)
-          pre += *reinterpret_cast<const f32x4_t*>(slabs + (long)s2 * M * N + row + 16 * j);
-        f32x4_t v = ks > 0 ? pre + acc[j][g] : acc[j][g];
-        for (int s2 = ks + 1; s2 < splits; ++s2)
-          v += *reinterpret_cast<const f32x4_t*>(slabs + (long)s2 * M * N + row + 16 * j);
-        acc[j][g] = v;
-      }
+    // every slab, this slice's own included, summed in slice order: the
+    // result is bitwise the same whichever slice arrives last, and the loads
+    // carry no per-element condition (a runtime "own or load" select makes
+    // hipcc wait vmcnt(0) per load: one L2 round trip each)
+    switch (splits) {
+      case 2: rs_combine<2>(acc, slabs, (long)M * N, M, N, nb, fr); break;
+      case 4: rs_combine<4>(acc, slabs, (long)M * N, M, N, nb, fr); break;
+      case 8: rs_combine<8>(acc, slabs, (long)M * N, M, N, nb, fr); break;
+      default: rs_combine<16>(acc, slabs, (long)M * N, M, N, nb, fr); break;
     }
   }
   if constexpr (EPI == 0) {
@@ -376,7 +405,12 @@ int rsgemm(void* C, const void* A, const void* W, float* slabs, unsigned* ticket
   if (M <= 0) return 0;
   if (M > 256 || N % RS_BN != 0 || splits < 1 || K % (splits * RS_BK) != 0) return -1;
   const int shape = cfg & 3, nt = (cfg >> 5) & 1, rm = (cfg >> 6) & 1;
-  if (shape == 3) return -1;
+  // shape 1 (D 8 / NA 5) needs 256+ VGPRs: the compiler spills, and a spill
+  // of an inline-asm load destination before its data lands is silent
+  // corruption (cdna guide §5.7 item 1) -- not built
+  if (shape == 3 || shape == 1) return -1;
+  if (splits > 1 && epi != 2 && splits != 2 && splits != 4 && splits != 8 && splits != 16)
+    return -1;
   const int U = shape == 1 ? 4 : shape == 2 ? 2 : 3;
   const int nk64 = (K / splits) / RS_BK;
   if (nk64 < U || nk64 % U != 0) return -1;
@@ -400,7 +434,6 @@ int rsgemm(void* C, const void* A, const void* W, float* slabs, unsigned* ticket
   if (rm) { LMX_RS_E(D, NA, 0, 1) }                    \
   LMX_RS_E(D, NA, 0, 0)
   switch (shape) {
-    case 1: { LMX_RS(8, 5) }
     case 2: { LMX_RS(4, 3) }
     default: { LMX_RS(6, 4) }
   }

@@ -997,7 +997,7 @@ def dgemm_partials(a: torch.Tensor, w: torch.Tensor, cfg: int, splits: int) -> P
 # ---------------------------------------------------------------------------
 RS_BN = 256
 RS_ROWMAJOR, RS_NT = 64, 32       # cfg bits: row-major weights, non-temporal stream
-RS_U = {0: 3, 1: 4, 2: 2}         # cfg & 3 -> K64 steps per ring block
+RS_U = {0: 3, 2: 2}               # cfg & 3 -> K64 steps per ring block (D6 / D4)
 RSGEMM_CALLS = [0]                # host-side launch count (tests: the K14 path ran)
 _RS_TABLE: dict | None = None
 _RS_WS: dict = {}
@@ -1029,7 +1029,7 @@ def rsgemm_supported(M: int, N: int, K: int, cfg: int, splits: int) -> bool:
     """Shapes K14 takes: <= 256 rows, 256-column tiles, a K slice that is a
     whole number of the configuration's ring blocks."""
     u = RS_U.get(cfg & 3)
-    if u is None or not (0 < M <= 256 and N % RS_BN == 0 and splits >= 1
+    if u is None or not (0 < M <= 256 and N % RS_BN == 0 and splits in (1, 2, 4, 8, 16)
                          and K % (64 * splits) == 0):
         return False
     nk = K // splits // 64
