@@ -41,22 +41,22 @@ namespace lmx {
 namespace {
 
 constexpr int RS_THREADS = 512, RS_BN = 256, RS_BK = 64;
-constexpr int RS_SLOT = 256 * RS_BK;   // bf16 elements of one A ring slot (32 KB)
 
 typedef __attribute__((address_space(3))) void rs_lds_t;
 
 __device__ __forceinline__ int rs_swz(int r) { return (r >> 1) & 7; }
 
-// one K64 step of the activation panel (256 rows, padded rows re-read row
-// M-1) into an LDS slot: 4 LDS-DMA instructions per thread
+// one K64 step of the activation panel (BM rows from m0, padded rows re-read
+// row M-1) into an LDS slot: BM / 64 LDS-DMA instructions per thread
+template <int BM>
 __device__ __forceinline__ void rs_stage_a(bf16_t* slot, const bf16_t* __restrict__ A, long lda,
-                                           int M, int k0) {
+                                           int M, int m0, int k0) {
   const int t = threadIdx.x, wave = t >> 6;
   const int rr = t >> 3, c = t & 7;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < BM / 64; ++i) {
     const int r = i * 64 + rr;
-    const int gr = r < M ? r : M - 1;
+    const int gr = m0 + r < M ? m0 + r : M - 1;
     __builtin_amdgcn_global_load_lds(A + (long)gr * lda + k0 + 8 * (c ^ rs_swz(r)),
                                      (rs_lds_t*)(slot + (i * 64 + wave * 8) * RS_BK), 16, 0, 0);
   }
@@ -100,17 +100,17 @@ __device__ __forceinline__ float rs_silu(float g) { return g / (1.f + __expf(-g)
 // split-K combine of the last arriving slice: acc[j][g] = sum over the S
 // slabs in slice order, with at most 8 loads (32 VGPRs) in flight at a time
 // beside the 128 accumulator registers
-template <int S>
-__device__ __forceinline__ void rs_combine(f32x4_t (&acc)[2][16], const float* __restrict__ slabs,
-                                           long MN, int M, int N, int nb, int fr) {
+template <int S, int NG>
+__device__ __forceinline__ void rs_combine(f32x4_t (&acc)[2][NG], const float* __restrict__ slabs,
+                                           long MN, int M, int N, int nb, int m0, int fr) {
   constexpr int SB = S < 8 ? S : 8;              // slabs per batch
   constexpr int UN = 8 / SB;                     // (row group, half) units per batch
 #pragma unroll
-  for (int u0 = 0; u0 < 32; u0 += UN) {
+  for (int u0 = 0; u0 < 2 * NG; u0 += UN) {
     long off[UN];
 #pragma unroll
     for (int u = 0; u < UN; ++u) {
-      const int m = 16 * ((u0 + u) >> 1) + fr;
+      const int m = m0 + 16 * ((u0 + u) >> 1) + fr;
       off[u] = (long)(m < M ? m : M - 1) * N + nb + 16 * ((u0 + u) & 1);
     }
     f32x4_t t[UN];
@@ -157,8 +157,11 @@ __global__ void rsgemm_pack_kernel(bf16_t* __restrict__ out, const bf16_t* __res
 // -> bf16 [M, N/2].  D: weight ring depth in K32 steps (even); NA: A slots.
 // RM: 0 packed weights (rsgemm_pack); 1 the plain row-major [N][ldw] weights,
 // read as fragment-shaped loads (16 rows x 64 B per instruction; a row's two
-// 64-B halves of a 128-B line are read by consecutive K32 steps)
-template <int EPI, int D, int NA, int NT, int RM>
+// 64-B halves of a 128-B line are read by consecutive K32 steps).
+// BM: rows per workgroup (256: all rows, or 128: the two row tiles of a column
+// tile run side by side, adjacent workgroup ids, and share its weight stream
+// through the XCD's L2 -- split-K-free at 224 workgroups for gate/up)
+template <int EPI, int D, int NA, int NT, int RM, int BM>
 __global__ void __launch_bounds__(RS_THREADS, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) rsgemm_kernel(
     bf16_t* __restrict__ C, const bf16_t* __restrict__ A, const bf16_t* __restrict__ Wp,
     float* __restrict__ slabs, unsigned* __restrict__ tickets, int M, int N, int K, long lda,
@@ -168,16 +171,20 @@ __global__ void __launch_bounds__(RS_THREADS, 2) __attribute__((amdgpu_waves_per
   // fewer slots the early steps would see fewer ops behind a load than the
   // steady-state counts assume)
   static_assert(D % 2 == 0 && U >= 2 && NA == U + 1, "ring shape");
-  constexpr int WAIT_A = 4 + 8 * (NA - 2);          // A(t) landed, at the top of step t
-  constexpr int WAIT_W0 = 2 + 8 * (U - 1);          // W(2t) landed
-  constexpr int WAIT_TOP = WAIT_A < WAIT_W0 ? WAIT_A : WAIT_W0;
-  constexpr int WAIT_W1 = 8 * (U - 1) + 6;          // W(2t + 1) landed, mid step
+  static_assert(BM == 256 || BM == 128, "row tile");
+  constexpr int NG = BM / 16, G = BM / 64, OPS = G + 4;   // row groups; VMEM ops per step
+  constexpr int SLOT = BM * RS_BK;                  // bf16 elements of one A ring slot
+  // with NA = U + 1, A(t) is issued just before W(2t) (step t - U): waiting
+  // for W(2t) covers it
+  constexpr int WAIT_TOP = 2 + OPS * (U - 1);       // W(2t) landed, top of step t
+  constexpr int WAIT_W1 = OPS * (U - 1) + G + 2;    // W(2t + 1) landed, mid step
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* const lds = reinterpret_cast<bf16_t*>(smem);
 
-  const int tiles = N / RS_BN, nwg = tiles * splits;
+  const int tiles_m = (M + BM - 1) / BM, tiles = N / RS_BN, nwg = tiles_m * tiles * splits;
   const int wg = xcd_remap(blockIdx.x, nwg);
-  const int ks = wg % splits, tn = wg / splits;
+  const int ks = wg % splits, rest = wg / splits;
+  const int tm = rest % tiles_m, tn = rest / tiles_m, m0 = tm * BM;
   const int kc = K / splits, k0 = ks * kc, nk64 = kc / RS_BK;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -200,18 +207,18 @@ __global__ void __launch_bounds__(RS_THREADS, 2) __attribute__((amdgpu_waves_per
     return (const void*)(wstream + (long)k * KSTEP);
   };
 
-  f32x4_t acc[2][16];
+  f32x4_t acc[2][NG];
 #pragma unroll
   for (int j = 0; j < 2; ++j)
 #pragma unroll
-    for (int g = 0; g < 16; ++g) acc[j][g] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int g = 0; g < NG; ++g) acc[j][g] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   bf16x8_t wr[D][2];
 
   // prologue: the steady-state issue pattern of the virtual steps -U .. -1
 #pragma unroll
   for (int s = -U; s < 0; ++s) {
-    if (s + NA - 1 >= 0) rs_stage_a(lds + ((s + NA - 1) % NA) * RS_SLOT, A, lda, M,
-                                    k0 + (s + NA - 1) * RS_BK);
+    if (s + NA - 1 >= 0) rs_stage_a<BM>(lds + ((s + NA - 1) % NA) * SLOT, A, lda, M, m0,
+                                        k0 + (s + NA - 1) * RS_BK);
     {
       const int k = 2 * (s + U);                     // K32 steps 2s + D, 2s + D + 1
       const void* b = wsb(k);
@@ -222,16 +229,16 @@ __global__ void __launch_bounds__(RS_THREADS, 2) __attribute__((amdgpu_waves_per
     }
   }
 
-  // one K32 sub-step: the 16 row-group fragments read in pairs, the next
+  // one K32 sub-step: the NG row-group fragments read in pairs, the next
   // pair in flight while the current pair's 4 MFMAs run
   auto compute = [&](const bf16_t* slot, int kk, const bf16x8_t& w0, const bf16x8_t& w1) {
     bf16x8_t cur0 = rs_afrag(slot, fr, kk * 4 + fg);
     bf16x8_t cur1 = rs_afrag(slot, 16 + fr, kk * 4 + fg);
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int p = 0; p < 8; ++p) {
+    for (int p = 0; p < NG / 2; ++p) {
       bf16x8_t nx0 = cur0, nx1 = cur1;
-      if (p < 7) {
+      if (p < NG / 2 - 1) {
         nx0 = rs_afrag(slot, 32 * (p + 1) + fr, kk * 4 + fg);
         nx1 = rs_afrag(slot, 32 * (p + 1) + 16 + fr, kk * 4 + fg);
       }
@@ -246,7 +253,7 @@ __global__ void __launch_bounds__(RS_THREADS, 2) __attribute__((amdgpu_waves_per
     // (it otherwise reuses one fragment pair and waits lgkmcnt(0) per pair)
     __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
 #pragma unroll
-    for (int p = 0; p < 7; ++p) {
+    for (int p = 0; p < NG / 2 - 1; ++p) {
       __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
       __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
     }
@@ -264,8 +271,9 @@ __global__ void __launch_bounds__(RS_THREADS, 2) __attribute__((amdgpu_waves_per
       rs_wait<WAIT_TOP>(wr[2 * u][0], wr[2 * u][1]);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-      rs_stage_a(lds + ((t + NA - 1) % NA) * RS_SLOT, A, lda, M, k0 + (t + NA - 1) * RS_BK);
-      const bf16_t* slot = lds + (t % NA) * RS_SLOT;
+      rs_stage_a<BM>(lds + ((t + NA - 1) % NA) * SLOT, A, lda, M, m0,
+                     k0 + (t + NA - 1) * RS_BK);
+      const bf16_t* slot = lds + (t % NA) * SLOT;
       const void* b = wsb(2 * t + D);
       compute(slot, 0, wr[2 * u][0], wr[2 * u][1]);
       __builtin_amdgcn_sched_barrier(0);
@@ -289,8 +297,8 @@ __global__ void __launch_bounds__(RS_THREADS, 2) __attribute__((amdgpu_waves_per
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (t + NA - 1 < nk64)
-      rs_stage_a(lds + ((t + NA - 1) % NA) * RS_SLOT, A, lda, M, k0 + (t + NA - 1) * RS_BK);
-    const bf16_t* slot = lds + (t % NA) * RS_SLOT;
+      rs_stage_a<BM>(lds + ((t + NA - 1) % NA) * SLOT, A, lda, M, m0, k0 + (t + NA - 1) * RS_BK);
+    const bf16_t* slot = lds + (t % NA) * SLOT;
     compute(slot, 0, wr[2 * u][0], wr[2 * u][1]);
     rs_wait0(wr[2 * u + 1][0], wr[2 * u + 1][1]);
     compute(slot, 1, wr[2 * u + 1][0], wr[2 * u + 1][1]);
@@ -298,13 +306,13 @@ __global__ void __launch_bounds__(RS_THREADS, 2) __attribute__((amdgpu_waves_per
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
 
-  // acc[j][g][r] = C[m][n]: m = 16 g + fr, n = 256 tn + 32 wave + 16 j + 4 fg + r
+  // acc[j][g][r] = C[m][n]: m = m0 + 16 g + fr, n = 256 tn + 32 wave + 16 j + 4 fg + r
   const int nb = tn * RS_BN + 32 * wave + 4 * fg;
   if (splits > 1 || EPI == 2) {
     float* slab = slabs + (long)ks * M * N;
 #pragma unroll
-    for (int g = 0; g < 16; ++g) {
-      const int m = 16 * g + fr;
+    for (int g = 0; g < NG; ++g) {
+      const int m = m0 + 16 * g + fr;
       if (m >= M) continue;
 #pragma unroll
       for (int j = 0; j < 2; ++j)
@@ -317,8 +325,8 @@ __global__ void __launch_bounds__(RS_THREADS, 2) __attribute__((amdgpu_waves_per
     if (threadIdx.x == 0) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const unsigned old = __hip_atomic_fetch_add(&tickets[tn], 1u, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned old = __hip_atomic_fetch_add(&tickets[tn * tiles_m + tm], 1u,
+                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       *flag = (old == (unsigned)(splits - 1));
     }
     __syncthreads();
@@ -326,7 +334,7 @@ __global__ void __launch_bounds__(RS_THREADS, 2) __attribute__((amdgpu_waves_per
     if (threadIdx.x == 0) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      tickets[tn] = 0u;       // re-armed: every slice of this call has arrived
+      tickets[tn * tiles_m + tm] = 0u;   // re-armed: every slice of this call has arrived
     }
     __syncthreads();
     // every slab, this slice's own included, summed in slice order: the
@@ -334,16 +342,16 @@ __global__ void __launch_bounds__(RS_THREADS, 2) __attribute__((amdgpu_waves_per
     // carry no per-element condition (a runtime "own or load" select makes
     // hipcc wait vmcnt(0) per load: one L2 round trip each)
     switch (splits) {
-      case 2: rs_combine<2>(acc, slabs, (long)M * N, M, N, nb, fr); break;
-      case 4: rs_combine<4>(acc, slabs, (long)M * N, M, N, nb, fr); break;
-      case 8: rs_combine<8>(acc, slabs, (long)M * N, M, N, nb, fr); break;
-      default: rs_combine<16>(acc, slabs, (long)M * N, M, N, nb, fr); break;
+      case 2: rs_combine<2, NG>(acc, slabs, (long)M * N, M, N, nb, m0, fr); break;
+      case 4: rs_combine<4, NG>(acc, slabs, (long)M * N, M, N, nb, m0, fr); break;
+      case 8: rs_combine<8, NG>(acc, slabs, (long)M * N, M, N, nb, m0, fr); break;
+      default: rs_combine<16, NG>(acc, slabs, (long)M * N, M, N, nb, m0, fr); break;
     }
   }
   if constexpr (EPI == 0) {
 #pragma unroll
-    for (int g = 0; g < 16; ++g) {
-      const int m = 16 * g + fr;
+    for (int g = 0; g < NG; ++g) {
+      const int m = m0 + 16 * g + fr;
       if (m >= M) continue;
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
@@ -356,8 +364,8 @@ __global__ void __launch_bounds__(RS_THREADS, 2) __attribute__((amdgpu_waves_per
   } else if constexpr (EPI == 3) {
     const int ob = (tn * RS_BN + 32 * wave) / 2 + 4 * fg;
 #pragma unroll
-    for (int g = 0; g < 16; ++g) {
-      const int m = 16 * g + fr;
+    for (int g = 0; g < NG; ++g) {
+      const int m = m0 + 16 * g + fr;
       if (m >= M) continue;
       bf16x4_t o;
 #pragma unroll
@@ -376,27 +384,27 @@ int rsgemm_pack(void* out, const void* W, int N, int K, long ldw, hipStream_t st
   return (int)hipGetLastError();
 }
 
-template <int EPI, int D, int NA, int NT, int RM>
+template <int EPI, int D, int NA, int NT, int RM, int BM>
 static int rs_launch(bf16_t* C, const bf16_t* A, const bf16_t* Wp, float* slabs,
                      unsigned* tickets, int M, int N, int K, long lda, long ldw, long ldc,
                      int splits, hipStream_t stream) {
-  constexpr size_t smem = (size_t)NA * RS_SLOT * sizeof(bf16_t);
+  constexpr size_t smem = (size_t)NA * BM * RS_BK * sizeof(bf16_t);
   static_assert(smem <= 160 * 1024, "LDS");
   static bool attr = false;
   if (!attr) {
-    const hipError_t e = hipFuncSetAttribute((const void*)rsgemm_kernel<EPI, D, NA, NT, RM>,
+    const hipError_t e = hipFuncSetAttribute((const void*)rsgemm_kernel<EPI, D, NA, NT, RM, BM>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return (int)e;
     attr = true;
   }
-  rsgemm_kernel<EPI, D, NA, NT, RM><<<dim3((N / RS_BN) * splits), dim3(RS_THREADS), smem,
-                                      stream>>>(C, A, Wp, slabs, tickets, M, N, K, lda, ldw, ldc,
-                                                splits);
+  rsgemm_kernel<EPI, D, NA, NT, RM, BM>
+      <<<dim3(((M + BM - 1) / BM) * (N / RS_BN) * splits), dim3(RS_THREADS), smem, stream>>>(
+          C, A, Wp, slabs, tickets, M, N, K, lda, ldw, ldc, splits);
   return (int)hipGetLastError();
 }
 
-// cfg: bits 0-1 ring shape (0: D 6 / NA 4 = 128 KB LDS, 1: D 8 / NA 5 = 160 KB,
-// 2: D 4 / NA 3 = 96 KB), bit 5 non-temporal weight loads, bit 6 row-major
+// cfg: bits 0-1 ring shape (0: D 6 / NA 4, 2: D 4 / NA 3), bit 2 128-row
+// tiles (else all 256 rows), bit 5 non-temporal weight loads, bit 6 row-major
 // weights (W [N][ldw] as stored; else W is rsgemm_pack's layout).  The K
 // slice must be a multiple of U = D / 2 K64 steps.
 int rsgemm(void* C, const void* A, const void* W, float* slabs, unsigned* tickets,
@@ -404,40 +412,45 @@ int rsgemm(void* C, const void* A, const void* W, float* slabs, unsigned* ticket
            int epi, hipStream_t stream) {
   if (M <= 0) return 0;
   if (M > 256 || N % RS_BN != 0 || splits < 1 || K % (splits * RS_BK) != 0) return -1;
-  const int shape = cfg & 3, nt = (cfg >> 5) & 1, rm = (cfg >> 6) & 1;
+  const int shape = cfg & 3, bm128 = (cfg >> 2) & 1, nt = (cfg >> 5) & 1, rm = (cfg >> 6) & 1;
   // shape 1 (D 8 / NA 5) needs 256+ VGPRs: the compiler spills, and a spill
   // of an inline-asm load destination before its data lands is silent
   // corruption (cdna guide §5.7 item 1) -- not built
   if (shape == 3 || shape == 1) return -1;
   if (splits > 1 && epi != 2 && splits != 2 && splits != 4 && splits != 8 && splits != 16)
     return -1;
-  const int U = shape == 1 ? 4 : shape == 2 ? 2 : 3;
+  const int U = shape == 2 ? 2 : 3;
   const int nk64 = (K / splits) / RS_BK;
   if (nk64 < U || nk64 % U != 0) return -1;
   if (epi != 0 && epi != 2 && epi != 3) return -1;
   if (rm && (ldw < K || ldw % 8 != 0 || 32L * ldw * 2 > (1L << 31))) return -1;
   if ((splits > 1 || epi == 2) && slabs == nullptr) return -2;
-  if (splits > 1 && epi != 2 && (tickets == nullptr || N / RS_BN > n_tickets)) return -3;
+  const int tiles = ((M + (bm128 ? 127 : 255)) / (bm128 ? 128 : 256)) * (N / RS_BN);
+  if (splits > 1 && epi != 2 && (tickets == nullptr || tiles > n_tickets)) return -3;
   auto C_ = (bf16_t*)C;
   auto A_ = (const bf16_t*)A;
   auto W_ = (const bf16_t*)W;
-#define LMX_RS_E(D, NA, NT, RM)                                                              \
-  if (epi == 3) return rs_launch<3, D, NA, NT, RM>(C_, A_, W_, slabs, tickets, M, N, K, lda, \
-                                                   ldw, ldc, splits, stream);                \
-  if (epi == 2) return rs_launch<2, D, NA, NT, RM>(C_, A_, W_, slabs, tickets, M, N, K, lda, \
-                                                   ldw, ldc, splits, stream);                \
-  return rs_launch<0, D, NA, NT, RM>(C_, A_, W_, slabs, tickets, M, N, K, lda, ldw, ldc,      \
-                                     splits, stream);
+#define LMX_RS_E(D, NA, NT, RM, BM)                                                             \
+  if (epi == 3) return rs_launch<3, D, NA, NT, RM, BM>(C_, A_, W_, slabs, tickets, M, N, K, lda, \
+                                                       ldw, ldc, splits, stream);               \
+  if (epi == 2) return rs_launch<2, D, NA, NT, RM, BM>(C_, A_, W_, slabs, tickets, M, N, K, lda, \
+                                                       ldw, ldc, splits, stream);               \
+  return rs_launch<0, D, NA, NT, RM, BM>(C_, A_, W_, slabs, tickets, M, N, K, lda, ldw, ldc,     \
+                                         splits, stream);
+#define LMX_RS_B(D, NA, NT, RM)                 \
+  if (bm128) { LMX_RS_E(D, NA, NT, RM, 128) }   \
+  LMX_RS_E(D, NA, NT, RM, 256)
 #define LMX_RS(D, NA)                                  \
-  if (nt && rm) { LMX_RS_E(D, NA, 1, 1) }              \
-  if (nt) { LMX_RS_E(D, NA, 1, 0) }                    \
-  if (rm) { LMX_RS_E(D, NA, 0, 1) }                    \
-  LMX_RS_E(D, NA, 0, 0)
+  if (nt && rm) { LMX_RS_B(D, NA, 1, 1) }              \
+  if (nt) { LMX_RS_B(D, NA, 1, 0) }                    \
+  if (rm) { LMX_RS_B(D, NA, 0, 1) }                    \
+  LMX_RS_B(D, NA, 0, 0)
   switch (shape) {
     case 2: { LMX_RS(4, 3) }
     default: { LMX_RS(6, 4) }
   }
 #undef LMX_RS
+#undef LMX_RS_B
 #undef LMX_RS_E
 }
 
