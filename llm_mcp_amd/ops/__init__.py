@@ -655,7 +655,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, defer: bool = False,
     if x.is_cuda and x.dim() == 2:
         M, N, K = x.shape[0], w.shape[0], w.shape[1]
         if bias is None:
-            rc = rs_choice(M, N, K, epi=2 if defer else 0)
+            rc = rs_choice(M, N, K, epi=2 if defer else 0, w=w)
             if rc is not None and rsgemm_operands_ok(x, w):
                 return rsgemm(x, w, rc[0], rc[1], epi=2 if defer else 0)
         if defer and bias is None:
@@ -693,7 +693,7 @@ def linear_swiglu(x: torch.Tensor, w: torch.Tensor, block: int) -> torch.Tensor:
     the LDS hand-off form (epi 1, tile BN = 2 * block)."""
     if x.is_cuda and x.dim() == 2:
         if block == SWIGLU16:
-            rc = rs_choice(x.shape[0], w.shape[0], w.shape[1], epi=3)
+            rc = rs_choice(x.shape[0], w.shape[0], w.shape[1], epi=3, w=w)
             if rc is not None and rsgemm_operands_ok(x, w):
                 return rsgemm(x, w, rc[0], rc[1], epi=3)     # K14, SwiGLU epilogue
             s = sk_choice(x.shape[0], w.shape[0], w.shape[1], epi=3)
@@ -1036,11 +1036,16 @@ def rsgemm_supported(M: int, N: int, K: int, cfg: int, splits: int) -> bool:
     return nk >= u and nk % u == 0
 
 
-def rs_choice(M: int, N: int, K: int, epi: int = 0) -> tuple[int, int] | None:
-    """(cfg, splits) of K14 for this decode GEMM, or None."""
+def rs_choice(M: int, N: int, K: int, epi: int = 0,
+              w: torch.Tensor | None = None) -> tuple[int, int] | None:
+    """(cfg, splits) of K14 for this decode GEMM, or None.  An entry on packed
+    weights applies only when ``w`` has its packed copy (rs_prepare)."""
     for m_min, m_max, cfg, s in _rs_table().get((N, K, epi), ()):
         if (m_min <= M <= m_max and rsgemm_supported(M, N, K, cfg, s)
                 and (epi != 2 or s in (1, 2, 4, 8, 16))):     # rmsnorm_slabs' S
+            if not (cfg & RS_ROWMAJOR) and (
+                    w is None or (w.data_ptr(), N, K) not in _RS_PACKED):
+                continue
             return cfg, s
     return None
 
@@ -1084,6 +1089,14 @@ def rs_prepare(w: torch.Tensor) -> bool:
         return False
     key = (w.data_ptr(), N, K)
     if key not in _RS_PACKED:
+        # the packed copies sit beside the row-major weights (prefill reads
+        # those): bounded by LMX_RS_PACK_GB so a model that fills the GPU
+        # (Llama-3-70B at TP=1) keeps its KV-cache room
+        import os
+        budget = float(os.environ.get("LMX_RS_PACK_GB", "24")) * (1 << 30)
+        used = sum(t.numel() * t.element_size() for t in _RS_PACKED.values())
+        if used + w.numel() * w.element_size() > budget:
+            return False
         _RS_PACKED[key] = rsgemm_pack(w)
     return True
 

@@ -187,7 +187,8 @@ def test_llama3_8b_shapes_on_decode_gemm_match_dense(graphs):
 def test_llama3_8b_shapes_k13_prefill_and_sk_lm_head(graphs):
     """Two layers of Llama-3-8B at a 200-row batch: the one-step prefill of
     200 x 4 tokens (M = 800) runs the projections on K13 (fused SwiGLU gate/up)
-    and the 200-row decode steps run the LM head on K13-SK (config "sk"), in
+    and the 200-row decode steps run the LM head on K13-SK (config "sk") and
+    gate/up / down on K14 (config "rs"), in
     captured graphs too (bucket 224); greedy tokens stay (near-)argmax of the dense fp32
     forward."""
     import dataclasses
@@ -196,13 +197,18 @@ def test_llama3_8b_shapes_k13_prefill_and_sk_lm_head(graphs):
     ops.native()
     cfg = dataclasses.replace(mc.resolve("llama-3-8b"), num_layers=2)
     assert ops.sk_choice(200, cfg.vocab_size, cfg.hidden_size) is not None
-    n0 = ops.PGEMM_CALLS[0]
+    n0, r0 = ops.PGEMM_CALLS[0], ops.RSGEMM_CALLS[0]
     e = LLMEngine(EngineConfig(model="llama-3-8b", max_num_seqs=224, max_batched_tokens=1024,
                                max_model_len=256, use_graphs=graphs, kv_cache_gb=1),
                   device="cuda", model_cfg=cfg)
     prompts = [[(13 * i + 5 * j) % 120000 + 100 for j in range(4)] for i in range(200)]
     outs = e.generate(prompts, SamplingParams(temperature=0, max_tokens=3, ignore_eos=True))
     assert ops.PGEMM_CALLS[0] > n0
+    # 200-row decode steps: gate/up + SwiGLU and down partials on K14 (packed
+    # weights, 128-row tiles; config "rs") when the table has those entries
+    if ops.rs_choice(200, 2 * cfg.intermediate_size, cfg.hidden_size, 3,
+                     w=e.model.w["layers"][0]["w_gate_up"]) is not None:
+        assert ops.RSGEMM_CALLS[0] > r0
     if graphs:
         assert e.stats["graph_steps"] > 0
     for p, o in list(zip(prompts, outs))[::37]:

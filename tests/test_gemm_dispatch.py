@@ -68,17 +68,24 @@ def test_rsgemm_shape_rules_and_cpu_reference(monkeypatch, tmp_path):
     assert not ops.rsgemm_supported(257, 4096, 4096, 2, 1)
     assert not ops.rsgemm_supported(256, 4000, 4096, 2, 1)
     table = {"entries": [], "rs": [{"N": 28672, "K": 4096, "epi": 3, "m_min": 129,
-                                    "m_max": 256, "cfg": 34, "splits": 2},
+                                    "m_max": 256, "cfg": 98, "splits": 2},
                                    {"N": 4096, "K": 4096, "epi": 2, "m_min": 129,
-                                    "m_max": 256, "cfg": 34, "splits": 16}]}
+                                    "m_max": 256, "cfg": 98, "splits": 16},
+                                   {"N": 4096, "K": 14336, "epi": 2, "m_min": 129,
+                                    "m_max": 256, "cfg": 38, "splits": 8}]}
     p = tmp_path / "t.json"
     p.write_text(json.dumps(table))
     monkeypatch.setenv("LMX_DGEMM_TABLE", str(p))
     monkeypatch.setattr(ops, "_RS_TABLE", None)
-    assert ops.rs_choice(256, 28672, 4096, 3) == (34, 2)
+    assert ops.rs_choice(256, 28672, 4096, 3) == (98, 2)           # row-major entry
     assert ops.rs_choice(128, 28672, 4096, 3) is None
-    assert ops.rs_choice(200, 4096, 4096, 2) == (34, 16)
+    assert ops.rs_choice(200, 4096, 4096, 2) == (98, 16)
     assert ops.rs_choice(200, 4096, 4096, 0) is None
+    # a packed-weight entry applies only to a weight rs_prepare packed
+    assert ops.rs_choice(256, 4096, 14336, 2) is None
+    w_cpu = torch.zeros(4096, 14336, dtype=torch.bfloat16)
+    assert not ops.rs_prepare(w_cpu)                                # CPU weights: never packed
+    assert ops.rs_choice(256, 4096, 14336, 2, w=w_cpu) is None
     monkeypatch.setattr(ops, "_RS_TABLE", None)
     a = torch.randn(5, 2048).to(torch.bfloat16)
     w = (torch.randn(512, 2048) * 0.02).to(torch.bfloat16)
