@@ -1043,8 +1043,7 @@ def rs_choice(M: int, N: int, K: int, epi: int = 0,
     for m_min, m_max, cfg, s in _rs_table().get((N, K, epi), ()):
         if (m_min <= M <= m_max and rsgemm_supported(M, N, K, cfg, s)
                 and (epi != 2 or s in (1, 2, 4, 8, 16))):     # rmsnorm_slabs' S
-            if not (cfg & RS_ROWMAJOR) and (
-                    w is None or (w.data_ptr(), N, K) not in _RS_PACKED):
+            if not (cfg & RS_ROWMAJOR) and _rs_packed_of(w) is None:
                 continue
             return cfg, s
     return None
@@ -1072,33 +1071,47 @@ def _rs_workspace(dev: torch.device, n_floats: int):
     return ws
 
 
-_RS_PACKED: dict = {}              # (data_ptr, N, K) of a weight -> its packed copy
+_RS_PACKED_BYTES = [0]             # live packed copies (a finalizer subtracts)
+
+
+def _rs_packed_of(w: torch.Tensor | None) -> torch.Tensor | None:
+    """The packed copy rs_prepare attached to this weight tensor object (the
+    copy lives and dies with the weight: a freed weight's address reused by
+    another tensor can never find a stale copy)."""
+    return getattr(w, "_lmx_rs_packed", None) if w is not None else None
 
 
 def rs_prepare(w: torch.Tensor) -> bool:
     """Called once per decode weight at model load: when the K14 table runs
     this weight's shape on PACKED weights (an entry whose cfg lacks
-    RS_ROWMAJOR), build and keep the packed copy (rsgemm_pack) that
-    ``rsgemm`` then finds by the weight's address.  Returns True if packed."""
+    RS_ROWMAJOR), build the packed copy (rsgemm_pack) and attach it to the
+    weight tensor, where ``rs_choice`` / ``rsgemm`` find it.  Returns True if
+    the weight has a packed copy."""
     if not w.is_cuda or w.dim() != 2:
         return False
+    if _rs_packed_of(w) is not None:
+        return True
     N, K = w.shape
     wants = any(not (cfg & RS_ROWMAJOR) for ep in (0, 2, 3)
                 for _, _, cfg, _ in _rs_table().get((N, K, ep), ()))
     if not wants or N % RS_BN or K % 32:
         return False
-    key = (w.data_ptr(), N, K)
-    if key not in _RS_PACKED:
-        # the packed copies sit beside the row-major weights (prefill reads
-        # those): bounded by LMX_RS_PACK_GB so a model that fills the GPU
-        # (Llama-3-70B at TP=1) keeps its KV-cache room
-        import os
-        budget = float(os.environ.get("LMX_RS_PACK_GB", "24")) * (1 << 30)
-        used = sum(t.numel() * t.element_size() for t in _RS_PACKED.values())
-        if used + w.numel() * w.element_size() > budget:
-            return False
-        _RS_PACKED[key] = rsgemm_pack(w)
+    # the packed copies sit beside the row-major weights (prefill reads
+    # those): bounded by LMX_RS_PACK_GB so a model that fills the GPU
+    # (Llama-3-70B at TP=1) keeps its KV-cache room
+    import os
+    import weakref
+    nbytes = w.numel() * w.element_size()
+    if _RS_PACKED_BYTES[0] + nbytes > float(os.environ.get("LMX_RS_PACK_GB", "24")) * (1 << 30):
+        return False
+    w._lmx_rs_packed = rsgemm_pack(w)
+    _RS_PACKED_BYTES[0] += nbytes
+    weakref.finalize(w, _rs_unpacked, nbytes)
     return True
+
+
+def _rs_unpacked(nbytes: int) -> None:
+    _RS_PACKED_BYTES[0] -= nbytes
 
 
 def rsgemm_pack(w: torch.Tensor) -> torch.Tensor:
@@ -1124,7 +1137,7 @@ def rsgemm(a: torch.Tensor, w: torch.Tensor, cfg: int, splits: int, epi: int = 0
     if not packed and not (cfg & RS_ROWMAJOR) and a.is_cuda:
         # a table entry on packed weights: the copy rs_prepare built, else
         # the row-major form of the same ring shape
-        wp = _RS_PACKED.get((w.data_ptr(), N, K))
+        wp = _rs_packed_of(w)
         if wp is not None:
             w, packed = wp, True
     cfg = (cfg & ~RS_ROWMAJOR) | (0 if packed else RS_ROWMAJOR)
