@@ -171,7 +171,7 @@ __global__ void __launch_bounds__(RS_THREADS, 2) __attribute__((amdgpu_waves_per
   // fewer slots the early steps would see fewer ops behind a load than the
   // steady-state counts assume)
   static_assert(D % 2 == 0 && U >= 2 && NA == U + 1, "ring shape");
-  static_assert(BM == 256 || BM == 128, "row tile");
+  static_assert(BM == 256 || BM == 128 || BM == 64, "row tile");
   constexpr int NG = BM / 16, G = BM / 64, OPS = G + 4;   // row groups; VMEM ops per step
   constexpr int SLOT = BM * RS_BK;                  // bf16 elements of one A ring slot
   // with NA = U + 1, A(t) is issued just before W(2t) (step t - U): waiting
@@ -404,7 +404,8 @@ static int rs_launch(bf16_t* C, const bf16_t* A, const bf16_t* Wp, float* slabs,
 }
 
 // cfg: bits 0-1 ring shape (0: D 6 / NA 4, 2: D 4 / NA 3), bit 2 128-row
-// tiles (else all 256 rows), bit 5 non-temporal weight loads, bit 6 row-major
+// tiles, bit 3 64-row tiles (else all 256 rows), bit 5 non-temporal weight
+// loads, bit 6 row-major
 // weights (W [N][ldw] as stored; else W is rsgemm_pack's layout).  The K
 // slice must be a multiple of U = D / 2 K64 steps.
 int rsgemm(void* C, const void* A, const void* W, float* slabs, unsigned* tickets,
@@ -412,7 +413,9 @@ int rsgemm(void* C, const void* A, const void* W, float* slabs, unsigned* ticket
            int epi, hipStream_t stream) {
   if (M <= 0) return 0;
   if (M > 256 || N % RS_BN != 0 || splits < 1 || K % (splits * RS_BK) != 0) return -1;
-  const int shape = cfg & 3, bm128 = (cfg >> 2) & 1, nt = (cfg >> 5) & 1, rm = (cfg >> 6) & 1;
+  const int shape = cfg & 3, bm128 = (cfg >> 2) & 1, bm64 = (cfg >> 3) & 1;
+  const int nt = (cfg >> 5) & 1, rm = (cfg >> 6) & 1;
+  const int bm = bm64 ? 64 : bm128 ? 128 : 256;
   // shape 1 (D 8 / NA 5) needs 256+ VGPRs: the compiler spills, and a spill
   // of an inline-asm load destination before its data lands is silent
   // corruption (cdna guide §5.7 item 1) -- not built
@@ -425,7 +428,7 @@ int rsgemm(void* C, const void* A, const void* W, float* slabs, unsigned* ticket
   if (epi != 0 && epi != 2 && epi != 3) return -1;
   if (rm && (ldw < K || ldw % 8 != 0 || 32L * ldw * 2 > (1L << 31))) return -1;
   if ((splits > 1 || epi == 2) && slabs == nullptr) return -2;
-  const int tiles = ((M + (bm128 ? 127 : 255)) / (bm128 ? 128 : 256)) * (N / RS_BN);
+  const int tiles = ((M + bm - 1) / bm) * (N / RS_BN);
   if (splits > 1 && epi != 2 && (tickets == nullptr || tiles > n_tickets)) return -3;
   auto C_ = (bf16_t*)C;
   auto A_ = (const bf16_t*)A;
@@ -438,7 +441,8 @@ int rsgemm(void* C, const void* A, const void* W, float* slabs, unsigned* ticket
   return rs_launch<0, D, NA, NT, RM, BM>(C_, A_, W_, slabs, tickets, M, N, K, lda, ldw, ldc,     \
                                          splits, stream);
 #define LMX_RS_B(D, NA, NT, RM)                 \
-  if (bm128) { LMX_RS_E(D, NA, NT, RM, 128) }   \
+  if (bm == 64) { LMX_RS_E(D, NA, NT, RM, 64) } \
+  if (bm == 128) { LMX_RS_E(D, NA, NT, RM, 128) } \
   LMX_RS_E(D, NA, NT, RM, 256)
 #define LMX_RS(D, NA)                                  \
   if (nt && rm) { LMX_RS_B(D, NA, 1, 1) }              \

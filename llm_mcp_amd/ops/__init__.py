@@ -996,7 +996,7 @@ def dgemm_partials(a: torch.Tensor, w: torch.Tensor, cfg: int, splits: int) -> P
 # K14: register-streamed decode GEMM, 129..256 rows (csrc/kernels/rsgemm.hip)
 # ---------------------------------------------------------------------------
 RS_BN = 256
-RS_ROWMAJOR, RS_NT, RS_BM128 = 64, 32, 4   # cfg bits: row-major weights, nt stream, 128-row tiles
+RS_ROWMAJOR, RS_NT, RS_BM128, RS_BM64 = 64, 32, 4, 8   # cfg bits: row-major W, nt, 128 / 64-row tiles
 RS_U = {0: 3, 2: 2}               # cfg & 3 -> K64 steps per ring block (D6 / D4)
 RSGEMM_CALLS = [0]                # host-side launch count (tests: the K14 path ran)
 _RS_TABLE: dict | None = None
@@ -1172,7 +1172,7 @@ def rsgemm(a: torch.Tensor, w: torch.Tensor, cfg: int, splits: int, epi: int = 0
          and out.data_ptr() % 8 == 0, "rsgemm output layout")
     slabs = cnt = None
     if splits > 1:
-        bm = 128 if cfg & RS_BM128 else 256
+        bm = 64 if cfg & RS_BM64 else 128 if cfg & RS_BM128 else 256
         _chk(-(-M // bm) * (N // RS_BN) <= _RS_CNT, "rsgemm tile count")
         slabs, cnt = _rs_workspace(a.device, splits * M * N)
     native().rsgemm(_ptr(out), _ptr(a), _ptr(w), _ptr(slabs), _ptr(cnt), _RS_CNT, M, N, K,

@@ -835,7 +835,7 @@ def test_prefill_fused_q_rope(Hq, Hkv, D, lead, prefill_waves):
 
 
 # ---- K14: register-streamed decode GEMM (csrc/kernels/rsgemm.hip) ----
-@pytest.mark.parametrize("cfg", [2, 2 | 32, 0, 0 | 32, 2 | 4 | 32, 0 | 4])
+@pytest.mark.parametrize("cfg", [2, 2 | 32, 0, 0 | 32, 2 | 4 | 32, 0 | 4, 2 | 8 | 32])
 @pytest.mark.parametrize("M", [256, 200, 129, 17])
 def test_rsgemm_vs_fp32(cfg, M):
     """K14 against the fp32 reference: row-major and packed weights, every
