@@ -216,7 +216,7 @@ def main() -> None:
                         max_model_len=min(8192, a.prompt_len + a.max_tokens + 64),
                         use_graphs=not a.no_graphs, seed=rank,
                         # rehearsal: every rank shares cuda:0's 288 GB
-                        kv_cache_gb=(max(4, min(24, 160 // world)) if a.rehearse_on_one_gpu
+                        kv_cache_gb=(max(4, min(24, 128 // world)) if a.rehearse_on_one_gpu
                                      else None) if not a.cpu else 0.05)
     follower = None
     if tpctx is None:
