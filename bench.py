@@ -390,6 +390,13 @@ def main() -> None:
                                   "decode_graph_buckets": len(engine.graphs),
                                   "kv_pages": "K [BS][D] token-major, V [BS/4][D][4] key-quad",
                                   "max_batched_tokens": a.max_batched_tokens},
+                       "tp_group": None if a.tp == 1 else {
+                           "collectives": "gloo (one-GPU rehearsal)" if (a.rehearse_on_one_gpu or a.cpu)
+                           else "nccl (RCCL)",
+                           "peer_memory_allreduce_allgather": tpctx is not None and
+                           tpctx.peer is not None,
+                           "startup_selftest": getattr(engine, "tp_selftest", None),
+                           "lookahead": bool(engine.lookahead)},
                        "engine_steps": sum(x["steps"] for x in allr),
                        "graph_steps": sum(x["graph_steps"] for x in allr)},
         }

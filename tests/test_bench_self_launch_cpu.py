@@ -49,6 +49,8 @@ def test_bench_self_launch_json_contract(gpus, tp):
     assert out["value"] > 0 and len(out["per_gpu_tok_s"]) == n_eng
     assert all(v > 0 for v in out["per_gpu_tok_s"])
     assert len(out["decode_step_ms"]) == gpus      # one entry per rank (max over ranks)
+    if tp > 1:     # the TP group's start-up collective self-test ran and passed
+        assert out["config"]["tp_group"]["startup_selftest"]["backend"] == "gloo"
     tokens = out["value"] * out["ms_per_step"] * out["steps"] / 1e3
     assert abs(tokens - 2 * (4 * n_eng) * 4) <= 0.02 * tokens
 
