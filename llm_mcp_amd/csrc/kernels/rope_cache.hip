@@ -143,11 +143,13 @@ __global__ void __launch_bounds__(256) rope_cache_tiled_kernel(
     const int* __restrict__ slot_mapping, bf16_t* __restrict__ k_cache,
     bf16_t* __restrict__ v_cache, int BS, int rotate_k_inplace,
     const bf16_t* __restrict__ q_norm, const bf16_t* __restrict__ k_norm, float eps, int skip_q) {
-  __shared__ __attribute__((aligned(16))) bf16_t vt[RT * (256 + 8)];
+  // V staging tile: up to VCOLS columns (HG whole heads) of 32 tokens
+  constexpr int VCOLS = 1024;
+  __shared__ __attribute__((aligned(16))) bf16_t vt[RT * (VCOLS + 8)];
   __shared__ int sslot[RT];
   const int t0 = row0 + blockIdx.x * RT;
   const int nt = min(RT, T - t0);
-  const int half = D >> 1, tph = half >> 2;
+  const int half = D >> 1, tph = half >> 3;   // 8-pair chunks per head
   if (threadIdx.x < RT)
     sslot[threadIdx.x] = (threadIdx.x < nt && slot_mapping) ? slot_mapping[t0 + threadIdx.x] : -1;
   __syncthreads();
@@ -157,22 +159,27 @@ __global__ void __launch_bounds__(256) rope_cache_tiled_kernel(
   const int H = Hq + Hkv;
   constexpr int HU = 4;
   for (int it = threadIdx.x; it < nt * tph; it += blockDim.x) {
-    const int tt = it / tph, i = (it % tph) * 4;
+    const int tt = it / tph, i = (it % tph) * 8;
     bf16_t* row = qkv + (long)(t0 + tt) * qkv_stride;
     const float* cs = cos_sin + (long)positions[t0 + tt] * D;
     const int slot = sslot[tt];
-    const float4 c = *reinterpret_cast<const float4*>(cs + i);
-    const float4 sn = *reinterpret_cast<const float4*>(cs + half + i);
-    const float cc[4] = {c.x, c.y, c.z, c.w}, ss[4] = {sn.x, sn.y, sn.z, sn.w};
+    float cc[8], ss[8];
+#pragma unroll
+    for (int q4 = 0; q4 < 2; ++q4) {
+      const float4 c = *reinterpret_cast<const float4*>(cs + i + 4 * q4);
+      const float4 sn = *reinterpret_cast<const float4*>(cs + half + i + 4 * q4);
+      cc[4 * q4] = c.x; cc[4 * q4 + 1] = c.y; cc[4 * q4 + 2] = c.z; cc[4 * q4 + 3] = c.w;
+      ss[4 * q4] = sn.x; ss[4 * q4 + 1] = sn.y; ss[4 * q4 + 2] = sn.z; ss[4 * q4 + 3] = sn.w;
+    }
     // skip_q: the prefill attention rotates q itself (paged_prefill rope_cs)
     for (int h0 = skip_q ? Hq : 0; h0 < H; h0 += HU) {
-      bf16x4_t x1[HU], x2[HU];
+      u16x8 x1[HU], x2[HU];
 #pragma unroll
       for (int u = 0; u < HU; ++u) {
         if (h0 + u < H) {
           const bf16_t* hp = row + (long)(h0 + u) * D;
-          x1[u] = *reinterpret_cast<const bf16x4_t*>(hp + i);
-          x2[u] = *reinterpret_cast<const bf16x4_t*>(hp + half + i);
+          x1[u] = *reinterpret_cast<const u16x8*>(hp + i);
+          x2[u] = *reinterpret_cast<const u16x8*>(hp + half + i);
         }
       }
 #pragma unroll
@@ -181,44 +188,66 @@ __global__ void __launch_bounds__(256) rope_cache_tiled_kernel(
         if (h >= H) break;
         bf16_t* hp = row + (long)h * D;
         const bool is_k = h >= Hq;
-        float a[4], b[4];
+        float a[8], b[8];
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          a[j] = bf2f((uint16_t)x1[u][j]), b[j] = bf2f((uint16_t)x2[u][j]);
-        if (q_norm) qk_norm(a, b, is_k ? k_norm : q_norm, i, half, D, eps);
-        bf16x4_t o1, o2;
+        for (int j = 0; j < 8; ++j) a[j] = bf2f(x1[u].v[j]), b[j] = bf2f(x2[u].v[j]);
+        if (q_norm) {
+          // per-head RMSNorm of q / k (Qwen3): the head's D values are spread
+          // over the 8 consecutive lanes of this (token, head)
+          float sq = 0.f;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          o1[j] = (short)f2bf(a[j] * cc[j] - b[j] * ss[j]);
-          o2[j] = (short)f2bf(b[j] * cc[j] + a[j] * ss[j]);
+          for (int j = 0; j < 8; ++j) sq += a[j] * a[j] + b[j] * b[j];
+#pragma unroll
+          for (int o = 4; o > 0; o >>= 1) sq += __shfl_xor(sq, o, 8);
+          const float r = rsqrtf(sq / (float)D + eps);
+          const bf16_t* w = is_k ? k_norm : q_norm;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            a[j] *= r * bf2f(w[i + j]);
+            b[j] *= r * bf2f(w[half + i + j]);
+          }
+        }
+        u16x8 o1, o2;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          o1.v[j] = f2bf(a[j] * cc[j] - b[j] * ss[j]);
+          o2.v[j] = f2bf(b[j] * cc[j] + a[j] * ss[j]);
         }
         if (!is_k || rotate_k_inplace || slot < 0) {
-          *reinterpret_cast<bf16x4_t*>(hp + i) = o1;
-          *reinterpret_cast<bf16x4_t*>(hp + half + i) = o2;
+          *reinterpret_cast<u16x8*>(hp + i) = o1;
+          *reinterpret_cast<u16x8*>(hp + half + i) = o2;
         }
         if (is_k && slot >= 0 && k_cache) {
           bf16_t* kp = k_cache + (((long)(slot / BS) * Hkv + (h - Hq)) * BS + slot % BS) * D;
-          *reinterpret_cast<bf16x4_t*>(kp + i) = o1;
-          *reinterpret_cast<bf16x4_t*>(kp + half + i) = o2;
+          *reinterpret_cast<u16x8*>(kp + i) = o1;
+          *reinterpret_cast<u16x8*>(kp + half + i) = o2;
         }
       }
     }
   }
   if (!v_cache || !slot_mapping) return;
-  const int LD = D + 8, chunks = D / 8;
-  for (int h = 0; h < Hkv; ++h) {
+  // HG heads per LDS pass (all 8 of Llama-3 at D 128): two barriers per pass
+  // instead of two per head
+  const int HG = VCOLS / D < Hkv ? VCOLS / D : Hkv;
+  const int LD = HG * D + 8, chunks = HG * D / 8;
+  for (int h0 = 0; h0 < Hkv; h0 += HG) {
+    const int hg = Hkv - h0 < HG ? Hkv - h0 : HG;
     for (int it = threadIdx.x; it < nt * chunks; it += blockDim.x) {
       const int tt = it / chunks, c = it - tt * chunks;
-      const bf16_t* src = qkv + (long)(t0 + tt) * qkv_stride + (long)(Hq + Hkv + h) * D + 8 * c;
+      if (8 * c >= hg * D) continue;
+      const bf16_t* src = qkv + (long)(t0 + tt) * qkv_stride + (long)(Hq + Hkv + h0) * D + 8 * c;
       *reinterpret_cast<u16x8*>(&vt[tt * LD + 8 * c]) = *reinterpret_cast<const u16x8*>(src);
     }
     __syncthreads();
-    // one 16-B store per (key quad, d pair): 4 tokens x 2 d of the
+    // one 16-B store per (head, key quad, d pair): 4 tokens x 2 d of the
     // key-quad page, whenever the quad's 4 slots are consecutive and
     // 4-aligned (always, inside a prefill chunk's whole pages)
-    for (int it = threadIdx.x; it < (D / 2) * (RT / 4); it += blockDim.x) {
-      const int d = 2 * (it % (D / 2)), tt0 = (it / (D / 2)) * 4;
+    const int per_h = (D / 2) * (RT / 4);
+    for (int it = threadIdx.x; it < hg * per_h; it += blockDim.x) {
+      const int hl = it / per_h, r = it - hl * per_h;
+      const int d = 2 * (r % (D / 2)), tt0 = (r / (D / 2)) * 4, h = h0 + hl;
       if (tt0 >= nt) continue;
+      const int col = hl * D + d;
       const int s0 = sslot[tt0];
       bool vec = tt0 + 4 <= nt && s0 >= 0 && (s0 % 4) == 0;
 #pragma unroll
@@ -227,8 +256,8 @@ __global__ void __launch_bounds__(256) rope_cache_tiled_kernel(
         u16x8 w;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          w.v[j] = vt[(tt0 + j) * LD + d];
-          w.v[4 + j] = vt[(tt0 + j) * LD + d + 1];
+          w.v[j] = vt[(tt0 + j) * LD + col];
+          w.v[4 + j] = vt[(tt0 + j) * LD + col + 1];
         }
         *reinterpret_cast<u16x8*>(v_cache + ((long)(s0 / BS) * Hkv + h) * BS * D +
                                   vq_off(d, s0 % BS, D)) = w;
@@ -237,8 +266,8 @@ __global__ void __launch_bounds__(256) rope_cache_tiled_kernel(
           const int sl = sslot[tt0 + j];
           if (sl < 0) continue;
           bf16_t* vp = v_cache + ((long)(sl / BS) * Hkv + h) * BS * D + vq_off(d, sl % BS, D);
-          vp[0] = vt[(tt0 + j) * LD + d];
-          vp[4] = vt[(tt0 + j) * LD + d + 1];
+          vp[0] = vt[(tt0 + j) * LD + col];
+          vp[4] = vt[(tt0 + j) * LD + col + 1];
         }
       }
     }
@@ -253,7 +282,7 @@ int rope_cache(void* qkv, long qkv_stride, const int* positions, const float* co
   if (T <= 0) return 0;
   // skip_q only for the tiled (prefill) rows and without q/k norms
   if (skip_q && (tile_from > 0 || q_norm != nullptr)) return -1;
-  if (D % 8 != 0 || D > 256) return -1;
+  if (D % 16 != 0 || D > 256) return -1;       // 8-pair rotation chunks
   if ((q_norm == nullptr) != (k_norm == nullptr) || (q_norm && D != 128)) return -1;
   const int n1 = tile_from < 0 ? 0 : (tile_from > T ? T : tile_from);
   if (n1 > 0) {

@@ -49,20 +49,24 @@ def main():
     slotsp = torch.arange(TP, device=dev, dtype=torch.int32)
     kcp = torch.zeros(TP // BS, Hkv, BS, D, device=dev, dtype=torch.bfloat16)
     vcp = torch.zeros(TP // BS, Hkv, BS // 4, D, 4, device=dev, dtype=torch.bfloat16)
-    for _ in range(5):
-        nat.rope_cache(qkvp.data_ptr(), qkvp.stride(0), posp.data_ptr(), cs.data_ptr(), TP, Hq,
-                       Hkv, D, slotsp.data_ptr(), kcp.data_ptr(), vcp.data_ptr(), BS, 0, 0, 0, 0,
-                       1e-6, 0, st)
-    torch.cuda.synchronize()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(50):
-        nat.rope_cache(qkvp.data_ptr(), qkvp.stride(0), posp.data_ptr(), cs.data_ptr(), TP, Hq,
-                       Hkv, D, slotsp.data_ptr(), kcp.data_ptr(), vcp.data_ptr(), BS, 0, 0, 0, 0,
-                       1e-6, 0, st)
-    e.record()
-    torch.cuda.synchronize()
-    print(f"rope_cache tiled T={TP} {s.elapsed_time(e) / 50 * 1e3:7.2f} us", flush=True)
+    for skip_q in (0, 1):      # 1: the engine's prefill form (q rotated in attention)
+        for _ in range(5):
+            nat.rope_cache(qkvp.data_ptr(), qkvp.stride(0), posp.data_ptr(), cs.data_ptr(), TP,
+                           Hq, Hkv, D, slotsp.data_ptr(), kcp.data_ptr(), vcp.data_ptr(), BS, 0,
+                           0, 0, 0, 1e-6, skip_q, st)
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(50):
+            nat.rope_cache(qkvp.data_ptr(), qkvp.stride(0), posp.data_ptr(), cs.data_ptr(), TP,
+                           Hq, Hkv, D, slotsp.data_ptr(), kcp.data_ptr(), vcp.data_ptr(), BS, 0,
+                           0, 0, 0, 1e-6, skip_q, st)
+        e.record()
+        torch.cuda.synchronize()
+        us = s.elapsed_time(e) / 50 * 1e3
+        nbytes = TP * Hkv * D * 2 * 4 + (0 if skip_q else TP * Hq * D * 2 * 2)
+        print(f"rope_cache tiled T={TP} skip_q={skip_q} {us:7.2f} us "
+              f"({nbytes / us / 1e6:.2f} TB/s of q/k/v/cache bytes)", flush=True)
     for name, args in variants.items():
         for _ in range(10):
             call(*args)
