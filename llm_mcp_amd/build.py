@@ -29,7 +29,7 @@ ARCH = os.environ.get("LMX_OFFLOAD_ARCH", "gfx950")
 EXT = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 
 KERNEL_SOURCES = ["norm.hip", "rope_cache.hip", "attention.hip", "sampling.hip",
-                  "elementwise.hip", "gemm.hip", "dgemm.hip", "wgemm.hip", "pgemm.hip",
+                  "elementwise.hip", "gemm.hip", "dgemm.hip", "pgemm.hip",
                   "rsgemm.hip", "allreduce.hip"]
 RUNTIME_SOURCES = ["job_queue.cpp", "block_manager.cpp", "scheduler.cpp", "bindings.cpp"]
 

@@ -54,15 +54,10 @@ int rsgemm_pack(void*, const void*, int, int, long, hipStream_t);
 int rmsnorm_slabs(void*, void*, const float*, int, long, const void*, int, int, long, float,
                   hipStream_t);
 int dgemm_config(int, int*, int*);
-int wgemm(void*, const void*, const void*, float*, unsigned*, int, int, int, int, long, long, long,
-          int, int, int, hipStream_t);
-int wgemm_pack(void*, const void*, int, int, long, int, hipStream_t);
 int pgemm(void*, const void*, const void*, const void*, int, int, int, long, long, long, int, int,
-          int, hipStream_t);
+          hipStream_t);
 int pgemm_sk(void*, const void*, const void*, void*, void*, int, int, int, int, long, long, long,
              int, int, int, hipStream_t);
-int wgemm_num_configs();
-int wgemm_config(int, int*, int*);
 long ar_region_bytes(long);
 int ar_alloc(void**, long);
 int ar_free(void*);
@@ -219,18 +214,11 @@ PYBIND11_MODULE(_lmx_kernels, m) {
   m.def("rsgemm_pack", [](uptr out, uptr W, int N, int K, long ldw, uptr stream) {
     check(lmx::rsgemm_pack(P<void>(out), P<void>(W), N, K, ldw, S(stream)), "rsgemm_pack");
   });
-  // ---- K12 weight-streaming GEMM (wgemm.hip) ----
-  m.def("wgemm", [](uptr C, uptr A, uptr W, uptr slabs, uptr cnt, int n_cnt, int M, int N, int K,
-                    long lda, long ldw, long ldc, int cfg, int splits, int epi, uptr stream) {
-    check(lmx::wgemm(P<void>(C), P<void>(A), P<void>(W), P<float>(slabs), P<unsigned>(cnt), n_cnt,
-                     M, N, K, lda, ldw, ldc, cfg, splits, epi, S(stream)),
-          "wgemm");
-  });
   // ---- K13 large-M GEMM (pgemm.hip) ----
   m.def("pgemm", [](uptr C, uptr A, uptr W, uptr bias, int M, int N, int K, long lda, long ldw,
-                    long ldc, int act, int grid, int variant, uptr stream) {
+                    long ldc, int act, int grid, uptr stream) {
     check(lmx::pgemm(P<void>(C), P<void>(A), P<void>(W), P<void>(bias), M, N, K, lda, ldw, ldc,
-                     act, grid, variant, S(stream)),
+                     act, grid, S(stream)),
           "pgemm");
   });
   m.def("pgemm_sk", [](uptr C, uptr A, uptr W, uptr slabs, uptr cnt, int n_cnt, int M, int N,
@@ -239,18 +227,6 @@ PYBIND11_MODULE(_lmx_kernels, m) {
     check(lmx::pgemm_sk(P<void>(C), P<void>(A), P<void>(W), P<void>(slabs), P<void>(cnt), n_cnt,
                         M, N, K, lda, ldw, ldc, act, splits, epi, S(stream)),
           "pgemm_sk");
-  });
-  m.def("wgemm_pack", [](uptr P_, uptr W, int N, int K, long ldw, int cfg, uptr stream) {
-    check(lmx::wgemm_pack(P<void>(P_), P<void>(W), N, K, ldw, cfg, S(stream)), "wgemm_pack");
-  });
-  m.def("wgemm_configs", []() {
-    std::vector<std::pair<int, int>> out;
-    for (int i = 0; i < lmx::wgemm_num_configs(); ++i) {
-      int bn = 0, bk = 0;
-      lmx::wgemm_config(i, &bn, &bk);
-      out.emplace_back(bn, bk);
-    }
-    return out;
   });
   // ---- peer-memory all-reduce (allreduce.hip) ----
   m.def("ar_region_bytes", [](long slot) { return lmx::ar_region_bytes(slot); });

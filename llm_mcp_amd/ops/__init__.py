@@ -1181,87 +1181,9 @@ def rsgemm(a: torch.Tensor, w: torch.Tensor, cfg: int, splits: int, epi: int = 0
 
 
 # ---------------------------------------------------------------------------
-# K12: weight-streaming GEMM for 129..256-row decode batches (csrc/kernels/wgemm.hip)
-# ---------------------------------------------------------------------------
-# configuration ids the library builds (wgemm.hip LMX_WG_CONFIGS):
-# id -> (BN, BK); 4 waves, one workgroup per CU, all 256 rows per tile
-WGEMM_CONFIGS = {3: (112, 64), 6: (128, 64), 8: (96, 64), 12: (128, 64), 13: (112, 64)}
-WGEMM_NT, WGEMM_PACKED, WGEMM_KMAJOR = 32, 128, 1024
-WGEMM_SWIGLU_BLOCK = 4         # gate/up interleave of the epi-3 form
-_WG_WS: dict = {}
-_WG_CNT = 4096
-
-
-def wgemm_pack(w: torch.Tensor, cfg: int, kmajor: bool = True) -> torch.Tensor:
-    """``w`` [N, K] rearranged into the packed layout of K12 configuration
-    ``cfg`` (every (column tile, K-step) LDS image contiguous; K-steps
-    outermost with ``kmajor``).  Same element count, opaque layout."""
-    _bf16(w, "w")
-    N, K = w.shape
-    bn, bk = WGEMM_CONFIGS[cfg & 31]
-    _chk(N % bn == 0 and K % bk == 0 and w.stride(1) == 1 and w.stride(0) % 8 == 0,
-         f"wgemm_pack shape N={N} K={K} cfg={cfg}")
-    out = torch.empty_like(w, memory_format=torch.contiguous_format)
-    native().wgemm_pack(_ptr(out), _ptr(w), N, K, w.stride(0),
-                        cfg | (WGEMM_KMAJOR if kmajor else 0), _stream())
-    return out
-
-
-def _wg_workspace(dev: torch.device, n_floats: int):
-    key = (dev.index, _stream())
-    ws = _WG_WS.get(key)
-    if ws is None or ws[0].numel() < n_floats:
-        if torch.cuda.is_current_stream_capturing():
-            raise RuntimeError("wgemm workspace must be allocated before graph capture")
-        n_floats = max(n_floats, ws[0].numel() if ws else 0, 1 << 20)
-        cnt = ws[1] if ws else torch.zeros(_WG_CNT, dtype=torch.int32, device=dev)
-        ws = (torch.empty(n_floats, dtype=torch.float32, device=dev), cnt)
-        _retire_ws(_WG_WS.get(key))
-        _WG_WS[key] = ws
-    return ws
-
-
-def wgemm(a: torch.Tensor, w: torch.Tensor, cfg: int, splits: int = 1, epi: int = 0,
-          packed: int = 0, out: torch.Tensor | None = None):
-    """a @ w^T on K12 for M <= 256 rows.  ``epi``: 0 bf16 [M, N]; 2 fp32
-    partials (``Partials``, summed by ``rms_norm``); 3 SwiGLU over gate/up
-    weights interleaved per 4 rows (``interleave_gate_up(w, 4)``), [M, N/2].
-    ``packed``: 0 row-major ``w``; 2 ``w`` from ``wgemm_pack`` (K-step-major;
-    the tile-major layout 1 is a lab-only build)."""
-    M, K = a.shape
-    N = w.shape[0]
-    bn, bk = WGEMM_CONFIGS[cfg & 31]
-    _bf16(a, "a"); _bf16(w, "w")
-    _chk(0 < M <= 256 and N % bn == 0 and K % bk == 0 and K // bk >= splits >= 1,
-         f"wgemm shape M={M} N={N} K={K} cfg={cfg} splits={splits}")
-    _chk(w.shape[1] == K and a.stride(1) == 1 and w.stride(1) == 1 and a.stride(0) % 8 == 0
-         and w.stride(0) % 8 == 0 and a.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0,
-         "wgemm operands need 16-B aligned rows")
-    code = cfg | (WGEMM_PACKED if packed else 0) | (WGEMM_KMAJOR if packed == 2 else 0)
-    slabs = cnt = None
-    if epi == 2:
-        slabs, cnt = _wg_workspace(a.device, splits * M * N)
-        native().wgemm(0, _ptr(a), _ptr(w), _ptr(slabs), _ptr(cnt), _WG_CNT, M, N, K,
-                       a.stride(0), w.stride(0), N, code, splits, 2, _stream())
-        return Partials(slabs[:splits * M * N].view(splits, M, N), splits, M, N)
-    ncols = N // 2 if epi == 3 else N
-    if out is None:
-        out = torch.empty((M, ncols), dtype=a.dtype, device=a.device)
-    _chk(out.shape == (M, ncols) and out.stride(1) == 1 and out.stride(0) % 4 == 0,
-         "wgemm output layout")
-    if splits > 1:
-        _chk(2 * (N // bn) <= _WG_CNT, "wgemm tile count")
-        slabs, cnt = _wg_workspace(a.device, splits * 256 * N)
-    native().wgemm(_ptr(out), _ptr(a), _ptr(w), _ptr(slabs), _ptr(cnt), _WG_CNT, M, N, K,
-                   a.stride(0), w.stride(0), out.stride(0), code, splits, epi, _stream())
-    return out
-
-
-# ---------------------------------------------------------------------------
 # K13: large-M GEMM (csrc/kernels/pgemm.hip): prefill chunks, encoder batches
 # ---------------------------------------------------------------------------
 PGEMM_MAX_BIAS = 8192
-PGEMM_VARIANT = 2
 PGEMM_CALLS = [0]          # host-side launch count (tests: the K13 path really ran)
 
 
@@ -1286,16 +1208,12 @@ def pgemm_bias_ok(bias: torch.Tensor | None, N: int) -> bool:
 
 
 def pgemm(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, act: int = 0,
-          out: torch.Tensor | None = None, grid: int = 0,
-          variant: int | None = None) -> torch.Tensor:
+          out: torch.Tensor | None = None, grid: int = 0) -> torch.Tensor:
     """act(a @ w^T + bias) on the persistent 256x256 MFMA GEMM (any M).
     act: ACT_NONE / ACT_GELU (tanh) / ACT_SILU / ACT_GELU_ERF, or ACT_SWIGLU
     with ``w`` from ``interleave_gate_up(w, 16)`` (result [M, N/2]).
-    ``grid``: workgroups (0 = one per CU); ``variant`` (default
-    PGEMM_VARIANT): 2 eight-wave ping-pong, 2 phases per K-step; 3 the same
-    with the DMA split 4/4 over the phases; 1 ping-pong with 4 phases per
-    K-step; 0 four waves (one per SIMD), 192x256 tiles -- the measured
-    design points of csrc/kernels/pgemm.hip."""
+    ``grid``: workgroups (0 = one per CU).  The losing design points of
+    the kernel (tools/lab_kernels/pgemm_lab.hip) are lab-only."""
     M, K = a.shape
     N = w.shape[0]
     ncols = N // 2 if act == ACT_SWIGLU else N
@@ -1325,8 +1243,7 @@ def pgemm(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, ac
          and out.data_ptr() % 8 == 0, "pgemm output layout")
     PGEMM_CALLS[0] += 1
     native().pgemm(_ptr(out), _ptr(a), _ptr(w), _ptr(bias), M, N, K, a.stride(0), w.stride(0),
-                   out.stride(0), act, grid, PGEMM_VARIANT if variant is None else variant,
-                   _stream())
+                   out.stride(0), act, grid, _stream())
     return out
 
 

@@ -27,7 +27,6 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--only", default="")
     ap.add_argument("--grid", type=int, default=0)
-    ap.add_argument("--variant", type=int, default=None, help="default: ops.PGEMM_VARIANT")
     a = ap.parse_args()
     ops.native()
     torch.manual_seed(0)
@@ -39,7 +38,7 @@ def main():
             w = (torch.rand(N, K, device="cuda", dtype=torch.bfloat16) * 2 - 1) * K ** -0.5
             out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
             ref = torch.nn.functional.linear(x, w)
-            ops.pgemm(x, w, out=out, grid=a.grid, variant=a.variant)
+            ops.pgemm(x, w, out=out, grid=a.grid)
             err = (out.float() - ref.float()).abs().max().item()
             fl = 2.0 * M * N * K
             iters = max(3, min(50, int(3e12 / fl)))
@@ -49,7 +48,7 @@ def main():
                 for kind in ("lib", "k13"):
                     s, e = ev(), ev()
                     fn = (lambda: torch.nn.functional.linear(x, w)) if kind == "lib" else \
-                        (lambda: ops.pgemm(x, w, out=out, grid=a.grid, variant=a.variant))
+                        (lambda: ops.pgemm(x, w, out=out, grid=a.grid))
                     fn()
                     s.record()
                     for _ in range(iters):

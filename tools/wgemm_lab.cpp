@@ -1,4 +1,4 @@
-// Standalone lab for the K12 weight-streaming GEMM (csrc/kernels/wgemm.hip):
+// Standalone lab for the K12 weight-streaming GEMM (tools/lab_kernels/wgemm.hip):
 // no torch, so a run on a fresh GPU box starts in seconds.  For one decode
 // projection shape it checks each configuration against a plain fp32
 // reference on a sample of rows, then times it on COLD weights (the weight
@@ -7,7 +7,7 @@
 // the achievable-HBM yardstick.
 //
 // build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -DLMX_WGEMM_LAB
-//          -I llm_mcp_amd/csrc/kernels tools/wgemm_lab.cpp -o gpurun_out/wgemm_lab
+//          -I llm_mcp_amd/csrc/kernels -I tools/lab_kernels tools/wgemm_lab.cpp -o tools/labbin/wgemm_lab
 // run:   wgemm_lab <N> <K> <M> <epi> <cfg:splits>[,...] [iters]
 #include <hip/hip_runtime.h>
 

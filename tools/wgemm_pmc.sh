@@ -18,7 +18,7 @@ for spec in "$@"; do
     rm -rf $d
     echo "[pmc] $spec pass $n" >&2
     timeout -s KILL 90 rocprofv3 --pmc $pass --kernel-trace -d $d -o run --output-format csv \
-        -- tools/bin/wgemm_lab $spec 5 > $d.log 2>&1
+        -- tools/labbin/wgemm_lab $spec 5 > $d.log 2>&1
     rc=$?
     if [ $rc -ne 0 ]; then echo "rc $rc"; tail -5 $d.log; exit $rc; fi
   done
