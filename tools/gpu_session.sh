@@ -139,11 +139,13 @@ for step in "$@"; do
       run encoder_bench 600 python -u -m llm_mcp_amd.bench.dgemm_bench --encoder 4096,32768 || exit $? ;;
     prof_bench)
       # the headline bench under a kernel trace; tools/prof_timeline.py splits it into waves/steps
-      rm -rf gpurun_out/prof_bench
-      run prof_bench 900 rocprofv3 --kernel-trace -d gpurun_out/prof_bench -o run \
+      # (PROF_TAG names the run: a second traced run under another env in the same call)
+      tag=${PROF_TAG:-prof_bench}
+      rm -rf gpurun_out/$tag
+      run $tag 900 rocprofv3 --kernel-trace -d gpurun_out/$tag -o run \
           -- python3 bench.py --steps 2 --warmup 1 || exit $?
-      python tools/prof_timeline.py gpurun_out/prof_bench/run_results.db --waves 2 \
-          > gpurun_out/prof_bench_timeline.md 2>&1 || true ;;
+      python tools/prof_timeline.py gpurun_out/$tag/run_results.db --waves 2 \
+          > gpurun_out/${tag}_timeline.md 2>&1 || true ;;
     attn_probe)
       run attn_probe 180 python -u tools/decode_attn_probe.py || exit $? ;;
     embed_bench)
