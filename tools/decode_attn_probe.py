@@ -34,11 +34,18 @@ def main():
                     help="the engine's fused form: q rows are whole unrotated QKV rows, the "
                          "kernel rotates q and writes the step's k/v at ctx-1")
     ap.add_argument("--modes", default="4,0,5,4,0,5")
+    ap.add_argument("--head-major", action="store_true",
+                    help="emulate a head-major cache ([kv head][block] pages): each (sequence, "
+                         "kv head) becomes its own 1-kv-head sequence of the same context, so with "
+                         "--layout contig every segment streams one contiguous run of pages")
     a = ap.parse_args()
     B, Hq, Hkv, D, BS = a.batch, 32, 8, 128, 32
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     ctx = torch.randint(a.ctx_lo, a.ctx_hi + 1, (B,), dtype=torch.int32)
+    if a.head_major:
+        ctx = ctx.repeat_interleave(Hkv)
+        B, Hq, a.pages, Hkv = B * Hkv, Hq // Hkv, a.pages * Hkv, 1
     if a.order != "random":
         ctx = ctx.sort(descending=a.order == "desc").values
     maxb = (a.ctx_hi + BS - 1) // BS
@@ -102,7 +109,7 @@ def main():
         e.record()
         torch.cuda.synchronize()
         us = s.elapsed_time(e) / a.iters * 1e3
-        print(f"decode attn {'rope ' if a.rope else ''}{a.layout} pages={nb} B={B} parts {a.parts}x{a.part_tokens} {a.order} mode {mode}: {us:7.1f} us  {kv_bytes / us / 1e6:5.2f} TB/s  "
+        print(f"decode attn {'rope ' if a.rope else ''}{'head-major ' if a.head_major else ''}{a.layout} pages={nb} B={B} parts {a.parts}x{a.part_tokens} {a.order} mode {mode}: {us:7.1f} us  {kv_bytes / us / 1e6:5.2f} TB/s  "
               f"vs first mode: {same}", flush=True)
     nat.set_decode_mode(0)
     if a.rope:

@@ -145,9 +145,20 @@ for step in "$@"; do
       run $tag 900 rocprofv3 --kernel-trace -d gpurun_out/$tag -o run \
           -- python3 bench.py --steps 2 --warmup 1 || exit $?
       python tools/prof_timeline.py gpurun_out/$tag/run_results.db --waves 2 \
-          > gpurun_out/${tag}_timeline.md 2>&1 || true ;;
+          > gpurun_out/${tag}_timeline.md 2>&1 || true
+      rm -rf gpurun_out/$tag ;;   # the trace database alone exceeds what gpurun copies back
     attn_probe)
       run attn_probe 180 python -u tools/decode_attn_probe.py || exit $? ;;
+    attn_layout)
+      # kv-head-major cache emulation (each segment one contiguous page run) vs the
+      # block-major cache, contiguous and random page placement, default loop form
+      : > gpurun_out/attn_layout.log
+      for args in "--layout contig" "--layout contig --head-major" "--layout random" \
+                  "--layout random --head-major" "--layout engine" "--layout engine --head-major"; do
+        timeout -k 10 120 python -u tools/decode_attn_probe.py $args --rope --modes 0,0,0 \
+            --iters 30 >> gpurun_out/attn_layout.log 2>&1 || exit $?
+      done
+      cat gpurun_out/attn_layout.log ;;
     embed_bench)
       run embed_bench 300 python -u -m llm_mcp_amd.bench.embed_engine_bench || exit $? ;;
     rope_probe)
