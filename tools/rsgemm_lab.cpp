@@ -82,7 +82,12 @@ int main(int argc, char** argv) {
   const int epi = std::atoi(argv[4]);
   const int iters = argc > 6 ? std::atoi(argv[6]) : 30;
   const long wbytes = (long)N * K * 2;
-  const int copies = (int)std::max<long>(2, (512l << 20) / wbytes + 1);
+  // LAB_COPIES: weight copies the calls rotate over (default: > 512 MB, so every
+  // call streams cold weights from HBM; 1 = the same copy every call: warm in L2 /
+  // the 256 MB Infinity Cache as far as it fits)
+  const char* ce = std::getenv("LAB_COPIES");
+  const int copies = ce ? std::max(1, std::atoi(ce))
+                        : (int)std::max<long>(2, (512l << 20) / wbytes + 1);
   std::printf("shape N=%d K=%d M=%d epi=%d: W %.1f MB x %d copies\n", N, K, M, epi, wbytes / 1e6,
               copies);
   bf16_t *A, *Wall, *Wpk, *C;
