@@ -125,40 +125,38 @@ class ChatHandler:
                                    "Cloud models are disabled (set LMX_ALLOW_CLOUD=1 and "
                                    "OPENROUTER_API_KEY)")
             return await cloud(request, body, model, extra_headers)
-        target = st.registry.select(model, "chat", getattr(st, "circuit", None))
-        if target is None:
-            st.metrics.chat_requests(model, "none", "no_device")
-            return write_error(503, "no_device", f"No online device has model '{model}'")
-        tok = target.tokenizer
-        try:
-            prompt_ids = apply_chat_template(tok, messages)
-        except Exception as e:
-            return write_error(400, "invalid_messages", str(e))
-        left = target.max_model_len - len(prompt_ids) - 1
-        if left < 1:
-            return write_error(400, "context_length_exceeded",
-                               f"prompt has {len(prompt_ids)} tokens; model context is "
-                               f"{target.max_model_len}")
-        params = sampling_from_body(body, left)
-        stream = bool(body.get("stream", False))
-        include_usage = bool((body.get("stream_options") or {}).get("include_usage", False))
-        n = body.get("n")
-        try:
-            n = 1 if n is None else int(n)
-        except (TypeError, ValueError):
-            n = 0
-        if not 1 <= n <= 16:
-            return write_error(400, "invalid_n", "'n' must be an integer in [1, 16]")
         # the replica that serves the request, counted against the node-wide
-        # load in the same step as its selection (failover moves it)
+        # load in the same step as its selection (failover moves it); one
+        # selection per request: a validation error below releases it
         target = st.registry.select(model, "chat", getattr(st, "circuit", None), acquire=True)
         if target is None:
             st.metrics.chat_requests(model, "none", "no_device")
             return write_error(503, "no_device", f"No online device has model '{model}'")
-        # vLLM's extension: logprobs entries name their token as "token_id:<id>"
-        box = {"target": target, "ids": bool(body.get("return_tokens_as_token_ids", False))}
-        t0 = time.time()
+        box = {"target": target}
         try:
+            tok = target.tokenizer
+            try:
+                prompt_ids = apply_chat_template(tok, messages)
+            except Exception as e:
+                return write_error(400, "invalid_messages", str(e))
+            left = target.max_model_len - len(prompt_ids) - 1
+            if left < 1:
+                return write_error(400, "context_length_exceeded",
+                                   f"prompt has {len(prompt_ids)} tokens; model context is "
+                                   f"{target.max_model_len}")
+            params = sampling_from_body(body, left)
+            stream = bool(body.get("stream", False))
+            include_usage = bool((body.get("stream_options") or {}).get("include_usage", False))
+            n = body.get("n")
+            try:
+                n = 1 if n is None else int(n)
+            except (TypeError, ValueError):
+                n = 0
+            if not 1 <= n <= 16:
+                return write_error(400, "invalid_n", "'n' must be an integer in [1, 16]")
+            # vLLM's extension: logprobs entries name their token as "token_id:<id>"
+            box["ids"] = bool(body.get("return_tokens_as_token_ids", False))
+            t0 = time.time()
             if n > 1:
                 return await self._multi(request, target, model, prompt_ids, params, n, stream,
                                          include_usage, extra_headers, t0, box["ids"])
