@@ -186,7 +186,7 @@ __device__ __forceinline__ void pg_store(const RT& R, const PgOut& O, const PgTh
     // above, rows 1/3 take tile 1's columns 0-3 from the row below
     // (v_permlane16_swap), so 4 stores per quadrant instead of 8
     f32x4_t b[2];
-    if constexpr (BIAS) {
+    if constexpr (BIAS == 1) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int bc = O.n0 + T.wn * 64 + QN * 32 + 16 * j + 4 * T.fg;
@@ -196,6 +196,19 @@ __device__ __forceinline__ void pg_store(const RT& R, const PgOut& O, const PgTh
       }
     }
     const int col = O.n0 + T.wn * 64 + QN * 32 + 16 * (T.fg & 1) + 8 * (T.fg >> 1);
+    typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+    // BIAS 2: residual epilogue -- C is the bf16 residual stream, updated in
+    // place: C = bf16(C + bf16(acc)), the rounding order of the separate
+    // residual-add pass it replaces.  The quadrant's residual rows are loaded
+    // (16 B per lane, rows >= M read as 0 and their stores dropped) before the
+    // conversions; the compiler waits for them at their first use.
+    u32x4_t res[4];
+    if constexpr (BIAS == 2) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        res[i] = __builtin_amdgcn_raw_buffer_load_b128(
+            O.rc, ((T.wm * 128 + QM * 64 + 16 * i + T.fr) * T.ldc + col) * 2, 0, 0);
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int row = T.wm * 128 + QM * 64 + 16 * i + T.fr;
@@ -206,7 +219,7 @@ __device__ __forceinline__ void pg_store(const RT& R, const PgOut& O, const PgTh
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
           float x0 = v[2 * q], x1 = v[2 * q + 1];
-          if constexpr (BIAS) {
+          if constexpr (BIAS == 1) {
             x0 += b[j][2 * q];
             x1 += b[j][2 * q + 1];
           }
@@ -215,8 +228,15 @@ __device__ __forceinline__ void pg_store(const RT& R, const PgOut& O, const PgTh
       }
       const auto p = __builtin_amdgcn_permlane16_swap(d[0][0], d[1][0], false, false);
       const auto q = __builtin_amdgcn_permlane16_swap(d[0][1], d[1][1], false, false);
-      typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
-      const u32x4_t o = {p[0], q[0], p[1], q[1]};
+      u32x4_t o = {p[0], q[0], p[1], q[1]};
+      if constexpr (BIAS == 2) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float lo = bf2f((uint16_t)(o[e] & 0xffff)) + bf2f((uint16_t)(res[i][e] & 0xffff));
+          const float hi = bf2f((uint16_t)(o[e] >> 16)) + bf2f((uint16_t)(res[i][e] >> 16));
+          o[e] = pack_bf16x2(lo, hi);
+        }
+      }
       __builtin_amdgcn_raw_buffer_store_b128(o, O.rc, (row * T.ldc + col) * 2, 0, 0);
     }
   }
@@ -363,7 +383,7 @@ __global__ void __launch_bounds__(PG_THREADS, 1) pgemm_pp2_kernel(
     T.co[1] = 16 * ((4 + T.fg) ^ s);
   }
 
-  if constexpr (BIAS) {
+  if constexpr (BIAS == 1) {
     for (int c = threadIdx.x * 8; c < N; c += PG_THREADS * 8)
       *reinterpret_cast<bf16x8_t*>(smem + PG_RING_B + c * 2) =
           *reinterpret_cast<const bf16x8_t*>(bias + c);
@@ -698,7 +718,7 @@ static int g_pg_cus = 0;
 template <int ACT, int BIAS>
 static int pg_launch(bf16_t* C, const bf16_t* A, const bf16_t* W, const bf16_t* bias, int M,
                      int N, int K, int lda, int ldw, int ldc, int grid, hipStream_t stream) {
-  constexpr size_t smem = PG_RING_B + (BIAS ? PG_MAX_BIAS * 2 : 0);
+  constexpr size_t smem = PG_RING_B + (BIAS == 1 ? PG_MAX_BIAS * 2 : 0);
   static_assert(smem <= 160 * 1024, "LDS");
   static bool attr = false;
   if (!attr) {
@@ -712,9 +732,12 @@ static int pg_launch(bf16_t* C, const bf16_t* A, const bf16_t* W, const bf16_t* 
   return (int)hipGetLastError();
 }
 
+// res 1: C is read as well -- C = bf16(C + bf16(A . W^T)) (the residual
+// stream of a pre-norm block, updated in place; act 0, no bias)
 int pgemm(void* C, const void* A, const void* W, const void* bias, int M, int N, int K, long lda,
-          long ldw, long ldc, int act, int grid, hipStream_t stream) {
+          long ldw, long ldc, int act, int grid, int res, hipStream_t stream) {
   if (M <= 0) return 0;
+  if (res && (act != 0 || bias != nullptr)) return -1;
   if (N % 256 != 0 || K % 64 != 0 || K < 192) return -1;
   if (lda % 8 || ldw % 8 || ldc % 4) return -1;
   if (act < 0 || act > 4 || (act == 3 && bias != nullptr)) return -1;
@@ -746,6 +769,7 @@ int pgemm(void* C, const void* A, const void* W, const void* bias, int M, int N,
     }
     return -1;
   }
+  if (res) return pg_launch<0, 2>(C_, A_, W_, b_, M, N, K, ia, iw, ic, grid, stream);
   switch (act) {
     case 0: return pg_launch<0, 0>(C_, A_, W_, b_, M, N, K, ia, iw, ic, grid, stream);
     case 1: return pg_launch<1, 0>(C_, A_, W_, b_, M, N, K, ia, iw, ic, grid, stream);

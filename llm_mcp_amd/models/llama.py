@@ -283,10 +283,16 @@ class LlamaModel:
         residual = None
         attn = torch.empty((T, Hq * D), dtype=self.dtype, device=self.device)
         all_rows = inp.sample_rows.numel() == T     # decode: rows 0..T-1, each sampled
+        # TP = 1 prefill: O / down on K13 add into the residual stream in their
+        # epilogue (ops.residual_gemm_ok); x is then None and the next norm
+        # reads the residual alone (two passes over the hidden rows fewer)
+        fold = tp.size == 1 and not sp
         for li, L in enumerate(w["layers"]):
             if residual is None:
                 residual = x
                 h = ops.rms_norm(x, L["ln1"], cfg.rms_eps)
+            elif x is None:
+                h = ops.rms_norm(residual, L["ln1"], cfg.rms_eps)
             else:
                 h = ops.rms_norm(x, L["ln1"], cfg.rms_eps, residual=residual)
             if sp:
@@ -328,10 +334,14 @@ class LlamaModel:
                                             else None)
             # TP = 1: the O projection may hand its split-K partials straight
             # to the residual-add RMSNorm (ops.Partials; K11 epi 2)
-            o = ops.linear(attn, L["wo"], defer=tp.size == 1)
-            if tp.size > 1:
-                o = tp.reduce_scatter_rows(o, Tp) if sp else tp.all_reduce(o)
-            h = ops.rms_norm(o, L["ln2"], cfg.rms_eps, residual=residual)
+            if fold and ops.residual_gemm_ok(attn, L["wo"], residual):
+                ops.pgemm(attn, L["wo"], residual=residual)
+                h = ops.rms_norm(residual, L["ln2"], cfg.rms_eps)
+            else:
+                o = ops.linear(attn, L["wo"], defer=tp.size == 1)
+                if tp.size > 1:
+                    o = tp.reduce_scatter_rows(o, Tp) if sp else tp.all_reduce(o)
+                h = ops.rms_norm(o, L["ln2"], cfg.rms_eps, residual=residual)
             if sp:
                 h = tp.all_gather_rows(h)[:T]
             if self.gu_block:
@@ -342,13 +352,20 @@ class LlamaModel:
             # last layer: the final norm runs on the sampled rows only)
             # the last layer's partials go to the final norm when every row is
             # sampled (pure decode): no gather of the sampled rows is needed
+            if fold and ops.residual_gemm_ok(a, L["w_down"], residual):
+                ops.pgemm(a, L["w_down"], residual=residual)
+                x = None
+                continue
             x = ops.linear(a, L["w_down"], defer=tp.size == 1 and
                            (li + 1 < len(w["layers"]) or all_rows))
             if tp.size > 1:
                 x = tp.reduce_scatter_rows(x, Tp) if sp else tp.all_reduce(x)
         # final norm only on the rows we sample from
         rows = inp.sample_rows
-        if sp:
+        if x is None:
+            hs = ops.rms_norm(residual if all_rows else residual.index_select(0, rows),
+                              w["norm"], cfg.rms_eps)
+        elif sp:
             hs = tp.all_gather_rows(ops.rms_norm(x, w["norm"], cfg.rms_eps,
                                                  residual=residual))[:T].index_select(0, rows)
         elif all_rows:

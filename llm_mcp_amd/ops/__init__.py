@@ -14,6 +14,7 @@ grid assumptions.
 from __future__ import annotations
 
 import importlib
+import os
 
 import torch
 
@@ -1185,6 +1186,7 @@ def rsgemm(a: torch.Tensor, w: torch.Tensor, cfg: int, splits: int, epi: int = 0
 # ---------------------------------------------------------------------------
 PGEMM_MAX_BIAS = 8192
 PGEMM_CALLS = [0]          # host-side launch count (tests: the K13 path really ran)
+RESIDUAL_EPILOGUE = os.environ.get("LMX_RESIDUAL_EPILOGUE", "1") != "0"
 
 
 def pgemm_supported(N: int, K: int, act: int = 0, bias: bool = False) -> bool:
@@ -1208,16 +1210,27 @@ def pgemm_bias_ok(bias: torch.Tensor | None, N: int) -> bool:
 
 
 def pgemm(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, act: int = 0,
-          out: torch.Tensor | None = None, grid: int = 0) -> torch.Tensor:
+          out: torch.Tensor | None = None, grid: int = 0,
+          residual: torch.Tensor | None = None) -> torch.Tensor:
     """act(a @ w^T + bias) on the persistent 256x256 MFMA GEMM (any M).
     act: ACT_NONE / ACT_GELU (tanh) / ACT_SILU / ACT_GELU_ERF, or ACT_SWIGLU
     with ``w`` from ``interleave_gate_up(w, 16)`` (result [M, N/2]).
-    ``grid``: workgroups (0 = one per CU).  The losing design points of
+    ``grid``: workgroups (0 = one per CU).  ``residual`` (bf16 [M, N], no
+    bias / act): the product is added into it in the epilogue, in place, with
+    the rounding of the separate pass it replaces -- residual = bf16(residual
+    + bf16(a @ w^T)) -- and it is returned.  The losing design points of
     the kernel (tools/lab_kernels/pgemm_lab.hip) are lab-only."""
     M, K = a.shape
     N = w.shape[0]
     ncols = N // 2 if act == ACT_SWIGLU else N
+    if residual is not None:
+        _chk(act == ACT_NONE and bias is None and out is None, "pgemm residual: plain product only")
+        _chk(residual.shape == (M, N) and residual.dtype == a.dtype, "pgemm residual shape")
     if not a.is_cuda:
+        if residual is not None:
+            y = ref.gemm_nt(a, w, None, ACT_NONE, None)
+            residual.copy_((residual.float() + y.float()).to(residual.dtype))
+            return residual
         if act == ACT_SWIGLU:
             y = (a.float() @ w.float().t()).view(M, N // 32, 2, 16)
             y = (torch.nn.functional.silu(y[:, :, 0]) * y[:, :, 1]).reshape(M, ncols).to(a.dtype)
@@ -1237,14 +1250,42 @@ def pgemm(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, ac
         _bf16(bias, "bias")
         _chk(bias.numel() == N and bias.is_contiguous() and bias.data_ptr() % 16 == 0,
              "pgemm bias")
+    if residual is not None:
+        _chk(residual_gemm_layout_ok(residual), "pgemm residual layout (16-B rows)")
+        out = residual
     if out is None:
         out = torch.empty((M, ncols), dtype=a.dtype, device=a.device)
     _chk(out.shape == (M, ncols) and out.stride(1) == 1 and out.stride(0) % 4 == 0
          and out.data_ptr() % 8 == 0, "pgemm output layout")
     PGEMM_CALLS[0] += 1
     native().pgemm(_ptr(out), _ptr(a), _ptr(w), _ptr(bias), M, N, K, a.stride(0), w.stride(0),
-                   out.stride(0), act, grid, _stream())
+                   out.stride(0), act, grid, int(residual is not None), _stream())
     return out
+
+
+def residual_gemm_layout_ok(residual: torch.Tensor) -> bool:
+    """A residual stream K13's epilogue reads and writes in 16-B runs."""
+    return (residual.dtype == torch.bfloat16 and residual.stride(1) == 1
+            and residual.stride(0) % 8 == 0 and residual.data_ptr() % 16 == 0)
+
+
+def residual_gemm_ok(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor | None) -> bool:
+    """``residual += x @ w^T`` can run as K13 with the residual epilogue:
+    the prefill-sized shapes ``linear`` sends to K13 (no decode-table kernel
+    claims them), operands and the residual stream in K13's layouts.
+    LMX_RESIDUAL_EPILOGUE=0 keeps the separate residual-add pass."""
+    if residual is None or not x.is_cuda or x.dim() != 2 or not RESIDUAL_EPILOGUE:
+        return False
+    M, N, K = x.shape[0], w.shape[0], w.shape[1]
+    if residual.shape != (M, N) or not residual_gemm_layout_ok(residual):
+        return False
+    if (rs_choice(M, N, K, epi=2, w=w) is not None or rs_choice(M, N, K, w=w) is not None
+            or sk_choice(M, N, K, epi=2) is not None or sk_choice(M, N, K) is not None
+            or dgemm_choice(M, N, K, epi=2) is not None or dgemm_choice(M, N, K) is not None
+            or splitk_preferred(M, N, K)):
+        return False
+    return (large_gemm_backend(M, N, K, 0, False) == "k13" and pgemm_supported(N, K)
+            and pgemm_operands_ok(x, w))
 
 
 _PG_WS: dict = {}

@@ -98,3 +98,23 @@ def test_rsgemm_shape_rules_and_cpu_reference(monkeypatch, tmp_path):
     yy = y.view(5, 16, 2, 16)
     torch.testing.assert_close(g.float(), (torch.nn.functional.silu(yy[:, :, 0]) * yy[:, :, 1])
                                .reshape(5, 256), atol=2e-2, rtol=2e-2)
+
+
+def test_pgemm_residual_cpu_reference_and_gate(monkeypatch):
+    """ops.pgemm(residual=) on CPU (the reference of K13's residual epilogue:
+    residual = bf16(residual + a @ w^T), in place, returned) and the gate that
+    sends only prefill-sized, K13-claimed shapes there (CPU tensors, decode
+    shapes and LMX_RESIDUAL_EPILOGUE=0 keep the separate residual-add pass)."""
+    import torch
+    torch.manual_seed(0)
+    a = torch.randn(37, 512).to(torch.bfloat16)
+    w = (torch.randn(256, 512) * 512 ** -0.5).to(torch.bfloat16)
+    r = torch.randn(37, 256).to(torch.bfloat16)
+    want = (r.float() + a.float() @ w.float().t()).to(torch.bfloat16)
+    out = ops.pgemm(a, w, residual=r)
+    assert out is r
+    torch.testing.assert_close(r.float(), want.float(), atol=1e-2, rtol=1e-2)
+    assert not ops.residual_gemm_ok(a, w, r)              # CPU tensors
+    assert not ops.residual_gemm_ok(a, w, None)
+    monkeypatch.setattr(ops, "RESIDUAL_EPILOGUE", False)
+    assert not ops.residual_gemm_ok(a, w, r)

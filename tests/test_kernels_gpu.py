@@ -665,6 +665,34 @@ def test_pgemm_vs_fp32(M, N, K, grid):
     assert ops.PGEMM_CALLS[0] - before == 6
 
 
+@pytest.mark.parametrize("M,N,K", [(256, 512, 192), (300, 768, 768), (1000, 2304, 768),
+                                   (4096, 1024, 4096), (77, 256, 4096)])
+@pytest.mark.parametrize("grid", [0, 3])
+def test_pgemm_residual_epilogue_vs_fp32(M, N, K, grid):
+    """K13 residual epilogue (pre-norm block): residual = bf16(residual +
+    bf16(a @ w^T)) in place -- the rounding of the separate residual-add pass
+    it replaces -- against the fp32 product; ragged M (rows >= M untouched),
+    a residual that is a strided view into a wider buffer (columns outside it
+    untouched), several tiles per workgroup (grid 3), repeatable."""
+    a = _bf(M, K)
+    w = _bf(N, K, scale=K ** -0.5)
+    big = _bf(M + 5, N + 64)
+    keep = big.clone()
+    res = big[:M, 32:32 + N]
+    want = (res.float() + (a.float() @ w.float().t()).to(torch.bfloat16).float()).to(torch.bfloat16)
+    before = ops.PGEMM_CALLS[0]
+    out = ops.pgemm(a, w, grid=grid, residual=res)
+    assert out.data_ptr() == res.data_ptr()
+    torch.testing.assert_close(res.float(), want.float(), atol=3e-2, rtol=2e-2)
+    assert torch.equal(big[:, :32], keep[:, :32]) and torch.equal(big[:, 32 + N:], keep[:, 32 + N:])
+    assert torch.equal(big[M:], keep[M:])
+    # same inputs again: bitwise the same result
+    res2 = keep[:M, 32:32 + N].clone()
+    ops.pgemm(a, w, grid=grid, residual=res2)
+    assert torch.equal(res2, res)
+    assert ops.PGEMM_CALLS[0] - before == 2
+
+
 @pytest.mark.parametrize("M,N,K", [(256, 1024, 4096), (200, 768, 1536), (37, 512, 512),
                                    (300, 512, 1024)])
 @pytest.mark.parametrize("splits", [1, 2, 3, 4])
