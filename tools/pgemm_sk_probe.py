@@ -22,7 +22,9 @@ SHAPES = {"l8b.qkv": (6144, 4096, 0, 0), "l8b.o": (4096, 4096, 0, 2),
           "l8b.gate_up": (28672, 4096, ops.ACT_SWIGLU, 0), "l8b.down": (4096, 14336, 0, 2),
           "l8b.lm_head": (128256, 4096, 0, 0),
           "l70b.qkv": (10240, 8192, 0, 0), "l70b.gate_up": (57344, 8192, ops.ACT_SWIGLU, 0),
-          "l70b.down": (8192, 28672, 0, 2), "l70b.o": (8192, 8192, 0, 2)}
+          "l70b.down": (8192, 28672, 0, 2), "l70b.o": (8192, 8192, 0, 2),
+          # Llama-3-70B TP = 8 per-rank shapes (LM head shard padded to 256-row tiles)
+          "l70b.tp8_lm_head": (16128, 8192, 0, 0), "l70b.tp8_qkv": (1280, 8192, 0, 0)}
 
 
 def bench(fn, iters, rounds_out, ws):
