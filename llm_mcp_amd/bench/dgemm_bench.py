@@ -27,6 +27,7 @@ import sys
 import torch
 
 from .. import ops
+from ..models.weights import vocab_shard
 
 BUCKETS = [16, 32, 48, 64, 80, 96, 112, 128, 160, 192, 224, 256]
 NT_TOP = 4      # configurations re-timed with the non-temporal weight stream (cfg | DGEMM_NT)
@@ -40,7 +41,7 @@ def shapes(model: str, tp: int = 1) -> dict:
     inter = c.intermediate_size // tp
     return {"qkv": (qkv, d, 0), "o": (d, c.num_heads // tp * hd, 0),
             "gate_up": (2 * inter, d, 1), "down": (d, inter, 0),
-            "lm_head": (-(-c.vocab_size // tp), d, 0)}
+            "lm_head": (vocab_shard(c.vocab_size, tp), d, 0)}
 
 
 # projections whose output feeds the fused residual-add RMSNorm (TP = 1):

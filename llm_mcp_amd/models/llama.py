@@ -34,6 +34,7 @@ import torch.nn.functional as F
 from .. import ops
 from ..ops import ref
 from .config import LlamaConfig
+from .weights import vocab_shard
 
 
 @dataclass
@@ -188,7 +189,7 @@ class LlamaModel:
         self.kv_replicas = max(1, T // cfg.num_kv_heads)
         self.D = cfg.head_dim
         self.I = cfg.intermediate_size // T
-        self.vocab_shard = (cfg.vocab_size + T - 1) // T
+        self.vocab_shard = vocab_shard(cfg.vocab_size, T)
         self.scale = 1.0 / math.sqrt(self.D)
         self.cos_sin = ref.rope_cos_sin(cfg.max_position, self.D, cfg.rope_theta, self.device,
                                         cfg.rope_scaling)
@@ -246,8 +247,13 @@ class LlamaModel:
                 "w_down": rnd(d, self.I, std=0.02 / math.sqrt(2 * cfg.num_layers)),
             })
         embed = rnd(cfg.vocab_size, d, std=1.0)
-        lm_head = embed[self.tp.rank * self.vocab_shard:(self.tp.rank + 1) * self.vocab_shard] \
-            if cfg.tie_embeddings else rnd(min(self.vocab_shard, cfg.vocab_size), d)
+        vs = self.vocab_shard
+        if cfg.tie_embeddings:
+            lm_head = embed[self.tp.rank * vs:(self.tp.rank + 1) * vs]
+            if lm_head.shape[0] < vs:        # the last shard: zero rows past the vocabulary
+                lm_head = torch.cat([lm_head, lm_head.new_zeros(vs - lm_head.shape[0], d)])
+        else:
+            lm_head = rnd(vs, d)
         return {"embed": embed, "norm": torch.ones(d, dtype=dt, device=dev), "lm_head": lm_head,
                 "layers": layers}
 

@@ -16,8 +16,10 @@ group) builds its own shard directly:
 Sharding (per rank r of T):  wqkv rows = this rank's q heads + its kv head
 group (kv heads replicated when T > num_kv_heads); wo / w_down split by
 input columns (row-parallel, followed by an all-reduce); w_gate_up split by
-output rows; lm_head split by vocab rows (zero-padded to ceil(V/T) so the
-all-gather is uniform); embeddings and norms replicated.
+output rows; lm_head split by vocab rows, each shard zero-padded to
+``vocab_shard(V, T)`` rows (ceil(V/T) rounded up to whole 256-row GEMM tiles,
+so the all-gather is uniform and the per-rank LM head runs on the hand-written
+decode kernels); embeddings and norms replicated.
 """
 from __future__ import annotations
 
@@ -30,6 +32,15 @@ import torch
 from .config import LlamaConfig
 
 
+def vocab_shard(vocab: int, size: int) -> int:
+    """Rows of one rank's LM-head shard: ceil(V/T) rounded up to a multiple of
+    256 under TP (whole K13 / K14 column tiles: Llama-3's 128256 / 8 = 16032
+    -> 16128); the whole vocabulary at T = 1."""
+    if size <= 1:
+        return vocab
+    return -(-(-(-vocab // size)) // 256) * 256
+
+
 def _geometry(cfg: LlamaConfig, size: int):
     if cfg.num_heads % size or cfg.intermediate_size % size:
         raise ValueError("TP size must divide heads and intermediate size")
@@ -39,7 +50,7 @@ def _geometry(cfg: LlamaConfig, size: int):
     hkv = max(1, cfg.num_kv_heads // size)
     rep = max(1, size // cfg.num_kv_heads)
     inter = cfg.intermediate_size // size
-    vs = (cfg.vocab_size + size - 1) // size
+    vs = vocab_shard(cfg.vocab_size, size)
     return hq, hkv, rep, inter, vs
 
 
