@@ -214,6 +214,7 @@ class LlamaModel:
                 for k in ("wqkv", "wo", "w_gate_up", "w_down"):
                     if k in L:
                         ops.rs_prepare(L[k])
+            ops.rs_prepare(self.w["lm_head"])
 
     # ----------------------------------------------------------- weights ----
     def _random_weights(self, seed: int) -> dict:
