@@ -67,7 +67,7 @@ def parse(argv=None):
     ap.add_argument("--max-tokens", type=int, default=256)
     ap.add_argument("--temperature", type=float, default=0.8)
     ap.add_argument("--top-p", type=float, default=0.95)
-    ap.add_argument("--max-batched-tokens", type=int, default=16384)
+    ap.add_argument("--max-batched-tokens", type=int, default=24576)
     ap.add_argument("--api-procs", type=int, default=0,
                     help="front-door API processes on the shared port (0: two per engine, "
                          "at most 16)")
