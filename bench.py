@@ -253,6 +253,7 @@ def main() -> None:
     def waves(n: int, label: str) -> list[dict]:
         out = []
         for k in range(n):
+            t_w = time.time()
             for p in lgs:
                 p.stdin.write("run\n")
                 p.stdin.flush()
@@ -272,6 +273,12 @@ def main() -> None:
             log(f"{label} {k}: {r['requests']} streams, {r['tokens']} tok in {r['elapsed']:.2f}s "
                 f"({r['tokens'] / r['elapsed']:.0f} tok/s), ttft p50 "
                 f"{pct(r['ttfts'], 50) * 1e3:.0f} ms, itl p50 {pct(r['itls'], 50) * 1e3:.1f} ms")
+            if engine.step_trace is not None:
+                # LMX_STEP_TRACE=1: this wave's eager steps (launch ms after the
+                # wave started: rows / decode rows / prefill tokens / waiting)
+                tr = [x for x in engine.step_trace if x[0] >= t_w]
+                log(f"{label} {k} eager steps: " + " ".join(
+                    f"{(x[0] - t_w) * 1e3:.0f}ms:T{x[1]}/d{x[2]}/p{x[3]}/w{x[4]}" for x in tr))
         return out
 
     import psutil

@@ -304,6 +304,8 @@ class LLMEngine:
         # (LMX_LOOKAHEAD=1, the sample_all mode below) until an RCCL run with
         # captured graphs has covered the followers' sampling path; by default
         # a TP group steps synchronously and the leader ships the tokens.
+        if os.environ.get("LMX_STEP_TRACE", "0") == "1":
+            self.step_trace = []
         la_env = os.environ.get("LMX_LOOKAHEAD", "")
         self.lookahead = la_env == "1" or (la_env != "0" and self.device.type == "cuda"
                                            and self.tp.size == 1)
@@ -461,6 +463,8 @@ class LLMEngine:
         return {"graph": graph, "parts": ws.max_parts}
 
     # --------------------------------------------------------- public API ---
+    step_trace: list | None = None     # set to [] by LMX_STEP_TRACE=1 (see _step_la)
+
     def submit(self, req: GenRequest) -> GenRequest:
         if not req.id:
             req.id = next(self._ids)
@@ -807,6 +811,11 @@ class LLMEngine:
             st["g_schedule"] += t1 - t0
             st["g_launch"] += t2 - t1
         st["prefill_tokens"] += plan["num_prefill_tokens"]
+        if self.step_trace is not None and bucket is None:
+            # eager (prefill / mixed) steps: launch time, rows, decode rows,
+            # prefill tokens, sequences still waiting (LMX_STEP_TRACE=1)
+            self.step_trace.append((time.time(), T, nd, int(plan["num_prefill_tokens"]),
+                                    int(self.sched.num_waiting)))
         return True
 
     def _la_resolve(self) -> np.ndarray:
