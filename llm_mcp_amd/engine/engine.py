@@ -306,6 +306,10 @@ class LLMEngine:
         # a TP group steps synchronously and the leader ships the tokens.
         if os.environ.get("LMX_STEP_TRACE", "0") == "1":
             self.step_trace = []
+        self._idle = True
+        self._admit_quiet_s = float(os.environ.get("LMX_ADMIT_QUIET_MS", "2")) / 1e3
+        self._admit_max_s = float(os.environ.get("LMX_ADMIT_MAX_MS", "25")) / 1e3
+        self._admit_tokens = 512          # tokens counted per waiting request (budget check)
         la_env = os.environ.get("LMX_LOOKAHEAD", "")
         self.lookahead = la_env == "1" or (la_env != "0" and self.device.type == "cuda"
                                            and self.tp.size == 1)
@@ -645,12 +649,39 @@ class LLMEngine:
         self._drain()
         if not self.sched.has_work and self._la is None:
             self._flush_pending()
+            self._idle = True
             return False
+        if self._idle:
+            self._idle = False
+            self._admission_window()
         self._step_started = time.monotonic()
         try:
             return self._step_la() if self.lookahead else self._step()
         finally:
             self._step_started = 0.0
+
+    def _admission_window(self) -> None:
+        """Idle -> busy: a burst of requests (a client wave, a batch job)
+        reaches the engine over tens of ms through the front door; the first
+        step would otherwise prefill whichever request came first alone and
+        the rest one step later.  Wait while requests keep arriving -- until
+        LMX_ADMIT_QUIET_MS (2) pass without one, LMX_ADMIT_MAX_MS (25) pass in
+        all, or a step's token budget is queued -- then schedule.  A lone
+        request pays the quiet interval once; a busy engine never waits."""
+        quiet = self._admit_quiet_s
+        if quiet <= 0 or self.sched.num_running:
+            return
+        t0 = time.monotonic()
+        n = self.sched.num_waiting
+        while (n < self.ecfg.max_num_seqs and n * self._admit_tokens < self.ecfg.max_batched_tokens
+               and time.monotonic() - t0 < self._admit_max_s):
+            self._wake.wait(timeout=quiet)
+            self._wake.clear()
+            self._drain()
+            m = self.sched.num_waiting
+            if m == n:
+                break
+            n = m
 
     def _step(self) -> bool:
         fl = faults()

@@ -99,6 +99,8 @@ VARS: list[Var] = [
     Var("LMX_DGEMM", str, "1", "0 disables the decode GEMM (K11) dispatch table (hipBLASLt everywhere)"),
     Var("LMX_PREFILL_WAVES", int, 4, "waves per prefill-attention workgroup at head dim 128 (4 or 8)"),
     Var("LMX_SK", str, "1", "0 disables the K13-SK (split-K 256x256 tile) entries of the decode GEMM table"),
+    Var("LMX_ADMIT_QUIET_MS", float, 2.0, "idle engine: wait for more arrivals until this long passes without one (0: schedule at once)"),
+    Var("LMX_ADMIT_MAX_MS", float, 25.0, "idle engine: longest wait for a burst of arrivals before the first step"),
     Var("LMX_STEP_TRACE", int, 0, "record the engine's eager (prefill / mixed) steps; bench.py logs each wave's steps"),
     Var("LMX_RESIDUAL_EPILOGUE", int, 1, "prefill O / down projections on K13 add into the residual stream in their epilogue (0: separate residual-add pass in the norm)"),
     Var("LMX_RS_PACK_GB", float, 24.0, "budget for K14's packed copies of decode weights (beside the row-major weights prefill reads)"),
