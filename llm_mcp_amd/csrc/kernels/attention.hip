@@ -213,81 +213,6 @@ __device__ __forceinline__ void compute_page(PageState<HD>& st, const bf16x8_t (
   }
 }
 
-// Half-page software pipeline (decode MODE 7): the next page's K fragments are
-// loaded into the registers the current page's QK MFMAs have just read, and its
-// V fragments into the ones the PV MFMAs have just read, so every wave keeps
-// about one page of K/V in flight through the softmax and the PV product
-// instead of none (MODE 0 issues a page's loads only after the previous page
-// is done).  No extra registers: the fragment set is the same PageFrags.
-template <int HD>
-__device__ __forceinline__ void load_page_k(PageFrags<HD>& f, const bf16_t* __restrict__ kpage) {
-  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
-#pragma unroll
-  for (int s = 0; s < HD / 32; ++s) {
-    f.ka[s] = load_frag16B(kpage + c * HD + 32 * s + 8 * g);
-    f.kb[s] = load_frag16B(kpage + (16 + c) * HD + 32 * s + 8 * g);
-  }
-}
-
-template <int HD>
-__device__ __forceinline__ void load_page_v(PageFrags<HD>& f, const bf16_t* __restrict__ vpage) {
-  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
-#pragma unroll
-  for (int i = 0; i < HD / 16; ++i)
-    f.vf[i] = load_frag_2x8B(vpage + vq_off(16 * i + c, 4 * g, HD),
-                             vpage + vq_off(16 * i + c, 16 + 4 * g, HD));
-}
-
-// compute_page with the next page's K issued right after the QK MFMAs and its
-// V right after the PV MFMAs
-template <int HD>
-__device__ __forceinline__ void compute_page_pipe(PageState<HD>& st, const bf16x8_t (&qf)[HD / 32],
-                                                  PageFrags<HD>& f, int page_pos0, int lim,
-                                                  float scale_log2, const bf16_t* nk,
-                                                  const bf16_t* nv) {
-  const int lane = threadIdx.x & 63, g = lane >> 4;
-  f32x4_t s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int s = 0; s < HD / 32; ++s) {
-    s0 = mfma16(f.ka[s], qf[s], s0);
-    s1 = mfma16(f.kb[s], qf[s], s1);
-  }
-  __builtin_amdgcn_sched_barrier(0);
-  load_page_k<HD>(f, nk);
-  __builtin_amdgcn_sched_barrier(0);
-  float x[8];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int k0 = page_pos0 + 4 * g + r, k1 = k0 + 16;
-    x[r] = (k0 <= lim) ? s0[r] * scale_log2 : -INFINITY;
-    x[4 + r] = (k1 <= lim) ? s1[r] * scale_log2 : -INFINITY;
-  }
-  float mx = x[0];
-#pragma unroll
-  for (int j = 1; j < 8; ++j) mx = fmaxf(mx, x[j]);
-  mx = col4_max(mx);
-  const float m_new = fmaxf(st.m, mx);
-  const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
-  const float alpha = fast_exp2(st.m - m_use);
-  float p[8], rs = 0.f;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) { p[j] = fast_exp2(x[j] - m_use); rs += p[j]; }
-  rs = col4_sum(rs);
-  st.l = st.l * alpha + rs;
-  st.m = m_new;
-  bf16x8_t pf;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) pf[j] = (short)f2bf(p[j]);
-#pragma unroll
-  for (int i = 0; i < HD / 16; ++i) {
-    st.acc[i] *= alpha;
-    st.acc[i] = mfma16(f.vf[i], pf, st.acc[i]);
-  }
-  __builtin_amdgcn_sched_barrier(0);
-  load_page_v<HD>(f, nv);
-  __builtin_amdgcn_sched_barrier(0);
-}
-
 // ---------------------------------------------------------------- decode ----
 // Optional fused K2 + K5 for decode rows (cos_sin == nullptr: off).  The row's
 // q / k / v are the unrotated QKV projection output (q at the row start, k at
@@ -408,11 +333,10 @@ __device__ __forceinline__ void decode_segment(
   const int G = Hq / Hkv;
   const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
   // wave-uniform in the compiler's view too: page indices, block ids and the
-  // page-loop control stay scalar (s_load / s_cbranch, no exec masking), so
-  // the vector-memory counts of the K/V loads are exact
+  // page-loop control stay scalar (s_load / s_cbranch, no exec masking)
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int t0 = p * part_tokens, t1 = min(t0 + part_tokens, ctx);
-  constexpr bool kOnePage = MODE == 0 || MODE == 5 || MODE == 6 || MODE == 7;
+  constexpr bool kOnePage = MODE == 0 || MODE == 5 || MODE == 6;
 
   bf16x8_t qf[HD / 32];
   const bf16_t* qrow = q + (long)b * q_stride + (long)(kvh * G + c) * HD;
@@ -453,28 +377,6 @@ __device__ __forceinline__ void decode_segment(
       return bt[pg];
     };
     int pg = pg0 + wave;
-    if constexpr (MODE == 7) {
-      // the writer retires its k / v stores before loading the page that
-      // holds them (its first page here, or a later one: then the first
-      // page's completed loads already retired them, in order)
-      if (writer && pg == pg1 - 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      PageFrags<HD> f;
-      if (pg < pg1) {
-        const long blk = blk_of(pg);
-        load_page_k<HD>(f, k_cache + (blk * Hkv + kvh) * (BS * HD));
-        load_page_v<HD>(f, v_cache + (blk * Hkv + kvh) * (BS * HD));
-      }
-      if (cs) rope_q_frags<HD>(qf, cs, g);
-      for (; pg < pg1; pg += 4) {
-        // the loads are unconditional (straight-line code keeps the compiler's
-        // vmcnt counts exact across the loop): past the wave's last page it
-        // re-reads the current one, an L2 hit nobody consumes
-        const long nb = blk_of(pg + 4 < pg1 ? pg + 4 : pg);
-        compute_page_pipe<HD>(st, qf, f, pg * BS, t1 - 1, scale_log2,
-                              k_cache + (nb * Hkv + kvh) * (BS * HD),
-                              v_cache + (nb * Hkv + kvh) * (BS * HD));
-      }
-    } else {
     if (cs) {
       if (pg < pg1 && !(writer && pg == pg1 - 1)) {
         // first page: its K/V fragments are in flight while q rotates (the
@@ -496,7 +398,6 @@ __device__ __forceinline__ void decode_segment(
       const bf16_t* kp = k_cache + (blk * Hkv + kvh) * (BS * HD);
       const bf16_t* vp = v_cache + (blk * Hkv + kvh) * (BS * HD);
       process_page<HD, MODE == 5>(st, qf, kp, vp, pg * BS, t1 - 1, scale_log2);
-    }
     }
   } else {
     int pg = pg0 + wave;
@@ -687,8 +588,6 @@ int paged_decode(const void* q, long q_stride, const void* k_cache, const void* 
   if (g_decode_mode == 0 && max_parts == 1) { LMX_DEC_P(HDV, 0) }                             \
   else if (g_decode_mode == 5 && max_parts == 1) { LMX_DEC_P(HDV, 5) }                        \
   else if (g_decode_mode == 6 && max_parts == 1) { LMX_DEC_P(HDV, 6) }                        \
-  else if (g_decode_mode == 7 && max_parts == 1) { LMX_DEC_P(HDV, 7) }                        \
-  else if (g_decode_mode == 7) { LMX_DEC_K(HDV, 7) }                                          \
   else if (g_decode_mode == 6) { LMX_DEC_K(HDV, 6) }                                          \
   else if (g_decode_mode == 5) { LMX_DEC_K(HDV, 5) }                                          \
   else if (g_decode_mode == 1) { LMX_DEC_K(HDV, 1) }                                          \
