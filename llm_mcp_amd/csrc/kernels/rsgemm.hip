@@ -41,6 +41,9 @@ namespace lmx {
 namespace {
 
 constexpr int RS_THREADS = 512, RS_BN = 256, RS_BK = 64;
+#ifndef RS_APF
+#define RS_APF 1          // A-fragment pairs read ahead of the MFMAs (lab: -DRS_APF=n)
+#endif
 
 typedef __attribute__((address_space(3))) void rs_lds_t;
 
@@ -229,35 +232,41 @@ __global__ void __launch_bounds__(RS_THREADS, 2) __attribute__((amdgpu_waves_per
     }
   }
 
-  // one K32 sub-step: the NG row-group fragments read in pairs, the next
-  // pair in flight while the current pair's 4 MFMAs run
+  // one K32 sub-step: the NG row-group fragments read in pairs, RS_APF pairs
+  // ahead of the pair whose 4 MFMAs run (a ds_read_b128 pair takes longer to
+  // land than one pair's 4 MFMAs: one pair ahead left the waves waiting on LDS)
   auto compute = [&](const bf16_t* slot, int kk, const bf16x8_t& w0, const bf16x8_t& w1) {
-    bf16x8_t cur0 = rs_afrag(slot, fr, kk * 4 + fg);
-    bf16x8_t cur1 = rs_afrag(slot, 16 + fr, kk * 4 + fg);
+    // (the all-rows tile keeps one pair: its D 6 ring has no registers left)
+    constexpr int NP = NG / 2, PFW = BM == 256 ? 1 : RS_APF;
+    constexpr int PF = PFW < NP ? PFW : NP - 1, RING = PF + 1;
+    bf16x8_t f0[RING], f1[RING];
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+      f0[q] = rs_afrag(slot, 32 * q + fr, kk * 4 + fg);
+      f1[q] = rs_afrag(slot, 32 * q + 16 + fr, kk * 4 + fg);
+    }
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int p = 0; p < NG / 2; ++p) {
-      bf16x8_t nx0 = cur0, nx1 = cur1;
-      if (p < NG / 2 - 1) {
-        nx0 = rs_afrag(slot, 32 * (p + 1) + fr, kk * 4 + fg);
-        nx1 = rs_afrag(slot, 32 * (p + 1) + 16 + fr, kk * 4 + fg);
+    for (int p = 0; p < NP; ++p) {
+      if (p + PF < NP) {
+        f0[(p + PF) % RING] = rs_afrag(slot, 32 * (p + PF) + fr, kk * 4 + fg);
+        f1[(p + PF) % RING] = rs_afrag(slot, 32 * (p + PF) + 16 + fr, kk * 4 + fg);
       }
-      acc[0][2 * p] = mfma16(w0, cur0, acc[0][2 * p]);
-      acc[1][2 * p] = mfma16(w1, cur0, acc[1][2 * p]);
-      acc[0][2 * p + 1] = mfma16(w0, cur1, acc[0][2 * p + 1]);
-      acc[1][2 * p + 1] = mfma16(w1, cur1, acc[1][2 * p + 1]);
-      cur0 = nx0;
-      cur1 = nx1;
+      const bf16x8_t& c0 = f0[p % RING];
+      const bf16x8_t& c1 = f1[p % RING];
+      acc[0][2 * p] = mfma16(w0, c0, acc[0][2 * p]);
+      acc[1][2 * p] = mfma16(w1, c0, acc[1][2 * p]);
+      acc[0][2 * p + 1] = mfma16(w0, c1, acc[0][2 * p + 1]);
+      acc[1][2 * p + 1] = mfma16(w1, c1, acc[1][2 * p + 1]);
     }
     // hold that order against the scheduler's register-pressure heuristic
     // (it otherwise reuses one fragment pair and waits lgkmcnt(0) per pair)
-    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, 2 * PF, 0);
 #pragma unroll
-    for (int p = 0; p < NG / 2 - 1; ++p) {
-      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+    for (int p = 0; p < NP; ++p) {
+      if (p + PF < NP) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
       __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
     }
-    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
     __builtin_amdgcn_s_setprio(0);
   };
 
