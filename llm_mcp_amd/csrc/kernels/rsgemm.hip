@@ -44,6 +44,9 @@ constexpr int RS_THREADS = 512, RS_BN = 256, RS_BK = 64;
 #ifndef RS_APF
 #define RS_APF 1          // A-fragment pairs read ahead of the MFMAs (lab: -DRS_APF=n)
 #endif
+#ifndef RS_ROT
+#define RS_ROT 0          // K64-step lag of a 128-row pair's second tile (lab: -DRS_ROT=n)
+#endif
 
 typedef __attribute__((address_space(3))) void rs_lds_t;
 
@@ -206,8 +209,14 @@ __global__ void __launch_bounds__(RS_THREADS, 2) __attribute__((amdgpu_waves_per
   const unsigned voff1 = RM ? (unsigned)(((lane & 15) + 16) * ldw * 2 + (lane >> 4) * 16)
                             : lane * 16;
   constexpr int I0 = 0, I1 = RM ? 0 : 1024, I2 = RM ? 64 : 2048, I3 = RM ? 64 : 3072;
-  auto wsb = [&](int k) -> const void* {   // wave-uniform base of K32 step k
-    return (const void*)(wstream + (long)k * KSTEP);
+  // K-order rotation of the second row tile of a column tile (BM 128 pairs,
+  // RS_ROT > 0): it walks the K64 steps starting RS_ROT behind the first, so
+  // it re-reads the weight lines its partner pulled into the XCD's L2 RS_ROT
+  // steps earlier (L2 hits) instead of merging into the same in-flight misses
+  const int rot = (RS_ROT > 0 && BM == 128 && (tm & 1) && nk64 > RS_ROT) ? nk64 - RS_ROT : 0;
+  auto phys = [&](int t64) { return t64 + rot < nk64 ? t64 + rot : t64 + rot - nk64; };
+  auto wsb = [&](int k) -> const void* {   // wave-uniform base of K32 step k (k even)
+    return (const void*)(wstream + (long)(2 * phys(k >> 1) + (k & 1)) * KSTEP);
   };
 
   f32x4_t acc[2][NG];
@@ -221,7 +230,7 @@ __global__ void __launch_bounds__(RS_THREADS, 2) __attribute__((amdgpu_waves_per
 #pragma unroll
   for (int s = -U; s < 0; ++s) {
     if (s + NA - 1 >= 0) rs_stage_a<BM>(lds + ((s + NA - 1) % NA) * SLOT, A, lda, M, m0,
-                                        k0 + (s + NA - 1) * RS_BK);
+                                        k0 + phys(s + NA - 1) * RS_BK);
     {
       const int k = 2 * (s + U);                     // K32 steps 2s + D, 2s + D + 1
       const void* b = wsb(k);
@@ -281,7 +290,7 @@ __global__ void __launch_bounds__(RS_THREADS, 2) __attribute__((amdgpu_waves_per
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       rs_stage_a<BM>(lds + ((t + NA - 1) % NA) * SLOT, A, lda, M, m0,
-                     k0 + (t + NA - 1) * RS_BK);
+                     k0 + phys(t + NA - 1) * RS_BK);
       const bf16_t* slot = lds + (t % NA) * SLOT;
       const void* b = wsb(2 * t + D);
       compute(slot, 0, wr[2 * u][0], wr[2 * u][1]);
@@ -306,7 +315,7 @@ __global__ void __launch_bounds__(RS_THREADS, 2) __attribute__((amdgpu_waves_per
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (t + NA - 1 < nk64)
-      rs_stage_a<BM>(lds + ((t + NA - 1) % NA) * SLOT, A, lda, M, m0, k0 + (t + NA - 1) * RS_BK);
+      rs_stage_a<BM>(lds + ((t + NA - 1) % NA) * SLOT, A, lda, M, m0, k0 + phys(t + NA - 1) * RS_BK);
     const bf16_t* slot = lds + (t % NA) * SLOT;
     compute(slot, 0, wr[2 * u][0], wr[2 * u][1]);
     rs_wait0(wr[2 * u + 1][0], wr[2 * u + 1][1]);
