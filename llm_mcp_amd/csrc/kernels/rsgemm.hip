@@ -41,12 +41,6 @@ namespace lmx {
 namespace {
 
 constexpr int RS_THREADS = 512, RS_BN = 256, RS_BK = 64;
-#ifndef RS_APF
-#define RS_APF 1          // A-fragment pairs read ahead of the MFMAs (lab: -DRS_APF=n)
-#endif
-#ifndef RS_ROT
-#define RS_ROT 0          // K64-step lag of a 128-row pair's second tile (lab: -DRS_ROT=n)
-#endif
 
 typedef __attribute__((address_space(3))) void rs_lds_t;
 
@@ -209,14 +203,8 @@ __global__ void __launch_bounds__(RS_THREADS, 2) __attribute__((amdgpu_waves_per
   const unsigned voff1 = RM ? (unsigned)(((lane & 15) + 16) * ldw * 2 + (lane >> 4) * 16)
                             : lane * 16;
   constexpr int I0 = 0, I1 = RM ? 0 : 1024, I2 = RM ? 64 : 2048, I3 = RM ? 64 : 3072;
-  // K-order rotation of the second row tile of a column tile (BM 128 pairs,
-  // RS_ROT > 0): it walks the K64 steps starting RS_ROT behind the first, so
-  // it re-reads the weight lines its partner pulled into the XCD's L2 RS_ROT
-  // steps earlier (L2 hits) instead of merging into the same in-flight misses
-  const int rot = (RS_ROT > 0 && BM == 128 && (tm & 1) && nk64 > RS_ROT) ? nk64 - RS_ROT : 0;
-  auto phys = [&](int t64) { return t64 + rot < nk64 ? t64 + rot : t64 + rot - nk64; };
-  auto wsb = [&](int k) -> const void* {   // wave-uniform base of K32 step k (k even)
-    return (const void*)(wstream + (long)(2 * phys(k >> 1) + (k & 1)) * KSTEP);
+  auto wsb = [&](int k) -> const void* {   // wave-uniform base of K32 step k
+    return (const void*)(wstream + (long)k * KSTEP);
   };
 
   f32x4_t acc[2][NG];
@@ -230,7 +218,7 @@ __global__ void __launch_bounds__(RS_THREADS, 2) __attribute__((amdgpu_waves_per
 #pragma unroll
   for (int s = -U; s < 0; ++s) {
     if (s + NA - 1 >= 0) rs_stage_a<BM>(lds + ((s + NA - 1) % NA) * SLOT, A, lda, M, m0,
-                                        k0 + phys(s + NA - 1) * RS_BK);
+                                        k0 + (s + NA - 1) * RS_BK);
     {
       const int k = 2 * (s + U);                     // K32 steps 2s + D, 2s + D + 1
       const void* b = wsb(k);
@@ -241,41 +229,35 @@ __global__ void __launch_bounds__(RS_THREADS, 2) __attribute__((amdgpu_waves_per
     }
   }
 
-  // one K32 sub-step: the NG row-group fragments read in pairs, RS_APF pairs
-  // ahead of the pair whose 4 MFMAs run (a ds_read_b128 pair takes longer to
-  // land than one pair's 4 MFMAs: one pair ahead left the waves waiting on LDS)
+  // one K32 sub-step: the NG row-group fragments read in pairs, the next
+  // pair in flight while the current pair's 4 MFMAs run
   auto compute = [&](const bf16_t* slot, int kk, const bf16x8_t& w0, const bf16x8_t& w1) {
-    // (the all-rows tile keeps one pair: its D 6 ring has no registers left)
-    constexpr int NP = NG / 2, PFW = BM == 256 ? 1 : RS_APF;
-    constexpr int PF = PFW < NP ? PFW : NP - 1, RING = PF + 1;
-    bf16x8_t f0[RING], f1[RING];
-#pragma unroll
-    for (int q = 0; q < PF; ++q) {
-      f0[q] = rs_afrag(slot, 32 * q + fr, kk * 4 + fg);
-      f1[q] = rs_afrag(slot, 32 * q + 16 + fr, kk * 4 + fg);
-    }
+    bf16x8_t cur0 = rs_afrag(slot, fr, kk * 4 + fg);
+    bf16x8_t cur1 = rs_afrag(slot, 16 + fr, kk * 4 + fg);
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int p = 0; p < NP; ++p) {
-      if (p + PF < NP) {
-        f0[(p + PF) % RING] = rs_afrag(slot, 32 * (p + PF) + fr, kk * 4 + fg);
-        f1[(p + PF) % RING] = rs_afrag(slot, 32 * (p + PF) + 16 + fr, kk * 4 + fg);
+    for (int p = 0; p < NG / 2; ++p) {
+      bf16x8_t nx0 = cur0, nx1 = cur1;
+      if (p < NG / 2 - 1) {
+        nx0 = rs_afrag(slot, 32 * (p + 1) + fr, kk * 4 + fg);
+        nx1 = rs_afrag(slot, 32 * (p + 1) + 16 + fr, kk * 4 + fg);
       }
-      const bf16x8_t& c0 = f0[p % RING];
-      const bf16x8_t& c1 = f1[p % RING];
-      acc[0][2 * p] = mfma16(w0, c0, acc[0][2 * p]);
-      acc[1][2 * p] = mfma16(w1, c0, acc[1][2 * p]);
-      acc[0][2 * p + 1] = mfma16(w0, c1, acc[0][2 * p + 1]);
-      acc[1][2 * p + 1] = mfma16(w1, c1, acc[1][2 * p + 1]);
+      acc[0][2 * p] = mfma16(w0, cur0, acc[0][2 * p]);
+      acc[1][2 * p] = mfma16(w1, cur0, acc[1][2 * p]);
+      acc[0][2 * p + 1] = mfma16(w0, cur1, acc[0][2 * p + 1]);
+      acc[1][2 * p + 1] = mfma16(w1, cur1, acc[1][2 * p + 1]);
+      cur0 = nx0;
+      cur1 = nx1;
     }
     // hold that order against the scheduler's register-pressure heuristic
     // (it otherwise reuses one fragment pair and waits lgkmcnt(0) per pair)
-    __builtin_amdgcn_sched_group_barrier(0x100, 2 * PF, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
 #pragma unroll
-    for (int p = 0; p < NP; ++p) {
-      if (p + PF < NP) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+    for (int p = 0; p < NG / 2 - 1; ++p) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
       __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
     }
+    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
     __builtin_amdgcn_s_setprio(0);
   };
 
@@ -290,7 +272,7 @@ __global__ void __launch_bounds__(RS_THREADS, 2) __attribute__((amdgpu_waves_per
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       rs_stage_a<BM>(lds + ((t + NA - 1) % NA) * SLOT, A, lda, M, m0,
-                     k0 + phys(t + NA - 1) * RS_BK);
+                     k0 + (t + NA - 1) * RS_BK);
       const bf16_t* slot = lds + (t % NA) * SLOT;
       const void* b = wsb(2 * t + D);
       compute(slot, 0, wr[2 * u][0], wr[2 * u][1]);
@@ -315,7 +297,7 @@ __global__ void __launch_bounds__(RS_THREADS, 2) __attribute__((amdgpu_waves_per
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (t + NA - 1 < nk64)
-      rs_stage_a<BM>(lds + ((t + NA - 1) % NA) * SLOT, A, lda, M, m0, k0 + phys(t + NA - 1) * RS_BK);
+      rs_stage_a<BM>(lds + ((t + NA - 1) % NA) * SLOT, A, lda, M, m0, k0 + (t + NA - 1) * RS_BK);
     const bf16_t* slot = lds + (t % NA) * SLOT;
     compute(slot, 0, wr[2 * u][0], wr[2 * u][1]);
     rs_wait0(wr[2 * u + 1][0], wr[2 * u + 1][1]);
