@@ -9,6 +9,7 @@ def test_swiglu_block_follows_the_largest_batch_bucket(monkeypatch):
     table = {(57344, 8192, 1): [(64, 16 | ops.DGEMM_NT, 1), (128, 11, 1), (256, -1, 0)]}
     monkeypatch.setattr(ops, "DGEMM_TABLE", table)
     monkeypatch.setattr(ops, "_SK_TABLE", {})
+    monkeypatch.setattr(ops, "_RS_TABLE", {})
     assert ops.swiglu_block(57344, 8192) == 128
     assert ops.dgemm_choice(128, 57344, 8192, epi=1) == (11, 1)
     assert ops.dgemm_choice(200, 57344, 8192, epi=1) is None     # library bucket
