@@ -309,7 +309,6 @@ class LLMEngine:
         self._idle = True
         self._admit_quiet_s = float(os.environ.get("LMX_ADMIT_QUIET_MS", "2")) / 1e3
         self._admit_max_s = float(os.environ.get("LMX_ADMIT_MAX_MS", "25")) / 1e3
-        self._admit_tokens = 512          # tokens counted per waiting request (budget check)
         la_env = os.environ.get("LMX_LOOKAHEAD", "")
         self.lookahead = la_env == "1" or (la_env != "0" and self.device.type == "cuda"
                                            and self.tp.size == 1)
@@ -672,16 +671,22 @@ class LLMEngine:
         if quiet <= 0 or self.sched.num_running:
             return
         t0 = time.monotonic()
-        n = self.sched.num_waiting
-        while (n < self.ecfg.max_num_seqs and n * self._admit_tokens < self.ecfg.max_batched_tokens
-               and time.monotonic() - t0 < self._admit_max_s):
-            self._wake.wait(timeout=quiet)
+        n = len(self._reqs)                # all waiting: nothing was running
+
+        def queued_tokens():
+            return sum(len(r.prompt_ids) for r in self._reqs.values())
+        self._wake.clear()
+        last = t0                          # the latest arrival seen
+        while (n < self.ecfg.max_num_seqs and queued_tokens() < self.ecfg.max_batched_tokens):
+            now = time.monotonic()
+            if now - last >= quiet or now - t0 >= self._admit_max_s:
+                break
+            self._wake.wait(timeout=min(quiet - (now - last), self._admit_max_s - (now - t0)))
             self._wake.clear()
             self._drain()
-            m = self.sched.num_waiting
-            if m == n:
-                break
-            n = m
+            m = len(self._reqs)
+            if m != n:
+                n, last = m, time.monotonic()
 
     def _step(self) -> bool:
         fl = faults()
@@ -743,6 +748,9 @@ class LLMEngine:
             st["g_launch"] += t2 - t1
             st["g_update"] += t5 - t4
         st["prefill_tokens"] += plan["num_prefill_tokens"]
+        if self.step_trace is not None and bucket is None:
+            self.step_trace.append((time.time(), T, nd, int(plan["num_prefill_tokens"]),
+                                    int(self.sched.num_waiting)))
         return True
 
     def _publish(self, plan, bucket, probe: bool) -> None:

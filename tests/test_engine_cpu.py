@@ -226,3 +226,36 @@ def test_lookahead_recovers_after_a_step_failure(monkeypatch):
     assert sum(1 for x in evs if x.finish == "error") == 3 and e.num_active == 0
     outs = e.generate([list(range(50, 80))], sp)
     assert len(outs[0]) == 8
+
+
+def test_admission_window_gathers_a_burst(monkeypatch):
+    """An idle engine that sees its first request waits while more keep
+    arriving (LMX_ADMIT_QUIET_MS / LMX_ADMIT_MAX_MS) before the first step,
+    so a burst is prefilled together instead of the first arrival alone;
+    with the window off the first step holds what had arrived."""
+    import threading
+    import time as _t
+    from llm_mcp_amd.engine.engine import GenRequest
+    sp = SamplingParams(temperature=0, max_tokens=2, ignore_eos=True)
+
+    def run(quiet_ms):
+        monkeypatch.setenv("LMX_STEP_TRACE", "1")
+        monkeypatch.setenv("LMX_ADMIT_QUIET_MS", str(quiet_ms))
+        monkeypatch.setenv("LMX_ADMIT_MAX_MS", "400")
+        e = _engine(max_batched_tokens=512)
+        e.submit(GenRequest(list(range(1, 21)), sp))
+
+        def later():
+            for i in range(5):            # the rest of the burst, 10 ms apart
+                _t.sleep(0.01)
+                e.submit(GenRequest(list(range(30 + i, 50 + i)), sp))
+        th = threading.Thread(target=later)
+        th.start()
+        e.step()
+        th.join()
+        return e.step_trace[0]
+
+    first = run(40.0)
+    assert first[3] == 6 * 20           # all six prompts in the first step
+    first = run(0.0)
+    assert first[3] < 6 * 20            # window off: only what had arrived
