@@ -305,7 +305,8 @@ class LLMEngine:
         # captured graphs has covered the followers' sampling path; by default
         # a TP group steps synchronously and the leader ships the tokens.
         if os.environ.get("LMX_STEP_TRACE", "0") == "1":
-            self.step_trace = []
+            import collections
+            self.step_trace = collections.deque(maxlen=4096)   # bounded in long runs
         self._idle = True
         self._admit_quiet_s = float(os.environ.get("LMX_ADMIT_QUIET_MS", "2")) / 1e3
         self._admit_max_s = float(os.environ.get("LMX_ADMIT_MAX_MS", "25")) / 1e3
@@ -466,7 +467,7 @@ class LLMEngine:
         return {"graph": graph, "parts": ws.max_parts}
 
     # --------------------------------------------------------- public API ---
-    step_trace: list | None = None     # set to [] by LMX_STEP_TRACE=1 (see _step_la)
+    step_trace = None   # a bounded deque of eager steps with LMX_STEP_TRACE=1 (see _step_la)
 
     def submit(self, req: GenRequest) -> GenRequest:
         if not req.id:
