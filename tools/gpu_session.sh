@@ -161,6 +161,9 @@ for step in "$@"; do
       cat gpurun_out/attn_layout.log ;;
     embed_bench)
       run embed_bench 300 python -u -m llm_mcp_amd.bench.embed_engine_bench || exit $? ;;
+    embed_http)
+      # config 2: /v1/embeddings (HTTP, sync path), 32 concurrent 16-doc requests of 1k-token docs
+      run embed_http 600 python -u -m llm_mcp_amd.bench.serving_bench embed --requests 1024 || exit $? ;;
     rope_probe)
       run rope_probe 120 python -u tools/rope_probe.py || exit $? ;;
     smoke)
