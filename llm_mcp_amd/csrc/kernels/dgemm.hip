@@ -394,6 +394,11 @@ static const DgCfg kDgCfgs[] = {
     {128, 224, 8, 3, 1, 64},   // 23
     {256, 224, 8, 2, 1, 64},   // 24
     {256, 224, 8, 4, 1, 32},   // 25
+    // 64 x 96 tiles, 4 x 2 waves: 4 x 64 = 256 workgroups at M = 256 for the
+    // 6144-column QKV without split-K (hipBLASLt's decomposition of that shape)
+    {64, 96, 4, 4, 0, 64},     // 26
+    {64, 96, 4, 6, 0, 64},     // 27
+    {64, 96, 4, 4, 1, 64},     // 28
 };
 constexpr int kNumDgCfgs = sizeof(kDgCfgs) / sizeof(kDgCfgs[0]);
 
@@ -491,6 +496,9 @@ int dgemm(void* C, const void* A, const void* W, float* slabs, unsigned* tickets
     LMX_DG(23, 128, 224, 8, 3, 1, 64)
     LMX_DG(24, 256, 224, 8, 2, 1, 64)
     LMX_DG(25, 256, 224, 8, 4, 1, 32)
+    LMX_DG(26, 64, 96, 4, 4, 0, 64)
+    LMX_DG(27, 64, 96, 4, 6, 0, 64)
+    LMX_DG(28, 64, 96, 4, 4, 1, 64)
   }
 #undef LMX_DG
 #undef LMX_DG_E
