@@ -4,7 +4,9 @@
 # copy (LMX_RS_PACK_GB=80)
 set -o pipefail
 mkdir -p gpurun_out
-bash tools/call30.sh || exit $?
+timeout -k 10 600 python -u -m llm_mcp_amd.bench.dgemm_bench --only qkv --m 128,160,192,224,256 \
+    --json gpurun_out/dg96_rows.json > gpurun_out/dg96_bench.log 2>&1 || exit $?
+grep -i "qkv" gpurun_out/dg96_bench.log | tail -12
 timeout -k 10 900 python bench.py --model llama-3-70b --concurrency 128 --max-tokens 128 --steps 2 --warmup 1 \
     > gpurun_out/l70_tp1.log 2>&1 || exit $?
 tail -1 gpurun_out/l70_tp1.log | cut -c1-400
