@@ -565,9 +565,9 @@ def test_dgemm_configs_vs_fp32(cfg, M):
     epilogue (plain; SwiGLU with the LDS hand-off, epi 1; SwiGLU on 16-column
     pairs, epi 3, where the wave tile allows), against an fp32 PyTorch
     reference (rows past M masked).  224-column tiles stage their last W slab
-    from half the waves (per-wave counted waits)."""
+    from half the waves (per-wave counted waits); 96-column tiles take N = 1536."""
     bm, bn = ops.DGEMM_CONFIGS[cfg & ops.DGEMM_CFG_MASK]
-    K, N = 1024, (1792 if bn == 224 else 2 * 1024)
+    K, N = 1024, {224: 1792, 96: 1536}.get(bn, 2 * 1024)
     a = torch.randn(M, K, device=DEV).to(torch.bfloat16)
     w = (torch.randn(N, K, device=DEV) * K ** -0.5).to(torch.bfloat16)
     y = a.float() @ w.float().t()

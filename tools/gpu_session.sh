@@ -139,11 +139,12 @@ for step in "$@"; do
       run encoder_bench 600 python -u -m llm_mcp_amd.bench.dgemm_bench --encoder 4096,32768 || exit $? ;;
     prof_bench)
       # the headline bench under a kernel trace; tools/prof_timeline.py splits it into waves/steps
-      # (PROF_TAG names the run: a second traced run under another env in the same call)
+      # (PROF_TAG names the run: a second traced run under another env in the same call;
+      # PROF_ARGS adds bench.py options, e.g. another model)
       tag=${PROF_TAG:-prof_bench}
       rm -rf gpurun_out/$tag
       run $tag 900 rocprofv3 --kernel-trace -d gpurun_out/$tag -o run \
-          -- python3 bench.py --steps 2 --warmup 1 || exit $?
+          -- python3 bench.py --steps 2 --warmup 1 ${PROF_ARGS:-} || exit $?
       python tools/prof_timeline.py gpurun_out/$tag/run_results.db --waves 2 \
           > gpurun_out/${tag}_timeline.md 2>&1 || true
       rm -rf gpurun_out/$tag ;;   # the trace database alone exceeds what gpurun copies back
