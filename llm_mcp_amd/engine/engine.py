@@ -321,6 +321,7 @@ class LLMEngine:
         self.sample_all = self.tp.size > 1 and self.lookahead
         self.tp.logits_to_all = self.sample_all
         self._la = None                    # the launched step not yet read back
+        self._la_end = 0.0                 # when the last launched step was read back
         self._penalized: set[int] = set()  # active requests with penalty windows
         # a gloo TP group (one-GPU rehearsals, CPU-hosted collectives) cannot be
         # captured: its host-staged collectives synchronise inside the step
@@ -834,7 +835,7 @@ class LLMEngine:
             self._la_resolve()
         t3 = time.perf_counter()
         self._la = {"seq_ids": plan["seq_ids"], "sample_seq": plan["sample_seq"], "N": N,
-                    "slot": k}
+                    "slot": k, "graph": bucket is not None, "t_launch": t1}
         if probe:
             self._comm_probe()
         st = self.stats
@@ -846,8 +847,7 @@ class LLMEngine:
         st["step_time_s"] += t3 - t0
         st["decode_steps"] += int(nd == S)
         st["graph_steps"] += int(bucket is not None)
-        if bucket is not None:
-            st["decode_step_s"] += t3 - t0
+        if bucket is not None:      # (decode_step_s: timed when the step resolves)
             st["g_schedule"] += t1 - t0
             st["g_launch"] += t2 - t1
         st["prefill_tokens"] += plan["num_prefill_tokens"]
@@ -865,6 +865,12 @@ class LLMEngine:
         t = time.perf_counter()
         toks, lps = self._finish_fetch(la["N"], la["slot"])
         t2 = time.perf_counter()
+        if la["graph"]:
+            # a queued step runs from the previous step's end (or from its own
+            # launch if the GPU was idle), so a decode step queued behind a
+            # prefill step is not charged that prefill's time
+            self.stats["decode_step_s"] += t2 - max(la["t_launch"], self._la_end)
+        self._la_end = t2
         fin = self.sched.patch(toks)
         self.stats["t_update"] += time.perf_counter() - t2
         self.stats["t_events"] += t2 - t
