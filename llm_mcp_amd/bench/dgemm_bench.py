@@ -151,6 +151,15 @@ def run(model: str, tp: int, ms: list[int], margin: float, only: str = "",
                 t = attempt(cfg | ops.DGEMM_NT, s, bm, bn)
                 if t is not None:
                     timed.append((t, cfg | ops.DGEMM_NT, s, bm, bn))
+            # the stream-K form (one workgroup per CU, pieces summed by a
+            # second kernel) of every tile, non-temporal weights, plain epilogue
+            if epi == 0:
+                for cfg, (bm, bn) in enumerate(cfgs):
+                    if N % bn or (bm > 2 * max(64, M) and bm > 64):
+                        continue
+                    t = attempt(cfg | ops.DGEMM_SK | ops.DGEMM_NT, 0, bm, bn)
+                    if t is not None:
+                        timed.append((t, cfg | ops.DGEMM_SK | ops.DGEMM_NT, 0, bm, bn))
             if timed:
                 best = min(timed)
             line = f"{name:8s} M={M:4d} lib {t_lib:7.1f} us ({nbytes / t_lib / 1e6:5.2f} TB/s)"

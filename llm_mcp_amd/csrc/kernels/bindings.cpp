@@ -54,6 +54,7 @@ int rsgemm_pack(void*, const void*, int, int, long, hipStream_t);
 int rmsnorm_slabs(void*, void*, const float*, int, long, const void*, int, int, long, float,
                   hipStream_t);
 int dgemm_config(int, int*, int*);
+int dgemm_sk_pieces(int, int, int, int, int);
 int pgemm(void*, const void*, const void*, const void*, int, int, int, long, long, long, int, int,
           int, hipStream_t);
 int pgemm_sk(void*, const void*, const void*, void*, void*, int, int, int, int, long, long, long,
@@ -193,6 +194,9 @@ PYBIND11_MODULE(_lmx_kernels, m) {
     check(lmx::rmsnorm_slabs(P<void>(out), P<void>(residual), P<float>(slabs), nsl, slab_stride,
                              P<void>(w), rows, cols, out_stride, eps, S(stream)),
           "rmsnorm_slabs");
+  });
+  m.def("dgemm_sk_pieces", [](int M, int N, int K, int cfg, int groups) {
+    return lmx::dgemm_sk_pieces(M, N, K, cfg, groups);
   });
   m.def("dgemm_configs", []() {
     std::vector<std::pair<int, int>> out;

@@ -39,6 +39,8 @@
 //     decode graph needs no memset node per GEMM.
 #include "common.h"
 
+#include <algorithm>
+
 namespace lmx {
 namespace {
 
@@ -112,53 +114,26 @@ __device__ __forceinline__ void dg_stage(bf16_t* lds_a, bf16_t* lds_w, const bf1
 
 __device__ __forceinline__ float dg_silu(float g) { return g / (1.f + __expf(-g)); }
 
-}  // namespace
-
-template <int BM, int BN, int WM, int NST, int EPI, int ROT, int NT, int BK>
-__global__ void __launch_bounds__(DTHREADS, 2) dgemm_kernel(
-    bf16_t* __restrict__ C, const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
-    float* __restrict__ slabs, unsigned* __restrict__ tickets, int M, int N, int K, long lda,
-    long ldw, long ldc, int splits) {
+// The K loop of one output tile over nk K-steps starting at kbeg (rotated by
+// rot steps): NST-deep LDS-DMA ring, counted vmcnt, raw s_barrier; returns
+// with the ring drained and every wave past its last ds_read, so the caller
+// may restage the ring or reuse the LDS for an epilogue.
+template <int BM, int BN, int WM, int NST, int NT, int BK, int TM, int TN>
+__device__ __forceinline__ void dg_kloop(f32x4_t (&acc)[TM][TN], bf16_t* lds,
+                                         const bf16_t* __restrict__ A, long lda, int m0, int M,
+                                         const bf16_t* __restrict__ W, long ldw, int n0, int kbeg,
+                                         int nk, int rot) {
   constexpr int WN = 8 / WM;
-  constexpr int WTM = BM / WM, WTN = BN / WN;       // wave tile
-  constexpr int TM = WTM / 16, TN = WTN / 16;       // 16x16 MFMA tiles per wave
-  constexpr int RPI = DTHREADS * 8 / BK, RPW = RPI / 8;  // rows per glds instruction / per wave
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int RPI = DTHREADS * 8 / BK, RPW = RPI / 8;
   // LDS-DMA instructions per thread per stage: LPS_F for the waves that stage
   // the partial last W slab of a BN % RPI != 0 tile, LPS_P for the others
   constexpr int LPS_P = BM / RPI + BN / RPI, LPS_F = LPS_P + (BN % RPI != 0);
   constexpr int WFULL = BN % RPI == 0 ? 8 : (BN % RPI) / RPW;
   constexpr int STAGE = (BM + BN) * BK;             // bf16 elements per ring slot
-  static_assert(WM * WN == 8 && TM >= 1 && TN >= 1 && WTM % 16 == 0 && WTN % 16 == 0, "tile");
-  static_assert(BK == 32 || BK == 64, "BK");
-  static_assert(BM % RPI == 0 && BN % RPW == 0, "stage rows");
-  static_assert(EPI != 1 || (WN % 2 == 0 || WN == 1), "swiglu wave split");
-  static_assert(EPI != 3 || WTN % 32 == 0, "swiglu16: gate/up 16-column pairs inside a wave");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  bf16_t* const lds = reinterpret_cast<bf16_t*>(smem);
-
-  const int tiles_m = (M + BM - 1) / BM, tiles_n = N / BN;
-  const int nwg = tiles_m * tiles_n * splits;
-  const int wg = xcd_remap(blockIdx.x, nwg);
-  const int ks = wg % splits, rest = wg / splits;
-  const int tm = rest % tiles_m, tn = rest / tiles_m;
-  const int m0 = tm * BM, n0 = tn * BN;
-  const int kc = K / splits, kbeg = ks * kc, nk = kc / BK;
-  // K-step order rotated per column tile: the workgroups of an XCD start at
-  // different k-offsets, so their concurrent reads of the shared activation
-  // rows (and of their W rows, all at the same 8-KB-strided offsets
-  // otherwise) spread over the L2 / HBM channels instead of camping on one.
-  // ROT 2 also staggers the M-tiles that share a W panel by 2 K-steps: the
-  // leader's W reads miss to HBM, its followers re-read those lines from the
-  // XCD's L2 two steps later (short latency) instead of merging into the same
-  // in-flight misses -- per-CU throughput is bounded by the L1's outstanding
-  // misses x their latency (profiles/r2_pmc_kernels.md)
-  const int rot = ROT == 0 ? 0 : ((tn * 5 + (ROT == 2 ? 2 * tm : 0)) % nk);
-
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wr = wave % WM, wc = wave / WM;
   const int fr = lane & 15, fg = lane >> 4;
-
-  f32x4_t acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -204,6 +179,51 @@ __global__ void __launch_bounds__(DTHREADS, 2) dgemm_kernel(
   dg_vmwait<0>();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __syncthreads();
+}
+
+}  // namespace
+
+template <int BM, int BN, int WM, int NST, int EPI, int ROT, int NT, int BK>
+__global__ void __launch_bounds__(DTHREADS, 2) dgemm_kernel(
+    bf16_t* __restrict__ C, const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
+    float* __restrict__ slabs, unsigned* __restrict__ tickets, int M, int N, int K, long lda,
+    long ldw, long ldc, int splits) {
+  constexpr int WN = 8 / WM;
+  constexpr int WTM = BM / WM, WTN = BN / WN;       // wave tile
+  constexpr int TM = WTM / 16, TN = WTN / 16;       // 16x16 MFMA tiles per wave
+  constexpr int RPI = DTHREADS * 8 / BK, RPW = RPI / 8;  // rows per glds instruction / per wave
+  static_assert(WM * WN == 8 && TM >= 1 && TN >= 1 && WTM % 16 == 0 && WTN % 16 == 0, "tile");
+  static_assert(BK == 32 || BK == 64, "BK");
+  static_assert(BM % RPI == 0 && BN % RPW == 0, "stage rows");
+  static_assert(EPI != 1 || (WN % 2 == 0 || WN == 1), "swiglu wave split");
+  static_assert(EPI != 3 || WTN % 32 == 0, "swiglu16: gate/up 16-column pairs inside a wave");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* const lds = reinterpret_cast<bf16_t*>(smem);
+
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = N / BN;
+  const int nwg = tiles_m * tiles_n * splits;
+  const int wg = xcd_remap(blockIdx.x, nwg);
+  const int ks = wg % splits, rest = wg / splits;
+  const int tm = rest % tiles_m, tn = rest / tiles_m;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kc = K / splits, kbeg = ks * kc, nk = kc / BK;
+  // K-step order rotated per column tile: the workgroups of an XCD start at
+  // different k-offsets, so their concurrent reads of the shared activation
+  // rows (and of their W rows, all at the same 8-KB-strided offsets
+  // otherwise) spread over the L2 / HBM channels instead of camping on one.
+  // ROT 2 also staggers the M-tiles that share a W panel by 2 K-steps: the
+  // leader's W reads miss to HBM, its followers re-read those lines from the
+  // XCD's L2 two steps later (short latency) instead of merging into the same
+  // in-flight misses -- per-CU throughput is bounded by the L1's outstanding
+  // misses x their latency (profiles/r2_pmc_kernels.md)
+  const int rot = ROT == 0 ? 0 : ((tn * 5 + (ROT == 2 ? 2 * tm : 0)) % nk);
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wr = wave % WM, wc = wave / WM;
+  const int fr = lane & 15, fg = lane >> 4;
+
+  f32x4_t acc[TM][TN];
+  dg_kloop<BM, BN, WM, NST, NT, BK>(acc, lds, A, lda, m0, M, W, ldw, n0, kbeg, nk, rot);
 
   // acc[i][j][r] = C[m][n]:  m = m0 + wr*WTM + 16i + fr,  n = n0 + wc*WTN + 16j + 4fg + r
   if (splits > 1 || EPI == 2) {
@@ -356,6 +376,72 @@ __global__ void __launch_bounds__(DTHREADS, 2) dgemm_kernel(
   }
 }
 
+// ---- stream-K form (cfg bit 6) ------------------------------------------------
+// Split-K with S slices runs tiles x S workgroups: for a shape with few column
+// tiles (the Llama-3-70B QKV at 128 rows: 40 tiles of 128 x 256) no S fills the
+// 256 CUs evenly (S 4 = 160 workgroups, S 8 = 320 = 1.25 rounds), and the last
+// arriver then reads S-1 partial tiles alone.  Here the (tile, K-step) space is
+// cut into G equal runs of `per` steps, one workgroup each, so every CU streams
+// the same bytes; a run that crosses a tile boundary finishes one tile's piece
+// and starts the next.  Piece p of tile t (p = g - first workgroup of t) goes to
+// slab p; dg_sk_reduce_kernel then sums each tile's pieces in piece order
+// (bitwise reproducible) and writes bf16 -- the reduction is spread over the
+// whole grid instead of one workgroup per tile.
+template <int BM, int BN, int WM, int NST, int NT, int BK>
+__global__ void __launch_bounds__(DTHREADS, 2) dgemm_sk_kernel(
+    const bf16_t* __restrict__ A, const bf16_t* __restrict__ W, float* __restrict__ slabs, int M,
+    int N, int K, long lda, long ldw, int per) {
+  constexpr int WN = 8 / WM;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* const lds = reinterpret_cast<bf16_t*>(smem);
+  const int tiles_m = (M + BM - 1) / BM, nk = K / BK;
+  const int total = tiles_m * (N / BN) * nk;
+  const int g = blockIdx.x;
+  const int end = min(g * per + per, total);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wr = wave % WM, wc = wave / WM;
+  const int fr = lane & 15, fg = lane >> 4;
+  for (int it = g * per; it < end;) {
+    const int t = it / nk, kb = it - t * nk, n_it = min(nk - kb, end - it);
+    const int tm = t % tiles_m, tn = t / tiles_m;
+    const int m0 = tm * BM, n0 = tn * BN;
+    f32x4_t acc[TM][TN];
+    dg_kloop<BM, BN, WM, NST, NT, BK>(acc, lds, A, lda, m0, M, W, ldw, n0, kb * BK, n_it, 0);
+    float* slab = slabs + (long)(g - t * nk / per) * M * N;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + wr * WTM + 16 * i + fr;
+      if (m >= M) continue;
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        *reinterpret_cast<f32x4_t*>(slab + (long)m * N + n0 + wc * WTN + 16 * j + 4 * fg) = acc[i][j];
+    }
+    it += n_it;
+  }
+}
+
+// C[m][n..n+3] = sum over tile(m, n)'s pieces, 4 columns per thread
+__global__ void __launch_bounds__(256) dg_sk_reduce_kernel(bf16_t* __restrict__ C,
+                                                           const float* __restrict__ slabs, int M,
+                                                           int N, long ldc, int BM, int BN, int nk,
+                                                           int per) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int q = N >> 2;
+  if (i >= (long)M * q) return;
+  const int m = (int)(i / q), n = (int)(i - (long)m * q) * 4;
+  const int t = (n / BN) * ((M + BM - 1) / BM) + m / BM;
+  const int np = (t * nk + nk - 1) / per - t * nk / per + 1;
+  const float* src = slabs + (long)m * N + n;
+  f32x4_t s = *reinterpret_cast<const f32x4_t*>(src);
+  for (int p = 1; p < np; ++p) s += *reinterpret_cast<const f32x4_t*>(src + (long)p * M * N);
+  bf16x4_t o;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) o[r] = (short)f2bf(s[r]);
+  *reinterpret_cast<bf16x4_t*>(C + (long)m * ldc + n) = o;
+}
+
 // ---- launcher ---------------------------------------------------------------
 // cfg ids (BM, BN, WM, NST, ROT, BK); kept in sync with ops.DGEMM_CONFIGS
 struct DgCfg { int bm, bn, wm, nst, rot, bk; };
@@ -411,6 +497,22 @@ int dgemm_config(int cfg, int* bm, int* bn) {
   return 0;
 }
 
+// K-steps per workgroup of the stream-K form and its slab count (the most
+// pieces any tile is cut into): ops sizes the workspace as pieces x M x N
+int dgemm_sk_per(int M, int N, int K, int bm, int bn, int bk, int groups) {
+  const long total = (long)((M + bm - 1) / bm) * (N / bn) * (K / bk);
+  const int G = groups > 0 ? groups : 256;
+  return (int)std::max<long>(1, (total + G - 1) / G);
+}
+
+int dgemm_sk_pieces(int M, int N, int K, int cfg, int groups) {
+  cfg &= 31;
+  if (cfg < 0 || cfg >= kNumDgCfgs) return -1;
+  const DgCfg c = kDgCfgs[cfg];
+  const int nk = K / c.bk, per = dgemm_sk_per(M, N, K, c.bm, c.bn, c.bk, groups);
+  return (nk + per - 1) / per + 1;
+}
+
 template <int BM, int BN, int WM, int NST, int EPI, int ROT, int NT, int BK>
 static int dg_launch(bf16_t* C, const bf16_t* A, const bf16_t* W, float* slabs,
                      unsigned* tickets, int M, int N, int K, long lda, long ldw, long ldc,
@@ -433,17 +535,47 @@ static int dg_launch(bf16_t* C, const bf16_t* A, const bf16_t* W, float* slabs,
   return (int)hipGetLastError();
 }
 
+// stream-K launch: G = `groups` workgroups (0: one per CU), then the reduction
+template <int BM, int BN, int WM, int NST, int NT, int BK>
+static int dg_sk_launch(bf16_t* C, const bf16_t* A, const bf16_t* W, float* slabs, int M, int N,
+                        int K, long lda, long ldw, long ldc, int groups, hipStream_t stream) {
+  constexpr size_t smem = (size_t)NST * (BM + BN) * BK * sizeof(bf16_t);
+  static_assert(smem <= 160 * 1024, "LDS");
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e = hipFuncSetAttribute((const void*)dgemm_sk_kernel<BM, BN, WM, NST, NT, BK>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    if (e != hipSuccess) return (int)e;
+    attr = true;
+  }
+  const int nk = K / BK, total = ((M + BM - 1) / BM) * (N / BN) * nk;
+  const int per = dgemm_sk_per(M, N, K, BM, BN, BK, groups);
+  const int G = (total + per - 1) / per;
+  dgemm_sk_kernel<BM, BN, WM, NST, NT, BK><<<dim3(G), dim3(DTHREADS), smem, stream>>>(
+      A, W, slabs, M, N, K, lda, ldw, per);
+  const long n4 = (long)M * (N / 4);
+  dg_sk_reduce_kernel<<<dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, stream>>>(
+      C, slabs, M, N, ldc, BM, BN, nk, per);
+  return (int)hipGetLastError();
+}
+
 int dgemm(void* C, const void* A, const void* W, float* slabs, unsigned* tickets, int n_tickets,
           int M, int N, int K, long lda, long ldw, long ldc, int cfg, int splits, int epi,
           hipStream_t stream) {
   if (M <= 0) return 0;
   const int nt = (cfg >> 5) & 1;      // bit 5: non-temporal weight stream
+  const int sk = (cfg >> 6) & 1;      // bit 6: stream-K, `splits` = workgroups (0: 256)
   cfg &= 31;
-  if (cfg < 0 || cfg >= kNumDgCfgs || splits < 1 || epi < 0 || epi > 3) return -1;
+  if (cfg < 0 || cfg >= kNumDgCfgs || splits < 0 || epi < 0 || epi > 3) return -1;
   const DgCfg c = kDgCfgs[cfg];
-  if (N % c.bn != 0 || K % (splits * c.bk) != 0) return -1;
+  if (sk) {
+    if (epi != 0 || N % c.bn != 0 || K % c.bk != 0) return -1;
+    if (slabs == nullptr) return -2;
+  } else if (splits < 1 || N % c.bn != 0 || K % (splits * c.bk) != 0) {
+    return -1;
+  }
   if (epi == 2 && slabs == nullptr) return -2;
-  if (splits > 1 && epi != 2) {
+  if (!sk && splits > 1 && epi != 2) {
     if (slabs == nullptr || tickets == nullptr) return -2;
     if (((M + c.bm - 1) / c.bm) * (N / c.bn) > n_tickets) return -3;
   }
@@ -451,6 +583,9 @@ int dgemm(void* C, const void* A, const void* W, float* slabs, unsigned* tickets
   auto A_ = (const bf16_t*)A;
   auto W_ = (const bf16_t*)W;
 #define LMX_DG_E(BM, BN, WM, NST, ROT, NT, BK)                                                 \
+  if (sk)                                                                                     \
+    return dg_sk_launch<BM, BN, WM, NST, NT, BK>(C_, A_, W_, slabs, M, N, K, lda, ldw, ldc,   \
+                                                 splits, stream);                             \
   if (epi == 3) {                                                                             \
     if constexpr ((BN / (8 / WM)) % 32 == 0)                                                  \
       return dg_launch<BM, BN, WM, NST, 3, ROT, NT, BK>(C_, A_, W_, slabs, tickets, M, N, K, \

@@ -754,6 +754,9 @@ DGEMM_MAX_M = 256
 # a configuration id with bit 5 set (cfg | DGEMM_NT) streams the weights
 # non-temporal (dgemm.hip NT): the low bits select the tile
 DGEMM_NT, DGEMM_CFG_MASK = 32, 31
+# cfg | DGEMM_SK: the stream-K form (dgemm.hip dgemm_sk_kernel + its reduction):
+# ``splits`` is then the workgroup count G (0: one per CU), plain epilogue only
+DGEMM_SK = 64
 _DG_WS: dict = {}          # (device, stream) -> (slabs fp32, tickets uint32)
 _DG_TICKETS = 8192
 DGEMM_TABLE: dict | None = None
@@ -943,7 +946,9 @@ def dgemm(a: torch.Tensor, w: torch.Tensor, cfg: int, splits: int, epi: int = 0,
     N = w.shape[0]
     bm, bn = DGEMM_CONFIGS[cfg & DGEMM_CFG_MASK]
     ncols = N // 2 if epi in (1, 3) else N
+    sk = bool(cfg & DGEMM_SK)
     _chk(epi != 3 or swiglu16_ok(cfg), f"dgemm cfg {cfg} cannot run the epi-3 epilogue")
+    _chk(not sk or epi == 0, "the stream-K form has the plain epilogue only")
     if not a.is_cuda:
         y = a.float() @ w.float().t()
         if epi in (1, 3):
@@ -956,7 +961,7 @@ def dgemm(a: torch.Tensor, w: torch.Tensor, cfg: int, splits: int, epi: int = 0,
             return out
         return y
     _bf16(a, "a"); _bf16(w, "w")
-    _chk(M > 0 and N % bn == 0 and K % (64 * splits) == 0,
+    _chk(M > 0 and N % bn == 0 and K % (64 * (1 if sk else splits)) == 0 and splits >= 0,
          f"dgemm shape M={M} N={N} K={K} cfg={cfg} splits={splits}")
     _chk(w.shape[1] == K and a.stride(1) == 1 and w.stride(1) == 1, "dgemm layout")
     _chk(a.stride(0) % 8 == 0 and w.stride(0) % 8 == 0 and a.data_ptr() % 16 == 0
@@ -966,7 +971,10 @@ def dgemm(a: torch.Tensor, w: torch.Tensor, cfg: int, splits: int, epi: int = 0,
     _chk(out.shape == (M, ncols) and out.stride(1) == 1 and out.stride(0) % 4 == 0
          and out.data_ptr() % 8 == 0, "dgemm output layout")
     slabs = tickets = None
-    if splits > 1:
+    if sk:
+        slabs, tickets = _dg_workspace(a.device, native().dgemm_sk_pieces(M, N, K, cfg, splits)
+                                       * M * N)
+    elif splits > 1:
         _chk(-(-M // bm) * (N // bn) <= _DG_TICKETS, "dgemm tile count")
         slabs, tickets = _dg_workspace(a.device, splits * M * N)
     native().dgemm(_ptr(out), _ptr(a), _ptr(w), _ptr(slabs), _ptr(tickets), _DG_TICKETS, M, N, K,

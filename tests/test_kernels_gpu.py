@@ -588,6 +588,28 @@ def test_dgemm_configs_vs_fp32(cfg, M):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cfg", [6, 1, 0, 22, 26, 23])
+@pytest.mark.parametrize("M,N,K,groups", [(1, 2048, 1024, 0), (37, 2048, 1024, 7),
+                                          (128, 2048, 1024, 0), (130, 2048, 2048, 300),
+                                          (256, 2048, 1024, 64)])
+def test_dgemm_stream_k_vs_fp32(cfg, M, N, K, groups):
+    """K11 stream-K form (cfg | DGEMM_SK): equal runs of K-steps per
+    workgroup crossing tile boundaries (runs shorter and longer than a tile,
+    a grid smaller than the tile count), pieces summed by the reduction
+    kernel, against an fp32 reference; bitwise repeatable."""
+    bm, bn = ops.DGEMM_CONFIGS[cfg]
+    if bn in (96, 224):
+        N = {96: 1536, 224: 1792}[bn]
+    a = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) * K ** -0.5).to(torch.bfloat16)
+    y = a.float() @ w.float().t()
+    for c in (cfg | ops.DGEMM_SK, cfg | ops.DGEMM_SK | ops.DGEMM_NT):
+        out = ops.dgemm(a, w, c, groups)
+        torch.testing.assert_close(out.float(), y, atol=2e-2, rtol=2e-2)
+        assert torch.equal(out, ops.dgemm(a, w, c, groups))
+
+
+@pytest.mark.gpu
 def test_dgemm_in_graph_strided_input_long_k():
     M, K, N = 96, 14336, 4096
     x = torch.randn(M, K + 64, device=DEV).to(torch.bfloat16)[:, :K]   # row stride K + 64
