@@ -485,12 +485,6 @@ static const DgCfg kDgCfgs[] = {
     {64, 96, 4, 4, 0, 64},     // 26
     {64, 96, 4, 6, 0, 64},     // 27
     {64, 96, 4, 4, 1, 64},     // 28
-    // 256 x 96 tiles, 8 x 1 waves: 64 column tiles x S 4 = 256 workgroups for the
-    // same QKV at M = 256, each reading a quarter of K -- 720 KB per CU against
-    // 1.3 MB for 64 x 96 (whose activation re-reads outweigh the weights); the
-    // W slab's last 32 rows are staged by waves 0-3 (as the 224-column tiles)
-    {256, 96, 8, 3, 1, 64},    // 29
-    {256, 96, 8, 6, 1, 32},    // 30
 };
 constexpr int kNumDgCfgs = sizeof(kDgCfgs) / sizeof(kDgCfgs[0]);
 
@@ -640,8 +634,6 @@ int dgemm(void* C, const void* A, const void* W, float* slabs, unsigned* tickets
     LMX_DG(26, 64, 96, 4, 4, 0, 64)
     LMX_DG(27, 64, 96, 4, 6, 0, 64)
     LMX_DG(28, 64, 96, 4, 4, 1, 64)
-    LMX_DG(29, 256, 96, 8, 3, 1, 64)
-    LMX_DG(30, 256, 96, 8, 6, 1, 32)
   }
 #undef LMX_DG
 #undef LMX_DG_E
