@@ -141,7 +141,8 @@ def run(model: str, tp: int, ms: list[int], margin: float, only: str = "",
                     continue
                 for s in (1, 2, 4, 8, 16):
                     nwg = tiles * s
-                    if K % (64 * s) or nwg < 32 or nwg > 1536 or (s > 1 and K // s < 256):
+                    bk = 128 if cfg in ops.DGEMM_BK128 else 64
+                    if K % (bk * s) or nwg < 32 or nwg > 1536 or (s > 1 and K // s < 256):
                         continue
                     t = attempt(cfg, s, bm, bn)
                     if t is not None:
@@ -222,7 +223,8 @@ def deferred(name, N, K, M, x, ws, ncopy, iters, cfgs, margin, rows) -> dict:
         tiles = -(-M // bm) * (N // bn)
         for s_ in (1, 2, 4, 8, 16):
             nwg = tiles * s_
-            if K % (64 * s_) or nwg < 32 or nwg > 1536 or (s_ > 1 and K // s_ < 256):
+            bk = 128 if cfg in ops.DGEMM_BK128 else 64
+            if K % (bk * s_) or nwg < 32 or nwg > 1536 or (s_ > 1 and K // s_ < 256):
                 continue
             t = attempt(cfg, s_, bm, bn)
             if t is not None:

@@ -56,11 +56,13 @@ __device__ __forceinline__ void dg_glds16(const void* gsrc, void* lds_base) {
 // XOR swizzle of the 16-B chunk index in row r of a [row][BK] image, chosen
 // so that the 16-lane groups of a ds_read_b128 (lanes {0-3,12-15,20-27},
 // {4-11,16-19,28-31}, ... : 16 rows x chunk fg) hit 16 distinct 16-B slots
-// of the 256-B bank row.  BK 64 (128-B rows): chunk ^ (r/2 mod 8).  BK 32
-// (64-B rows, 4 rows per bank row): chunk ^ {0,2,3,1}[r/4 mod 4].
+// of the 256-B bank row.  BK 128 (256-B rows): chunk ^ (r mod 16).  BK 64
+// (128-B rows): chunk ^ (r/2 mod 8).  BK 32 (64-B rows, 4 rows per bank
+// row): chunk ^ {0,2,3,1}[r/4 mod 4].
 template <int BK>
 __device__ __forceinline__ int dg_swz(int r) {
-  if constexpr (BK == 64) return (r >> 1) & 7;
+  if constexpr (BK == 128) return r & 15;     // 256-B rows: one row per bank row
+  else if constexpr (BK == 64) return (r >> 1) & 7;
   else return (0x78 >> (2 * ((r >> 2) & 3))) & 3;
 }
 
@@ -193,7 +195,7 @@ __global__ void __launch_bounds__(DTHREADS, 2) dgemm_kernel(
   constexpr int TM = WTM / 16, TN = WTN / 16;       // 16x16 MFMA tiles per wave
   constexpr int RPI = DTHREADS * 8 / BK, RPW = RPI / 8;  // rows per glds instruction / per wave
   static_assert(WM * WN == 8 && TM >= 1 && TN >= 1 && WTM % 16 == 0 && WTN % 16 == 0, "tile");
-  static_assert(BK == 32 || BK == 64, "BK");
+  static_assert(BK == 32 || BK == 64 || BK == 128, "BK");
   static_assert(BM % RPI == 0 && BN % RPW == 0, "stage rows");
   static_assert(EPI != 1 || (WN % 2 == 0 || WN == 1), "swiglu wave split");
   static_assert(EPI != 3 || WTN % 32 == 0, "swiglu16: gate/up 16-column pairs inside a wave");
@@ -485,6 +487,10 @@ static const DgCfg kDgCfgs[] = {
     {64, 96, 4, 4, 0, 64},     // 26
     {64, 96, 4, 6, 0, 64},     // 27
     {64, 96, 4, 4, 1, 64},     // 28
+    // the same tile with 128-deep K-steps (256-B LDS rows): half the ring
+    // barriers and waits per weight byte of the 64-deep form
+    {64, 96, 4, 3, 0, 128},    // 29
+    {64, 96, 4, 3, 1, 128},    // 30
 };
 constexpr int kNumDgCfgs = sizeof(kDgCfgs) / sizeof(kDgCfgs[0]);
 
@@ -634,6 +640,8 @@ int dgemm(void* C, const void* A, const void* W, float* slabs, unsigned* tickets
     LMX_DG(26, 64, 96, 4, 4, 0, 64)
     LMX_DG(27, 64, 96, 4, 6, 0, 64)
     LMX_DG(28, 64, 96, 4, 4, 1, 64)
+    LMX_DG(29, 64, 96, 4, 3, 0, 128)
+    LMX_DG(30, 64, 96, 4, 3, 1, 128)
   }
 #undef LMX_DG
 #undef LMX_DG_E

@@ -745,11 +745,14 @@ DGEMM_CONFIGS = [(256, 128), (128, 128), (64, 128), (256, 64), (128, 64), (64, 6
                  (64, 64), (128, 64), (64, 128), (128, 128), (128, 256),
                  (256, 256), (256, 256), (256, 128), (128, 256),     # 19-22: 32-deep K-steps
                  (128, 224), (256, 224), (256, 224),                 # 23-25: 224-column tiles
-                 (64, 96), (64, 96), (64, 96)]                       # 26-28: 64 x 96 tiles
+                 (64, 96), (64, 96), (64, 96),                       # 26-28: 64 x 96 tiles
+                 (64, 96), (64, 96)]                                 # 29-30: the same, 128-deep K
 # waves along M of each configuration (dgemm.hip kDgCfgs): the fused SwiGLU on
 # 16-column gate/up pairs (epi 3) needs a wave tile width BN*WM/8 divisible by 32
-DGEMM_WM = [4, 2, 2, 8, 4, 2, 2, 2, 4, 2, 2, 2, 4, 4, 2, 4, 2, 2, 2, 4, 4, 4, 2, 8, 8, 8, 4, 4, 4]
+DGEMM_WM = [4, 2, 2, 8, 4, 2, 2, 2, 4, 2, 2, 2, 4, 4, 2, 4, 2, 2, 2, 4, 4, 4, 2, 8, 8, 8, 4, 4, 4,
+            4, 4]
 SWIGLU16 = 16              # gate/up interleave block of the epi-3 form
+DGEMM_BK128 = (29, 30)     # configurations with 128-deep K-steps (K % (128 S) == 0)
 DGEMM_MAX_M = 256
 # a configuration id with bit 5 set (cfg | DGEMM_NT) streams the weights
 # non-temporal (dgemm.hip NT): the low bits select the tile
@@ -961,7 +964,8 @@ def dgemm(a: torch.Tensor, w: torch.Tensor, cfg: int, splits: int, epi: int = 0,
             return out
         return y
     _bf16(a, "a"); _bf16(w, "w")
-    _chk(M > 0 and N % bn == 0 and K % (64 * (1 if sk else splits)) == 0 and splits >= 0,
+    bk = 128 if (cfg & DGEMM_CFG_MASK) in DGEMM_BK128 else 64
+    _chk(M > 0 and N % bn == 0 and K % (bk * (1 if sk else splits)) == 0 and splits >= 0,
          f"dgemm shape M={M} N={N} K={K} cfg={cfg} splits={splits}")
     _chk(w.shape[1] == K and a.stride(1) == 1 and w.stride(1) == 1, "dgemm layout")
     _chk(a.stride(0) % 8 == 0 and w.stride(0) % 8 == 0 and a.data_ptr() % 16 == 0
@@ -990,7 +994,8 @@ def dgemm_partials(a: torch.Tensor, w: torch.Tensor, cfg: int, splits: int) -> P
     N = w.shape[0]
     bm, bn = DGEMM_CONFIGS[cfg & DGEMM_CFG_MASK]
     _bf16(a, "a"); _bf16(w, "w")
-    _chk(0 < M <= DGEMM_MAX_M and N % bn == 0 and K % (64 * splits) == 0,
+    bk = 128 if (cfg & DGEMM_CFG_MASK) in DGEMM_BK128 else 64
+    _chk(0 < M <= DGEMM_MAX_M and N % bn == 0 and K % (bk * splits) == 0,
          f"dgemm_partials shape M={M} N={N} K={K} cfg={cfg} splits={splits}")
     _chk(w.shape[1] == K and a.stride(1) == 1 and w.stride(1) == 1, "dgemm layout")
     _chk(a.stride(0) % 8 == 0 and w.stride(0) % 8 == 0 and a.data_ptr() % 16 == 0
