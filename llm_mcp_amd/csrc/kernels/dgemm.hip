@@ -491,6 +491,7 @@ static const DgCfg kDgCfgs[] = {
     // barriers and waits per weight byte of the 64-deep form
     {64, 96, 4, 3, 0, 128},    // 29
     {64, 96, 4, 3, 1, 128},    // 30
+    {64, 128, 2, 3, 1, 128},   // 31: 64 x 128, 128-deep (the last id below the NT bit)
 };
 constexpr int kNumDgCfgs = sizeof(kDgCfgs) / sizeof(kDgCfgs[0]);
 
@@ -642,6 +643,7 @@ int dgemm(void* C, const void* A, const void* W, float* slabs, unsigned* tickets
     LMX_DG(28, 64, 96, 4, 4, 1, 64)
     LMX_DG(29, 64, 96, 4, 3, 0, 128)
     LMX_DG(30, 64, 96, 4, 3, 1, 128)
+    LMX_DG(31, 64, 128, 2, 3, 1, 128)
   }
 #undef LMX_DG
 #undef LMX_DG_E
