@@ -469,19 +469,16 @@ static const DgCfg kDgCfgs[] = {
     {64, 128, 2, 5, 2, 64},    // 16
     {128, 128, 2, 4, 2, 64},   // 17
     {128, 256, 2, 3, 2, 64},   // 18
-    // 32-deep K-steps: half-size ring slots, so the 256-row tiles keep 2-3
-    // K-steps in flight across the barrier (cfg 13's 64-deep slots fit only
-    // a 2-slot ring in 160 KB and drain every step)
-    {256, 256, 4, 4, 1, 32},   // 19
-    {256, 256, 4, 5, 1, 32},   // 20
-    {256, 128, 4, 6, 1, 32},   // 21
-    {128, 256, 2, 6, 1, 32},   // 22
-    // 224-column tiles (28672 = 128 x 224: one workgroup per CU at M = 256 with
-    // 128-row tiles), 8 x 1 waves; the W slab's last 32 rows are staged by
-    // waves 0-3 only
-    {128, 224, 8, 3, 1, 64},   // 23
-    {256, 224, 8, 2, 1, 64},   // 24
-    {256, 224, 8, 4, 1, 32},   // 25
+    // 128-deep K-steps (256-B LDS rows): half the ring barriers and counted
+    // waits per weight byte of the 64-deep forms (ids 19-25 held 32-deep and
+    // 224-column tiles until round 4; those lost every measured shape)
+    {64, 96, 4, 4, 1, 128},    // 19
+    {128, 64, 4, 3, 1, 128},   // 20
+    {64, 64, 2, 4, 1, 128},    // 21
+    {128, 128, 2, 2, 1, 128},  // 22
+    {256, 64, 8, 2, 1, 128},   // 23
+    {64, 128, 2, 3, 0, 128},   // 24
+    {64, 64, 2, 5, 1, 128},    // 25
     // 64 x 96 tiles, 4 x 2 waves: 4 x 64 = 256 workgroups at M = 256 for the
     // 6144-column QKV without split-K (hipBLASLt's decomposition of that shape)
     {64, 96, 4, 4, 0, 64},     // 26
@@ -631,13 +628,13 @@ int dgemm(void* C, const void* A, const void* W, float* slabs, unsigned* tickets
     LMX_DG(16, 64, 128, 2, 5, 2, 64)
     LMX_DG(17, 128, 128, 2, 4, 2, 64)
     LMX_DG(18, 128, 256, 2, 3, 2, 64)
-    LMX_DG(19, 256, 256, 4, 4, 1, 32)
-    LMX_DG(20, 256, 256, 4, 5, 1, 32)
-    LMX_DG(21, 256, 128, 4, 6, 1, 32)
-    LMX_DG(22, 128, 256, 2, 6, 1, 32)
-    LMX_DG(23, 128, 224, 8, 3, 1, 64)
-    LMX_DG(24, 256, 224, 8, 2, 1, 64)
-    LMX_DG(25, 256, 224, 8, 4, 1, 32)
+    LMX_DG(19, 64, 96, 4, 4, 1, 128)
+    LMX_DG(20, 128, 64, 4, 3, 1, 128)
+    LMX_DG(21, 64, 64, 2, 4, 1, 128)
+    LMX_DG(22, 128, 128, 2, 2, 1, 128)
+    LMX_DG(23, 256, 64, 8, 2, 1, 128)
+    LMX_DG(24, 64, 128, 2, 3, 0, 128)
+    LMX_DG(25, 64, 64, 2, 5, 1, 128)
     LMX_DG(26, 64, 96, 4, 4, 0, 64)
     LMX_DG(27, 64, 96, 4, 6, 0, 64)
     LMX_DG(28, 64, 96, 4, 4, 1, 64)

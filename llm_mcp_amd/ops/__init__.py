@@ -743,17 +743,18 @@ def swiglu16_ok(cfg: int) -> bool:
 DGEMM_CONFIGS = [(256, 128), (128, 128), (64, 128), (256, 64), (128, 64), (64, 64), (128, 256),
                  (64, 64), (128, 64), (64, 128), (128, 128), (128, 256), (256, 128), (256, 256),
                  (64, 64), (128, 64), (64, 128), (128, 128), (128, 256),
-                 (256, 256), (256, 256), (256, 128), (128, 256),     # 19-22: 32-deep K-steps
-                 (128, 224), (256, 224), (256, 224),                 # 23-25: 224-column tiles
+                 (64, 96), (128, 64), (64, 64), (128, 128), (256, 64), (64, 128),  # 19-25:
+                 (64, 64),                                                          # 128-deep K
                  (64, 96), (64, 96), (64, 96),                       # 26-28: 64 x 96 tiles
                  (64, 96), (64, 96),                                 # 29-30: the same, 128-deep K
                  (64, 128)]                                          # 31: 64 x 128, 128-deep K
 # waves along M of each configuration (dgemm.hip kDgCfgs): the fused SwiGLU on
 # 16-column gate/up pairs (epi 3) needs a wave tile width BN*WM/8 divisible by 32
-DGEMM_WM = [4, 2, 2, 8, 4, 2, 2, 2, 4, 2, 2, 2, 4, 4, 2, 4, 2, 2, 2, 4, 4, 4, 2, 8, 8, 8, 4, 4, 4,
-            4, 4, 2]
+DGEMM_WM = [4, 2, 2, 8, 4, 2, 2, 2, 4, 2, 2, 2, 4, 4, 2, 4, 2, 2, 2,
+            4, 4, 2, 2, 8, 2, 2,
+            4, 4, 4, 4, 4, 2]
 SWIGLU16 = 16              # gate/up interleave block of the epi-3 form
-DGEMM_BK128 = (29, 30, 31) # configurations with 128-deep K-steps (K % (128 S) == 0)
+DGEMM_BK128 = (19, 20, 21, 22, 23, 24, 25, 29, 30, 31)  # configurations with 128-deep K-steps (K % (128 S) == 0)
 DGEMM_MAX_M = 256
 # a configuration id with bit 5 set (cfg | DGEMM_NT) streams the weights
 # non-temporal (dgemm.hip NT): the low bits select the tile
