@@ -631,7 +631,8 @@ def test_dgemm_in_graph_strided_input_long_k():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg,splits", [(0, 8), (5, 1), (1, 4), (13, 16), (1 | 32, 4), (19, 16), (21, 8)])
+@pytest.mark.parametrize("cfg,splits", [(0, 8), (5, 1), (1, 4), (13, 16), (1 | 32, 4), (23, 16), (21, 8),
+                                       (31, 2), (20, 2)])
 def test_dgemm_partials_into_rmsnorm(cfg, splits):
     """K11 partials-only epilogue summed by the residual-add RMSNorm equals the
     fp32 reference of norm(residual + x @ w^T)."""
