@@ -497,8 +497,8 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
 // longest-first order with a grid stride, so no workgroup launches ragged
 // rounds behind the first and the per-workgroup start-up is paid once per
 // resident slot.
-template <int HD, int MODE, int OCC = 3>
-__global__ void __launch_bounds__(256, OCC) paged_decode_persist_kernel(
+template <int HD, int MODE>
+__global__ void __launch_bounds__(256, 3) paged_decode_persist_kernel(
     const bf16_t* __restrict__ q, long q_stride, const bf16_t* __restrict__ k_cache,
     const bf16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ context_lens, const int* __restrict__ order,
@@ -541,24 +541,22 @@ __global__ void __launch_bounds__(128) paged_decode_reduce_kernel(
 // loop form (probe / A-B knob): 0 default -- the persistent grid when every
 // sequence is one partition, else one workgroup per segment; 1 pipelined
 // pages; 2, 3 load-only diagnostics; 4 one workgroup per segment always; 5 the
-// default forms with non-temporal K/V loads; 8 the persistent form at 4
-// workgroups per CU
+// default forms with non-temporal K/V loads
 static int g_decode_mode = 0;
 void set_decode_mode(int mode) { g_decode_mode = mode; }
 
-// resident 256-thread decode workgroups per CU: 3 (146 VGPRs) or, mode 8, 4
-// (capped at 128 VGPRs)
-static int decode_resident_wgs(int per_cu = 3) {
-  static int cus = 0;
-  if (cus == 0) {
-    int dev = 0, n = 0;
+// resident 256-thread decode workgroups: 3 per CU (168 VGPRs incl. AGPRs)
+static int decode_resident_wgs() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        n <= 0)
-      n = 256;
-    cus = n;
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+    n = 3 * cus;
   }
-  return per_cu * cus;
+  return n;
 }
 
 int paged_decode(const void* q, long q_stride, const void* k_cache, const void* v_cache,
@@ -586,16 +584,9 @@ int paged_decode(const void* q, long q_stride, const void* k_cache, const void* 
       (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, \
       bt_stride, context_lens, order, (bf16_t*)out, out_stride, B, Hq, Hkv, scale, part_tokens, \
       rp);
-#define LMX_DEC_P4(HDV)                                                                       \
-  paged_decode_persist_kernel<HDV, 0, 4><<<dim3(std::min(B * Hkv, decode_resident_wgs(4))),    \
-                                         dim3(256), 0, stream>>>(                             \
-      (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, \
-      bt_stride, context_lens, order, (bf16_t*)out, out_stride, B, Hq, Hkv, scale, part_tokens, \
-      rp);
 #define LMX_DEC(HDV)                                                                          \
   if (g_decode_mode == 0 && max_parts == 1) { LMX_DEC_P(HDV, 0) }                             \
   else if (g_decode_mode == 5 && max_parts == 1) { LMX_DEC_P(HDV, 5) }                        \
-  else if (g_decode_mode == 8 && max_parts == 1) { LMX_DEC_P4(HDV) }                          \
   else if (g_decode_mode == 6 && max_parts == 1) { LMX_DEC_P(HDV, 6) }                        \
   else if (g_decode_mode == 6) { LMX_DEC_K(HDV, 6) }                                          \
   else if (g_decode_mode == 5) { LMX_DEC_K(HDV, 5) }                                          \
@@ -610,7 +601,6 @@ int paged_decode(const void* q, long q_stride, const void* k_cache, const void* 
 #undef LMX_DEC
 #undef LMX_DEC_K
 #undef LMX_DEC_P
-#undef LMX_DEC_P4
   return (int)hipGetLastError();
 }
 
