@@ -54,10 +54,57 @@ def _torch_libdir() -> str | None:
     return None
 
 
-def _run(cmd: list[str]) -> None:
+def _run(cmd: list[str]) -> str:
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"build failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return r.stderr
+
+
+# Kernels that keep inline-asm load destinations in flight across code the
+# compiler schedules (hand-counted vmcnt rings): a spill or scratch use of such
+# a register before its data lands is silent corruption, so every
+# instantiation must compile with no VGPR spill and no scratch.  The compile of
+# these sources adds -Rpass-analysis=kernel-resource-usage and the build fails
+# on a violation; the parsed table is kept in build/kernels/resource_usage.json.
+ASM_RING_KERNELS = {"rsgemm.hip": r"rsgemm_kernel",
+                    "attention.hip": r"paged_decode_\w*kernelILi\d+ELi9E"}
+
+
+def parse_resource_usage(text: str) -> dict:
+    """{kernel: {"vgpr_spill": n, "sgpr_spill": n, "scratch": bytes, "vgprs": n}}
+    from hipcc -Rpass-analysis=kernel-resource-usage remarks."""
+    import re
+    out, cur = {}, None
+    for line in text.splitlines():
+        m = re.search(r"remark: Function Name: (\S+)", line)
+        if m:
+            cur = out.setdefault(m.group(1), {})
+            continue
+        if cur is None:
+            continue
+        for key, pat in (("vgpr_spill", r"VGPRs Spill: (\d+)"), ("sgpr_spill", r"SGPRs Spill: (\d+)"),
+                         ("scratch", r"ScratchSize \[bytes/lane\]: (\d+)"),
+                         ("vgprs", r"remark:\s+VGPRs: (\d+)")):
+            m = re.search(pat, line)
+            if m:
+                cur[key] = int(m.group(1))
+    return out
+
+
+def audit_asm_rings(usage: dict[str, dict]) -> list[str]:
+    """Violations (empty list: clean) of the no-spill / no-scratch rule."""
+    import re
+    bad = []
+    for src, pat in ASM_RING_KERNELS.items():
+        fns = {k: v for k, v in usage.get(src, {}).items() if re.search(pat, k)}
+        if not fns:
+            bad.append(f"{src}: no kernel matching {pat} in the resource report")
+        for k, v in fns.items():
+            if v.get("vgpr_spill", 0) or v.get("scratch", 0) or v.get("sgpr_spill", 0):
+                bad.append(f"{src}: {k} spills (vgpr {v.get('vgpr_spill')}, "
+                           f"sgpr {v.get('sgpr_spill')}, scratch {v.get('scratch')} B/lane)")
+    return bad
 
 
 def _stale(out: Path, deps: list[Path]) -> bool:
@@ -87,11 +134,17 @@ def build_kernels(force: bool = False, verbose: bool = False) -> Path:
               "-munsafe-fp-atomics", f"-I{kdir}"]
     objs = []
     jobs = []
+    audit_file = objdir / "resource_usage.json"
+    audit_srcs = []
     for s in srcs:
         o = objdir / (s.stem + ".o")
         objs.append(o)
-        if force or _stale(o, [s] + headers):
-            jobs.append(common + ["-c", str(s), "-o", str(o)])
+        ring = s.name in ASM_RING_KERNELS
+        if force or _stale(o, [s] + headers) or (ring and _stale(audit_file, [s] + headers)):
+            extra = ["-Rpass-analysis=kernel-resource-usage"] if ring else []
+            jobs.append(common + extra + ["-c", str(s), "-o", str(o)])
+            if ring:
+                audit_srcs.append((len(jobs) - 1, s.name))
     bo = objdir / "bindings.o"
     objs.append(bo)
     bsrc = kdir / "bindings.cpp"
@@ -100,7 +153,18 @@ def build_kernels(force: bool = False, verbose: bool = False) -> Path:
                      *_py_includes(), "-c", str(bsrc), "-o", str(bo)])
     if jobs:
         with ThreadPoolExecutor(max_workers=min(8, len(jobs))) as ex:
-            list(ex.map(_run, jobs))
+            logs = list(ex.map(_run, jobs))
+        if audit_srcs:
+            import json
+            usage = json.loads(audit_file.read_text()) if audit_file.exists() else {}
+            for i, name in audit_srcs:
+                usage[name] = parse_resource_usage(logs[i])
+            bad = audit_asm_rings(usage)
+            if bad:
+                for i, _ in audit_srcs:
+                    Path(jobs[i][jobs[i].index("-o") + 1]).unlink(missing_ok=True)
+                raise RuntimeError("inline-asm ring kernels spill:\n  " + "\n  ".join(bad))
+            audit_file.write_text(json.dumps(usage, indent=1, sort_keys=True))
     if force or jobs or _stale(out, objs):
         link = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(out),
                 *[str(o) for o in objs]]

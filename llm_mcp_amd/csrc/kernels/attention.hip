@@ -24,6 +24,7 @@
 #include <algorithm>
 #include <climits>
 #include <type_traits>
+#include <utility>
 
 #include "common.h"
 
@@ -170,6 +171,175 @@ __device__ __forceinline__ void load_page(PageFrags<HD>& f, const bf16_t* __rest
   for (int i = 0; i < HD / 16; ++i)
     f.vf[i] = load_frag_2x8B(vpage + vq_off(16 * i + c, 4 * g, HD),
                              vpage + vq_off(16 * i + c, 16 + 4 * g, HD));
+}
+
+template <int HD>
+__device__ __forceinline__ void compute_page(PageState<HD>& st, const bf16x8_t (&qf)[HD / 32],
+                                             const PageFrags<HD>& f, int page_pos0, int lim,
+                                             float scale_log2);
+
+// ---- rolling register ring with hand-counted waits (decode MODE 9) --------
+// A page's K and V^T fragments are issued as inline-asm loads from a
+// wave-uniform SGPR page base + the lane's offset + an immediate, so hipcc
+// neither counts them nor drains them with its own vmcnt(0) at the loop top
+// (why the compiler-scheduled pipelines, modes 1 and 7, never kept the next
+// page in flight: profiles/r4_decode_attention_pmc.md).  Rolling ring, one
+// page of registers: the next page's K loads issue as soon as this page's QK
+// MFMAs have read K, its V loads as soon as PV has read V, so every wave keeps
+// 8-16 KB in flight through the whole loop.  Waits are counted in issue order
+// (K(j) is followed by V(j): vmcnt(VOPS); V(j) by K(j + 1): vmcnt(KOPS)), the
+// discipline of K14's weight ring (rsgemm.hip).
+template <int HD>
+struct RingK { bf16x8_t a[HD / 32], b[HD / 32]; };   // key rows c / 16 + c
+template <int HD>
+struct RingV { bf16x4_t lo[HD / 16], hi[HD / 16]; }; // V^T keys 4g.. / 16 + 4g..
+template <int HD>
+constexpr int ring_kops() { return 2 * (HD / 32); }
+template <int HD>
+constexpr int ring_vops() { return 2 * (HD / 16); }
+
+template <int IMM>
+__device__ __forceinline__ void ring_ld16(bf16x8_t& r, const void* sbase, unsigned voff) {
+  asm volatile("global_load_dwordx4 %0, %1, %2 offset:%3"
+               : "=v"(r) : "v"(voff), "s"(sbase), "i"(IMM) : "memory");
+}
+template <int IMM>
+__device__ __forceinline__ void ring_ld8(bf16x4_t& r, const void* sbase, unsigned voff) {
+  asm volatile("global_load_dwordx2 %0, %1, %2 offset:%3"
+               : "=v"(r) : "v"(voff), "s"(sbase), "i"(IMM) : "memory");
+}
+
+// lane offsets (bytes) inside a K page [BS][HD] and a key-quad V page
+// [BS/4][HD][4]: K rows c and 16 + c (+ 64 s by immediate); V^T lo = keys
+// 4g.., hi = keys 16 + 4g.. of d = 16 i + c (+ 128 i by immediate)
+struct RingOffs { unsigned ka, kb, vlo, vhi; };
+template <int HD>
+__device__ __forceinline__ RingOffs ring_offs() {
+  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  RingOffs o;
+  o.ka = (unsigned)(c * HD * 2 + 16 * g);
+  o.kb = o.ka + 16 * HD * 2;
+  o.vlo = (unsigned)(g * HD * 8 + 8 * c);
+  o.vhi = o.vlo + 4 * HD * 8;
+  return o;
+}
+
+template <int HD, int... I>
+__device__ __forceinline__ void ring_issue_k(RingK<HD>& f, const void* kp, const RingOffs& o,
+                                             std::integer_sequence<int, I...>) {
+  (ring_ld16<64 * I>(f.a[I], kp, o.ka), ...);
+  (ring_ld16<64 * I>(f.b[I], kp, o.kb), ...);
+}
+template <int HD, int... I>
+__device__ __forceinline__ void ring_issue_v(RingV<HD>& f, const void* vp, const RingOffs& o,
+                                             std::integer_sequence<int, I...>) {
+  (ring_ld8<128 * I>(f.lo[I], vp, o.vlo), ...);
+  (ring_ld8<128 * I>(f.hi[I], vp, o.vhi), ...);
+}
+
+// wait until at most CNT vector-memory ops are outstanding; the fragments are
+// in/out operands so nothing reads them before the wait
+template <int CNT, int HD>
+__device__ __forceinline__ void ring_wait_k(RingK<HD>& f) {
+  if constexpr (HD == 128)
+    asm volatile("s_waitcnt vmcnt(%8)"
+                 : "+v"(f.a[0]), "+v"(f.a[1]), "+v"(f.a[2]), "+v"(f.a[3]), "+v"(f.b[0]),
+                   "+v"(f.b[1]), "+v"(f.b[2]), "+v"(f.b[3])
+                 : "n"(CNT) : "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(%4)"
+                 : "+v"(f.a[0]), "+v"(f.a[1]), "+v"(f.b[0]), "+v"(f.b[1]) : "n"(CNT) : "memory");
+}
+template <int CNT, int HD>
+__device__ __forceinline__ void ring_wait_v(RingV<HD>& f) {
+  if constexpr (HD == 128)
+    asm volatile("s_waitcnt vmcnt(%16)"
+                 : "+v"(f.lo[0]), "+v"(f.lo[1]), "+v"(f.lo[2]), "+v"(f.lo[3]), "+v"(f.lo[4]),
+                   "+v"(f.lo[5]), "+v"(f.lo[6]), "+v"(f.lo[7]), "+v"(f.hi[0]), "+v"(f.hi[1]),
+                   "+v"(f.hi[2]), "+v"(f.hi[3]), "+v"(f.hi[4]), "+v"(f.hi[5]), "+v"(f.hi[6]),
+                   "+v"(f.hi[7])
+                 : "n"(CNT) : "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(%8)"
+                 : "+v"(f.lo[0]), "+v"(f.lo[1]), "+v"(f.lo[2]), "+v"(f.lo[3]), "+v"(f.hi[0]),
+                   "+v"(f.hi[1]), "+v"(f.hi[2]), "+v"(f.hi[3])
+                 : "n"(CNT) : "memory");
+}
+
+template <int CNT>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(CNT) : "memory");
+}
+
+// the ring refill overwrites registers MFMAs just read; hipcc pads no hazard
+// for an asm instruction (rsgemm.hip rs_mfma_war_pad)
+__device__ __forceinline__ void ring_war_pad() {
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
+}
+
+__device__ __forceinline__ f32x4_t mfma16k16(bf16x4_t a, bf16x4_t b, f32x4_t c) {
+  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
+}
+
+// S^T of one page from the K slot
+template <int HD>
+__device__ __forceinline__ void ring_qk(const RingK<HD>& k, const bf16x8_t (&qf)[HD / 32],
+                                        f32x4_t& s0, f32x4_t& s1) {
+  s0 = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  s1 = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < HD / 32; ++s) {
+    s0 = mfma16(k.a[s], qf[s], s0);
+    s1 = mfma16(k.b[s], qf[s], s1);
+  }
+}
+
+// masked, scaled scores of one page.  The empty asm pins their computation
+// (VALU reads of the QK MFMA results, which wait for the MFMAs to finish)
+// before the K slot refill that follows in program order.
+template <int HD>
+__device__ __forceinline__ void ring_scores(f32x4_t s0, f32x4_t s1, int page_pos0, int lim,
+                                            float scale_log2, float (&x)[8]) {
+  const int g = (threadIdx.x & 63) >> 4;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int k0 = page_pos0 + 4 * g + k, k1 = k0 + 16;
+    x[k] = (k0 <= lim) ? s0[k] * scale_log2 : -INFINITY;
+    x[4 + k] = (k1 <= lim) ? s1[k] * scale_log2 : -INFINITY;
+  }
+  asm volatile("" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]),
+                    "+v"(x[6]), "+v"(x[7]));
+}
+
+// online softmax + PV from the V slot.  The V^T halves stay in their own
+// 2-VGPR load destinations (a 4-VGPR reassembly would be copies of registers
+// whose data may not have landed), so PV runs as two 16x16x16 MFMAs per 16-row
+// d block: keys 4g.. against P's first four values, 16 + 4g.. the last four.
+template <int HD>
+__device__ __forceinline__ void ring_pv(PageState<HD>& st, const RingV<HD>& v,
+                                        const float (&x)[8]) {
+  float mx = x[0];
+#pragma unroll
+  for (int j = 1; j < 8; ++j) mx = fmaxf(mx, x[j]);
+  mx = col4_max(mx);
+  const float m_new = fmaxf(st.m, mx);
+  const float m_use = (m_new == -INFINITY) ? 0.f : m_new;
+  const float alpha = fast_exp2(st.m - m_use);
+  float p[8], rs = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { p[j] = fast_exp2(x[j] - m_use); rs += p[j]; }
+  rs = col4_sum(rs);
+  st.l = st.l * alpha + rs;
+  st.m = m_new;
+  bf16x4_t plo, phi;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { plo[j] = (short)f2bf(p[j]); phi[j] = (short)f2bf(p[4 + j]); }
+#pragma unroll
+  for (int i = 0; i < HD / 16; ++i) {
+    st.acc[i] *= alpha;
+    st.acc[i] = mfma16k16(v.lo[i], plo, st.acc[i]);
+    st.acc[i] = mfma16k16(v.hi[i], phi, st.acc[i]);
+  }
 }
 
 template <int HD>
@@ -337,6 +507,7 @@ __device__ __forceinline__ void decode_segment(
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int t0 = p * part_tokens, t1 = min(t0 + part_tokens, ctx);
   constexpr bool kOnePage = MODE == 0 || MODE == 5 || MODE == 6;
+  constexpr bool kRing = MODE == 9;
 
   bf16x8_t qf[HD / 32];
   const bf16_t* qrow = q + (long)b * q_stride + (long)(kvh * G + c) * HD;
@@ -359,7 +530,9 @@ __device__ __forceinline__ void decode_segment(
       const bf16_t* krow = q + (long)b * q_stride + (long)(Hq + kvh) * HD;
       rope_write_kv<HD>(krow, krow + (long)Hkv * HD, cs, rp.slots[b], kvh, Hkv,
                         const_cast<bf16_t*>(k_cache), const_cast<bf16_t*>(v_cache));
-      if constexpr (!kOnePage) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // the ring retires the stores by count just before it issues the page
+      // that holds the slot
+      if constexpr (!kOnePage && !kRing) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
   }
 
@@ -367,7 +540,69 @@ __device__ __forceinline__ void decode_segment(
   state_init(st);
   const float scale_log2 = scale * LOG2E;
   const int* bt = block_tables + (long)b * bt_stride;
-  if constexpr (kOnePage) {
+  if constexpr (kRing) {
+    // pages of this wave: j-th = pg0 + wave + 4 j.  Block ids by readlane from
+    // one VGPR holding the wave's ids (lane j: its j-th page, 8192 tokens of
+    // context); its compiler-counted load is consumed before the first ring
+    // load issues (a later one would make hipcc drain the ring)
+    const int wpg = pg0 + wave + 4 * lane;
+    const int btv = wpg < pg1 ? bt[wpg] : 0;
+    auto blk_of = [&](int j) -> long {
+      if (j < 64) return __builtin_amdgcn_readlane(btv, j);
+      return bt[pg0 + wave + 4 * j];
+    };
+    const int npg = pg1 - pg0;
+    const int nw = npg > wave ? (npg - wave + 3) / 4 : 0;
+    const RingOffs ro = ring_offs<HD>();
+    auto page_k = [&](int j) -> const void* {
+      return k_cache + (blk_of(j) * Hkv + kvh) * (BS * HD);
+    };
+    auto page_v = [&](int j) -> const void* {
+      return v_cache + (blk_of(j) * Hkv + kvh) * (BS * HD);
+    };
+    constexpr int KOPS = ring_kops<HD>(), VOPS = ring_vops<HD>();
+    // Every compiler-counted load used below is consumed before the first
+    // ring load issues (hipcc would wait for it with vmcnt(0) inside the loop).
+#pragma unroll
+    for (int s = 0; s < HD / 32; ++s) asm volatile("" : "+v"(qf[s]));
+    const int lim = t1 - 1;
+    auto pos_of = [&](int j) { return (pg0 + wave + 4 * j) * BS; };
+    // The writer's last page (j = nw - 1) holds the slot: before its K loads
+    // issue, every op but the V loads of the page before it retires (the
+    // stores are older than every ring load).
+    RingK<HD> rk;
+    RingV<HD> rv;
+    f32x4_t s0, s1;
+    float x[8];
+    if (nw > 0) {
+      if (writer && nw == 1) vm_wait<0>();
+      ring_issue_k<HD>(rk, page_k(0), ro, std::make_integer_sequence<int, HD / 32>{});
+      ring_issue_v<HD>(rv, page_v(0), ro, std::make_integer_sequence<int, HD / 16>{});
+    }
+    // steady state: one exit, the same waits every iteration (no branch merges
+    // two asm-defined copies of a slot; hipcc would place that phi's copies
+    // before the wait)
+    int j = 0;
+    for (; j + 1 < nw; ++j) {
+      ring_wait_k<VOPS>(rk);
+      ring_qk<HD>(rk, qf, s0, s1);
+      ring_scores<HD>(s0, s1, pos_of(j), lim, scale_log2, x);
+      ring_war_pad();
+      if (writer && j + 1 == nw - 1) vm_wait<VOPS>();
+      ring_issue_k<HD>(rk, page_k(j + 1), ro, std::make_integer_sequence<int, HD / 32>{});
+      ring_wait_v<KOPS>(rv);
+      ring_pv<HD>(st, rv, x);
+      ring_war_pad();
+      ring_issue_v<HD>(rv, page_v(j + 1), ro, std::make_integer_sequence<int, HD / 16>{});
+    }
+    if (nw > 0) {
+      ring_wait_k<VOPS>(rk);
+      ring_qk<HD>(rk, qf, s0, s1);
+      ring_scores<HD>(s0, s1, pos_of(j), lim, scale_log2, x);
+      ring_wait_v<0>(rv);
+      ring_pv<HD>(st, rv, x);
+    }
+  } else if constexpr (kOnePage) {
     int btv = 0;
     if constexpr (MODE != 6) btv = pg0 + lane < pg1 ? bt[pg0 + lane] : 0;
     auto blk_of = [&](int pg) -> long {
@@ -497,8 +732,8 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
 // longest-first order with a grid stride, so no workgroup launches ragged
 // rounds behind the first and the per-workgroup start-up is paid once per
 // resident slot.
-template <int HD, int MODE>
-__global__ void __launch_bounds__(256, 3) paged_decode_persist_kernel(
+template <int HD, int MODE, int OCC = 3>
+__global__ void __launch_bounds__(256, OCC) paged_decode_persist_kernel(
     const bf16_t* __restrict__ q, long q_stride, const bf16_t* __restrict__ k_cache,
     const bf16_t* __restrict__ v_cache, const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ context_lens, const int* __restrict__ order,
@@ -545,18 +780,18 @@ __global__ void __launch_bounds__(128) paged_decode_reduce_kernel(
 static int g_decode_mode = 0;
 void set_decode_mode(int mode) { g_decode_mode = mode; }
 
-// resident 256-thread decode workgroups: 3 per CU (168 VGPRs incl. AGPRs)
-static int decode_resident_wgs() {
-  static int n = 0;
-  if (n == 0) {
-    int dev = 0, cus = 0;
+// resident 256-thread decode workgroups: occ per CU (3: 168 VGPRs incl. AGPRs)
+static int decode_resident_wgs(int occ = 3) {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0, n = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        cus <= 0)
-      cus = 256;
-    n = 3 * cus;
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        n <= 0)
+      n = 256;
+    cus = n;
   }
-  return n;
+  return occ * cus;
 }
 
 int paged_decode(const void* q, long q_stride, const void* k_cache, const void* v_cache,
@@ -584,8 +819,17 @@ int paged_decode(const void* q, long q_stride, const void* k_cache, const void* 
       (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, \
       bt_stride, context_lens, order, (bf16_t*)out, out_stride, B, Hq, Hkv, scale, part_tokens, \
       rp);
+#define LMX_DEC_R(HDV, OCC)                                                                   \
+  paged_decode_persist_kernel<HDV, 9, OCC>                                                    \
+      <<<dim3(std::min(B * Hkv, decode_resident_wgs(OCC))), dim3(256), 0, stream>>>(          \
+      (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, \
+      bt_stride, context_lens, order, (bf16_t*)out, out_stride, B, Hq, Hkv, scale, part_tokens, \
+      rp);
 #define LMX_DEC(HDV)                                                                          \
-  if (g_decode_mode == 0 && max_parts == 1) { LMX_DEC_P(HDV, 0) }                             \
+  if (g_decode_mode == 9 && max_parts == 1) { LMX_DEC_R(HDV, 2) }                             \
+  else if (g_decode_mode == 10 && max_parts == 1) { LMX_DEC_R(HDV, 3) }                       \
+  else if ((g_decode_mode == 9 || g_decode_mode == 10)) { LMX_DEC_K(HDV, 9) }                 \
+  else if (g_decode_mode == 0 && max_parts == 1) { LMX_DEC_P(HDV, 0) }                        \
   else if (g_decode_mode == 5 && max_parts == 1) { LMX_DEC_P(HDV, 5) }                        \
   else if (g_decode_mode == 6 && max_parts == 1) { LMX_DEC_P(HDV, 6) }                        \
   else if (g_decode_mode == 6) { LMX_DEC_K(HDV, 6) }                                          \
@@ -601,6 +845,7 @@ int paged_decode(const void* q, long q_stride, const void* k_cache, const void* 
 #undef LMX_DEC
 #undef LMX_DEC_K
 #undef LMX_DEC_P
+#undef LMX_DEC_R
   return (int)hipGetLastError();
 }
 

@@ -440,10 +440,15 @@ int rsgemm(void* C, const void* A, const void* W, float* slabs, unsigned* ticket
                                                        ldw, ldc, splits, stream);               \
   return rs_launch<0, D, NA, NT, RM, BM>(C_, A_, W_, slabs, tickets, M, N, K, lda, ldw, ldc,     \
                                          splits, stream);
+  // all-rows tiles (BM 256) are built for the partials epilogue only: the
+  // bf16 and SwiGLU epilogues spill there (a spilled ring register is silent
+  // corruption; build.py audits every instantiation) and no table entry uses them
 #define LMX_RS_B(D, NA, NT, RM)                 \
   if (bm == 64) { LMX_RS_E(D, NA, NT, RM, 64) } \
   if (bm == 128) { LMX_RS_E(D, NA, NT, RM, 128) } \
-  LMX_RS_E(D, NA, NT, RM, 256)
+  if (epi != 2) return -1;                      \
+  return rs_launch<2, D, NA, NT, RM, 256>(C_, A_, W_, slabs, tickets, M, N, K, lda, ldw, ldc, \
+                                          splits, stream);
 #define LMX_RS(D, NA)                                  \
   if (nt && rm) { LMX_RS_B(D, NA, 1, 1) }              \
   if (nt) { LMX_RS_B(D, NA, 1, 0) }                    \

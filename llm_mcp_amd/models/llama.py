@@ -209,12 +209,11 @@ class LlamaModel:
                     L["w_gate_up"] = ops.interleave_gate_up(L["w_gate_up"], blk)
                 self.gu_block = blk
             # K14 decode shapes the table runs on packed weights get their
-            # packed copies now (row-major entries need nothing)
-            for L in self.w["layers"]:
-                for k in ("wqkv", "wo", "w_gate_up", "w_down"):
-                    if k in L:
-                        ops.rs_prepare(L[k])
-            ops.rs_prepare(self.w["lm_head"])
+            # packed copies now, all or nothing per shape (row-major entries
+            # need nothing)
+            ops.rs_prepare_all([L[k] for L in self.w["layers"]
+                                for k in ("wqkv", "wo", "w_gate_up", "w_down") if k in L]
+                               + [self.w["lm_head"]])
 
     # ----------------------------------------------------------- weights ----
     def _random_weights(self, seed: int) -> dict:

@@ -1042,12 +1042,16 @@ def _rs_table() -> dict:
     return _RS_TABLE
 
 
-def rsgemm_supported(M: int, N: int, K: int, cfg: int, splits: int) -> bool:
+def rsgemm_supported(M: int, N: int, K: int, cfg: int, splits: int, epi: int = 0) -> bool:
     """Shapes K14 takes: <= 256 rows, 256-column tiles, a K slice that is a
-    whole number of the configuration's ring blocks."""
+    whole number of the configuration's ring blocks; all-rows tiles (no 64 /
+    128-row bit) only with the partials epilogue (the others spill there and
+    are not built: rsgemm.hip, build.py ASM_RING_KERNELS)."""
     u = RS_U.get(cfg & 3)
     if u is None or not (0 < M <= 256 and N % RS_BN == 0 and splits in (1, 2, 4, 8, 16)
                          and K % (64 * splits) == 0):
+        return False
+    if not (cfg & (RS_BM64 | RS_BM128)) and epi != 2:
         return False
     nk = K // splits // 64
     return nk >= u and nk % u == 0
@@ -1058,7 +1062,7 @@ def rs_choice(M: int, N: int, K: int, epi: int = 0,
     """(cfg, splits) of K14 for this decode GEMM, or None.  An entry on packed
     weights applies only when ``w`` has its packed copy (rs_prepare)."""
     for m_min, m_max, cfg, s in _rs_table().get((N, K, epi), ()):
-        if (m_min <= M <= m_max and rsgemm_supported(M, N, K, cfg, s)
+        if (m_min <= M <= m_max and rsgemm_supported(M, N, K, cfg, s, epi)
                 and (epi != 2 or s in (1, 2, 4, 8, 16))):     # rmsnorm_slabs' S
             if not (cfg & RS_ROWMAJOR) and _rs_packed_of(w) is None:
                 continue
@@ -1098,33 +1102,64 @@ def _rs_packed_of(w: torch.Tensor | None) -> torch.Tensor | None:
     return getattr(w, "_lmx_rs_packed", None) if w is not None else None
 
 
-def rs_prepare(w: torch.Tensor) -> bool:
-    """Called once per decode weight at model load: when the K14 table runs
-    this weight's shape on PACKED weights (an entry whose cfg lacks
-    RS_ROWMAJOR), build the packed copy (rsgemm_pack) and attach it to the
-    weight tensor, where ``rs_choice`` / ``rsgemm`` find it.  Returns True if
-    the weight has a packed copy."""
+def _rs_wants_packed(w: torch.Tensor) -> bool:
     if not w.is_cuda or w.dim() != 2:
         return False
-    if _rs_packed_of(w) is not None:
-        return True
     N, K = w.shape
-    wants = any(not (cfg & RS_ROWMAJOR) for ep in (0, 2, 3)
-                for _, _, cfg, _ in _rs_table().get((N, K, ep), ()))
-    if not wants or N % RS_BN or K % 32:
+    if N % RS_BN or K % 32:
         return False
-    # the packed copies sit beside the row-major weights (prefill reads
-    # those): bounded by LMX_RS_PACK_GB so a model that fills the GPU
-    # (Llama-3-70B at TP=1) keeps its KV-cache room
-    import os
+    return any(not (cfg & RS_ROWMAJOR) for ep in (0, 2, 3)
+               for _, _, cfg, _ in _rs_table().get((N, K, ep), ()))
+
+
+def _rs_attach_packed(w: torch.Tensor) -> None:
     import weakref
     nbytes = w.numel() * w.element_size()
-    if _RS_PACKED_BYTES[0] + nbytes > float(os.environ.get("LMX_RS_PACK_GB", "24")) * (1 << 30):
-        return False
     w._lmx_rs_packed = rsgemm_pack(w)
     _RS_PACKED_BYTES[0] += nbytes
     weakref.finalize(w, _rs_unpacked, nbytes)
-    return True
+
+
+def rs_prepare(w: torch.Tensor) -> bool:
+    """One weight alone (tests, single layers): ``rs_prepare_all([w])``."""
+    return bool(rs_prepare_all([w]).get(tuple(w.shape), False))
+
+
+def rs_prepare_all(weights: list, budget_gb: float | None = None) -> dict:
+    """Called once at model load with every decode weight: when the K14 table
+    runs a weight shape on PACKED weights (an entry whose cfg lacks
+    RS_ROWMAJOR), build the packed copies (rsgemm_pack) and attach them to the
+    weight tensors, where ``rs_choice`` / ``rsgemm`` find them.
+
+    The copies sit beside the row-major weights prefill reads, so they are
+    bounded by ``LMX_RS_PACK_GB`` (default 24) -- decided per SHAPE, all or
+    nothing: the bytes of every weight of a shape are summed and the shape is
+    packed only if all of them fit (a running per-weight test would pack the
+    first layers of a big model and leave the rest on another kernel, taking
+    HBM from the KV cache for a mixed setup).  Returns {(N, K): packed}."""
+    import logging
+    import os
+    if budget_gb is None:
+        budget_gb = float(os.environ.get("LMX_RS_PACK_GB", "24"))
+    budget = budget_gb * (1 << 30)
+    groups: dict = {}
+    for w in weights:
+        if w is None or not _rs_wants_packed(w):
+            continue
+        groups.setdefault(tuple(w.shape), []).append(w)
+    out = {}
+    for shape, ws in groups.items():
+        todo = [w for w in ws if _rs_packed_of(w) is None]
+        need = sum(w.numel() * w.element_size() for w in todo)
+        ok = _RS_PACKED_BYTES[0] + need <= budget
+        if ok:
+            for w in todo:
+                _rs_attach_packed(w)
+        out[shape] = ok
+        logging.getLogger("lmx.ops").info(
+            "K14 packed weights %s: %d tensors, %.2f GB -> %s (LMX_RS_PACK_GB=%g)", shape,
+            len(ws), need / 2**30, "packed" if ok else "row-major (over budget)", budget_gb)
+    return out
 
 
 def _rs_unpacked(nbytes: int) -> None:
@@ -1158,7 +1193,7 @@ def rsgemm(a: torch.Tensor, w: torch.Tensor, cfg: int, splits: int, epi: int = 0
         if wp is not None:
             w, packed = wp, True
     cfg = (cfg & ~RS_ROWMAJOR) | (0 if packed else RS_ROWMAJOR)
-    _chk(rsgemm_supported(M, N, K, cfg, splits), f"rsgemm shape M={M} N={N} K={K} "
+    _chk(rsgemm_supported(M, N, K, cfg, splits, epi), f"rsgemm shape M={M} N={N} K={K} "
                                                  f"cfg={cfg} S={splits}")
     if not a.is_cuda:
         _chk(not packed, "rsgemm: the CPU reference takes row-major weights")

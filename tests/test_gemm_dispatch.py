@@ -63,24 +63,28 @@ def test_rsgemm_shape_rules_and_cpu_reference(monkeypatch, tmp_path):
     import torch
     from llm_mcp_amd import ops
     # ring blocks: D4 (cfg 2) takes K slices of 2 K64 steps, D6 (cfg 0) of 3
-    assert ops.rsgemm_supported(256, 28672, 4096, 2, 2)
-    assert not ops.rsgemm_supported(256, 28672, 4096, 0, 2)        # 32 K64 steps % 3
-    assert ops.rsgemm_supported(256, 4096, 14336, 2 | 32, 16)      # 14 K64 steps
-    assert not ops.rsgemm_supported(257, 4096, 4096, 2, 1)
-    assert not ops.rsgemm_supported(256, 4000, 4096, 2, 1)
+    assert ops.rsgemm_supported(256, 28672, 4096, 2 | 4, 2)
+    assert not ops.rsgemm_supported(256, 28672, 4096, 0 | 4, 2)    # 32 K64 steps % 3
+    assert ops.rsgemm_supported(256, 4096, 14336, 2 | 32, 16, 2)   # 14 K64 steps
+    assert not ops.rsgemm_supported(257, 4096, 4096, 2 | 4, 1)
+    assert not ops.rsgemm_supported(256, 4000, 4096, 2 | 4, 1)
+    # all-rows tiles: the partials epilogue only (bf16 / SwiGLU spill there, not built)
+    assert not ops.rsgemm_supported(256, 28672, 4096, 2, 2)
+    assert not ops.rsgemm_supported(256, 28672, 4096, 2, 2, 3)
+    assert ops.rsgemm_supported(256, 28672, 4096, 2, 2, 2)
     table = {"entries": [], "rs": [{"N": 28672, "K": 4096, "epi": 3, "m_min": 129,
-                                    "m_max": 256, "cfg": 98, "splits": 2},
+                                    "m_max": 256, "cfg": 102, "splits": 2},
                                    {"N": 4096, "K": 4096, "epi": 2, "m_min": 129,
-                                    "m_max": 256, "cfg": 98, "splits": 16},
+                                    "m_max": 256, "cfg": 102, "splits": 16},
                                    {"N": 4096, "K": 14336, "epi": 2, "m_min": 129,
                                     "m_max": 256, "cfg": 38, "splits": 8}]}
     p = tmp_path / "t.json"
     p.write_text(json.dumps(table))
     monkeypatch.setenv("LMX_DGEMM_TABLE", str(p))
     monkeypatch.setattr(ops, "_RS_TABLE", None)
-    assert ops.rs_choice(256, 28672, 4096, 3) == (98, 2)           # row-major entry
+    assert ops.rs_choice(256, 28672, 4096, 3) == (102, 2)           # row-major entry
     assert ops.rs_choice(128, 28672, 4096, 3) is None
-    assert ops.rs_choice(200, 4096, 4096, 2) == (98, 16)
+    assert ops.rs_choice(200, 4096, 4096, 2) == (102, 16)
     assert ops.rs_choice(200, 4096, 4096, 0) is None
     # a packed-weight entry applies only to a weight rs_prepare packed
     assert ops.rs_choice(256, 4096, 14336, 2) is None
@@ -91,11 +95,11 @@ def test_rsgemm_shape_rules_and_cpu_reference(monkeypatch, tmp_path):
     a = torch.randn(5, 2048).to(torch.bfloat16)
     w = (torch.randn(512, 2048) * 0.02).to(torch.bfloat16)
     y = a.float() @ w.float().t()
-    torch.testing.assert_close(ops.rsgemm(a, w, 2, 2).float(), y, atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(ops.rsgemm(a, w, 2 | 4, 2).float(), y, atol=2e-2, rtol=2e-2)
     part = ops.rsgemm(a, w, 2, 4, epi=2)
     assert part.slabs.shape == (4, 5, 512)
     torch.testing.assert_close(part.slabs.sum(0), y, atol=1e-3, rtol=1e-3)
-    g = ops.rsgemm(a, w, 2, 1, epi=3)
+    g = ops.rsgemm(a, w, 2 | 4, 1, epi=3)
     yy = y.view(5, 16, 2, 16)
     torch.testing.assert_close(g.float(), (torch.nn.functional.silu(yy[:, :, 0]) * yy[:, :, 1])
                                .reshape(5, 256), atol=2e-2, rtol=2e-2)
@@ -119,3 +123,30 @@ def test_pgemm_residual_cpu_reference_and_gate(monkeypatch):
     assert not ops.residual_gemm_ok(a, w, None)
     monkeypatch.setattr(ops, "RESIDUAL_EPILOGUE", False)
     assert not ops.residual_gemm_ok(a, w, r)
+
+
+def test_rs_prepare_all_packs_whole_shapes_or_none(monkeypatch):
+    import torch
+    """ADVICE r4: the K14 packed-copy budget (LMX_RS_PACK_GB) is decided per
+    weight SHAPE, all or nothing -- never the first layers of a shape packed and
+    the rest left row-major."""
+    packed = []
+
+    def attach(w):
+        w._lmx_rs_packed = w
+        ops._RS_PACKED_BYTES[0] += w.numel() * w.element_size()
+        packed.append(w)
+
+    monkeypatch.setattr(ops, "_rs_wants_packed", lambda w: True)
+    monkeypatch.setattr(ops, "_rs_attach_packed", attach)
+    monkeypatch.setattr(ops, "_RS_PACKED_BYTES", [0])
+    mib = 1 << 20
+    small = [torch.empty(256, 1024, dtype=torch.bfloat16) for _ in range(4)]      # 0.5 MiB each
+    big = [torch.empty(1024, 1024, dtype=torch.bfloat16) for _ in range(4)]       # 2 MiB each
+    other = [torch.empty(512, 1024, dtype=torch.bfloat16) for _ in range(2)]      # 1 MiB each
+    layers = [t for trio in zip(small, big) for t in trio] + other
+    res = ops.rs_prepare_all(layers, budget_gb=5 * mib / 2**30)
+    assert res == {(256, 1024): True, (1024, 1024): False, (512, 1024): True}
+    assert all(ops._rs_packed_of(w) is not None for w in small + other)
+    assert all(ops._rs_packed_of(w) is None for w in big)          # 8 MiB: none of them
+    assert ops._RS_PACKED_BYTES[0] == 4 * mib

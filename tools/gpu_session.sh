@@ -150,6 +150,19 @@ for step in "$@"; do
       rm -rf gpurun_out/$tag ;;   # the trace database alone exceeds what gpurun copies back
     attn_probe)
       run attn_probe 180 python -u tools/decode_attn_probe.py || exit $? ;;
+    attn_tests)
+      run attn_tests 300 python -u -m pytest tests/test_kernels_gpu.py -k paged_decode -x -q \
+          --timeout 120 --timeout-method thread -p no:cacheprovider || exit $? ;;
+    attn_ring)
+      # the rolling register ring (modes 9/10) against the default loop, headline and 70B shapes
+      : > gpurun_out/attn_ring.log
+      for args in "--layout engine --rope --modes ${ATTN_MODES:-0,10,9,0,10,9}" \
+                  "--layout random --modes ${ATTN_MODES:-0,10,0,10}" \
+                  "--layout engine --rope --hq 64 --batch 128 --ctx-lo 512 --ctx-hi 640 --modes ${ATTN_MODES:-0,10,0,10}"; do
+        timeout -k 10 150 python -u tools/decode_attn_probe.py $args --iters 40 \
+            >> gpurun_out/attn_ring.log 2>&1 || exit $?
+      done
+      cat gpurun_out/attn_ring.log ;;
     attn_layout)
       # kv-head-major cache emulation (each segment one contiguous page run) vs the
       # block-major cache, contiguous and random page placement, default loop form
