@@ -67,18 +67,26 @@ def parse(argv=None):
     ap.add_argument("--max-tokens", type=int, default=256)
     ap.add_argument("--temperature", type=float, default=0.8)
     ap.add_argument("--top-p", type=float, default=0.95)
-    ap.add_argument("--max-batched-tokens", type=int, default=24576)
+    ap.add_argument("--max-batched-tokens", type=int, default=None,
+                    help="tokens per engine step (default: the engine's, LMX_MAX_BATCHED_TOKENS)")
+    ap.add_argument("--mixed-prefill-tokens", type=int, default=None,
+                    help="prompt tokens per mixed step (default: the engine's, "
+                         "LMX_MIXED_PREFILL_TOKENS; 0 = no cap)")
     ap.add_argument("--api-procs", type=int, default=0,
                     help="front-door API processes on the shared port (0: two per engine, "
                          "at most 16)")
     ap.add_argument("--loadgen-procs", type=int, default=0,
                     help="load-generator processes (0: two per engine, at most 16)")
     ap.add_argument("--no-graphs", action="store_true")
-    ap.add_argument("--load", choices=("waves", "closed"), default="waves",
-                    help="waves (the headline: K synchronized waves of C streams per GPU) or "
+    ap.add_argument("--load", choices=("waves", "closed", "poisson"), default="waves",
+                    help="waves (the headline: K synchronized waves of C streams per GPU), "
                          "closed (C streams per GPU at constant concurrency, each client sending "
                          "its next request when its stream ends, for --duration seconds after "
-                         "--closed-warmup seconds; a separate record, never the headline)")
+                         "--closed-warmup seconds) or poisson (open loop: --rate requests/s per "
+                         "GPU arriving as a Poisson process); the latter two are separate "
+                         "records, never the headline")
+    ap.add_argument("--rate", type=float, default=60.0,
+                    help="--load poisson: arrivals per second per GPU")
     ap.add_argument("--duration", type=float, default=30.0)
     ap.add_argument("--closed-warmup", type=float, default=10.0)
     ap.add_argument("--cpu", action="store_true",
@@ -214,8 +222,10 @@ def main() -> None:
                 tpctx = TPContext(grank, a.tp, tg, cpu_group=cg)
 
     t_init = time.time()
-    ecfg = EngineConfig(model=a.model, max_num_seqs=max(a.concurrency, 1),
-                        max_batched_tokens=a.max_batched_tokens,
+    # the serving defaults `serve` ships (engine.EngineConfig) unless overridden
+    knobs = {k: v for k, v in (("max_batched_tokens", a.max_batched_tokens),
+                               ("mixed_prefill_tokens", a.mixed_prefill_tokens)) if v is not None}
+    ecfg = EngineConfig(model=a.model, max_num_seqs=max(a.concurrency, 1), **knobs,
                         max_model_len=min(8192, a.prompt_len + a.max_tokens + 64),
                         use_graphs=not a.no_graphs, seed=rank,
                         # rehearsal: every rank shares cuda:0's 288 GB
@@ -267,7 +277,8 @@ def main() -> None:
                  "elapsed": max(x["elapsed"] for x in parts),
                  "requests": sum(x["requests"] for x in parts),
                  "ttfts": [t for x in parts for t in x["ttfts"]],
-                 "itls": [t for x in parts for t in x["itls"]]}
+                 "itls": [t for x in parts for t in x["itls"]],
+                 "gaps": [sum(c) for c in zip(*(x["gaps"] for x in parts))]}
             out.append(r)
             from llm_mcp_amd.bench.loadgen import percentile as pct
             log(f"{label} {k}: {r['requests']} streams, {r['tokens']} tok in {r['elapsed']:.2f}s "
@@ -313,11 +324,17 @@ def main() -> None:
         return sum(sum(p.cpu_times()[:2]) for p in ps)
     cpu0 = {k: cpu_s(v) for k, v in procs.items()}
 
-    if a.load == "closed":
-        closed(a, rank, world, n_eng, lgs, barrier, sync)
+    if a.load in ("closed", "poisson"):
+        closed(a, rank, world, n_eng, lgs, barrier, sync, engine.ecfg)
         shutdown(a, world, lgs, apis, server, ready_files, engine, follower)
         return
 
+    # clocks / power / temperature around the timed waves (rank 0, every card
+    # of the node): a slower box is told apart from a regression
+    clocks = {}
+    if rank == 0 and not a.cpu:
+        from llm_mcp_amd.devices.rocm_enum import gpu_clock_snapshot
+        clocks["start"] = gpu_clock_snapshot()
     barrier()
     sync()
     t0 = time.perf_counter()
@@ -326,6 +343,8 @@ def main() -> None:
     sync()
     barrier()
     elapsed = time.perf_counter() - t0
+    if rank == 0 and not a.cpu:
+        clocks["end"] = gpu_clock_snapshot()
 
     cpu = {k: (cpu_s(v) - cpu0[k]) / elapsed * 100 for k, v in procs.items()}
     st = engine.stats
@@ -377,6 +396,9 @@ def main() -> None:
             "ttft_p50_ms": round(percentile(ttfts, 50) * 1e3, 1),
             "ttft_p95_ms": round(percentile(ttfts, 95) * 1e3, 1),
             "itl_p50_ms": round(percentile(itls, 50) * 1e3, 2),
+            "itl_p95_ms": round(percentile(itls, 95) * 1e3, 2),
+            "itl_p99_ms": round(percentile(itls, 99) * 1e3, 2),
+            **gap_percentiles(results),
             "per_gpu_tok_s": per_gpu,
             "gpu_balance_max_over_min": round(max(nz) / min(nz), 3) if nz else None,
             "decode_step_ms": [round(x["decode_ms"], 2) for x in allr],
@@ -385,6 +407,7 @@ def main() -> None:
             "front_door_cpu_pct": round(cpu.get("api", 0.0), 1),
             "loadgen_cpu_pct": round(cpu.get("loadgen", 0.0), 1),
             "engine_cpu_pct": [round(x["engine_cpu_pct"], 1) for x in allr],
+            "gpu_clocks": clocks or None,
             "config": {"model": a.model, "global_batch": a.concurrency * n_eng,
                        "seq_len": a.prompt_len + a.max_tokens, "prompt_len": a.prompt_len,
                        "max_tokens": a.max_tokens,
@@ -399,7 +422,9 @@ def main() -> None:
                        "engine": {"lookahead_stepping": bool(engine.lookahead),
                                   "decode_graph_buckets": len(engine.graphs),
                                   "kv_pages": "K [BS][D] token-major, V [BS/4][D][4] key-quad",
-                                  "max_batched_tokens": a.max_batched_tokens},
+                                  "max_batched_tokens": ecfg.max_batched_tokens,
+                                  "mixed_prefill_tokens": ecfg.mixed_prefill_tokens,
+                                  "mixed_min_decodes": engine.ecfg.mixed_min_decodes},
                        "tp_group": None if a.tp == 1 else {
                            "collectives": "gloo (one-GPU rehearsal)" if (a.rehearse_on_one_gpu or a.cpu)
                            else "nccl (RCCL)",
@@ -452,16 +477,32 @@ def shutdown(a, world, lgs, apis, server, ready_files, engine=None, follower=Non
         dist.destroy_process_group()
 
 
-def closed(a, rank, world, n_eng, lgs, barrier, sync) -> None:
-    """--load closed: one constant-concurrency window through the same front
-    door; prints its own JSON line (metric tagged "closed loop")."""
+def gap_percentiles(parts) -> dict:
+    """Per-token inter-arrival gap p50 / p95 / p99 (ms) from the load
+    generators' merged histograms (bench/loadgen.py GAP_BINS)."""
+    from llm_mcp_amd.bench.loadgen import GAP_BINS, hist_percentile
+    h = [0] * GAP_BINS
+    for x in parts:
+        for i, c in enumerate(x.get("gaps") or ()):
+            h[i] += c
+    return {f"token_gap_p{q}_ms": round(hist_percentile(h, q) * 1e3, 2) for q in (50, 95, 99)}
+
+
+def closed(a, rank, world, n_eng, lgs, barrier, sync, ecfg) -> None:
+    """--load closed / poisson: one steady-load window through the same front
+    door; prints its own JSON line (metric tagged "closed loop" / "poisson")."""
     from llm_mcp_amd.bench.loadgen import percentile
     barrier()
     sync()
     parts = []
     if rank == 0:
         for p in lgs:
-            p.stdin.write(f"closed {a.closed_warmup} {a.duration}\n")
+            if a.load == "poisson":
+                # the engine's rate split over its load generators
+                per = a.rate * n_eng / len(lgs)
+                p.stdin.write(f"open {per} {a.closed_warmup} {a.duration}\n")
+            else:
+                p.stdin.write(f"closed {a.closed_warmup} {a.duration}\n")
             p.stdin.flush()
         for p in lgs:
             parts.append(json.loads(p.stdout.readline()))
@@ -470,18 +511,27 @@ def closed(a, rank, world, n_eng, lgs, barrier, sync) -> None:
         tok = sum(x["tokens"] for x in parts)
         ttfts = [t for x in parts for t in x["ttfts"]]
         itls = [t for x in parts for t in x["itls"]]
-        out = {"metric": METRIC + " [closed loop]", "value": round(tok / a.duration, 1),
+        tag = "closed loop" if a.load == "closed" else "poisson arrivals"
+        load = (f"closed loop: {a.concurrency} streams per GPU, next request on stream end"
+                if a.load == "closed" else
+                f"open loop: Poisson arrivals at {a.rate:g} requests/s per GPU "
+                f"({sum(x.get('arrivals', 0) for x in parts)} arrivals)")
+        out = {"metric": METRIC + f" [{tag}]", "value": round(tok / a.duration, 1),
                "unit": "tokens/s", "n_gpus": world, "duration_s": a.duration,
                "requests": sum(x["requests"] for x in parts), "dtype": "bf16",
                "data": "synthetic prompts, random-init weights",
                "ttft_p50_ms": round(percentile(ttfts, 50) * 1e3, 1),
                "ttft_p95_ms": round(percentile(ttfts, 95) * 1e3, 1),
+               "ttft_p99_ms": round(percentile(ttfts, 99) * 1e3, 1),
                "itl_p50_ms": round(percentile(itls, 50) * 1e3, 2),
                "itl_p95_ms": round(percentile(itls, 95) * 1e3, 2),
+               "itl_p99_ms": round(percentile(itls, 99) * 1e3, 2),
+               **gap_percentiles(parts),
                "config": {"model": a.model, "concurrency": a.concurrency * n_eng,
                           "prompt_len": a.prompt_len, "max_tokens": a.max_tokens,
-                          "load": f"closed loop: {a.concurrency} streams per GPU, next request "
-                                  f"on stream end, {a.closed_warmup:g} s warm-up, "
+                          "max_batched_tokens": ecfg.max_batched_tokens,
+                          "mixed_prefill_tokens": ecfg.mixed_prefill_tokens,
+                          "load": f"{load}, {a.closed_warmup:g} s warm-up, "
                                   f"{a.duration:g} s window",
                           "sampling": {"temperature": a.temperature, "top_p": a.top_p}}}
         if a.rehearse_on_one_gpu:

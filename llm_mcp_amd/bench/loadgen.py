@@ -9,7 +9,8 @@ interpolation.
 Runs standalone (``python -m llm_mcp_amd.bench.loadgen --url ...``) or as the
 client subprocess of bench.py: then it reads one command per line on stdin
 ("run" = one wave, "closed WARMUP_S DURATION_S" = a constant-concurrency
-window, "quit") and answers one JSON line per command on stdout.
+window, "open RATE WARMUP_S DURATION_S" = Poisson arrivals, "quit") and
+answers one JSON line per command on stdout.
 """
 from __future__ import annotations
 
@@ -37,6 +38,32 @@ def percentile(xs: list[float], q: float) -> float:
 
 _ALPHABET = string.ascii_letters + string.digits + "     "
 
+# per-token inter-arrival gaps (SSE content chunk to the next one of the same
+# stream) as a log-spaced histogram: 40 bins per decade from 10 us to 100 s,
+# merged across load generators by summing; the per-request mean ITL hides a
+# long prefill step that stalls every decoding stream once, this does not
+GAP_BINS, GAP_LO, GAP_PER_DEC = 280, 1e-5, 40
+
+
+def gap_bin(g: float) -> int:
+    import math
+    if g <= GAP_LO:
+        return 0
+    return min(GAP_BINS - 1, int(math.log10(g / GAP_LO) * GAP_PER_DEC))
+
+
+def hist_percentile(h: list[int], q: float) -> float:
+    """Upper edge (seconds) of the bin holding the q-th percentile of ``h``."""
+    n = sum(h)
+    if n == 0:
+        return 0.0
+    target, acc = n * q / 100.0, 0
+    for i, c in enumerate(h):
+        acc += c
+        if acc >= target:
+            return GAP_LO * 10 ** ((i + 1) / GAP_PER_DEC)
+    return GAP_LO * 10 ** (GAP_BINS / GAP_PER_DEC)
+
 
 def synthetic_prompt(n_chars: int, rng: random.Random) -> str:
     return "".join(rng.choices(_ALPHABET, k=n_chars))
@@ -53,7 +80,8 @@ def wave_prompts(seed: int, concurrency: int, prompt_len: int) -> list[str]:
     return [synthetic_prompt(prompt_len, rng) for _ in range(concurrency)]
 
 
-async def one_chat(session, url, model, prompt, max_tokens, temperature, top_p, ignore_eos=True):
+async def one_chat(session, url, model, prompt, max_tokens, temperature, top_p, ignore_eos=True,
+                   gaps: list | None = None):
     body = {"model": model, "messages": [{"role": "user", "content": prompt}], "stream": True,
             "max_tokens": max_tokens, "temperature": temperature, "top_p": top_p,
             "ignore_eos": ignore_eos, "stream_options": {"include_usage": True}}
@@ -84,6 +112,8 @@ async def one_chat(session, url, model, prompt, max_tokens, temperature, top_p, 
             now = time.perf_counter()
             if ttft is None:
                 ttft = now - t0
+            elif gaps is not None:
+                gaps[gap_bin(now - last)] += 1
             last = now
             chunks += 1
     t1 = time.perf_counter()
@@ -104,9 +134,11 @@ async def wave(url, model, concurrency, prompt_len, max_tokens, temperature, top
         0.5, lambda: _PROMPTS.setdefault(nxt, wave_prompts(*nxt)))
     own = session is None
     s = session or new_session()
+    gaps = [0] * GAP_BINS
     try:
         t0 = time.perf_counter()
-        res = await asyncio.gather(*[one_chat(s, url, model, p, max_tokens, temperature, top_p)
+        res = await asyncio.gather(*[one_chat(s, url, model, p, max_tokens, temperature, top_p,
+                                              gaps=gaps)
                                      for p in prompts])
         el = time.perf_counter() - t0
     finally:
@@ -116,7 +148,7 @@ async def wave(url, model, concurrency, prompt_len, max_tokens, temperature, top
     tok = sum(r["tokens"] for r in res)
     itl = [r["decode_s"] / (r["tokens"] - 1) for r in res if r["tokens"] > 1]
     return {"elapsed": el, "tokens": tok, "requests": len(res), "ttfts": ttfts, "itls": itl,
-            "ttft_p50": percentile(ttfts, 50), "ttft_p95": percentile(ttfts, 95),
+            "gaps": gaps, "ttft_p50": percentile(ttfts, 50), "ttft_p95": percentile(ttfts, 95),
             "itl_p50": percentile(itl, 50), "tok_s": tok / el if el > 0 else 0.0}
 
 
@@ -133,12 +165,14 @@ async def closed_loop(url, model, concurrency, prompt_len, max_tokens, temperatu
     w0, w1 = t_start + warmup_s, t_start + warmup_s + duration_s
     recs = []
     s = session or new_session()
+    gaps = [0] * GAP_BINS
 
     async def client(k):
         while time.perf_counter() < w1:
             p = synthetic_prompt(prompt_len, rng)
             t0 = time.perf_counter()
-            r = await one_chat(s, url, model, p, max_tokens, temperature, top_p)
+            r = await one_chat(s, url, model, p, max_tokens, temperature, top_p,
+                               gaps=gaps if t0 >= w0 else None)
             r["t0"] = t0
             recs.append(r)
 
@@ -147,6 +181,46 @@ async def closed_loop(url, model, concurrency, prompt_len, max_tokens, temperatu
     finally:
         if session is None:
             await s.close()
+    return _window_summary(recs, w0, w1, duration_s, gaps)
+
+
+async def open_loop(url, model, rate, prompt_len, max_tokens, temperature, top_p, seed,
+                    warmup_s: float, duration_s: float, session=None):
+    """Open loop: requests arrive as a Poisson process of ``rate`` per second
+    (exponential gaps, seeded), each streamed to its end whatever else is in
+    flight, for ``warmup_s`` + ``duration_s`` seconds; the window is summarised
+    as in ``closed_loop``."""
+    rng = random.Random(seed)
+    t_start = time.perf_counter()
+    w0, w1 = t_start + warmup_s, t_start + warmup_s + duration_s
+    recs, tasks = [], []
+    s = session or new_session()
+    gaps = [0] * GAP_BINS
+
+    async def one(p, t0):
+        r = await one_chat(s, url, model, p, max_tokens, temperature, top_p,
+                           gaps=gaps if t0 >= w0 else None)
+        r["t0"] = t0
+        recs.append(r)
+
+    try:
+        t_next = t_start
+        while t_next < w1:
+            now = time.perf_counter()
+            if t_next > now:
+                await asyncio.sleep(t_next - now)
+            tasks.append(asyncio.ensure_future(one(synthetic_prompt(prompt_len, rng), t_next)))
+            t_next += rng.expovariate(rate)
+        await asyncio.gather(*tasks)
+    finally:
+        if session is None:
+            await s.close()
+    out = _window_summary(recs, w0, w1, duration_s, gaps)
+    out["arrivals"] = len(tasks)
+    return out
+
+
+def _window_summary(recs, w0, w1, duration_s, gaps):
     tok = 0.0
     for r in recs:
         a, b = r["t0"] + r["ttft"], r["t0"] + r["latency"]     # token-producing span
@@ -158,9 +232,9 @@ async def closed_loop(url, model, concurrency, prompt_len, max_tokens, temperatu
     ttfts = [r["ttft"] for r in inside]
     itl = [r["decode_s"] / (r["tokens"] - 1) for r in inside if r["tokens"] > 1]
     return {"elapsed": duration_s, "tokens": tok, "requests": len(inside), "ttfts": ttfts,
-            "itls": itl, "ttft_p50": percentile(ttfts, 50), "ttft_p95": percentile(ttfts, 95),
-            "itl_p50": percentile(itl, 50), "itl_p95": percentile(itl, 95),
-            "tok_s": tok / duration_s}
+            "itls": itl, "gaps": gaps, "ttft_p50": percentile(ttfts, 50),
+            "ttft_p95": percentile(ttfts, 95), "itl_p50": percentile(itl, 50),
+            "itl_p95": percentile(itl, 95), "tok_s": tok / duration_s}
 
 
 def new_session() -> aiohttp.ClientSession:
@@ -212,6 +286,13 @@ def main(argv=None):
             cmd = line.strip()
             if cmd == "quit":
                 break
+            if cmd.startswith("open"):
+                _, rate, warm, dur = cmd.split()
+                r = loop.run_until_complete(open_loop(
+                    a.url, a.model, float(rate), a.prompt_len, a.max_tokens, a.temperature,
+                    a.top_p, (a.seed_base << 20) + 777, float(warm), float(dur), session=session))
+                print(json.dumps(r), flush=True)
+                continue
             if cmd.startswith("closed"):
                 _, warm, dur = cmd.split()
                 r = loop.run_until_complete(closed_loop(
@@ -233,6 +314,7 @@ def main(argv=None):
                                          (a.seed_base << 20) + i))
         r.pop("ttfts")
         r.pop("itls")
+        r.pop("gaps")
         print(json.dumps(r), flush=True)
 
 

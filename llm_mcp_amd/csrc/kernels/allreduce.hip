@@ -164,6 +164,159 @@ __global__ void __launch_bounds__(AR_THREADS) allreduce_kernel(
   }
 }
 
+// ------------------------------------------- all-reduce + residual + RMSNorm --
+// One TP sub-layer tail in one kernel: o = sum over ranks of the row-parallel
+// projection's bf16 partial (rank order, fp32, rounded to bf16 -- exactly what
+// allreduce_kernel returns), residual += o (bf16, as rmsnorm_kernel keeps the
+// hidden state), h = rmsnorm(residual) * w.  Replaces the GEMM -> all-reduce ->
+// residual-add RMSNorm triple's last two launches and the o round trip
+// between them; bitwise equal to them.
+//   one-shot: block b owns rows b, b + nb, ...: publishes them, meets its
+//     peers' block b, sums every rank's copy and norms the row;
+//   two-shot: rows are sharded by rank (S = ceil(T / W) rows each); block b
+//     owns shard rows i = b, b + nb, ... of EVERY shard, so the per-block
+//     rendezvous orders each read after the write it needs: publish those
+//     rows -> meet -> sum own shard's rows into the result slot -> meet ->
+//     read every shard's summed rows from their owners and norm them.
+// rmsnorm over one row by the whole block: d8 = cols / 8 <= VPT * AR_THREADS
+template <int VPT>
+__device__ __forceinline__ void ar_norm_row(u16x8* __restrict__ h_row, u16x8* __restrict__ res_row,
+                                            const u16x8* __restrict__ w, const float (&o)[VPT][8],
+                                            int d8, float eps, float* scratch) {
+  const int t = threadIdx.x;
+  float v[VPT][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int c = t + k * AR_THREADS;
+    if (c < d8) {
+      const u16x8 r = res_row[c];
+      u16x8 hb;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        hb.v[j] = f2bf(bf2f(f2bf(o[k][j])) + bf2f(r.v[j]));
+        v[k][j] = bf2f(hb.v[j]);
+        ss += v[k][j] * v[k][j];
+      }
+      res_row[c] = hb;
+    }
+  }
+  ss = block_sum(ss, scratch);
+  const float inv = rsqrtf(ss / (float)(d8 * 8) + eps);
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int c = t + k * AR_THREADS;
+    if (c < d8) {
+      const u16x8 wv = w[c];
+      u16x8 y;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) y.v[j] = f2bf(v[k][j] * inv * bf2f(wv.v[j]));
+      h_row[c] = y;
+    }
+  }
+  __syncthreads();          // scratch reuse by the next row's block_sum
+}
+
+template <int W, int VPT>
+__global__ void __launch_bounds__(AR_THREADS) allreduce_norm_kernel(
+    u16x8* __restrict__ h_out, u16x8* __restrict__ residual, const u16x8* __restrict__ inp,
+    const u16x8* __restrict__ w, int T, int d8, float eps, int rank, ArPeers peers,
+    long slot_bytes, int two_shot, int spin_max) {
+  __shared__ float scratch[16];
+  char* own = peers.p[rank];
+  uint32_t* ctl = reinterpret_cast<uint32_t*>(own + AR_CTL);
+  const uint32_t e = ctl[0] + 1u;
+  const long par_off = AR_DATA + (long)(e & 1u) * 2 * slot_bytes;
+  const int b = blockIdx.x, nb = gridDim.x, t = threadIdx.x;
+  auto in_slot = [&](int q) { return reinterpret_cast<u16x8*>(peers.p[q] + par_off); };
+  auto res_slot = [&](int q) { return reinterpret_cast<u16x8*>(peers.p[q] + par_off + slot_bytes); };
+  auto publish = [&](int row) {
+    u16x8* dst = in_slot(rank) + (long)row * d8;
+    const u16x8* src = inp + (long)row * d8;
+    for (int c = t; c < d8; c += AR_THREADS) dst[c] = src[c];
+  };
+  // fp32 rank-order sum of every rank's copy of one row (this thread's chunks)
+  auto row_sum = [&](int row, float (&o)[VPT][8]) {
+#pragma unroll
+    for (int k = 0; k < VPT; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[k][j] = 0.f;
+#pragma unroll
+    for (int q = 0; q < W; ++q) {
+      const u16x8* src = in_slot(q) + (long)row * d8;
+#pragma unroll
+      for (int k = 0; k < VPT; ++k) {
+        const int c = t + k * AR_THREADS;
+        if (c < d8) {
+          const u16x8 v = src[c];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[k][j] += bf2f(v.v[j]);
+        }
+      }
+    }
+  };
+  float o[VPT][8];
+  if (!two_shot) {
+    for (int row = b; row < T; row += nb) publish(row);
+    ar_barrier<W>(peers, rank, 0, b, e, spin_max);
+    for (int row = b; row < T; row += nb) {
+      row_sum(row, o);
+      ar_norm_row<VPT>(h_out + (long)row * d8, residual + (long)row * d8, w, o, d8, eps,
+                       scratch);
+    }
+  } else {
+    const int S = (T + W - 1) / W;
+#pragma unroll
+    for (int q = 0; q < W; ++q)
+      for (int i = b; i < S && q * S + i < T; i += nb) publish(q * S + i);
+    ar_barrier<W>(peers, rank, 0, b, e, spin_max);
+    for (int i = b; i < S && rank * S + i < T; i += nb) {
+      const int row = rank * S + i;
+      row_sum(row, o);
+      u16x8* dst = res_slot(rank) + (long)row * d8;
+#pragma unroll
+      for (int k = 0; k < VPT; ++k) {
+        const int c = t + k * AR_THREADS;
+        if (c < d8) {
+          u16x8 y;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) y.v[j] = f2bf(o[k][j]);
+          dst[c] = y;
+        }
+      }
+    }
+    ar_barrier<W>(peers, rank, 1, b, e, spin_max);
+#pragma unroll
+    for (int q = 0; q < W; ++q) {
+      for (int i = b; i < S && q * S + i < T; i += nb) {
+        const int row = q * S + i;
+        const u16x8* src = res_slot(q) + (long)row * d8;
+#pragma unroll
+        for (int k = 0; k < VPT; ++k) {
+          const int c = t + k * AR_THREADS;
+          if (c < d8) {
+            const u16x8 v = src[c];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[k][j] = bf2f(v.v[j]);
+          }
+        }
+        ar_norm_row<VPT>(h_out + (long)row * d8, residual + (long)row * d8, w, o, d8, eps,
+                         scratch);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) {
+    const uint32_t old = __hip_atomic_fetch_add(ctl + 1, 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+    if (old == (uint32_t)(nb - 1)) {
+      __hip_atomic_store(ctl + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ctl, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 // ----------------------------------------------------------------- host ----
 long ar_region_bytes(long slot_bytes) { return AR_DATA + 4 * slot_bytes; }
 
@@ -209,6 +362,12 @@ int ar_error(void* own, int clear) {
   return (int)v;
 }
 
+// the error word copied into pinned host memory on the stream (no sync): a
+// step's host code reads the copy a later step left there
+int ar_error_async(void* own, void* host, hipStream_t stream) {
+  return (int)hipMemcpyAsync(host, (char*)own + AR_CTL + 8, 4, hipMemcpyDeviceToHost, stream);
+}
+
 int allreduce(void* out, const void* inp, long nbytes, int rank, int world,
               const unsigned long long* peer_ptrs, long slot_bytes, int two_shot, int blocks,
               int spin_max, hipStream_t stream) {
@@ -237,6 +396,43 @@ int allreduce(void* out, const void* inp, long nbytes, int rank, int world,
     default: LMX_AR(8) break;
   }
 #undef LMX_AR
+  return (int)hipGetLastError();
+}
+
+// fused all-reduce + residual add + RMSNorm of [T, cols] bf16 rows
+int allreduce_norm(void* h_out, void* residual, const void* inp, const void* w, int T, int cols,
+                   float eps, int rank, int world, const unsigned long long* peer_ptrs,
+                   long slot_bytes, int two_shot, int blocks, int spin_max, hipStream_t stream) {
+  if (T <= 0) return 0;
+  if (world < 2 || world > AR_MAX_W || rank < 0 || rank >= world) return -1;
+  if (cols % 8 != 0 || cols > 8 * AR_THREADS * 4) return -2;
+  if ((long)T * cols * 2 > slot_bytes) return -2;
+  if (blocks < 1 || blocks > AR_MAX_BLOCKS) return -4;
+  if (((uintptr_t)h_out | (uintptr_t)residual | (uintptr_t)inp | (uintptr_t)w) % 16 != 0)
+    return -5;
+  if (two_shot < 0 || two_shot > 1) return -7;
+  ArPeers p;
+  for (int q = 0; q < AR_MAX_W; ++q) p.p[q] = q < world ? (char*)peer_ptrs[q] : nullptr;
+  for (int q = 0; q < world; ++q)
+    if (!p.p[q]) return -6;
+  const int d8 = cols / 8;
+  const int vpt = (d8 + AR_THREADS - 1) / AR_THREADS;
+#define LMX_ARN(WV, VV)                                                                        \
+  allreduce_norm_kernel<WV, VV><<<dim3(blocks), dim3(AR_THREADS), 0, stream>>>(                \
+      (u16x8*)h_out, (u16x8*)residual, (const u16x8*)inp, (const u16x8*)w, T, d8, eps, rank, p,  \
+      slot_bytes, two_shot, spin_max);
+#define LMX_ARN_W(WV)                 \
+  if (vpt <= 1) { LMX_ARN(WV, 1) }    \
+  else if (vpt <= 2) { LMX_ARN(WV, 2) } \
+  else { LMX_ARN(WV, 4) }
+  switch (world) {
+    case 2: LMX_ARN_W(2) break;
+    case 4: LMX_ARN_W(4) break;
+    case 8: LMX_ARN_W(8) break;
+    default: return -1;
+  }
+#undef LMX_ARN_W
+#undef LMX_ARN
   return (int)hipGetLastError();
 }
 

@@ -67,6 +67,9 @@ int ar_ipc_open(void**, const void*);
 int ar_ipc_close(void*);
 int ar_ipc_handle_size();
 int ar_error(void*, int);
+int ar_error_async(void*, void*, hipStream_t);
+int allreduce_norm(void*, void*, const void*, const void*, int, int, float, int, int,
+                   const unsigned long long*, long, int, int, int, hipStream_t);
 int allreduce(void*, const void*, long, int, int, const unsigned long long*, long, int, int, int,
               hipStream_t);
 }  // namespace lmx
@@ -258,6 +261,18 @@ PYBIND11_MODULE(_lmx_kernels, m) {
     const int v = lmx::ar_error(P<void>(own), clear);
     if (v < 0) check(-v, "ar_error");
     return v;
+  });
+  m.def("allreduce_norm", [](uptr h_out, uptr residual, uptr inp, uptr w, int T, int cols,
+                             float eps, int rank, int world, std::vector<unsigned long long> peers,
+                             long slot_bytes, int two_shot, int blocks, int spin_max, uptr stream) {
+    if ((int)peers.size() < world) throw std::runtime_error("allreduce_norm: peers < world");
+    check(lmx::allreduce_norm(P<void>(h_out), P<void>(residual), P<void>(inp), P<void>(w), T,
+                              cols, eps, rank, world, peers.data(), slot_bytes, two_shot, blocks,
+                              spin_max, S(stream)),
+          "allreduce_norm");
+  });
+  m.def("ar_error_async", [](uptr own, uptr host, uptr stream) {
+    check(lmx::ar_error_async(P<void>(own), P<void>(host), S(stream)), "ar_error_async");
   });
   m.def("allreduce", [](uptr out, uptr inp, long nbytes, int rank, int world,
                         std::vector<unsigned long long> peers, long slot_bytes, int two_shot,

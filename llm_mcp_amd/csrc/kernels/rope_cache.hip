@@ -136,6 +136,13 @@ __global__ void __launch_bounds__(256) rope_cache_kernel(
 // The per-token kernel's 2-B stores remain for decode rows (one token per
 // page per step, nothing to coalesce).
 constexpr int RT = 32;
+constexpr int RT_VCOLS = 1024;   // V staging columns per LDS pass
+
+// bytes of the tiled kernel's dynamic LDS (the V staging tile)
+static size_t rope_tile_smem(int Hkv, int D) {
+  const int hg = RT_VCOLS / D < Hkv ? RT_VCOLS / D : Hkv;
+  return (size_t)RT * (hg * D + 8) * sizeof(bf16_t);
+}
 
 __global__ void __launch_bounds__(256) rope_cache_tiled_kernel(
     bf16_t* __restrict__ qkv, long qkv_stride, const int* __restrict__ positions,
@@ -143,9 +150,11 @@ __global__ void __launch_bounds__(256) rope_cache_tiled_kernel(
     const int* __restrict__ slot_mapping, bf16_t* __restrict__ k_cache,
     bf16_t* __restrict__ v_cache, int BS, int rotate_k_inplace,
     const bf16_t* __restrict__ q_norm, const bf16_t* __restrict__ k_norm, float eps, int skip_q) {
-  // V staging tile: up to VCOLS columns (HG whole heads) of 32 tokens
-  constexpr int VCOLS = 1024;
-  __shared__ __attribute__((aligned(16))) bf16_t vt[RT * (VCOLS + 8)];
+  // V staging tile (dynamic LDS, sized by the launcher): HG = min(RT_VCOLS / D,
+  // Hkv) whole heads of 32 tokens, rows of HG * D + 8 elements -- a TP rank's
+  // single kv head takes 8.7 KB instead of a fixed 66 KB (more workgroups per
+  // CU; and the 64 KB static limit of older parts is not crossed)
+  extern __shared__ __attribute__((aligned(16))) bf16_t vt[];
   __shared__ int sslot[RT];
   const int t0 = row0 + blockIdx.x * RT;
   const int nt = min(RT, T - t0);
@@ -228,7 +237,7 @@ __global__ void __launch_bounds__(256) rope_cache_tiled_kernel(
   if (!v_cache || !slot_mapping) return;
   // HG heads per LDS pass (all 8 of Llama-3 at D 128): two barriers per pass
   // instead of two per head
-  const int HG = VCOLS / D < Hkv ? VCOLS / D : Hkv;
+  const int HG = RT_VCOLS / D < Hkv ? RT_VCOLS / D : Hkv;
   const int LD = HG * D + 8, chunks = HG * D / 8;
   for (int h0 = 0; h0 < Hkv; h0 += HG) {
     const int hg = Hkv - h0 < HG ? Hkv - h0 : HG;
@@ -300,11 +309,21 @@ int rope_cache(void* qkv, long qkv_stride, const int* positions, const float* co
     else LMX_RC(6);
 #undef LMX_RC
   }
-  if (T > n1)
-    rope_cache_tiled_kernel<<<dim3((T - n1 + RT - 1) / RT), dim3(256), 0, stream>>>(
+  if (T > n1) {
+    const size_t smem = v_cache && slot_mapping ? rope_tile_smem(Hkv, D) : 0;
+    static size_t attr = 0;
+    if (smem > 65536 && smem > attr) {
+      const hipError_t e = hipFuncSetAttribute((const void*)rope_cache_tiled_kernel,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               (int)smem);
+      if (e != hipSuccess) return (int)e;
+      attr = smem;
+    }
+    rope_cache_tiled_kernel<<<dim3((T - n1 + RT - 1) / RT), dim3(256), smem, stream>>>(
         (bf16_t*)qkv, qkv_stride, positions, cos_sin, n1, T, Hq, Hkv, D, slot_mapping,
         (bf16_t*)k_cache, (bf16_t*)v_cache, BS, rotate_k_inplace, (const bf16_t*)q_norm,
         (const bf16_t*)k_norm, eps, skip_q);
+  }
   return (int)hipGetLastError();
 }
 

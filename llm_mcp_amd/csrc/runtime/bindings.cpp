@@ -99,6 +99,8 @@ PYBIND11_MODULE(_lmx_runtime, m) {
            py::arg("temperature") = 1.f, py::arg("top_k") = 0, py::arg("top_p") = 1.f,
            py::arg("seed") = 0)
       .def("abort", &Scheduler::abort)
+      .def("set_mixed_prefill_cap", &Scheduler::set_mixed_prefill_cap, py::arg("tokens"),
+           py::arg("min_decodes"))
       .def("set_penalties", &Scheduler::set_penalties, py::arg("id"), py::arg("repetition"),
            py::arg("presence"), py::arg("frequency"), py::arg("last_n"))
       .def("schedule", [](Scheduler& s, int q_per_tile) {

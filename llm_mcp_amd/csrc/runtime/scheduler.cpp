@@ -1,5 +1,7 @@
 #include "scheduler.h"
 
+#include <climits>
+
 #include <algorithm>
 #include <stdexcept>
 
@@ -140,13 +142,26 @@ const StepPlan& Scheduler::schedule(int q_per_tile) {
   plan_seqs_.clear();
 
   int budget = max_batched_tokens_;
+  // mixed steps: with at least mixed_min_decodes_ decode rows running, the
+  // step's prefill tokens are capped (a long prefill chunk stalls every
+  // decoding stream for the whole step); a step without decodes -- an idle
+  // engine taking a burst -- keeps the full max_batched_tokens
+  int prefill_left = INT_MAX;
+  if (mixed_prefill_cap_ > 0) {
+    int nd = 0;
+    for (Seq* s : running_)
+      nd += ((int)s->tokens.size() - s->num_computed) == 1;
+    if (nd >= mixed_min_decodes_) prefill_left = mixed_prefill_cap_;
+  }
   std::vector<Seq*> decodes, prefills;
   // 1. running sequences, oldest first
   for (size_t i = 0; i < running_.size() && budget > 0;) {
     Seq* s = running_[i];
     const int remaining = (int)s->tokens.size() - s->num_computed;
     if (remaining <= 0) { ++i; continue; }
-    const int n = std::min(remaining, budget);
+    int n = std::min(remaining, budget);
+    if (remaining > 1) n = std::min(n, prefill_left);
+    if (n <= 0) { ++i; continue; }       // prefill capped this step: wait for the next
     bool preempted_self = false;
     while (!bm_.ensure(s->id, s->num_computed + n)) {
       Seq* victim = running_.back();
@@ -156,6 +171,7 @@ const StepPlan& Scheduler::schedule(int q_per_tile) {
     if (preempted_self) break;
     s->scheduled = n;
     budget -= n;
+    if (remaining > 1) prefill_left -= n;
     (n == 1 ? decodes : prefills).push_back(s);
     ++i;
   }
@@ -165,7 +181,9 @@ const StepPlan& Scheduler::schedule(int q_per_tile) {
     if (s->num_computed == 0 && !bm_.has(s->id))
       s->num_computed = bm_.match_prefix(s->id, s->tokens.data(), (int)s->tokens.size());
     const int remaining = (int)s->tokens.size() - s->num_computed;
-    const int n = std::min(remaining, budget);
+    int n = std::min(remaining, budget);
+    if (remaining > 1) n = std::min(n, prefill_left);
+    if (n <= 0) break;
     if (!bm_.ensure(s->id, s->num_computed + n)) {
       // a waiting sequence must not keep the prefix pages it just matched:
       // with every runner preempted, waiting sequences each pinning their
@@ -179,6 +197,7 @@ const StepPlan& Scheduler::schedule(int q_per_tile) {
     running_.push_back(s);
     s->scheduled = n;
     budget -= n;
+    if (remaining > 1) prefill_left -= n;
     (n == 1 ? decodes : prefills).push_back(s);
   }
 

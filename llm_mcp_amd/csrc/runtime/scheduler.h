@@ -130,6 +130,12 @@ class Scheduler {
   // in flight are forgotten, finished objects released
   void discard_lookahead();
 
+  // prefill tokens of a step that also carries >= min_decodes decode rows
+  // (0: no cap beyond max_batched_tokens)
+  void set_mixed_prefill_cap(int tokens, int min_decodes) {
+    mixed_prefill_cap_ = tokens > 0 ? tokens : 0;
+    mixed_min_decodes_ = min_decodes > 0 ? min_decodes : 1;
+  }
   int num_waiting() const { return (int)waiting_.size(); }
   int num_running() const { return (int)running_.size(); }
   bool has_work() const { return !waiting_.empty() || !running_.empty(); }
@@ -145,6 +151,7 @@ class Scheduler {
 
   BlockManager bm_;
   int max_num_seqs_, max_batched_tokens_, max_model_len_, max_blocks_;
+  int mixed_prefill_cap_ = 0, mixed_min_decodes_ = 1;
   std::unordered_map<int64_t, std::unique_ptr<Seq>> seqs_;
   std::deque<Seq*> waiting_;
   std::vector<Seq*> running_;

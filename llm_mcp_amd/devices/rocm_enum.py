@@ -201,6 +201,51 @@ def gpu_telemetry(drm_root: str = "/sys/class/drm") -> dict[int, dict]:
     return out
 
 
+def gpu_clock_snapshot(timeout_s: float = 15.0) -> dict:
+    """Clocks, power and temperature of every card, for benchmark records
+    (two runs of the same commit on two boxes differ by a few percent; the
+    record says whether a box ran slower or the code regressed):
+    {card: {"sclk_mhz", "mclk_mhz", "power_w", "power_cap_w", "temp_c": {...}}}
+    parsed tolerantly from ``rocm-smi --json``; {"error": ...} when unavailable."""
+    exe = shutil.which("rocm-smi") or ("/opt/rocm/bin/rocm-smi"
+                                       if os.path.exists("/opt/rocm/bin/rocm-smi") else None)
+    if exe is None:
+        return {"error": "rocm-smi not found"}
+    try:
+        r = subprocess.run([exe, "--showclocks", "--showpower", "--showmaxpower", "--showtemp",
+                            "--json"], capture_output=True, text=True, timeout=timeout_s)
+        data = json.loads(r.stdout or "{}")
+    except (subprocess.SubprocessError, OSError, ValueError) as ex:
+        return {"error": str(ex)[:200]}
+    return parse_clock_snapshot(data) or {"error": (r.stderr or "no card")[:200]}
+
+
+def parse_clock_snapshot(data: dict) -> dict:
+    def num(v):
+        m = re.search(r"-?\d+(?:\.\d+)?", str(v))
+        return float(m.group(0)) if m else None
+    out = {}
+    for card, kv in data.items():
+        if not isinstance(kv, dict) or not card.lower().startswith("card"):
+            continue
+        rec: dict = {"temp_c": {}}
+        for k, v in kv.items():
+            kl = k.lower()
+            if "sclk" in kl and "clock" in kl:
+                rec["sclk_mhz"] = num(v)
+            elif "mclk" in kl and "clock" in kl:
+                rec["mclk_mhz"] = num(v)
+            elif "power" in kl and "max" in kl:
+                rec["power_cap_w"] = num(v)
+            elif "power" in kl and "(w)" in kl:
+                rec["power_w"] = num(v)
+            elif "temperature" in kl:
+                sensor = re.search(r"sensor ([a-z0-9 ]+)\)", kl)
+                rec["temp_c"][sensor.group(1).strip() if sensor else kl] = num(v)
+        out[card] = rec
+    return out
+
+
 def host_id() -> str:
     return os.environ.get("LMX_NODE_ID") or socket.gethostname()
 

@@ -87,11 +87,28 @@ class TokenEvent:
     finish: str | None  # None while running
 
 
+def _env_int(name: str, default: int) -> int:
+    v = os.environ.get(name, "")
+    return int(v) if v.strip() else default
+
+
 @dataclass
 class EngineConfig:
+    """One set of serving defaults for ``serve`` / ``worker`` and bench.py
+    (environment-overridable, settings.py): a step takes up to
+    max_batched_tokens tokens -- an idle engine takes a whole burst of
+    prompts in few steps -- but a step that also carries at least
+    mixed_min_decodes decode rows takes at most mixed_prefill_tokens prompt
+    tokens, so a long prefill chunk cannot stall the running streams for the
+    length of a 24k-token step."""
     model: str = "llama-3-8b"
     max_num_seqs: int = 256
-    max_batched_tokens: int = 8192
+    max_batched_tokens: int = field(
+        default_factory=lambda: _env_int("LMX_MAX_BATCHED_TOKENS", 24576))
+    mixed_prefill_tokens: int = field(
+        default_factory=lambda: _env_int("LMX_MIXED_PREFILL_TOKENS", 8192))
+    mixed_min_decodes: int = field(
+        default_factory=lambda: _env_int("LMX_MIXED_MIN_DECODES", 32))
     max_model_len: int = 8192
     kv_fraction: float = 0.6        # of free HBM after weights
     kv_cache_gb: float | None = None
@@ -256,6 +273,8 @@ class LLMEngine:
         self.sched = _runtime.Scheduler(self.num_blocks, BLOCK_SIZE, ecfg.max_num_seqs,
                                         ecfg.max_batched_tokens, self.max_model_len,
                                         ecfg.prefix_cache)
+        if ecfg.mixed_prefill_tokens and ecfg.mixed_prefill_tokens < ecfg.max_batched_tokens:
+            self.sched.set_mixed_prefill_cap(ecfg.mixed_prefill_tokens, ecfg.mixed_min_decodes)
         self.max_blocks = math.ceil(self.max_model_len / BLOCK_SIZE)
         self.max_parts = max(1, min(16, math.ceil(self.max_model_len / ecfg.part_tokens)))
         self.decode_ws = ops.DecodeWorkspace(ecfg.max_num_seqs, self.Hq, self.D, self.max_parts,
@@ -323,10 +342,15 @@ class LLMEngine:
         self._la = None                    # the launched step not yet read back
         self._la_end = 0.0                 # when the last launched step was read back
         self._penalized: set[int] = set()  # active requests with penalty windows
-        # a gloo TP group (one-GPU rehearsals, CPU-hosted collectives) cannot be
-        # captured: its host-staged collectives synchronise inside the step
+        # a gloo TP group (one-GPU rehearsals) captures its decode graphs when
+        # every decode collective runs on the peer-memory kernels (all-reduces
+        # and the logits gather within a slot); host-staged gloo collectives
+        # synchronise inside the step and cannot be captured
         host_tp = self.tp.size > 1 and self.tp.group is not None and \
-            torch.distributed.get_backend(self.tp.group) == "gloo"
+            torch.distributed.get_backend(self.tp.group) == "gloo" and \
+            not self.tp.device_collectives_cover(max(self._graph_buckets(), default=1),
+                                                 self.cfg.hidden_size,
+                                                 self.model.vocab_shard)
         if ecfg.use_graphs and self.device.type == "cuda" and not ops.debug_sync() and not host_tp:
             self._capture_graphs()
         self._bucket_list = sorted(self.graphs)
@@ -427,21 +451,18 @@ class LLMEngine:
         self._gstream = torch.cuda.Stream(device=dev)
         self.pen_graphs: dict[int, dict] = {}
         for B in sorted(self._graph_buckets(), reverse=True):
-            self.graphs[B] = self._capture_bucket(B, penalties=False)
+            self.graphs[B] = self._capture_bucket(B)
         torch.cuda.synchronize(dev)
         log.info("captured %d decode graphs in %.1fs", len(self.graphs), time.time() - t0)
 
-    def _capture_bucket(self, B: int, penalties: bool) -> dict:
-        """Capture the decode step of bucket B.  Penalty variants (the penalty
-        kernel ahead of the sampler) are captured lazily, the first time a
-        step of that bucket carries a penalised row, so batches without
-        penalties replay graphs without the extra node."""
+    def _capture_bucket(self, B: int) -> dict:
+        """Capture the decode step of bucket B (forward + sampling)."""
         g, dev, stream = self._gbuf, self.device, self._gstream
-        pmeta = self._pmeta
         inp = StepInputs(g["ids"][:B], g["pos"][:B], g["slots"][:B], B, g["bt"][:B],
                          g["ctx"][:B], g["cu"][:B + 1], g["tiles"], g["rows"][:B], B, B,
                          decode_order=g["order"][:B])
         ws = self._decode_ws(B)
+        out = {}
 
         def run():
             # lookahead rows: input tokens still on the device (previous step's samples)
@@ -449,23 +470,49 @@ class LLMEngine:
             logits = self.model.forward(inp, self.k_caches, self.v_caches, ws,
                                         self.ecfg.part_tokens)
             if self.is_leader or self.sample_all:
-                if penalties:
-                    pd = pmeta.d
-                    ops.apply_penalties(logits, pd["win"][:B], pd["ngen"][:B], pd["pen"][:B])
                 ops.sample(logits, g["temp"][:B], g["topk"][:B], g["topp"][:B],
                            g["seeds"][:B], g["offs"][:B], g["tok"][:B], g["lp"][:B])
+            out["logits"] = logits
 
+        if self.tp.size > 1:
+            # every rank enters a bucket's warm-up together: its collectives
+            # (peer kernels with bounded waits, or RCCL) pair up across ranks
+            from ..parallel.peer_allreduce import _cpu_group
+            torch.distributed.barrier(group=self.tp.cpu_group or _cpu_group(self.tp.group))
         stream.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(stream):
-            run()  # warm-up (allocator, kernels, hipBLASLt heuristics)
-            if not penalties:
-                run()
+            run()  # warm-up (allocator, kernels, library heuristics)
+            run()
         torch.cuda.current_stream(dev).wait_stream(stream)
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph, pool=self._gpool, stream=stream):
             run()
         self._gpool = graph.pool()
-        return {"graph": graph, "parts": ws.max_parts}
+        return {"graph": graph, "parts": ws.max_parts, "logits": out["logits"]}
+
+    def _capture_penalty(self, B: int) -> dict:
+        """Penalty variant of bucket B, captured lazily the first time a step
+        of that bucket carries a penalised row: the penalty kernel and a
+        second sampling pass over the logits the bucket's decode graph left in
+        its pool (replayed right after it).  No forward pass -- so no
+        collective -- runs in this capture, which any rank that samples can
+        make on its own mid-serving."""
+        g, dev, stream = self._gbuf, self.device, self._gstream
+        pd = self._pmeta.d
+        logits = self.graphs[B]["logits"]
+
+        def run():
+            ops.apply_penalties(logits, pd["win"][:B], pd["ngen"][:B], pd["pen"][:B])
+            ops.sample(logits, g["temp"][:B], g["topk"][:B], g["topp"][:B],
+                       g["seeds"][:B], g["offs"][:B], g["tok"][:B], g["lp"][:B])
+
+        stream.wait_stream(torch.cuda.current_stream(dev))
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, pool=self._gpool, stream=stream):
+            run()
+        self._gpool = graph.pool()
+        torch.cuda.current_stream(dev).wait_stream(stream)
+        return {"graph": graph}
 
     # --------------------------------------------------------- public API ---
     step_trace = None   # a bounded deque of eager steps with LMX_STEP_TRACE=1 (see _step_la)
@@ -960,6 +1007,7 @@ class LLMEngine:
                          d["cu"], d["tiles"], d["rows"], T, S, decode_order=d.get("order"))
         ws = self._decode_ws(plan["num_decode"]) if plan["num_decode"] else self.decode_ws
         logits = self.model.forward(inp, self.k_caches, self.v_caches, ws, self.ecfg.part_tokens)
+        self._peer_check()
         if not samples:
             return None, None
         if pen:
@@ -973,18 +1021,10 @@ class LLMEngine:
         mb = plan["max_blocks"]
         pen = bool(plan.get("any_penalty")) and (self.is_leader or self.sample_all)
         if pen and B not in self.pen_graphs:
-            # one-time capture of this bucket's penalty variant; its warm-up
-            # run must not write the KV cache: no slots, 1-token contexts
-            h["slots"][:B] = -1
-            h["ctx"][:B] = 1
-            h["bt"][:B, 0] = 0
-            self._gmeta.upload()
             t0 = time.time()
-            self.pen_graphs[B] = self._capture_bucket(B, penalties=True)
-            log.info("captured the penalty decode graph of bucket %d in %.2fs", B,
+            self.pen_graphs[B] = self._capture_penalty(B)
+            log.info("captured the penalty sampling graph of bucket %d in %.2fs", B,
                      time.time() - t0)
-            self._gmeta.next()
-            h = self._gmeta.h
         # rows n..B-1 are padding: no cache write (slot -1), a 1-token context
         for k, fill in (("ids", 0), ("pos", 0), ("slots", -1), ("ctx", 1), ("temp", 0),
                         ("topk", 0), ("topp", 1), ("seeds", 0), ("offs", 0)):
@@ -1014,11 +1054,27 @@ class LLMEngine:
         self._gmeta.upload()
         self._mark_upload()
         tb = time.perf_counter()
-        (self.pen_graphs if pen else self.graphs)[B]["graph"].replay()
+        self.graphs[B]["graph"].replay()
+        if pen:
+            self.pen_graphs[B]["graph"].replay()
+        self._peer_check()
         st = self.stats
         st["g_upload"] += tb - ta
         st["g_replay"] += time.perf_counter() - tb
         return g["tok"][:B], g["lp"][:B]
+
+    def _peer_check(self) -> None:
+        """TP: a peer-memory collective of this rank that gave up waiting for a
+        peer (bounded spin) produced a wrong sum; its error word is copied to
+        pinned memory behind every step and read (as of an earlier step) here.
+        Raised as a HIP error: the engine turns unhealthy and the worker is
+        restarted instead of serving corrupted tokens."""
+        peer = self.tp.peer
+        if peer is None or self.device.type != "cuda":
+            return
+        if peer.failed():
+            raise RuntimeError("HIP error: peer all-reduce timed out waiting for a TP peer")
+        peer.check_async(torch.cuda.current_stream(self.device))
 
     def _start_fetch(self, tok: torch.Tensor, lp: torch.Tensor, n: int) -> int:
         """Queue the D2H copy of the sampled tokens/logprobs into pinned

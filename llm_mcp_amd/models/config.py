@@ -33,6 +33,12 @@ class LlamaConfig:
     kind: str = "chat"
     qkv_bias: bool = False          # Qwen2 / Qwen2.5: biased q/k/v projections
     qk_norm: bool = False           # Qwen3: per-head RMSNorm of q and k before RoPE
+    # > 1: a one-GPU stand-in for ONE rank of a TP group of this size (the
+    # preset's shapes are already the per-rank shard): the O / down GEMMs
+    # produce bf16 as a TP rank does before its all-reduce (no split-K
+    # partials handed to the norm, no residual epilogue), so the proxy runs
+    # exactly the rank's kernels; the all-reduces themselves are not run
+    proxy_tp: int = 0
 
     @property
     def params(self) -> int:
@@ -176,6 +182,15 @@ PRESETS: dict[str, object] = {
                                   intermediate_size=1024, num_layers=2, num_heads=16,
                                   num_kv_heads=8, head_dim=128, max_position=2048,
                                   bos_token_id=1018, eos_token_ids=(1022,)),
+    # one rank of Llama-3-70B at TP = 8 (config 4) as a TP = 1 model: 8 q / 1 kv
+    # heads, FFN 28672 / 8, the vocab shard 16128 (128256 / 8 padded to 256-row
+    # tiles), 80 layers -- QKV 1280 x 8192, O 8192 x 1024, gate/up 7168 x 8192,
+    # down 8192 x 3584, LM head 16128 x 8192 per decode step, measured on one GPU
+    "llama-3-70b-tp8-rank": LlamaConfig(name="llama-3-70b-tp8-rank", vocab_size=16128,
+                                        hidden_size=8192, intermediate_size=3584,
+                                        num_layers=80, num_heads=8, num_kv_heads=1,
+                                        bos_token_id=16122, eos_token_ids=(16123,),
+                                        proxy_tp=8),
     # Qwen2.5 (biased QKV, GQA group 7 / 7 -- not a divisor of 16)
     "qwen2.5-7b": LlamaConfig(name="qwen2.5-7b", vocab_size=152064, hidden_size=3584,
                               intermediate_size=18944, num_layers=28, num_heads=28,

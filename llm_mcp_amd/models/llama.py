@@ -113,6 +113,20 @@ class TPContext:
         torch.distributed.all_gather_into_tensor(out, src, group=self.group)
         return out
 
+    def device_collectives_cover(self, rows: int, hidden: int, logit_cols: int) -> bool:
+        """Every collective of a pure-decode step of ``rows`` rows runs as one
+        peer-memory kernel (no RCCL / gloo call): the O / down all-reduces of
+        [rows, hidden] bf16 and the vocab-split logits gather of
+        [rows, logit_cols] bf16 fit a slot, and no decode step is
+        sequence-parallel.  Such a step captures into a hipGraph whatever the
+        group's backend -- a gloo group (one-GPU rehearsals) included."""
+        if self.size == 1:
+            return True
+        if self.peer is None or self.use_sp(rows):
+            return False
+        slot = self.peer.slot
+        return rows * hidden * 2 <= slot and rows * logit_cols * 2 <= slot
+
     def global_rank(self, group_rank: int) -> int:
         """World rank of a rank of this TP group (collectives that name a
         root take world ranks)."""
@@ -132,6 +146,15 @@ class TPContext:
                 torch.distributed.all_reduce(t, group=self.group)
         return t
 
+    def all_reduce_norm(self, t: torch.Tensor, w: torch.Tensor, eps: float,
+                        residual: torch.Tensor) -> torch.Tensor:
+        """residual += all_reduce(t); returns rms_norm(residual) * w.  One
+        peer-memory kernel when it covers the message (decode sizes), else the
+        group's all-reduce followed by the residual-add RMSNorm."""
+        if self.peer is not None and self.peer.norm_supports(t, residual):
+            return self.peer.all_reduce_norm(t, w, eps, residual)
+        return ops.rms_norm(self.all_reduce(t), w, eps, residual=residual)
+
     def _host_staged(self, t: torch.Tensor) -> bool:
         # gloo only reduces device tensors; it gathers host tensors
         return t.is_cuda and torch.distributed.get_backend(self.group) == "gloo"
@@ -145,7 +168,8 @@ class TPContext:
             return t
         src = t.contiguous()
         B, Vs = src.shape
-        if not src.is_cuda or self._host_staged(src):
+        peer = self.peer is not None and self.peer.gather_supports(src)
+        if not peer and (not src.is_cuda or self._host_staged(src)):
             h = src.cpu()
             if self.logits_to_all:
                 parts = [torch.empty_like(h) for _ in range(self.size)]
@@ -156,7 +180,7 @@ class TPContext:
             if self.rank:
                 return None
             return torch.cat(parts, dim=-1).to(t.device, non_blocking=True)
-        if self.peer is not None and self.peer.gather_supports(src):
+        if peer:
             # one kernel over the peer-memory slots: no RCCL collective in the
             # captured decode graph (followers only publish unless every rank
             # samples)
@@ -292,9 +316,15 @@ class LlamaModel:
         # TP = 1 prefill: O / down on K13 add into the residual stream in their
         # epilogue (ops.residual_gemm_ok); x is then None and the next norm
         # reads the residual alone (two passes over the hidden rows fewer)
-        fold = tp.size == 1 and not sp
-        for li, L in enumerate(w["layers"]):
-            if residual is None:
+        # (a TP-rank proxy preset keeps the rank's bf16 O / down outputs)
+        solo = tp.size == 1 and not cfg.proxy_tp
+        fold = solo and not sp
+        pending = None            # h of this layer from the previous layer's fused AR + norm
+        layers = w["layers"]
+        for li, L in enumerate(layers):
+            if pending is not None:
+                h, pending = pending, None
+            elif residual is None:
                 residual = x
                 h = ops.rms_norm(x, L["ln1"], cfg.rms_eps)
             elif x is None:
@@ -344,10 +374,14 @@ class LlamaModel:
                 ops.pgemm(attn, L["wo"], residual=residual)
                 h = ops.rms_norm(residual, L["ln2"], cfg.rms_eps)
             else:
-                o = ops.linear(attn, L["wo"], defer=tp.size == 1)
-                if tp.size > 1:
-                    o = tp.reduce_scatter_rows(o, Tp) if sp else tp.all_reduce(o)
-                h = ops.rms_norm(o, L["ln2"], cfg.rms_eps, residual=residual)
+                o = ops.linear(attn, L["wo"], defer=solo)
+                if tp.size > 1 and not sp:
+                    # one kernel: all-reduce + residual add + RMSNorm (peer memory)
+                    h = tp.all_reduce_norm(o, L["ln2"], cfg.rms_eps, residual)
+                else:
+                    if sp:
+                        o = tp.reduce_scatter_rows(o, Tp)
+                    h = ops.rms_norm(o, L["ln2"], cfg.rms_eps, residual=residual)
             if sp:
                 h = tp.all_gather_rows(h)[:T]
             if self.gu_block:
@@ -362,13 +396,26 @@ class LlamaModel:
                 ops.pgemm(a, L["w_down"], residual=residual)
                 x = None
                 continue
-            x = ops.linear(a, L["w_down"], defer=tp.size == 1 and
-                           (li + 1 < len(w["layers"]) or all_rows))
+            x = ops.linear(a, L["w_down"], defer=solo and
+                           (li + 1 < len(layers) or all_rows))
             if tp.size > 1:
-                x = tp.reduce_scatter_rows(x, Tp) if sp else tp.all_reduce(x)
+                if sp:
+                    x = tp.reduce_scatter_rows(x, Tp)
+                elif li + 1 < len(layers):
+                    # the next layer's input norm fused into this all-reduce
+                    pending = tp.all_reduce_norm(x, layers[li + 1]["ln1"], cfg.rms_eps,
+                                                 residual)
+                    x = None
+                elif all_rows:
+                    pending = tp.all_reduce_norm(x, w["norm"], cfg.rms_eps, residual)
+                    x = None
+                else:
+                    x = tp.all_reduce(x)
         # final norm only on the rows we sample from
         rows = inp.sample_rows
-        if x is None:
+        if pending is not None:
+            hs = pending          # decode under TP: the final norm fused into the last all-reduce
+        elif x is None:
             hs = ops.rms_norm(residual if all_rows else residual.index_select(0, rows),
                               w["norm"], cfg.rms_eps)
         elif sp:

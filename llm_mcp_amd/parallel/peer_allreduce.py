@@ -37,14 +37,19 @@ MAX_WORLD, MAX_BLOCKS = 8, 64
 class PeerAllReduce:
     def __init__(self, group, rank: int, world: int, device: torch.device,
                  slot_bytes: int | None = None, oneshot_max: int | None = None,
-                 spin_max: int = 1 << 22):
+                 spin_max: int | None = None):
         if not 2 <= world <= MAX_WORLD:
             raise ValueError(f"peer all-reduce supports 2..{MAX_WORLD} ranks, got {world}")
         self.group, self.rank, self.world, self.device = group, rank, world, device
         self.slot = int(slot_bytes or float(os.environ.get("LMX_AR_SLOT_MB", "16")) * (1 << 20))
         self.slot -= self.slot % (16 * world)
         self.oneshot_max = int(oneshot_max or os.environ.get("LMX_AR_ONESHOT_MAX", 512 << 10))
-        self.spin_max = spin_max
+        # bounded waits: ~2^25 polls of s_sleep(1) is a few seconds, longer than
+        # any scheduling skew between healthy ranks (the old 2^22 bound, ~0.2 s,
+        # could expire while a follower process was descheduled); a timed-out
+        # kernel sets the error word, which check_async / failed() surface
+        self.spin_max = int(spin_max or os.environ.get("LMX_AR_SPIN", 1 << 25))
+        self._err_h = None
         self.k = native()
         self.own, self.peers, self.calls = None, [], 0
         # every rank reaches the handle exchange, even when its own
@@ -92,6 +97,34 @@ class PeerAllReduce:
         self.calls += 1
         return out
 
+    def norm_supports(self, t: torch.Tensor, residual: torch.Tensor) -> bool:
+        """``t`` [T, cols] can take the fused all-reduce + residual + RMSNorm."""
+        return (self.supports(t) and t.dim() == 2 and t.shape[1] % 8 == 0
+                and t.shape[1] <= 16384 and self.world in (2, 4, 8)
+                and residual.is_contiguous() and residual.shape == t.shape
+                and residual.dtype == torch.bfloat16 and residual.data_ptr() % 16 == 0)
+
+    def all_reduce_norm(self, t: torch.Tensor, w: torch.Tensor, eps: float,
+                        residual: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        """One kernel for a TP sub-layer's tail: residual += sum over the group
+        of ``t`` (bf16-rounded like ``__call__``), returns rmsnorm(residual) * w
+        -- bitwise what the all-reduce followed by ``ops.rms_norm(...,
+        residual=)`` gives.  One-shot up to ``oneshot_max`` bytes, else
+        row-sharded two-shot."""
+        T, cols = t.shape
+        if out is None:
+            out = torch.empty_like(t)
+        n = T * cols * 2
+        two = int(n > self.oneshot_max and T >= self.world)
+        rows = -(-T // self.world) if two else T
+        blocks = max(1, min(MAX_BLOCKS, rows))
+        self.k.allreduce_norm(out.data_ptr(), residual.data_ptr(), t.data_ptr(), w.data_ptr(),
+                              T, cols, float(eps), self.rank, self.world, self.peers, self.slot,
+                              two, blocks, self.spin_max,
+                              torch.cuda.current_stream(t.device).cuda_stream)
+        self.calls += 1
+        return out
+
     def gather_supports(self, t: torch.Tensor) -> bool:
         """``t`` can be all-gathered through the slots (bf16, 16-B rows)."""
         return self.supports(t)
@@ -111,6 +144,20 @@ class PeerAllReduce:
                          torch.cuda.current_stream(t.device).cuda_stream)
         self.calls += 1
         return out if (to_all or self.rank == 0) else None
+
+    def check_async(self, stream) -> None:
+        """Enqueue a copy of the error word into pinned host memory (after a
+        step's collectives, no synchronisation); ``failed`` reads it."""
+        if self.own is None:
+            return
+        if self._err_h is None:
+            self._err_h = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        self.k.ar_error_async(self.own, self._err_h.data_ptr(), stream.cuda_stream)
+
+    def failed(self) -> bool:
+        """A kernel of this rank gave up waiting for a peer (its result was
+        wrong): as of the last copy ``check_async`` enqueued that has landed."""
+        return self._err_h is not None and int(self._err_h[0]) != 0
 
     def error(self, clear: bool = False) -> int:
         """Non-zero when a kernel gave up waiting for a peer (synchronous)."""

@@ -196,8 +196,9 @@ def run_tp_worker(a) -> None:
     if tp.size != a.tp:
         raise SystemExit(f"--tp {a.tp} but the launcher started {tp.size} ranks")
     ecfg = EngineConfig(model=a.chat_model, max_num_seqs=a.max_num_seqs,
-                        max_batched_tokens=a.max_batched_tokens, max_model_len=a.max_model_len,
-                        kv_fraction=a.kv_fraction)
+                        max_model_len=a.max_model_len, kv_fraction=a.kv_fraction)
+    if a.max_batched_tokens:
+        ecfg.max_batched_tokens = a.max_batched_tokens
     tag = f"{rocm_enum.host_id()}-{os.environ.get('MASTER_PORT', '0')}"
     engine = build_tp_engine(ecfg, dev, tp, tag, a.weights)
     log.info("TP rank %d/%d ready: %d KV blocks, %d graphs", tp.rank, tp.size,

@@ -79,6 +79,10 @@ VARS: list[Var] = [
     Var("LMX_MODEL_REGISTRY", str, "", "per-GPU placement 'GPUS:[tpN:|embed:]MODEL;...' "
         "(overrides LMX_CHAT_MODEL / LMX_TP for `serve`)"),
     Var("LMX_MAX_BATCH", int, 256, "max concurrent sequences per engine"),
+    Var("LMX_MAX_BATCHED_TOKENS", int, 24576, "tokens per engine step (an idle engine takes a burst of prompts in steps this large); bench.py and serve share it"),
+    Var("LMX_MIXED_PREFILL_TOKENS", int, 8192, "prompt tokens per step while >= LMX_MIXED_MIN_DECODES decode rows run (bounds the stall a prefill chunk puts on every decoding stream); 0 = no cap"),
+    Var("LMX_MIXED_MIN_DECODES", int, 32, "decode rows that make a step 'mixed' for LMX_MIXED_PREFILL_TOKENS"),
+    Var("LMX_AR_SPIN", int, 1 << 25, "peer all-reduce: polls (s_sleep 1 each) a kernel waits for a TP peer before it gives up and sets the error word (the engine then fails the step)"),
     Var("LMX_ALLOW_CLOUD", int, 0, "1: allow cloud providers (never on the GPU hot path)"),
     Var("LMX_JOB_RETENTION_DAYS", float, 7.0, "purge finished jobs older than this"),
     Var("LMX_MAINTENANCE_INTERVAL", int, 60, "seconds between store maintenance ticks"),

@@ -27,7 +27,8 @@ def build_parser():
     ap.add_argument("--core", default=os.environ.get("CORE_GRPC_ADDR", "127.0.0.1:9090"))
     ap.add_argument("--no-jobs", action="store_true", help="serve the sync path only")
     ap.add_argument("--max-num-seqs", type=int, default=int(os.environ.get("LMX_MAX_BATCH", "256")))
-    ap.add_argument("--max-batched-tokens", type=int, default=8192)
+    ap.add_argument("--max-batched-tokens", type=int, default=None,
+                    help="default: LMX_MAX_BATCHED_TOKENS (engine.EngineConfig, shared with bench.py)")
     ap.add_argument("--max-model-len", type=int, default=8192)
     ap.add_argument("--kv-fraction", type=float, default=0.6)
     ap.add_argument("--lease-seconds", type=int, default=int(os.environ.get("WORKER_LEASE_SECONDS", "60")))
@@ -78,8 +79,9 @@ def main(argv=None):
             from ..models.weights import load_llama_weights
             weights = load_llama_weights(a.weights, cfg, dev)
         ecfg = EngineConfig(model=a.chat_model, max_num_seqs=a.max_num_seqs,
-                            max_batched_tokens=a.max_batched_tokens,
                             max_model_len=a.max_model_len, kv_fraction=a.kv_fraction)
+        if a.max_batched_tokens:
+            ecfg.max_batched_tokens = a.max_batched_tokens
         if a.embed_model:
             ecfg.kv_fraction = min(ecfg.kv_fraction, 0.5)
         engine = LLMEngine(ecfg, device=dev, model_cfg=cfg, weights=weights)

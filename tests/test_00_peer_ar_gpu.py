@@ -125,6 +125,57 @@ def _rank(rank, world, port, q):
                     1.0, want.abs().max().item()):
                 errs.append(f"graph all_reduce after gather {salt}")
         errs += ["graph all_gather: error word set"] if ar.error(clear=True) else []
+        # fused all-reduce + residual add + RMSNorm (a TP sub-layer's tail):
+        # bitwise equal to the all-reduce followed by ops.rms_norm(residual=),
+        # one-shot and row-sharded two-shot (T not a multiple of the world too)
+        from llm_mcp_amd import ops
+        for salt, (T, cols) in enumerate([(1, 8192), (16, 8192), (37, 1024), (256, 8192),
+                                          (300, 4096)], start=400):
+            xs = [x.view(T, cols) for x in _inputs(world, T * cols, salt)]
+            res0 = _inputs(1, T * cols, salt + 7)[0].view(T, cols)
+            wgt = (1 + 0.1 * torch.randn(cols, generator=torch.Generator().manual_seed(salt))
+                   ).to(torch.bfloat16)
+            x, res, wd = xs[rank].to(dev), res0.to(dev), wgt.to(dev)
+            h = ar.all_reduce_norm(x, wd, 1e-5, res)
+            res_u = res0.to(dev)
+            h_u = ops.rms_norm(ar(x.clone()), wd, 1e-5, residual=res_u)
+            torch.cuda.synchronize()
+            if not (torch.equal(h, h_u) and torch.equal(res, res_u)):
+                errs.append(f"fused norm T={T} cols={cols}: differs from all-reduce + rms_norm")
+            o = torch.stack([v.float() for v in xs]).sum(0).to(torch.bfloat16)
+            r = (o.float() + res0.float()).to(torch.bfloat16).float()
+            want = (r * torch.rsqrt(r.pow(2).mean(-1, keepdim=True) + 1e-5) * wgt.float())
+            if not torch.allclose(h.float().cpu(), want, atol=3e-2, rtol=3e-2):
+                errs.append(f"fused norm T={T} cols={cols}: vs fp32 reference")
+        errs += ["fused norm: error word set"] if ar.error(clear=True) else []
+        # ... and inside a captured graph (device epochs), new inputs per replay
+        T, cols = 64, 8192
+        x = torch.zeros(T, cols, dtype=torch.bfloat16, device=dev)
+        res = torch.zeros_like(x)
+        wd = torch.ones(cols, dtype=torch.bfloat16, device=dev)
+        hg = torch.empty_like(x)
+        with torch.cuda.stream(s):
+            ar.all_reduce_norm(x, wd, 1e-5, res, out=hg)
+        torch.cuda.synchronize()
+        dist.barrier()
+        g3 = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g3, stream=s):
+            ar.all_reduce_norm(x, wd, 1e-5, res, out=hg)
+        for salt in range(500, 503):
+            xs = [v.view(T, cols) for v in _inputs(world, T * cols, salt)]
+            res0 = _inputs(1, T * cols, salt + 7)[0].view(T, cols)
+            x.copy_(xs[rank].to(dev))
+            res.copy_(res0.to(dev))
+            torch.cuda.synchronize()
+            dist.barrier()
+            g3.replay()
+            torch.cuda.synchronize()
+            o = torch.stack([v.float() for v in xs]).sum(0).to(torch.bfloat16)
+            r = (o.float() + res0.float()).to(torch.bfloat16).float()
+            want = r * torch.rsqrt(r.pow(2).mean(-1, keepdim=True) + 1e-5)
+            if not torch.allclose(hg.float().cpu(), want, atol=3e-2, rtol=3e-2):
+                errs.append(f"graph fused norm {salt} mismatch")
+        errs += ["graph fused norm: error word set"] if ar.error(clear=True) else []
         q.put(("done", rank, errs))
     except Exception as ex:   # report instead of hanging the parent
         q.put(("done", rank, [f"{type(ex).__name__}: {ex}"]))

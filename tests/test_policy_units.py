@@ -237,3 +237,19 @@ def test_sse_frame_format():
                                       ("abc", None), (True, None)])
 def test_to_int(v, expect):
     assert helpers.to_int(v) == expect
+
+
+def test_clock_snapshot_parser():
+    """bench.py records sclk / mclk / power / temperature per card at the start
+    and end of the timed region (rocm-smi --json, parsed tolerantly)."""
+    from llm_mcp_amd.devices.rocm_enum import parse_clock_snapshot
+    data = {"card0": {"sclk clock speed:": "(2100Mhz)", "mclk clock speed:": "(1900Mhz)",
+                      "Current Socket Graphics Package Power (W)": "1012.0",
+                      "Max Graphics Package Power (W)": "1400.0",
+                      "Temperature (Sensor junction) (C)": "71.0",
+                      "Temperature (Sensor memory) (C)": "60.0"},
+            "system": {"Driver version": "x"}}
+    got = parse_clock_snapshot(data)
+    assert got == {"card0": {"sclk_mhz": 2100.0, "mclk_mhz": 1900.0, "power_w": 1012.0,
+                             "power_cap_w": 1400.0,
+                             "temp_c": {"junction": 71.0, "memory": 60.0}}}

@@ -204,3 +204,38 @@ def test_stop_of_a_preempted_sequence_leaves_the_waiting_queue():
     assert s.abort(1)
     assert not s.has_work
     assert s.kv_usage == 0.0
+
+
+def test_mixed_step_prefill_cap():
+    """With >= min_decodes decode rows running, a step's prompt tokens are
+    capped (set_mixed_prefill_cap), so a long prompt arriving mid-stream is
+    split into capped chunks instead of stalling every decoding stream for a
+    max_batched_tokens step; an idle engine (no decode rows) still takes the
+    full budget."""
+    s = runtime().Scheduler(4096, 32, 64, 4096, 8192, False)
+    s.set_mixed_prefill_cap(256, 4)
+    for i in range(8):
+        s.add(i, [10 + i] * 40, 50, [], True, 0)
+    p = s.schedule(16)
+    assert p["num_decode"] == 0 and p["num_tokens"] == 8 * 40       # burst: full budget
+    s.update(np.full(len(p["sample_rows"]), 11, np.int32))
+    s.add(100, list(range(20, 1020)), 10, [], True, 0)             # a 1000-token prompt
+    steps = []
+    while True:
+        p = s.schedule(16)
+        steps.append((p["num_decode"], p["num_tokens"] - p["num_decode"]))
+        s.update(np.full(len(p["sample_rows"]), 11, np.int32))
+        if steps[-1][1] == 0:
+            break
+    assert [pf for _, pf in steps[:-1]] == [256, 256, 256, 232]
+    assert all(nd >= 8 for nd, _ in steps)                          # the decodes keep running
+    # below min_decodes the cap does not apply
+    s2 = runtime().Scheduler(4096, 32, 64, 4096, 8192, False)
+    s2.set_mixed_prefill_cap(256, 16)
+    for i in range(8):
+        s2.add(i, [10 + i] * 40, 50, [], True, 0)
+    p = s2.schedule(16)
+    s2.update(np.full(len(p["sample_rows"]), 11, np.int32))
+    s2.add(100, list(range(20, 1020)), 10, [], True, 0)
+    p = s2.schedule(16)
+    assert p["num_tokens"] - p["num_decode"] == 1000

@@ -150,6 +150,12 @@ for step in "$@"; do
       rm -rf gpurun_out/$tag ;;   # the trace database alone exceeds what gpurun copies back
     attn_probe)
       run attn_probe 180 python -u tools/decode_attn_probe.py || exit $? ;;
+    tp_graph_tests)
+      run tp_graph_tests 900 python -u -m pytest tests/test_00_tp_gpu.py -x -v --timeout 400 \
+          --timeout-method thread -p no:cacheprovider || exit $? ;;
+    engine_tests)
+      run engine_tests 600 python -u -m pytest tests/test_engine_gpu.py -x -q --timeout 200 \
+          --timeout-method thread -p no:cacheprovider || exit $? ;;
     attn_tests)
       run attn_tests 300 python -u -m pytest tests/test_kernels_gpu.py -k paged_decode -x -q \
           --timeout 120 --timeout-method thread -p no:cacheprovider || exit $? ;;
