@@ -170,7 +170,8 @@ __global__ void __launch_bounds__(AR_THREADS) allreduce_kernel(
 // allreduce_kernel returns), residual += o (bf16, as rmsnorm_kernel keeps the
 // hidden state), h = rmsnorm(residual) * w.  Replaces the GEMM -> all-reduce ->
 // residual-add RMSNorm triple's last two launches and the o round trip
-// between them; bitwise equal to them.
+// between them; the residual stream is bitwise what they produce, h up to the
+// summation order of the row's sum of squares.
 //   one-shot: block b owns rows b, b + nb, ...: publishes them, meets its
 //     peers' block b, sums every rank's copy and norms the row;
 //   two-shot: rows are sharded by rank (S = ceil(T / W) rows each); block b

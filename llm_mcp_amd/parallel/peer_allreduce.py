@@ -108,8 +108,9 @@ class PeerAllReduce:
                         residual: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
         """One kernel for a TP sub-layer's tail: residual += sum over the group
         of ``t`` (bf16-rounded like ``__call__``), returns rmsnorm(residual) * w
-        -- bitwise what the all-reduce followed by ``ops.rms_norm(...,
-        residual=)`` gives.  One-shot up to ``oneshot_max`` bytes, else
+        -- the residual bitwise what the all-reduce followed by
+        ``ops.rms_norm(..., residual=)`` gives, h up to the order of the row's
+        sum of squares.  One-shot up to ``oneshot_max`` bytes, else
         row-sharded two-shot."""
         T, cols = t.shape
         if out is None:

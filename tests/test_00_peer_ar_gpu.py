@@ -140,7 +140,10 @@ def _rank(rank, world, port, q):
             res_u = res0.to(dev)
             h_u = ops.rms_norm(ar(x.clone()), wd, 1e-5, residual=res_u)
             torch.cuda.synchronize()
-            if not (torch.equal(h, h_u) and torch.equal(res, res_u)):
+            # the residual stream bitwise; h up to the order of the sum of squares
+            # (512 vs 256 threads per row): a last-bit difference of the scale
+            if not (torch.equal(res, res_u) and torch.allclose(h.float(), h_u.float(),
+                                                                atol=1e-2, rtol=1e-2)):
                 errs.append(f"fused norm T={T} cols={cols}: differs from all-reduce + rms_norm")
             o = torch.stack([v.float() for v in xs]).sum(0).to(torch.bfloat16)
             r = (o.float() + res0.float()).to(torch.bfloat16).float()

@@ -41,6 +41,10 @@ for step in "$@"; do
       # config 4's launcher shape: one TP-8 engine of the 70B layer shapes (8 layers)
       run tp8s 900 python3 bench.py --gpus 8 --tp 8 --rehearse-on-one-gpu \
           --model llama-3-70b@L8 --steps 2 --warmup 1 --concurrency 32 --max-tokens 64 || exit $? ;;
+    tp8s_la)
+      # the same with TP lookahead stepping (every rank samples the all-gathered logits)
+      LMX_LOOKAHEAD=1 run tp8s_la 900 python3 bench.py --gpus 8 --tp 8 --rehearse-on-one-gpu \
+          --model llama-3-70b@L8 --steps 2 --warmup 1 --concurrency 32 --max-tokens 64 || exit $? ;;
     dgemm_tests)
       run dgemm_tests 600 python -u -m pytest tests/test_kernels_gpu.py -k dgemm -x -q --timeout 120 \
           --timeout-method thread -p no:cacheprovider || exit $? ;;
@@ -153,9 +157,42 @@ for step in "$@"; do
     tp_graph_tests)
       run tp_graph_tests 900 python -u -m pytest tests/test_00_tp_gpu.py -x -v --timeout 400 \
           --timeout-method thread -p no:cacheprovider || exit $? ;;
+    bench_nocap)
+      # the round-4 behaviour (no mixed-step prefill cap) for the A/B
+      run bench_nocap 600 python bench.py --steps 3 --warmup 1 --mixed-prefill-tokens 0 || exit $? ;;
+    closed_default)
+      run closed_default 600 python bench.py --load closed --duration 30 --closed-warmup 10 \
+          || exit $? ;;
+    closed_nocap)
+      run closed_nocap 600 python bench.py --load closed --duration 30 --closed-warmup 10 \
+          --mixed-prefill-tokens 0 || exit $? ;;
+    poisson)
+      run poisson 600 python bench.py --load poisson --rate ${POISSON_RATE:-60} --duration 30 \
+          --closed-warmup 10 || exit $? ;;
+    long2k)
+      run long2k 900 python bench.py --steps 2 --warmup 1 --prompt-len 2048 --max-tokens 256 \
+          || exit $? ;;
+    long8k)
+      run long8k 900 python bench.py --steps 2 --warmup 1 --prompt-len 7680 --max-tokens 256 \
+          --concurrency 64 || exit $? ;;
+    proxy70)
+      # config 4's per-rank decode on one GPU (llama-3-70b-tp8-rank), under a kernel trace
+      rm -rf gpurun_out/proxy70
+      run proxy70 900 rocprofv3 --kernel-trace -d gpurun_out/proxy70 -o run \
+          -- python3 bench.py --model llama-3-70b-tp8-rank --concurrency 256 --max-tokens 128 \
+          --steps 2 --warmup 1 || exit $?
+      python tools/prof_timeline.py gpurun_out/proxy70/run_results.db --waves 2 \
+          > gpurun_out/proxy70_timeline.md 2>&1 || true
+      rm -rf gpurun_out/proxy70 ;;
+    peer_tests)
+      run peer_tests 600 python -u -m pytest tests/test_00_peer_ar_gpu.py -x -v --timeout 300 \
+          --timeout-method thread -p no:cacheprovider || exit $? ;;
     engine_tests)
       run engine_tests 600 python -u -m pytest tests/test_engine_gpu.py -x -q --timeout 200 \
           --timeout-method thread -p no:cacheprovider || exit $? ;;
+    pf_probe)
+      run pf_probe 300 python -u tools/prefill_attn_probe.py \
+          --shapes ${PF_SHAPES:-llama8b,llama8b_2k,llama8b_8k,nomic} --waves 4,8 || exit $? ;;
     attn_tests)
       run attn_tests 300 python -u -m pytest tests/test_kernels_gpu.py -k paged_decode -x -q \
           --timeout 120 --timeout-method thread -p no:cacheprovider || exit $? ;;

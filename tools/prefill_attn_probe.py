@@ -16,7 +16,10 @@ import torch  # noqa: E402
 from llm_mcp_amd import ops  # noqa: E402
 
 SHAPES = {"nomic": (32, 1024, 12, 12, 64, False), "mxbai": (64, 512, 16, 16, 64, False),
-          "llama8b": (30, 546, 32, 8, 128, True)}
+          "llama8b": (30, 546, 32, 8, 128, True),
+          # long-context prefill steps (one 24576-token step of 2K / 7.7K prompts)
+          "llama8b_2k": (12, 2048, 32, 8, 128, True),
+          "llama8b_8k": (3, 7680, 32, 8, 128, True)}
 
 
 def run(name, S, L, Hq, Hkv, D, causal, iters, ng=0, tag="", waves=4):
@@ -60,6 +63,8 @@ def run(name, S, L, Hq, Hkv, D, causal, iters, ng=0, tag="", waves=4):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--shapes", default="nomic,mxbai,llama8b",
+                    help="comma list of " + ", ".join(SHAPES))
     ap.add_argument("--ng", type=int, default=0,
                     help="column groups per wave of the loaded build (A/B of an older .so)")
     ap.add_argument("--thr", default="8",
@@ -75,7 +80,7 @@ def main():
     wl = [int(t) for t in a.waves.split(",")]
     nat = ops.native()
     for _ in range(2):
-        for name, shp in SHAPES.items():
+        for name, shp in [(n, SHAPES[n]) for n in a.shapes.split(",")]:
             for thr in thrs:
                 for st, xo, w in [(st, xo, w) for st in stages for xo in xcds for w in wl]:
                     if shp[4] != 128 and w != wl[0]:

@@ -7,6 +7,11 @@
 //             1: pages in random order over a 4 GB buffer
 //             2: random pages, each wave reads a page as 16 rows x 64 B per
 //                instruction (the decode kernel's K fragment shape)
+//             3: the decode-attention pattern: a "page" is an 8 KB K page AND an
+//                8 KB V page from two random places; K as the 16 rows x 64 B
+//                fragments, V as the kernel's 8-B key-quad fragment loads
+//                (16 dwordx2 per lane instead of 8 dwordx4)
+//             4: as 3 with V read as 8 dwordx4 (1 KB contiguous per instruction)
 //     INFLIGHT: pages per wave in flight (1 or 2)
 // Every launch reads 768 MB; launches rotate over disjoint page sets so the
 // 256 MB Infinity Cache holds nothing a launch reads.
@@ -36,6 +41,48 @@ __device__ __forceinline__ void load_page(u32x4 (&r)[NL], const char* base, int 
     }
     r[i] = *reinterpret_cast<const u32x4*>(base + off);
   }
+}
+
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+
+// pattern 3 / 4: one 8 KB K page (16 rows x 64 B fragments) + one 8 KB V page
+template <int V16>
+__global__ void __launch_bounds__(256) kv_stream(const char* __restrict__ buf,
+                                                 const int* __restrict__ pages, int npairs,
+                                                 unsigned* __restrict__ sink) {
+  const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+  const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int nwaves = gridDim.x * 4;
+  unsigned acc = 0;
+  for (int p = wave; p < npairs; p += nwaves) {
+    const char* kp = buf + (long)pages[2 * p] * 8192;
+    const char* vp = buf + (long)pages[2 * p + 1] * 8192;
+    u32x4 k[8];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      k[s] = *reinterpret_cast<const u32x4*>(kp + c * 256 + 64 * s + 16 * g);
+      k[4 + s] = *reinterpret_cast<const u32x4*>(kp + (16 + c) * 256 + 64 * s + 16 * g);
+    }
+    if constexpr (V16) {
+      u32x4 v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = *reinterpret_cast<const u32x4*>(vp + i * 1024 + lane * 16);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc ^= v[i].x ^ v[i].w;
+    } else {
+      u32x2 v[16];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        v[i] = *reinterpret_cast<const u32x2*>(vp + g * 1024 + 128 * i + 8 * c);
+        v[8 + i] = *reinterpret_cast<const u32x2*>(vp + (4 + g) * 1024 + 128 * i + 8 * c);
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc ^= v[i].x ^ v[i].y;
+    }
+#pragma unroll
+    for (int s = 0; s < 8; ++s) acc ^= k[s].x ^ k[s].w;
+  }
+  if (acc == 0x12345678u) sink[0] = acc;
 }
 
 template <int NL, int FRAG, int INFL>
@@ -126,6 +173,30 @@ int main(int argc, char** argv) {
   const int wgs = wpc * cus;
   const int frag = pattern == 2;
   float us = -1;
+  if (pattern >= 3) {
+    if (page_kb != 8) { printf("patterns 3/4 use 8 KB pages\n"); return 2; }
+    const int npairs = npages / 2;
+    hipEvent_t s0, e0;
+    CHECK(hipEventCreate(&s0));
+    CHECK(hipEventCreate(&e0));
+    auto launch = [&](const int* t) {
+      if (pattern == 4) kv_stream<1><<<wgs, 256>>>(buf, t, npairs, sink);
+      else kv_stream<0><<<wgs, 256>>>(buf, t, npairs, sink);
+    };
+    launch(tables[0]);
+    CHECK(hipDeviceSynchronize());
+    CHECK(hipEventRecord(s0));
+    for (int i = 0; i < 30; ++i) launch(tables[i % rot]);
+    CHECK(hipEventRecord(e0));
+    CHECK(hipEventSynchronize(e0));
+    float ms = 0;
+    CHECK(hipEventElapsedTime(&ms, s0, e0));
+    us = ms * 1000.f / 30;
+    printf("page  8 KB pattern %d (%s) wgs/CU %d: %7.1f us  %5.2f TB/s\n", pattern,
+           pattern == 3 ? "K frag + V 8-B frag pages" : "K frag + V 1-KB rows", wpc, us,
+           read / us / 1e6);
+    return 0;
+  }
 #define RUN(NL)                                                                           \
   if (frag && infl == 2) us = run<NL, 1, 2>(buf, nullptr, npages, wgs, sink, rot, tables); \
   else if (frag) us = run<NL, 1, 1>(buf, nullptr, npages, wgs, sink, rot, tables);         \
