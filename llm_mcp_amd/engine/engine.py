@@ -1004,7 +1004,8 @@ class LLMEngine:
         d = self.packer.pack(items)
         self._mark_upload()
         inp = StepInputs(d["ids"], d["pos"], d["slots"], plan["num_decode"], d["bt"], d["ctx"],
-                         d["cu"], d["tiles"], d["rows"], T, S, decode_order=d.get("order"))
+                         d["cu"], d["tiles"], d["rows"], T, S, decode_order=d.get("order"),
+                         host={"cu_q": plan["cu_q"], "tiles": plan["prefill_tiles"], "rows": rows})
         ws = self._decode_ws(plan["num_decode"]) if plan["num_decode"] else self.decode_ws
         logits = self.model.forward(inp, self.k_caches, self.v_caches, ws, self.ecfg.part_tokens)
         self._peer_check()

@@ -52,6 +52,9 @@ class StepInputs:
     num_tokens: int
     num_seqs: int
     decode_order: torch.Tensor | None = None   # int32 [num_decode] (ops.decode_order)
+    # host copies of the plan's cu_q / prefill_tiles / sample_rows (numpy), when
+    # the caller has them: lets the model split a step without a device sync
+    host: dict | None = None
 
 
 class TPContext:
@@ -146,6 +149,16 @@ class TPContext:
                 torch.distributed.all_reduce(t, group=self.group)
         return t
 
+    def all_reduce_async(self, t: torch.Tensor):
+        """Start the sum of ``t`` over the group in place; returns a handle
+        whose ``wait()`` orders the caller's stream after it (RCCL: the
+        collective runs on its own stream, overlapping the compute issued
+        meanwhile).  Host-staged (gloo) and peer paths complete here."""
+        if self.size > 1 and self.peer is None and not self._host_staged(t):
+            return torch.distributed.all_reduce(t, group=self.group, async_op=True)
+        self.all_reduce(t)
+        return _Done()
+
     def all_reduce_norm(self, t: torch.Tensor, w: torch.Tensor, eps: float,
                         residual: torch.Tensor) -> torch.Tensor:
         """residual += all_reduce(t); returns rms_norm(residual) * w.  One
@@ -193,6 +206,11 @@ class TPContext:
             if self.rank and not self.logits_to_all:
                 return None
         return out.view(self.size, B, Vs).permute(1, 0, 2).reshape(B, self.size * Vs)
+
+
+class _Done:
+    def wait(self):
+        return True
 
 
 class LlamaModel:
@@ -292,9 +310,126 @@ class LlamaModel:
         return n
 
     # ----------------------------------------------------------- forward ----
+    # ------------------------------------------- TP prefill micro-batches ----
+    def _microbatch_split(self, inp: StepInputs) -> int:
+        """Pure-prefill TP step split point (prefill-sequence index) for two
+        micro-batches whose row-parallel all-reduces overlap the other
+        micro-batch's compute, or 0 for one batch.  LMX_TP_MICROBATCH: auto
+        (RCCL groups, steps of >= LMX_TP_MICROBATCH_MIN tokens, default 2048),
+        1 (any group, any size: tests), 0 (off)."""
+        tp = self.tp
+        mode = os.environ.get("LMX_TP_MICROBATCH", "auto")
+        if (tp.size < 2 or mode == "0" or inp.num_decode or inp.host is None
+                or tp.use_sp(inp.num_tokens) or tp.group is None):
+            return 0
+        if mode != "1":
+            if torch.distributed.get_backend(tp.group) != "nccl":
+                return 0
+            if inp.num_tokens < int(os.environ.get("LMX_TP_MICROBATCH_MIN", "2048")):
+                return 0
+        cu = inp.host["cu_q"]
+        S = len(cu) - 1
+        if S < 2:
+            return 0
+        half = cu[-1] / 2.0
+        j = int(min(range(1, S), key=lambda k: abs(cu[k] - half)))
+        return j
+
+    def _microbatch(self, inp: StepInputs, s0: int, s1: int) -> StepInputs:
+        """Rows of prefill sequences [s0, s1) of a pure-prefill step as a step
+        of their own (device slices and rebased index tensors; no sync)."""
+        import numpy as np
+        h = inp.host
+        cu, tiles, rows = h["cu_q"], h["tiles"].reshape(-1, 2), h["rows"]
+        r0, r1 = int(cu[s0]), int(cu[s1])
+        t0 = int(np.searchsorted(tiles[:, 0], s0, "left"))
+        t1 = int(np.searchsorted(tiles[:, 0], s1, "left"))
+        k0 = int(np.searchsorted(rows, r0, "left"))
+        k1 = int(np.searchsorted(rows, r1, "left"))
+        dev_tiles = inp.prefill_tiles.view(-1, 2)[t0:t1]
+        shift = torch.tensor([s0, 0], dtype=dev_tiles.dtype, device=dev_tiles.device)
+        return StepInputs(
+            inp.input_ids[r0:r1], inp.positions[r0:r1], inp.slots[r0:r1], 0,
+            inp.block_tables[s0:s1], inp.context_lens[s0:s1], inp.cu_q[s0:s1 + 1] - r0,
+            (dev_tiles - shift).reshape(-1).contiguous(), inp.sample_rows[k0:k1] - r0,
+            r1 - r0, s1 - s0,
+            host={"cu_q": cu[s0:s1 + 1] - r0, "tiles": tiles[t0:t1] - [s0, 0],
+                  "rows": rows[k0:k1] - r0})
+
+    def _mb_pipeline(self, inp: StepInputs, k_caches: list, v_caches: list):
+        """One micro-batch's layer loop as a generator: it yields the handle of
+        each row-parallel all-reduce it starts and resumes (after the caller
+        waited on it) with the next stage; returns the final normed rows."""
+        cfg, w, tp = self.cfg, self.w, self.tp
+        Hq, Hkv, D = self.Hq, self.Hkv, self.D
+        x = ops.embed_gather(w["embed"], inp.input_ids)
+        residual = x
+        layers = w["layers"]
+        h = ops.rms_norm(x, layers[0]["ln1"], cfg.rms_eps)
+        for li, L in enumerate(layers):
+            qkv = ops.linear(h, L["wqkv"], bias=L.get("bqkv"))
+            kc, vc = k_caches[li], v_caches[li]
+            fuse_pf = self.fuse_prefill_rope and "q_norm" not in L and qkv.is_cuda
+            ops.rope_and_cache(qkv, inp.positions, self.cos_sin, Hq, Hkv, D, inp.slots, kc, vc,
+                               tile_from=0, q_norm=L.get("q_norm"), k_norm=L.get("k_norm"),
+                               eps=cfg.rms_eps, skip_q=fuse_pf)
+            attn = torch.empty((inp.num_tokens, Hq * D), dtype=self.dtype, device=self.device)
+            ops.paged_prefill_attention(qkv, kc, vc, inp.block_tables, inp.cu_q,
+                                        inp.context_lens, inp.prefill_tiles, self.scale, attn,
+                                        Hq=Hq, rope=(inp.positions, self.cos_sin) if fuse_pf
+                                        else None)
+            o = ops.linear(attn, L["wo"])
+            yield tp.all_reduce_async(o)
+            h = ops.rms_norm(o, L["ln2"], cfg.rms_eps, residual=residual)
+            if self.gu_block:
+                a = ops.linear_swiglu(h, L["w_gate_up"], self.gu_block)
+            else:
+                a = ops.silu_mul(ops.linear(h, L["w_gate_up"]))
+            x = ops.linear(a, L["w_down"])
+            yield tp.all_reduce_async(x)
+            nxt = layers[li + 1]["ln1"] if li + 1 < len(layers) else None
+            if nxt is not None:
+                h = ops.rms_norm(x, nxt, cfg.rms_eps, residual=residual)
+        rows = inp.sample_rows
+        return ops.rms_norm(x.index_select(0, rows), w["norm"], cfg.rms_eps,
+                            residual=residual.index_select(0, rows))
+
+    def _forward_tp_mb(self, inp: StepInputs, j: int, k_caches: list,
+                       v_caches: list) -> torch.Tensor | None:
+        """Pure-prefill TP step as two micro-batches (prefill sequences [0, j)
+        and [j, S)) stepped alternately: micro-batch A's all-reduce after its
+        O (or down) GEMM runs on the collective stream while B's attention /
+        GEMMs run, and the other way round; every rank issues the collectives
+        in the same order (A, B, A, B, ...)."""
+        S = inp.num_seqs
+        gens = [self._mb_pipeline(self._microbatch(inp, 0, j), k_caches, v_caches),
+                self._mb_pipeline(self._microbatch(inp, j, S), k_caches, v_caches)]
+        handles = [next(g) for g in gens]
+        outs: list = [None, None]
+        live = [True, True]
+        while any(live):
+            for i in (0, 1):
+                if not live[i]:
+                    continue
+                handles[i].wait()
+                try:
+                    handles[i] = gens[i].send(None)
+                except StopIteration as stop:
+                    outs[i] = stop.value
+                    live[i] = False
+        hs = torch.cat(outs, dim=0)
+        logits = ops.linear(hs, self.w["lm_head"])
+        logits = self.tp.gather_last_to_leader(logits)
+        if logits is not None:
+            logits = logits[:, :self.cfg.vocab_size]
+        return logits
+
     def forward(self, inp: StepInputs, k_caches: list, v_caches: list,
                 decode_ws: ops.DecodeWorkspace | None, part_tokens: int = 512) -> torch.Tensor:
         """Returns logits [len(sample_rows), vocab] (bf16)."""
+        j = self._microbatch_split(inp)
+        if j:
+            return self._forward_tp_mb(inp, j, k_caches, v_caches)
         cfg, w = self.cfg, self.w
         Hq, Hkv, D = self.Hq, self.Hkv, self.D
         T, nd = inp.num_tokens, inp.num_decode

@@ -33,11 +33,11 @@ def _ecfg(model="tiny-llama"):
 
 
 def _rank_main(rank, size, port, ckpt, tag, q, sp_min_tokens=0, model="tiny-llama",
-               lookahead="0"):
+               lookahead="0", microbatch="0"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(size), LOCAL_RANK=str(rank),
                       LMX_SP_MIN_TOKENS=str(sp_min_tokens), LMX_TP_PROBE_STEPS="3",
-                      LMX_LOOKAHEAD=lookahead)
+                      LMX_LOOKAHEAD=lookahead, LMX_TP_MICROBATCH=microbatch)
     torch.set_num_threads(2 if size <= 2 else 1)
     import torch.distributed as dist
 
@@ -101,14 +101,17 @@ def test_plan_roundtrip(tmp_path):
     leader.close()
 
 
-@pytest.mark.parametrize("sp_min_tokens,lookahead", [(0, "0"), (7, "0"), (0, "1")])
-def test_tp2_generation_matches_single_process(full_model, sp_min_tokens, lookahead):
+@pytest.mark.parametrize("sp_min_tokens,lookahead,microbatch",
+                         [(0, "0", "0"), (7, "0", "0"), (0, "1", "0"), (0, "0", "1")])
+def test_tp2_generation_matches_single_process(full_model, sp_min_tokens, lookahead, microbatch):
     """sp_min_tokens=7: every prefill / mixed step of >= 7 tokens runs
     sequence-parallel (reduce-scatter + row-sharded RMSNorm + all-gather),
     odd token counts included (padded rows); pure decode steps stay on the
     all-reduce path.  lookahead=1: the leader launches step n+1 before it
     reads step n back; every rank samples the all-gathered logits itself
-    (engine.sample_all) and gathers its inputs from its own samples."""
+    (engine.sample_all) and gathers its inputs from its own samples.
+    microbatch=1: pure-prefill steps of >= 2 sequences run as two
+    micro-batches whose all-reduces alternate (LlamaModel._forward_tp_mb)."""
     m, path = full_model
     single = LLMEngine(_ecfg(), device="cpu", model_cfg=m.cfg, weights=m.w)
     ref_sampled = single.generate(PROMPTS[:2], SamplingParams(temperature=0.8, top_p=0.9,
@@ -118,7 +121,8 @@ def test_tp2_generation_matches_single_process(full_model, sp_min_tokens, lookah
     q = ctx.Queue()
     port, tag = _free_port(), f"test-{os.getpid()}-{_free_port()}"
     procs = [ctx.Process(target=_rank_main,
-                         args=(r, 2, port, path, tag, q, sp_min_tokens, "tiny-llama", lookahead),
+                         args=(r, 2, port, path, tag, q, sp_min_tokens, "tiny-llama", lookahead,
+                               microbatch),
                          daemon=True)
              for r in range(2)]
     for p in procs:
@@ -278,3 +282,44 @@ def test_follower_exits_on_stale_heartbeat(tmp_path):
     assert time.time() - t0 < 10
     follower.close()
     leader.close()
+
+
+def test_prefill_microbatches_match_one_batch(full_model, monkeypatch):
+    """The micro-batch split of a pure-prefill step (LlamaModel._microbatch):
+    the two halves' rows, rebased cu_q / tile lists / sampled rows, run through
+    the per-micro-batch pipeline, give the logits of the unsplit forward
+    (single process: the all-reduces are no-ops, the split is what is tested)."""
+    import numpy as np
+    from llm_mcp_amd import ops
+    from llm_mcp_amd.models.llama import StepInputs
+    m, _ = full_model
+    cfg = m.cfg
+    lens = [7, 12, 5, 9]
+    BS, D = 32, cfg.head_dim
+    nb = 8
+    kc = [torch.zeros(nb, cfg.num_kv_heads, BS, D, dtype=torch.bfloat16) for _ in range(cfg.num_layers)]
+    vc = [torch.zeros(nb, cfg.num_kv_heads, BS // 4, D, 4, dtype=torch.bfloat16)
+          for _ in range(cfg.num_layers)]
+    ids = torch.arange(sum(lens), dtype=torch.int32) % 400 + 3
+    cu = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+    pos = torch.cat([torch.arange(n, dtype=torch.int32) for n in lens])
+    bt = torch.arange(len(lens), dtype=torch.int32).view(-1, 1)
+    slots = torch.cat([torch.arange(n, dtype=torch.int32) + 32 * i for i, n in enumerate(lens)])
+    qpt = ops.prefill_q_per_tile(cfg.num_heads, cfg.num_kv_heads, D)
+    tiles = np.array([v for s_, n in enumerate(lens) for q0 in range(0, n, qpt) for v in (s_, q0)],
+                     np.int32)
+    rows = (cu[1:] - 1).astype(np.int64)
+    inp = StepInputs(ids, pos, slots, 0, bt, torch.tensor(lens, dtype=torch.int32),
+                     torch.from_numpy(cu), torch.from_numpy(tiles), torch.from_numpy(rows),
+                     int(cu[-1]), len(lens),
+                     host={"cu_q": cu, "tiles": tiles, "rows": rows})
+    ref = m.forward(inp, kc, vc, None).float()
+    # the split the model would take, then the micro-batched path itself
+    j = 2
+    a, b = m._microbatch(inp, 0, j), m._microbatch(inp, j, len(lens))
+    assert a.num_tokens + b.num_tokens == inp.num_tokens
+    assert a.host["cu_q"].tolist() == [0, 7, 19] and b.host["cu_q"].tolist() == [0, 5, 14]
+    assert b.prefill_tiles.view(-1, 2)[:, 0].tolist() == sorted(b.prefill_tiles.view(-1, 2)[:, 0].tolist())
+    assert b.sample_rows.tolist() == [4, 13]
+    got = m._forward_tp_mb(inp, j, kc, vc).float()
+    torch.testing.assert_close(got, ref, atol=1e-2, rtol=1e-2)
