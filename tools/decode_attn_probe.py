@@ -19,6 +19,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--hq", type=int, default=32, help="query heads (8 kv heads): 64 = Llama-3-70B")
+    ap.add_argument("--hkv", type=int, default=8, help="kv heads (1 = a Llama-3-70B TP = 8 rank)")
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--ctx-lo", type=int, default=535)
     ap.add_argument("--ctx-hi", type=int, default=791)
@@ -40,7 +41,7 @@ def main():
                          "kv head) becomes its own 1-kv-head sequence of the same context, so with "
                          "--layout contig every segment streams one contiguous run of pages")
     a = ap.parse_args()
-    B, Hq, Hkv, D, BS = a.batch, a.hq, 8, 128, 32
+    B, Hq, Hkv, D, BS = a.batch, a.hq, a.hkv, 128, 32
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     ctx = torch.randint(a.ctx_lo, a.ctx_hi + 1, (B,), dtype=torch.int32)

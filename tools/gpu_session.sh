@@ -41,6 +41,32 @@ for step in "$@"; do
       # config 4's launcher shape: one TP-8 engine of the 70B layer shapes (8 layers)
       run tp8s 900 python3 bench.py --gpus 8 --tp 8 --rehearse-on-one-gpu \
           --model llama-3-70b@L8 --steps 2 --warmup 1 --concurrency 32 --max-tokens 64 || exit $? ;;
+    dgemm70)
+      # every TP = 8 rank projection shape: K11 tiles / splits / stream-K vs the library
+      # (rows kept for --from-rows; the table is rewritten on the CPU side)
+      run dgemm70 1100 python -u -m llm_mcp_amd.bench.dgemm_bench --model llama-3-70b --tp 8 \
+          --only ${DG_ONLY:-qkv,o,gate_up,down} --json gpurun_out/dgemm70_rows.json || exit $? ;;
+    rs70)
+      # K14 on the TP = 8 rank's gate/up (SwiGLU16) and down at M = 256
+      : > gpurun_out/rs70.log
+      timeout -k 10 200 tools/labbin/rsgemm_lab 7168 8192 256 3 \
+          rs:38:1,rs:38:2,rs:38:4,rs:46:1,rs:46:2,rs:34:2,rs:34:4 >> gpurun_out/rs70.log 2>&1 || exit $?
+      timeout -k 10 200 tools/labbin/rsgemm_lab 8192 3584 256 0 \
+          rs:38:1,rs:38:2,rs:38:4,rs:46:1,rs:46:2,dg:4:1,dg:8:1 >> gpurun_out/rs70.log 2>&1 || exit $?
+      cat gpurun_out/rs70.log ;;
+    attn70)
+      # one TP = 8 rank's decode attention: 256 rows x 1 kv head x 8 q heads, split-K partitions
+      : > gpurun_out/attn70.log
+      for parts in 1 2 3 4; do
+        timeout -k 10 120 python -u tools/decode_attn_probe.py --layout engine --rope --hq 8 \
+            --hkv 1 --batch 256 --ctx-lo 512 --ctx-hi 640 --parts $parts --modes 0,10,4 --pages 100000 \
+            --iters 40 >> gpurun_out/attn70.log 2>&1 || exit $?
+      done
+      cat gpurun_out/attn70.log ;;
+    qkv70)
+      # the TP = 8 rank's narrow QKV (1280 x 8192): every K11 tile / split / stream-K form
+      run qkv70 600 python -u -m llm_mcp_amd.bench.dgemm_bench --model llama-3-70b --tp 8 \
+          --only qkv --m ${QKV_MS:-64,128,192,256} --json gpurun_out/qkv70_rows.json || exit $? ;;
     tp8s_la)
       # the same with TP lookahead stepping (every rank samples the all-gathered logits)
       LMX_LOOKAHEAD=1 run tp8s_la 900 python3 bench.py --gpus 8 --tp 8 --rehearse-on-one-gpu \
@@ -157,6 +183,12 @@ for step in "$@"; do
     tp_graph_tests)
       run tp_graph_tests 900 python -u -m pytest tests/test_00_tp_gpu.py -x -v --timeout 400 \
           --timeout-method thread -p no:cacheprovider || exit $? ;;
+    bench_cap16)
+      run bench_cap16 600 python bench.py --steps 3 --warmup 1 --mixed-prefill-tokens 16384 \
+          || exit $? ;;
+    closed_cap16)
+      run closed_cap16 600 python bench.py --load closed --duration 30 --closed-warmup 10 \
+          --mixed-prefill-tokens 16384 || exit $? ;;
     bench_nocap)
       # the round-4 behaviour (no mixed-step prefill cap) for the A/B
       run bench_nocap 600 python bench.py --steps 3 --warmup 1 --mixed-prefill-tokens 0 || exit $? ;;
