@@ -825,18 +825,24 @@ int paged_decode(const void* q, long q_stride, const void* k_cache, const void* 
       (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, \
       bt_stride, context_lens, order, (bf16_t*)out, out_stride, B, Hq, Hkv, scale, part_tokens, \
       rp);
+  // mode 0 with no more segments than CUs (a TP rank's single kv head, e.g.
+  // 256 rows x 1 kv head): one workgroup per segment, the grid form -- the
+  // persistent form walks one segment per workgroup there anyway and measured
+  // 22.2 vs 19.6 us (profiles/r5_proxy70.md)
+  const int mode = (g_decode_mode == 0 && max_parts == 1 && B * Hkv <= decode_resident_wgs(1))
+                       ? 4 : g_decode_mode;
 #define LMX_DEC(HDV)                                                                          \
-  if (g_decode_mode == 9 && max_parts == 1) { LMX_DEC_R(HDV, 2) }                             \
-  else if (g_decode_mode == 10 && max_parts == 1) { LMX_DEC_R(HDV, 3) }                       \
-  else if ((g_decode_mode == 9 || g_decode_mode == 10)) { LMX_DEC_K(HDV, 9) }                 \
-  else if (g_decode_mode == 0 && max_parts == 1) { LMX_DEC_P(HDV, 0) }                        \
-  else if (g_decode_mode == 5 && max_parts == 1) { LMX_DEC_P(HDV, 5) }                        \
-  else if (g_decode_mode == 6 && max_parts == 1) { LMX_DEC_P(HDV, 6) }                        \
-  else if (g_decode_mode == 6) { LMX_DEC_K(HDV, 6) }                                          \
-  else if (g_decode_mode == 5) { LMX_DEC_K(HDV, 5) }                                          \
-  else if (g_decode_mode == 1) { LMX_DEC_K(HDV, 1) }                                          \
-  else if (g_decode_mode == 2) { LMX_DEC_K(HDV, 2) }                                          \
-  else if (g_decode_mode == 3) { LMX_DEC_K(HDV, 3) }                                          \
+  if (mode == 9 && max_parts == 1) { LMX_DEC_R(HDV, 2) }                                      \
+  else if (mode == 10 && max_parts == 1) { LMX_DEC_R(HDV, 3) }                       \
+  else if ((mode == 9 || mode == 10)) { LMX_DEC_K(HDV, 9) }                 \
+  else if (mode == 0 && max_parts == 1) { LMX_DEC_P(HDV, 0) }                        \
+  else if (mode == 5 && max_parts == 1) { LMX_DEC_P(HDV, 5) }                        \
+  else if (mode == 6 && max_parts == 1) { LMX_DEC_P(HDV, 6) }                        \
+  else if (mode == 6) { LMX_DEC_K(HDV, 6) }                                          \
+  else if (mode == 5) { LMX_DEC_K(HDV, 5) }                                          \
+  else if (mode == 1) { LMX_DEC_K(HDV, 1) }                                          \
+  else if (mode == 2) { LMX_DEC_K(HDV, 2) }                                          \
+  else if (mode == 3) { LMX_DEC_K(HDV, 3) }                                          \
   else { LMX_DEC_K(HDV, 0) }                                                                  \
   if (max_parts > 1)                                                                          \
     paged_decode_reduce_kernel<HDV><<<dim3(Hq, B), dim3(HDV), 0, stream>>>(                   \

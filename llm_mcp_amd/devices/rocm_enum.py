@@ -231,9 +231,11 @@ def parse_clock_snapshot(data: dict) -> dict:
         rec: dict = {"temp_c": {}}
         for k, v in kv.items():
             kl = k.lower()
-            if "sclk" in kl and "clock" in kl:
+            if ("sclk" in kl or "mclk" in kl) and "mhz" not in str(v).lower():
+                continue              # clock *level* indices, not frequencies
+            if "sclk" in kl:
                 rec["sclk_mhz"] = num(v)
-            elif "mclk" in kl and "clock" in kl:
+            elif "mclk" in kl:
                 rec["mclk_mhz"] = num(v)
             elif "power" in kl and "max" in kl:
                 rec["power_cap_w"] = num(v)

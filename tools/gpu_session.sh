@@ -183,6 +183,9 @@ for step in "$@"; do
     tp_graph_tests)
       run tp_graph_tests 900 python -u -m pytest tests/test_00_tp_gpu.py -x -v --timeout 400 \
           --timeout-method thread -p no:cacheprovider || exit $? ;;
+    smi_dump)
+      rocm-smi --showclocks --showpower --showmaxpower --showtemp --json > gpurun_out/smi_dump.json \
+          2>&1 || true ;;
     bench_cap16)
       run bench_cap16 600 python bench.py --steps 3 --warmup 1 --mixed-prefill-tokens 16384 \
           || exit $? ;;
