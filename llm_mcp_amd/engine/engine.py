@@ -318,11 +318,13 @@ class LLMEngine:
             self._out_evs = [torch.cuda.Event(), torch.cuda.Event()]
         self._slot = 0
         # lookahead stepping (step n+1 scheduled and launched before step n's
-        # tokens are read back): on by default for a single-GPU engine;
-        # LMX_LOOKAHEAD=0 turns it off.  In a TP group it is opt-in
-        # (LMX_LOOKAHEAD=1, the sample_all mode below) until an RCCL run with
-        # captured graphs has covered the followers' sampling path; by default
-        # a TP group steps synchronously and the leader ships the tokens.
+        # tokens are read back): on by default for GPU engines, TP groups
+        # included (every rank then samples the all-gathered logits itself:
+        # sample_all below).  The TP form runs in captured decode graphs with
+        # the peer-memory collectives inside and gives the eager path's greedy
+        # tokens (tests/test_00_tp_gpu.py::test_tp_group_captured_decode_graphs);
+        # one-GPU TP8 rehearsal: decode step 6.44 -> 6.16 ms
+        # (profiles/r5_tp_rehearsal.md).  LMX_LOOKAHEAD=0 turns it off.
         if os.environ.get("LMX_STEP_TRACE", "0") == "1":
             import collections
             self.step_trace = collections.deque(maxlen=4096)   # bounded in long runs
@@ -330,8 +332,7 @@ class LLMEngine:
         self._admit_quiet_s = float(os.environ.get("LMX_ADMIT_QUIET_MS", "2")) / 1e3
         self._admit_max_s = float(os.environ.get("LMX_ADMIT_MAX_MS", "25")) / 1e3
         la_env = os.environ.get("LMX_LOOKAHEAD", "")
-        self.lookahead = la_env == "1" or (la_env != "0" and self.device.type == "cuda"
-                                           and self.tp.size == 1)
+        self.lookahead = la_env == "1" or (la_env != "0" and self.device.type == "cuda")
         # lookahead in a TP group: the followers sample the step too (the
         # logits are all-gathered to every rank, the sampler is seeded and
         # deterministic), so every rank holds step n's tokens on its device

@@ -88,7 +88,7 @@ VARS: list[Var] = [
     Var("LMX_MAINTENANCE_INTERVAL", int, 60, "seconds between store maintenance ticks"),
     Var("LMX_JOB_STREAM_MAX_S", int, 3600, "max duration of one /v1/jobs/{id}/stream"),
     Var("LMX_SP_MIN_TOKENS", int, 0, "TP: steps with at least this many tokens run sequence-parallel (reduce-scatter/all-gather residual stream); 0 disables (default until the RCCL branch is measured on a multi-GPU node)"),
-    Var("LMX_LOOKAHEAD", str, "", "engine lookahead stepping (step n+1 scheduled and launched before step n's tokens are read back; input tokens gathered on the device): default on for a single-GPU engine, 1 forces it (also on CPU and in TP groups, where every rank then samples the all-gathered logits itself: sample_all mode), 0 off; TP groups step synchronously unless set to 1"),
+    Var("LMX_LOOKAHEAD", str, "", "engine lookahead stepping (step n+1 scheduled and launched before step n's tokens are read back; input tokens gathered on the device): default on for GPU engines, TP groups included (every rank then samples the all-gathered logits itself: sample_all mode), 1 forces it (also on CPU), 0 off"),
     Var("LMX_FUSED_PREFILL_ROPE", str, "1", "1: prefill rows' q rotation runs inside the prefill attention kernel (the rope/cache kernel only rotates k and writes the cache); 0: the rope/cache kernel rotates q in place"),
     Var("LMX_FUSED_ENCODER_ROPE", str, "0", "1: the embedding encoders (nomic) rotate q inside the attention kernel as LMX_FUSED_PREFILL_ROPE does for Llama (measured slower once: off)"),
     Var("LMX_FUSED_DECODE_ROPE", str, "1", "1: decode rows' rotary embedding and KV-cache write run inside the paged decode attention kernel; 0: separate rope/cache kernel"),
