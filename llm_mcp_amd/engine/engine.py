@@ -99,14 +99,17 @@ class EngineConfig:
     max_batched_tokens tokens -- an idle engine takes a whole burst of
     prompts in few steps -- but a step that also carries at least
     mixed_min_decodes decode rows takes at most mixed_prefill_tokens prompt
-    tokens, so a long prefill chunk cannot stall the running streams for the
-    length of a 24k-token step."""
+    tokens (when set), so a long prefill chunk cannot stall the running
+    streams for the length of a 24k-token step.  Off by default: measured on
+    one box it costs 1.6 % (16384) / 4.6 % (8192) of the headline waves'
+    throughput for a 1.6-2.2x lower worst token gap (profiles/r5_serving.md);
+    latency-first deployments set LMX_MIXED_PREFILL_TOKENS=8192."""
     model: str = "llama-3-8b"
     max_num_seqs: int = 256
     max_batched_tokens: int = field(
         default_factory=lambda: _env_int("LMX_MAX_BATCHED_TOKENS", 24576))
     mixed_prefill_tokens: int = field(
-        default_factory=lambda: _env_int("LMX_MIXED_PREFILL_TOKENS", 8192))
+        default_factory=lambda: _env_int("LMX_MIXED_PREFILL_TOKENS", 0))
     mixed_min_decodes: int = field(
         default_factory=lambda: _env_int("LMX_MIXED_MIN_DECODES", 32))
     max_model_len: int = 8192

@@ -243,7 +243,8 @@ def test_clock_snapshot_parser():
     """bench.py records sclk / mclk / power / temperature per card at the start
     and end of the timed region (rocm-smi --json, parsed tolerantly)."""
     from llm_mcp_amd.devices.rocm_enum import parse_clock_snapshot
-    data = {"card0": {"sclk clock speed:": "(2100Mhz)", "mclk clock speed:": "(1900Mhz)",
+    data = {"card0": {"sclk clock level:": "1", "mclk clock level:": "0",
+                      "sclk clock speed:": "(2100Mhz)", "mclk clock speed:": "(1900Mhz)",
                       "Current Socket Graphics Package Power (W)": "1012.0",
                       "Max Graphics Package Power (W)": "1400.0",
                       "Temperature (Sensor junction) (C)": "71.0",
