@@ -80,7 +80,7 @@ VARS: list[Var] = [
         "(overrides LMX_CHAT_MODEL / LMX_TP for `serve`)"),
     Var("LMX_MAX_BATCH", int, 256, "max concurrent sequences per engine"),
     Var("LMX_MAX_BATCHED_TOKENS", int, 24576, "tokens per engine step (an idle engine takes a burst of prompts in steps this large); bench.py and serve share it"),
-    Var("LMX_MIXED_PREFILL_TOKENS", int, 8192, "prompt tokens per step while >= LMX_MIXED_MIN_DECODES decode rows run (bounds the stall a prefill chunk puts on every decoding stream); 0 = no cap"),
+    Var("LMX_MIXED_PREFILL_TOKENS", int, 0, "prompt tokens per step while >= LMX_MIXED_MIN_DECODES decode rows run (bounds the stall a prefill chunk puts on every decoding stream; 8192 halves the closed-loop TTFT and worst token gap for ~3-5 % throughput); 0 = no cap (default)"),
     Var("LMX_MIXED_MIN_DECODES", int, 32, "decode rows that make a step 'mixed' for LMX_MIXED_PREFILL_TOKENS"),
     Var("LMX_AR_SPIN", int, 1 << 25, "peer all-reduce: polls (s_sleep 1 each) a kernel waits for a TP peer before it gives up and sets the error word (the engine then fails the step)"),
     Var("LMX_ALLOW_CLOUD", int, 0, "1: allow cloud providers (never on the GPU hot path)"),
@@ -88,6 +88,8 @@ VARS: list[Var] = [
     Var("LMX_MAINTENANCE_INTERVAL", int, 60, "seconds between store maintenance ticks"),
     Var("LMX_JOB_STREAM_MAX_S", int, 3600, "max duration of one /v1/jobs/{id}/stream"),
     Var("LMX_SP_MIN_TOKENS", int, 0, "TP: steps with at least this many tokens run sequence-parallel (reduce-scatter/all-gather residual stream); 0 disables (default until the RCCL branch is measured on a multi-GPU node)"),
+    Var("LMX_TP_MICROBATCH", str, "auto", "TP prefill micro-batches (two halves whose async RCCL all-reduces overlap the other half's compute): auto = RCCL groups at >= LMX_TP_MICROBATCH_MIN tokens, 1 always (also gloo), 0 off"),
+    Var("LMX_TP_MICROBATCH_MIN", int, 2048, "step tokens from which LMX_TP_MICROBATCH=auto splits a pure-prefill TP step"),
     Var("LMX_LOOKAHEAD", str, "", "engine lookahead stepping (step n+1 scheduled and launched before step n's tokens are read back; input tokens gathered on the device): default on for GPU engines, TP groups included (every rank then samples the all-gathered logits itself: sample_all mode), 1 forces it (also on CPU), 0 off"),
     Var("LMX_FUSED_PREFILL_ROPE", str, "1", "1: prefill rows' q rotation runs inside the prefill attention kernel (the rope/cache kernel only rotates k and writes the cache); 0: the rope/cache kernel rotates q in place"),
     Var("LMX_FUSED_ENCODER_ROPE", str, "0", "1: the embedding encoders (nomic) rotate q inside the attention kernel as LMX_FUSED_PREFILL_ROPE does for Llama (measured slower once: off)"),
@@ -107,7 +109,8 @@ VARS: list[Var] = [
     Var("LMX_ADMIT_MAX_MS", float, 25.0, "idle engine: longest wait for a burst of arrivals before the first step"),
     Var("LMX_STEP_TRACE", int, 0, "record the engine's eager (prefill / mixed) steps; bench.py logs each wave's steps"),
     Var("LMX_RESIDUAL_EPILOGUE", int, 1, "prefill O / down projections on K13 add into the residual stream in their epilogue (0: separate residual-add pass in the norm)"),
-    Var("LMX_RS_PACK_GB", float, 24.0, "budget for K14's packed copies of decode weights (beside the row-major weights prefill reads)"),
+    Var("LMX_RS_SINGLE", str, "1", "one copy of the MLP weights: gate/up and down stored only in K14's packed layout (K14 decode, K13 prefill with packed W) when the table runs them packed; 0 keeps row-major + packed copies"),
+    Var("LMX_RS_PACK_GB", float, 24.0, "budget for K14's packed copies of decode weights that are not stored packed-only (beside the row-major weights prefill reads)"),
     Var("LMX_RS", str, "1", "0 disables the K14 (register-streamed weights, csrc/kernels/rsgemm.hip) entries of the decode GEMM table"),
     Var("LMX_TP_SELFTEST_S", float, 180.0, "TP engines: seconds the start-up collective self-test may wait before the rank exits (code 3) instead of hanging"),
     Var("LMX_DGEMM_TABLE", str, "", "decode GEMM dispatch table (default llm_mcp_amd/config/dgemm_gfx950.json)"),
