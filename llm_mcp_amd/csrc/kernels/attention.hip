@@ -39,13 +39,29 @@ constexpr float LOG2E = 1.4426950408889634f;
 // serial chain.  permlane16_swap(x, x) yields {rows 0,0,2,2 ; rows 1,1,3,3} of
 // x (16-lane rows), so op(first, second) is the xor-16 reduction; the 32-lane
 // form does the same across halves.
+// v_max_f32 as one instruction (fmaxf on values hipcc cannot prove canonical
+// -- MFMA results, lane swaps -- gets a canonicalising v_max per operand)
+__device__ __forceinline__ float max2f(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
+// v_max3_f32 as one instruction (the same canonicalisation otherwise doubles
+// the row-max VALU of the softmax)
+__device__ __forceinline__ float max3f(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
 __device__ __forceinline__ float col4_max(float x) {
   const unsigned u = __float_as_uint(x);
   const auto a = __builtin_amdgcn_permlane16_swap(u, u, false, false);
-  x = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  x = max2f(__uint_as_float(a[0]), __uint_as_float(a[1]));
   const unsigned v = __float_as_uint(x);
   const auto b = __builtin_amdgcn_permlane32_swap(v, v, false, false);
-  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+  return max2f(__uint_as_float(b[0]), __uint_as_float(b[1]));
 }
 
 __device__ __forceinline__ float col4_sum(float x) {
@@ -1151,9 +1167,11 @@ __global__ void __launch_bounds__(64 * PW, 8 / PW) paged_prefill_kernel(
               x[2 * kb + (r >> 1)][r & 1] = key <= lim[n] ? x[2 * kb + (r >> 1)][r & 1] : -INFINITY;
             }
         }
-        float mx = fmaxf(x[0].x, x[0].y);
-#pragma unroll
-        for (int j = 1; j < 8; ++j) mx = fmaxf(mx, fmaxf(x[j].x, x[j].y));
+        // 16 values: a max3 tree (8 instructions, depth 3)
+        const float t0 = max3f(x[0].x, x[0].y, x[1].x), t1 = max3f(x[1].y, x[2].x, x[2].y);
+        const float t2 = max3f(x[3].x, x[3].y, x[4].x), t3 = max3f(x[4].y, x[5].x, x[5].y);
+        const float t4 = max3f(x[6].x, x[6].y, x[7].x);
+        float mx = max3f(max3f(t0, t1, t2), max3f(t3, t4, x[7].y), -INFINITY);
         mx = col4_max(mx);
         const float mx2 = mx * scale_log2;               // -inf stays -inf (scale > 0)
         // lazy rescale (guide T13): the running max m (log2 units) is raised
@@ -1161,7 +1179,7 @@ __global__ void __launch_bounds__(64 * PW, 8 / PW) paged_prefill_kernel(
         // p = 2^(x - m) <= 2^thr.  The wave rescales together (exact alpha per
         // column, 1 where it did not grow).
         const bool nd = __ballot(mx2 > m[n] + rescale_thr) != 0;
-        const float m_new = nd ? fmaxf(m[n], mx2) : m[n];
+        const float m_new = nd ? max2f(m[n], mx2) : m[n];
         const float al = (nd && m_new != -INFINITY) ? fast_exp2(m[n] - m_new) : 1.f;
         l[n] *= al;
         m[n] = m_new;
@@ -1190,7 +1208,10 @@ __global__ void __launch_bounds__(64 * PW, 8 / PW) paged_prefill_kernel(
           }
       };
       auto rescale = [&](int n) {
+        // a real (wave-uniform) branch: the lazy rescale is rare, and hipcc
+        // otherwise may speculate it into an unconditional acc *= alpha
         if (need[n]) {
+          asm volatile("" ::: "memory");
 #pragma unroll
           for (int i = 0; i < NT; ++i) acc[n][i] *= alpha[n];
         }
@@ -1237,19 +1258,42 @@ __global__ void __launch_bounds__(64 * PW, 8 / PW) paged_prefill_kernel(
     const bool need_mask = key0 + PF_TK - 1 > wave_lo;
     if (need_mask) tile_body(std::true_type{}); else tile_body(std::false_type{});
   }
+  // Epilogue: O^T through LDS, so every output row leaves as whole 16-B pieces
+  // (8 global_store_dwordx4 per lane instead of 16 dwordx2 at a 32-B stride;
+  // per-lane row-stride stores are issue-bound, guide T21).  Each wave stages
+  // its PF_NG x 16 columns into its own [column][16-B chunk] image, chunk index
+  // XOR the column's low bits (2-way conflicts on the 8-B writes, none on the
+  // 16-B reads), after a barrier that retires every wave's reads of the last
+  // K/V tile (the ring has no DMA in flight after the last tile).
+  constexpr int OCOLS = PF_NG * 16, CH = HD / 8, ROWB = HD * 2;
+  static_assert(PW * OCOLS * ROWB <= NST * 4 * PAGE * 2, "O image fits the ring");
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  char* const oimg = pf_smem + wave * OCOLS * ROWB;
 #pragma unroll
   for (int n = 0; n < PF_NG; ++n) {
-    if (!valid[n]) continue;
-    const int head = kvh * G + (c % G);
     const float inv = l[n] > 0.f ? 1.f / l[n] : 0.f;
-    bf16_t* orow = out + (long)(qbeg + qi[n]) * out_stride + (long)head * HD;
+    const int col = n * 16 + c;
 #pragma unroll
     for (int i = 0; i < NT; ++i) {
       bf16x4_t o4;
 #pragma unroll
       for (int r = 0; r < 4; ++r) o4[r] = (short)f2bf(acc[n][i][r] * inv);
-      *reinterpret_cast<bf16x4_t*>(orow + 16 * i + 4 * g) = o4;
+      const int chunk = 2 * i + (g >> 1);                 // d = 16 i + 4 g
+      *reinterpret_cast<bf16x4_t*>(oimg + col * ROWB + 16 * (chunk ^ (col & (CH - 1))) +
+                                   8 * (g & 1)) = o4;
     }
+  }
+#pragma unroll
+  for (int k = 0; k < OCOLS * CH / 64; ++k) {
+    const int e = k * 64 + lane, col = e / CH, j = e % CH;
+    const bf16x8_t v =
+        *reinterpret_cast<const bf16x8_t*>(oimg + col * ROWB + 16 * (j ^ (col & (CH - 1))));
+    const int n = col / 16, cc = col % 16;
+    const int qq = q_start + (wave * PF_NG + n) * QG + cc / G;
+    if (cc < QG * G && qq < qlen)
+      *reinterpret_cast<bf16x8_t*>(out + (long)(qbeg + qq) * out_stride +
+                                   (long)(kvh * G + cc % G) * HD + 8 * j) = v;
   }
 }
 

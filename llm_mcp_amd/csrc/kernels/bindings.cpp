@@ -56,7 +56,7 @@ int rmsnorm_slabs(void*, void*, const float*, int, long, const void*, int, int, 
 int dgemm_config(int, int*, int*);
 int dgemm_sk_pieces(int, int, int, int, int);
 int pgemm(void*, const void*, const void*, const void*, int, int, int, long, long, long, int, int,
-          int, hipStream_t);
+          int, int, hipStream_t);
 int pgemm_sk(void*, const void*, const void*, void*, void*, int, int, int, int, long, long, long,
              int, int, int, hipStream_t);
 long ar_region_bytes(long);
@@ -223,9 +223,9 @@ PYBIND11_MODULE(_lmx_kernels, m) {
   });
   // ---- K13 large-M GEMM (pgemm.hip) ----
   m.def("pgemm", [](uptr C, uptr A, uptr W, uptr bias, int M, int N, int K, long lda, long ldw,
-                    long ldc, int act, int grid, int res, uptr stream) {
+                    long ldc, int act, int grid, int res, int wpacked, uptr stream) {
     check(lmx::pgemm(P<void>(C), P<void>(A), P<void>(W), P<void>(bias), M, N, K, lda, ldw, ldc,
-                     act, grid, res, S(stream)),
+                     act, grid, res, wpacked, S(stream)),
           "pgemm");
   });
   m.def("pgemm_sk", [](uptr C, uptr A, uptr W, uptr slabs, uptr cnt, int n_cnt, int M, int N,

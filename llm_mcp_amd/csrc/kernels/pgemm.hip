@@ -38,6 +38,15 @@
 // The other measured design points (4-phase ping-pong, 4/4 DMA split, 4-wave
 // 192 x 256 tiles) live in tools/lab_kernels/pgemm_lab.hip, out of the extension.
 //
+// WP (packed weights): W is K14's packed layout (rsgemm.hip rsgemm_pack: each
+// (256-column tile, 32-column wave block, K32 block, 16-column half) one 1-KB
+// run in MFMA fragment order) instead of row-major -- one copy of a weight
+// serves the K14 decode GEMM and this prefill GEMM.  K14's wave block 2 wn + H
+// is exactly this kernel's W half-image H of wave column wn, so a half-image
+// of one K-step is 16 such runs (4 KB contiguous per wn); the DMA copies them
+// 1 KB per wave-instruction and the fragment reads are linear (lane x 16 B,
+// conflict-free without the XOR swizzle).
+//
 // Requirements (checked by the launcher): N % 256 == 0, K % 64 == 0, K >= 192,
 // lda / ldw / ldc multiples of 8 elements, 16-B aligned operands; bias (if
 // any) N <= 8192.
@@ -109,6 +118,8 @@ struct PgThr {
   int w_voff;                    // W source offset of this thread (instr / half parts uniform)
   int w_uoff[2][2];              // [half][instr]: uniform W row offset (bytes)
   int ra_off, rw_off;            // fragment row offsets in a half image (bytes)
+  int wp_voff[2][2];             // WP: [half][instr] packed-run source offset (bytes, + lane)
+  int rwp_off;                   // WP: this lane's fragment offset in a half image
   int co[2];                     // fragment chunk offsets for k32 step 0 / 1 (bytes)
   int wave, wm, wn, fr, fg;
   int ldc;
@@ -124,7 +135,7 @@ __device__ __forceinline__ void pg_tile_coords(int lin, int tiles_m, int tiles_n
   tn = r / gsize;
 }
 
-template <int H>
+template <int H, int WP = 0>
 __device__ __forceinline__ void pg_issue(char* smem, int stage, const PgLoad& L, const PgThr& T) {
   char* dst = smem + stage * PG_STAGE_B + H * PG_HALF_B + T.wave * 1024;
 #pragma unroll
@@ -132,6 +143,10 @@ __device__ __forceinline__ void pg_issue(char* smem, int stage, const PgLoad& L,
     if constexpr (H == HA0 || H == HA1) {
       __builtin_amdgcn_raw_ptr_buffer_load_lds(L.ra, (lds_void_t*)(dst + i * 8192), 16,
                                                T.a_voff[H][i], L.kbyte, 0, 0);
+    } else if constexpr (WP) {
+      // K-step s of a packed tile starts at s * 4 KB of every wave block
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(L.rw, (lds_void_t*)(dst + i * 8192), 16,
+                                               T.wp_voff[H - HW0][i], L.kbyte * 32, 0, 0);
     } else {
       __builtin_amdgcn_raw_ptr_buffer_load_lds(L.rw, (lds_void_t*)(dst + i * 8192), 16,
                                                T.w_voff, L.kbyte + T.w_uoff[H - HW0][i], 0, 0);
@@ -154,14 +169,23 @@ __device__ __forceinline__ void pg_read_a(bf16x8_t (&a)[4][2], const char* smem,
     for (int kk = 0; kk < 2; ++kk) a[i][kk] = pg_frag(b + i * 2048 + T.co[kk]);
 }
 
-template <int H>
+template <int H, int WP = 0>
 __device__ __forceinline__ void pg_read_w(bf16x8_t (&w)[2][2], const char* smem, int stage,
                                           const PgThr& T) {
-  const char* b = smem + stage * PG_STAGE_B + (HW0 + H) * PG_HALF_B + T.rw_off;
+  if constexpr (WP) {
+    // run (wn, kk, j) at wn * 4 KB + kk * 2 KB + j * 1 KB of the half image
+    const char* b = smem + stage * PG_STAGE_B + (HW0 + H) * PG_HALF_B + T.rwp_off;
 #pragma unroll
-  for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < 2; ++j)
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) w[j][kk] = pg_frag(b + j * 2048 + T.co[kk]);
+      for (int kk = 0; kk < 2; ++kk) w[j][kk] = pg_frag(b + kk * 2048 + j * 1024);
+  } else {
+    const char* b = smem + stage * PG_STAGE_B + (HW0 + H) * PG_HALF_B + T.rw_off;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) w[j][kk] = pg_frag(b + j * 2048 + T.co[kk]);
+  }
 }
 
 template <int QM, int QN, int ACT, int BIAS, class RT>
@@ -306,7 +330,7 @@ __device__ __forceinline__ void pp_mma(PpRegs& R) {
   }
 }
 
-template <int Q, int MODE, int ACT, int BIAS, int SCHED>
+template <int Q, int MODE, int ACT, int BIAS, int SCHED, int WP = 0>
 __device__ __forceinline__ void pp_phase(PpRegs& R, char* smem, int stage, const PgLoad& L1,
                                          const PgLoad& L2, const PgOut& O, const PgThr& T) {
   if constexpr (MODE == MODE_K0) {
@@ -317,15 +341,15 @@ __device__ __forceinline__ void pp_phase(PpRegs& R, char* smem, int stage, const
   }
   if constexpr (Q == 0) {
     pg_read_a<HA0>(R.a, smem, stage, T);
-    pg_read_w<0>(R.w0, smem, stage, T);
-    pg_read_w<1>(R.w1, smem, stage, T);
+    pg_read_w<0, WP>(R.w0, smem, stage, T);
+    pg_read_w<1, WP>(R.w1, smem, stage, T);
     pg_issue<HA1>(smem, stage ^ 1, L1, T);
-    if constexpr (SCHED == 1) pg_issue<HW1>(smem, stage ^ 1, L1, T);
+    if constexpr (SCHED == 1) pg_issue<HW1, WP>(smem, stage ^ 1, L1, T);
   } else {
     pg_read_a<HA1>(R.a, smem, stage, T);
     pg_issue<HA0>(smem, stage, L2, T);
-    pg_issue<HW0>(smem, stage, L2, T);
-    if constexpr (SCHED == 0) pg_issue<HW1>(smem, stage, L2, T);
+    pg_issue<HW0, WP>(smem, stage, L2, T);
+    if constexpr (SCHED == 0) pg_issue<HW1, WP>(smem, stage, L2, T);
   }
   pg_vmwait<pp_vmcnt<Q, MODE, ACT, SCHED>()>();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -336,16 +360,16 @@ __device__ __forceinline__ void pp_phase(PpRegs& R, char* smem, int stage, const
   pg_barrier();
 }
 
-template <int MODE, int ACT, int BIAS, int SCHED>
+template <int MODE, int ACT, int BIAS, int SCHED, int WP = 0>
 __device__ __forceinline__ void pp_step(PpRegs& R, char* smem, int stage, const PgLoad& L1,
                                         const PgLoad& L2, const PgOut& O, const PgThr& T) {
-  pp_phase<0, MODE, ACT, BIAS, SCHED>(R, smem, stage, L1, L2, O, T);
-  pp_phase<1, MODE, ACT, BIAS, SCHED>(R, smem, stage, L1, L2, O, T);
+  pp_phase<0, MODE, ACT, BIAS, SCHED, WP>(R, smem, stage, L1, L2, O, T);
+  pp_phase<1, MODE, ACT, BIAS, SCHED, WP>(R, smem, stage, L1, L2, O, T);
 }
 
 }  // namespace
 
-template <int ACT, int BIAS, int SCHED>
+template <int ACT, int BIAS, int SCHED, int WP = 0>
 __global__ void __launch_bounds__(PG_THREADS, 1) pgemm_pp2_kernel(
     bf16_t* __restrict__ C, const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
     const bf16_t* __restrict__ bias, int M, int N, int K, int lda, int ldw, int ldc) {
@@ -381,6 +405,19 @@ __global__ void __launch_bounds__(PG_THREADS, 1) pgemm_pp2_kernel(
     const int s = (T.fr >> 1) & 7;
     T.co[0] = 16 * (T.fg ^ s);
     T.co[1] = 16 * ((4 + T.fg) ^ s);
+    if constexpr (WP) {
+      // instruction i of wave v fills run r = 8 i + v of a half image: (wn, kk, j) =
+      // (r / 4, r / 2 % 2, r % 2), K14 wave block 2 wn + H, K32 block 2 s + kk, half j
+      const int kb = K / 32;
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int r = 8 * i + T.wave, wn = r >> 2, kk = (r >> 1) & 1, j = r & 1;
+          T.wp_voff[h][i] = (2 * wn + h) * kb * 2048 + kk * 2048 + j * 1024 + lane * 16;
+        }
+      T.rwp_off = T.wn * 4096 + lane * 16;
+    }
   }
 
   if constexpr (BIAS == 1) {
@@ -439,24 +476,24 @@ __global__ void __launch_bounds__(PG_THREADS, 1) pgemm_pp2_kernel(
   // ---- prologue: the DMA of the phases before K-step 0, in loop order
   if constexpr (SCHED == 0) {
     pg_issue<HA0>(smem, 0, L2, T);
-    pg_issue<HW0>(smem, 0, L2, T);
-    pg_issue<HW1>(smem, 0, L2, T);
+    pg_issue<HW0, WP>(smem, 0, L2, T);
+    pg_issue<HW1, WP>(smem, 0, L2, T);
     pg_issue<HA1>(smem, 0, L2, T);
     advance(L2);
     pg_issue<HA0>(smem, 1, L2, T);
-    pg_issue<HW0>(smem, 1, L2, T);
-    pg_issue<HW1>(smem, 1, L2, T);
+    pg_issue<HW0, WP>(smem, 1, L2, T);
+    pg_issue<HW1, WP>(smem, 1, L2, T);
     L1 = L2;
     advance(L2);
     pg_vmwait<8>();                 // A0, W0, W1 of K-step 0
   } else {
     pg_issue<HA0>(smem, 0, L2, T);
-    pg_issue<HW0>(smem, 0, L2, T);
+    pg_issue<HW0, WP>(smem, 0, L2, T);
     pg_issue<HA1>(smem, 0, L2, T);
-    pg_issue<HW1>(smem, 0, L2, T);
+    pg_issue<HW1, WP>(smem, 0, L2, T);
     advance(L2);
     pg_issue<HA0>(smem, 1, L2, T);
-    pg_issue<HW0>(smem, 1, L2, T);
+    pg_issue<HW0, WP>(smem, 1, L2, T);
     L1 = L2;
     advance(L2);
     pg_vmwait<4>();                 // A0, W0, W1 of K-step 0
@@ -472,18 +509,18 @@ __global__ void __launch_bounds__(PG_THREADS, 1) pgemm_pp2_kernel(
   };
   for (int t = 0; t < my_tiles; ++t) {
     if (t == 0) {
-      pp_step<MODE_FIRST, ACT, BIAS, SCHED>(R, smem, stage, L1, L2, O, T);
+      pp_step<MODE_FIRST, ACT, BIAS, SCHED, WP>(R, smem, stage, L1, L2, O, T);
       next();
-      pp_step<MODE_PLAIN, ACT, BIAS, SCHED>(R, smem, stage, L1, L2, O, T);
+      pp_step<MODE_PLAIN, ACT, BIAS, SCHED, WP>(R, smem, stage, L1, L2, O, T);
     } else {
-      pp_step<MODE_K0, ACT, BIAS, SCHED>(R, smem, stage, L1, L2, O, T);   // stores tile t-1
+      pp_step<MODE_K0, ACT, BIAS, SCHED, WP>(R, smem, stage, L1, L2, O, T);   // stores tile t-1
       next();
       set_out(O, t);
-      pp_step<MODE_K1, ACT, BIAS, SCHED>(R, smem, stage, L1, L2, O, T);
+      pp_step<MODE_K1, ACT, BIAS, SCHED, WP>(R, smem, stage, L1, L2, O, T);
     }
     next();
     for (int k = 2; k < nk; ++k) {
-      pp_step<MODE_PLAIN, ACT, BIAS, SCHED>(R, smem, stage, L1, L2, O, T);
+      pp_step<MODE_PLAIN, ACT, BIAS, SCHED, WP>(R, smem, stage, L1, L2, O, T);
       next();
     }
   }
@@ -715,28 +752,32 @@ __global__ void __launch_bounds__(PG_THREADS, 1) pgemm_sk_kernel(
 // ---- launcher ---------------------------------------------------------------
 static int g_pg_cus = 0;
 
-template <int ACT, int BIAS>
+template <int ACT, int BIAS, int WP = 0>
 static int pg_launch(bf16_t* C, const bf16_t* A, const bf16_t* W, const bf16_t* bias, int M,
                      int N, int K, int lda, int ldw, int ldc, int grid, hipStream_t stream) {
   constexpr size_t smem = PG_RING_B + (BIAS == 1 ? PG_MAX_BIAS * 2 : 0);
   static_assert(smem <= 160 * 1024, "LDS");
   static bool attr = false;
   if (!attr) {
-    const hipError_t e = hipFuncSetAttribute((const void*)pgemm_pp2_kernel<ACT, BIAS, 0>,
+    const hipError_t e = hipFuncSetAttribute((const void*)pgemm_pp2_kernel<ACT, BIAS, 0, WP>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return (int)e;
     attr = true;
   }
-  pgemm_pp2_kernel<ACT, BIAS, 0><<<dim3(grid), dim3(PG_THREADS), smem, stream>>>(
+  pgemm_pp2_kernel<ACT, BIAS, 0, WP><<<dim3(grid), dim3(PG_THREADS), smem, stream>>>(
       C, A, W, bias, M, N, K, lda, ldw, ldc);
   return (int)hipGetLastError();
 }
 
 // res 1: C is read as well -- C = bf16(C + bf16(A . W^T)) (the residual
 // stream of a pre-norm block, updated in place; act 0, no bias)
+// wpacked 1: W is rsgemm_pack's layout of the [N][K] weight (ldw == K); the
+// plain product, the residual epilogue and SwiGLU (no bias, no other act)
 int pgemm(void* C, const void* A, const void* W, const void* bias, int M, int N, int K, long lda,
-          long ldw, long ldc, int act, int grid, int res, hipStream_t stream) {
+          long ldw, long ldc, int act, int grid, int res, int wpacked, hipStream_t stream) {
   if (M <= 0) return 0;
+  if (wpacked && (bias != nullptr || ldw != K || (act != 0 && act != 3) || (res && act != 0)))
+    return -1;
   if (res && (act != 0 || bias != nullptr)) return -1;
   if (N % 256 != 0 || K % 64 != 0 || K < 192) return -1;
   if (lda % 8 || ldw % 8 || ldc % 4) return -1;
@@ -768,6 +809,11 @@ int pgemm(void* C, const void* A, const void* W, const void* bias, int M, int N,
       case 4: return pg_launch<4, 1>(C_, A_, W_, b_, M, N, K, ia, iw, ic, grid, stream);
     }
     return -1;
+  }
+  if (wpacked) {
+    if (res) return pg_launch<0, 2, 1>(C_, A_, W_, b_, M, N, K, ia, iw, ic, grid, stream);
+    if (act == 3) return pg_launch<3, 0, 1>(C_, A_, W_, b_, M, N, K, ia, iw, ic, grid, stream);
+    return pg_launch<0, 0, 1>(C_, A_, W_, b_, M, N, K, ia, iw, ic, grid, stream);
   }
   if (res) return pg_launch<0, 2>(C_, A_, W_, b_, M, N, K, ia, iw, ic, grid, stream);
   switch (act) {

@@ -250,6 +250,15 @@ class LlamaModel:
                 for L in self.w["layers"]:
                     L["w_gate_up"] = ops.interleave_gate_up(L["w_gate_up"], blk)
                 self.gu_block = blk
+            # one copy of the MLP weights: gate/up (SwiGLU16 interleave) and
+            # down stored only in K14's packed layout when every consumer
+            # reads it (K14 decode, K13 prefill with packed W; TP = 1 path)
+            if self.tp.size == 1 and not cfg.proxy_tp:
+                for L in self.w["layers"]:
+                    if self.gu_block == ops.SWIGLU16 and ops.rs_single_ok(L["w_gate_up"], True):
+                        L["w_gate_up"] = ops.rs_pack_only(L["w_gate_up"])
+                    if ops.rs_single_ok(L["w_down"]):
+                        L["w_down"] = ops.rs_pack_only(L["w_down"])
             # K14 decode shapes the table runs on packed weights get their
             # packed copies now, all or nothing per shape (row-major entries
             # need nothing)

@@ -653,6 +653,9 @@ def linear(x: torch.Tensor, w: torch.Tensor, defer: bool = False,
     hipBLASLt (bias in its epilogue).  ``defer``: the caller feeds the result to
     ``rms_norm(..., residual=)``, so a table entry for the partials-only form
     (epi 2) may return ``Partials`` and leave the K reduction to the norm."""
+    if is_packed_only(w):
+        _chk(bias is None and x.is_cuda and x.dim() == 2, "packed-only weight: plain CUDA product")
+        return _packed_product(x, w, 2 if defer and x.shape[0] <= 256 else 0)
     if x.is_cuda and x.dim() == 2:
         M, N, K = x.shape[0], w.shape[0], w.shape[1]
         if bias is None:
@@ -692,6 +695,10 @@ def linear_swiglu(x: torch.Tensor, w: torch.Tensor, block: int) -> torch.Tensor:
     library GEMM + the GLU kernel.  block 16: the in-register
     epilogue over 16-column gate/up pairs (epi 3, any tile width); otherwise
     the LDS hand-off form (epi 1, tile BN = 2 * block)."""
+    if is_packed_only(w):
+        _chk(block == SWIGLU16 and x.is_cuda and x.dim() == 2,
+             "packed-only gate/up: the SwiGLU16 interleave on CUDA")
+        return _packed_product(x, w, 3)
     if x.is_cuda and x.dim() == 2:
         if block == SWIGLU16:
             rc = rs_choice(x.shape[0], w.shape[0], w.shape[1], epi=3, w=w)
@@ -1098,8 +1105,89 @@ _RS_PACKED_BYTES = [0]             # live packed copies (a finalizer subtracts)
 def _rs_packed_of(w: torch.Tensor | None) -> torch.Tensor | None:
     """The packed copy rs_prepare attached to this weight tensor object (the
     copy lives and dies with the weight: a freed weight's address reused by
-    another tensor can never find a stale copy)."""
-    return getattr(w, "_lmx_rs_packed", None) if w is not None else None
+    another tensor can never find a stale copy); a packed-only weight
+    (rs_pack_only) is its own."""
+    if w is None:
+        return None
+    if getattr(w, "_lmx_packed_only", False):
+        return w
+    return getattr(w, "_lmx_rs_packed", None)
+
+
+# ---- one copy of the MLP weights (round 5) ---------------------------------
+# A weight whose every consumer reads K14's packed layout is stored ONLY
+# packed: decode batches (M <= 256) run K14 on it (the measured "rs" entry of
+# the batch size, else rs_default's), prefill-sized M runs K13 with packed W
+# (pgemm.hip WP).  No row-major copy is kept, so the model takes its own size
+# in HBM and the KV pool gets the rest.  LMX_RS_SINGLE=0 keeps the old
+# row-major + packed-copy scheme.
+RS_SINGLE = os.environ.get("LMX_RS_SINGLE", "1") != "0"
+
+
+def is_packed_only(w: torch.Tensor | None) -> bool:
+    return bool(getattr(w, "_lmx_packed_only", False))
+
+
+def rs_single_ok(w: torch.Tensor, swiglu: bool = False) -> bool:
+    """``w`` can be stored packed-only: a CUDA bf16 [N, K] weight of a shape
+    the K14 table runs on packed weights, with K13 (packed W) taking its
+    prefill-sized products -- the plain / residual product, or SwiGLU for a
+    gate/up weight in the 16-row interleave (``swiglu``)."""
+    if not (RS_SINGLE and w.is_cuda and w.dim() == 2 and w.dtype == torch.bfloat16
+            and w.is_contiguous()):
+        return False
+    N, K = w.shape
+    return (_rs_wants_packed(w) and pgemm_supported(N, K, ACT_SWIGLU if swiglu else 0)
+            and rs_default(1, N, K, 3 if swiglu else 0) is not None)
+
+
+def rs_pack_only(w: torch.Tensor) -> torch.Tensor:
+    """The packed-only form of ``w`` (a new tensor; drop the row-major one)."""
+    p = rsgemm_pack(w)
+    p._lmx_packed_only = True
+    return p
+
+
+def rs_unpack(p: torch.Tensor) -> torch.Tensor:
+    """Row-major [N, K] of a packed weight (references, export): packed is
+    [N/256][8 waves][K/32][2 halves][4 k-chunks][16 rows][8]."""
+    N, K = p.shape
+    v = p.reshape(N // RS_BN, 8, K // 32, 2, 4, 16, 8)
+    return v.permute(0, 1, 3, 5, 2, 4, 6).reshape(N, K)
+
+
+def dense_weight(w: torch.Tensor) -> torch.Tensor:
+    """``w`` row-major, whatever form the model keeps it in."""
+    return rs_unpack(w) if is_packed_only(w) else w
+
+
+def rs_default(M: int, N: int, K: int, epi: int) -> tuple[int, int] | None:
+    """K14 configuration of a packed-only weight at a batch size the table
+    has no entry for: 64-row tiles up to 64 rows, else 128-row; the fewest
+    K slices that give >= 192 workgroups (K-slice partials: S <= 16)."""
+    cfg = RS_NT | 2 | (RS_BM64 if M <= 64 else RS_BM128)
+    tiles = -(-M // (64 if M <= 64 else 128)) * (N // RS_BN)
+    ok = [s for s in (1, 2, 4, 8, 16) if rsgemm_supported(M, N, K, cfg, s, epi)]
+    if not ok:
+        return None
+    for s in ok:
+        if tiles * s >= 192:
+            return cfg, s
+    return cfg, ok[-1]
+
+
+def _packed_product(x: torch.Tensor, w: torch.Tensor, epi: int) -> torch.Tensor | Partials:
+    """x @ w^T for a packed-only ``w``: K14 at decode batch sizes (epi 0 / 2
+    partials / 3 SwiGLU16), K13 with packed W above 256 rows."""
+    M, N, K = x.shape[0], w.shape[0], w.shape[1]
+    if M <= 256:
+        rc = rs_choice(M, N, K, epi=epi, w=w) or rs_default(M, N, K, epi)
+        _chk(rc is not None and rsgemm_operands_ok(x, w),
+             f"packed-only weight {tuple(w.shape)}: no K14 form for M={M} epi={epi}")
+        return rsgemm(x, w, rc[0], rc[1], epi=epi)
+    if not x.is_contiguous():
+        x = x.contiguous()
+    return pgemm(x, w, act=ACT_SWIGLU if epi == 3 else ACT_NONE, packed=True)
 
 
 def _rs_wants_packed(w: torch.Tensor) -> bool:
@@ -1144,7 +1232,7 @@ def rs_prepare_all(weights: list, budget_gb: float | None = None) -> dict:
     budget = budget_gb * (1 << 30)
     groups: dict = {}
     for w in weights:
-        if w is None or not _rs_wants_packed(w):
+        if w is None or is_packed_only(w) or not _rs_wants_packed(w):
             continue
         groups.setdefault(tuple(w.shape), []).append(w)
     out = {}
@@ -1192,6 +1280,8 @@ def rsgemm(a: torch.Tensor, w: torch.Tensor, cfg: int, splits: int, epi: int = 0
         wp = _rs_packed_of(w)
         if wp is not None:
             w, packed = wp, True
+    if is_packed_only(w):
+        packed = True           # the only copy there is, whatever the entry said
     cfg = (cfg & ~RS_ROWMAJOR) | (0 if packed else RS_ROWMAJOR)
     _chk(rsgemm_supported(M, N, K, cfg, splits, epi), f"rsgemm shape M={M} N={N} K={K} "
                                                  f"cfg={cfg} S={splits}")
@@ -1262,7 +1352,7 @@ def pgemm_bias_ok(bias: torch.Tensor | None, N: int) -> bool:
 
 def pgemm(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, act: int = 0,
           out: torch.Tensor | None = None, grid: int = 0,
-          residual: torch.Tensor | None = None) -> torch.Tensor:
+          residual: torch.Tensor | None = None, packed: bool = False) -> torch.Tensor:
     """act(a @ w^T + bias) on the persistent 256x256 MFMA GEMM (any M).
     act: ACT_NONE / ACT_GELU (tanh) / ACT_SILU / ACT_GELU_ERF, or ACT_SWIGLU
     with ``w`` from ``interleave_gate_up(w, 16)`` (result [M, N/2]).
@@ -1273,6 +1363,9 @@ def pgemm(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, ac
     the kernel (tools/lab_kernels/pgemm_lab.hip) are lab-only."""
     M, K = a.shape
     N = w.shape[0]
+    packed = packed or is_packed_only(w)
+    _chk(not packed or (bias is None and act in (ACT_NONE, ACT_SWIGLU) and a.is_cuda),
+         "pgemm on packed W: plain / residual / SwiGLU products on CUDA")
     ncols = N // 2 if act == ACT_SWIGLU else N
     if residual is not None:
         _chk(act == ACT_NONE and bias is None and out is None, "pgemm residual: plain product only")
@@ -1310,7 +1403,7 @@ def pgemm(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, ac
          and out.data_ptr() % 8 == 0, "pgemm output layout")
     PGEMM_CALLS[0] += 1
     native().pgemm(_ptr(out), _ptr(a), _ptr(w), _ptr(bias), M, N, K, a.stride(0), w.stride(0),
-                   out.stride(0), act, grid, int(residual is not None), _stream())
+                   out.stride(0), act, grid, int(residual is not None), int(packed), _stream())
     return out
 
 
@@ -1330,6 +1423,8 @@ def residual_gemm_ok(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor | 
     M, N, K = x.shape[0], w.shape[0], w.shape[1]
     if residual.shape != (M, N) or not residual_gemm_layout_ok(residual):
         return False
+    if is_packed_only(w):
+        return M > 256 and pgemm_operands_ok(x, w)
     if (rs_choice(M, N, K, epi=2, w=w) is not None or rs_choice(M, N, K, w=w) is not None
             or sk_choice(M, N, K, epi=2) is not None or sk_choice(M, N, K) is not None
             or dgemm_choice(M, N, K, epi=2) is not None or dgemm_choice(M, N, K) is not None

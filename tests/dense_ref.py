@@ -4,7 +4,7 @@ import math
 
 import torch
 
-from llm_mcp_amd.ops import ref
+from llm_mcp_amd.ops import dense_weight, ref
 
 
 def dense_logits(model, tokens: list[int]) -> torch.Tensor:
@@ -31,11 +31,11 @@ def dense_logits(model, tokens: list[int]) -> torch.Tensor:
         a = ref.attention_dense(q, k, v, 1.0 / math.sqrt(D), 0).reshape(T, Hq * D)
         x = x + a @ L["wo"].float().t()
         h = ref.rms_norm(x, L["ln2"].float(), cfg.rms_eps)
-        gu = h @ L["w_gate_up"].float().t()
+        gu = h @ dense_weight(L["w_gate_up"]).float().t()
         if getattr(model, "gu_block", 0):      # fused-SwiGLU weight layout (K11)
             from llm_mcp_amd.ops import deinterleave_gate_up
             gu = deinterleave_gate_up(gu, model.gu_block)
-        x = x + ref.silu_mul(gu) @ L["w_down"].float().t()
+        x = x + ref.silu_mul(gu) @ dense_weight(L["w_down"]).float().t()
     h = ref.rms_norm(x[-1:], w["norm"].float(), cfg.rms_eps)
     return (h @ w["lm_head"].float().t())[0]
 

@@ -123,6 +123,24 @@ for step in "$@"; do
       done
       python tools/pmc_table.py gpurun_out/pmc_attn_1 gpurun_out/pmc_attn_2 gpurun_out/pmc_attn_3 \
           --match paged_decode > gpurun_out/pmc_attn_table.md 2>&1 || true ;;
+    pmc_pf)
+      # prefill attention (K3), one shape at a time (PF_SHAPES, comma list): MFMA busy,
+      # waits, LDS, L2 fetch -- one counter pass each
+      for shape in ${PF_SHAPES//,/ }; do
+        n=0
+        for pass in \
+          "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE" \
+          "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_VALU_MFMA_MOPS_BF16 GRBM_GUI_ACTIVE" \
+          "FETCH_SIZE TCC_HIT_sum GRBM_GUI_ACTIVE" ; do
+          n=$(( n + 1 ))
+          rm -rf gpurun_out/pmc_pf_${shape}_$n
+          run pmc_pf_${shape}_$n 120 timeout -s KILL 100 rocprofv3 --pmc $pass --kernel-trace \
+              -d gpurun_out/pmc_pf_${shape}_$n -o run --output-format csv -- python3 \
+              tools/prefill_attn_probe.py --shapes $shape --waves 4 --iters 10 || exit $?
+        done
+        python tools/pmc_table.py gpurun_out/pmc_pf_${shape}_1 gpurun_out/pmc_pf_${shape}_2 \
+            gpurun_out/pmc_pf_${shape}_3 --match paged_prefill > gpurun_out/pmc_pf_${shape}.md 2>&1 || true
+      done ;;
     list_counters)
       run list_counters 120 rocprofv3 -L || exit $? ;;
     tp_tests)
@@ -228,6 +246,57 @@ for step in "$@"; do
     pf_probe)
       run pf_probe 300 python -u tools/prefill_attn_probe.py \
           --shapes ${PF_SHAPES:-llama8b,llama8b_2k,llama8b_8k,nomic} --waves 4,8 || exit $? ;;
+    pf_tests)
+      run pf_tests 400 python -u -m pytest tests/test_kernels_gpu.py -k prefill -x -q \
+          --timeout 120 --timeout-method thread -p no:cacheprovider || exit $? ;;
+    pf_ab)
+      # prefill attention forms A/B: 4- vs 8-wave, 2 vs 3 ring slots
+      run pf_ab 400 python -u tools/prefill_attn_probe.py \
+          --shapes ${PF_SHAPES:-llama8b,llama8b_2k,llama8b_8k,nomic} --waves 4,8 --stages 0,3 \
+          || exit $? ;;
+    pf_abab)
+      # same-box A/B of two builds (ab/head: the committed tree's package), alternating
+      : > gpurun_out/pf_abab.log
+      for i in 1 2; do
+        for root in ${PF_ROOTS:-ab/head .}; do
+          echo "== build $root" >> gpurun_out/pf_abab.log
+          timeout -k 10 200 python -u tools/prefill_attn_probe.py --pkg-root $root \
+              --shapes ${PF_SHAPES:-llama8b,llama8b_2k,llama8b_8k,nomic} --waves 4 \
+              >> gpurun_out/pf_abab.log 2>&1 || exit $?
+        done
+      done
+      grep -E "==|prefill attn" gpurun_out/pf_abab.log ;;
+    packed_tests)
+      run packed_tests 600 python -u -m pytest tests/test_packed_weights_gpu.py tests/test_engine_gpu.py \
+          -x -v --timeout 200 --timeout-method thread -p no:cacheprovider || exit $? ;;
+    bench_two_copies)
+      LMX_RS_SINGLE=0 run bench_two_copies 600 python bench.py --steps 3 --warmup 1 || exit $? ;;
+    l70)
+      # Llama-3-70B at TP = 1 (review round 4, item 6): one copy of the MLP weights, K14 decode
+      run l70 1000 python bench.py --model llama-3-70b --concurrency 128 --max-tokens 128 \
+          --steps 2 --warmup 1 || exit $? ;;
+    l70_two)
+      LMX_RS_SINGLE=0 run l70_two 1000 python bench.py --model llama-3-70b --concurrency 128 \
+          --max-tokens 128 --steps 2 --warmup 1 || exit $? ;;
+    rs_small)
+      # K14 on packed weights at every decode batch size vs the K11 entries the
+      # table serves today: can one packed copy serve all of decode (one weight copy)?
+      : > gpurun_out/rs_small.log
+      for M in ${RS_MS:-16 32 64 96 128}; do
+        timeout -k 10 200 tools/labbin/rsgemm_lab 28672 4096 $M 3 \
+            rs:42:1,rs:42:2,rs:38:1,rs:38:2,dg:48:1,dg:17:1 >> gpurun_out/rs_small.log 2>&1 || exit $?
+        timeout -k 10 200 tools/labbin/rsgemm_lab 4096 14336 $M 2 \
+            rs:42:8,rs:42:16,rs:38:8,rs:38:16,dg:33:8,dg:53:4 >> gpurun_out/rs_small.log 2>&1 || exit $?
+        timeout -k 10 200 tools/labbin/rsgemm_lab 4096 14336 $M 0 \
+            rs:42:8,rs:42:16,rs:38:8,rs:38:16,dg:121:0,dg:97:0 >> gpurun_out/rs_small.log 2>&1 || exit $?
+      done
+      for M in ${RS70_MS:-16 64 128}; do
+        timeout -k 10 200 tools/labbin/rsgemm_lab 57344 8192 $M 3 \
+            rs:42:1,rs:42:2,rs:38:1,rs:38:2,dg:50:1 >> gpurun_out/rs_small.log 2>&1 || exit $?
+        timeout -k 10 200 tools/labbin/rsgemm_lab 8192 28672 $M 2 \
+            rs:42:8,rs:42:16,rs:38:8,rs:38:16,dg:38:8 >> gpurun_out/rs_small.log 2>&1 || exit $?
+      done
+      grep -E "shape|rs cfg|dg cfg|stream" gpurun_out/rs_small.log ;;
     attn_tests)
       run attn_tests 300 python -u -m pytest tests/test_kernels_gpu.py -k paged_decode -x -q \
           --timeout 120 --timeout-method thread -p no:cacheprovider || exit $? ;;

@@ -10,7 +10,13 @@ import math
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+# --pkg-root DIR: import llm_mcp_amd from DIR instead (a same-box A/B against another build)
+_root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if "--pkg-root" in sys.argv:
+    _i = sys.argv.index("--pkg-root")
+    _root = os.path.abspath(sys.argv[_i + 1])
+    del sys.argv[_i:_i + 2]
+sys.path.insert(0, _root)
 import torch  # noqa: E402
 
 from llm_mcp_amd import ops  # noqa: E402
@@ -91,7 +97,8 @@ def main():
                         nat.set_prefill_rescale_thr(thr)
                     if hasattr(nat, "set_prefill_stages"):
                         nat.set_prefill_stages(st)
-                    run(name, *shp, a.iters, a.ng, tag=f"thr={thr:g} nst={st} xcd={xo} w={w}", waves=w)
+                    run(name, *shp, a.iters, a.ng,
+                        tag=f"thr={thr:g} nst={st} xcd={xo} w={w}", waves=w)
     nat.set_prefill_stages(0)
     nat.set_prefill_xcd(2)
 
