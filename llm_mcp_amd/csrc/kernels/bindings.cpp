@@ -56,7 +56,8 @@ int rmsnorm_slabs(void*, void*, const float*, int, long, const void*, int, int, 
 int dgemm_config(int, int*, int*);
 int dgemm_sk_pieces(int, int, int, int, int);
 int pgemm(void*, const void*, const void*, const void*, int, int, int, long, long, long, int, int,
-          int, int, hipStream_t);
+          int, int, float*, hipStream_t);
+int row_scale(float*, const float*, int, const void*, long, int, int, float, hipStream_t);
 int pgemm_sk(void*, const void*, const void*, void*, void*, int, int, int, int, long, long, long,
              int, int, int, hipStream_t);
 long ar_region_bytes(long);
@@ -223,11 +224,17 @@ PYBIND11_MODULE(_lmx_kernels, m) {
   });
   // ---- K13 large-M GEMM (pgemm.hip) ----
   m.def("pgemm", [](uptr C, uptr A, uptr W, uptr bias, int M, int N, int K, long lda, long ldw,
-                    long ldc, int act, int grid, int res, int wpacked, uptr stream) {
+                    long ldc, int act, int grid, int res, int wpacked, uptr nrm, uptr stream) {
     check(lmx::pgemm(P<void>(C), P<void>(A), P<void>(W), P<void>(bias), M, N, K, lda, ldw, ldc,
-                     act, grid, res, wpacked, S(stream)),
+                     act, grid, res, wpacked, P<float>(nrm), S(stream)),
           "pgemm");
   });
+  m.def("row_scale", [](uptr s, uptr part, int np, uptr x, long x_stride, int M, int cols,
+                        float eps, uptr stream) {
+    check(lmx::row_scale(P<float>(s), P<float>(part), np, P<void>(x), x_stride, M, cols, eps,
+                         S(stream)),
+          "row_scale");
+  }, "RMSNorm row scales rsqrt(mean(x^2) + eps): from fp32 partials [M][P] or bf16 rows x");
   m.def("pgemm_sk", [](uptr C, uptr A, uptr W, uptr slabs, uptr cnt, int n_cnt, int M, int N,
                        int K, long lda, long ldw, long ldc, int act, int splits, int epi,
                        uptr stream) {

@@ -217,6 +217,76 @@ int rmsnorm(void* out, void* residual, const void* x, const void* w, int rows, i
   return (int)hipGetLastError();
 }
 
+// Row scales of the RMSNorm folded into the projections (pgemm.hip NRM, prefill):
+//   s[r] = rsqrt(sum_j part[r][j] / cols + eps)
+// from the producing residual GEMM's fixed per-64-column partials (P per row,
+// summed in slot order: deterministic), or -- part == null -- from the bf16
+// rows of x themselves (the first layer's input: the embedding rows).
+__global__ void __launch_bounds__(256) row_scale_part_kernel(float* __restrict__ s,
+                                                             const float* __restrict__ part,
+                                                             int M, int P, float inv_cols,
+                                                             float eps) {
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r >= M) return;
+  const float4* p = reinterpret_cast<const float4*>(part + (long)r * P);
+  float acc = 0.f;
+  for (int j = 0; j < P / 4; ++j) {
+    const float4 v = p[j];
+    acc += v.x;
+    acc += v.y;
+    acc += v.z;
+    acc += v.w;
+  }
+  s[r] = rsqrtf(acc * inv_cols + eps);
+}
+
+template <int VPT>
+__global__ void __launch_bounds__(256) row_scale_x_kernel(float* __restrict__ s,
+                                                          const bf16_t* __restrict__ x,
+                                                          long stride, int cols, float eps) {
+  __shared__ float scratch[16];
+  const bf16_t* xr = x + (long)blockIdx.x * stride;
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = threadIdx.x + i * blockDim.x;
+    if (c < cols / 8) {
+      const u16x8 a = *reinterpret_cast<const u16x8*>(xr + c * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float v = bf2f(a.v[j]);
+        ss += v * v;
+      }
+    }
+  }
+  ss = block_sum(ss, scratch);
+  if (threadIdx.x == 0) s[blockIdx.x] = rsqrtf(ss / (float)cols + eps);
+}
+
+int row_scale(float* s, const float* part, int P, const void* x, long x_stride, int M, int cols,
+              float eps, hipStream_t stream) {
+  if (M <= 0) return 0;
+  if (cols % 8 != 0) return -1;
+  if (part) {
+    if (P % 4 != 0 || P <= 0) return -1;
+    row_scale_part_kernel<<<dim3((M + 255) / 256), dim3(256), 0, stream>>>(s, part, M, P,
+                                                                          1.f / (float)cols, eps);
+  } else {
+    const int nchunk = cols / 8, threads = pick_threads(nchunk);
+    const int vpt = (nchunk + threads - 1) / threads;
+#define LMX_RSX(V)                                                                      \
+  row_scale_x_kernel<V><<<dim3(M), dim3(threads), 0, stream>>>(s, (const bf16_t*)x, x_stride, \
+                                                               cols, eps)
+    if (vpt <= 1) LMX_RSX(1);
+    else if (vpt <= 2) LMX_RSX(2);
+    else if (vpt <= 4) LMX_RSX(4);
+    else if (vpt <= 8) LMX_RSX(8);
+    else return -2;
+#undef LMX_RSX
+  }
+  return (int)hipGetLastError();
+}
+
 // workgroup cap of the slab norm (probe knob: tools/slab_norm_probe.py)
 static int g_slab_threads = 512;
 void set_slab_norm_threads(int t) { g_slab_threads = t < 64 ? 64 : (t > 512 ? 512 : t); }

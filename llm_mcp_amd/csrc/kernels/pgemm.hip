@@ -109,6 +109,7 @@ struct PgLoad {
 // output side of the tile whose quadrants are stored
 struct PgOut {
   __amdgpu_buffer_rsrc_t rc;     // C rows [m0, M)
+  __amdgpu_buffer_rsrc_t rn;     // NRM 1: row scales [m0, M); NRM 2: ssq partials of rows [m0, M)
   int n0;
 };
 
@@ -188,16 +189,34 @@ __device__ __forceinline__ void pg_read_w(bf16x8_t (&w)[2][2], const char* smem,
   }
 }
 
-template <int QM, int QN, int ACT, int BIAS, class RT>
-__device__ __forceinline__ void pg_store(const RT& R, const PgOut& O, const PgThr& T,
-                                         const char* smem) {
+// NRM (the RMSNorm folded into the projections, prefill):
+//   1  consumer: the rows of A are the raw residual stream and the norm gain is
+//      folded into W; every output row is scaled by its rsqrt(mean(x^2) + eps)
+//      (O.rn: fp32 [M], ops.row_scale) before bias / activation / SwiGLU;
+//   2  producer (residual epilogue): the sum of squares of each new residual
+//      row over this wave's 64 columns goes to O.rn [M][N / 64] (fixed
+//      slots, summed in order by the row-scale kernel: no float atomics).
+template <int QM, int QN, int ACT, int BIAS, int NRM = 0, class RT>
+__device__ __forceinline__ void pg_store(RT& R, const PgOut& O, const PgThr& T,
+                                         const char* smem, int N = 0) {
+  float rs[4];
+  if constexpr (NRM == 1) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      rs[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+          O.rn, (T.wm * 128 + QM * 64 + 16 * i + T.fr) * 4, 0, 0));
+  }
   if constexpr (ACT == 3) {
     // SwiGLU: 16-col tiles 0 (gate) and 1 (up) of the quadrant are one pair
     const int col = (O.n0 >> 1) + T.wn * 32 + QN * 16 + 4 * T.fg;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int row = T.wm * 128 + QM * 64 + 16 * i + T.fr;
-      const f32x4_t g = R.acc[QM][QN][i][0], u = R.acc[QM][QN][i][1];
+      f32x4_t g = R.acc[QM][QN][i][0], u = R.acc[QM][QN][i][1];
+      if constexpr (NRM == 1) {
+        g *= rs[i];
+        u *= rs[i];
+      }
       bf16x4_t o;
 #pragma unroll
       for (int r = 0; r < 4; ++r) o[r] = (short)f2bf(g[r] / (1.f + __expf(-g[r])) * u[r]);
@@ -239,7 +258,8 @@ __device__ __forceinline__ void pg_store(const RT& R, const PgOut& O, const PgTh
       unsigned d[2][2];
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const f32x4_t v = R.acc[QM][QN][i][j];
+        f32x4_t v = R.acc[QM][QN][i][j];
+        if constexpr (NRM == 1) v *= rs[i];
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
           float x0 = v[2 * q], x1 = v[2 * q + 1];
@@ -260,8 +280,36 @@ __device__ __forceinline__ void pg_store(const RT& R, const PgOut& O, const PgTh
           const float hi = bf2f((uint16_t)(o[e] >> 16)) + bf2f((uint16_t)(res[i][e] >> 16));
           o[e] = pack_bf16x2(lo, hi);
         }
+        if constexpr (NRM == 2) {
+          // squares of the bf16 residual values the next norm would read
+          float sq = QN == 0 ? 0.f : R.ssq[i];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float lo = bf2f((uint16_t)(o[e] & 0xffff)), hi = bf2f((uint16_t)(o[e] >> 16));
+            sq += lo * lo + hi * hi;
+          }
+          R.ssq[i] = sq;
+        }
       }
       __builtin_amdgcn_raw_buffer_store_b128(o, O.rc, (row * T.ldc + col) * 2, 0, 0);
+    }
+    if constexpr (BIAS == 2 && NRM == 2 && QN == 1) {
+      // the wave's 64 columns of each row: the 4 lanes c, c+16, c+32, c+48, then
+      // one fp32 per (row, wave column block); every lane stores (the 4 lanes of
+      // a row write the same value to the same slot), so the store count is fixed
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float x = R.ssq[i];
+        const unsigned u0 = __float_as_uint(x);
+        const auto a = __builtin_amdgcn_permlane16_swap(u0, u0, false, false);
+        x = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+        const unsigned u1 = __float_as_uint(x);
+        const auto b2 = __builtin_amdgcn_permlane32_swap(u1, u1, false, false);
+        x = __uint_as_float(b2[0]) + __uint_as_float(b2[1]);
+        const int row = T.wm * 128 + QM * 64 + 16 * i + T.fr;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x), O.rn,
+                                              (row * (N / 64) + (O.n0 >> 6) + T.wn) * 4, 0, 0);
+      }
     }
   }
 }
@@ -296,17 +344,20 @@ struct PpRegs {
   f32x4_t acc[2][2][4][2];
   bf16x8_t a[4][2];
   bf16x8_t w0[2][2], w1[2][2];
+  float ssq[4];                   // NRM 2: a quadrant pair's row sums of squares
 };
 
-template <int ACT>
-constexpr int pp_nsp() { return 2 * pg_ns<ACT>(); }   // stores per phase (two quadrants)
+template <int ACT, int NRM = 0>
+constexpr int pp_nsp() {   // stores per phase (two quadrants; + the 4 ssq partials of NRM 2)
+  return 2 * pg_ns<ACT>() + (NRM == 2 ? 4 : 0);
+}
 
 // SCHED 0: phase 0 issues A1 of s+1, phase 1 A0 W0 W1 of s+2 (2 / 6 DMA per
 // wave); SCHED 1: phase 0 A1 and W1 of s+1, phase 1 A0 W0 of s+2 (4 / 4; W1 then
 // has one phase less to land)
-template <int Q, int MODE, int ACT, int SCHED>
+template <int Q, int MODE, int ACT, int SCHED, int NRM = 0>
 constexpr int pp_vmcnt() {
-  constexpr int ns = pp_nsp<ACT>();
+  constexpr int ns = pp_nsp<ACT, NRM>();
   constexpr int b0 = SCHED == 0 ? 8 : 10, b1 = SCHED == 0 ? 8 : 4;
   if constexpr (MODE == MODE_K0) return Q == 0 ? b0 + ns : (SCHED == 0 ? b1 + 2 * ns : b1 + ns);
   else if constexpr (MODE == MODE_K1) return Q == 0 ? b0 + ns : b1;
@@ -330,13 +381,14 @@ __device__ __forceinline__ void pp_mma(PpRegs& R) {
   }
 }
 
-template <int Q, int MODE, int ACT, int BIAS, int SCHED, int WP = 0>
+template <int Q, int MODE, int ACT, int BIAS, int SCHED, int WP = 0, int NRM = 0>
 __device__ __forceinline__ void pp_phase(PpRegs& R, char* smem, int stage, const PgLoad& L1,
-                                         const PgLoad& L2, const PgOut& O, const PgThr& T) {
+                                         const PgLoad& L2, const PgOut& O, const PgThr& T,
+                                         int N = 0) {
   if constexpr (MODE == MODE_K0) {
-    pg_store<Q, 0, ACT, BIAS>(R, O, T, smem);
+    pg_store<Q, 0, ACT, BIAS, NRM>(R, O, T, smem, N);
     __builtin_amdgcn_sched_barrier(0);
-    pg_store<Q, 1, ACT, BIAS>(R, O, T, smem);
+    pg_store<Q, 1, ACT, BIAS, NRM>(R, O, T, smem, N);
     __builtin_amdgcn_sched_barrier(0);   // epilogue temporaries die before the fragment reads
   }
   if constexpr (Q == 0) {
@@ -351,7 +403,7 @@ __device__ __forceinline__ void pp_phase(PpRegs& R, char* smem, int stage, const
     pg_issue<HW0, WP>(smem, stage, L2, T);
     if constexpr (SCHED == 0) pg_issue<HW1, WP>(smem, stage, L2, T);
   }
-  pg_vmwait<pp_vmcnt<Q, MODE, ACT, SCHED>()>();
+  pg_vmwait<pp_vmcnt<Q, MODE, ACT, SCHED, NRM>()>();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   pg_barrier();
   __builtin_amdgcn_s_setprio(1);
@@ -360,19 +412,21 @@ __device__ __forceinline__ void pp_phase(PpRegs& R, char* smem, int stage, const
   pg_barrier();
 }
 
-template <int MODE, int ACT, int BIAS, int SCHED, int WP = 0>
+template <int MODE, int ACT, int BIAS, int SCHED, int WP = 0, int NRM = 0>
 __device__ __forceinline__ void pp_step(PpRegs& R, char* smem, int stage, const PgLoad& L1,
-                                        const PgLoad& L2, const PgOut& O, const PgThr& T) {
-  pp_phase<0, MODE, ACT, BIAS, SCHED, WP>(R, smem, stage, L1, L2, O, T);
-  pp_phase<1, MODE, ACT, BIAS, SCHED, WP>(R, smem, stage, L1, L2, O, T);
+                                        const PgLoad& L2, const PgOut& O, const PgThr& T,
+                                        int N = 0) {
+  pp_phase<0, MODE, ACT, BIAS, SCHED, WP, NRM>(R, smem, stage, L1, L2, O, T, N);
+  pp_phase<1, MODE, ACT, BIAS, SCHED, WP, NRM>(R, smem, stage, L1, L2, O, T, N);
 }
 
 }  // namespace
 
-template <int ACT, int BIAS, int SCHED, int WP = 0>
+template <int ACT, int BIAS, int SCHED, int WP = 0, int NRM = 0>
 __global__ void __launch_bounds__(PG_THREADS, 1) pgemm_pp2_kernel(
     bf16_t* __restrict__ C, const bf16_t* __restrict__ A, const bf16_t* __restrict__ W,
-    const bf16_t* __restrict__ bias, int M, int N, int K, int lda, int ldw, int ldc) {
+    const bf16_t* __restrict__ bias, int M, int N, int K, int lda, int ldw, int ldc,
+    float* __restrict__ nrm) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tiles_m = (M + 255) / 256, tiles_n = N / 256, ntiles = tiles_m * tiles_n;
   const int G = gridDim.x;
@@ -446,6 +500,12 @@ __global__ void __launch_bounds__(PG_THREADS, 1) pgemm_pp2_kernel(
     O.rc = __builtin_amdgcn_make_buffer_rsrc((void*)(C + (long)m0 * ldc), (short)0,
                                              (int)(cbytes < 0x7fffffffL ? cbytes : 0x7fffffffL),
                                              0x00020000);
+    if constexpr (NRM == 1)
+      O.rn = __builtin_amdgcn_make_buffer_rsrc((void*)(nrm + m0), (short)0, (M - m0) * 4,
+                                               0x00020000);
+    if constexpr (NRM == 2)
+      O.rn = __builtin_amdgcn_make_buffer_rsrc((void*)(nrm + (long)m0 * (N / 64)), (short)0,
+                                               (M - m0) * (N / 64) * 4, 0x00020000);
     O.n0 = tn * 256;
   };
   auto advance = [&](PgLoad& L) {
@@ -509,27 +569,27 @@ __global__ void __launch_bounds__(PG_THREADS, 1) pgemm_pp2_kernel(
   };
   for (int t = 0; t < my_tiles; ++t) {
     if (t == 0) {
-      pp_step<MODE_FIRST, ACT, BIAS, SCHED, WP>(R, smem, stage, L1, L2, O, T);
+      pp_step<MODE_FIRST, ACT, BIAS, SCHED, WP, NRM>(R, smem, stage, L1, L2, O, T, N);
       next();
-      pp_step<MODE_PLAIN, ACT, BIAS, SCHED, WP>(R, smem, stage, L1, L2, O, T);
+      pp_step<MODE_PLAIN, ACT, BIAS, SCHED, WP, NRM>(R, smem, stage, L1, L2, O, T, N);
     } else {
-      pp_step<MODE_K0, ACT, BIAS, SCHED, WP>(R, smem, stage, L1, L2, O, T);   // stores tile t-1
+      pp_step<MODE_K0, ACT, BIAS, SCHED, WP, NRM>(R, smem, stage, L1, L2, O, T, N);   // stores tile t-1
       next();
       set_out(O, t);
-      pp_step<MODE_K1, ACT, BIAS, SCHED, WP>(R, smem, stage, L1, L2, O, T);
+      pp_step<MODE_K1, ACT, BIAS, SCHED, WP, NRM>(R, smem, stage, L1, L2, O, T, N);
     }
     next();
     for (int k = 2; k < nk; ++k) {
-      pp_step<MODE_PLAIN, ACT, BIAS, SCHED, WP>(R, smem, stage, L1, L2, O, T);
+      pp_step<MODE_PLAIN, ACT, BIAS, SCHED, WP, NRM>(R, smem, stage, L1, L2, O, T, N);
       next();
     }
   }
   if (T.wm == 0) pg_barrier();
   pg_vmwait<0>();
-  pg_store<0, 0, ACT, BIAS>(R, O, T, smem);
-  pg_store<0, 1, ACT, BIAS>(R, O, T, smem);
-  pg_store<1, 0, ACT, BIAS>(R, O, T, smem);
-  pg_store<1, 1, ACT, BIAS>(R, O, T, smem);
+  pg_store<0, 0, ACT, BIAS, NRM>(R, O, T, smem, N);
+  pg_store<0, 1, ACT, BIAS, NRM>(R, O, T, smem, N);
+  pg_store<1, 0, ACT, BIAS, NRM>(R, O, T, smem, N);
+  pg_store<1, 1, ACT, BIAS, NRM>(R, O, T, smem, N);
 }
 
 // ============================================================================
@@ -752,20 +812,21 @@ __global__ void __launch_bounds__(PG_THREADS, 1) pgemm_sk_kernel(
 // ---- launcher ---------------------------------------------------------------
 static int g_pg_cus = 0;
 
-template <int ACT, int BIAS, int WP = 0>
+template <int ACT, int BIAS, int WP = 0, int NRM = 0>
 static int pg_launch(bf16_t* C, const bf16_t* A, const bf16_t* W, const bf16_t* bias, int M,
-                     int N, int K, int lda, int ldw, int ldc, int grid, hipStream_t stream) {
+                     int N, int K, int lda, int ldw, int ldc, int grid, hipStream_t stream,
+                     float* nrm = nullptr) {
   constexpr size_t smem = PG_RING_B + (BIAS == 1 ? PG_MAX_BIAS * 2 : 0);
   static_assert(smem <= 160 * 1024, "LDS");
   static bool attr = false;
   if (!attr) {
-    const hipError_t e = hipFuncSetAttribute((const void*)pgemm_pp2_kernel<ACT, BIAS, 0, WP>,
+    const hipError_t e = hipFuncSetAttribute((const void*)pgemm_pp2_kernel<ACT, BIAS, 0, WP, NRM>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return (int)e;
     attr = true;
   }
-  pgemm_pp2_kernel<ACT, BIAS, 0, WP><<<dim3(grid), dim3(PG_THREADS), smem, stream>>>(
-      C, A, W, bias, M, N, K, lda, ldw, ldc);
+  pgemm_pp2_kernel<ACT, BIAS, 0, WP, NRM><<<dim3(grid), dim3(PG_THREADS), smem, stream>>>(
+      C, A, W, bias, M, N, K, lda, ldw, ldc, nrm);
   return (int)hipGetLastError();
 }
 
@@ -773,11 +834,16 @@ static int pg_launch(bf16_t* C, const bf16_t* A, const bf16_t* W, const bf16_t* 
 // stream of a pre-norm block, updated in place; act 0, no bias)
 // wpacked 1: W is rsgemm_pack's layout of the [N][K] weight (ldw == K); the
 // plain product, the residual epilogue and SwiGLU (no bias, no other act)
+// nrm (the RMSNorm folded into the projections): with res, the new residual
+// rows' sums of squares per 64-column block go to nrm [M][N / 64]; without,
+// the output rows are scaled by nrm [M] (plain product or SwiGLU, no bias)
 int pgemm(void* C, const void* A, const void* W, const void* bias, int M, int N, int K, long lda,
-          long ldw, long ldc, int act, int grid, int res, int wpacked, hipStream_t stream) {
+          long ldw, long ldc, int act, int grid, int res, int wpacked, float* nrm,
+          hipStream_t stream) {
   if (M <= 0) return 0;
   if (wpacked && (bias != nullptr || ldw != K || (act != 0 && act != 3) || (res && act != 0)))
     return -1;
+  if (nrm && (bias != nullptr || (act != 0 && act != 3) || (res && act != 0))) return -1;
   if (res && (act != 0 || bias != nullptr)) return -1;
   if (N % 256 != 0 || K % 64 != 0 || K < 192) return -1;
   if (lda % 8 || ldw % 8 || ldc % 4) return -1;
@@ -809,6 +875,16 @@ int pgemm(void* C, const void* A, const void* W, const void* bias, int M, int N,
       case 4: return pg_launch<4, 1>(C_, A_, W_, b_, M, N, K, ia, iw, ic, grid, stream);
     }
     return -1;
+  }
+  if (nrm) {
+    // the folded-norm forms: producer (residual) and consumers (QKV plain,
+    // gate/up SwiGLU), row-major or packed W
+#define LMX_PG_N(WPV)                                                                        \
+    if (res) return pg_launch<0, 2, WPV, 2>(C_, A_, W_, b_, M, N, K, ia, iw, ic, grid, stream, nrm); \
+    if (act == 3) return pg_launch<3, 0, WPV, 1>(C_, A_, W_, b_, M, N, K, ia, iw, ic, grid, stream, nrm); \
+    return pg_launch<0, 0, WPV, 1>(C_, A_, W_, b_, M, N, K, ia, iw, ic, grid, stream, nrm);
+    if (wpacked) { LMX_PG_N(1) } else { LMX_PG_N(0) }
+#undef LMX_PG_N
   }
   if (wpacked) {
     if (res) return pg_launch<0, 2, 1>(C_, A_, W_, b_, M, N, K, ia, iw, ic, grid, stream);

@@ -244,6 +244,18 @@ class LlamaModel:
         # fused-SwiGLU decode GEMM (K11 epi=1): gate|up rows interleaved per
         # BN/2 channels when the measured dispatch table uses it for this shape
         self.gu_block = 0
+        # the RMSNorm gains folded into the projections they feed (QKV <- ln1,
+        # gate/up <- ln2; W' = W diag(g) at load, the norms then run with unit
+        # gains): prefill steps may then skip the per-layer norm pass entirely
+        # (_norm_fold_step) -- TP = 1 only
+        self.norm_folded = False
+        if (self.device.type == "cuda" and self.tp.size == 1 and not cfg.proxy_tp
+                and os.environ.get("LMX_NORM_FOLD", "0") == "1"):
+            for L in self.w["layers"]:
+                for g, wk in (("ln1", "wqkv"), ("ln2", "w_gate_up")):
+                    L[wk] = (L[wk].float() * L[g].float()[None, :]).to(L[wk].dtype)
+                    L[g] = torch.ones_like(L[g])
+            self.norm_folded = True
         if self.device.type == "cuda":
             blk = ops.swiglu_block(2 * self.I, cfg.hidden_size)
             if blk:
@@ -433,6 +445,23 @@ class LlamaModel:
             logits = logits[:, :self.cfg.vocab_size]
         return logits
 
+    def _norm_fold_step(self, T: int, fold: bool) -> bool:
+        """This step runs the folded norm: gains folded at load, TP = 1, and
+        every projection of the layer on K13 (prefill-sized T, no QKV bias,
+        the 16-row gate/up interleave, residual epilogues on)."""
+        if not (self.norm_folded and fold and ops.RESIDUAL_EPILOGUE and T > 256
+                and self.gu_block == ops.SWIGLU16):
+            return False
+        L = self.w["layers"][0]
+        if "bqkv" in L:
+            return False
+        d = self.cfg.hidden_size
+        shapes = ((L["wqkv"], ops.ACT_NONE), (L["wo"], ops.ACT_NONE),
+                  (L["w_gate_up"], ops.ACT_SWIGLU), (L["w_down"], ops.ACT_NONE))
+        return d % 64 == 0 and all(
+            ops.large_gemm_backend(T, w.shape[0], w.shape[1], act) == "k13"
+            and ops.pgemm_supported(w.shape[0], w.shape[1], act) for w, act in shapes)
+
     def forward(self, inp: StepInputs, k_caches: list, v_caches: list,
                 decode_ws: ops.DecodeWorkspace | None, part_tokens: int = 512) -> torch.Tensor:
         """Returns logits [len(sample_rows), vocab] (bf16)."""
@@ -465,19 +494,37 @@ class LlamaModel:
         fold = solo and not sp
         pending = None            # h of this layer from the previous layer's fused AR + norm
         layers = w["layers"]
+        # the folded norm (prefill-sized TP = 1 steps): no norm pass at all --
+        # O / down's residual epilogue leaves per-64-column sums of squares,
+        # ops.row_scale turns them into rsqrt(mean + eps), and QKV / gate-up
+        # (gains folded into their weights) scale their output rows by it
+        nf = self._norm_fold_step(T, fold)
+        part = (torch.empty((T, cfg.hidden_size // 64), dtype=torch.float32, device=self.device)
+                if nf else None)
+        s_row = None
         for li, L in enumerate(layers):
+            h = None
             if pending is not None:
                 h, pending = pending, None
             elif residual is None:
                 residual = x
-                h = ops.rms_norm(x, L["ln1"], cfg.rms_eps)
+                if nf:
+                    s_row = ops.row_scale(cfg.rms_eps, x=x)
+                else:
+                    h = ops.rms_norm(x, L["ln1"], cfg.rms_eps)
             elif x is None:
-                h = ops.rms_norm(residual, L["ln1"], cfg.rms_eps)
+                if nf:
+                    s_row = ops.row_scale(cfg.rms_eps, part=part, cols=cfg.hidden_size)
+                else:
+                    h = ops.rms_norm(residual, L["ln1"], cfg.rms_eps)
             else:
                 h = ops.rms_norm(x, L["ln1"], cfg.rms_eps, residual=residual)
             if sp:
                 h = tp.all_gather_rows(h)[:T]
-            qkv = ops.linear(h, L["wqkv"], bias=L.get("bqkv"))   # Qwen2: biased q/k/v
+            if nf:
+                qkv = ops.pgemm(residual, L["wqkv"], row_scale=s_row)
+            else:
+                qkv = ops.linear(h, L["wqkv"], bias=L.get("bqkv"))   # Qwen2: biased q/k/v
             kc, vc = k_caches[li], v_caches[li]
             # decode rows: rotary + cache write fused into the decode attention
             # kernel (one launch and one boundary fewer per layer); prefill rows
@@ -514,7 +561,10 @@ class LlamaModel:
                                             else None)
             # TP = 1: the O projection may hand its split-K partials straight
             # to the residual-add RMSNorm (ops.Partials; K11 epi 2)
-            if fold and ops.residual_gemm_ok(attn, L["wo"], residual):
+            if nf:
+                ops.pgemm(attn, L["wo"], residual=residual, ssq=part)
+                s_row = ops.row_scale(cfg.rms_eps, part=part, cols=cfg.hidden_size)
+            elif fold and ops.residual_gemm_ok(attn, L["wo"], residual):
                 ops.pgemm(attn, L["wo"], residual=residual)
                 h = ops.rms_norm(residual, L["ln2"], cfg.rms_eps)
             else:
@@ -528,7 +578,9 @@ class LlamaModel:
                     h = ops.rms_norm(o, L["ln2"], cfg.rms_eps, residual=residual)
             if sp:
                 h = tp.all_gather_rows(h)[:T]
-            if self.gu_block:
+            if nf:
+                a = ops.pgemm(residual, L["w_gate_up"], act=ops.ACT_SWIGLU, row_scale=s_row)
+            elif self.gu_block:
                 a = ops.linear_swiglu(h, L["w_gate_up"], self.gu_block)
             else:
                 a = ops.silu_mul(ops.linear(h, L["w_gate_up"]))
@@ -536,6 +588,10 @@ class LlamaModel:
             # last layer: the final norm runs on the sampled rows only)
             # the last layer's partials go to the final norm when every row is
             # sampled (pure decode): no gather of the sampled rows is needed
+            if nf:
+                ops.pgemm(a, L["w_down"], residual=residual, ssq=part)
+                x = None
+                continue
             if fold and ops.residual_gemm_ok(a, L["w_down"], residual):
                 ops.pgemm(a, L["w_down"], residual=residual)
                 x = None

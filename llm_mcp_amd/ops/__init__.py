@@ -1352,7 +1352,9 @@ def pgemm_bias_ok(bias: torch.Tensor | None, N: int) -> bool:
 
 def pgemm(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, act: int = 0,
           out: torch.Tensor | None = None, grid: int = 0,
-          residual: torch.Tensor | None = None, packed: bool = False) -> torch.Tensor:
+          residual: torch.Tensor | None = None, packed: bool = False,
+          row_scale: torch.Tensor | None = None,
+          ssq: torch.Tensor | None = None) -> torch.Tensor:
     """act(a @ w^T + bias) on the persistent 256x256 MFMA GEMM (any M).
     act: ACT_NONE / ACT_GELU (tanh) / ACT_SILU / ACT_GELU_ERF, or ACT_SWIGLU
     with ``w`` from ``interleave_gate_up(w, 16)`` (result [M, N/2]).
@@ -1374,7 +1376,19 @@ def pgemm(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, ac
         if residual is not None:
             y = ref.gemm_nt(a, w, None, ACT_NONE, None)
             residual.copy_((residual.float() + y.float()).to(residual.dtype))
+            if ssq is not None:
+                ssq.copy_(residual.float().pow(2).view(M, N // 64, 64).sum(-1))
             return residual
+        if row_scale is not None:
+            y = (a.float() @ w.float().t()) * row_scale.float()[:, None]
+            if act == ACT_SWIGLU:
+                y = y.view(M, N // 32, 2, 16)
+                y = (torch.nn.functional.silu(y[:, :, 0]) * y[:, :, 1]).reshape(M, ncols)
+            y = y.to(a.dtype)
+            if out is not None:
+                out.copy_(y)
+                return out
+            return y
         if act == ACT_SWIGLU:
             y = (a.float() @ w.float().t()).view(M, N // 32, 2, 16)
             y = (torch.nn.functional.silu(y[:, :, 0]) * y[:, :, 1]).reshape(M, ncols).to(a.dtype)
@@ -1397,14 +1411,53 @@ def pgemm(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, ac
     if residual is not None:
         _chk(residual_gemm_layout_ok(residual), "pgemm residual layout (16-B rows)")
         out = residual
+    nrm = None
+    if ssq is not None:
+        # the RMSNorm folded into the projections: the new residual rows' sums
+        # of squares per 64-column block, for row_scale
+        _chk(residual is not None and ssq.dtype == torch.float32 and ssq.is_contiguous()
+             and ssq.shape == (M, N // 64), "pgemm ssq: fp32 [M, N/64] with the residual epilogue")
+        nrm = ssq
+    if row_scale is not None:
+        _chk(residual is None and bias is None and row_scale.dtype == torch.float32
+             and row_scale.is_contiguous() and row_scale.numel() == M,
+             "pgemm row_scale: fp32 [M], plain product or SwiGLU")
+        _chk(nrm is None, "pgemm: row_scale and ssq are exclusive")
+        nrm = row_scale
     if out is None:
         out = torch.empty((M, ncols), dtype=a.dtype, device=a.device)
     _chk(out.shape == (M, ncols) and out.stride(1) == 1 and out.stride(0) % 4 == 0
          and out.data_ptr() % 8 == 0, "pgemm output layout")
     PGEMM_CALLS[0] += 1
     native().pgemm(_ptr(out), _ptr(a), _ptr(w), _ptr(bias), M, N, K, a.stride(0), w.stride(0),
-                   out.stride(0), act, grid, int(residual is not None), int(packed), _stream())
+                   out.stride(0), act, grid, int(residual is not None), int(packed), _ptr(nrm),
+                   _stream())
     return out
+
+
+def row_scale(eps: float, part: torch.Tensor | None = None,
+              x: torch.Tensor | None = None, cols: int | None = None) -> torch.Tensor:
+    """RMSNorm row scales rsqrt(mean(x^2) + eps), fp32 [M]: from the fixed
+    per-64-column partial sums a residual epilogue wrote (``part`` [M, P],
+    summed in slot order; ``cols`` = the row length), or from the bf16 rows of
+    ``x`` (the first layer's input)."""
+    if part is not None:
+        M, P = part.shape
+        cols = cols or 64 * P
+        if not part.is_cuda:
+            return torch.rsqrt(part.float().sum(-1) / cols + eps)
+        s = torch.empty(M, dtype=torch.float32, device=part.device)
+        native().row_scale(_ptr(s), _ptr(part), P, 0, 0, M, cols, float(eps), _stream())
+        return s
+    _chk(x is not None and x.dim() == 2, "row_scale: partials or rows")
+    M, cols = x.shape
+    if not x.is_cuda:
+        return torch.rsqrt(x.float().pow(2).mean(-1) + eps)
+    _bf16(x, "x")
+    _chk(x.stride(1) == 1 and cols % 8 == 0, "row_scale rows")
+    s = torch.empty(M, dtype=torch.float32, device=x.device)
+    native().row_scale(_ptr(s), 0, 0, _ptr(x), x.stride(0), M, cols, float(eps), _stream())
+    return s
 
 
 def residual_gemm_layout_ok(residual: torch.Tensor) -> bool:

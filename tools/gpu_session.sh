@@ -278,6 +278,15 @@ for step in "$@"; do
     l70_two)
       LMX_RS_SINGLE=0 run l70_two 1000 python bench.py --model llama-3-70b --concurrency 128 \
           --max-tokens 128 --steps 2 --warmup 1 || exit $? ;;
+    nf_tests)
+      run nf_tests 600 python -u -m pytest tests/test_norm_fold_gpu.py tests/test_packed_weights_gpu.py \
+          tests/test_engine_gpu.py tests/test_kernels_gpu.py -k "norm or fold or pgemm or packed or engine or prefill or lookahead" \
+          -x -q --timeout 200 --timeout-method thread -p no:cacheprovider || exit $? ;;
+    bench_fold)
+      LMX_NORM_FOLD=1 run bench_fold 600 python bench.py --steps 3 --warmup 1 || exit $? ;;
+    long8k_fold)
+      LMX_NORM_FOLD=1 run long8k_fold 900 python bench.py --steps 2 --warmup 1 --prompt-len 7680 \
+          --max-tokens 256 --concurrency 64 || exit $? ;;
     rs_small)
       # K14 on packed weights at every decode batch size vs the K11 entries the
       # table serves today: can one packed copy serve all of decode (one weight copy)?
