@@ -212,11 +212,11 @@ __device__ __forceinline__ void pg_store(RT& R, const PgOut& O, const PgThr& T,
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int row = T.wm * 128 + QM * 64 + 16 * i + T.fr;
-      f32x4_t g = R.acc[QM][QN][i][0], u = R.acc[QM][QN][i][1];
-      if constexpr (NRM == 1) {
-        g *= rs[i];
-        u *= rs[i];
+      if constexpr (NRM == 1) {       // in place: no second copy of the quadrant live
+        R.acc[QM][QN][i][0] *= rs[i];
+        R.acc[QM][QN][i][1] *= rs[i];
       }
+      const f32x4_t g = R.acc[QM][QN][i][0], u = R.acc[QM][QN][i][1];
       bf16x4_t o;
 #pragma unroll
       for (int r = 0; r < 4; ++r) o[r] = (short)f2bf(g[r] / (1.f + __expf(-g[r])) * u[r]);
@@ -258,8 +258,8 @@ __device__ __forceinline__ void pg_store(RT& R, const PgOut& O, const PgThr& T,
       unsigned d[2][2];
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        f32x4_t v = R.acc[QM][QN][i][j];
-        if constexpr (NRM == 1) v *= rs[i];
+        if constexpr (NRM == 1) R.acc[QM][QN][i][j] *= rs[i];
+        const f32x4_t v = R.acc[QM][QN][i][j];
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
           float x0 = v[2 * q], x1 = v[2 * q + 1];

@@ -250,7 +250,7 @@ class LlamaModel:
         # (_norm_fold_step) -- TP = 1 only
         self.norm_folded = False
         if (self.device.type == "cuda" and self.tp.size == 1 and not cfg.proxy_tp
-                and os.environ.get("LMX_NORM_FOLD", "0") == "1"):
+                and os.environ.get("LMX_NORM_FOLD", "1") != "0"):
             for L in self.w["layers"]:
                 for g, wk in (("ln1", "wqkv"), ("ln2", "w_gate_up")):
                     L[wk] = (L[wk].float() * L[g].float()[None, :]).to(L[wk].dtype)

@@ -282,10 +282,10 @@ for step in "$@"; do
       run nf_tests 600 python -u -m pytest tests/test_norm_fold_gpu.py tests/test_packed_weights_gpu.py \
           tests/test_engine_gpu.py tests/test_kernels_gpu.py -k "norm or fold or pgemm or packed or engine or prefill or lookahead" \
           -x -q --timeout 200 --timeout-method thread -p no:cacheprovider || exit $? ;;
-    bench_fold)
-      LMX_NORM_FOLD=1 run bench_fold 600 python bench.py --steps 3 --warmup 1 || exit $? ;;
-    long8k_fold)
-      LMX_NORM_FOLD=1 run long8k_fold 900 python bench.py --steps 2 --warmup 1 --prompt-len 7680 \
+    bench_nofold)
+      LMX_NORM_FOLD=0 run bench_nofold 600 python bench.py --steps 3 --warmup 1 || exit $? ;;
+    long8k_nofold)
+      LMX_NORM_FOLD=0 run long8k_nofold 900 python bench.py --steps 2 --warmup 1 --prompt-len 7680 \
           --max-tokens 256 --concurrency 64 || exit $? ;;
     rs_small)
       # K14 on packed weights at every decode batch size vs the K11 entries the
