@@ -287,6 +287,10 @@ for step in "$@"; do
     long8k_nofold)
       LMX_NORM_FOLD=0 run long8k_nofold 900 python bench.py --steps 2 --warmup 1 --prompt-len 7680 \
           --max-tokens 256 --concurrency 64 || exit $? ;;
+    qkv70tp1)
+      # Llama-3-70B TP = 1 QKV (10240 x 8192) at every decode bucket (M 17-48 were library)
+      run qkv70tp1 900 python -u -m llm_mcp_amd.bench.dgemm_bench --model llama-3-70b --tp 1 \
+          --only qkv --json gpurun_out/qkv70tp1_rows.json || exit $? ;;
     rs_small)
       # K14 on packed weights at every decode batch size vs the K11 entries the
       # table serves today: can one packed copy serve all of decode (one weight copy)?
