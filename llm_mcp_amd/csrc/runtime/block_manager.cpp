@@ -1,5 +1,7 @@
 #include "block_manager.h"
 
+#include <algorithm>
+#include <functional>
 #include <stdexcept>
 
 namespace lmxrt {
@@ -23,7 +25,7 @@ BlockManager::BlockManager(int num_blocks, int block_size, bool enable_prefix_ca
     : num_blocks_(num_blocks), block_size_(block_size), prefix_(enable_prefix_cache) {
   if (num_blocks <= 0 || block_size <= 0) throw std::invalid_argument("bad block manager size");
   free_.reserve(num_blocks);
-  for (int i = num_blocks - 1; i >= 0; --i) free_.push_back(i);
+  for (int i = 0; i < num_blocks; ++i) free_.push_back(i);  // ascending = a min-heap
   ref_.assign(num_blocks, 0);
   page_hash_.assign(num_blocks, 0);
   lru_pos_.resize(num_blocks);
@@ -33,6 +35,7 @@ BlockManager::BlockManager(int num_blocks, int block_size, bool enable_prefix_ca
 int BlockManager::alloc_page() {
   int p;
   if (!free_.empty()) {
+    std::pop_heap(free_.begin(), free_.end(), std::greater<int32_t>());
     p = free_.back();
     free_.pop_back();
   } else if (!lru_.empty()) {
@@ -60,6 +63,7 @@ void BlockManager::release_page(int p) {
   } else {
     page_hash_[p] = 0;
     free_.push_back(p);
+    std::push_heap(free_.begin(), free_.end(), std::greater<int32_t>());
   }
 }
 

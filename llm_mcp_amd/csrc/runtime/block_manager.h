@@ -2,7 +2,12 @@
 //
 // Owns the mapping sequence -> list of physical KV pages of the device cache
 // (see csrc/kernels/rope_cache.hip for the page layout) with
-//   * O(1) allocate / free from a free stack,
+//   * O(log n) allocate / free from a min-heap of free pages: a page is always
+//     the lowest free one, so a prompt's pages form ascending runs and every
+//     wave reuses the same compact region instead of the previous wave's pages
+//     in reverse release order (a LIFO stack); level with the stack on the
+//     headline (same box, profiles/r5_serving.md), but the layout no longer
+//     depends on the release history,
 //   * reference counts, so full pages can be shared between sequences,
 //   * automatic prefix caching: every *full* page is identified by a chained
 //     64-bit hash of its tokens (h_i = H(h_{i-1}, tokens of page i)); a new
@@ -51,7 +56,7 @@ class BlockManager {
 
   int num_blocks_, block_size_;
   bool prefix_;
-  std::vector<int32_t> free_;
+  std::vector<int32_t> free_;         // min-heap (std::greater)
   std::vector<int32_t> ref_;
   std::vector<uint64_t> page_hash_;   // 0 = not cached
   std::unordered_map<uint64_t, int32_t> cache_;  // hash -> page

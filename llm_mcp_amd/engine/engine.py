@@ -115,7 +115,8 @@ class EngineConfig:
     max_model_len: int = 8192
     kv_fraction: float = 0.6        # of free HBM after weights
     kv_cache_gb: float | None = None
-    prefix_cache: bool = True
+    prefix_cache: bool = field(
+        default_factory=lambda: _env_int("LMX_PREFIX_CACHE", 1) != 0)
     use_graphs: bool = True
     part_tokens: int = 512
     seed: int = 0

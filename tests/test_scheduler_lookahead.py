@@ -239,3 +239,19 @@ def test_mixed_step_prefill_cap():
     s2.add(100, list(range(20, 1020)), 10, [], True, 0)
     p = s2.schedule(16)
     assert p["num_tokens"] - p["num_decode"] == 1000
+
+
+def test_block_manager_hands_out_lowest_free_pages():
+    """KV pages come from a min-heap: a prompt's pages are one ascending run and a
+    new wave reuses the lowest freed pages, in order (block_manager.h)."""
+    bm = runtime().BlockManager(64, 16, False)
+    assert bm.ensure(1, 16 * 5) and bm.ensure(2, 16 * 3)
+    assert list(bm.table(1)) == [0, 1, 2, 3, 4] and list(bm.table(2)) == [5, 6, 7]
+    bm.free_seq(1)
+    assert bm.ensure(3, 16 * 6)
+    assert list(bm.table(3)) == [0, 1, 2, 3, 4, 8]
+    bm.free_seq(2)
+    bm.free_seq(3)
+    assert bm.ensure(4, 16 * 9)
+    assert list(bm.table(4)) == list(range(9))
+    assert bm.num_free == 64 - 9

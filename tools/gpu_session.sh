@@ -291,6 +291,29 @@ for step in "$@"; do
       # Llama-3-70B TP = 1 QKV (10240 x 8192) at every decode bucket (M 17-48 were library)
       run qkv70tp1 900 python -u -m llm_mcp_amd.bench.dgemm_bench --model llama-3-70b --tp 1 \
           --only qkv --json gpurun_out/qkv70tp1_rows.json || exit $? ;;
+    lm70tp1)
+      run lm70tp1 900 python -u -m llm_mcp_amd.bench.dgemm_bench --model llama-3-70b --tp 1 \
+          --only lm_head --json gpurun_out/lm70tp1_rows.json || exit $? ;;
+    bench20)
+      # the driver's own command (20 timed waves after 5 warm-up waves)
+      run bench20 900 python bench.py --gpus 1 --steps 20 --warmup 5 || exit $? ;;
+    pc_ab)
+      # same box, alternating: prefix cache on / off (LMX_PREFIX_CACHE), 12 waves each
+      for i in 1 2; do
+        LMX_PREFIX_CACHE=1 run pc_ab_on_$i 600 python bench.py --steps 12 --warmup 2 || exit $?
+        LMX_PREFIX_CACHE=0 run pc_ab_off_$i 600 python bench.py --steps 12 --warmup 2 || exit $?
+      done ;;
+    alloc_ab)
+      # same box, alternating: KV pages from the min-heap (this tree) / the old LIFO stack
+      # (ab/lifo, a copy of the tree with the old block manager), 12 waves each
+      for i in 1 2; do
+        run alloc_ab_heap_$i 600 python bench.py --steps 12 --warmup 2 || exit $?
+        (cd ab/lifo && mkdir -p gpurun_out && run alloc_ab_lifo_$i 600 python bench.py --steps 12 --warmup 2) || exit $?
+        cp ab/lifo/gpurun_out/alloc_ab_lifo_$i.log gpurun_out/ || exit $?
+      done ;;
+    bench20_nopc)
+      # the same without the prefix cache (KV pages recycled in place every wave)
+      LMX_PREFIX_CACHE=0 run bench20_nopc 900 python bench.py --gpus 1 --steps 20 --warmup 5 || exit $? ;;
     rs_small)
       # K14 on packed weights at every decode batch size vs the K11 entries the
       # table serves today: can one packed copy serve all of decode (one weight copy)?
