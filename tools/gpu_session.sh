@@ -311,6 +311,15 @@ for step in "$@"; do
         (cd ab/lifo && mkdir -p gpurun_out && run alloc_ab_lifo_$i 600 python bench.py --steps 12 --warmup 2) || exit $?
         cp ab/lifo/gpurun_out/alloc_ab_lifo_$i.log gpurun_out/ || exit $?
       done ;;
+    overlap)
+      # decode attention under the decode GEMMs: serial vs two streams (tools/overlap_probe.py)
+      : > gpurun_out/overlap.log
+      for w in gateup down qkv; do
+        for m in 128 256; do
+          timeout -k 10 120 python -u tools/overlap_probe.py --what $w --rows $m >> gpurun_out/overlap.log 2>&1 || exit $?
+        done
+      done
+      cat gpurun_out/overlap.log ;;
     bench20_nopc)
       # the same without the prefix cache (KV pages recycled in place every wave)
       LMX_PREFIX_CACHE=0 run bench20_nopc 900 python bench.py --gpus 1 --steps 20 --warmup 5 || exit $? ;;
