@@ -320,6 +320,19 @@ for step in "$@"; do
         done
       done
       cat gpurun_out/overlap.log ;;
+    rs70tp1)
+      # K14 (packed) on the 70B TP = 1 QKV (10240 x 8192, bf16 out) and O (8192 x 8192, fp32
+      # partials for the slab norm) at the decode buckets, against the K11 entries served today
+      : > gpurun_out/rs70tp1.log
+      for M in ${RS_MS:-32 64 96 128}; do
+        timeout -k 10 200 tools/labbin/rsgemm_lab 10240 8192 $M 0 \
+            rs:42:1,rs:42:2,rs:42:4,rs:38:1,rs:38:2,rs:38:4,rs:46:2,dg:106:0,dg:117:0 >> gpurun_out/rs70tp1.log 2>&1 || exit $?
+        timeout -k 10 200 tools/labbin/rsgemm_lab 10240 8192 $M 2 \
+            rs:42:2,rs:42:4,rs:38:2,rs:38:4 >> gpurun_out/rs70tp1.log 2>&1 || exit $?
+        timeout -k 10 200 tools/labbin/rsgemm_lab 8192 8192 $M 2 \
+            rs:42:2,rs:42:4,rs:42:8,rs:38:2,rs:38:4,rs:38:8,dg:42:4,dg:63:4 >> gpurun_out/rs70tp1.log 2>&1 || exit $?
+      done
+      cat gpurun_out/rs70tp1.log ;;
     bench20_nopc)
       # the same without the prefix cache (KV pages recycled in place every wave)
       LMX_PREFIX_CACHE=0 run bench20_nopc 900 python bench.py --gpus 1 --steps 20 --warmup 5 || exit $? ;;
