@@ -333,6 +333,18 @@ for step in "$@"; do
             rs:42:2,rs:42:4,rs:42:8,rs:38:2,rs:38:4,rs:38:8,dg:42:4,dg:63:4 >> gpurun_out/rs70tp1.log 2>&1 || exit $?
       done
       cat gpurun_out/rs70tp1.log ;;
+    sample_ab)
+      # K6 sampling at the headline shape: this tree vs ab/old (a copy with the previous kernel)
+      : > gpurun_out/sample_ab.log
+      for i in 1 2; do
+        timeout -k 10 120 python -u tools/sample_probe.py >> gpurun_out/sample_ab.log 2>&1 || exit $?
+        echo "--- ab/old" >> gpurun_out/sample_ab.log
+        (cd ab/old && timeout -k 10 120 python -u tools/sample_probe.py) >> gpurun_out/sample_ab.log 2>&1 || exit $?
+        echo "--- this tree" >> gpurun_out/sample_ab.log
+      done
+      timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -k "sample or tp8_lm_head" -x -q --timeout 120 \
+          --timeout-method thread -p no:cacheprovider >> gpurun_out/sample_ab.log 2>&1 || exit $?
+      cat gpurun_out/sample_ab.log ;;
     bench20_nopc)
       # the same without the prefix cache (KV pages recycled in place every wave)
       LMX_PREFIX_CACHE=0 run bench20_nopc 900 python bench.py --gpus 1 --steps 20 --warmup 5 || exit $? ;;
