@@ -34,6 +34,20 @@ def test_chunked_prefill_and_prefix_cache_consistent():
     assert e.sched.prefix_hits > 0
 
 
+def test_prefix_cache_switch(monkeypatch):
+    """LMX_PREFIX_CACHE=0: finished pages go straight back to the free list, a
+    repeated prompt is recomputed (no hits) and gives the same tokens."""
+    monkeypatch.setenv("LMX_PREFIX_CACHE", "0")
+    assert EngineConfig().prefix_cache is False
+    e = _engine(max_batched_tokens=40)
+    p = list(range(1, 96))
+    a = e.generate([p], SamplingParams(temperature=0, max_tokens=4, ignore_eos=True))[0]
+    b = e.generate([p], SamplingParams(temperature=0, max_tokens=4, ignore_eos=True))[0]
+    assert a == b and e.sched.prefix_hits == 0
+    monkeypatch.setenv("LMX_PREFIX_CACHE", "1")
+    assert EngineConfig().prefix_cache is True
+
+
 def test_preemption_recompute_keeps_outputs():
     # tiny KV: 16 blocks x 32 tokens; 4 sequences of ~120 tokens cannot all fit
     e = _engine(kv_cache_gb=None)
