@@ -42,6 +42,7 @@ import os
 import socket
 import subprocess
 import sys
+import threading
 import time
 
 BASELINE = None  # the reference publishes no throughput number (BASELINE.json "published": {})
@@ -504,8 +505,19 @@ def closed(a, rank, world, n_eng, lgs, barrier, sync, ecfg) -> None:
             else:
                 p.stdin.write(f"closed {a.closed_warmup} {a.duration}\n")
             p.stdin.flush()
+        # a heartbeat line a minute, so a long window (--duration 600: a soak run)
+        # is not mistaken for a hung process by whoever watches the log
+        done = threading.Event()
+
+        def beat():
+            t0 = time.time()
+            while not done.wait(60.0):
+                log(f"{a.load} window: {time.time() - t0:.0f} s of "
+                    f"{a.closed_warmup + a.duration:g} s")
+        threading.Thread(target=beat, daemon=True).start()
         for p in lgs:
             parts.append(json.loads(p.stdout.readline()))
+        done.set()
     barrier()
     if rank == 0:
         tok = sum(x["tokens"] for x in parts)

@@ -345,6 +345,10 @@ for step in "$@"; do
       timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -k "sample or tp8_lm_head" -x -q --timeout 120 \
           --timeout-method thread -p no:cacheprovider >> gpurun_out/sample_ab.log 2>&1 || exit $?
       cat gpurun_out/sample_ab.log ;;
+    soak)
+      # 10-minute closed-loop window at 256 streams with the shipped defaults: the KV pool
+      # fills, the prefix cache evicts, and throughput / latency must hold
+      run soak 900 python bench.py --load closed --duration ${SOAK_S:-600} --closed-warmup 10 || exit $? ;;
     bench20_nopc)
       # the same without the prefix cache (KV pages recycled in place every wave)
       LMX_PREFIX_CACHE=0 run bench20_nopc 900 python bench.py --gpus 1 --steps 20 --warmup 5 || exit $? ;;
