@@ -326,7 +326,7 @@ def main() -> None:
     cpu0 = {k: cpu_s(v) for k, v in procs.items()}
 
     if a.load in ("closed", "poisson"):
-        closed(a, rank, world, n_eng, lgs, barrier, sync, engine.ecfg)
+        closed(a, rank, world, n_eng, lgs, barrier, sync, engine.ecfg, engine)
         shutdown(a, world, lgs, apis, server, ready_files, engine, follower)
         return
 
@@ -489,7 +489,7 @@ def gap_percentiles(parts) -> dict:
     return {f"token_gap_p{q}_ms": round(hist_percentile(h, q) * 1e3, 2) for q in (50, 95, 99)}
 
 
-def closed(a, rank, world, n_eng, lgs, barrier, sync, ecfg) -> None:
+def closed(a, rank, world, n_eng, lgs, barrier, sync, ecfg, engine=None) -> None:
     """--load closed / poisson: one steady-load window through the same front
     door; prints its own JSON line (metric tagged "closed loop" / "poisson")."""
     from llm_mcp_amd.bench.loadgen import percentile
@@ -511,9 +511,15 @@ def closed(a, rank, world, n_eng, lgs, barrier, sync, ecfg) -> None:
 
         def beat():
             t0 = time.time()
+            g0 = engine.stats["generated_tokens"] if engine is not None else 0
             while not done.wait(60.0):
+                extra = ""
+                if engine is not None:      # this rank's engine, over the last minute
+                    g = engine.stats["generated_tokens"]
+                    extra = f"; engine r0 {(g - g0) / 60.0:,.0f} generated tok/s"
+                    g0 = g
                 log(f"{a.load} window: {time.time() - t0:.0f} s of "
-                    f"{a.closed_warmup + a.duration:g} s")
+                    f"{a.closed_warmup + a.duration:g} s{extra}")
         threading.Thread(target=beat, daemon=True).start()
         for p in lgs:
             parts.append(json.loads(p.stdout.readline()))
