@@ -349,6 +349,19 @@ for step in "$@"; do
       # 10-minute closed-loop window at 256 streams with the shipped defaults: the KV pool
       # fills, the prefix cache evicts, and throughput / latency must hold
       run soak 900 python bench.py --load closed --duration ${SOAK_S:-600} --closed-warmup 10 || exit $? ;;
+    attn70tp1)
+      # Llama-3-70B TP = 1 decode attention: 128 rows x 8 kv heads x 8-query groups, the bench's
+      # contexts (512-640): split-K partitions vs one per segment (1024 segments on 256 CUs)
+      : > gpurun_out/attn70tp1.log
+      for parts in 1 2 3; do
+        for pt in 256 384; do
+          timeout -k 10 120 python -u tools/decode_attn_probe.py --layout engine --rope --hq 64 \
+              --hkv 8 --batch 128 --ctx-lo 512 --ctx-hi 640 --parts $parts --part-tokens $pt \
+              --modes 0,10 --iters 40 >> gpurun_out/attn70tp1.log 2>&1 || exit $?
+          [ $parts = 1 ] && break
+        done
+      done
+      cat gpurun_out/attn70tp1.log ;;
     bench20_nopc)
       # the same without the prefix cache (KV pages recycled in place every wave)
       LMX_PREFIX_CACHE=0 run bench20_nopc 900 python bench.py --gpus 1 --steps 20 --warmup 5 || exit $? ;;
