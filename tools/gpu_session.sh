@@ -2,7 +2,11 @@
 # One gpurun session: each GPU step under its own time limit, chained so the
 # first failure ends the call.  Usage (on the GPU box, from the repo root):
 #   bash tools/gpu_session.sh STEP [STEP...]
-# Steps: tests | bench1 | rehearse2 | prof
+# Steps: the case labels below (tests, smoke, bench1, bench20, soak, rehearse*, tp8s, the
+# probes and counter passes).  Same-box A/B steps (pf_ab, pf_abab, alloc_ab, sample_ab, ...)
+# also run a second package tree under ab/<name> (git-ignored, built on the CPU side before
+# the call): a copy of the repo with the older sources checked out and
+# `python -c "from llm_mcp_amd import build; build.build_kernels(); build.build_runtime()"`.
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
