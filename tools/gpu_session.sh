@@ -171,6 +171,13 @@ for step in "$@"; do
       run config5det 1100 python -u -m llm_mcp_amd.bench.serving_bench mixed --gpus 0 \
           --replicas-per-gpu 2 --fault gpu_error@300 --fault-device gpu0.r1 --runs 3 \
           --jobs 4096 --concurrency 256 --sync-every 4 --max-tokens 64 --chars 512 || exit $? ;;
+    config5r4)
+      # round 4's recorded config-5 command (profiles/r4_config5.md): the faulty worker fails
+      # once (its first life), then the run waits for its recovery; median of 3 runs
+      run config5r4 1100 python -u -m llm_mcp_amd.bench.serving_bench mixed --gpus 0 \
+          --replicas-per-gpu 2 --fault gpu_error@300 --fault-device gpu0.r1 --fault-lives 1 \
+          --runs 3 --jobs 4096 --concurrency 256 --sync-every 4 --max-tokens 64 --chars 512 \
+          --await-recovery 150 || exit $? ;;
     config5b)
       # config 5, round 4: the faulty worker's first life fails at its 300th
       # engine step (LMX_FAULT_LIVES=1), the breaker trips from the released
