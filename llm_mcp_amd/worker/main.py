@@ -18,6 +18,9 @@ import signal
 log = logging.getLogger("lmx.worker")
 
 
+SHARED_GPU_BATCHED_TOKENS = 8192   # prefill budget of a chat engine sharing its GPU
+
+
 def build_parser():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpu", type=int, default=int(os.environ.get("LOCAL_RANK", "0")))
@@ -82,6 +85,13 @@ def main(argv=None):
                             max_model_len=a.max_model_len, kv_fraction=a.kv_fraction)
         if a.max_batched_tokens:
             ecfg.max_batched_tokens = a.max_batched_tokens
+        elif (a.embed_model or a.replica) and not os.environ.get("LMX_MAX_BATCHED_TOKENS"):
+            # the GPU is shared: with an embedding engine in this worker, or with other
+            # workers on the same card (--replica), a 24k-token prefill step (~235 ms)
+            # holds the other engine's batches behind it.  Config 5 (two chat + embed
+            # workers on one GPU, faults on one): 58.5 -> 76.9 jobs/s median at 8192
+            # (profiles/r5_config5.md).  A chat-only worker keeps the bench's budget.
+            ecfg.max_batched_tokens = SHARED_GPU_BATCHED_TOKENS
         if a.embed_model:
             ecfg.kv_fraction = min(ecfg.kv_fraction, 0.5)
         engine = LLMEngine(ecfg, device=dev, model_cfg=cfg, weights=weights)
