@@ -89,8 +89,9 @@ def main(argv=None):
             # the GPU is shared: with an embedding engine in this worker, or with other
             # workers on the same card (--replica), a 24k-token prefill step (~235 ms)
             # holds the other engine's batches behind it.  Config 5 (two chat + embed
-            # workers on one GPU, faults on one): 58.5 -> 76.9 jobs/s median at 8192
-            # (profiles/r5_config5.md).  A chat-only worker keeps the bench's budget.
+            # workers on one GPU, faults on one): 73.2 jobs/s mean over nine runs at 8192,
+            # 67.6 over six at 24576, with a wide run-to-run spread (profiles/r5_config5.md).
+            # A chat-only worker keeps the bench's budget.
             ecfg.max_batched_tokens = SHARED_GPU_BATCHED_TOKENS
         if a.embed_model:
             ecfg.kv_fraction = min(ecfg.kv_fraction, 0.5)
