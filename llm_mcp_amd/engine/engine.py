@@ -1071,16 +1071,28 @@ class LLMEngine:
 
     def _peer_check(self) -> None:
         """TP: a peer-memory collective of this rank that gave up waiting for a
-        peer (bounded spin) produced a wrong sum; its error word is copied to
-        pinned memory behind every step and read (as of an earlier step) here.
-        Raised as a HIP error: the engine turns unhealthy and the worker is
-        restarted instead of serving corrupted tokens."""
+        peer (bounded spin) produced a wrong sum.  Behind every step its error
+        word is copied to pinned memory, ahead of the step's token D2H copy on
+        the same stream, so it has landed once the tokens have: the ranks that
+        emit tokens check it where the tokens are read back (``_peer_raise``
+        in ``_finish_fetch``), before any of that step's tokens reach the
+        scheduler or a client.  Followers emit nothing and raise as soon as
+        they see it.  Raised as a HIP error: the engine turns unhealthy and
+        the worker is restarted instead of serving corrupted tokens."""
         peer = self.tp.peer
-        if peer is None or self.device.type != "cuda":
+        if peer is None:
             return
-        if peer.failed():
+        if not (self.is_leader or self.sample_all):
+            self._peer_raise()
+        if self.device.type == "cuda":
+            peer.check_async(torch.cuda.current_stream(self.device))
+        else:
+            peer.check_async(None)
+
+    def _peer_raise(self) -> None:
+        peer = self.tp.peer
+        if peer is not None and peer.failed():
             raise RuntimeError("HIP error: peer all-reduce timed out waiting for a TP peer")
-        peer.check_async(torch.cuda.current_stream(self.device))
 
     def _start_fetch(self, tok: torch.Tensor, lp: torch.Tensor, n: int) -> int:
         """Queue the D2H copy of the sampled tokens/logprobs into pinned
@@ -1097,8 +1109,10 @@ class LLMEngine:
     def _finish_fetch(self, n: int, k: int | None = None):
         k = self._slot if k is None else k
         if self.device.type != "cuda":
+            self._peer_raise()
             return self._fetch_cpu[k]
         self._out_evs[k].synchronize()
+        self._peer_raise()      # this step's collectives were sound (see _peer_check)
         h = self._hout_np[k]
         return h[0, :n].copy(), h[1, :n].view(np.float32).copy()
 

@@ -153,11 +153,19 @@ class TPContext:
         """Start the sum of ``t`` over the group in place; returns a handle
         whose ``wait()`` orders the caller's stream after it (RCCL: the
         collective runs on its own stream, overlapping the compute issued
-        meanwhile).  Host-staged (gloo) and peer paths complete here."""
-        if self.size > 1 and self.peer is None and not self._host_staged(t):
+        meanwhile).  Host-staged (gloo) and peer-slot messages complete here;
+        a message the peer slot does not hold (prefill sizes) goes to RCCL
+        asynchronously even when the group has the peer kernel."""
+        if self.size > 1 and self._async_rccl(t):
             return torch.distributed.all_reduce(t, group=self.group, async_op=True)
         self.all_reduce(t)
         return _Done()
+
+    def _async_rccl(self, t: torch.Tensor) -> bool:
+        """``all_reduce_async`` hands ``t`` to RCCL with async_op=True."""
+        if self.peer is not None and self.peer.supports(t):
+            return False
+        return not self._host_staged(t)
 
     def all_reduce_norm(self, t: torch.Tensor, w: torch.Tensor, eps: float,
                         residual: torch.Tensor) -> torch.Tensor:
@@ -240,6 +248,11 @@ class LlamaModel:
         self.fuse_prefill_rope = os.environ.get("LMX_FUSED_PREFILL_ROPE", "1") == "1"
         if weights is None:
             weights = self._random_weights(seed)
+        else:
+            # the folds / interleaves / packing below replace entries of the
+            # layer dicts: work on copies so the caller's dict keeps the
+            # checkpoint's tensors (export_weights gives the served form back)
+            weights = {**weights, "layers": [dict(L) for L in weights["layers"]]}
         self.w = weights
         # fused-SwiGLU decode GEMM (K11 epi=1): gate|up rows interleaved per
         # BN/2 channels when the measured dispatch table uses it for this shape
@@ -319,6 +332,21 @@ class LlamaModel:
             lm_head = rnd(vs, d)
         return {"embed": embed, "norm": torch.ones(d, dtype=dt, device=dev), "lm_head": lm_head,
                 "layers": layers}
+
+    def export_weights(self) -> dict:
+        """The served weights as a plain fused dict (``weights.save_hf_llama``,
+        ``shard_llama``): row-major (K14-packed copies unpacked), gate/up back
+        in [gate; up] row order.  With the norm gains folded at load the
+        projections carry them and ln1 / ln2 are ones: the exact model that is
+        served, and loading it folds nothing further."""
+        layers = []
+        for L in self.w["layers"]:
+            d = {k: ops.dense_weight(v) for k, v in L.items()}
+            if self.gu_block:
+                d["w_gate_up"] = ops.deinterleave_gate_up(d["w_gate_up"], self.gu_block)
+            layers.append(d)
+        return {"embed": self.w["embed"], "norm": self.w["norm"],
+                "lm_head": ops.dense_weight(self.w["lm_head"]), "layers": layers}
 
     def weight_bytes(self) -> int:
         n = 0

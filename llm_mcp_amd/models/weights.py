@@ -196,8 +196,16 @@ def load_llama_weights(path: str, cfg: LlamaConfig, device, rank: int = 0, size:
 
 def save_hf_llama(full: dict, cfg: LlamaConfig, path: str) -> None:
     """Write a full fused weight dict as a HF-layout safetensors checkpoint
-    (tests, and exporting random-init models for other tools)."""
+    (tests, and exporting random-init models for other tools).  ``full`` may
+    be a ``LlamaModel``: its served weights are exported
+    (``LlamaModel.export_weights``: packed copies unpacked, gate/up rows
+    de-interleaved).  A raw model dict with packed-only tensors is refused."""
     from safetensors.torch import save_file
+    from .. import ops
+    if hasattr(full, "export_weights"):
+        full = full.export_weights()
+    if any(ops.is_packed_only(v) for L in full["layers"] for v in L.values()):
+        raise ValueError("packed weights: export LlamaModel.export_weights(), not model.w")
     os.makedirs(path, exist_ok=True)
     D = cfg.head_dim
     qn, kvn, I = cfg.num_heads * D, cfg.num_kv_heads * D, cfg.intermediate_size

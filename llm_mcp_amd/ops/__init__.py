@@ -502,6 +502,13 @@ def interleave_gate_up(w: torch.Tensor, block: int = 64) -> torch.Tensor:
     return w.view(2, I // block, block, d).transpose(0, 1).reshape(I2, d).contiguous()
 
 
+def deinterleave_gate_up(w: torch.Tensor, block: int) -> torch.Tensor:
+    """Inverse of ``interleave_gate_up``: back to [gate(I); up(I)] rows."""
+    I2, d = w.shape
+    I = I2 // 2
+    return w.view(I // block, 2, block, d).transpose(0, 1).reshape(I2, d).contiguous()
+
+
 def gemm_nt(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, act: int = 0,
             residual: torch.Tensor | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
     """act(a @ w^T + bias) (+ residual) on the hand-written MFMA GEMM.

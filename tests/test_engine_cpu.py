@@ -273,3 +273,43 @@ def test_admission_window_gathers_a_burst(monkeypatch):
     assert first[3] == 6 * 20           # all six prompts in the first step
     first = run(0.0)
     assert first[3] < 6 * 20            # window off: only what had arrived
+
+
+def test_peer_failure_withholds_that_steps_tokens():
+    """A TP peer collective that timed out (its error word set) during step n:
+    the error is raised where step n's tokens are read back, so none of them
+    reaches the scheduler or the event sink -- only the earlier, sound steps'
+    tokens were emitted (the check used to run at launch and read
+    an older step's word)."""
+    import pytest
+    from llm_mcp_amd.engine.engine import GenRequest
+
+    class StubPeer:
+        # the word goes bad during the armed step's kernels: it is visible
+        # only through the copy enqueued behind that step (check_async)
+        armed = bad = False
+
+        def failed(self):
+            return self.bad
+
+        def check_async(self, stream):
+            self.bad = self.bad or self.armed
+
+    e = _engine()
+    peer = StubPeer()
+    e.tp.peer = peer
+    got = []
+    e.event_sink = got.extend
+    e.submit(GenRequest(list(range(10, 30)), SamplingParams(temperature=0, max_tokens=8,
+                                                            ignore_eos=True)))
+    ok_steps = 0
+    for _ in range(3):
+        assert e.step()
+        ok_steps += 1
+    peer.armed = True
+    with pytest.raises(RuntimeError, match="peer all-reduce"):
+        e.step()
+    # step k's events are flushed during step k + 1: every sound step's token
+    # and none of the failing step's
+    assert len(got) == ok_steps
+    assert e.stats["generated_tokens"] == ok_steps

@@ -74,3 +74,53 @@ def test_packed_only_weights_every_batch_size(M):
         torch.testing.assert_close(r.float(), res.float() + y, atol=5e-2, rtol=3e-2)
     else:
         assert M <= 256
+
+
+def test_gpu_model_export_round_trip(tmp_path):
+    """A TP = 1 model built on the GPU folds its norm gains, interleaves
+    gate/up and stores the MLP weights packed-only -- in its own copies: the
+    caller's weight dict is untouched, and ``save_hf_llama(model)`` exports
+    the served weights (unpacked, de-interleaved) so a model loaded from the
+    export serves bitwise the same weights and the same logits."""
+    from llm_mcp_amd.models import config as mc
+    from llm_mcp_amd.models.llama import LlamaModel, StepInputs
+    from llm_mcp_amd.models.weights import load_llama_weights, save_hf_llama
+    cfg = mc.resolve("llama-3-8b@L2")
+    src = LlamaModel(cfg, DEV, seed=3)
+    given = src.export_weights()
+    # non-unit gains, so the fold is visible
+    for L in given["layers"]:
+        L["ln1"] = (1 + 0.1 * torch.randn_like(L["ln1"].float())).to(L["ln1"].dtype)
+        L["ln2"] = (1 + 0.1 * torch.randn_like(L["ln2"].float())).to(L["ln2"].dtype)
+    before = {(i, k): v for i, L in enumerate(given["layers"]) for k, v in L.items()}
+    m = LlamaModel(cfg, DEV, weights=given)
+    assert all(given["layers"][i][k] is v for (i, k), v in before.items())
+    if any(ops.is_packed_only(v) for L in m.w["layers"] for v in L.values()):
+        with pytest.raises(ValueError, match="packed"):
+            save_hf_llama(m.w, cfg, str(tmp_path / "raw"))
+    save_hf_llama(m, cfg, str(tmp_path))
+    m2 = LlamaModel(cfg, DEV, weights=load_llama_weights(str(tmp_path), cfg, DEV))
+    e1, e2 = m.export_weights(), m2.export_weights()
+    for L1, L2 in zip(e1["layers"], e2["layers"]):
+        for k in L1:
+            assert torch.equal(L1[k], L2[k]), k
+    # and the two models give bitwise the same logits
+    T = 7
+    ids = torch.arange(100, 100 + T, dtype=torch.int32, device=DEV)
+    pos = torch.arange(T, dtype=torch.int32, device=DEV)
+    nb = 4
+    D = cfg.head_dim
+    kc = [torch.zeros(nb, cfg.num_kv_heads, 32, D, dtype=torch.bfloat16, device=DEV)
+          for _ in range(cfg.num_layers)]
+    vc = [torch.zeros(nb, cfg.num_kv_heads, 8, D, 4, dtype=torch.bfloat16, device=DEV)
+          for _ in range(cfg.num_layers)]
+    qpt = ops.prefill_q_per_tile(cfg.num_heads, cfg.num_kv_heads, D)
+    tiles = torch.tensor([v for q0 in range(0, T, qpt) for v in (0, q0)], dtype=torch.int32,
+                         device=DEV)
+    inp = StepInputs(ids, pos, pos.clone(), 0, torch.zeros(1, 1, dtype=torch.int32, device=DEV),
+                     torch.tensor([T], dtype=torch.int32, device=DEV),
+                     torch.tensor([0, T], dtype=torch.int32, device=DEV), tiles,
+                     torch.tensor([T - 1], dtype=torch.int64, device=DEV), T, 1)
+    l1 = m.forward(inp, kc, vc, None).float()
+    l2 = m2.forward(inp, [k.zero_() for k in kc], [v.zero_() for v in vc], None).float()
+    assert torch.equal(l1, l2)

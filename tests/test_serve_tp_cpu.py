@@ -85,7 +85,7 @@ def test_serve_tp8_chat_matches_dense_and_survives_a_leader_kill():
     cfg = mc.resolve("tiny-llama-tp8")
     model = LlamaModel(cfg, "cpu", seed=11)
     ckpt = tempfile.mkdtemp()
-    save_hf_llama(model.w, cfg, ckpt)
+    save_hf_llama(model, cfg, ckpt)
     d = tempfile.mkdtemp()
     http, grpc = _port(), _port()
     url = f"http://127.0.0.1:{http}"

@@ -65,7 +65,7 @@ def full_model(tmp_path_factory):
     cfg = mc.resolve("tiny-llama")
     m = LlamaModel(cfg, "cpu", seed=3)
     path = str(tmp_path_factory.mktemp("ckpt"))
-    save_hf_llama(m.w, cfg, path)
+    save_hf_llama(m, cfg, path)
     return m, path
 
 
@@ -154,7 +154,7 @@ def test_tp2_generation_matches_single_process(full_model, sp_min_tokens, lookah
 def test_qwen_loader_roundtrip_with_bias(tmp_path):
     cfg = mc.resolve("tiny-qwen")
     m = LlamaModel(cfg, "cpu", seed=5)
-    save_hf_llama(m.w, cfg, str(tmp_path))
+    save_hf_llama(m, cfg, str(tmp_path))
     assert mc.from_hf_config(str(tmp_path / "config.json")).qkv_bias
     a = load_llama_weights(str(tmp_path), cfg, "cpu")
     for la, lb in zip(a["layers"], m.w["layers"]):
@@ -164,7 +164,7 @@ def test_qwen_loader_roundtrip_with_bias(tmp_path):
 def test_qwen3_loader_roundtrip_and_tp_shards(tmp_path):
     cfg = mc.resolve("tiny-qwen3")
     m = LlamaModel(cfg, "cpu", seed=9)
-    save_hf_llama(m.w, cfg, str(tmp_path))
+    save_hf_llama(m, cfg, str(tmp_path))
     hf = mc.from_hf_config(str(tmp_path / "config.json"))
     assert hf.qk_norm and not hf.qkv_bias and hf.family == "qwen3"
     for size in (1, 2):
@@ -182,7 +182,7 @@ def full_model_tp8(tmp_path_factory):
     cfg = mc.resolve("tiny-llama-tp8")
     m = LlamaModel(cfg, "cpu", seed=5)
     path = str(tmp_path_factory.mktemp("ckpt8"))
-    save_hf_llama(m.w, cfg, path)
+    save_hf_llama(m, cfg, path)
     return m, path
 
 
@@ -323,3 +323,43 @@ def test_prefill_microbatches_match_one_batch(full_model, monkeypatch):
     assert b.sample_rows.tolist() == [4, 13]
     got = m._forward_tp_mb(inp, j, kc, vc).float()
     torch.testing.assert_close(got, ref, atol=1e-2, rtol=1e-2)
+
+
+def test_all_reduce_async_takes_rccl_beside_the_peer_kernel(monkeypatch):
+    """An RCCL TP group with the peer all-reduce installed (the 8-GPU default):
+    messages the peer slot holds run on the peer kernel, anything larger (the
+    prefill micro-batch all-reduces) must go to RCCL with async_op=True, or
+    the two micro-batches of _forward_tp_mb serialise."""
+    import torch.distributed as dist
+    from llm_mcp_amd.models.llama import TPContext, _Done
+
+    calls = []
+
+    class StubPeer:
+        slot = 1 << 10
+
+        def supports(self, t):
+            return t.numel() * t.element_size() <= self.slot
+
+        def __call__(self, t):
+            calls.append(("peer", t.numel()))
+            return t
+
+    class Handle:
+        def wait(self):
+            return True
+
+    def fake_all_reduce(t, group=None, async_op=False, **kw):
+        calls.append(("rccl_async" if async_op else "rccl_sync", t.numel()))
+        return Handle() if async_op else None
+
+    monkeypatch.setattr(dist, "get_backend", lambda group=None: "nccl")
+    monkeypatch.setattr(dist, "all_reduce", fake_all_reduce)
+    tp = TPContext(rank=0, size=8, group=object())
+    tp.peer = StubPeer()
+    small = torch.zeros(256)            # 1 KB fp32: inside the slot
+    big = torch.zeros(64, 1024)         # 256 KB: prefill-sized
+    h_small = tp.all_reduce_async(small)
+    h_big = tp.all_reduce_async(big)
+    assert isinstance(h_small, _Done) and isinstance(h_big, Handle)
+    assert calls == [("peer", 256), ("rccl_async", 64 * 1024)]
