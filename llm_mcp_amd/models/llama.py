@@ -343,7 +343,7 @@ class LlamaModel:
         for L in self.w["layers"]:
             d = {k: ops.dense_weight(v) for k, v in L.items()}
             if self.gu_block:
-                d["w_gate_up"] = ops.deinterleave_gate_up(d["w_gate_up"], self.gu_block)
+                d["w_gate_up"] = ops.deinterleave_gate_up_rows(d["w_gate_up"], self.gu_block)
             layers.append(d)
         return {"embed": self.w["embed"], "norm": self.w["norm"],
                 "lm_head": ops.dense_weight(self.w["lm_head"]), "layers": layers}

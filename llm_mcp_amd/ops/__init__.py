@@ -502,8 +502,8 @@ def interleave_gate_up(w: torch.Tensor, block: int = 64) -> torch.Tensor:
     return w.view(2, I // block, block, d).transpose(0, 1).reshape(I2, d).contiguous()
 
 
-def deinterleave_gate_up(w: torch.Tensor, block: int) -> torch.Tensor:
-    """Inverse of ``interleave_gate_up``: back to [gate(I); up(I)] rows."""
+def deinterleave_gate_up_rows(w: torch.Tensor, block: int) -> torch.Tensor:
+    """Inverse of ``interleave_gate_up`` (weight rows): back to [gate(I); up(I)]."""
     I2, d = w.shape
     I = I2 // 2
     return w.view(I // block, 2, block, d).transpose(0, 1).reshape(I2, d).contiguous()
