@@ -36,7 +36,10 @@ int sample(const void*, int, long, int, int, const float*, const int*, const flo
            const uint64_t*, const int*, int*, float*, int, hipStream_t);
 int glu(void*, const void*, long, int, int, int, hipStream_t);
 int apply_penalties(void*, long, int, int, const int*, const int*, const float*, const int*, int,
-                    hipStream_t);
+                    int, hipStream_t);
+int race_sample_phase(int, int, int, const void*, int, long, int, int, int, int, const float*,
+                      const int*, const float*, const uint64_t*, const int*, const float*, int,
+                      float*, float*, int*, float*, hipStream_t);
 int embed_gather(void*, const void*, const int*, int, int, int, int, hipStream_t);
 int ids_from_prev(int*, const int*, const int*, int, hipStream_t);
 int mean_pool_l2(float*, float*, const void*, const int*, int, int, int, int, int, hipStream_t);
@@ -290,10 +293,21 @@ PYBIND11_MODULE(_lmx_kernels, m) {
           "allreduce");
   });
   m.def("apply_penalties", [](uptr logits, long ld, int B, int V, uptr win, uptr ngen, uptr pen,
-                              uptr on, int W, uptr stream) {
+                              uptr on, int W, int v0, uptr stream) {
     check(lmx::apply_penalties(P<void>(logits), ld, B, V, P<const int>(win), P<const int>(ngen),
-                               P<const float>(pen), P<const int>(on), W, S(stream)),
+                               P<const float>(pen), P<const int>(on), W, v0, S(stream)),
           "apply_penalties");
+  });
+  m.def("race_sample_phase", [](int phase, int round, int max_rounds, uptr logits, int is_bf16,
+                                long stride, int B, int Vs, int v0, int V, uptr temp, uptr topk,
+                                uptr topp, uptr seeds, uptr offsets, uptr gath, int W, uptr rec,
+                                uptr st, uptr out_tok, uptr out_lp, uptr stream) {
+    check(lmx::race_sample_phase(phase, round, max_rounds, P<void>(logits), is_bf16, stride, B, Vs,
+                                 v0, V, P<float>(temp), P<int>(topk), P<float>(topp),
+                                 P<uint64_t>(seeds), P<int>(offsets), P<float>(gath), W,
+                                 P<float>(rec), P<float>(st), P<int>(out_tok), P<float>(out_lp),
+                                 S(stream)),
+          "race_sample_phase");
   });
   m.def("gemm_nt", [](uptr C, uptr A, uptr W, uptr bias, uptr residual, int M, int N, int K,
                       long lda, long ldw, long ldc, int act, uptr stream) {

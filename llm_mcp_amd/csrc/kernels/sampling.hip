@@ -315,6 +315,214 @@ int sample(const void* logits, int logits_bf16, long stride, int B, int V, const
 }
 
 // --------------------------------------------------------------------------
+// K6-R: the same truncated sampler in exponential-race form, decomposable
+// over vocabulary shards (vocab-parallel LM head under TP: every rank holds
+// logits [B, V/TP] and NO rank gathers the full rows).
+//
+// A draw from softmax(x / T) restricted to {x > pivot} is
+//     j = argmax over {x_i > pivot} of  x_i / T + G_i,   G_i = -log(-log U_i)
+// (Gumbel-max / exponential race) with U_i a hash of (seed, offset, round,
+// GLOBAL vocabulary index i): the key of element i does not depend on which
+// rank holds it, so the argmax over the shards' local argmaxes is bitwise the
+// argmax over the whole row.  Truncation is the same pivot rejection as
+// sample_kernel: accept j iff the mass strictly above x_j is < top_p and the
+// count strictly above x_j is < top_k, else pivot on x_j and race again with
+// fresh noise (round + 1).  Rounds are capped; the fallback is the argmax.
+//
+// Per row and rank a phase writes an 8-float record; the caller exchanges the
+// records (one all-gather of B x 32 B per rank: the peer slots under TP, an
+// alias at W = 1) and every rank combines them in rank order into the same
+// row state, so every rank ends with the same token.  Phases:
+//   0  local max / normaliser / argmax and the round-0 race winner;
+//   1  combine the race winners (round 0: also max / normaliser / argmax;
+//      greedy and untruncated rows finish) -> local mass and count above x_j;
+//   2  combine mass / count -> accept or pivot; race round `round` over
+//      {x > pivot} (round == max_rounds: argmax fallback, write the tokens).
+// Record slots: phase 0 {m, s, ax, aj, key, j, xj}, phase 1 {mass, cnt},
+// phase 2 {-, -, -, -, key, j, xj}: the slots a phase reads and writes are
+// disjoint, so at W = 1 the record may be its own exchange.
+namespace {
+constexpr int RACE_REC = 8, RACE_ST = 12;
+enum { ST_XMAX, ST_S, ST_PIVOT, ST_CJ, ST_CX, ST_DONE, ST_AX, ST_AJ, ST_TOK, ST_LP };
+
+__device__ __forceinline__ float race_gumbel(RowKey k, uint32_t gi) {
+  const uint32_t h = lowbias32(lowbias32(gi ^ k.k0) + k.k1);
+  const float u = ((float)(h >> 8) + 0.5f) * (1.0f / 16777216.0f);
+  return -__logf(-__logf(u));
+}
+}  // namespace
+
+template <typename T>
+__global__ void __launch_bounds__(1024) race_kernel(
+    int phase, int round, int max_rounds, const T* __restrict__ logits, long stride, int Vs,
+    int v0, int V, const float* __restrict__ temperature, const int* __restrict__ top_k,
+    const float* __restrict__ top_p, const uint64_t* __restrict__ seeds,
+    const int* __restrict__ offsets, const float* __restrict__ gath, int W,
+    float* __restrict__ rec, float* __restrict__ st, int* __restrict__ out_tok,
+    float* __restrict__ out_lp) {
+  __shared__ float sv[16], sv2[16];
+  __shared__ int si[16];
+  const int row = blockIdx.x, B = gridDim.x;
+  const T* x = logits + (long)row * stride;
+  float* s = st + (long)row * RACE_ST;
+  float* r = rec + (long)row * RACE_REC;
+  const float temp = temperature[row];
+  const int kk = top_k ? top_k[row] : 0;
+  const bool greedy = !(temp > 0.f) || kk == 1;
+  const float inv_t = greedy ? 1.f : 1.f / temp;
+  const float tp = top_p ? top_p[row] : 1.f;
+  const bool truncate = !greedy && ((tp < 1.f) || (kk > 0 && kk < V));
+  const uint64_t seed = seeds ? seeds[row] : 0x1234ULL;
+  const uint64_t off = offsets ? (uint64_t)offsets[row] : 0ULL;
+  auto g = [&](int q, int slot) { return gath[((long)q * B + row) * RACE_REC + slot]; };
+  // race over {x > pivot} with round `rnd`'s noise: (key, global index, x)
+  auto race = [&](int rnd, float pivot, float* out3) {
+    const RowKey key = row_key(seed, off, rnd);
+    ArgMax c{-INFINITY, 0x7fffffff};
+    scan_row(x, Vs, [&](int i, float v) {
+      if (v > pivot) {
+        const float k = v * inv_t + race_gumbel(key, (uint32_t)(v0 + i));
+        if (k > c.v) { c.v = k; c.i = v0 + i; }   // ascending i per thread: ties keep the lowest
+      }
+    });
+    c = block_argmax(c, sv, si);
+    out3[0] = c.v;
+    out3[1] = __int_as_float(c.i);
+    out3[2] = c.v == -INFINITY ? -INFINITY : ld<T>(x, c.i - v0);
+  };
+  auto finish = [&](int tok, float lp) {
+    if (threadIdx.x == 0) {
+      s[ST_TOK] = __int_as_float(tok);
+      s[ST_LP] = lp;
+      s[ST_DONE] = 1.f;
+    }
+  };
+
+  if (phase == 0) {
+    MaxSum ms{-INFINITY, 0.f};
+    ArgMax am{-INFINITY, 0x7fffffff};
+    scan_row(x, Vs, [&](int i, float v) {
+      if (v > ms.m) { ms.s = ms.s * __expf((ms.m - v) * inv_t) + 1.f; ms.m = v; }
+      else ms.s += __expf((v - ms.m) * inv_t);
+      if (v > am.v) { am.v = v; am.i = v0 + i; }
+    });
+    ms = block_maxsum(ms, inv_t, sv, sv2);
+    am = block_argmax(am, sv, si);
+    float c3[3] = {-INFINITY, __int_as_float(0x7fffffff), -INFINITY};
+    if (!greedy) race(0, -INFINITY, c3);
+    if (threadIdx.x == 0) {
+      r[0] = ms.m; r[1] = ms.s; r[2] = am.v; r[3] = __int_as_float(am.i);
+      r[4] = c3[0]; r[5] = c3[1]; r[6] = c3[2]; r[7] = 0.f;
+    }
+    return;
+  }
+
+  if (phase == 1) {
+    if (round == 0) {
+      // the row state from the ranks' statistics, combined in rank order
+      float xmax = -INFINITY;
+      for (int q = 0; q < W; ++q) xmax = fmaxf(xmax, g(q, 0));
+      float S = 0.f;
+      ArgMax am{-INFINITY, 0x7fffffff};
+      for (int q = 0; q < W; ++q) {
+        if (g(q, 0) != -INFINITY) S += g(q, 1) * __expf((g(q, 0) - xmax) * inv_t);
+        am = argmax_combine(am, ArgMax{g(q, 2), __float_as_int(g(q, 3))});
+      }
+      if (threadIdx.x == 0) {
+        s[ST_XMAX] = xmax; s[ST_S] = S; s[ST_PIVOT] = -INFINITY; s[ST_DONE] = 0.f;
+        s[ST_AX] = am.v; s[ST_AJ] = __int_as_float(am.i);
+      }
+      if (greedy) {
+        finish(am.i, am.v - xmax - __logf(S));
+        if (threadIdx.x == 0) { r[0] = 0.f; r[1] = 0.f; }
+        return;
+      }
+      __syncthreads();
+    }
+    const float xmax = s[ST_XMAX], S = s[ST_S];
+    bool done = s[ST_DONE] != 0.f;
+    ArgMax c{-INFINITY, 0x7fffffff};
+    float cx = -INFINITY;
+    for (int q = 0; q < W; ++q) {
+      const ArgMax b{g(q, 4), __float_as_int(g(q, 5))};
+      if (b.v > c.v || (b.v == c.v && b.i < c.i)) { c = b; cx = g(q, 6); }
+    }
+    __syncthreads();   // every thread has read the state before it changes
+    if (!done && c.v == -INFINITY) {   // nothing above the pivot: the argmax
+      finish(__float_as_int(s[ST_AJ]), (s[ST_AX] - xmax) * inv_t - __logf(S));
+      done = true;
+    } else if (!done && !truncate) {
+      finish(c.i, (cx - xmax) * inv_t - __logf(S));
+      done = true;
+    } else if (!done && threadIdx.x == 0) {
+      s[ST_CJ] = __int_as_float(c.i);
+      s[ST_CX] = cx;
+    }
+    float mass = 0.f, cnt = 0.f;
+    if (!done) {
+      scan_row(x, Vs, [&](int i, float v) {
+        if (v > cx) { mass += __expf((v - xmax) * inv_t); cnt += 1.f; }
+      });
+      mass = block_sum(mass, sv);
+      cnt = block_sum(cnt, sv);
+    }
+    if (threadIdx.x == 0) { r[0] = mass; r[1] = cnt; }
+    return;
+  }
+
+  // phase 2: decide the previous round's candidate, race round `round`
+  const float xmax = s[ST_XMAX], S = s[ST_S];
+  bool done = s[ST_DONE] != 0.f;
+  float pivot = s[ST_PIVOT];
+  if (!done) {
+    float mass = 0.f, cnt = 0.f;
+    for (int q = 0; q < W; ++q) { mass += g(q, 0); cnt += g(q, 1); }
+    mass /= S;
+    const float cx = s[ST_CX];
+    __syncthreads();
+    if (mass < tp && (kk <= 0 || cnt < (float)kk)) {
+      finish(__float_as_int(s[ST_CJ]), (cx - xmax) * inv_t - __logf(S));
+      done = true;
+    } else if (round >= max_rounds) {
+      finish(__float_as_int(s[ST_AJ]), (s[ST_AX] - xmax) * inv_t - __logf(S));
+      done = true;
+    } else {
+      pivot = cx;
+      if (threadIdx.x == 0) s[ST_PIVOT] = pivot;
+    }
+  }
+  float c3[3] = {-INFINITY, __int_as_float(0x7fffffff), -INFINITY};
+  if (!done) race(round, pivot, c3);
+  if (threadIdx.x == 0) { r[4] = c3[0]; r[5] = c3[1]; r[6] = c3[2]; }
+  if (round >= max_rounds) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      out_tok[row] = __float_as_int(s[ST_TOK]);
+      if (out_lp) out_lp[row] = s[ST_LP];
+    }
+  }
+}
+
+int race_sample_phase(int phase, int round, int max_rounds, const void* logits, int logits_bf16,
+                      long stride, int B, int Vs, int v0, int V, const float* temperature,
+                      const int* top_k, const float* top_p, const uint64_t* seeds,
+                      const int* offsets, const float* gath, int W, float* rec, float* st,
+                      int* out_tok, float* out_lp, hipStream_t stream) {
+  if (B <= 0) return 0;
+  if (phase < 0 || phase > 2 || W < 1 || Vs < 1 || max_rounds < 1) return -1;
+  const int threads = Vs > 32768 ? 1024 : 256;
+  if (logits_bf16)
+    race_kernel<bf16_t><<<dim3(B), dim3(threads), 0, stream>>>(
+        phase, round, max_rounds, (const bf16_t*)logits, stride, Vs, v0, V, temperature, top_k,
+        top_p, seeds, offsets, gath, W, rec, st, out_tok, out_lp);
+  else
+    race_kernel<float><<<dim3(B), dim3(threads), 0, stream>>>(
+        phase, round, max_rounds, (const float*)logits, stride, Vs, v0, V, temperature, top_k,
+        top_p, seeds, offsets, gath, W, rec, st, out_tok, out_lp);
+  return (int)hipGetLastError();
+}
+
+// --------------------------------------------------------------------------
 // Repetition / presence / frequency penalties applied to the logits in place,
 // before sampling.  One wave per sampled row, lane i owns entry i of the row's
 // right-aligned window of the last W (<= 64) context tokens (-1 = empty); the
@@ -330,21 +538,21 @@ __global__ void __launch_bounds__(64) penalty_kernel(bf16_t* __restrict__ logits
                                                      const int* __restrict__ win,
                                                      const int* __restrict__ ngen,
                                                      const float* __restrict__ pen,
-                                                     const int* __restrict__ on, int W) {
+                                                     const int* __restrict__ on, int W, int v0) {
   if (on != nullptr && on[0] == 0) return;
   __shared__ int ids[64];
   const int row = blockIdx.x, lane = threadIdx.x;
   const int t = lane < W ? win[(long)row * W + lane] : -1;
   ids[lane] = t;
   __syncthreads();
-  if (t < 0 || t >= V) return;
+  if (t < v0 || t >= v0 + V) return;           // another rank's vocabulary shard
   for (int j = 0; j < lane; ++j)
     if (ids[j] == t) return;                   // not the first occurrence
   const int g0 = W - ngen[row];
   int cnt = 0;
   for (int j = lane > g0 ? lane : g0; j < W; ++j) cnt += ids[j] == t;
   const float rep = pen[3 * row], pres = pen[3 * row + 1], freq = pen[3 * row + 2];
-  bf16_t* p = logits + (long)row * ld + t;
+  bf16_t* p = logits + (long)row * ld + (t - v0);
   float l = bf2f(*p);
   if (rep != 1.f) l = l > 0.f ? l / rep : l * rep;
   l -= freq * (float)cnt + (cnt > 0 ? pres : 0.f);
@@ -352,10 +560,11 @@ __global__ void __launch_bounds__(64) penalty_kernel(bf16_t* __restrict__ logits
 }
 
 int apply_penalties(void* logits, long ld, int B, int V, const int* win, const int* ngen,
-                    const float* pen, const int* on, int W, hipStream_t stream) {
+                    const float* pen, const int* on, int W, int v0, hipStream_t stream) {
   if (B <= 0) return 0;
   if (W <= 0 || W > 64) return -1;
-  penalty_kernel<<<dim3(B), dim3(64), 0, stream>>>((bf16_t*)logits, ld, V, win, ngen, pen, on, W);
+  penalty_kernel<<<dim3(B), dim3(64), 0, stream>>>((bf16_t*)logits, ld, V, win, ngen, pen, on, W,
+                                                    v0);
   return (int)hipGetLastError();
 }
 

@@ -336,14 +336,29 @@ class LLMEngine:
         self._admit_quiet_s = float(os.environ.get("LMX_ADMIT_QUIET_MS", "2")) / 1e3
         self._admit_max_s = float(os.environ.get("LMX_ADMIT_MAX_MS", "25")) / 1e3
         la_env = os.environ.get("LMX_LOOKAHEAD", "")
-        self.lookahead = la_env == "1" or (la_env != "0" and self.device.type == "cuda")
-        # lookahead in a TP group: the followers sample the step too (the
-        # logits are all-gathered to every rank, the sampler is seeded and
-        # deterministic), so every rank holds step n's tokens on its device
-        # for step n+1's ids_from_prev gather and the leader never has to
-        # ship tokens to them
-        self.sample_all = self.tp.size > 1 and self.lookahead
-        self.tp.logits_to_all = self.sample_all
+        # TP groups: vocab-sharded sampling (ops.sample_race) by default --
+        # every rank samples its own logits shard and a B x 32-B record
+        # exchange per phase picks the same token everywhere, so no rank
+        # gathers logits and every rank holds each step's tokens on its device
+        # (LMX_TP_SAMPLER=gather: the logits gathered to the sampling ranks)
+        self.race_tp = self.tp.size > 1 and os.environ.get("LMX_TP_SAMPLER", "race") != "gather"
+        self.tp.shard_logits = self.race_tp
+        # LMX_SAMPLER=race: the race form at TP = 1 too (one shard: the same
+        # tokens a TP group draws for the same seeds; the default K6 kernel is
+        # 2.7x faster over full rows, profiles/r6_sampling.md)
+        self.race = self.race_tp or os.environ.get("LMX_SAMPLER", "") == "race"
+        rccl_tp = (self.tp.size > 1 and self.tp.group is not None
+                   and torch.distributed.get_backend(self.tp.group) == "nccl")
+        # lookahead: on by default for GPU engines and one-GPU (gloo) TP
+        # rehearsals; an RCCL TP group opts in with LMX_LOOKAHEAD=1 until a
+        # multi-GPU run has covered it
+        self.lookahead = la_env == "1" or (la_env != "0" and self.device.type == "cuda"
+                                           and not rccl_tp)
+        # every rank samples: the race sampler is a collective; the gather
+        # form all-gathers the logits under lookahead (each rank then holds
+        # step n's tokens for step n+1's ids_from_prev gather)
+        self.sample_all = self.tp.size > 1 and (self.race_tp or self.lookahead)
+        self.tp.logits_to_all = self.sample_all and not self.race_tp
         self._la = None                    # the launched step not yet read back
         self._la_end = 0.0                 # when the last launched step was read back
         self._penalized: set[int] = set()  # active requests with penalty windows
@@ -355,7 +370,7 @@ class LLMEngine:
             torch.distributed.get_backend(self.tp.group) == "gloo" and \
             not self.tp.device_collectives_cover(max(self._graph_buckets(), default=1),
                                                  self.cfg.hidden_size,
-                                                 self.model.vocab_shard)
+                                                 16 if self.race_tp else self.model.vocab_shard)
         if ecfg.use_graphs and self.device.type == "cuda" and not ops.debug_sync() and not host_tp:
             self._capture_graphs()
         self._bucket_list = sorted(self.graphs)
@@ -389,6 +404,26 @@ class LLMEngine:
                          for l in range(cfg.num_layers)]
         log.info("KV cache: %d blocks x %d tokens (%.1f GB)", self.num_blocks, BLOCK_SIZE,
                  self.kv.numel() * 2 / 1e9)
+
+    # ----------------------------------------------------------- sampling ---
+    def _sample(self, logits, temp, topk, topp, seeds, offs, out_tok=None, out_lp=None):
+        """Sample the step's rows: the K6 kernel over full rows, or under TP
+        the vocab-sharded race sampler over this rank's shard (collective:
+        every rank of the group calls it with the same rows)."""
+        if not self.race:
+            return ops.sample(logits, temp, topk, topp, seeds, offs, out_tok, out_lp)
+        tp = self.tp
+        if tp.size == 1:
+            return ops.sample_race(logits, temp, topk, topp, seeds, offs, out_tok=out_tok,
+                                   out_lp=out_lp)
+        return ops.sample_race(logits, temp, topk, topp, seeds, offs,
+                               exchange=tp.all_gather_records,
+                               v0=tp.rank * self.model.vocab_shard, vocab=self.cfg.vocab_size,
+                               world=tp.size, out_tok=out_tok, out_lp=out_lp)
+
+    def _penalize(self, logits, win, ngen, pen):
+        v0 = self.tp.rank * self.model.vocab_shard if self.race_tp else 0
+        return ops.apply_penalties(logits, win, ngen, pen, v0=v0)
 
     # ------------------------------------------------------------- graphs ---
     def _graph_buckets(self) -> list[int]:
@@ -475,8 +510,8 @@ class LLMEngine:
             logits = self.model.forward(inp, self.k_caches, self.v_caches, ws,
                                         self.ecfg.part_tokens)
             if self.is_leader or self.sample_all:
-                ops.sample(logits, g["temp"][:B], g["topk"][:B], g["topp"][:B],
-                           g["seeds"][:B], g["offs"][:B], g["tok"][:B], g["lp"][:B])
+                self._sample(logits, g["temp"][:B], g["topk"][:B], g["topp"][:B],
+                             g["seeds"][:B], g["offs"][:B], g["tok"][:B], g["lp"][:B])
             out["logits"] = logits
 
         if self.tp.size > 1:
@@ -499,17 +534,19 @@ class LLMEngine:
         """Penalty variant of bucket B, captured lazily the first time a step
         of that bucket carries a penalised row: the penalty kernel and a
         second sampling pass over the logits the bucket's decode graph left in
-        its pool (replayed right after it).  No forward pass -- so no
-        collective -- runs in this capture, which any rank that samples can
-        make on its own mid-serving."""
+        its pool (replayed right after it).  No forward pass runs in this
+        capture; under vocab-sharded TP sampling its sampler exchanges records
+        with the other ranks, which capture it at the same step (every rank
+        replays the same plans) -- nothing runs during a capture, so the
+        ranks need not meet there."""
         g, dev, stream = self._gbuf, self.device, self._gstream
         pd = self._pmeta.d
         logits = self.graphs[B]["logits"]
 
         def run():
-            ops.apply_penalties(logits, pd["win"][:B], pd["ngen"][:B], pd["pen"][:B])
-            ops.sample(logits, g["temp"][:B], g["topk"][:B], g["topp"][:B],
-                       g["seeds"][:B], g["offs"][:B], g["tok"][:B], g["lp"][:B])
+            self._penalize(logits, pd["win"][:B], pd["ngen"][:B], pd["pen"][:B])
+            self._sample(logits, g["temp"][:B], g["topk"][:B], g["topp"][:B],
+                         g["seeds"][:B], g["offs"][:B], g["tok"][:B], g["lp"][:B])
 
         stream.wait_stream(torch.cuda.current_stream(dev))
         graph = torch.cuda.CUDAGraph()
@@ -1017,8 +1054,8 @@ class LLMEngine:
         if not samples:
             return None, None
         if pen:
-            ops.apply_penalties(logits, d["win"], d["ngen"], d["pen"])
-        return ops.sample(logits, d["temp"], d["topk"], d["topp"], d["seeds"], d["offs"])
+            self._penalize(logits, d["win"], d["ngen"], d["pen"])
+        return self._sample(logits, d["temp"], d["topk"], d["topp"], d["seeds"], d["offs"])
 
     def _run_graph(self, plan, B):
         self._gmeta.next()

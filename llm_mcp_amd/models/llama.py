@@ -72,6 +72,9 @@ class TPContext:
         # and samples them itself, so each rank holds the step's tokens on
         # its device for the next step's ids_from_prev gather
         self.logits_to_all = False
+        # vocab-sharded sampling (engine race_tp): forward returns this rank's
+        # logits shard; nothing is gathered
+        self.shard_logits = False
         self.peer = None      # parallel.peer_allreduce.PeerAllReduce when enabled
         # Sequence parallelism (SURVEY.md §2.4 "SP" row): steps with at least
         # this many tokens keep the residual stream row-sharded across the TP
@@ -175,6 +178,27 @@ class TPContext:
         if self.peer is not None and self.peer.norm_supports(t, residual):
             return self.peer.all_reduce_norm(t, w, eps, residual)
         return ops.rms_norm(self.all_reduce(t), w, eps, residual=residual)
+
+    def all_gather_records(self, rec: torch.Tensor) -> torch.Tensor:
+        """Every rank's fp32 [B, 8] sampler records in rank order, [size, B, 8]
+        (ops.sample_race's exchange: B x 32 B per rank).  Peer slots when the
+        group has them (graph-capturable, no RCCL call), else the group's
+        all-gather."""
+        shape = (self.size,) + tuple(rec.shape)
+        if self.size == 1:
+            return rec.view(shape)
+        src = rec.contiguous()
+        raw = src.view(torch.bfloat16).reshape(-1)
+        if self.peer is not None and self.peer.gather_supports(raw):
+            return self.peer.all_gather(raw, None, to_all=True).view(torch.float32).view(shape)
+        if not src.is_cuda or self._host_staged(src):
+            h = src.cpu()
+            parts = [torch.empty_like(h) for _ in range(self.size)]
+            torch.distributed.all_gather(parts, h, group=self.group)
+            return torch.stack(parts).to(rec.device, non_blocking=True)
+        out = torch.empty(shape, dtype=rec.dtype, device=rec.device)
+        torch.distributed.all_gather_into_tensor(out, src, group=self.group)
+        return out
 
     def _host_staged(self, t: torch.Tensor) -> bool:
         # gloo only reduces device tensors; it gathers host tensors
@@ -467,11 +491,17 @@ class LlamaModel:
                     outs[i] = stop.value
                     live[i] = False
         hs = torch.cat(outs, dim=0)
-        logits = ops.linear(hs, self.w["lm_head"])
-        logits = self.tp.gather_last_to_leader(logits)
-        if logits is not None:
-            logits = logits[:, :self.cfg.vocab_size]
-        return logits
+        return self._tp_logits(ops.linear(hs, self.w["lm_head"]))
+
+    def _tp_logits(self, logits: torch.Tensor) -> torch.Tensor | None:
+        """The vocab-parallel LM head's output under TP: this rank's valid
+        shard columns (vocab-sharded sampling) or the rows gathered to the
+        sampling ranks (None on the others)."""
+        tp, V = self.tp, self.cfg.vocab_size
+        if tp.shard_logits:
+            return logits[:, :max(1, min(self.vocab_shard, V - tp.rank * self.vocab_shard))]
+        logits = tp.gather_last_to_leader(logits)
+        return None if logits is None else logits[:, :V]
 
     def _norm_fold_step(self, T: int, fold: bool) -> bool:
         """This step runs the folded norm: gains folded at load, TP = 1, and
@@ -657,7 +687,5 @@ class LlamaModel:
             hs = ops.rms_norm(xs, w["norm"], cfg.rms_eps, residual=rs)
         logits = ops.linear(hs, w["lm_head"])
         if self.tp.size > 1:
-            logits = self.tp.gather_last_to_leader(logits)
-            if logits is not None:
-                logits = logits[:, :cfg.vocab_size]
+            logits = self._tp_logits(logits)
         return logits

@@ -346,6 +346,11 @@ def prefill_q_per_tile(Hq: int, Hkv: int, D: int = 128) -> int:
 
 
 # ---------------------------------------------------------------- sampling ---
+# race rounds of sample_race: a row still rejected after them (top-p 0.95:
+# ~0.05^4) takes the argmax
+RACE_ROUNDS = int(os.environ.get("LMX_RACE_ROUNDS", "4"))
+
+
 def sample(logits: torch.Tensor, temperature: torch.Tensor, top_k: torch.Tensor,
            top_p: torch.Tensor, seeds: torch.Tensor, offsets: torch.Tensor,
            out_tok: torch.Tensor | None = None, out_lp: torch.Tensor | None = None,
@@ -369,24 +374,78 @@ def sample(logits: torch.Tensor, temperature: torch.Tensor, top_k: torch.Tensor,
     return out_tok, out_lp
 
 
+def sample_race(logits: torch.Tensor, temperature: torch.Tensor, top_k: torch.Tensor,
+                top_p: torch.Tensor, seeds: torch.Tensor, offsets: torch.Tensor,
+                exchange=None, v0: int = 0, vocab: int | None = None, world: int = 1,
+                out_tok: torch.Tensor | None = None, out_lp: torch.Tensor | None = None,
+                max_rounds: int = RACE_ROUNDS):
+    """K6-R: the truncated sampler in exponential-race form over a vocabulary
+    shard (sampling.hip ``race_kernel``).  ``logits`` [B, Vs]: columns
+    [v0, v0 + Vs) of the vocabulary (``vocab`` columns in all);
+    ``exchange(rec)`` all-gathers the fp32 [B, 8] records of the ``world``
+    shards in rank order ([world, B, 8]; None: one shard).  Every rank
+    returns the same (tokens int32 [B], logprobs fp32 [B]); at ``world`` 1
+    over the whole row it is the single-GPU form of the same sampler."""
+    B, Vs = logits.shape
+    V = Vs if vocab is None else vocab
+    if exchange is None:
+        exchange = lambda r: r.view(1, B, 8)   # noqa: E731 (slots keep an alias safe)
+    if not logits.is_cuda:
+        return ref.sample_race(logits, temperature, top_k, top_p, seeds, offsets, exchange,
+                               v0, V, max_rounds)
+    _chk(logits.dtype in (torch.bfloat16, torch.float32) and logits.stride(1) == 1, "logits")
+    _chk(temperature.dtype == torch.float32 and top_p.dtype == torch.float32, "fp32 params")
+    _chk(top_k.dtype == torch.int32 and offsets.dtype == torch.int32, "int32 params")
+    _chk(seeds.dtype == torch.int64, "int64 seeds")
+    for t in (temperature, top_k, top_p, seeds, offsets):
+        _chk(t.numel() >= B and t.is_cuda, "sampling param rows")
+    dev = logits.device
+    if out_tok is None:
+        out_tok = torch.empty(B, dtype=torch.int32, device=dev)
+    if out_lp is None:
+        out_lp = torch.empty(B, dtype=torch.float32, device=dev)
+    rec = torch.empty((B, 8), dtype=torch.float32, device=dev)
+    st = torch.empty((B, 12), dtype=torch.float32, device=dev)
+    k, bf, stream = native(), int(logits.dtype == torch.bfloat16), _stream()
+    common = (_ptr(logits), bf, logits.stride(0), B, Vs, v0, V, _ptr(temperature), _ptr(top_k),
+              _ptr(top_p), _ptr(seeds), _ptr(offsets))
+
+    def phase(ph, rnd, g):
+        _chk(g.shape == (world, B, 8) and g.is_contiguous() and g.dtype == torch.float32,
+             "race records exchange")
+        k.race_sample_phase(ph, rnd, max_rounds, *common, _ptr(g), world, _ptr(rec), _ptr(st),
+                            _ptr(out_tok), _ptr(out_lp), stream)
+
+    k.race_sample_phase(0, 0, max_rounds, *common, _ptr(rec), world, _ptr(rec), _ptr(st),
+                        _ptr(out_tok), _ptr(out_lp), stream)    # phase 0 reads no records
+    phase(1, 0, exchange(rec))
+    for rnd in range(1, max_rounds + 1):
+        phase(2, rnd, exchange(rec))
+        if rnd < max_rounds:
+            phase(1, rnd, exchange(rec))
+    return out_tok, out_lp
+
+
 def apply_penalties(logits: torch.Tensor, window: torch.Tensor, ngen: torch.Tensor,
-                    pen: torch.Tensor, on: torch.Tensor | None = None) -> torch.Tensor:
+                    pen: torch.Tensor, on: torch.Tensor | None = None,
+                    v0: int = 0) -> torch.Tensor:
     """Repetition / presence / frequency penalties on logits [B, V] in place
     (K6 prologue).  window int32 [B, W<=64] right-aligned context tokens (-1
     padded), ngen int32 [B] generated tokens at its tail, pen fp32 [B, 3] =
-    (repetition, presence, frequency); ``on`` int32 [1] device flag."""
+    (repetition, presence, frequency); ``on`` int32 [1] device flag.  ``v0``:
+    the logits are vocabulary columns [v0, v0 + V) (a TP rank's shard)."""
     B, V = logits.shape
     if not logits.is_cuda:
         if on is not None and int(on[0]) == 0:
             return logits
-        return ref.apply_penalties(logits, window, ngen, pen)
+        return ref.apply_penalties(logits, window, ngen, pen, v0)
     _chk(logits.dtype == torch.bfloat16 and logits.stride(1) == 1, "bf16 logits rows")
     _chk(window.dtype == torch.int32 and window.is_contiguous() and window.shape[0] >= B
          and window.shape[1] <= 64, "penalty window")
     _chk(ngen.dtype == torch.int32 and pen.dtype == torch.float32 and pen.is_contiguous(),
          "penalty params")
     native().apply_penalties(_ptr(logits), logits.stride(0), B, V, _ptr(window), _ptr(ngen),
-                             _ptr(pen), _ptr(on), window.shape[1], _stream())
+                             _ptr(pen), _ptr(on), window.shape[1], v0, _stream())
     return logits
 
 

@@ -232,7 +232,157 @@ def sample(logits, temperature, top_k, top_p, seeds, offsets):
     return toks, lps
 
 
-def apply_penalties(logits, window, ngen, pen):
+_M32 = 0xFFFFFFFF
+
+
+def _lowbias32(x: torch.Tensor) -> torch.Tensor:
+    x = x ^ (x >> 16)
+    x = (x * 0x7FEB352D) & _M32
+    x = x ^ (x >> 15)
+    x = (x * 0x846CA68B) & _M32
+    return x ^ (x >> 16)
+
+
+def _mix64(z: int) -> int:
+    m = (1 << 64) - 1
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & m
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & m
+    return z ^ (z >> 31)
+
+
+def _row_key(seed: int, off: int, rnd: int) -> tuple[int, int]:
+    m = (1 << 64) - 1
+    h = _mix64((seed & m) ^ _mix64((off * 0x9E3779B97F4A7C15 + rnd) & m))
+    return h & _M32, h >> 32
+
+
+def race_gumbel(seed: int, off: int, rnd: int, idx: torch.Tensor) -> torch.Tensor:
+    """The race kernel's per-element noise G_i = -log(-log U_i), U_i a hash of
+    (seed, offset, round, global index i)."""
+    k0, k1 = _row_key(seed, off, rnd)
+    h = _lowbias32((_lowbias32(idx.to(torch.int64) ^ k0) + k1) & _M32)
+    u = ((h >> 8).to(torch.float32) + 0.5) * (1.0 / 16777216.0)
+    return -torch.log(-torch.log(u))
+
+
+def sample_race(logits, temperature, top_k, top_p, seeds, offsets, exchange, v0, V,
+                max_rounds):
+    """CPU mirror of ops.sample_race (the race_kernel phases, same records and
+    exchanges): exact race winners, so every rank -- and a one-shard run over
+    the whole row -- picks the same tokens."""
+    B, Vs = logits.shape
+    x = logits.float()
+    idx = torch.arange(v0, v0 + Vs, dtype=torch.int64)
+    rec = torch.zeros(B, 8)
+    temp = [float(t) for t in temperature[:B]]
+    kk = [int(k) for k in top_k[:B]] if top_k is not None else [0] * B
+    tp = [float(p) for p in top_p[:B]] if top_p is not None else [1.0] * B
+    sd = [int(s) for s in seeds[:B]] if seeds is not None else [0x1234] * B
+    of = [int(o) for o in offsets[:B]] if offsets is not None else [0] * B
+    greedy = [not (t > 0) or k == 1 for t, k in zip(temp, kk)]
+    inv_t = [1.0 if g else 1.0 / t for g, t in zip(greedy, temp)]
+    trunc = [not g and (p < 1.0 or 0 < k < V) for g, p, k in zip(greedy, tp, kk)]
+
+    def race(b, rnd, pivot):
+        keep = x[b] > pivot
+        if not bool(keep.any()):
+            return -math.inf, 0x7FFFFFFF, -math.inf
+        key = x[b] * inv_t[b] + race_gumbel(sd[b], of[b], rnd, idx)
+        key = torch.where(keep, key, torch.full_like(key, -math.inf))
+        j = int(torch.argmax(key))          # first maximum: the lowest index
+        return float(key[j]), v0 + j, float(x[b, j])
+
+    for b in range(B):                       # phase 0
+        m = float(x[b].max())
+        s = float(torch.exp((x[b] - m) * inv_t[b]).sum())
+        j = int(torch.argmax(x[b]))
+        c = race(b, 0, -math.inf) if not greedy[b] else (-math.inf, 0x7FFFFFFF, -math.inf)
+        rec[b] = torch.tensor([m, s, float(x[b, j]), 0, c[0], 0, c[2], 0])
+        rec[b, 3] = float(v0 + j)           # indices travel as floats here (exact < 2^24)
+        rec[b, 5] = float(c[1])
+    g = exchange(rec)
+    W = g.shape[0]
+    xmax, S = [0.0] * B, [0.0] * B
+    am = [(0.0, 0)] * B
+    done = [False] * B
+    tok, lp = [0] * B, [0.0] * B
+    cand = [(0, 0.0)] * B
+    pivot = [-math.inf] * B
+
+    def combine_cands(b):
+        best = (-math.inf, 0x7FFFFFFF, -math.inf)
+        for q in range(W):
+            k_, j_, x_ = float(g[q, b, 4]), int(g[q, b, 5]), float(g[q, b, 6])
+            if k_ > best[0] or (k_ == best[0] and j_ < best[1]):
+                best = (k_, j_, x_)
+        return best
+
+    def mass_pass():
+        out = torch.zeros(B, 8)
+        for b in range(B):
+            if not done[b]:
+                above = x[b] > cand[b][1]
+                out[b, 0] = float(torch.exp((x[b][above] - xmax[b]) * inv_t[b]).sum())
+                out[b, 1] = float(above.sum())
+        return out
+
+    for b in range(B):                       # phase 1, round 0
+        xmax[b] = max(float(g[q, b, 0]) for q in range(W))
+        S[b] = sum(float(g[q, b, 1]) * math.exp((float(g[q, b, 0]) - xmax[b]) * inv_t[b])
+                   for q in range(W) if float(g[q, b, 0]) != -math.inf)
+        best = (-math.inf, 0x7FFFFFFF)
+        for q in range(W):
+            v, j = float(g[q, b, 2]), int(g[q, b, 3])
+            if v > best[0] or (v == best[0] and j < best[1]):
+                best = (v, j)
+        am[b] = best
+        if greedy[b]:
+            done[b], tok[b], lp[b] = True, best[1], best[0] - xmax[b] - math.log(S[b])
+            continue
+        k_, j_, x_ = combine_cands(b)
+        if k_ == -math.inf:
+            done[b], tok[b] = True, am[b][1]
+            lp[b] = (am[b][0] - xmax[b]) * inv_t[b] - math.log(S[b])
+        elif not trunc[b]:
+            done[b], tok[b], lp[b] = True, j_, (x_ - xmax[b]) * inv_t[b] - math.log(S[b])
+        else:
+            cand[b] = (j_, x_)
+    g = exchange(mass_pass())
+    for rnd in range(1, max_rounds + 1):     # phase 2 (+ phase 1)
+        rec = torch.zeros(B, 8)
+        rec[:, 4] = -math.inf
+        for b in range(B):
+            if done[b]:
+                continue
+            mass = sum(float(g[q, b, 0]) for q in range(W)) / S[b]
+            cnt = sum(float(g[q, b, 1]) for q in range(W))
+            if mass < tp[b] and (kk[b] <= 0 or cnt < kk[b]):
+                done[b], tok[b] = True, cand[b][0]
+                lp[b] = (cand[b][1] - xmax[b]) * inv_t[b] - math.log(S[b])
+            elif rnd >= max_rounds:
+                done[b], tok[b] = True, am[b][1]
+                lp[b] = (am[b][0] - xmax[b]) * inv_t[b] - math.log(S[b])
+            else:
+                pivot[b] = cand[b][1]
+                k_, j_, x_ = race(b, rnd, pivot[b])
+                rec[b, 4], rec[b, 5], rec[b, 6] = k_, float(j_), x_
+        if rnd >= max_rounds:
+            break
+        g = exchange(rec)
+        for b in range(B):
+            if done[b]:
+                continue
+            k_, j_, x_ = combine_cands(b)
+            if k_ == -math.inf:
+                done[b], tok[b] = True, am[b][1]
+                lp[b] = (am[b][0] - xmax[b]) * inv_t[b] - math.log(S[b])
+            else:
+                cand[b] = (j_, x_)
+        g = exchange(mass_pass())
+    return torch.tensor(tok, dtype=torch.int32), torch.tensor(lp, dtype=torch.float32)
+
+
+def apply_penalties(logits, window, ngen, pen, v0: int = 0):
     """In place: repetition (every window token), presence / frequency (counts
     over the generated tail of the right-aligned window)."""
     B, W = window.shape
@@ -242,13 +392,15 @@ def apply_penalties(logits, window, ngen, pen):
         rep, pres, freq = (float(v) for v in pen[b])
         seen = set()
         for i, t in enumerate(ids):
-            if t < 0 or t in seen or t >= logits.shape[1]:
+            if t < 0 or t in seen:
                 continue
             seen.add(t)
+            if not v0 <= t < v0 + logits.shape[1]:     # another rank's vocabulary shard
+                continue
             cnt = sum(1 for j in range(max(i, g0), W) if ids[j] == t)
-            x = float(logits[b, t])
+            x = float(logits[b, t - v0])
             if rep != 1.0:
                 x = x / rep if x > 0 else x * rep
             x -= freq * cnt + (pres if cnt > 0 else 0.0)
-            logits[b, t] = x
+            logits[b, t - v0] = x
     return logits

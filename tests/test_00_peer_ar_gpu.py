@@ -215,3 +215,117 @@ def test_peer_allreduce_matches_fp32_sum(world):
                 p.kill()
     assert modes == {0, 1}                        # both one-shot and two-shot ran
     assert all(not e for e in done.values()), done
+
+
+def _race_rank(rank, world, port, q):
+    """Vocab-sharded sampling (ops.sample_race) at TP = world on the one GPU:
+    each rank holds its vocabulary shard of the logits, the records travel
+    through the peer slots, and every rank gets the tokens of the one-shard
+    run over the full rows -- eagerly and in a captured graph."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world))
+    import torch.distributed as dist
+
+    from llm_mcp_amd import ops
+    from llm_mcp_amd.models.llama import TPContext
+    from llm_mcp_amd.models.weights import vocab_shard
+    from llm_mcp_amd.parallel.peer_allreduce import PeerAllReduce
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("gloo")
+    errs, ar = [], None
+    try:
+        ops.native()
+        ar = PeerAllReduce(dist.group.WORLD, rank, world, dev, slot_bytes=4 << 20)
+        tp = TPContext(rank, world, dist.group.WORLD)
+        tp.peer = ar
+        V, B = 128256, 256
+        vs = vocab_shard(V, world)
+        lo, hi = rank * vs, min(V, (rank + 1) * vs)
+
+        def params(salt):
+            g = torch.Generator().manual_seed(salt)
+            t = torch.full((B,), 0.8)
+            t[::17] = 0.0                               # greedy rows
+            k = torch.zeros(B, dtype=torch.int32)
+            k[1::5] = 40                                # top-k rows
+            p = torch.full((B,), 0.95)
+            p[2::7] = 0.5
+            seeds = torch.randint(0, 1 << 40, (B,), generator=g)
+            off = torch.randint(0, 1000, (B,), generator=g, dtype=torch.int32)
+            return [x.to(dev) for x in (t, k, p, seeds, off)]
+
+        def logits(salt):
+            g = torch.Generator().manual_seed(1000 + salt)
+            # a peaked head over a flat tail: nucleus sizes from 1 to thousands
+            x = torch.randn(B, V, generator=g) * torch.linspace(0.5, 4.0, B)[:, None]
+            return x.to(torch.bfloat16).to(dev)
+
+        for salt in range(3):
+            full, prm = logits(salt), params(salt)
+            want_t, want_lp = ops.sample_race(full, *prm)
+            shard = full[:, lo:hi].contiguous()
+            got_t, got_lp = ops.sample_race(shard, *prm, exchange=tp.all_gather_records,
+                                            v0=lo, vocab=V, world=world)
+            torch.cuda.synchronize()
+            if not torch.equal(got_t, want_t):
+                n = int((got_t != want_t).sum())
+                errs.append(f"salt {salt}: {n}/{B} tokens differ from the one-shard run")
+            if not torch.allclose(got_lp, want_lp, atol=1e-3, rtol=1e-3):
+                errs.append(f"salt {salt}: logprobs differ")
+        # captured: new logits / params per replay
+        buf = torch.zeros(B, hi - lo, dtype=torch.bfloat16, device=dev)
+        pb = params(0)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            out = ops.sample_race(buf, *pb, exchange=tp.all_gather_records, v0=lo, vocab=V,
+                                  world=world)
+        torch.cuda.synchronize()
+        dist.barrier()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            out = ops.sample_race(buf, *pb, exchange=tp.all_gather_records, v0=lo, vocab=V,
+                                  world=world)
+        for salt in range(10, 13):
+            full, prm = logits(salt), params(salt)
+            buf.copy_(full[:, lo:hi])
+            for dst, src in zip(pb, prm):
+                dst.copy_(src)
+            want_t, _ = ops.sample_race(full, *prm)
+            torch.cuda.synchronize()
+            dist.barrier()
+            g.replay()
+            torch.cuda.synchronize()
+            if not torch.equal(out[0], want_t):
+                errs.append(f"graph salt {salt}: tokens differ")
+        errs += ["race: error word set"] if ar.error(clear=True) else []
+        q.put(("done", rank, errs))
+    except Exception as ex:   # report instead of hanging the parent
+        q.put(("done", rank, [f"{type(ex).__name__}: {ex}"]))
+    finally:
+        if ar is not None:
+            dist.barrier()
+            ar.close()
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_vocab_sharded_sampling_matches_one_shard(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_race_rank, args=(r, world, port, q), daemon=True)
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = [q.get(timeout=300) for _ in procs]
+        for p in procs:
+            p.join(timeout=60)
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+    errs = [e for r in res for e in r[2]]
+    assert not errs, errs

@@ -330,30 +330,34 @@ def _params(B, t=1.0, k=0, p=1.0):
             torch.arange(B, dtype=torch.int64, device=DEV) * 7 + 1, f(0, torch.int32))
 
 
+@pytest.mark.parametrize("fn", ["sample", "sample_race"])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_sample_greedy_and_logprob(dtype):
+def test_sample_greedy_and_logprob(dtype, fn):
     B, V = 5, 128256
     lg = (torch.randn(B, V, device=DEV) * 3).to(dtype)
-    tok, lp = ops.sample(lg, *_params(B, t=0.0))
+    tok, lp = getattr(ops, fn)(lg, *_params(B, t=0.0))
     assert torch.equal(tok.long(), lg.float().argmax(-1))
     ref_lp = torch.log_softmax(lg.float(), -1).gather(1, tok.long()[:, None])[:, 0]
     torch.testing.assert_close(lp, ref_lp, atol=1e-3, rtol=1e-3)
 
 
-def test_sample_distribution_matches_softmax():
+@pytest.mark.parametrize("fn", ["sample", "sample_race"])
+def test_sample_distribution_matches_softmax(fn):
     V, B = 8, 4096
     base = torch.tensor([2.0, 1.0, 0.5, 0.0, -1.0, -2.0, 0.3, 1.5], device=DEV)
     lg = base.repeat(B, 1)
     t, k, p, _, off = _params(B, t=0.7)
     seeds = torch.arange(B, dtype=torch.int64, device=DEV) * 977 + 3
-    tok, _ = ops.sample(lg, t, k, p, seeds, off)
+    tok, _ = getattr(ops, fn)(lg, t, k, p, seeds, off)
     freq = torch.bincount(tok.long(), minlength=V).float() / B
     expect = torch.softmax(base / 0.7, -1)
     assert torch.allclose(freq, expect, atol=0.03), (freq, expect)
 
 
-def test_sample_distribution_full_vocab():
-    """Inverse-CDF draw over the whole 128k vocabulary: five hot tokens placed
+@pytest.mark.parametrize("fn", ["sample", "sample_race"])
+def test_sample_distribution_full_vocab(fn):
+    """A draw over the whole 128k vocabulary (inverse CDF; the race form's
+    Gumbel keys): five hot tokens placed
     in different threads' element sets (a flat tail carries the remaining
     ~0.7 % of the mass) are drawn at their softmax frequencies; with top_p
     0.8 only the nucleus (mass strictly above < 0.8) is ever drawn."""
@@ -364,12 +368,12 @@ def test_sample_distribution_full_vocab():
     lg = lg.repeat(B, 1).to(torch.bfloat16)
     seeds = torch.arange(B, dtype=torch.int64, device=DEV) * 131 + 7
     t, k, p, _, off = _params(B, t=1.0)
-    tok, _ = ops.sample(lg, t, k, p, seeds, off)
+    tok, _ = getattr(ops, fn)(lg, t, k, p, seeds, off)
     probs = torch.softmax(lg[0].float(), -1)
     cnt = torch.bincount(tok.long(), minlength=V).float() / B
     torch.testing.assert_close(cnt[hot], probs[hot], atol=0.03, rtol=0)
     t, k, p, _, off = _params(B, t=1.0, p=0.8)
-    tok, _ = ops.sample(lg, t, k, p, seeds, off)
+    tok, _ = getattr(ops, fn)(lg, t, k, p, seeds, off)
     order = probs.argsort(descending=True)
     above = torch.cumsum(probs[order], 0) - probs[order]
     nucleus = set(order[above < 0.8].tolist())
@@ -377,13 +381,14 @@ def test_sample_distribution_full_vocab():
     assert set(tok.tolist()) == nucleus
 
 
-def test_sample_top_k_top_p_support():
+@pytest.mark.parametrize("fn", ["sample", "sample_race"])
+def test_sample_top_k_top_p_support(fn):
     V, B = 1000, 2048
     lg = torch.randn(V, device=DEV).repeat(B, 1) * 2
     order = lg[0].argsort(descending=True)
     seeds = torch.arange(B, dtype=torch.int64, device=DEV) * 31 + 5
     t, k, p, _, off = _params(B, t=1.0, k=5)
-    tok, _ = ops.sample(lg, t, k, p, seeds, off)
+    tok, _ = getattr(ops, fn)(lg, t, k, p, seeds, off)
     assert set(tok.tolist()) <= set(order[:5].tolist())
     assert len(set(tok.tolist())) > 1
     # nucleus: expected support = smallest prefix with mass >= 0.5
@@ -391,10 +396,10 @@ def test_sample_top_k_top_p_support():
     above = torch.cumsum(probs, 0) - probs
     nucleus = set(order[above < 0.5].tolist())
     t, k, p, _, off = _params(B, t=1.0, p=0.5)
-    tok, _ = ops.sample(lg, t, k, p, seeds, off)
+    tok, _ = getattr(ops, fn)(lg, t, k, p, seeds, off)
     assert set(tok.tolist()) <= nucleus
     # determinism: same seeds -> same tokens
-    tok2, _ = ops.sample(lg, t, k, p, seeds, off)
+    tok2, _ = getattr(ops, fn)(lg, t, k, p, seeds, off)
     assert torch.equal(tok, tok2)
 
 
