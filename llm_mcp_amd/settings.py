@@ -91,7 +91,10 @@ VARS: list[Var] = [
     Var("LMX_SP_MIN_TOKENS", int, 0, "TP: steps with at least this many tokens run sequence-parallel (reduce-scatter/all-gather residual stream); 0 disables (default until the RCCL branch is measured on a multi-GPU node)"),
     Var("LMX_TP_MICROBATCH", str, "auto", "TP prefill micro-batches (two halves whose async RCCL all-reduces overlap the other half's compute): auto = RCCL groups at >= LMX_TP_MICROBATCH_MIN tokens, 1 always (also gloo), 0 off"),
     Var("LMX_TP_MICROBATCH_MIN", int, 2048, "step tokens from which LMX_TP_MICROBATCH=auto splits a pure-prefill TP step"),
-    Var("LMX_LOOKAHEAD", str, "", "engine lookahead stepping (step n+1 scheduled and launched before step n's tokens are read back; input tokens gathered on the device): default on for GPU engines, TP groups included (every rank then samples the all-gathered logits itself: sample_all mode), 1 forces it (also on CPU), 0 off"),
+    Var("LMX_LOOKAHEAD", str, "", "engine lookahead stepping (step n+1 scheduled and launched before step n's tokens are read back; input tokens gathered on the device): default on for GPU engines and one-GPU (gloo) TP rehearsals, opt-in (1) on RCCL TP groups until a multi-GPU run covers it; 1 forces it (also on CPU), 0 off"),
+    Var("LMX_TP_SAMPLER", str, "race", "TP sampling: race = vocab-sharded exponential-race sampler (every rank samples its logits shard, B x 32-B record exchanges, no logits gathered); gather = the logits gathered to the sampling ranks and the K6 kernel"),
+    Var("LMX_SAMPLER", str, "", "race: the vocab-sharded race sampler at TP = 1 too (the tokens a TP group draws for the same seeds); default: the K6 inverse-CDF kernel"),
+    Var("LMX_RACE_ROUNDS", int, 4, "race sampler rejection rounds before the argmax fallback (top-p 0.95: ~0.05^rounds of rows)"),
     Var("LMX_FUSED_PREFILL_ROPE", str, "1", "1: prefill rows' q rotation runs inside the prefill attention kernel (the rope/cache kernel only rotates k and writes the cache); 0: the rope/cache kernel rotates q in place"),
     Var("LMX_FUSED_ENCODER_ROPE", str, "0", "1: the embedding encoders (nomic) rotate q inside the attention kernel as LMX_FUSED_PREFILL_ROPE does for Llama (measured slower once: off)"),
     Var("LMX_FUSED_DECODE_ROPE", str, "1", "1: decode rows' rotary embedding and KV-cache write run inside the paged decode attention kernel; 0: separate rope/cache kernel"),
