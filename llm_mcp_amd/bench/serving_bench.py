@@ -197,6 +197,7 @@ async def _mixed_load(url, chat_model, embed_model, jobs, concurrency, embed_eve
     sem = asyncio.Semaphore(concurrency)
     lat, errs, kinds = [], [], {}
     per_dev: dict[str, int] = {}
+    done_at: list[tuple[float, str]] = []     # (monotonic time, device) per finished job
     requeued = [0]
     sync = {"ok": 0, "error": 0}
 
@@ -248,6 +249,7 @@ async def _mixed_load(url, chat_model, embed_model, jobs, concurrency, embed_eve
                     jj = await r.json()
                 d = ((jj.get("result") or {}).get("device_id") or jj.get("device_id") or "?")
                 per_dev[d] = per_dev.get(d, 0) + 1
+                done_at.append((time.monotonic(), d))
                 requeued[0] += int((jj.get("attempts") or 1) > 1)
             if len(lat) % 64 == 0:
                 _log(f"{len(lat)}/{jobs} jobs finished, {len(errs)} errors")
@@ -255,6 +257,7 @@ async def _mixed_load(url, chat_model, embed_model, jobs, concurrency, embed_eve
     async with aiohttp.ClientSession(connector=aiohttp.TCPConnector(limit=0),
                                      timeout=aiohttp.ClientTimeout(total=3600)) as s:
         t0 = time.perf_counter()
+        t0_mono = time.monotonic()
         await asyncio.gather(*[one(s, i) for i in range(jobs)])
         el = time.perf_counter() - t0
     n_async = jobs - sync["ok"] - sync["error"]
@@ -263,7 +266,7 @@ async def _mixed_load(url, chat_model, embed_model, jobs, concurrency, embed_eve
             "p95_s": round(percentile(lat, 95), 3),
             "error_rate": round(len(errs) / max(1, n_async), 4),
             "jobs_done_by_device": per_dev, "jobs_requeued": requeued[0],
-            "sync_chat": sync}
+            "sync_chat": sync, "_done_at": done_at, "_t0": t0_mono}
 
 
 def bench_mixed(a) -> dict:
@@ -308,15 +311,37 @@ def bench_mixed(a) -> dict:
                 status_seen.setdefault(k, set()).add(dev.get("status", "?"))
                 trips[k] = max(trips.get(k, 0), int(dev.get("circuit_trips") or 0))
 
+        # fault-recovery timeline (monotonic seconds): every change of a
+        # device's circuit / status and of a worker's alive flag / restarts
+        timeline: list[tuple[float, str, str, str]] = []
+        last: dict[tuple[str, str], str] = {}
+
+        def note(key, what, val):
+            if last.get((key, what)) != val:
+                last[(key, what)] = val
+                timeline.append((time.monotonic(), key, what, val))
+
         async def watch_circuit():
             import aiohttp
             async with aiohttp.ClientSession() as s:
                 while True:
                     try:
-                        await poll_dashboard(s)
+                        async with s.get(url + "/v1/dashboard") as r:
+                            d = await r.json()
+                        for dev in d.get("devices") or []:
+                            k = dev.get("id", "?")
+                            circ.setdefault(k, set()).add(dev.get("circuit", "ok"))
+                            status_seen.setdefault(k, set()).add(dev.get("status", "?"))
+                            trips[k] = max(trips.get(k, 0), int(dev.get("circuit_trips") or 0))
+                            note(k, "circuit", str(dev.get("circuit", "ok")))
+                            note(k, "status", str(dev.get("status", "?")))
+                        async with s.get(url + "/v1/debug/workers") as r:
+                            for w in (await r.json()).get("workers") or []:
+                                note(w.get("name", "?"), "alive", str(bool(w.get("alive"))))
+                                note(w.get("name", "?"), "restarts", str(w.get("restarts", 0)))
                     except Exception:
                         pass
-                    await asyncio.sleep(0.25)
+                    await asyncio.sleep(0.1)
 
         async def run():
             w = asyncio.ensure_future(watch_circuit())
@@ -325,7 +350,11 @@ def bench_mixed(a) -> dict:
                                          a.embed_every, a.max_tokens, a.chars, a.sync_every)
             finally:
                 w.cancel()
-        out.update(loop.run_until_complete(run()))
+        res = loop.run_until_complete(run())
+        done_at, t0m = res.pop("_done_at"), res.pop("_t0")
+        out.update(res)
+        if a.fault:
+            out["recovery"] = _recovery(timeline, done_at, t0m, a.fault_device)
 
         async def final_poll():
             import aiohttp
@@ -370,6 +399,37 @@ def bench_mixed(a) -> dict:
             core.wait(timeout=60)
         except subprocess.TimeoutExpired:
             core.kill()
+
+
+def _recovery(timeline, done_at, t0, fault_device: str) -> dict:
+    """Fault -> recovery phases of the faulty device (seconds from the load's
+    start): its last job served before the fault, the breaker trip, the
+    worker's death and restart, the device back online, and its first job
+    served after the restart.  ``recovery_s`` = fault (last good job) ->
+    first job served by the replacement."""
+    def first(pred, after=0.0):
+        return next((round(t - t0, 2) for t, k, w, v in timeline
+                     if t - t0 >= after and pred(k, w, v)), None)
+
+    dev = fault_device
+    died = first(lambda k, w, v: w == "alive" and v == "False")
+    restarted = first(lambda k, w, v: w == "restarts" and v not in ("0", "None"))
+    trip = first(lambda k, w, v: k.endswith(dev) and w == "circuit" and v == "degraded")
+    mine = sorted(t - t0 for t, d in done_at if d.endswith(dev))
+    cut = min(x for x in (died, trip) if x is not None) if (died or trip) else None
+    before = [t for t in mine if cut is not None and t <= cut]
+    after = [t for t in mine if restarted is not None and t >= restarted]
+    back = first(lambda k, w, v: k.endswith(dev) and w == "status" and v == "online",
+                 after=restarted or 0.0) if restarted is not None else None
+    last_ok = round(before[-1], 2) if before else None
+    first_new = round(after[0], 2) if after else None
+    return {"last_job_before_fault_s": last_ok, "breaker_trip_s": trip, "worker_died_s": died,
+            "worker_restarted_s": restarted, "device_online_again_s": back,
+            "first_job_after_restart_s": first_new,
+            "recovery_s": (round(first_new - last_ok, 2)
+                           if first_new is not None and last_ok is not None else None),
+            "events": [(round(t - t0, 2), k, w, v) for t, k, w, v in timeline
+                       if k.endswith(dev) or w in ("alive", "restarts")][:60]}
 
 
 async def _wait_workers(url: str, n: int, timeout: float = 900) -> None:

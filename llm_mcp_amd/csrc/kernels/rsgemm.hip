@@ -37,6 +37,14 @@
 //     the gate and up values of the same 16 channels, in the same lanes).
 #include "common.h"
 
+// RS_LAB (tools/rsgemm_lab.cpp only, never in the extension): bit 0 drops the
+// MFMAs, bit 1 points every weight load at the wave's first K32 step (L1 /
+// L2-hot), bit 2 every activation DMA at the first K64 step -- the time each
+// part adds to the kernel.  Results are garbage in these builds.
+#ifndef RS_LAB
+#define RS_LAB 0
+#endif
+
 namespace lmx {
 namespace {
 
@@ -57,6 +65,7 @@ __device__ __forceinline__ void rs_stage_a(bf16_t* slot, const bf16_t* __restric
   for (int i = 0; i < BM / 64; ++i) {
     const int r = i * 64 + rr;
     const int gr = m0 + r < M ? m0 + r : M - 1;
+    if constexpr ((RS_LAB & 4) != 0) k0 = 0;
     __builtin_amdgcn_global_load_lds(A + (long)gr * lda + k0 + 8 * (c ^ rs_swz(r)),
                                      (rs_lds_t*)(slot + (i * 64 + wave * 8) * RS_BK), 16, 0, 0);
   }
@@ -204,6 +213,7 @@ __global__ void __launch_bounds__(RS_THREADS, 2) __attribute__((amdgpu_waves_per
                             : lane * 16;
   constexpr int I0 = 0, I1 = RM ? 0 : 1024, I2 = RM ? 64 : 2048, I3 = RM ? 64 : 3072;
   auto wsb = [&](int k) -> const void* {   // wave-uniform base of K32 step k
+    if constexpr ((RS_LAB & 2) != 0) k = 0;
     return (const void*)(wstream + (long)k * KSTEP);
   };
 
@@ -242,10 +252,14 @@ __global__ void __launch_bounds__(RS_THREADS, 2) __attribute__((amdgpu_waves_per
         nx0 = rs_afrag(slot, 32 * (p + 1) + fr, kk * 4 + fg);
         nx1 = rs_afrag(slot, 32 * (p + 1) + 16 + fr, kk * 4 + fg);
       }
-      acc[0][2 * p] = mfma16(w0, cur0, acc[0][2 * p]);
-      acc[1][2 * p] = mfma16(w1, cur0, acc[1][2 * p]);
-      acc[0][2 * p + 1] = mfma16(w0, cur1, acc[0][2 * p + 1]);
-      acc[1][2 * p + 1] = mfma16(w1, cur1, acc[1][2 * p + 1]);
+      if constexpr ((RS_LAB & 1) == 0) {
+        acc[0][2 * p] = mfma16(w0, cur0, acc[0][2 * p]);
+        acc[1][2 * p] = mfma16(w1, cur0, acc[1][2 * p]);
+        acc[0][2 * p + 1] = mfma16(w0, cur1, acc[0][2 * p + 1]);
+        acc[1][2 * p + 1] = mfma16(w1, cur1, acc[1][2 * p + 1]);
+      } else {   // keep the fragment reads live without the MFMAs
+        asm volatile("" :: "v"(w0), "v"(w1), "v"(cur0), "v"(cur1));
+      }
       cur0 = nx0;
       cur1 = nx1;
     }

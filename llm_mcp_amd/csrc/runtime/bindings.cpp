@@ -100,7 +100,8 @@ PYBIND11_MODULE(_lmx_runtime, m) {
            py::arg("seed") = 0)
       .def("abort", &Scheduler::abort)
       .def("set_mixed_prefill_cap", &Scheduler::set_mixed_prefill_cap, py::arg("tokens"),
-           py::arg("min_decodes"))
+           py::arg("min_decodes"), py::arg("later_steps") = 0)
+      .def_property_readonly("steps", &Scheduler::steps)
       .def("set_penalties", &Scheduler::set_penalties, py::arg("id"), py::arg("repetition"),
            py::arg("presence"), py::arg("frequency"), py::arg("last_n"))
       .def("schedule", [](Scheduler& s, int q_per_tile) {

@@ -40,6 +40,7 @@ void Scheduler::add(int64_t id, const std::vector<int32_t>& prompt, int max_new,
   s->top_p = top_p;
   s->seed = seed;
   s->arrival = arrival_++;
+  s->arrival_step = steps_;
   Seq* raw = s.get();
   seqs_[id] = std::move(s);
   // priority first (higher earlier), FIFO inside a priority
@@ -147,10 +148,19 @@ const StepPlan& Scheduler::schedule(int q_per_tile) {
   // decoding stream for the whole step); a step without decodes -- an idle
   // engine taking a burst -- keeps the full max_batched_tokens
   int prefill_left = INT_MAX;
+  ++steps_;
   if (mixed_prefill_cap_ > 0) {
+    // the newest request with prompt tokens left (running chunks, waiting)
+    int64_t newest = -1;
+    if (mixed_later_ > 0) {
+      for (Seq* s : running_)
+        if ((int)s->tokens.size() - s->num_computed > 1) newest = std::max(newest, s->arrival_step);
+      for (Seq* s : waiting_) newest = std::max(newest, s->arrival_step);
+    }
     int nd = 0;
     for (Seq* s : running_)
-      nd += ((int)s->tokens.size() - s->num_computed) == 1;
+      nd += ((int)s->tokens.size() - s->num_computed) == 1 &&
+            (mixed_later_ == 0 || newest - s->arrival_step >= mixed_later_);
     if (nd >= mixed_min_decodes_) prefill_left = mixed_prefill_cap_;
   }
   std::vector<Seq*> decodes, prefills;

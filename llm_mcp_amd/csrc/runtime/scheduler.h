@@ -39,6 +39,7 @@ struct Seq {
   int num_generated = 0;
   int priority = 0;
   int64_t arrival = 0;
+  int64_t arrival_step = 0;     // the scheduler step count when it was added
   bool ignore_eos = false;
   std::vector<int32_t> stop_ids;
   // sampling parameters travel with the sequence so the plan carries them
@@ -131,11 +132,17 @@ class Scheduler {
   void discard_lookahead();
 
   // prefill tokens of a step that also carries >= min_decodes decode rows
-  // (0: no cap beyond max_batched_tokens)
-  void set_mixed_prefill_cap(int tokens, int min_decodes) {
+  // (0: no cap beyond max_batched_tokens).  later_steps > 0: only decode rows
+  // whose request was added at least later_steps scheduler steps before the
+  // newest request with prefill work count -- streams interrupted by LATER
+  // arrivals (steady serving); the rows of one burst, prefilled together,
+  // never cap each other (a wave keeps the full token budget)
+  void set_mixed_prefill_cap(int tokens, int min_decodes, int later_steps = 0) {
     mixed_prefill_cap_ = tokens > 0 ? tokens : 0;
     mixed_min_decodes_ = min_decodes > 0 ? min_decodes : 1;
+    mixed_later_ = later_steps > 0 ? later_steps : 0;
   }
+  int64_t steps() const { return steps_; }
   int num_waiting() const { return (int)waiting_.size(); }
   int num_running() const { return (int)running_.size(); }
   bool has_work() const { return !waiting_.empty() || !running_.empty(); }
@@ -151,7 +158,8 @@ class Scheduler {
 
   BlockManager bm_;
   int max_num_seqs_, max_batched_tokens_, max_model_len_, max_blocks_;
-  int mixed_prefill_cap_ = 0, mixed_min_decodes_ = 1;
+  int mixed_prefill_cap_ = 0, mixed_min_decodes_ = 1, mixed_later_ = 0;
+  int64_t steps_ = 0;
   std::unordered_map<int64_t, std::unique_ptr<Seq>> seqs_;
   std::deque<Seq*> waiting_;
   std::vector<Seq*> running_;

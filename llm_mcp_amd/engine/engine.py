@@ -112,6 +112,11 @@ class EngineConfig:
         default_factory=lambda: _env_int("LMX_MIXED_PREFILL_TOKENS", 0))
     mixed_min_decodes: int = field(
         default_factory=lambda: _env_int("LMX_MIXED_MIN_DECODES", 32))
+    # the cap counts only decode rows whose request came >= this many
+    # scheduler steps before the newest request with prompt tokens left
+    # (0: every decode row): one burst's rows never cap each other
+    mixed_later_steps: int = field(
+        default_factory=lambda: _env_int("LMX_MIXED_LATER_STEPS", 2))
     max_model_len: int = 8192
     kv_fraction: float = 0.6        # of free HBM after weights
     kv_cache_gb: float | None = None
@@ -278,7 +283,8 @@ class LLMEngine:
                                         ecfg.max_batched_tokens, self.max_model_len,
                                         ecfg.prefix_cache)
         if ecfg.mixed_prefill_tokens and ecfg.mixed_prefill_tokens < ecfg.max_batched_tokens:
-            self.sched.set_mixed_prefill_cap(ecfg.mixed_prefill_tokens, ecfg.mixed_min_decodes)
+            self.sched.set_mixed_prefill_cap(ecfg.mixed_prefill_tokens, ecfg.mixed_min_decodes,
+                                             ecfg.mixed_later_steps)
         self.max_blocks = math.ceil(self.max_model_len / BLOCK_SIZE)
         self.max_parts = max(1, min(16, math.ceil(self.max_model_len / ecfg.part_tokens)))
         self.decode_ws = ops.DecodeWorkspace(ecfg.max_num_seqs, self.Hq, self.D, self.max_parts,

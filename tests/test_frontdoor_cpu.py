@@ -239,3 +239,7 @@ def test_config5_mixed_load_with_a_faulty_replica():
     assert faulty["restarts"] >= 1 and healthy["restarts"] == 0, r["workers"]
     dev = next(d for d in r["circuit_states_seen"] if d.endswith("gpu0.r1"))
     assert "degraded" in r["circuit_states_seen"][dev], r["circuit_states_seen"]
+    # the fault -> recovery phases on the bench's own clock
+    rec = r["recovery"]
+    assert rec["breaker_trip_s"] is not None and rec["worker_restarted_s"] is not None, rec
+    assert rec["worker_died_s"] <= rec["worker_restarted_s"], rec
