@@ -425,6 +425,27 @@ for step in "$@"; do
       run embed_http 600 python -u -m llm_mcp_amd.bench.serving_bench embed --requests 1024 || exit $? ;;
     rope_probe)
       run rope_probe 120 python -u tools/rope_probe.py || exit $? ;;
+    prof_embed)
+      # nomic engine at 1k-token docs under a kernel trace: the kernel-class split
+      rm -rf gpurun_out/prof_embed
+      run prof_embed 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_embed -o run \
+          -- python3 -m llm_mcp_amd.bench.embed_engine_bench || exit $?
+      python tools/prof_summary.py gpurun_out/prof_embed/run_results.db --top 30 \
+          > gpurun_out/prof_embed_summary.md 2>&1 || true
+      find gpurun_out/prof_embed -name "*.db" -delete 2>/dev/null || true ;;
+    closed_cap)
+      # closed loop at 256 streams with a mixed-step cap of CAP tokens (burst-aware:
+      # LMX_MIXED_LATER_STEPS) -- the per-token gap p99 against the uncapped default
+      LMX_MIXED_PREFILL_TOKENS=${CAP:-2048} run closed_cap_${CAP:-2048} 600 python bench.py \
+          --load closed --duration ${CLOSED_S:-40} --closed-warmup 10 || exit $? ;;
+    closed_nocap0)
+      LMX_MIXED_PREFILL_TOKENS=0 run closed_nocap0 600 python bench.py --load closed \
+          --duration ${CLOSED_S:-40} --closed-warmup 10 || exit $? ;;
+    bench_cap)
+      LMX_MIXED_PREFILL_TOKENS=${CAP:-2048} run bench_cap_${CAP:-2048} 600 python bench.py \
+          --steps 6 --warmup 1 || exit $? ;;
+    bench6)
+      run bench6 600 python bench.py --steps 6 --warmup 1 || exit $? ;;
     smoke)
       run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     *)
