@@ -67,7 +67,7 @@ def _run(cmd: list[str]) -> str:
 # instantiation must compile with no VGPR spill and no scratch.  The compile of
 # these sources adds -Rpass-analysis=kernel-resource-usage and the build fails
 # on a violation; the parsed table is kept in build/kernels/resource_usage.json.
-ASM_RING_KERNELS = {"rsgemm.hip": r"rsgemm_kernel",
+ASM_RING_KERNELS = {"rsgemm.hip": r"rsgemm4?_kernel",
                     "attention.hip": r"paged_decode_\w*kernelILi\d+ELi9E"}
 
 
@@ -145,6 +145,9 @@ def build_kernels(force: bool = False, verbose: bool = False) -> Path:
             jobs.append(common + extra + ["-c", str(s), "-o", str(o)])
             if ring:
                 audit_srcs.append((len(jobs) - 1, s.name))
+                # the device listing for the in-flight-register audit below
+                jobs.append(common + ["--cuda-device-only", "-S", str(s), "-o",
+                                      str(objdir / (s.stem + ".s"))])
     bo = objdir / "bindings.o"
     objs.append(bo)
     bsrc = kdir / "bindings.cpp"
@@ -160,6 +163,15 @@ def build_kernels(force: bool = False, verbose: bool = False) -> Path:
             for i, name in audit_srcs:
                 usage[name] = parse_resource_usage(logs[i])
             bad = audit_asm_rings(usage)
+            # no instruction may touch an inline-asm load's destination while
+            # the load is in flight (the compiler cannot see those loads)
+            from .utils.vmem_audit import audit_listing
+            for _, name in audit_srcs:
+                lst = (objdir / (Path(name).stem + ".s")).read_text()
+                for fn, iss in audit_listing(lst, ASM_RING_KERNELS[name]).items():
+                    if iss:
+                        bad.append(f"{name}: {fn[:80]} touches in-flight load registers "
+                                   f"({len(iss)}x, first: {iss[0][1]})")
             if bad:
                 for i, _ in audit_srcs:
                     Path(jobs[i][jobs[i].index("-o") + 1]).unlink(missing_ok=True)

@@ -104,6 +104,14 @@ __device__ __forceinline__ void rs_wait0(bf16x8_t& a, bf16x8_t& b) {
   asm volatile("s_waitcnt vmcnt(0)" : "+v"(a), "+v"(b) :: "memory");
 }
 
+// the same for K14W's four loads per K32 step: every destination of the
+// step is an operand, so none of them is touched before the wait
+template <int CNT>
+__device__ __forceinline__ void rs_wait4(bf16x8_t (&w)[4]) {
+  asm volatile("s_waitcnt vmcnt(%4)" : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3])
+               : "n"(CNT) : "memory");
+}
+
 __device__ __forceinline__ float rs_silu(float g) { return g / (1.f + __expf(-g)); }
 
 // split-K combine of the last arriving slice: acc[j][g] = sum over the S
@@ -174,7 +182,7 @@ template <int EPI, int D, int NA, int NT, int RM, int BM>
 __global__ void __launch_bounds__(RS_THREADS, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) rsgemm_kernel(
     bf16_t* __restrict__ C, const bf16_t* __restrict__ A, const bf16_t* __restrict__ Wp,
     float* __restrict__ slabs, unsigned* __restrict__ tickets, int M, int N, int K, long lda,
-    long ldw, long ldc, int splits) {
+    long ldw, long ldc, int splits, int rot_mul) {
   constexpr int U = D / 2;
   // NA = U + 1: the prologue then issues every A slot it counts on (with
   // fewer slots the early steps would see fewer ops behind a load than the
@@ -195,6 +203,12 @@ __global__ void __launch_bounds__(RS_THREADS, 2) __attribute__((amdgpu_waves_per
   const int ks = wg % splits, rest = wg / splits;
   const int tm = rest % tiles_m, tn = rest / tiles_m, m0 = tm * BM;
   const int kc = K / splits, k0 = ks * kc, nk64 = kc / RS_BK;
+  // K-step order rotated per column tile (rot_mul > 0; the two row tiles of
+  // a column tile keep the same order, so their weight reads still merge):
+  // the workgroups of an XCD then read different activation k-slices and
+  // weight offsets at any moment instead of all hitting the same L2 lines
+  const int rot = (BM != 256 && rot_mul) ? (tn * rot_mul) % nk64 : 0;   // (all-rows tiles: none, registers)
+  auto kofs = [&](int step) { return k0 + ((step + rot) % nk64) * RS_BK; };
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int fr = lane & 15, fg = lane >> 4;
@@ -214,6 +228,7 @@ __global__ void __launch_bounds__(RS_THREADS, 2) __attribute__((amdgpu_waves_per
   constexpr int I0 = 0, I1 = RM ? 0 : 1024, I2 = RM ? 64 : 2048, I3 = RM ? 64 : 3072;
   auto wsb = [&](int k) -> const void* {   // wave-uniform base of K32 step k
     if constexpr ((RS_LAB & 2) != 0) k = 0;
+    if (rot) k = (k + 2 * rot) % (2 * nk64);   // even k: the step pair stays contiguous
     return (const void*)(wstream + (long)k * KSTEP);
   };
 
@@ -228,7 +243,7 @@ __global__ void __launch_bounds__(RS_THREADS, 2) __attribute__((amdgpu_waves_per
 #pragma unroll
   for (int s = -U; s < 0; ++s) {
     if (s + NA - 1 >= 0) rs_stage_a<BM>(lds + ((s + NA - 1) % NA) * SLOT, A, lda, M, m0,
-                                        k0 + (s + NA - 1) * RS_BK);
+                                        kofs(s + NA - 1));
     {
       const int k = 2 * (s + U);                     // K32 steps 2s + D, 2s + D + 1
       const void* b = wsb(k);
@@ -286,7 +301,7 @@ __global__ void __launch_bounds__(RS_THREADS, 2) __attribute__((amdgpu_waves_per
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       rs_stage_a<BM>(lds + ((t + NA - 1) % NA) * SLOT, A, lda, M, m0,
-                     k0 + (t + NA - 1) * RS_BK);
+                     kofs(t + NA - 1));
       const bf16_t* slot = lds + (t % NA) * SLOT;
       const void* b = wsb(2 * t + D);
       compute(slot, 0, wr[2 * u][0], wr[2 * u][1]);
@@ -311,7 +326,7 @@ __global__ void __launch_bounds__(RS_THREADS, 2) __attribute__((amdgpu_waves_per
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (t + NA - 1 < nk64)
-      rs_stage_a<BM>(lds + ((t + NA - 1) % NA) * SLOT, A, lda, M, m0, k0 + (t + NA - 1) * RS_BK);
+      rs_stage_a<BM>(lds + ((t + NA - 1) % NA) * SLOT, A, lda, M, m0, kofs(t + NA - 1));
     const bf16_t* slot = lds + (t % NA) * SLOT;
     compute(slot, 0, wr[2 * u][0], wr[2 * u][1]);
     rs_wait0(wr[2 * u + 1][0], wr[2 * u + 1][1]);
@@ -389,6 +404,240 @@ __global__ void __launch_bounds__(RS_THREADS, 2) __attribute__((amdgpu_waves_per
   }
 }
 
+// ---- K14W: one wave per SIMD, 64 columns per wave ---------------------------
+// Why (profiles/r6_decode_gemm.md, tools/rs_decomp.sh): K14 at 256 rows sits on
+// two separate ceilings of about its own run time -- the weight stream alone
+// (MFMAs removed: 67.7 us for gate/up) is latency-bound at ~64 KB in flight
+// per CU (8 waves x a 4-step register ring), and the LDS fragment reads plus
+// the MFMAs alone (memory made L1-hot: 62.6 us) serialise at 512 + 512 cycles
+// per K32 step, because every one of the 8 waves re-reads the whole
+// activation panel from LDS for its 32 columns.  Here a 256-thread workgroup
+// (one wave per SIMD, up to 512 VGPRs incl. AGPRs) owns the same BM x 256
+// tile: wave w owns columns [64 w, 64 w + 64) = K14 wave units 2w, 2w + 1
+// (the packed layout is unchanged), so
+//   * each activation fragment read from LDS feeds 4 MFMAs (LDS traffic per
+//     CU halves: 256 cycles per K32 step against 512 MFMA cycles per SIMD);
+//   * the weight ring is D = 8 K32 steps deep (32 KB per wave, 128 KB per CU
+//     in flight, twice K14's);
+//   * issue order per K64 step t: [GA LDS-DMA: A(t + NA - 1)] [4 loads:
+//     W(2t + D)] [4 loads: W(2t + 1 + D)] with the same hand-counted waits.
+// Epilogues: bf16, fp32 partials (split-K, no in-kernel combine) and SwiGLU16.
+template <int EPI, int D, int NA, int NT, int BM>
+__global__ void __launch_bounds__(256, 1) rsgemm4_kernel(
+    bf16_t* __restrict__ C, const bf16_t* __restrict__ A, const bf16_t* __restrict__ Wp,
+    float* __restrict__ slabs, int M, int N, int K, long lda, long ldc, int splits) {
+  constexpr int U = D / 2;
+  static_assert(D % 2 == 0 && U >= 2 && NA == U + 1, "ring shape");
+  static_assert(BM == 128 || BM == 64, "row tile");
+  constexpr int NG = BM / 16, GA = BM / 32, OPS = GA + 8;
+  constexpr int SLOT = BM * RS_BK;
+  constexpr int WAIT_TOP = 4 + OPS * (U - 1);       // W(2t) landed, top of step t
+  constexpr int WAIT_W1 = OPS * (U - 1) + GA + 4;   // W(2t + 1) landed, mid step
+  static_assert(WAIT_W1 < 64 && WAIT_TOP < 64, "vmcnt is 6 bits");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* const lds = reinterpret_cast<bf16_t*>(smem);
+
+  const int tiles_m = (M + BM - 1) / BM, tiles = N / RS_BN, nwg = tiles_m * tiles * splits;
+  const int wg = xcd_remap(blockIdx.x, nwg);
+  const int ks = wg % splits, rest = wg / splits;
+  const int tm = rest % tiles_m, tn = rest / tiles_m, m0 = tm * BM;
+  const int kc = K / splits, k0 = ks * kc, nk64 = kc / RS_BK;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int fr = lane & 15, fg = lane >> 4;
+
+  // the two K14 wave units of this wave: 2 x 1 KB runs per K32 step each
+  const char* ws0 = reinterpret_cast<const char*>(Wp) +
+                    ((long)(tn * 8 + 2 * wave) * (K / 32) + k0 / 32) * 2048;
+  const char* ws1 = ws0 + (long)(K / 32) * 2048;
+  const unsigned voff = lane * 16;
+  auto wsb = [&](const char* ws, int k) -> const void* {   // K32 step k
+    if constexpr ((RS_LAB & 2) != 0) k = 0;
+    return (const void*)(ws + (long)k * 2048);
+  };
+  // A: BM rows x 64 k per K64 step, 256 lanes x 16 B per instruction
+  auto stage_a = [&](bf16_t* slot, int kk) {
+    const int t = threadIdx.x, rr = t >> 3, c = t & 7;
+    if constexpr ((RS_LAB & 4) != 0) kk = 0;
+#pragma unroll
+    for (int i = 0; i < GA; ++i) {
+      const int r = i * 32 + rr;
+      const int gr = m0 + r < M ? m0 + r : M - 1;
+      __builtin_amdgcn_global_load_lds(A + (long)gr * lda + kk + 8 * (c ^ rs_swz(r)),
+                                       (rs_lds_t*)(slot + (i * 32 + wave * 8) * RS_BK), 16, 0, 0);
+    }
+  };
+
+  f32x4_t acc[4][NG];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int g = 0; g < NG; ++g) acc[j][g] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  bf16x8_t wr[D][4];   // [K32 step][col tile 2u + j]
+
+  auto issue_w = [&](int k, bf16x8_t (&dst)[4], int imm_half) {
+    // imm_half 0: K32 step k at [base, +2 KB); 1: the step after it at [+2, +4 KB)
+    const void* b0 = wsb(ws0, k - imm_half);
+    const void* b1 = wsb(ws1, k - imm_half);
+    if (imm_half == 0) {
+      rs_ldw<NT, 0>(dst[0], b0, voff);
+      rs_ldw<NT, 1024>(dst[1], b0, voff);
+      rs_ldw<NT, 0>(dst[2], b1, voff);
+      rs_ldw<NT, 1024>(dst[3], b1, voff);
+    } else {
+      rs_ldw<NT, 2048>(dst[0], b0, voff);
+      rs_ldw<NT, 3072>(dst[1], b0, voff);
+      rs_ldw<NT, 2048>(dst[2], b1, voff);
+      rs_ldw<NT, 3072>(dst[3], b1, voff);
+    }
+  };
+
+#pragma unroll
+  for (int s = -U; s < 0; ++s) {
+    stage_a(lds + ((s + NA - 1) % NA) * SLOT, k0 + (s + NA - 1) * RS_BK);
+    const int k = 2 * (s + U);
+    issue_w(k, wr[k], 0);
+    issue_w(k + 1, wr[k + 1], 1);
+  }
+
+  // one K32 sub-step: row-group fragments in pairs, the next pair in flight
+  // while the current pair's 8 MFMAs run
+  auto compute = [&](const bf16_t* slot, int kk, const bf16x8_t (&w)[4]) {
+    bf16x8_t cur0 = rs_afrag(slot, fr, kk * 4 + fg);
+    bf16x8_t cur1 = rs_afrag(slot, 16 + fr, kk * 4 + fg);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int p = 0; p < NG / 2; ++p) {
+      bf16x8_t nx0 = cur0, nx1 = cur1;
+      if (p < NG / 2 - 1) {
+        nx0 = rs_afrag(slot, 32 * (p + 1) + fr, kk * 4 + fg);
+        nx1 = rs_afrag(slot, 32 * (p + 1) + 16 + fr, kk * 4 + fg);
+      }
+      if constexpr ((RS_LAB & 1) == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc[j][2 * p] = mfma16(w[j], cur0, acc[j][2 * p]);
+          acc[j][2 * p + 1] = mfma16(w[j], cur1, acc[j][2 * p + 1]);
+        }
+      } else {
+        asm volatile("" :: "v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]), "v"(cur0), "v"(cur1));
+      }
+      cur0 = nx0;
+      cur1 = nx1;
+    }
+    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+#pragma unroll
+    for (int p = 0; p < NG / 2 - 1; ++p) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // a do-while (the host guarantees nk64 >= 2U): a loop entered on a branch
+  // gets phi copies of the ring registers at its entry, taken while their
+  // loads are still in flight (tools/vmem_hazard_audit.py)
+  int t0 = 0;
+  do {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int t = t0 + u;
+      rs_wait4<WAIT_TOP>(wr[2 * u]);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      stage_a(lds + ((t + NA - 1) % NA) * SLOT, k0 + (t + NA - 1) * RS_BK);
+      const bf16_t* slot = lds + (t % NA) * SLOT;
+      compute(slot, 0, wr[2 * u]);
+      __builtin_amdgcn_sched_barrier(0);
+      rs_mfma_war_pad();
+      issue_w(2 * t + D, wr[2 * u], 0);
+      rs_wait4<WAIT_W1>(wr[2 * u + 1]);
+      compute(slot, 1, wr[2 * u + 1]);
+      __builtin_amdgcn_sched_barrier(0);
+      rs_mfma_war_pad();
+      issue_w(2 * t + 1 + D, wr[2 * u + 1], 1);
+    }
+    t0 += U;
+  } while (t0 + U <= nk64 - U);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int t = t0 + u;
+    if (t >= nk64) break;
+    rs_wait4<0>(wr[2 * u]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (t + NA - 1 < nk64) stage_a(lds + ((t + NA - 1) % NA) * SLOT, k0 + (t + NA - 1) * RS_BK);
+    const bf16_t* slot = lds + (t % NA) * SLOT;
+    compute(slot, 0, wr[2 * u]);
+    rs_wait4<0>(wr[2 * u + 1]);
+    compute(slot, 1, wr[2 * u + 1]);
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+
+  // acc[j][g][r] = C[m][n]: m = m0 + 16 g + fr, n = 256 tn + 64 wave + 16 j + 4 fg + r
+  const int nb = tn * RS_BN + 64 * wave + 4 * fg;
+  if constexpr (EPI == 2) {
+    float* slab = slabs + (long)ks * M * N;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      const int m = m0 + 16 * g + fr;
+      if (m >= M) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        *reinterpret_cast<f32x4_t*>(slab + (long)m * N + nb + 16 * j) = acc[j][g];
+    }
+  } else if constexpr (EPI == 0) {
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      const int m = m0 + 16 * g + fr;
+      if (m >= M) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        bf16x4_t o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = (short)f2bf(acc[j][g][r]);
+        *reinterpret_cast<bf16x4_t*>(C + (long)m * ldc + nb + 16 * j) = o;
+      }
+    }
+  } else {
+    // SwiGLU16: unit u's tiles 2u (gate) and 2u + 1 (up) hold the same 16
+    // channels; unit u of this wave is K14 wave unit 2 wave + u
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      const int m = m0 + 16 * g + fr;
+      if (m >= M) continue;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        bf16x4_t o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          o[r] = (short)f2bf(rs_silu(acc[2 * u][g][r]) * acc[2 * u + 1][g][r]);
+        *reinterpret_cast<bf16x4_t*>(C + (long)m * ldc + (tn * RS_BN + 64 * wave + 32 * u) / 2 +
+                                     4 * fg) = o;
+      }
+    }
+  }
+}
+
+template <int EPI, int D, int NA, int NT, int BM>
+static int rs4_launch(bf16_t* C, const bf16_t* A, const bf16_t* Wp, float* slabs, int M, int N,
+                      int K, long lda, long ldc, int splits, hipStream_t stream) {
+  constexpr size_t smem = (size_t)NA * BM * RS_BK * sizeof(bf16_t);
+  static_assert(smem <= 160 * 1024, "LDS");
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e = hipFuncSetAttribute((const void*)rsgemm4_kernel<EPI, D, NA, NT, BM>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    if (e != hipSuccess) return (int)e;
+    attr = true;
+  }
+  rsgemm4_kernel<EPI, D, NA, NT, BM>
+      <<<dim3(((M + BM - 1) / BM) * (N / RS_BN) * splits), dim3(256), smem, stream>>>(
+          C, A, Wp, slabs, M, N, K, lda, ldc, splits);
+  return (int)hipGetLastError();
+}
+
 // ---- host -------------------------------------------------------------------
 int rsgemm_pack(void* out, const void* W, int N, int K, long ldw, hipStream_t stream) {
   if (N % RS_BN != 0 || K % 32 != 0) return -1;
@@ -401,7 +650,7 @@ int rsgemm_pack(void* out, const void* W, int N, int K, long ldw, hipStream_t st
 template <int EPI, int D, int NA, int NT, int RM, int BM>
 static int rs_launch(bf16_t* C, const bf16_t* A, const bf16_t* Wp, float* slabs,
                      unsigned* tickets, int M, int N, int K, long lda, long ldw, long ldc,
-                     int splits, hipStream_t stream) {
+                     int splits, int rot_mul, hipStream_t stream) {
   constexpr size_t smem = (size_t)NA * BM * RS_BK * sizeof(bf16_t);
   static_assert(smem <= 160 * 1024, "LDS");
   static bool attr = false;
@@ -413,7 +662,7 @@ static int rs_launch(bf16_t* C, const bf16_t* A, const bf16_t* Wp, float* slabs,
   }
   rsgemm_kernel<EPI, D, NA, NT, RM, BM>
       <<<dim3(((M + BM - 1) / BM) * (N / RS_BN) * splits), dim3(RS_THREADS), smem, stream>>>(
-          C, A, Wp, slabs, tickets, M, N, K, lda, ldw, ldc, splits);
+          C, A, Wp, slabs, tickets, M, N, K, lda, ldw, ldc, splits, rot_mul);
   return (int)hipGetLastError();
 }
 
@@ -427,8 +676,36 @@ int rsgemm(void* C, const void* A, const void* W, float* slabs, unsigned* ticket
            int epi, hipStream_t stream) {
   if (M <= 0) return 0;
   if (M > 256 || N % RS_BN != 0 || splits < 1 || K % (splits * RS_BK) != 0) return -1;
+  if ((cfg >> 4) & 1) {
+    // K14W (bit 4): packed weights, non-temporal (bit 5), 128- or 64-row
+    // tiles, ring D 8; split-K only with the partials epilogue.  Measured
+    // against K14 and not used by the dispatch table (profiles/r6_decode_gemm.md).
+    // All 256 rows do not fit: 256 accumulator rows x 64 columns per wave
+    // spill even with a 4-step ring.
+    const int shape = cfg & 3, bm64 = (cfg >> 3) & 1, nt = (cfg >> 5) & 1;
+    if ((cfg >> 6) & 1 || !((cfg >> 2) & 1 || bm64) || shape != 0 || !nt) return -1;
+    if (epi != 0 && epi != 2 && epi != 3) return -1;
+    if (splits > 1 && epi != 2) return -1;
+    if (epi == 2 && slabs == nullptr) return -2;
+    const int U = 4;
+    const int nk64 = (K / splits) / RS_BK;
+    if (nk64 < 2 * U || nk64 % U != 0) return -1;
+    auto C_ = (bf16_t*)C;
+    auto A_ = (const bf16_t*)A;
+    auto W_ = (const bf16_t*)W;
+#define LMX_RS4_E(BM)                                                                           \
+  if (epi == 3) return rs4_launch<3, 8, 5, 1, BM>(C_, A_, W_, slabs, M, N, K, lda, ldc, splits,   \
+                                                  stream);                                       \
+  if (epi == 2) return rs4_launch<2, 8, 5, 1, BM>(C_, A_, W_, slabs, M, N, K, lda, ldc, splits,   \
+                                                  stream);                                       \
+  return rs4_launch<0, 8, 5, 1, BM>(C_, A_, W_, slabs, M, N, K, lda, ldc, splits, stream);
+    if (bm64) { LMX_RS4_E(64) }
+    LMX_RS4_E(128)
+#undef LMX_RS4_E
+  }
   const int shape = cfg & 3, bm128 = (cfg >> 2) & 1, bm64 = (cfg >> 3) & 1;
   const int nt = (cfg >> 5) & 1, rm = (cfg >> 6) & 1;
+  const int rot = (cfg >> 7) & 1 ? 5 : 0;     // bit 7: K order rotated per column tile
   const int bm = bm64 ? 64 : bm128 ? 128 : 256;
   // shape 1 (D 8 / NA 5) needs 256+ VGPRs: the compiler spills, and a spill
   // of an inline-asm load destination before its data lands is silent
@@ -449,11 +726,11 @@ int rsgemm(void* C, const void* A, const void* W, float* slabs, unsigned* ticket
   auto W_ = (const bf16_t*)W;
 #define LMX_RS_E(D, NA, NT, RM, BM)                                                             \
   if (epi == 3) return rs_launch<3, D, NA, NT, RM, BM>(C_, A_, W_, slabs, tickets, M, N, K, lda, \
-                                                       ldw, ldc, splits, stream);               \
+                                                       ldw, ldc, splits, rot, stream);               \
   if (epi == 2) return rs_launch<2, D, NA, NT, RM, BM>(C_, A_, W_, slabs, tickets, M, N, K, lda, \
-                                                       ldw, ldc, splits, stream);               \
+                                                       ldw, ldc, splits, rot, stream);               \
   return rs_launch<0, D, NA, NT, RM, BM>(C_, A_, W_, slabs, tickets, M, N, K, lda, ldw, ldc,     \
-                                         splits, stream);
+                                         splits, rot, stream);
   // all-rows tiles (BM 256) are built for the partials epilogue only: the
   // bf16 and SwiGLU epilogues spill there (a spilled ring register is silent
   // corruption; build.py audits every instantiation) and no table entry uses them
@@ -462,7 +739,7 @@ int rsgemm(void* C, const void* A, const void* W, float* slabs, unsigned* ticket
   if (bm == 128) { LMX_RS_E(D, NA, NT, RM, 128) } \
   if (epi != 2) return -1;                      \
   return rs_launch<2, D, NA, NT, RM, 256>(C_, A_, W_, slabs, tickets, M, N, K, lda, ldw, ldc, \
-                                          splits, stream);
+                                          splits, rot, stream);
 #define LMX_RS(D, NA)                                  \
   if (nt && rm) { LMX_RS_B(D, NA, 1, 1) }              \
   if (nt) { LMX_RS_B(D, NA, 1, 0) }                    \

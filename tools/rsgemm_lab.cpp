@@ -43,10 +43,10 @@ __global__ void fill_kernel(bf16_t* p, long n, unsigned seed, float scale) {
 }
 
 __global__ void ref_kernel(float* out, const bf16_t* A, const bf16_t* W, const int* rows, int nrows,
-                           int N, int K) {
+                           int N, int K, long lda) {
   const int n = blockIdx.x * blockDim.x + threadIdx.x, ri = blockIdx.y;
   if (n >= N || ri >= nrows) return;
-  const bf16_t* a = A + (long)rows[ri] * K;
+  const bf16_t* a = A + (long)rows[ri] * lda;
   const bf16_t* w = W + (long)n * K;
   float s = 0.f;
   for (int k = 0; k < K; k += 8) {
@@ -88,13 +88,17 @@ int main(int argc, char** argv) {
   const char* ce = std::getenv("LAB_COPIES");
   const int copies = ce ? std::max(1, std::atoi(ce))
                         : (int)std::max<long>(2, (512l << 20) / wbytes + 1);
-  std::printf("shape N=%d K=%d M=%d epi=%d: W %.1f MB x %d copies\n", N, K, M, epi, wbytes / 1e6,
-              copies);
+  // LAB_LDA_PAD: elements of padding per activation row (the row stride the
+  // kernels see), to move rows off a common L2 channel
+  const char* pe = std::getenv("LAB_LDA_PAD");
+  const long lda = K + (pe ? std::atol(pe) : 0);
+  std::printf("shape N=%d K=%d M=%d epi=%d: W %.1f MB x %d copies, lda %ld\n", N, K, M, epi,
+              wbytes / 1e6, copies, lda);
   bf16_t *A, *Wall, *Wpk, *C;
   float *slabs, *ref, *sink;
   unsigned* cnt;
   int* rows_d;
-  CK(hipMalloc(&A, (long)M * K * 2));
+  CK(hipMalloc(&A, (long)M * lda * 2));
   CK(hipMalloc(&Wall, wbytes * copies));
   CK(hipMalloc(&Wpk, wbytes * copies));
   CK(hipMalloc(&C, (long)M * N * 2));
@@ -103,7 +107,7 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&cnt, 65536 * 4));
   CK(hipMemset(cnt, 0, 65536 * 4));
   CK(hipMalloc(&sink, 16));
-  fill_kernel<<<1024, 256>>>(A, (long)M * K, 17u, 1.f);
+  fill_kernel<<<1024, 256>>>(A, (long)M * lda, 17u, 1.f);
   for (int c = 0; c < copies; ++c)
     fill_kernel<<<4096, 256>>>(Wall + (long)c * N * K, (long)N * K, 99u, 0.05f);  // same data
   for (int c = 0; c < copies; ++c)
@@ -119,7 +123,7 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&rows_d, nr * 4));
   CK(hipMemcpy(rows_d, rows.data(), nr * 4, hipMemcpyHostToDevice));
   CK(hipMalloc(&ref, (long)nr * N * 4));
-  ref_kernel<<<dim3((N + 255) / 256, nr), 256>>>(ref, A, Wall, rows_d, nr, N, K);
+  ref_kernel<<<dim3((N + 255) / 256, nr), 256>>>(ref, A, Wall, rows_d, nr, N, K, lda);
   CK(hipDeviceSynchronize());
   std::vector<float> href((long)nr * N);
   CK(hipMemcpy(href.data(), ref, href.size() * 4, hipMemcpyDeviceToHost));
@@ -155,8 +159,8 @@ int main(int argc, char** argv) {
     auto launch = [&](int i) {
       if (rs)
         return lmx::rsgemm(C, A, ((cfg & 64) ? Wall : Wpk) + (long)(i % copies) * N * K, slabs,
-                           cnt, 65536, M, N, K, K, K, ncol, cfg, S, epi, nullptr);
-      return lmx::dgemm(C, A, Wall + (long)(i % copies) * N * K, slabs, cnt, 65536, M, N, K, K, K,
+                           cnt, 65536, M, N, K, lda, K, ncol, cfg, S, epi, nullptr);
+      return lmx::dgemm(C, A, Wall + (long)(i % copies) * N * K, slabs, cnt, 65536, M, N, K, lda, K,
                         ncol, cfg, S, epi, nullptr);
     };
     int rc = launch(0);
