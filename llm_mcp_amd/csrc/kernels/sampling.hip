@@ -332,18 +332,23 @@ int sample(const void* logits, int logits_bf16, long stride, int B, int V, const
 // Per row and rank a phase writes an 8-float record; the caller exchanges the
 // records (one all-gather of B x 32 B per rank: the peer slots under TP, an
 // alias at W = 1) and every rank combines them in rank order into the same
-// row state, so every rank ends with the same token.  Phases:
+// row state, so every rank ends with the same token.  Each mass pass also
+// races the NEXT round over {x > x_j} speculatively (its winner is used only
+// when x_j is rejected), so a round costs one exchange:
 //   0  local max / normaliser / argmax and the round-0 race winner;
-//   1  combine the race winners (round 0: also max / normaliser / argmax;
-//      greedy and untruncated rows finish) -> local mass and count above x_j;
-//   2  combine mass / count -> accept or pivot; race round `round` over
-//      {x > pivot} (round == max_rounds: argmax fallback, write the tokens).
-// Record slots: phase 0 {m, s, ax, aj, key, j, xj}, phase 1 {mass, cnt},
-// phase 2 {-, -, -, -, key, j, xj}: the slots a phase reads and writes are
-// disjoint, so at W = 1 the record may be its own exchange.
+//   1  (round r) r = 0: the row state from the statistics (greedy rows
+//      finish); r > 0: accept round r-1's candidate or pivot on it.  Then
+//      combine round r's winners (untruncated rows finish) -> local mass and
+//      count above x_j + the round r+1 race over {x > x_j};
+//   2  (round = max_rounds) accept the last candidate or take the argmax;
+//      write the tokens.
+// Records: phase 0 {m, s, ax, aj, key, j, xj}, phase 1 {mass, cnt, -, -, key,
+// j, xj}.  Every thread reads the exchanged records before any block-level
+// barrier and thread 0 writes the record after one, so at W = 1 the record
+// may be its own exchange.
 namespace {
 constexpr int RACE_REC = 8, RACE_ST = 12;
-enum { ST_XMAX, ST_S, ST_PIVOT, ST_CJ, ST_CX, ST_DONE, ST_AX, ST_AJ, ST_TOK, ST_LP };
+enum { ST_XMAX, ST_S, ST_CJ, ST_CX, ST_DONE, ST_AX, ST_AJ, ST_TOK, ST_LP };
 
 __device__ __forceinline__ float race_gumbel(RowKey k, uint32_t gi) {
   const uint32_t h = lowbias32(lowbias32(gi ^ k.k0) + k.k1);
@@ -390,13 +395,6 @@ __global__ void __launch_bounds__(1024) race_kernel(
     out3[1] = __int_as_float(c.i);
     out3[2] = c.v == -INFINITY ? -INFINITY : ld<T>(x, c.i - v0);
   };
-  auto finish = [&](int tok, float lp) {
-    if (threadIdx.x == 0) {
-      s[ST_TOK] = __int_as_float(tok);
-      s[ST_LP] = lp;
-      s[ST_DONE] = 1.f;
-    }
-  };
 
   if (phase == 0) {
     MaxSum ms{-INFINITY, 0.f};
@@ -417,86 +415,81 @@ __global__ void __launch_bounds__(1024) race_kernel(
     return;
   }
 
-  if (phase == 1) {
-    if (round == 0) {
-      // the row state from the ranks' statistics, combined in rank order
-      float xmax = -INFINITY;
-      for (int q = 0; q < W; ++q) xmax = fmaxf(xmax, g(q, 0));
-      float S = 0.f;
-      ArgMax am{-INFINITY, 0x7fffffff};
-      for (int q = 0; q < W; ++q) {
-        if (g(q, 0) != -INFINITY) S += g(q, 1) * __expf((g(q, 0) - xmax) * inv_t);
-        am = argmax_combine(am, ArgMax{g(q, 2), __float_as_int(g(q, 3))});
-      }
-      if (threadIdx.x == 0) {
-        s[ST_XMAX] = xmax; s[ST_S] = S; s[ST_PIVOT] = -INFINITY; s[ST_DONE] = 0.f;
-        s[ST_AX] = am.v; s[ST_AJ] = __int_as_float(am.i);
-      }
-      if (greedy) {
-        finish(am.i, am.v - xmax - __logf(S));
-        if (threadIdx.x == 0) { r[0] = 0.f; r[1] = 0.f; }
-        return;
-      }
-      __syncthreads();
+  // ---- every read of the exchanged records and of the row state first ----
+  float xmax, S, ax;
+  int aj;
+  bool done;
+  float mass_in = 0.f, cnt_in = 0.f;
+  if (round == 0) {
+    xmax = -INFINITY;
+    for (int q = 0; q < W; ++q) xmax = fmaxf(xmax, g(q, 0));
+    S = 0.f;
+    ArgMax am{-INFINITY, 0x7fffffff};
+    for (int q = 0; q < W; ++q) {
+      if (g(q, 0) != -INFINITY) S += g(q, 1) * __expf((g(q, 0) - xmax) * inv_t);
+      am = argmax_combine(am, ArgMax{g(q, 2), __float_as_int(g(q, 3))});
     }
-    const float xmax = s[ST_XMAX], S = s[ST_S];
-    bool done = s[ST_DONE] != 0.f;
-    ArgMax c{-INFINITY, 0x7fffffff};
-    float cx = -INFINITY;
+    ax = am.v;
+    aj = am.i;
+    done = false;
+  } else {
+    xmax = s[ST_XMAX]; S = s[ST_S]; ax = s[ST_AX]; aj = __float_as_int(s[ST_AJ]);
+    done = s[ST_DONE] != 0.f;
+    for (int q = 0; q < W; ++q) { mass_in += g(q, 0); cnt_in += g(q, 1); }
+  }
+  ArgMax c{-INFINITY, 0x7fffffff};
+  float cx = -INFINITY;
+  if (phase == 1) {
     for (int q = 0; q < W; ++q) {
       const ArgMax b{g(q, 4), __float_as_int(g(q, 5))};
       if (b.v > c.v || (b.v == c.v && b.i < c.i)) { c = b; cx = g(q, 6); }
     }
-    __syncthreads();   // every thread has read the state before it changes
-    if (!done && c.v == -INFINITY) {   // nothing above the pivot: the argmax
-      finish(__float_as_int(s[ST_AJ]), (s[ST_AX] - xmax) * inv_t - __logf(S));
-      done = true;
-    } else if (!done && !truncate) {
-      finish(c.i, (cx - xmax) * inv_t - __logf(S));
-      done = true;
-    } else if (!done && threadIdx.x == 0) {
-      s[ST_CJ] = __int_as_float(c.i);
-      s[ST_CX] = cx;
-    }
-    float mass = 0.f, cnt = 0.f;
-    if (!done) {
-      scan_row(x, Vs, [&](int i, float v) {
-        if (v > cx) { mass += __expf((v - xmax) * inv_t); cnt += 1.f; }
-      });
-      mass = block_sum(mass, sv);
-      cnt = block_sum(cnt, sv);
-    }
-    if (threadIdx.x == 0) { r[0] = mass; r[1] = cnt; }
-    return;
   }
+  const int prev_j = __float_as_int(s[ST_CJ]);
+  const float prev_x = s[ST_CX];
+  __syncthreads();    // nothing below writes before every thread has read
 
-  // phase 2: decide the previous round's candidate, race round `round`
-  const float xmax = s[ST_XMAX], S = s[ST_S];
-  bool done = s[ST_DONE] != 0.f;
-  float pivot = s[ST_PIVOT];
-  if (!done) {
-    float mass = 0.f, cnt = 0.f;
-    for (int q = 0; q < W; ++q) { mass += g(q, 0); cnt += g(q, 1); }
-    mass /= S;
-    const float cx = s[ST_CX];
-    __syncthreads();
-    if (mass < tp && (kk <= 0 || cnt < (float)kk)) {
-      finish(__float_as_int(s[ST_CJ]), (cx - xmax) * inv_t - __logf(S));
-      done = true;
-    } else if (round >= max_rounds) {
-      finish(__float_as_int(s[ST_AJ]), (s[ST_AX] - xmax) * inv_t - __logf(S));
-      done = true;
-    } else {
-      pivot = cx;
-      if (threadIdx.x == 0) s[ST_PIVOT] = pivot;
+  int tok = 0;
+  float lp = 0.f;
+  const float logS = __logf(S);
+  if (round == 0 && greedy) {
+    done = true; tok = aj; lp = ax - xmax - logS;
+  } else if (round > 0 && !done) {
+    // round - 1's candidate: accepted, or the pivot of this round's race
+    if (mass_in / S < tp && (kk <= 0 || cnt_in < (float)kk)) {
+      done = true; tok = prev_j; lp = (prev_x - xmax) * inv_t - logS;
+    } else if (phase == 2) {
+      done = true; tok = aj; lp = (ax - xmax) * inv_t - logS;   // rounds used up: the argmax
     }
   }
+  if (phase == 1 && !done) {
+    if (c.v == -INFINITY) {                   // nothing above the pivot: the argmax
+      done = true; tok = aj; lp = (ax - xmax) * inv_t - logS;
+    } else if (!truncate) {
+      done = true; tok = c.i; lp = (cx - xmax) * inv_t - logS;
+    }
+  }
+  float mass = 0.f, cnt = 0.f;
   float c3[3] = {-INFINITY, __int_as_float(0x7fffffff), -INFINITY};
-  if (!done) race(round, pivot, c3);
-  if (threadIdx.x == 0) { r[4] = c3[0]; r[5] = c3[1]; r[6] = c3[2]; }
-  if (round >= max_rounds) {
-    __syncthreads();
-    if (threadIdx.x == 0) {
+  if (phase == 1 && !done) {
+    scan_row(x, Vs, [&](int i, float v) {
+      if (v > cx) { mass += __expf((v - xmax) * inv_t); cnt += 1.f; }
+    });
+    mass = block_sum(mass, sv);
+    cnt = block_sum(cnt, sv);
+    // the next round's race over {x > x_j}, used only if x_j is rejected
+    if (round + 1 < max_rounds) race(round + 1, cx, c3);
+  }
+  if (threadIdx.x == 0) {
+    const bool was_done = round > 0 && s[ST_DONE] != 0.f;   // (round 0: last call's state)
+    if (round == 0) {
+      s[ST_XMAX] = xmax; s[ST_S] = S; s[ST_AX] = ax; s[ST_AJ] = __int_as_float(aj);
+    }
+    if (phase == 1 && !done) { s[ST_CJ] = __int_as_float(c.i); s[ST_CX] = cx; }
+    if (done && !was_done) { s[ST_TOK] = __int_as_float(tok); s[ST_LP] = lp; }
+    s[ST_DONE] = done ? 1.f : 0.f;
+    r[0] = mass; r[1] = cnt; r[4] = c3[0]; r[5] = c3[1]; r[6] = c3[2];
+    if (phase == 2) {
       out_tok[row] = __float_as_int(s[ST_TOK]);
       if (out_lp) out_lp[row] = s[ST_LP];
     }

@@ -348,7 +348,7 @@ def prefill_q_per_tile(Hq: int, Hkv: int, D: int = 128) -> int:
 # ---------------------------------------------------------------- sampling ---
 # race rounds of sample_race: a row still rejected after them (top-p 0.95:
 # ~0.05^4) takes the argmax
-RACE_ROUNDS = int(os.environ.get("LMX_RACE_ROUNDS", "4"))
+RACE_ROUNDS = int(os.environ.get("LMX_RACE_ROUNDS", "4"))     # max_rounds + 1 exchanges
 
 
 def sample(logits: torch.Tensor, temperature: torch.Tensor, top_k: torch.Tensor,
@@ -418,11 +418,9 @@ def sample_race(logits: torch.Tensor, temperature: torch.Tensor, top_k: torch.Te
 
     k.race_sample_phase(0, 0, max_rounds, *common, _ptr(rec), world, _ptr(rec), _ptr(st),
                         _ptr(out_tok), _ptr(out_lp), stream)    # phase 0 reads no records
-    phase(1, 0, exchange(rec))
-    for rnd in range(1, max_rounds + 1):
-        phase(2, rnd, exchange(rec))
-        if rnd < max_rounds:
-            phase(1, rnd, exchange(rec))
+    for rnd in range(max_rounds):       # one exchange per round (race_kernel phase 1)
+        phase(1, rnd, exchange(rec))
+    phase(2, max_rounds, exchange(rec))
     return out_tok, out_lp
 
 

@@ -267,13 +267,13 @@ def race_gumbel(seed: int, off: int, rnd: int, idx: torch.Tensor) -> torch.Tenso
 
 def sample_race(logits, temperature, top_k, top_p, seeds, offsets, exchange, v0, V,
                 max_rounds):
-    """CPU mirror of ops.sample_race (the race_kernel phases, same records and
-    exchanges): exact race winners, so every rank -- and a one-shard run over
-    the whole row -- picks the same tokens."""
+    """CPU mirror of ops.sample_race (race_kernel's phases, same records and
+    exchanges -- one per round, the next round raced speculatively with each
+    mass pass): exact race winners, so every rank -- and a one-shard run
+    over the whole row -- picks the same tokens."""
     B, Vs = logits.shape
     x = logits.float()
     idx = torch.arange(v0, v0 + Vs, dtype=torch.int64)
-    rec = torch.zeros(B, 8)
     temp = [float(t) for t in temperature[:B]]
     kk = [int(k) for k in top_k[:B]] if top_k is not None else [0] * B
     tp = [float(p) for p in top_p[:B]] if top_p is not None else [1.0] * B
@@ -282,24 +282,25 @@ def sample_race(logits, temperature, top_k, top_p, seeds, offsets, exchange, v0,
     greedy = [not (t > 0) or k == 1 for t, k in zip(temp, kk)]
     inv_t = [1.0 if g else 1.0 / t for g, t in zip(greedy, temp)]
     trunc = [not g and (p < 1.0 or 0 < k < V) for g, p, k in zip(greedy, tp, kk)]
+    NONE = (-math.inf, 0x7FFFFFFF, -math.inf)
 
     def race(b, rnd, pivot):
         keep = x[b] > pivot
         if not bool(keep.any()):
-            return -math.inf, 0x7FFFFFFF, -math.inf
+            return NONE
         key = x[b] * inv_t[b] + race_gumbel(sd[b], of[b], rnd, idx)
         key = torch.where(keep, key, torch.full_like(key, -math.inf))
         j = int(torch.argmax(key))          # first maximum: the lowest index
         return float(key[j]), v0 + j, float(x[b, j])
 
+    rec = torch.zeros(B, 8)
     for b in range(B):                       # phase 0
         m = float(x[b].max())
-        s = float(torch.exp((x[b] - m) * inv_t[b]).sum())
+        s_ = float(torch.exp((x[b] - m) * inv_t[b]).sum())
         j = int(torch.argmax(x[b]))
-        c = race(b, 0, -math.inf) if not greedy[b] else (-math.inf, 0x7FFFFFFF, -math.inf)
-        rec[b] = torch.tensor([m, s, float(x[b, j]), 0, c[0], 0, c[2], 0])
-        rec[b, 3] = float(v0 + j)           # indices travel as floats here (exact < 2^24)
-        rec[b, 5] = float(c[1])
+        c = race(b, 0, -math.inf) if not greedy[b] else NONE
+        # indices travel as floats here (exact below 2^24)
+        rec[b] = torch.tensor([m, s_, float(x[b, j]), float(v0 + j), c[0], float(c[1]), c[2], 0])
     g = exchange(rec)
     W = g.shape[0]
     xmax, S = [0.0] * B, [0.0] * B
@@ -307,78 +308,57 @@ def sample_race(logits, temperature, top_k, top_p, seeds, offsets, exchange, v0,
     done = [False] * B
     tok, lp = [0] * B, [0.0] * B
     cand = [(0, 0.0)] * B
-    pivot = [-math.inf] * B
 
-    def combine_cands(b):
-        best = (-math.inf, 0x7FFFFFFF, -math.inf)
-        for q in range(W):
-            k_, j_, x_ = float(g[q, b, 4]), int(g[q, b, 5]), float(g[q, b, 6])
-            if k_ > best[0] or (k_ == best[0] and j_ < best[1]):
-                best = (k_, j_, x_)
-        return best
+    def finish(b, t, x_):
+        done[b], tok[b], lp[b] = True, t, (x_ - xmax[b]) * inv_t[b] - math.log(S[b])
 
-    def mass_pass():
-        out = torch.zeros(B, 8)
-        for b in range(B):
-            if not done[b]:
-                above = x[b] > cand[b][1]
-                out[b, 0] = float(torch.exp((x[b][above] - xmax[b]) * inv_t[b]).sum())
-                out[b, 1] = float(above.sum())
-        return out
-
-    for b in range(B):                       # phase 1, round 0
-        xmax[b] = max(float(g[q, b, 0]) for q in range(W))
-        S[b] = sum(float(g[q, b, 1]) * math.exp((float(g[q, b, 0]) - xmax[b]) * inv_t[b])
-                   for q in range(W) if float(g[q, b, 0]) != -math.inf)
-        best = (-math.inf, 0x7FFFFFFF)
-        for q in range(W):
-            v, j = float(g[q, b, 2]), int(g[q, b, 3])
-            if v > best[0] or (v == best[0] and j < best[1]):
-                best = (v, j)
-        am[b] = best
-        if greedy[b]:
-            done[b], tok[b], lp[b] = True, best[1], best[0] - xmax[b] - math.log(S[b])
-            continue
-        k_, j_, x_ = combine_cands(b)
-        if k_ == -math.inf:
-            done[b], tok[b] = True, am[b][1]
-            lp[b] = (am[b][0] - xmax[b]) * inv_t[b] - math.log(S[b])
-        elif not trunc[b]:
-            done[b], tok[b], lp[b] = True, j_, (x_ - xmax[b]) * inv_t[b] - math.log(S[b])
-        else:
-            cand[b] = (j_, x_)
-    g = exchange(mass_pass())
-    for rnd in range(1, max_rounds + 1):     # phase 2 (+ phase 1)
+    for rnd in range(max_rounds + 1):        # phase 1 rounds, then phase 2
+        last = rnd == max_rounds
         rec = torch.zeros(B, 8)
         rec[:, 4] = -math.inf
         for b in range(B):
-            if done[b]:
+            if rnd == 0:
+                xmax[b] = max(float(g[q, b, 0]) for q in range(W))
+                S[b] = sum(float(g[q, b, 1]) * math.exp((float(g[q, b, 0]) - xmax[b]) * inv_t[b])
+                           for q in range(W) if float(g[q, b, 0]) != -math.inf)
+                best = (-math.inf, 0x7FFFFFFF)
+                for q in range(W):
+                    v, j = float(g[q, b, 2]), int(g[q, b, 3])
+                    if v > best[0] or (v == best[0] and j < best[1]):
+                        best = (v, j)
+                am[b] = best
+                if greedy[b]:
+                    done[b], tok[b] = True, best[1]
+                    lp[b] = best[0] - xmax[b] - math.log(S[b])
+            elif not done[b]:
+                mass = sum(float(g[q, b, 0]) for q in range(W)) / S[b]
+                cnt = sum(float(g[q, b, 1]) for q in range(W))
+                if mass < tp[b] and (kk[b] <= 0 or cnt < kk[b]):
+                    finish(b, cand[b][0], cand[b][1])
+                elif last:
+                    finish(b, am[b][1], am[b][0])
+            if last or done[b]:
                 continue
-            mass = sum(float(g[q, b, 0]) for q in range(W)) / S[b]
-            cnt = sum(float(g[q, b, 1]) for q in range(W))
-            if mass < tp[b] and (kk[b] <= 0 or cnt < kk[b]):
-                done[b], tok[b] = True, cand[b][0]
-                lp[b] = (cand[b][1] - xmax[b]) * inv_t[b] - math.log(S[b])
-            elif rnd >= max_rounds:
-                done[b], tok[b] = True, am[b][1]
-                lp[b] = (am[b][0] - xmax[b]) * inv_t[b] - math.log(S[b])
-            else:
-                pivot[b] = cand[b][1]
-                k_, j_, x_ = race(b, rnd, pivot[b])
+            best = NONE
+            for q in range(W):
+                k_, j_, x_ = float(g[q, b, 4]), int(g[q, b, 5]), float(g[q, b, 6])
+                if k_ > best[0] or (k_ == best[0] and j_ < best[1]):
+                    best = (k_, j_, x_)
+            if best[0] == -math.inf:
+                finish(b, am[b][1], am[b][0])
+                continue
+            if not trunc[b]:
+                finish(b, best[1], best[2])
+                continue
+            cand[b] = (best[1], best[2])
+            above = x[b] > best[2]
+            rec[b, 0] = float(torch.exp((x[b][above] - xmax[b]) * inv_t[b]).sum())
+            rec[b, 1] = float(above.sum())
+            if rnd + 1 < max_rounds:
+                k_, j_, x_ = race(b, rnd + 1, best[2])
                 rec[b, 4], rec[b, 5], rec[b, 6] = k_, float(j_), x_
-        if rnd >= max_rounds:
-            break
-        g = exchange(rec)
-        for b in range(B):
-            if done[b]:
-                continue
-            k_, j_, x_ = combine_cands(b)
-            if k_ == -math.inf:
-                done[b], tok[b] = True, am[b][1]
-                lp[b] = (am[b][0] - xmax[b]) * inv_t[b] - math.log(S[b])
-            else:
-                cand[b] = (j_, x_)
-        g = exchange(mass_pass())
+        if not last:
+            g = exchange(rec)
     return torch.tensor(tok, dtype=torch.int32), torch.tensor(lp, dtype=torch.float32)
 
 
