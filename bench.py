@@ -425,7 +425,8 @@ def main() -> None:
                                   "kv_pages": "K [BS][D] token-major, V [BS/4][D][4] key-quad",
                                   "max_batched_tokens": ecfg.max_batched_tokens,
                                   "mixed_prefill_tokens": ecfg.mixed_prefill_tokens,
-                                  "mixed_min_decodes": engine.ecfg.mixed_min_decodes},
+                                  "mixed_min_decodes": engine.ecfg.mixed_min_decodes,
+                                  "mixed_later_steps": engine.ecfg.mixed_later_steps},
                        "tp_group": None if a.tp == 1 else {
                            "collectives": "gloo (one-GPU rehearsal)" if (a.rehearse_on_one_gpu or a.cpu)
                            else "nccl (RCCL)",
@@ -549,6 +550,7 @@ def closed(a, rank, world, n_eng, lgs, barrier, sync, ecfg, engine=None) -> None
                           "prompt_len": a.prompt_len, "max_tokens": a.max_tokens,
                           "max_batched_tokens": ecfg.max_batched_tokens,
                           "mixed_prefill_tokens": ecfg.mixed_prefill_tokens,
+                          "mixed_later_steps": ecfg.mixed_later_steps,
                           "load": f"{load}, {a.closed_warmup:g} s warm-up, "
                                   f"{a.duration:g} s window",
                           "sampling": {"temperature": a.temperature, "top_p": a.top_p}}}

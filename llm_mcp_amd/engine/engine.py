@@ -98,25 +98,27 @@ class EngineConfig:
     (environment-overridable, settings.py): a step takes up to
     max_batched_tokens tokens -- an idle engine takes a whole burst of
     prompts in few steps -- but a step that also carries at least
-    mixed_min_decodes decode rows takes at most mixed_prefill_tokens prompt
-    tokens (when set), so a long prefill chunk cannot stall the running
-    streams for the length of a 24k-token step.  Off by default: measured on
-    one box it costs 1.6 % (16384) / 4.6 % (8192) of the headline waves'
-    throughput for a 1.6-2.2x lower worst token gap (profiles/r5_serving.md);
-    latency-first deployments set LMX_MIXED_PREFILL_TOKENS=8192."""
+    mixed_min_decodes decode rows of streams that were running before the
+    newest request with prompt tokens left arrived (>= mixed_later_steps
+    scheduler steps earlier) takes at most mixed_prefill_tokens prompt
+    tokens.  One burst's rows never cap each other, so a wave of requests is
+    prefilled at the full budget, while in steady serving a new request's
+    prefill is chunked so it cannot stall the running streams for a
+    24k-token step (closed loop at 256 streams: per-token gap p99 251 -> 35
+    ms, TTFT p50 756 -> 101 ms; profiles/r6_serving.md)."""
     model: str = "llama-3-8b"
     max_num_seqs: int = 256
     max_batched_tokens: int = field(
         default_factory=lambda: _env_int("LMX_MAX_BATCHED_TOKENS", 24576))
     mixed_prefill_tokens: int = field(
-        default_factory=lambda: _env_int("LMX_MIXED_PREFILL_TOKENS", 0))
+        default_factory=lambda: _env_int("LMX_MIXED_PREFILL_TOKENS", 2048))
     mixed_min_decodes: int = field(
         default_factory=lambda: _env_int("LMX_MIXED_MIN_DECODES", 32))
     # the cap counts only decode rows whose request came >= this many
     # scheduler steps before the newest request with prompt tokens left
     # (0: every decode row): one burst's rows never cap each other
     mixed_later_steps: int = field(
-        default_factory=lambda: _env_int("LMX_MIXED_LATER_STEPS", 2))
+        default_factory=lambda: _env_int("LMX_MIXED_LATER_STEPS", 8))
     max_model_len: int = 8192
     kv_fraction: float = 0.6        # of free HBM after weights
     kv_cache_gb: float | None = None

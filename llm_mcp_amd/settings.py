@@ -80,10 +80,10 @@ VARS: list[Var] = [
         "(overrides LMX_CHAT_MODEL / LMX_TP for `serve`)"),
     Var("LMX_MAX_BATCH", int, 256, "max concurrent sequences per engine"),
     Var("LMX_MAX_BATCHED_TOKENS", int, 24576, "tokens per engine step (an idle engine takes a burst of prompts in steps this large); bench.py and serve share it"),
-    Var("LMX_MIXED_PREFILL_TOKENS", int, 0, "prompt tokens per step while >= LMX_MIXED_MIN_DECODES decode rows run (bounds the stall a prefill chunk puts on every decoding stream; 8192 halves the closed-loop TTFT and worst token gap for ~3-5 % throughput); 0 = no cap (default)"),
+    Var("LMX_MIXED_PREFILL_TOKENS", int, 2048, "prompt tokens per step while >= LMX_MIXED_MIN_DECODES decode rows of earlier-arrived streams run (bounds the stall a new request's prefill puts on every decoding stream; burst-aware, see LMX_MIXED_LATER_STEPS); 0 = no cap"),
     Var("LMX_PREFIX_CACHE", int, 1, "1: full KV pages are hashed and kept (LRU) for reuse by later prompts with the same prefix; 0: pages return to the free list when their sequence ends"),
     Var("LMX_MIXED_MIN_DECODES", int, 32, "decode rows that make a step 'mixed' for LMX_MIXED_PREFILL_TOKENS"),
-    Var("LMX_MIXED_LATER_STEPS", int, 2, "LMX_MIXED_PREFILL_TOKENS counts only decode rows whose request came >= this many scheduler steps before the newest request with prompt tokens left (streams interrupted by later arrivals); 0 = every decode row"),
+    Var("LMX_MIXED_LATER_STEPS", int, 8, "LMX_MIXED_PREFILL_TOKENS counts only decode rows whose request came >= this many scheduler steps before the newest request with prompt tokens left (streams interrupted by later arrivals); 0 = every decode row"),
     Var("LMX_AR_SPIN", int, 1 << 25, "peer all-reduce: polls (s_sleep 1 each) a kernel waits for a TP peer before it gives up and sets the error word (the engine then fails the step)"),
     Var("LMX_ALLOW_CLOUD", int, 0, "1: allow cloud providers (never on the GPU hot path)"),
     Var("LMX_JOB_RETENTION_DAYS", float, 7.0, "purge finished jobs older than this"),

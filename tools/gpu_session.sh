@@ -425,6 +425,31 @@ for step in "$@"; do
       run embed_http 600 python -u -m llm_mcp_amd.bench.serving_bench embed --requests 1024 || exit $? ;;
     rope_probe)
       run rope_probe 120 python -u tools/rope_probe.py || exit $? ;;
+    config5a)
+      # config 5 steady state: the same mixed load with NO fault, 3 fresh runs (the spread
+      # is the run-to-run noise of the capacity itself)
+      run config5a 1100 python -u -m llm_mcp_amd.bench.serving_bench mixed --gpus 0 \
+          --replicas-per-gpu 2 --runs 3 --jobs 4096 --concurrency 256 --sync-every 4 \
+          --max-tokens 64 --chars 512 || exit $? ;;
+    config5rec)
+      # config 5 fault recovery: the faulty worker fails once at its 300th engine step;
+      # the bench records the fault -> breaker -> restart -> first-job timeline
+      run config5rec 900 python -u -m llm_mcp_amd.bench.serving_bench mixed --gpus 0 \
+          --replicas-per-gpu 2 --fault gpu_error@300 --fault-device gpu0.r1 --fault-lives 1 \
+          --jobs 4096 --concurrency 256 --sync-every 4 --max-tokens 64 --chars 512 \
+          --await-recovery 150 || exit $? ;;
+    embed_batch)
+      # the nomic engine at 32k / 64k tokens per batch
+      : > gpurun_out/embed_batch.log
+      for bt in 32768 65536; do
+        timeout -k 10 200 python -u -m llm_mcp_amd.bench.embed_engine_bench --batch-tokens $bt \
+            >> gpurun_out/embed_batch.log 2>&1 || exit $?
+      done
+      grep emb_per_s gpurun_out/embed_batch.log ;;
+    race_tests)
+      run race_tests 400 python -u -m pytest tests/test_00_peer_ar_gpu.py tests/test_kernels_gpu.py \
+          -k "race or sharded or sample" -x -v --timeout 300 --timeout-method thread \
+          -p no:cacheprovider || exit $? ;;
     prof_embed)
       # nomic engine at 1k-token docs under a kernel trace: the kernel-class split
       rm -rf gpurun_out/prof_embed
