@@ -15,12 +15,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--docs", type=int, default=512)
     ap.add_argument("--doc-len", type=int, default=1024)
-    ap.add_argument("--batch-tokens", type=int, default=32768)
+    ap.add_argument("--batch-tokens", type=int, default=None,
+                    help="tokens per forward (default: the engine's, LMX_EMBED_BATCH_TOKENS)")
     ap.add_argument("--model", default="nomic-embed-text")
     a = ap.parse_args()
     cfg = mc.resolve(a.model)
     a.doc_len = min(a.doc_len, cfg.max_position)
     e = EmbeddingEngine(cfg, device="cuda", max_batch_tokens=a.batch_tokens)
+    a.batch_tokens = e.max_batch_tokens
     g = torch.Generator().manual_seed(0)
     docs = [torch.randint(1000, 30000, (a.doc_len,), generator=g).tolist()
             for _ in range(a.docs)]

@@ -74,6 +74,7 @@ VARS: list[Var] = [
     Var("LMX_GPUS", str, "", "GPUs served by `serve` (e.g. 0-7); default all enumerated"),
     Var("LMX_CHAT_MODEL", str, "llama-3-8b", "chat model preset / alias"),
     Var("LMX_EMBED_MODEL", str, "", "embedding model preset (e.g. nomic-embed-text)"),
+    Var("LMX_EMBED_BATCH_TOKENS", int, 65536, "tokens per embedding-engine forward (whole requests packed up to this many tokens)"),
     Var("LMX_TP", int, 1, "tensor-parallel degree of a chat-model group"),
     Var("LMX_WEIGHTS", str, "", "safetensors dir of the chat model's real weights (`serve`)"),
     Var("LMX_MODEL_REGISTRY", str, "", "per-GPU placement 'GPUS:[tpN:|embed:]MODEL;...' "

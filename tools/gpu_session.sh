@@ -438,6 +438,15 @@ for step in "$@"; do
           --replicas-per-gpu 2 --fault gpu_error@300 --fault-device gpu0.r1 --fault-lives 1 \
           --jobs 4096 --concurrency 256 --sync-every 4 --max-tokens 64 --chars 512 \
           --await-recovery 150 || exit $? ;;
+    budget_ab)
+      # the wave's prefill step budget: 24576 vs BUDGETS (median request done after
+      # 2 full steps from ~33.1k), same box, alternating
+      for i in 1 2; do
+        for b in 24576 ${BUDGETS:-33280 36864}; do
+          run budget_${b}_$i 400 python bench.py --steps 4 --warmup 1 --max-batched-tokens $b \
+              || exit $?
+        done
+      done ;;
     embed_batch)
       # the nomic engine at 32k / 64k tokens per batch
       : > gpurun_out/embed_batch.log
