@@ -431,6 +431,24 @@ for step in "$@"; do
       run config5a 1100 python -u -m llm_mcp_amd.bench.serving_bench mixed --gpus 0 \
           --replicas-per-gpu 2 --runs 3 --jobs 4096 --concurrency 256 --sync-every 4 \
           --max-tokens 64 --chars 512 || exit $? ;;
+    c5ab)
+      # config 5 steady state, shipped default vs no mixed-step cap, 2048 jobs each, alternating
+      for i in 1 2; do
+        run c5ab_default_$i 400 python -u -m llm_mcp_amd.bench.serving_bench mixed --gpus 0 \
+            --replicas-per-gpu 2 --jobs 2048 --concurrency 256 --sync-every 4 --max-tokens 64 \
+            --chars 512 || exit $?
+        LMX_MIXED_PREFILL_TOKENS=0 run c5ab_nocap_$i 400 python -u -m llm_mcp_amd.bench.serving_bench \
+            mixed --gpus 0 --replicas-per-gpu 2 --jobs 2048 --concurrency 256 --sync-every 4 \
+            --max-tokens 64 --chars 512 || exit $?
+      done ;;
+    prof_c5)
+      # config 5 steady state under a kernel trace: GPU busy vs wall per process
+      rm -rf gpurun_out/prof_c5
+      run prof_c5 600 rocprofv3 --kernel-trace -d gpurun_out/prof_c5 -o %pid% -- python3 -u -m \
+          llm_mcp_amd.bench.serving_bench mixed --gpus 0 --replicas-per-gpu 2 --jobs 2048 \
+          --concurrency 256 --sync-every 4 --max-tokens 64 --chars 512 || exit $?
+      python tools/prof_busy.py gpurun_out/prof_c5 > gpurun_out/prof_c5_busy.md 2>&1 || true
+      find gpurun_out/prof_c5 -name "*.db" -delete 2>/dev/null || true ;;
     config5rec)
       # config 5 fault recovery: the faulty worker fails once at its 300th engine step;
       # the bench records the fault -> breaker -> restart -> first-job timeline
