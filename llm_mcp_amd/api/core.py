@@ -9,6 +9,9 @@ planner), gRPC server, graceful shutdown of HTTP *and* gRPC.
 from __future__ import annotations
 
 import asyncio
+import atexit
+import threading
+import weakref
 import logging
 import os
 import time
@@ -48,6 +51,74 @@ def open_store(spec: str | None = None):
                        snapshot_path=os.environ.get("LMX_SNAPSHOT", ""))
 
 
+class JobChangeHub:
+    """One thread blocks in the store's change wait (native condition
+    variable, or Postgres LISTEN) and wakes every asyncio waiter of the loop
+    through one shared future.  A job SSE stream, a gRPC StreamJob or a
+    claim long-poll awaiting a change then costs no thread: with one
+    ``to_thread`` per waiter, 256 streams contended for the 32-thread default
+    executor and every store change cycled all of them through it -- the
+    config-5 core spent its CPU handing threads around (profiles/r6_config5.md)."""
+
+    def __init__(self, store, loop: asyncio.AbstractEventLoop):
+        self.store, self.loop = store, loop
+        self.ver = store.job_version()
+        self._fut = loop.create_future()
+        self._stop = threading.Event()
+        self._thread = threading.Thread(target=self._run, name="lmx-job-hub", daemon=True)
+        self._thread.start()
+        _HUBS.add(self)
+
+    def _run(self):
+        v = self.ver
+        while not self._stop.is_set():
+            try:
+                v2 = self.store.wait_job_change(v, 0.25)
+            except Exception:          # a store hiccup: retry after a pause
+                self._stop.wait(0.5)
+                continue
+            if v2 != v:
+                v = v2
+                try:
+                    self.loop.call_soon_threadsafe(self._notify, v2)
+                except RuntimeError:    # the loop closed
+                    return
+
+    def _notify(self, v):
+        self.ver = v
+        fut, self._fut = self._fut, self.loop.create_future()
+        if not fut.done():
+            fut.set_result(v)
+
+    async def wait(self, since, timeout_s: float):
+        """The version after ``since`` changed, or the current one after
+        ``timeout_s`` (the wait_job_change contract, without a thread)."""
+        if self.ver != since:
+            return self.ver
+        try:
+            await asyncio.wait_for(asyncio.shield(self._fut), timeout_s)
+        except asyncio.TimeoutError:
+            pass
+        return self.ver
+
+    def close(self):
+        self._stop.set()
+        _HUBS.discard(self)
+        if self._thread is not threading.current_thread():
+            self._thread.join(timeout=2.0)
+
+
+# Hubs still open at interpreter exit are stopped first: a daemon thread left
+# inside the native wait while the interpreter finalises aborts the process.
+_HUBS: "weakref.WeakSet[JobChangeHub]" = weakref.WeakSet()
+
+
+@atexit.register
+def _close_hubs():
+    for h in list(_HUBS):
+        h.close()
+
+
 class CoreState:
     def __init__(self, store=None, registry: ModelRegistry | None = None,
                  metrics: Metrics | None = None, circuit: CircuitBreaker | None = None,
@@ -67,6 +138,16 @@ class CoreState:
         self.cloud_embed = None
         self.cloud_chat = None
         self._tasks: list[asyncio.Task] = []
+        self._hub: JobChangeHub | None = None
+
+    def job_hub(self) -> JobChangeHub:
+        """The change hub of the running loop (created on first use)."""
+        loop = asyncio.get_running_loop()
+        if self._hub is None or self._hub.loop is not loop:
+            if self._hub is not None:
+                self._hub.close()
+            self._hub = JobChangeHub(self.store, loop)
+        return self._hub
 
     def _capacity_of(self, device_id: str):
         caps = [m.capacity for m in self.registry.all() if m.device_id == device_id]
@@ -181,6 +262,9 @@ class CoreState:
         for t in self._tasks:
             t.cancel()
         self._tasks.clear()
+        if self._hub is not None:
+            self._hub.close()
+            self._hub = None
 
 
 def create_core_app(state: CoreState, background: bool = True) -> web.Application:

@@ -202,6 +202,9 @@ PYBIND11_MODULE(_lmx_runtime, m) {
       .def("expire_deadlines", &JobQueue::expire_deadlines)
       .def("purge_finished", &JobQueue::purge_finished)
       .def("counts", &JobQueue::counts)
+      .def("kind_counts", &JobQueue::kind_counts)
+      .def("active_on", &JobQueue::active_on, py::call_guard<py::gil_scoped_release>())
+      .def("device_stats", &JobQueue::device_stats)
       .def("stuck", &JobQueue::stuck)
       .def("list", [](const JobQueue& q, const std::string& status, int limit) {
         py::list l;

@@ -1,5 +1,8 @@
 #include "job_queue.h"
 
+#include <cctype>
+#include <cstdlib>
+
 #include <algorithm>
 #include <chrono>
 #include <random>
@@ -95,6 +98,8 @@ void JobQueue::index_insert(const JobRow& j) {
   if (j.status == "queued" || j.status == "running")
     claimable_.insert(ReadyKey(-j.priority, j.queued_at, j.seq, j.id));
   if (j.status == "running" && !j.device_id.empty()) running_per_device_[j.device_id].insert(j.id);
+  if ((j.status == "queued" || j.status == "running") && !j.device_id.empty())
+    ++active_per_device_[j.device_id];
 }
 
 void JobQueue::index_erase(const JobRow& j) {
@@ -105,6 +110,10 @@ void JobQueue::index_erase(const JobRow& j) {
       it->second.erase(j.id);
       if (it->second.empty()) running_per_device_.erase(it);
     }
+  }
+  if ((j.status == "queued" || j.status == "running") && !j.device_id.empty()) {
+    auto it = active_per_device_.find(j.device_id);
+    if (it != active_per_device_.end() && --it->second <= 0) active_per_device_.erase(it);
   }
 }
 
@@ -470,6 +479,54 @@ std::map<std::string, int> JobQueue::counts() const {
   std::map<std::string, int> c{{"queued", 0}, {"running", 0}, {"done", 0}, {"error", 0}};
   for (auto& kv : jobs_) c[kv.second.status]++;
   return c;
+}
+
+std::map<std::string, int> JobQueue::kind_counts(const std::string& prefix) const {
+  std::lock_guard<std::mutex> g(mu_);
+  std::map<std::string, int> c;
+  for (auto& kv : jobs_)
+    if (kv.second.kind.compare(0, prefix.size(), prefix) == 0) c[kv.second.status]++;
+  return c;
+}
+
+int JobQueue::active_on(const std::string& device) const {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = active_per_device_.find(device);
+  return it == active_per_device_.end() ? 0 : it->second;
+}
+
+// the number after "ms": in a metrics JSON object (-1: absent / not a number)
+static double metrics_ms(const std::string& m) {
+  const size_t k = m.find("\"ms\"");
+  if (k == std::string::npos) return -1;
+  size_t i = k + 4;
+  while (i < m.size() && (m[i] == ' ' || m[i] == ':')) ++i;
+  if (i >= m.size() || !(std::isdigit((unsigned char)m[i]) || m[i] == '-' || m[i] == '.'))
+    return -1;
+  return std::strtod(m.c_str() + i, nullptr);
+}
+
+std::map<std::string, int64_t> JobQueue::device_stats(const std::string& device,
+                                                      int64_t since) const {
+  std::lock_guard<std::mutex> g(mu_);
+  int64_t total = 0, done = 0, ms_n = 0;
+  double ms_sum = 0;
+  for (auto& kv : jobs_) {
+    const JobRow& j = kv.second;
+    if (j.device_id != device || j.updated_at < since) continue;
+    if (j.status != "done" && j.status != "error") continue;
+    ++total;
+    if (j.status != "done") continue;
+    ++done;
+    auto it = attempts_.find(j.id);
+    if (it == attempts_.end()) continue;
+    for (auto& a : it->second)
+      if (a.status == "done") {
+        const double ms = metrics_ms(a.metrics);
+        if (ms >= 0) { ms_sum += ms; ++ms_n; }
+      }
+  }
+  return {{"total", total}, {"done", done}, {"ms_sum", (int64_t)ms_sum}, {"ms_n", ms_n}};
 }
 
 int JobQueue::stuck(int64_t now) const {

@@ -87,6 +87,15 @@ class JobQueue {
   int purge_finished(int64_t older_than);  // retention cleanup (planner)
 
   std::map<std::string, int> counts() const;
+  // jobs per status whose kind starts with ``prefix`` (dashboard benchmark
+  // counts without converting every row)
+  std::map<std::string, int> kind_counts(const std::string& prefix) const;
+  // queued + running rows whose device is ``device`` (O(1), indexed)
+  int active_on(const std::string& device) const;
+  // v_device_stats from the rows: finished jobs of ``device`` updated at or
+  // after ``since`` -> {total, done, ms_sum, ms_n} (ms from the done
+  // attempts' metrics)
+  std::map<std::string, int64_t> device_stats(const std::string& device, int64_t since) const;
   int stuck(int64_t now) const;  // running with expired lease
   std::vector<JobRow> list(const std::string& status, int limit) const;
   std::vector<AttemptRow> attempts(const std::string& job_id) const;
@@ -114,6 +123,8 @@ class JobQueue {
   std::set<ReadyKey> claimable_;  // queued + running (lease may expire)
   std::unordered_map<std::string, std::vector<AttemptRow>> attempts_;
   std::unordered_map<std::string, std::unordered_set<std::string>> running_per_device_;
+  // queued + running rows placed on each device (the router's load signal)
+  std::unordered_map<std::string, int> active_per_device_;
   int live_running(const std::string& dev, int64_t now, const std::string& except) const;
   std::string path_;
   FILE* jf_ = nullptr;

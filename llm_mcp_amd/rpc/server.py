@@ -106,7 +106,7 @@ class CoreService:
                                                         "error": j.get("error")}))
             if j["status"] in ("done", "error"):
                 return
-            ver = await asyncio.to_thread(self.store.wait_job_change, ver, 15.0)
+            ver = await self.st.job_hub().wait(ver, 15.0)
             j = await self._db(self.store.get_job, req.job_id)
             if j is None:
                 return

@@ -203,12 +203,7 @@ class MemoryStore:
                  "finished_at": _s(a["finished_at"])} for a in self.q.attempts(job_id)]
 
     def active_jobs_on(self, device_id):
-        n = 0
-        for st in ("running", "queued"):
-            for r in self.q.list(st, 0):
-                if r["device_id"] == device_id:
-                    n += 1
-        return n
+        return self.q.active_on(device_id or "")
 
     def job_version(self):
         return self.q.version
@@ -456,21 +451,14 @@ class MemoryStore:
             return out
 
     def device_stats_7d(self, device_id):
-        """v_device_stats (04_smart_routing.sql:71-94) from job attempts."""
-        since = _ms(self.clock() - 7 * 86400)
-        total = done = 0
-        ms = []
-        for st in ("done", "error"):
-            for r in self.q.list(st, 0):
-                if r["device_id"] != device_id or r["updated_at"] < since:
-                    continue
-                total += 1
-                if st == "done":
-                    done += 1
-                    for a in self.q.attempts(r["id"]):
-                        m = _loads(a["metrics"], {})
-                        if a["status"] == "done" and isinstance(m.get("ms"), (int, float)):
-                            ms.append(m["ms"])
+        """v_device_stats (04_smart_routing.sql:71-94) from job attempts, counted
+        in the native queue (the dashboard asks per device on every poll)."""
+        s = self.q.device_stats(device_id, _ms(self.clock() - 7 * 86400))
+        total, done = s["total"], s["done"]
         return {"total_jobs_7d": total, "done_jobs_7d": done,
                 "success_rate": (done / total) if total else 0.0,
-                "avg_latency_ms": int(sum(ms) / len(ms)) if ms else 0}
+                "avg_latency_ms": int(s["ms_sum"] / s["ms_n"]) if s["ms_n"] else 0}
+
+    def kind_counts(self, prefix):
+        """{status: jobs} of the jobs whose kind starts with ``prefix``."""
+        return dict(self.q.kind_counts(prefix))

@@ -273,6 +273,12 @@ class PostgresStore:
             out[r["status"]] = r["n"]
         return out
 
+    def kind_counts(self, prefix):
+        """{status: jobs} of the jobs whose kind starts with ``prefix``."""
+        return {r["status"]: r["n"] for r in self._q(
+            "SELECT status, COUNT(*)::int AS n FROM jobs WHERE starts_with(kind, $1) "
+            "GROUP BY status", prefix)}
+
     def running_jobs(self, limit=10):
         return self.list_jobs("running", limit)
 

@@ -320,3 +320,87 @@ def test_maintenance_exports_live_allreduce_samples():
     lm.tags["live"] = {"tp_comm_live": {"seq": 2, "us": {"rccl": 33.0}}}
     st._maintenance()
     assert count("rccl") == 3
+
+
+def test_dashboard_counts_are_native_and_match_rows():
+    """The dashboard's benchmark counts and per-device 7-day stats come from
+    the native queue (no per-row conversion on every poll) and agree with a
+    count over the rows."""
+    from llm_mcp_amd.store.memory import MemoryStore
+    st = MemoryStore()
+    ids = [st.submit_job("benchmark.ollama.generate", {"model": "m"}) for _ in range(3)]
+    ids += [st.submit_job("engine.generate", {"model": "m"}) for _ in range(2)]
+    done = 0
+    for _ in range(5):
+        j = st.claim_job("w1", [], 30, worker_device="dev-a", check_online=False)
+        if j is None:
+            break
+        if done < 3:
+            st.complete_job(j["id"], "w1", {"ok": True}, {"ms": 100 + 10 * done},
+                            j["attempt_id"])
+        else:
+            st.fail_job(j["id"], "w1", "boom", {"ms": 5}, j["attempt_id"])
+        done += 1
+    kc = st.kind_counts("benchmark.")
+    rows = {}
+    for s_ in ("queued", "running", "done", "error"):
+        for r in st.list_jobs(s_, 0):
+            if r["kind"].startswith("benchmark."):
+                rows[s_] = rows.get(s_, 0) + 1
+    assert {k: v for k, v in kc.items() if v} == rows
+    stats = st.device_stats_7d("dev-a")
+    # the two failed attempts were requeued (attempts < max_attempts): only
+    # finished jobs count
+    assert done == 5 and stats["total_jobs_7d"] == 3 and stats["done_jobs_7d"] == 3
+    assert stats["avg_latency_ms"] == 110      # mean of 100, 110, 120
+
+
+def test_job_change_hub_wakes_many_waiters_without_threads():
+    """Hundreds of job streams / claim long-polls wait on one hub thread:
+    one store change wakes all of them, and none holds an executor thread
+    while it waits (routes.job_stream, routes._claim, rpc StreamJob)."""
+    import threading
+    from llm_mcp_amd.api.core import JobChangeHub
+
+    async def go():
+        st = CoreState(store=MemoryStore())
+        hub = st.job_hub()
+        assert st.job_hub() is hub
+        v0 = hub.ver
+        threads0 = threading.active_count()
+        waiters = [asyncio.ensure_future(hub.wait(v0, 10.0)) for _ in range(300)]
+        await asyncio.sleep(0.05)
+        assert not any(w.done() for w in waiters)
+        assert threading.active_count() == threads0      # no thread per waiter
+        t = time.monotonic()
+        await asyncio.to_thread(st.store.submit_job, "llm_generate", {"prompt": "x"})
+        got = await asyncio.gather(*waiters)
+        assert time.monotonic() - t < 2.0
+        assert all(g != v0 for g in got) and len(set(got)) >= 1
+        # a stale version returns at once; an unchanged one times out
+        assert await hub.wait(v0, 5.0) == hub.ver
+        t = time.monotonic()
+        assert await hub.wait(hub.ver, 0.2) == hub.ver
+        assert 0.15 < time.monotonic() - t < 1.5
+        await st.stop_background()
+        assert st._hub is None and not hub._thread.is_alive()
+        assert isinstance(hub, JobChangeHub)
+    run(go())
+
+
+def test_active_jobs_on_is_indexed_and_tracks_transitions():
+    """The router's per-device load (queued + running rows placed on a
+    device) comes from an index kept by the native queue, not a row scan."""
+    s = MemoryStore()
+    s.upsert_device("gpu0", status="online")
+    ids = [s.submit_job("llm_generate", {"device_id": "gpu0"}) for _ in range(3)]
+    s.submit_job("llm_generate", {"device_id": "gpu1"})
+    s.submit_job("llm_generate", {})
+    assert s.active_jobs_on("gpu0") == 3 and s.active_jobs_on("gpu1") == 1
+    j = s.claim_job("w", ["llm_generate"], 30, worker_device="gpu0", device_max_concurrency=0)
+    assert j is not None and s.active_jobs_on("gpu0") == 3     # queued -> running
+    assert s.complete_job(j["id"], "w", {}, {}, token=j.get("lease_token", ""))
+    assert s.active_jobs_on("gpu0") == 2
+    brute = sum(1 for st_ in ("queued", "running") for r in s.list_jobs(st_, 0)
+                if r.get("device_id") == "gpu0")
+    assert brute == s.active_jobs_on("gpu0") and ids

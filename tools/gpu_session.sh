@@ -472,6 +472,9 @@ for step in "$@"; do
         timeout -k 10 200 python -u -m llm_mcp_amd.bench.embed_engine_bench --batch-tokens $bt \
             >> gpurun_out/embed_batch.log 2>&1 || exit $?
       done
+      # q rotated inside the attention kernel (the rope/cache kernel skips q's write-back)
+      LMX_FUSED_ENCODER_ROPE=1 timeout -k 10 200 python -u -m llm_mcp_amd.bench.embed_engine_bench \
+          --batch-tokens 65536 >> gpurun_out/embed_batch.log 2>&1 || exit $?
       grep emb_per_s gpurun_out/embed_batch.log ;;
     race_tests)
       run race_tests 400 python -u -m pytest tests/test_00_peer_ar_gpu.py tests/test_kernels_gpu.py \
