@@ -242,7 +242,9 @@ class Supervisor:
     def __len__(self):
         return len(self.entries)
 
-    def stop(self, timeout: float = 20) -> None:
+    def stop(self, timeout: float | None = None) -> None:
+        if timeout is None:
+            timeout = float(os.environ.get("LMX_STOP_GRACE_S", "20"))
         for e in self.entries:
             e["restart_at"] = None
         live = [e["proc"] for e in self.entries if e["proc"] is not None]

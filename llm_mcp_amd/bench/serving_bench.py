@@ -26,6 +26,7 @@ import json
 import os
 import random
 import socket
+import signal
 import subprocess
 import sys
 import threading
@@ -395,11 +396,31 @@ def bench_mixed(a) -> dict:
             out["device_status_after_recovery"] = {k: sorted(v) for k, v in status_seen.items()}
         return out
     finally:
-        core.terminate()
+        _stop_group(core)
+
+
+def _stop_group(core: subprocess.Popen, grace_s: float = 60.0) -> None:
+    """Stop the core and its worker processes.  The core stops its workers
+    itself (SIGTERM, then a wait); if it has not exited after ``grace_s`` the
+    whole process group it leads (``start_new_session``) gets SIGTERM -- each
+    worker then still exits through its own handler, so a profiler attached
+    to it writes its trace -- and SIGKILL only after a second grace."""
+    core.terminate()
+    try:
+        core.wait(timeout=grace_s)
+        return
+    except subprocess.TimeoutExpired:
+        pass
+    for sig, wait in ((signal.SIGTERM, 30.0), (signal.SIGKILL, 10.0)):
         try:
-            core.wait(timeout=60)
+            os.killpg(core.pid, sig)
+        except ProcessLookupError:
+            return
+        try:
+            core.wait(timeout=wait)
+            return
         except subprocess.TimeoutExpired:
-            core.kill()
+            pass
 
 
 def _recovery(timeline, done_at, t0, fault_device: str) -> dict:

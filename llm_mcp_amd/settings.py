@@ -107,6 +107,7 @@ VARS: list[Var] = [
     Var("LMX_ENGINE_INFO_S", float, 5.0, "API process: cadence of live engine info polls (KV usage, running, waiting)"),
     Var("LMX_RESTART_BACKOFF_S", float, 1.0, "serve: first restart delay of a dead GPU worker (doubles per consecutive death)"),
     Var("LMX_RESTART_MAX_S", float, 60.0, "serve: cap of the worker restart backoff"),
+    Var("LMX_STOP_GRACE_S", float, 20.0, "serve: seconds a worker gets to exit after SIGTERM at shutdown before SIGKILL"),
     Var("LMX_SOCKET_DIR", str, "", "serve: directory of the engine sockets (default /tmp)"),
     Var("LMX_DGEMM", str, "1", "0 disables the decode GEMM (K11) dispatch table (hipBLASLt everywhere)"),
     Var("LMX_PREFILL_WAVES", int, 4, "waves per prefill-attention workgroup at head dim 128 (4 or 8)"),
