@@ -80,7 +80,7 @@ VARS: list[Var] = [
     Var("LMX_MODEL_REGISTRY", str, "", "per-GPU placement 'GPUS:[tpN:|embed:]MODEL;...' "
         "(overrides LMX_CHAT_MODEL / LMX_TP for `serve`)"),
     Var("LMX_MAX_BATCH", int, 256, "max concurrent sequences per engine"),
-    Var("LMX_MAX_BATCHED_TOKENS", int, 24576, "tokens per engine step (an idle engine takes a burst of prompts in steps this large); bench.py and serve share it"),
+    Var("LMX_MAX_BATCHED_TOKENS", int, 36864, "tokens per engine step (an idle engine takes a burst of prompts in steps this large); bench.py and serve share it"),
     Var("LMX_MIXED_PREFILL_TOKENS", int, 2048, "prompt tokens per step while >= LMX_MIXED_MIN_DECODES decode rows of earlier-arrived streams run (bounds the stall a new request's prefill puts on every decoding stream; burst-aware, see LMX_MIXED_LATER_STEPS); 0 = no cap"),
     Var("LMX_PREFIX_CACHE", int, 1, "1: full KV pages are hashed and kept (LRU) for reuse by later prompts with the same prefix; 0: pages return to the free list when their sequence ends"),
     Var("LMX_MIXED_MIN_DECODES", int, 32, "decode rows that make a step 'mixed' for LMX_MIXED_PREFILL_TOKENS"),

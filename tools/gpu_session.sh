@@ -447,7 +447,12 @@ for step in "$@"; do
       LMX_STOP_GRACE_S=90 run prof_c5 600 rocprofv3 --kernel-trace -d gpurun_out/prof_c5 -o %pid% -- python3 -u -m \
           llm_mcp_amd.bench.serving_bench mixed --gpus 0 --replicas-per-gpu 2 --jobs 2048 \
           --concurrency 256 --sync-every 4 --max-tokens 64 --chars 512 || exit $?
-      find gpurun_out/prof_c5 -name "*.db" -printf "%s %p\n" || true
+      # the worker processes finish writing their databases after the bench returns
+      for i in $(seq 60); do
+        ls gpurun_out/prof_c5/*.db-journal > /dev/null 2>&1 || break
+        sleep 2
+      done
+      find gpurun_out/prof_c5 -name "*.db*" -printf "%s %p\n" || true
       python tools/prof_busy.py gpurun_out/prof_c5 > gpurun_out/prof_c5_busy.md 2>&1 || true
       find gpurun_out/prof_c5 -name "*.db" -delete 2>/dev/null || true ;;
     config5rec)
