@@ -482,6 +482,18 @@ for step in "$@"; do
       LMX_FUSED_ENCODER_ROPE=1 timeout -k 10 200 python -u -m llm_mcp_amd.bench.embed_engine_bench \
           --batch-tokens 65536 >> gpurun_out/embed_batch.log 2>&1 || exit $?
       grep emb_per_s gpurun_out/embed_batch.log ;;
+    embed_rope_ab)
+      # nomic at 64k tokens per batch: q rotated in the rope/cache kernel vs inside attention,
+      # alternating, 3 pairs
+      : > gpurun_out/embed_rope_ab.log
+      for i in 1 2 3; do
+        for f in 0 1; do
+          echo "fused_rope=$f run $i" >> gpurun_out/embed_rope_ab.log
+          LMX_FUSED_ENCODER_ROPE=$f timeout -k 10 200 python -u -m llm_mcp_amd.bench.embed_engine_bench \
+              --batch-tokens 65536 --docs 2048 >> gpurun_out/embed_rope_ab.log 2>&1 || exit $?
+        done
+      done
+      grep -E "fused_rope|emb_per_s" gpurun_out/embed_rope_ab.log ;;
     race_tests)
       run race_tests 400 python -u -m pytest tests/test_00_peer_ar_gpu.py tests/test_kernels_gpu.py \
           -k "race or sharded or sample" -x -v --timeout 300 --timeout-method thread \
