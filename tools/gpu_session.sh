@@ -482,6 +482,12 @@ for step in "$@"; do
       LMX_FUSED_ENCODER_ROPE=1 timeout -k 10 200 python -u -m llm_mcp_amd.bench.embed_engine_bench \
           --batch-tokens 65536 >> gpurun_out/embed_batch.log 2>&1 || exit $?
       grep emb_per_s gpurun_out/embed_batch.log ;;
+    budget_trace)
+      # one run per budget with the engine's step trace (bench.py logs each wave's steps)
+      for b in ${BUDGETS:-33280 36864 65664}; do
+        LMX_STEP_TRACE=1 run budget_trace_$b 400 python bench.py --steps 3 --warmup 1 \
+            --max-batched-tokens $b || exit $?
+      done ;;
     embed_rope_ab)
       # nomic at 64k tokens per batch: q rotated in the rope/cache kernel vs inside attention,
       # alternating, 3 pairs
