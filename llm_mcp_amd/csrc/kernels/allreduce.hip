@@ -17,8 +17,8 @@
 // "stores; s_waitcnt vmcnt(0); barrier; flag store" with no L2 write-back.
 // Layout of a region (bytes):
 //   [0, 256)           control: epoch (u32), arrival ticket (u32), error (u32)
-//   [256, 256 + 4 KB)  flags[2 phases][64 blocks][8 ranks] (u32 epochs)
-//   [8 KB, ...)        2 parities x {input copy (slot_bytes), result (slot_bytes)}
+//   [256, 256 + 12 KB) flags[3 phases][128 blocks][8 ranks] (u32 epochs)
+//   [16 KB, ...)       2 parities x {input copy (slot_bytes), result (slot_bytes)}
 // Epochs live on the device (read at kernel start, advanced by the last block
 // to finish) so a captured hipGraph replays correctly.  Consecutive calls
 // alternate the data parity; a rank can only reach call e + 2 after every
@@ -35,8 +35,8 @@
 
 namespace lmx {
 
-constexpr int AR_MAX_W = 8, AR_MAX_BLOCKS = 64, AR_THREADS = 512;
-constexpr long AR_CTL = 0, AR_FLAGS = 256, AR_DATA = 8192;
+constexpr int AR_MAX_W = 8, AR_MAX_BLOCKS = 128, AR_THREADS = 512;
+constexpr long AR_CTL = 0, AR_FLAGS = 256, AR_DATA = 16384;
 
 struct ArPeers {
   char* p[AR_MAX_W];
@@ -60,6 +60,40 @@ __device__ __forceinline__ void ar_barrier(const ArPeers& peers, int rank, int p
     const uint32_t* mine = ar_flags(peers.p[rank], phase) + b * AR_MAX_W + t;
     int it = 0;
     while ((int)(__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
+      if (++it > spin_max) {
+        __hip_atomic_store(reinterpret_cast<uint32_t*>(peers.p[rank] + AR_CTL) + 2, 1u,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+}
+
+// rendezvous of a group of ``cs`` blocks [g0, g0 + cs): block b signals its
+// own flag (to every rank, or only to this rank when ``local``), then waits
+// until every block of the group has signalled on every rank (local: on
+// this rank) -- the fused norm's column-split blocks of one row group
+template <int W>
+__device__ __forceinline__ void ar_group_barrier(const ArPeers& peers, int rank, int phase, int b,
+                                                 int g0, int cs, bool local, uint32_t e,
+                                                 int spin_max) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int t = threadIdx.x, nr = local ? 1 : W;
+  if (t < nr) {
+    const int q = local ? rank : t;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __hip_atomic_store(ar_flags(peers.p[q], phase) + b * AR_MAX_W + rank, e, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (t < nr * cs) {
+    const int q = local ? rank : t % W, blk = g0 + t / nr;
+    const uint32_t* f = ar_flags(peers.p[rank], phase) + blk * AR_MAX_W + q;
+    int it = 0;
+    while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
       if (++it > spin_max) {
         __hip_atomic_store(reinterpret_cast<uint32_t*>(peers.p[rank] + AR_CTL) + 2, 1u,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -172,71 +206,102 @@ __global__ void __launch_bounds__(AR_THREADS) allreduce_kernel(
 // residual-add RMSNorm triple's last two launches and the o round trip
 // between them; the residual stream is bitwise what they produce, h up to the
 // summation order of the row's sum of squares.
-//   one-shot: block b owns rows b, b + nb, ...: publishes them, meets its
-//     peers' block b, sums every rank's copy and norms the row;
-//   two-shot: rows are sharded by rank (S = ceil(T / W) rows each); block b
-//     owns shard rows i = b, b + nb, ... of EVERY shard, so the per-block
-//     rendezvous orders each read after the write it needs: publish those
-//     rows -> meet -> sum own shard's rows into the result slot -> meet ->
-//     read every shard's summed rows from their owners and norm them.
-// rmsnorm over one row by the whole block: d8 = cols / 8 <= VPT * AR_THREADS
+//
+// Grid: row groups x ``cs`` column chunks.  Block b = (row group b / cs, chunk
+// b % cs) moves and sums only its chunk of each row, so a decode step's few
+// rows per rank (T / W at two-shot: 32 at 256 rows and W = 8) still spread
+// over up to 128 CUs instead of one CU per row.  The chunks of a row meet
+// through per-chunk partial sums of squares kept beside the data:
+//   one-shot: block (g, c) publishes chunk c of its rows, meets block (g, c)
+//     of every rank, sums every rank's copy, writes residual chunk c and its
+//     partial; a LOCAL rendezvous of the row group's cs blocks then makes the
+//     row's partials visible, and each block norms its chunk;
+//   two-shot: rows are sharded by rank (S = ceil(T / W) rows each); the owner's
+//     block (g, c) sums chunk c of its shard rows into its result slot with the
+//     partial sum of squares of residual + o beside it (the residual is the
+//     same on every rank); after a rendezvous over the row group's cs blocks on
+//     every rank, each block reads chunk c and the cs partials of every row from
+//     its owner and norms it.  Every rank sums the same partials in the same
+//     order, so h is the same on every rank.
 template <int VPT>
-__device__ __forceinline__ void ar_norm_row(u16x8* __restrict__ h_row, u16x8* __restrict__ res_row,
-                                            const u16x8* __restrict__ w, const float (&o)[VPT][8],
-                                            int d8, float eps, float* scratch) {
-  const int t = threadIdx.x;
-  float v[VPT][8];
+__device__ __forceinline__ void ar_load_chunk(float (&o)[VPT][8], const u16x8* __restrict__ src,
+                                              int dc) {
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int c = threadIdx.x + k * AR_THREADS;
+    if (c < dc) {
+      const u16x8 v = src[c];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[k][j] = bf2f(v.v[j]);
+    }
+  }
+}
+
+// residual chunk += bf16(o) (written back), returns the block's sum of squares
+template <int VPT>
+__device__ __forceinline__ float ar_residual_chunk(u16x8* __restrict__ res, const float (&o)[VPT][8],
+                                                   int dc, bool write, float* scratch) {
   float ss = 0.f;
 #pragma unroll
   for (int k = 0; k < VPT; ++k) {
-    const int c = t + k * AR_THREADS;
-    if (c < d8) {
-      const u16x8 r = res_row[c];
+    const int c = threadIdx.x + k * AR_THREADS;
+    if (c < dc) {
+      const u16x8 r = res[c];
       u16x8 hb;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         hb.v[j] = f2bf(bf2f(f2bf(o[k][j])) + bf2f(r.v[j]));
-        v[k][j] = bf2f(hb.v[j]);
-        ss += v[k][j] * v[k][j];
+        const float v = bf2f(hb.v[j]);
+        ss += v * v;
       }
-      res_row[c] = hb;
+      if (write) res[c] = hb;
     }
   }
-  ss = block_sum(ss, scratch);
-  const float inv = rsqrtf(ss / (float)(d8 * 8) + eps);
+  return block_sum(ss, scratch);
+}
+
+// h chunk = residual chunk (already updated) * inv * w
+template <int VPT>
+__device__ __forceinline__ void ar_scale_chunk(u16x8* __restrict__ h, const u16x8* __restrict__ res,
+                                               const u16x8* __restrict__ w, float inv, int dc) {
 #pragma unroll
   for (int k = 0; k < VPT; ++k) {
-    const int c = t + k * AR_THREADS;
-    if (c < d8) {
-      const u16x8 wv = w[c];
+    const int c = threadIdx.x + k * AR_THREADS;
+    if (c < dc) {
+      const u16x8 r = res[c], wv = w[c];
       u16x8 y;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) y.v[j] = f2bf(v[k][j] * inv * bf2f(wv.v[j]));
-      h_row[c] = y;
+      for (int j = 0; j < 8; ++j) y.v[j] = f2bf(bf2f(r.v[j]) * inv * bf2f(wv.v[j]));
+      h[c] = y;
     }
   }
-  __syncthreads();          // scratch reuse by the next row's block_sum
 }
 
 template <int W, int VPT>
 __global__ void __launch_bounds__(AR_THREADS) allreduce_norm_kernel(
     u16x8* __restrict__ h_out, u16x8* __restrict__ residual, const u16x8* __restrict__ inp,
     const u16x8* __restrict__ w, int T, int d8, float eps, int rank, ArPeers peers,
-    long slot_bytes, int two_shot, int spin_max) {
+    long slot_bytes, int two_shot, int cs, int spin_max) {
   __shared__ float scratch[16];
   char* own = peers.p[rank];
   uint32_t* ctl = reinterpret_cast<uint32_t*>(own + AR_CTL);
   const uint32_t e = ctl[0] + 1u;
   const long par_off = AR_DATA + (long)(e & 1u) * 2 * slot_bytes;
   const int b = blockIdx.x, nb = gridDim.x, t = threadIdx.x;
+  const int nr = nb / cs, rg = b / cs, ch = b % cs, g0 = rg * cs;
+  const int dc = d8 / cs, c0 = ch * dc;               // this block's 16-B columns
+  const long ss_off = (long)T * d8 * 16;              // partials [T][cs] after the rows
   auto in_slot = [&](int q) { return reinterpret_cast<u16x8*>(peers.p[q] + par_off); };
-  auto res_slot = [&](int q) { return reinterpret_cast<u16x8*>(peers.p[q] + par_off + slot_bytes); };
-  auto publish = [&](int row) {
-    u16x8* dst = in_slot(rank) + (long)row * d8;
-    const u16x8* src = inp + (long)row * d8;
-    for (int c = t; c < d8; c += AR_THREADS) dst[c] = src[c];
+  auto res_base = [&](int q) { return peers.p[q] + par_off + slot_bytes; };
+  auto partials = [&](int q, int row) {
+    return reinterpret_cast<float*>(res_base(q) + ss_off) + (long)row * cs;
   };
-  // fp32 rank-order sum of every rank's copy of one row (this thread's chunks)
+  auto publish = [&](int row) {
+    u16x8* dst = in_slot(rank) + (long)row * d8 + c0;
+    const u16x8* src = inp + (long)row * d8 + c0;
+    for (int c = t; c < dc; c += AR_THREADS) dst[c] = src[c];
+  };
+  // fp32 rank-order sum of every rank's copy of this block's chunk of a row
   auto row_sum = [&](int row, float (&o)[VPT][8]) {
 #pragma unroll
     for (int k = 0; k < VPT; ++k)
@@ -244,11 +309,11 @@ __global__ void __launch_bounds__(AR_THREADS) allreduce_norm_kernel(
       for (int j = 0; j < 8; ++j) o[k][j] = 0.f;
 #pragma unroll
     for (int q = 0; q < W; ++q) {
-      const u16x8* src = in_slot(q) + (long)row * d8;
+      const u16x8* src = in_slot(q) + (long)row * d8 + c0;
 #pragma unroll
       for (int k = 0; k < VPT; ++k) {
         const int c = t + k * AR_THREADS;
-        if (c < d8) {
+        if (c < dc) {
           const u16x8 v = src[c];
 #pragma unroll
           for (int j = 0; j < 8; ++j) o[k][j] += bf2f(v.v[j]);
@@ -256,53 +321,63 @@ __global__ void __launch_bounds__(AR_THREADS) allreduce_norm_kernel(
       }
     }
   };
+  // the row's inverse RMS from the cs partials a rank left beside its rows
+  auto row_inv = [&](int q, int row) {
+    const float* pp = partials(q, row);
+    float ss = 0.f;
+    for (int c = 0; c < cs; ++c) ss += pp[c];
+    return rsqrtf(ss / (float)(d8 * 8) + eps);
+  };
   float o[VPT][8];
   if (!two_shot) {
-    for (int row = b; row < T; row += nb) publish(row);
-    ar_barrier<W>(peers, rank, 0, b, e, spin_max);
-    for (int row = b; row < T; row += nb) {
+    for (int row = rg; row < T; row += nr) publish(row);
+    ar_group_barrier<W>(peers, rank, 0, b, b, 1, false, e, spin_max);
+    for (int row = rg; row < T; row += nr) {
       row_sum(row, o);
-      ar_norm_row<VPT>(h_out + (long)row * d8, residual + (long)row * d8, w, o, d8, eps,
-                       scratch);
+      const float ss = ar_residual_chunk<VPT>(residual + (long)row * d8 + c0, o, dc, true,
+                                              scratch);
+      if (t == 0) partials(rank, row)[ch] = ss;
     }
+    ar_group_barrier<W>(peers, rank, 2, b, g0, cs, true, e, spin_max);
+    for (int row = rg; row < T; row += nr)
+      ar_scale_chunk<VPT>(h_out + (long)row * d8 + c0, residual + (long)row * d8 + c0, w + c0,
+                          row_inv(rank, row), dc);
   } else {
     const int S = (T + W - 1) / W;
 #pragma unroll
     for (int q = 0; q < W; ++q)
-      for (int i = b; i < S && q * S + i < T; i += nb) publish(q * S + i);
-    ar_barrier<W>(peers, rank, 0, b, e, spin_max);
-    for (int i = b; i < S && rank * S + i < T; i += nb) {
+      for (int i = rg; i < S && q * S + i < T; i += nr) publish(q * S + i);
+    ar_group_barrier<W>(peers, rank, 0, b, b, 1, false, e, spin_max);
+    for (int i = rg; i < S && rank * S + i < T; i += nr) {
       const int row = rank * S + i;
       row_sum(row, o);
-      u16x8* dst = res_slot(rank) + (long)row * d8;
+      u16x8* dst = reinterpret_cast<u16x8*>(res_base(rank)) + (long)row * d8 + c0;
 #pragma unroll
       for (int k = 0; k < VPT; ++k) {
         const int c = t + k * AR_THREADS;
-        if (c < d8) {
+        if (c < dc) {
           u16x8 y;
 #pragma unroll
           for (int j = 0; j < 8; ++j) y.v[j] = f2bf(o[k][j]);
           dst[c] = y;
         }
       }
+      // the partial of residual + o, as every rank will form it (not written here)
+      const float ss = ar_residual_chunk<VPT>(residual + (long)row * d8 + c0, o, dc, false,
+                                              scratch);
+      if (t == 0) partials(rank, row)[ch] = ss;
     }
-    ar_barrier<W>(peers, rank, 1, b, e, spin_max);
+    ar_group_barrier<W>(peers, rank, 1, b, g0, cs, false, e, spin_max);
 #pragma unroll
     for (int q = 0; q < W; ++q) {
-      for (int i = b; i < S && q * S + i < T; i += nb) {
+      for (int i = rg; i < S && q * S + i < T; i += nr) {
         const int row = q * S + i;
-        const u16x8* src = res_slot(q) + (long)row * d8;
-#pragma unroll
-        for (int k = 0; k < VPT; ++k) {
-          const int c = t + k * AR_THREADS;
-          if (c < d8) {
-            const u16x8 v = src[c];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) o[k][j] = bf2f(v.v[j]);
-          }
-        }
-        ar_norm_row<VPT>(h_out + (long)row * d8, residual + (long)row * d8, w, o, d8, eps,
-                         scratch);
+        ar_load_chunk<VPT>(o, reinterpret_cast<const u16x8*>(res_base(q)) + (long)row * d8 + c0,
+                           dc);
+        u16x8* res_row = residual + (long)row * d8 + c0;
+        // o is bf16 already: f2bf(o) inside is exact
+        (void)ar_residual_chunk<VPT>(res_row, o, dc, true, scratch);
+        ar_scale_chunk<VPT>(h_out + (long)row * d8 + c0, res_row, w + c0, row_inv(q, row), dc);
       }
     }
   }
@@ -400,15 +475,18 @@ int allreduce(void* out, const void* inp, long nbytes, int rank, int world,
   return (int)hipGetLastError();
 }
 
-// fused all-reduce + residual add + RMSNorm of [T, cols] bf16 rows
+// fused all-reduce + residual add + RMSNorm of [T, cols] bf16 rows: ``groups``
+// row groups x ``cs`` column chunks (cs divides cols / 8)
 int allreduce_norm(void* h_out, void* residual, const void* inp, const void* w, int T, int cols,
                    float eps, int rank, int world, const unsigned long long* peer_ptrs,
-                   long slot_bytes, int two_shot, int blocks, int spin_max, hipStream_t stream) {
+                   long slot_bytes, int two_shot, int groups, int cs, int spin_max,
+                   hipStream_t stream) {
   if (T <= 0) return 0;
   if (world < 2 || world > AR_MAX_W || rank < 0 || rank >= world) return -1;
-  if (cols % 8 != 0 || cols > 8 * AR_THREADS * 4) return -2;
-  if ((long)T * cols * 2 > slot_bytes) return -2;
-  if (blocks < 1 || blocks > AR_MAX_BLOCKS) return -4;
+  if (cols % 8 != 0 || cs < 1 || (cols / 8) % cs != 0 || cols / 8 / cs > AR_THREADS * 4)
+    return -2;
+  if ((long)T * cols * 2 + (long)T * cs * 4 > slot_bytes) return -2;
+  if (groups < 1 || groups * cs > AR_MAX_BLOCKS) return -4;
   if (((uintptr_t)h_out | (uintptr_t)residual | (uintptr_t)inp | (uintptr_t)w) % 16 != 0)
     return -5;
   if (two_shot < 0 || two_shot > 1) return -7;
@@ -417,11 +495,11 @@ int allreduce_norm(void* h_out, void* residual, const void* inp, const void* w, 
   for (int q = 0; q < world; ++q)
     if (!p.p[q]) return -6;
   const int d8 = cols / 8;
-  const int vpt = (d8 + AR_THREADS - 1) / AR_THREADS;
+  const int vpt = (d8 / cs + AR_THREADS - 1) / AR_THREADS;
 #define LMX_ARN(WV, VV)                                                                        \
-  allreduce_norm_kernel<WV, VV><<<dim3(blocks), dim3(AR_THREADS), 0, stream>>>(                \
+  allreduce_norm_kernel<WV, VV><<<dim3(groups * cs), dim3(AR_THREADS), 0, stream>>>(           \
       (u16x8*)h_out, (u16x8*)residual, (const u16x8*)inp, (const u16x8*)w, T, d8, eps, rank, p,  \
-      slot_bytes, two_shot, spin_max);
+      slot_bytes, two_shot, cs, spin_max);
 #define LMX_ARN_W(WV)                 \
   if (vpt <= 1) { LMX_ARN(WV, 1) }    \
   else if (vpt <= 2) { LMX_ARN(WV, 2) } \

@@ -73,7 +73,7 @@ int ar_ipc_handle_size();
 int ar_error(void*, int);
 int ar_error_async(void*, void*, hipStream_t);
 int allreduce_norm(void*, void*, const void*, const void*, int, int, float, int, int,
-                   const unsigned long long*, long, int, int, int, hipStream_t);
+                   const unsigned long long*, long, int, int, int, int, hipStream_t);
 int allreduce(void*, const void*, long, int, int, const unsigned long long*, long, int, int, int,
               hipStream_t);
 }  // namespace lmx
@@ -274,11 +274,12 @@ PYBIND11_MODULE(_lmx_kernels, m) {
   });
   m.def("allreduce_norm", [](uptr h_out, uptr residual, uptr inp, uptr w, int T, int cols,
                              float eps, int rank, int world, std::vector<unsigned long long> peers,
-                             long slot_bytes, int two_shot, int blocks, int spin_max, uptr stream) {
+                             long slot_bytes, int two_shot, int groups, int cs, int spin_max,
+                             uptr stream) {
     if ((int)peers.size() < world) throw std::runtime_error("allreduce_norm: peers < world");
     check(lmx::allreduce_norm(P<void>(h_out), P<void>(residual), P<void>(inp), P<void>(w), T,
-                              cols, eps, rank, world, peers.data(), slot_bytes, two_shot, blocks,
-                              spin_max, S(stream)),
+                              cols, eps, rank, world, peers.data(), slot_bytes, two_shot, groups,
+                              cs, spin_max, S(stream)),
           "allreduce_norm");
   });
   m.def("ar_error_async", [](uptr own, uptr host, uptr stream) {

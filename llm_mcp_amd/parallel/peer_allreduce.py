@@ -32,6 +32,7 @@ from ..native import kernels as native
 log = logging.getLogger("lmx.tp")
 
 MAX_WORLD, MAX_BLOCKS = 8, 64
+NORM_BLOCKS = 128       # fused norm grid cap (allreduce.hip AR_MAX_BLOCKS)
 
 
 class PeerAllReduce:
@@ -49,6 +50,8 @@ class PeerAllReduce:
         # could expire while a follower process was descheduled); a timed-out
         # kernel sets the error word, which check_async / failed() surface
         self.spin_max = int(spin_max or os.environ.get("LMX_AR_SPIN", 1 << 25))
+        # column chunks per row of the fused all-reduce + norm (1: one block per row)
+        self.norm_max_cs = max(1, int(os.environ.get("LMX_AR_NORM_CS", "2")))
         self._err_h = None
         self.k = native()
         self.own, self.peers, self.calls = None, [], 0
@@ -60,8 +63,18 @@ class PeerAllReduce:
             mine = self.k.ar_ipc_handle(self.own)
         except RuntimeError as ex:
             why = str(ex)
+        # ranks sharing this rank's GPU (a one-GPU rehearsal puts them all on
+        # one card): their fused-norm grids must be co-resident together, so the
+        # per-rank grid shrinks with it (norm_plan)
+        import socket
+        key = (socket.gethostname(), os.environ.get("HIP_VISIBLE_DEVICES", ""),
+               os.environ.get("CUDA_VISIBLE_DEVICES", ""),
+               os.environ.get("ROCR_VISIBLE_DEVICES", ""), device.index)
         handles = [None] * world
-        dist.all_gather_object(handles, mine, group=group)
+        dist.all_gather_object(handles, (mine, key), group=group)
+        keys = [h[1] for h in handles]
+        handles = [h[0] for h in handles]
+        self.co_resident = max(keys.count(k) for k in keys)
         if not all(handles):
             self.close()
             raise RuntimeError(f"peer all-reduce: a rank could not export its region ({why})")
@@ -101,8 +114,25 @@ class PeerAllReduce:
         """``t`` [T, cols] can take the fused all-reduce + residual + RMSNorm."""
         return (self.supports(t) and t.dim() == 2 and t.shape[1] % 8 == 0
                 and t.shape[1] <= 16384 and self.world in (2, 4, 8)
+                and t.numel() * 2 + t.shape[0] * 16 <= self.slot
                 and residual.is_contiguous() and residual.shape == t.shape
                 and residual.dtype == torch.bfloat16 and residual.data_ptr() % 16 == 0)
+
+    def norm_plan(self, T: int, cols: int, two: int) -> tuple[int, int]:
+        """(row groups, column chunks) of the fused norm's grid: a row's 16-B
+        columns split over up to NORM_MAX_CS blocks (>= 256 per block) while
+        the grid stays within NORM_BLOCKS, so the few rows a rank owns at
+        decode (T / W at two-shot) still spread over many CUs."""
+        rows = -(-T // self.world) if two else T
+        # every block of every rank on a card must be resident at once (they
+        # wait on each other): 128 per rank alone on its GPU, 32 per rank when
+        # a rehearsal shares one GPU between up to 8 ranks
+        cap = max(32, min(NORM_BLOCKS, 256 // max(1, getattr(self, "co_resident", 1))))
+        d8, cs = cols // 8, 1
+        while (cs * 2 <= self.norm_max_cs and d8 % (cs * 2) == 0 and d8 // (cs * 2) >= 256
+               and min(rows, cap // (cs * 2)) * cs * 2 > min(rows, cap // cs) * cs):
+            cs *= 2
+        return max(1, min(rows, cap // cs)), cs
 
     def all_reduce_norm(self, t: torch.Tensor, w: torch.Tensor, eps: float,
                         residual: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
@@ -117,11 +147,10 @@ class PeerAllReduce:
             out = torch.empty_like(t)
         n = T * cols * 2
         two = int(n > self.oneshot_max and T >= self.world)
-        rows = -(-T // self.world) if two else T
-        blocks = max(1, min(MAX_BLOCKS, rows))
+        groups, cs = self.norm_plan(T, cols, two)
         self.k.allreduce_norm(out.data_ptr(), residual.data_ptr(), t.data_ptr(), w.data_ptr(),
                               T, cols, float(eps), self.rank, self.world, self.peers, self.slot,
-                              two, blocks, self.spin_max,
+                              two, groups, cs, self.spin_max,
                               torch.cuda.current_stream(t.device).cuda_stream)
         self.calls += 1
         return out

@@ -85,6 +85,7 @@ VARS: list[Var] = [
     Var("LMX_PREFIX_CACHE", int, 1, "1: full KV pages are hashed and kept (LRU) for reuse by later prompts with the same prefix; 0: pages return to the free list when their sequence ends"),
     Var("LMX_MIXED_MIN_DECODES", int, 32, "decode rows that make a step 'mixed' for LMX_MIXED_PREFILL_TOKENS"),
     Var("LMX_MIXED_LATER_STEPS", int, 8, "LMX_MIXED_PREFILL_TOKENS counts only decode rows whose request came >= this many scheduler steps before the newest request with prompt tokens left (streams interrupted by later arrivals); 0 = every decode row"),
+    Var("LMX_AR_NORM_CS", int, 2, "fused TP all-reduce + RMSNorm: column chunks per row (blocks per row, >= 256 16-B columns each), so a rank's few decode rows spread over more CUs; 1 = one block per row"),
     Var("LMX_AR_SPIN", int, 1 << 25, "peer all-reduce: polls (s_sleep 1 each) a kernel waits for a TP peer before it gives up and sets the error word (the engine then fails the step)"),
     Var("LMX_ALLOW_CLOUD", int, 0, "1: allow cloud providers (never on the GPU hot path)"),
     Var("LMX_JOB_RETENTION_DAYS", float, 7.0, "purge finished jobs older than this"),

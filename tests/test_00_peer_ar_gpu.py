@@ -129,8 +129,11 @@ def _rank(rank, world, port, q):
         # bitwise equal to the all-reduce followed by ops.rms_norm(residual=),
         # one-shot and row-sharded two-shot (T not a multiple of the world too)
         from llm_mcp_amd import ops
-        for salt, (T, cols) in enumerate([(1, 8192), (16, 8192), (37, 1024), (256, 8192),
-                                          (300, 4096)], start=400):
+        # column-split grids (up to 4 chunks; 2 by default) and one block per row
+        shapes = [(1, 8192), (16, 8192), (37, 1024), (256, 8192), (300, 4096)]
+        for salt, (T, cols, mcs) in enumerate([(T, c, m) for m in (4, 1) for T, c in shapes],
+                                              start=400):
+            ar.norm_max_cs = mcs
             xs = [x.view(T, cols) for x in _inputs(world, T * cols, salt)]
             res0 = _inputs(1, T * cols, salt + 7)[0].view(T, cols)
             wgt = (1 + 0.1 * torch.randn(cols, generator=torch.Generator().manual_seed(salt))
@@ -144,13 +147,15 @@ def _rank(rank, world, port, q):
             # (512 vs 256 threads per row): a last-bit difference of the scale
             if not (torch.equal(res, res_u) and torch.allclose(h.float(), h_u.float(),
                                                                 atol=1e-2, rtol=1e-2)):
-                errs.append(f"fused norm T={T} cols={cols}: differs from all-reduce + rms_norm")
+                errs.append(f"fused norm T={T} cols={cols} cs<={mcs}: differs from all-reduce "
+                            "+ rms_norm")
             o = torch.stack([v.float() for v in xs]).sum(0).to(torch.bfloat16)
             r = (o.float() + res0.float()).to(torch.bfloat16).float()
             want = (r * torch.rsqrt(r.pow(2).mean(-1, keepdim=True) + 1e-5) * wgt.float())
             if not torch.allclose(h.float().cpu(), want, atol=3e-2, rtol=3e-2):
-                errs.append(f"fused norm T={T} cols={cols}: vs fp32 reference")
+                errs.append(f"fused norm T={T} cols={cols} cs<={mcs}: vs fp32 reference")
         errs += ["fused norm: error word set"] if ar.error(clear=True) else []
+        ar.norm_max_cs = 4
         # ... and inside a captured graph (device epochs), new inputs per replay
         T, cols = 64, 8192
         x = torch.zeros(T, cols, dtype=torch.bfloat16, device=dev)

@@ -500,6 +500,13 @@ for step in "$@"; do
         done
       done
       grep -E "fused_rope|emb_per_s" gpurun_out/embed_rope_ab.log ;;
+    ar_norm)
+      # fused all-reduce + norm at world 8 on one GPU (local cost), cs 1/2/4, then the peer
+      # all-reduce GPU tests (correctness at world 2/4/8, both grids)
+      run ar_norm_probe 300 python -u tools/ar_norm_probe.py --worlds 2,8 || exit $?
+      cat gpurun_out/ar_norm_probe.log
+      run ar_tests 400 python -u -m pytest tests/test_00_peer_ar_gpu.py -x -v --timeout 300 \
+          --timeout-method thread -p no:cacheprovider || exit $? ;;
     race_tests)
       run race_tests 400 python -u -m pytest tests/test_00_peer_ar_gpu.py tests/test_kernels_gpu.py \
           -k "race or sharded or sample" -x -v --timeout 300 --timeout-method thread \
