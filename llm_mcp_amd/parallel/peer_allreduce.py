@@ -68,7 +68,6 @@ class PeerAllReduce:
         # per-rank grid shrinks with it (norm_plan)
         import socket
         key = (socket.gethostname(), os.environ.get("HIP_VISIBLE_DEVICES", ""),
-               os.environ.get("CUDA_VISIBLE_DEVICES", ""),
                os.environ.get("ROCR_VISIBLE_DEVICES", ""), device.index)
         handles = [None] * world
         dist.all_gather_object(handles, (mine, key), group=group)
