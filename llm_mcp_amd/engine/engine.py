@@ -104,8 +104,8 @@ class EngineConfig:
     tokens.  One burst's rows never cap each other, so a wave of requests is
     prefilled at the full budget, while in steady serving a new request's
     prefill is chunked so it cannot stall the running streams for a
-    24k-token step (closed loop at 256 streams: per-token gap p99 251 -> 35
-    ms, TTFT p50 756 -> 101 ms; profiles/r6_serving.md).  36864-token steps
+    full-budget step (closed loop at 256 streams: per-token gap p99 251 -> 35
+    ms, TTFT p50 756 -> 454 ms; profiles/r6_serving.md).  36864-token steps
     take a 256 x 512-token wave in 4 steps instead of 6: equal throughput and
     TTFT to 24576, fewer stalled decode gaps (token-gap p99 168 -> 13 ms;
     profiles/r6_serving.md "Prefill budget")."""
