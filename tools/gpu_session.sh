@@ -286,6 +286,17 @@ for step in "$@"; do
       # Llama-3-70B at TP = 1 (review round 4, item 6): one copy of the MLP weights, K14 decode
       run l70 1000 python bench.py --model llama-3-70b --concurrency 128 --max-tokens 128 \
           --steps 2 --warmup 1 || exit $? ;;
+    l70_ab)
+      # Llama-3-70B TP = 1 under the round-6 serving defaults vs the round-5 budget / no cap,
+      # alternating, twice
+      for i in 1 2; do
+        run l70_def_$i 600 python bench.py --model llama-3-70b --concurrency 128 --max-tokens 128 \
+            --steps 2 --warmup 1 || exit $?
+        LMX_MAX_BATCHED_TOKENS=24576 run l70_b24k_$i 600 python bench.py --model llama-3-70b \
+            --concurrency 128 --max-tokens 128 --steps 2 --warmup 1 || exit $?
+        LMX_MAX_BATCHED_TOKENS=24576 LMX_MIXED_PREFILL_TOKENS=0 run l70_r5_$i 600 python bench.py \
+            --model llama-3-70b --concurrency 128 --max-tokens 128 --steps 2 --warmup 1 || exit $?
+      done ;;
     l70_two)
       LMX_RS_SINGLE=0 run l70_two 1000 python bench.py --model llama-3-70b --concurrency 128 \
           --max-tokens 128 --steps 2 --warmup 1 || exit $? ;;
