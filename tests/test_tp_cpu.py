@@ -370,3 +370,29 @@ def test_all_reduce_async_takes_rccl_beside_the_peer_kernel(monkeypatch):
     h_big = tp.all_reduce_async(big)
     assert isinstance(h_small, _Done) and isinstance(h_big, Handle)
     assert calls == [("peer", 256), ("rccl_async", 64 * 1024)]
+
+
+def test_fused_norm_grid_plan():
+    """PeerAllReduce.norm_plan: a rank's few decode rows split over column
+    chunks (>= 256 16-B columns each, LMX_AR_NORM_CS at most), at most 128
+    blocks per rank alone on its GPU and 256 / ranks-per-card when a one-GPU
+    rehearsal puts the whole group on one card (all blocks must co-reside)."""
+    from llm_mcp_amd.parallel.peer_allreduce import PeerAllReduce
+
+    def plan(world, T, cols, two, co=1, mcs=2):
+        p = PeerAllReduce.__new__(PeerAllReduce)
+        p.world, p.norm_max_cs, p.co_resident = world, mcs, co
+        return p.norm_plan(T, cols, two)
+
+    assert plan(8, 256, 8192, 1) == (32, 2)            # 32 rows per rank -> 64 blocks
+    assert plan(8, 256, 8192, 1, mcs=4) == (32, 4)
+    assert plan(8, 256, 8192, 1, mcs=1) == (32, 1)
+    assert plan(2, 256, 4096, 1) == (128, 1)           # the grid is already full
+    assert plan(8, 37, 1024, 0) == (37, 1)             # 128 columns: no split
+    assert plan(8, 256, 8192, 1, co=8, mcs=4) == (32, 1)   # 8 ranks on one card: 32 blocks
+    g, cs = plan(8, 16, 8192, 0, co=8, mcs=4)
+    assert g * cs <= 32 and cs == 2
+    for world, T, cols, two, co, mcs in [(2, 300, 4096, 1, 1, 4), (4, 64, 8192, 1, 4, 4),
+                                        (8, 1, 8192, 0, 1, 4)]:
+        g, cs = plan(world, T, cols, two, co, mcs)
+        assert g * cs <= max(32, min(128, 256 // co)) and (cols // 8) % cs == 0
