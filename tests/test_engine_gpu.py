@@ -183,6 +183,32 @@ def test_llama3_8b_shapes_on_decode_gemm_match_dense(graphs):
         assert_greedy_consistent(e.model, p, o, tol=0.08)
 
 
+@pytest.mark.parametrize("preset", ["qwen3-8b", "qwen2.5-7b", "llama-3.2-3b"])
+def test_family_shapes_on_decode_gemm_match_dense(preset):
+    """Two layers of the other served chat families at their real shapes
+    (Qwen3 q/k-norm, Qwen2.5 GQA-7 with QKV bias, Llama-3.2-3B): the round-6
+    family sweep's K11 table entries (bench/dgemm_bench.py, tools/dg_merge.py)
+    put the decode projections on the hand-written GEMM -- fused SwiGLU
+    gate/up, split-K partials summed in the residual-add RMSNorm -- in captured
+    graphs, and greedy tokens stay (near-)argmax of the dense fp32 forward."""
+    import dataclasses
+
+    from llm_mcp_amd.models import config as mc
+    ops.native()
+    cfg = dataclasses.replace(mc.resolve(preset), num_layers=2)
+    n0 = ops.DGEMM_CALLS[0]
+    e = LLMEngine(EngineConfig(model=preset, max_num_seqs=64, max_batched_tokens=512,
+                               max_model_len=512, use_graphs=True, kv_cache_gb=1),
+                  device="cuda", model_cfg=cfg)
+    assert e.model.gu_block == ops.SWIGLU16, "fused SwiGLU layout not selected from the table"
+    prompts = [[(17 * i + 3 * j) % 120000 + 100 for j in range(4)] for i in range(48)]
+    outs = e.generate(prompts, SamplingParams(temperature=0, max_tokens=3, ignore_eos=True))
+    assert ops.DGEMM_CALLS[0] > n0
+    assert e.stats["graph_steps"] > 0
+    for p, o in list(zip(prompts, outs))[::7]:
+        assert_greedy_consistent(e.model, p, o, tol=0.08)
+
+
 @pytest.mark.parametrize("graphs", [False, True])
 def test_llama3_8b_shapes_k13_prefill_and_sk_lm_head(graphs):
     """Two layers of Llama-3-8B at a 200-row batch: the one-step prefill of

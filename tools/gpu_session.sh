@@ -518,6 +518,27 @@ for step in "$@"; do
       cat gpurun_out/ar_norm_probe.log
       run ar_tests 400 python -u -m pytest tests/test_00_peer_ar_gpu.py -x -v --timeout 300 \
           --timeout-method thread -p no:cacheprovider || exit $? ;;
+    dgemm_fam)
+      # decode GEMM sweep (K11 tiles / splits / stream-K vs the library) for the other chat
+      # families' shapes; rows kept, the table is rebuilt on the CPU side (new shapes only)
+      for m in ${DG_MODELS:-qwen3-8b qwen2.5-7b}; do
+        run dg_$m 1000 python -u -m llm_mcp_amd.bench.dgemm_bench --model $m \
+            --json gpurun_out/dg_$m.json || exit $?
+      done ;;
+    fam_tests)
+      run fam_tests 600 python -u -m pytest tests/test_engine_gpu.py -k "family or llama3_8b" -x -v \
+          --timeout 300 --timeout-method thread -p no:cacheprovider || exit $? ;;
+    families)
+      # the other chat model families at the headline load (256 streams x 512-token prompts,
+      # 256 out), one wave-bench each, and the other embedding encoders
+      for m in ${FAMILIES:-qwen3-8b qwen2.5-7b llama-3.2-3b llama-3.2-1b qwen3-32b}; do
+        run fam_$m 600 python bench.py --model $m --steps 2 --warmup 1 || exit $?
+      done
+      for m in mxbai-embed-large bge-base-en-v1.5; do
+        timeout -k 10 300 python -u -m llm_mcp_amd.bench.embed_engine_bench --model $m \
+            --doc-len 512 > gpurun_out/fam_$m.log 2>&1 || exit $?
+        tail -1 gpurun_out/fam_$m.log
+      done ;;
     race_tests)
       run race_tests 400 python -u -m pytest tests/test_00_peer_ar_gpu.py tests/test_kernels_gpu.py \
           -k "race or sharded or sample" -x -v --timeout 300 --timeout-method thread \
