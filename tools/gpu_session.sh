@@ -254,14 +254,6 @@ for step in "$@"; do
     engine_tests)
       run engine_tests 600 python -u -m pytest tests/test_engine_gpu.py -x -q --timeout 200 \
           --timeout-method thread -p no:cacheprovider || exit $? ;;
-    ssm_ab)
-      # prefill attention: softmax as single-lane f32 ops vs f32 pairs, every served shape
-      # (two interleaved passes), then the prefill GPU tests with each form
-      run ssm_probe 300 python -u tools/prefill_attn_probe.py --waves 4 --ssm 0,1 --iters 30 \
-          --shapes nomic,mxbai,llama8b,llama8b_2k,llama8b_8k || exit $?
-      grep "prefill attn" gpurun_out/ssm_probe.log
-      LMX_PREFILL_SSM=1 run ssm_tests 400 python -u -m pytest tests/test_kernels_gpu.py -k prefill -x -q \
-          --timeout 300 --timeout-method thread -p no:cacheprovider || exit $? ;;
     pf_probe)
       run pf_probe 300 python -u tools/prefill_attn_probe.py \
           --shapes ${PF_SHAPES:-llama8b,llama8b_2k,llama8b_8k,nomic} --waves 4,8 || exit $? ;;
