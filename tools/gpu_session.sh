@@ -452,6 +452,16 @@ for step in "$@"; do
             mixed --gpus 0 --replicas-per-gpu 2 --jobs 2048 --concurrency 256 --sync-every 4 \
             --max-tokens 64 --chars 512 || exit $?
       done ;;
+    c5_budget)
+      # config 5 steady state (2048 jobs): the shared-GPU prefill budget (8192) vs 16384 / 4096,
+      # alternating, twice
+      for i in 1 2; do
+        for b in 8192 16384 4096; do
+          LMX_MAX_BATCHED_TOKENS=$b run c5b_${b}_$i 400 python -u -m llm_mcp_amd.bench.serving_bench \
+              mixed --gpus 0 --replicas-per-gpu 2 --jobs 2048 --concurrency 256 --sync-every 4 \
+              --max-tokens 64 --chars 512 || exit $?
+        done
+      done ;;
     prof_c5)
       # config 5 steady state under a kernel trace: GPU busy vs wall per process
       rm -rf gpurun_out/prof_c5
