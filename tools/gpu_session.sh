@@ -532,7 +532,7 @@ for step in "$@"; do
       # decode GEMM sweep (K11 tiles / splits / stream-K vs the library) for the other chat
       # families' shapes; rows kept, the table is rebuilt on the CPU side (new shapes only)
       for m in ${DG_MODELS:-qwen3-8b qwen2.5-7b}; do
-        run dg_$m 1000 python -u -m llm_mcp_amd.bench.dgemm_bench --model $m \
+        run dg_$m 1000 python -u -m llm_mcp_amd.bench.dgemm_bench --model $m --tp ${DG_TP:-1} \
             --json gpurun_out/dg_$m.json || exit $?
       done ;;
     fam_tests)
