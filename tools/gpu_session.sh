@@ -538,6 +538,16 @@ for step in "$@"; do
     fam_tests)
       run fam_tests 600 python -u -m pytest tests/test_engine_gpu.py -k "family or llama3_8b" -x -v \
           --timeout 300 --timeout-method thread -p no:cacheprovider || exit $? ;;
+    copies_ab)
+      # Llama-3-8B one packed copy of the MLP weights (K14 at every batch) vs two copies
+      # (K11 on row-major weights up to 128 rows), 64 and 256 streams, alternating, twice
+      for i in 1 2; do
+        for c in 64 256; do
+          run cp1_${c}_$i 400 python bench.py --steps 3 --warmup 1 --concurrency $c || exit $?
+          LMX_RS_SINGLE=0 run cp2_${c}_$i 400 python bench.py --steps 3 --warmup 1 \
+              --concurrency $c || exit $?
+        done
+      done ;;
     families)
       # the other chat model families at the headline load (256 streams x 512-token prompts,
       # 256 out), one wave-bench each, and the other embedding encoders
