@@ -302,7 +302,8 @@ class LlamaModel:
             # one copy of the MLP weights: gate/up (SwiGLU16 interleave) and
             # down stored only in K14's packed layout when every consumer
             # reads it (K14 decode, K13 prefill with packed W; TP = 1 path)
-            if self.tp.size == 1 and not cfg.proxy_tp:
+            if (self.tp.size == 1 and not cfg.proxy_tp
+                    and ops.rs_single_wanted(self.weight_bytes(), self.device)):
                 for L in self.w["layers"]:
                     if self.gu_block == ops.SWIGLU16 and ops.rs_single_ok(L["w_gate_up"], True):
                         L["w_gate_up"] = ops.rs_pack_only(L["w_gate_up"])

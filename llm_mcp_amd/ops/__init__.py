@@ -1107,10 +1107,20 @@ def _rs_table() -> dict:
                 and os.path.exists(path)):
             with open(path) as f:
                 for e in json.load(f).get("rs", []):
-                    _RS_TABLE.setdefault((int(e["N"]), int(e["K"]), int(e.get("epi", 0))),
-                                         []).append((int(e["m_min"]), int(e["m_max"]),
-                                                     int(e["cfg"]), int(e["splits"])))
+                    key = (int(e["N"]), int(e["K"]), int(e.get("epi", 0)))
+                    ent = (int(e["m_min"]), int(e["m_max"]), int(e["cfg"]), int(e["splits"]))
+                    _RS_TABLE.setdefault(key, []).append(ent)
+                    # entries measured slower than K11 exist to serve packed-only
+                    # weights (one copy: K11 cannot read the packed layout)
+                    pts = [(v, e["k11_" + k]) for k, v in e.items()
+                           if k.startswith("us_m") and isinstance(v, (int, float))
+                           and isinstance(e.get("k11_" + k), (int, float))]
+                    if pts and sum(a for a, _ in pts) > sum(b for _, b in pts):
+                        _RS_PACKED_ONLY_ENTRIES.add(key + ent)
     return _RS_TABLE
+
+
+_RS_PACKED_ONLY_ENTRIES: set = set()
 
 
 def rsgemm_supported(M: int, N: int, K: int, cfg: int, splits: int, epi: int = 0) -> bool:
@@ -1136,6 +1146,10 @@ def rs_choice(M: int, N: int, K: int, epi: int = 0,
         if (m_min <= M <= m_max and rsgemm_supported(M, N, K, cfg, s, epi)
                 and (epi != 2 or s in (1, 2, 4, 8, 16))):     # rmsnorm_slabs' S
             if not (cfg & RS_ROWMAJOR) and _rs_packed_of(w) is None:
+                continue
+            # K11 is faster here and can read this weight's row-major copy
+            if ((N, K, epi, m_min, m_max, cfg, s) in _RS_PACKED_ONLY_ENTRIES
+                    and w is not None and not is_packed_only(w)):
                 continue
             return cfg, s
     return None
@@ -1183,9 +1197,26 @@ def _rs_packed_of(w: torch.Tensor | None) -> torch.Tensor | None:
 # packed: decode batches (M <= 256) run K14 on it (the measured "rs" entry of
 # the batch size, else rs_default's), prefill-sized M runs K13 with packed W
 # (pgemm.hip WP).  No row-major copy is kept, so the model takes its own size
-# in HBM and the KV pool gets the rest.  LMX_RS_SINGLE=0 keeps the old
-# row-major + packed-copy scheme.
-RS_SINGLE = os.environ.get("LMX_RS_SINGLE", "1") != "0"
+# in HBM and the KV pool gets the rest.  LMX_RS_SINGLE: 1 always, 0 never
+# (row-major + packed copies), auto (default): one copy only when the model's
+# weights take more than RS_SINGLE_FRACTION of the GPU's memory -- a small
+# model keeps its row-major copy because K11 on it is faster than K14 below
+# 129 rows (Llama-3-8B, +11.3 GB = 4 % of HBM: decode step 5.23 -> 4.72 ms at
+# 64 rows, 6.70 -> 6.34 at 128, level at 256; profiles/r6_serving.md), while
+# Llama-3-70B at TP = 1 (141 GB) stays on one copy.
+RS_SINGLE_MODE = os.environ.get("LMX_RS_SINGLE", "auto")
+RS_SINGLE_FRACTION = 0.25
+RS_SINGLE = RS_SINGLE_MODE != "0"
+
+
+def rs_single_wanted(weight_bytes: int, device: torch.device) -> bool:
+    """Store the MLP weights packed-only (one copy) for a model of this size."""
+    if RS_SINGLE_MODE in ("0", "1"):
+        return RS_SINGLE_MODE == "1"
+    if device.type != "cuda":
+        return True
+    total = torch.cuda.get_device_properties(device).total_memory
+    return weight_bytes > RS_SINGLE_FRACTION * total
 
 
 def is_packed_only(w: torch.Tensor | None) -> bool:
@@ -1429,6 +1460,12 @@ def pgemm(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, ac
     the kernel (tools/lab_kernels/pgemm_lab.hip) are lab-only."""
     M, K = a.shape
     N = w.shape[0]
+    if not packed and bias is None and act in (ACT_NONE, ACT_SWIGLU) and a.is_cuda:
+        # a row-major weight with K14's packed copy beside it (two copies):
+        # prefill reads the packed one, as a packed-only weight would (WP)
+        wp = _rs_packed_of(w)
+        if wp is not None:
+            w, packed = wp, True
     packed = packed or is_packed_only(w)
     _chk(not packed or (bias is None and act in (ACT_NONE, ACT_SWIGLU) and a.is_cuda),
          "pgemm on packed W: plain / residual / SwiGLU products on CUDA")

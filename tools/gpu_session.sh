@@ -539,13 +539,14 @@ for step in "$@"; do
       run fam_tests 600 python -u -m pytest tests/test_engine_gpu.py -k "family or llama3_8b" -x -v \
           --timeout 300 --timeout-method thread -p no:cacheprovider || exit $? ;;
     copies_ab)
-      # Llama-3-8B one packed copy of the MLP weights (K14 at every batch) vs two copies
-      # (K11 on row-major weights up to 128 rows), 64 and 256 streams, alternating, twice
+      # Llama-3-8B one packed copy of the MLP weights (LMX_RS_SINGLE=1: K14 at every batch)
+      # vs the default for its size (auto: two copies, K11 up to 128 rows, K13 prefill on
+      # the packed copy), alternating, twice
       for i in 1 2; do
-        for c in 64 256; do
-          run cp1_${c}_$i 400 python bench.py --steps 3 --warmup 1 --concurrency $c || exit $?
-          LMX_RS_SINGLE=0 run cp2_${c}_$i 400 python bench.py --steps 3 --warmup 1 \
+        for c in ${COPIES_C:-64 256}; do
+          LMX_RS_SINGLE=1 run cp1_${c}_$i 400 python bench.py --steps 3 --warmup 1 \
               --concurrency $c || exit $?
+          run cp2_${c}_$i 400 python bench.py --steps 3 --warmup 1 --concurrency $c || exit $?
         done
       done ;;
     families)
