@@ -227,6 +227,9 @@ for step in "$@"; do
     closed_default)
       run closed_default 600 python bench.py --load closed --duration 30 --closed-warmup 10 \
           || exit $? ;;
+    closed64)
+      run closed64 600 python bench.py --load closed --duration 30 --closed-warmup 10 \
+          --concurrency 64 || exit $? ;;
     closed_nocap)
       run closed_nocap 600 python bench.py --load closed --duration 30 --closed-warmup 10 \
           --mixed-prefill-tokens 0 || exit $? ;;
