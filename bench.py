@@ -247,7 +247,8 @@ def main() -> None:
             follower.start()
     log(f"engine ready on {dev} in {time.time() - t_init:.1f}s: {engine.num_blocks} KV "
         f"blocks, {len(engine.graphs)} decode graphs, "
-        f"weights {engine.model.weight_bytes() / 1e9:.1f} GB"
+        f"weights {engine.model.weight_bytes() / 1e9:.1f} GB "
+        f"({engine.model.weight_bytes(copies=True) / 1e9:.1f} GB with packed copies)"
         + (f" (TP rank {grank}/{a.tp} of engine {grp})" if a.tp > 1 else ""))
     server = None
     if grank == 0:

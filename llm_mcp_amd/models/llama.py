@@ -373,14 +373,17 @@ class LlamaModel:
         return {"embed": self.w["embed"], "norm": self.w["norm"],
                 "lm_head": ops.dense_weight(self.w["lm_head"]), "layers": layers}
 
-    def weight_bytes(self) -> int:
+    def weight_bytes(self, copies: bool = False) -> int:
+        """Bytes of the model's weights; ``copies``: plus the K14 packed
+        copies kept beside row-major weights (HBM the weights hold)."""
         n = 0
-        for k, v in self.w.items():
-            if k == "layers":
-                for l in v:
-                    n += sum(t.numel() * t.element_size() for t in l.values())
-            else:
-                n += v.numel() * v.element_size()
+        ts = [t for k, v in self.w.items() if k != "layers" for t in [v]]
+        ts += [t for l in self.w["layers"] for t in l.values()]
+        for t in ts:
+            n += t.numel() * t.element_size()
+            p = getattr(t, "_lmx_rs_packed", None) if copies else None
+            if p is not None:
+                n += p.numel() * p.element_size()
         return n
 
     # ----------------------------------------------------------- forward ----
