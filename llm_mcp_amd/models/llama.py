@@ -520,6 +520,9 @@ class LlamaModel:
         d = self.cfg.hidden_size
         shapes = ((L["wqkv"], ops.ACT_NONE), (L["wo"], ops.ACT_NONE),
                   (L["w_gate_up"], ops.ACT_SWIGLU), (L["w_down"], ops.ACT_NONE))
+        if torch.device(self.device).type == "cuda" and any(
+                ops.rows_split(T, w.shape[0]) for w, _ in shapes):
+            return False      # a decode-sized step split into <= 256-row pieces
         return d % 64 == 0 and all(
             ops.large_gemm_backend(T, w.shape[0], w.shape[1], act) == "k13"
             and ops.pgemm_supported(w.shape[0], w.shape[1], act) for w, act in shapes)

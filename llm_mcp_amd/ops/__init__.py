@@ -709,23 +709,61 @@ def splitk_preferred(M: int, N: int, K: int) -> bool:
     return False
 
 
+# decode batches above the decode kernels' 256 rows: K13's 256 x 256 tiles
+# leave most of the CUs idle on the narrow projections (a 512-row step has 32
+# tiles for O / down at d = 4096: 237 us for the down projection, 6x its
+# 256-row K14 time), so such a product runs as equal row pieces of <= 256 rows
+# on the decode kernels instead (profiles/r6_serving.md "512 streams")
+ROWS_SPLIT_MAX = 1024      # largest batch split this way
+ROWS_SPLIT_TILES = 128     # K13 tiles below which the product is split
+
+
+def rows_split(M: int, N: int) -> int:
+    """Row-piece size for an M-row product with N output columns, or 0 (one
+    product): 256 < M <= ROWS_SPLIT_MAX and fewer than ROWS_SPLIT_TILES
+    256 x 256 tiles."""
+    if not (DGEMM_MAX_M < M <= ROWS_SPLIT_MAX) or -(-M // 256) * (N // 256) >= ROWS_SPLIT_TILES:
+        return 0
+    n = -(-M // DGEMM_MAX_M)
+    return -(-M // n)
+
+
+def _by_rows(x: torch.Tensor, piece: int, ncols: int, fn) -> torch.Tensor:
+    """fn(rows, out) over row pieces of x, each written in place into its rows
+    of one [M, ncols] result (no concatenation pass)."""
+    y = torch.empty((x.shape[0], ncols), dtype=x.dtype, device=x.device)
+    for i in range(0, x.shape[0], piece):
+        fn(x[i:i + piece], y[i:i + piece])
+    return y
+
+
+def _into(out: torch.Tensor | None, y: torch.Tensor) -> torch.Tensor:
+    if out is None or y.data_ptr() == out.data_ptr():
+        return y
+    return out.copy_(y)
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, defer: bool = False,
-           bias: torch.Tensor | None = None):
+           bias: torch.Tensor | None = None, out: torch.Tensor | None = None):
     """x @ w^T (+ bias): the decode GEMM (K11) where the measured table picks
     it, the older split-K kernel where it was measured faster, the large-M
     GEMM (K13) for prefill-sized M where ``large_gemm_backend`` picks it, else
     hipBLASLt (bias in its epilogue).  ``defer``: the caller feeds the result to
     ``rms_norm(..., residual=)``, so a table entry for the partials-only form
-    (epi 2) may return ``Partials`` and leave the K reduction to the norm."""
+    (epi 2) may return ``Partials`` and leave the K reduction to the norm.
+    ``out``: a bf16 [M, N] destination (plain products only, not with defer)."""
+    _chk(out is None or not defer, "linear: out= is for the plain product")
+    if x.is_cuda and x.dim() == 2 and (piece := rows_split(x.shape[0], w.shape[0])):
+        return _by_rows(x, piece, w.shape[0], lambda xs, o: linear(xs, w, bias=bias, out=o))
     if is_packed_only(w):
         _chk(bias is None and x.is_cuda and x.dim() == 2, "packed-only weight: plain CUDA product")
-        return _packed_product(x, w, 2 if defer and x.shape[0] <= 256 else 0)
+        return _packed_product(x, w, 2 if defer and x.shape[0] <= 256 else 0, out=out)
     if x.is_cuda and x.dim() == 2:
         M, N, K = x.shape[0], w.shape[0], w.shape[1]
         if bias is None:
             rc = rs_choice(M, N, K, epi=2 if defer else 0, w=w)
             if rc is not None and rsgemm_operands_ok(x, w):
-                return rsgemm(x, w, rc[0], rc[1], epi=2 if defer else 0)
+                return rsgemm(x, w, rc[0], rc[1], epi=2 if defer else 0, out=out)
         if defer and bias is None:
             s = sk_choice(M, N, K, epi=2)
             if s is not None and pgemm_operands_ok(x, w):
@@ -735,53 +773,56 @@ def linear(x: torch.Tensor, w: torch.Tensor, defer: bool = False,
                 return dgemm_partials(x, w, ch[0], ch[1])
         s = sk_choice(M, N, K) if bias is None else None
         if s is not None and pgemm_operands_ok(x, w):
-            return pgemm_sk(x, w, s)
+            return pgemm_sk(x, w, s, out=out)
         ch = dgemm_choice(M, N, K)
         y = None
         if ch is not None:
-            y = dgemm(x, w, ch[0], ch[1])
+            y = dgemm(x, w, ch[0], ch[1], out=out)
         elif splitk_preferred(M, N, K):
-            y = gemm_splitk(x, w)
+            y = _into(out, gemm_splitk(x, w))
         if y is not None:
             if bias is not None:
                 y += bias
             return y
         if (large_gemm_backend(M, N, K, 0, bias is not None) == "k13"
                 and pgemm_operands_ok(x, w) and pgemm_bias_ok(bias, N)):
-            return pgemm(x, w, bias=bias)
-    return torch.nn.functional.linear(x, w, bias)
+            return pgemm(x, w, bias=bias, out=out)
+    return _into(out, torch.nn.functional.linear(x, w, bias))
 
 
-def linear_swiglu(x: torch.Tensor, w: torch.Tensor, block: int) -> torch.Tensor:
+def linear_swiglu(x: torch.Tensor, w: torch.Tensor, block: int,
+                  out: torch.Tensor | None = None) -> torch.Tensor:
     """silu(gate) * up of x @ w^T for gate|up weights interleaved per
     ``block`` channels: the fused-epilogue decode GEMM where the table picks
     it, K13 with its SwiGLU epilogue for prefill-sized M (block 16), else the
     library GEMM + the GLU kernel.  block 16: the in-register
     epilogue over 16-column gate/up pairs (epi 3, any tile width); otherwise
     the LDS hand-off form (epi 1, tile BN = 2 * block)."""
+    if x.is_cuda and x.dim() == 2 and (piece := rows_split(x.shape[0], w.shape[0])):
+        return _by_rows(x, piece, w.shape[0] // 2, lambda xs, o: linear_swiglu(xs, w, block, out=o))
     if is_packed_only(w):
         _chk(block == SWIGLU16 and x.is_cuda and x.dim() == 2,
              "packed-only gate/up: the SwiGLU16 interleave on CUDA")
-        return _packed_product(x, w, 3)
+        return _packed_product(x, w, 3, out=out)
     if x.is_cuda and x.dim() == 2:
         if block == SWIGLU16:
             rc = rs_choice(x.shape[0], w.shape[0], w.shape[1], epi=3, w=w)
             if rc is not None and rsgemm_operands_ok(x, w):
-                return rsgemm(x, w, rc[0], rc[1], epi=3)     # K14, SwiGLU epilogue
+                return rsgemm(x, w, rc[0], rc[1], epi=3, out=out)     # K14, SwiGLU epilogue
             s = sk_choice(x.shape[0], w.shape[0], w.shape[1], epi=3)
             if s is not None and pgemm_operands_ok(x, w):
-                return pgemm_sk(x, w, s, act=ACT_SWIGLU)   # K13-SK, SwiGLU epilogue
+                return pgemm_sk(x, w, s, act=ACT_SWIGLU, out=out)   # K13-SK, SwiGLU epilogue
             ch = dgemm_choice(x.shape[0], w.shape[0], w.shape[1], epi=3)
             if ch is not None:
-                return dgemm(x, w, ch[0], ch[1], epi=3)
+                return dgemm(x, w, ch[0], ch[1], epi=3, out=out)
             if (large_gemm_backend(x.shape[0], w.shape[0], w.shape[1], ACT_SWIGLU) == "k13"
                     and pgemm_operands_ok(x, w)):
-                return pgemm(x, w, act=ACT_SWIGLU)     # K13 with the SwiGLU epilogue
+                return pgemm(x, w, act=ACT_SWIGLU, out=out)     # K13 with the SwiGLU epilogue
         else:
             ch = dgemm_choice(x.shape[0], w.shape[0], w.shape[1], epi=1)
             if ch is not None and DGEMM_CONFIGS[ch[0] & DGEMM_CFG_MASK][1] == 2 * block:
-                return dgemm(x, w, ch[0], ch[1], epi=1)
-    return silu_mul(linear(x, w), block=block)
+                return dgemm(x, w, ch[0], ch[1], epi=1, out=out)
+    return _into(out, silu_mul(linear(x, w), block=block))
 
 
 def swiglu_block(N: int, K: int) -> int:
@@ -1271,7 +1312,8 @@ def rs_default(M: int, N: int, K: int, epi: int) -> tuple[int, int] | None:
     return cfg, ok[-1]
 
 
-def _packed_product(x: torch.Tensor, w: torch.Tensor, epi: int) -> torch.Tensor | Partials:
+def _packed_product(x: torch.Tensor, w: torch.Tensor, epi: int,
+                    out: torch.Tensor | None = None) -> torch.Tensor | Partials:
     """x @ w^T for a packed-only ``w``: K14 at decode batch sizes (epi 0 / 2
     partials / 3 SwiGLU16), K13 with packed W above 256 rows."""
     M, N, K = x.shape[0], w.shape[0], w.shape[1]
@@ -1279,10 +1321,10 @@ def _packed_product(x: torch.Tensor, w: torch.Tensor, epi: int) -> torch.Tensor 
         rc = rs_choice(M, N, K, epi=epi, w=w) or rs_default(M, N, K, epi)
         _chk(rc is not None and rsgemm_operands_ok(x, w),
              f"packed-only weight {tuple(w.shape)}: no K14 form for M={M} epi={epi}")
-        return rsgemm(x, w, rc[0], rc[1], epi=epi)
+        return rsgemm(x, w, rc[0], rc[1], epi=epi, out=out)
     if not x.is_contiguous():
         x = x.contiguous()
-    return pgemm(x, w, act=ACT_SWIGLU if epi == 3 else ACT_NONE, packed=True)
+    return pgemm(x, w, act=ACT_SWIGLU if epi == 3 else ACT_NONE, packed=True, out=out)
 
 
 def _rs_wants_packed(w: torch.Tensor) -> bool:
@@ -1577,6 +1619,8 @@ def residual_gemm_ok(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor | 
     M, N, K = x.shape[0], w.shape[0], w.shape[1]
     if residual.shape != (M, N) or not residual_gemm_layout_ok(residual):
         return False
+    if rows_split(M, N):
+        return False          # row pieces on the decode kernels (linear), not one K13 product
     if is_packed_only(w):
         return M > 256 and pgemm_operands_ok(x, w)
     if (rs_choice(M, N, K, epi=2, w=w) is not None or rs_choice(M, N, K, w=w) is not None

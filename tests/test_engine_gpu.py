@@ -267,6 +267,47 @@ def test_llama3_8b_shapes_k13_prefill_and_sk_lm_head(graphs):
         assert_greedy_consistent(e.model, p, o, tol=0.08)
 
 
+@pytest.mark.parametrize("M", [300, 512, 640])
+def test_rows_split_products_match_dense(M):
+    """257-1024-row products on the narrow Llama-3-8B projections (QKV, O,
+    down; fewer than 128 K13 tiles) run as equal <= 256-row pieces on the
+    decode kernels (ops.rows_split): same values as the fp32 product."""
+    ops.native()
+    torch.manual_seed(M)
+    for N, K in ((6144, 4096), (4096, 4096), (4096, 14336)):
+        assert ops.rows_split(M, N)
+        x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+        w = (torch.randn(N, K, device="cuda") * K ** -0.5).to(torch.bfloat16)
+        ops.rs_prepare(w)
+        want = x.float() @ w.float().t()
+        torch.testing.assert_close(ops.linear(x, w).float(), want, atol=3e-2, rtol=3e-2)
+        d = ops.linear(x, w, defer=True)
+        d = d.sum() if isinstance(d, ops.Partials) else d
+        torch.testing.assert_close(d.float(), want, atol=3e-2, rtol=3e-2)
+
+
+def test_llama3_8b_400_stream_decode_in_row_pieces():
+    """Two layers of Llama-3-8B with 400 streams: the decode steps (graph
+    bucket above 256 rows) run QKV / O / down as 256-row-or-smaller pieces on the
+    decode kernels instead of a CU-starved K13 product; greedy tokens stay
+    (near-)argmax of the dense fp32 forward."""
+    import dataclasses
+
+    from llm_mcp_amd.models import config as mc
+    ops.native()
+    cfg = dataclasses.replace(mc.resolve("llama-3-8b"), num_layers=2)
+    d0, r0 = ops.DGEMM_CALLS[0], ops.RSGEMM_CALLS[0]      # decode graphs capture at load
+    e = LLMEngine(EngineConfig(model="llama-3-8b", max_num_seqs=512, max_batched_tokens=2048,
+                               max_model_len=256, use_graphs=True, kv_cache_gb=2),
+                  device="cuda", model_cfg=cfg)
+    prompts = [[(11 * i + 3 * j) % 120000 + 100 for j in range(4)] for i in range(400)]
+    outs = e.generate(prompts, SamplingParams(temperature=0, max_tokens=3, ignore_eos=True))
+    assert ops.DGEMM_CALLS[0] + ops.RSGEMM_CALLS[0] > d0 + r0
+    assert e.stats["graph_steps"] > 0
+    for p, o in list(zip(prompts, outs))[::61]:
+        assert_greedy_consistent(e.model, p, o, tol=0.08)
+
+
 def test_lookahead_graph_steps_match_synchronous(monkeypatch):
     """Lookahead stepping on the captured decode graphs (input tokens gathered
     on the device by ops.ids_from_prev from the previous step's samples) gives

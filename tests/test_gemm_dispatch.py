@@ -150,3 +150,21 @@ def test_rs_prepare_all_packs_whole_shapes_or_none(monkeypatch):
     assert all(ops._rs_packed_of(w) is not None for w in small + other)
     assert all(ops._rs_packed_of(w) is None for w in big)          # 8 MiB: none of them
     assert ops._RS_PACKED_BYTES[0] == 4 * mib
+
+
+def test_rows_split_for_cu_starved_decode_batches():
+    """256 < M <= 1024 rows on a narrow projection (fewer than 128 K13 tiles)
+    runs as equal <= 256-row pieces on the decode kernels; wide products (gate/
+    up, LM head) and prefill-sized batches stay one product."""
+    import torch
+    assert ops.rows_split(256, 4096) == 0                 # the decode kernels' own range
+    assert ops.rows_split(512, 4096) == 256
+    assert ops.rows_split(300, 6144) == 150               # two equal pieces, not 256 + 44
+    assert ops.rows_split(640, 4096) == 214
+    assert ops.rows_split(512, 28672) == 0                # 224 tiles: K13 fills the chip
+    assert ops.rows_split(1024, 8192) == 0                # 128 tiles
+    assert ops.rows_split(1100, 4096) == 0                # prefill-sized
+    x = torch.randn(300, 64)
+    w = torch.randn(32, 64)
+    y = ops._by_rows(x, ops.rows_split(300, 4096), 32, lambda xs, o: torch.mm(xs, w.t(), out=o))
+    torch.testing.assert_close(y, x @ w.t())

@@ -227,6 +227,8 @@ for step in "$@"; do
     closed_default)
       run closed_default 600 python bench.py --load closed --duration 30 --closed-warmup 10 \
           || exit $? ;;
+    conc512)
+      run conc512 600 python bench.py --steps 2 --warmup 1 --concurrency 512 || exit $? ;;
     closed64)
       run closed64 600 python bench.py --load closed --duration 30 --closed-warmup 10 \
           --concurrency 64 || exit $? ;;
@@ -538,6 +540,10 @@ for step in "$@"; do
         run dg_$m 1000 python -u -m llm_mcp_amd.bench.dgemm_bench --model $m --tp ${DG_TP:-1} \
             --json gpurun_out/dg_$m.json || exit $?
       done ;;
+    split_tests)
+      run split_tests 600 python -u -m pytest tests/test_engine_gpu.py tests/test_norm_fold_gpu.py \
+          -k "rows_split or row_pieces or norm" -x -v --timeout 300 --timeout-method thread \
+          -p no:cacheprovider || exit $? ;;
     fam_tests)
       run fam_tests 600 python -u -m pytest tests/test_engine_gpu.py -k "family or llama3_8b" -x -v \
           --timeout 300 --timeout-method thread -p no:cacheprovider || exit $? ;;
