@@ -521,7 +521,7 @@ class LlamaModel:
         shapes = ((L["wqkv"], ops.ACT_NONE), (L["wo"], ops.ACT_NONE),
                   (L["w_gate_up"], ops.ACT_SWIGLU), (L["w_down"], ops.ACT_NONE))
         if torch.device(self.device).type == "cuda" and any(
-                ops.rows_split(T, w.shape[0]) for w, _ in shapes):
+                ops.rows_split(T, w.shape[0], w.shape[1], 3 if act else 0, w) for w, act in shapes):
             return False      # a decode-sized step split into <= 256-row pieces
         return d % 64 == 0 and all(
             ops.large_gemm_backend(T, w.shape[0], w.shape[1], act) == "k13"

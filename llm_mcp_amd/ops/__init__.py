@@ -718,14 +718,22 @@ ROWS_SPLIT_MAX = 1024      # largest batch split this way
 ROWS_SPLIT_TILES = 128     # K13 tiles below which the product is split
 
 
-def rows_split(M: int, N: int) -> int:
+def rows_split(M: int, N: int, K: int | None = None, epi: int = 0,
+               w: torch.Tensor | None = None) -> int:
     """Row-piece size for an M-row product with N output columns, or 0 (one
-    product): 256 < M <= ROWS_SPLIT_MAX and fewer than ROWS_SPLIT_TILES
-    256 x 256 tiles."""
+    product): 256 < M <= ROWS_SPLIT_MAX, fewer than ROWS_SPLIT_TILES 256 x 256
+    tiles and (given K) a measured decode kernel for the pieces -- a packed-only
+    weight, or a K14 / K13-SK / K11 table entry (shapes without one, e.g. the
+    encoders' 768-wide projections, stay one product)."""
     if not (DGEMM_MAX_M < M <= ROWS_SPLIT_MAX) or -(-M // 256) * (N // 256) >= ROWS_SPLIT_TILES:
         return 0
     n = -(-M // DGEMM_MAX_M)
-    return -(-M // n)
+    piece = -(-M // n)
+    if K is not None and not (
+            (w is not None and is_packed_only(w)) or rs_choice(piece, N, K, epi, w=w) is not None
+            or sk_choice(piece, N, K, epi) is not None or dgemm_choice(piece, N, K, epi) is not None):
+        return 0
+    return piece
 
 
 def _by_rows(x: torch.Tensor, piece: int, ncols: int, fn) -> torch.Tensor:
@@ -753,7 +761,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, defer: bool = False,
     (epi 2) may return ``Partials`` and leave the K reduction to the norm.
     ``out``: a bf16 [M, N] destination (plain products only, not with defer)."""
     _chk(out is None or not defer, "linear: out= is for the plain product")
-    if x.is_cuda and x.dim() == 2 and (piece := rows_split(x.shape[0], w.shape[0])):
+    if x.is_cuda and x.dim() == 2 and (piece := rows_split(x.shape[0], w.shape[0], w.shape[1], 0, w)):
         return _by_rows(x, piece, w.shape[0], lambda xs, o: linear(xs, w, bias=bias, out=o))
     if is_packed_only(w):
         _chk(bias is None and x.is_cuda and x.dim() == 2, "packed-only weight: plain CUDA product")
@@ -798,7 +806,8 @@ def linear_swiglu(x: torch.Tensor, w: torch.Tensor, block: int,
     library GEMM + the GLU kernel.  block 16: the in-register
     epilogue over 16-column gate/up pairs (epi 3, any tile width); otherwise
     the LDS hand-off form (epi 1, tile BN = 2 * block)."""
-    if x.is_cuda and x.dim() == 2 and (piece := rows_split(x.shape[0], w.shape[0])):
+    if x.is_cuda and x.dim() == 2 and (piece := rows_split(
+            x.shape[0], w.shape[0], w.shape[1], 3 if block == SWIGLU16 else 1, w)):
         return _by_rows(x, piece, w.shape[0] // 2, lambda xs, o: linear_swiglu(xs, w, block, out=o))
     if is_packed_only(w):
         _chk(block == SWIGLU16 and x.is_cuda and x.dim() == 2,
@@ -1619,7 +1628,7 @@ def residual_gemm_ok(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor | 
     M, N, K = x.shape[0], w.shape[0], w.shape[1]
     if residual.shape != (M, N) or not residual_gemm_layout_ok(residual):
         return False
-    if rows_split(M, N):
+    if rows_split(M, N, K, 0, w):
         return False          # row pieces on the decode kernels (linear), not one K13 product
     if is_packed_only(w):
         return M > 256 and pgemm_operands_ok(x, w)

@@ -164,6 +164,9 @@ def test_rows_split_for_cu_starved_decode_batches():
     assert ops.rows_split(512, 28672) == 0                # 224 tiles: K13 fills the chip
     assert ops.rows_split(1024, 8192) == 0                # 128 tiles
     assert ops.rows_split(1100, 4096) == 0                # prefill-sized
+    # given K: only where the pieces have a measured decode kernel
+    assert ops.rows_split(512, 4096, 14336) == 256        # Llama-3-8B down
+    assert ops.rows_split(1000, 768, 768) == 0            # encoder projection: no table entry
     x = torch.randn(300, 64)
     w = torch.randn(32, 64)
     y = ops._by_rows(x, ops.rows_split(300, 4096), 32, lambda xs, o: torch.mm(xs, w.t(), out=o))

@@ -765,7 +765,7 @@ def test_linear_large_m_runs_k13(monkeypatch):
     K13 (LMX_LARGE_GEMM=k13), bias and the 16-row gate/up SwiGLU included,
     and match the library / GLU-kernel path."""
     monkeypatch.setenv("LMX_LARGE_GEMM", "k13")
-    M, K, N = 700, 1024, 2048
+    M, K, N = 1100, 1024, 2048          # above ops.ROWS_SPLIT_MAX: one K13 product
     x = _bf(M, K)
     w = _bf(N, K, scale=K ** -0.5)
     b = _bf(N)
