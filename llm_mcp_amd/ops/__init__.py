@@ -714,7 +714,7 @@ def splitk_preferred(M: int, N: int, K: int) -> bool:
 # tiles for O / down at d = 4096: 237 us for the down projection, 6x its
 # 256-row K14 time), so such a product runs as equal row pieces of <= 256 rows
 # on the decode kernels instead (profiles/r6_serving.md "512 streams")
-ROWS_SPLIT_MAX = 1024      # largest batch split this way
+ROWS_SPLIT_MAX = int(os.environ.get("LMX_ROWS_SPLIT_MAX", "1024"))   # largest batch split this way
 ROWS_SPLIT_TILES = 128     # K13 tiles below which the product is split
 
 

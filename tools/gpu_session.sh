@@ -229,6 +229,12 @@ for step in "$@"; do
           || exit $? ;;
     conc512)
       run conc512 600 python bench.py --steps 2 --warmup 1 --concurrency 512 || exit $? ;;
+    conc512_ab)
+      # 512 streams, same box: one K13 product (LMX_ROWS_SPLIT_MAX=0) vs decode-kernel row pieces
+      for i in 1 2; do
+        LMX_ROWS_SPLIT_MAX=0 run conc512_off_$i 600 python bench.py --steps 2 --warmup 1 --concurrency 512 || exit $?
+        run conc512_on_$i 600 python bench.py --steps 2 --warmup 1 --concurrency 512 || exit $?
+      done ;;
     closed64)
       run closed64 600 python bench.py --load closed --duration 30 --closed-warmup 10 \
           --concurrency 64 || exit $? ;;
