@@ -229,6 +229,9 @@ for step in "$@"; do
           || exit $? ;;
     conc512)
       run conc512 600 python bench.py --steps 2 --warmup 1 --concurrency 512 || exit $? ;;
+    down_norm)
+      run down_norm 180 python -u tools/down_norm_probe.py || exit $?
+      run down_norm_o 180 python -u tools/down_norm_probe.py --k 4096 || exit $? ;;
     conc512_ab)
       # 512 streams, same box: one K13 product (LMX_ROWS_SPLIT_MAX=0) vs decode-kernel row pieces
       for i in 1 2; do
