@@ -722,18 +722,16 @@ def rows_split(M: int, N: int, K: int | None = None, epi: int = 0,
                w: torch.Tensor | None = None) -> int:
     """Row-piece size for an M-row product with N output columns, or 0 (one
     product): 256 < M <= ROWS_SPLIT_MAX, fewer than ROWS_SPLIT_TILES 256 x 256
-    tiles and (given K) a measured decode kernel for the pieces -- a packed-only
-    weight, or a K14 / K13-SK / K11 table entry (shapes without one, e.g. the
-    encoders' 768-wide projections, stay one product)."""
+    tiles and (given K) a packed-only weight, whose only other form is K13 with
+    packed W (K14 then serves the pieces).  A row-major weight takes hipBLASLt
+    there instead (``large_gemm_backend``: 1.1-1.9x faster than these pieces,
+    profiles/r6_lab/rows_split_probe.log)."""
     if not (DGEMM_MAX_M < M <= ROWS_SPLIT_MAX) or -(-M // 256) * (N // 256) >= ROWS_SPLIT_TILES:
         return 0
-    n = -(-M // DGEMM_MAX_M)
-    piece = -(-M // n)
-    if K is not None and not (
-            (w is not None and is_packed_only(w)) or rs_choice(piece, N, K, epi, w=w) is not None
-            or sk_choice(piece, N, K, epi) is not None or dgemm_choice(piece, N, K, epi) is not None):
+    if K is not None and not (w is not None and is_packed_only(w)):
         return 0
-    return piece
+    n = -(-M // DGEMM_MAX_M)
+    return -(-M // n)
 
 
 def _by_rows(x: torch.Tensor, piece: int, ncols: int, fn) -> torch.Tensor:
@@ -974,6 +972,23 @@ def encoder_backend(N: int, K: int, act: int = 0,
 
 PGEMM_MIN_M = 512          # below: the decode-sized paths (K11 / split-K / library)
 PGEMM_LIB_MARGIN = 0.05    # "auto": hipBLASLt only where measured > 5 % faster than K13
+# K13 is persistent over 256 x 256 tiles on the 256 CUs, so a product of fewer
+# tiles than about 1.5 waves takes a whole wave's time: at 512-1536 rows the
+# narrow Llama-3-8B projections ran 1.1-2.6x slower on K13 than on hipBLASLt
+# (QKV / O flat at ~72 / ~67 us from 512 to 1536 rows; tools/rows_split_probe.py,
+# profiles/r6_lab/rows_split_probe.log).  Below this fraction of its last
+# tile wave filled (first two waves only) the product goes to the library.
+PGEMM_NUM_CUS = 256
+PGEMM_MIN_FILL = float(os.environ.get("LMX_K13_MIN_FILL", "0.6"))
+
+
+def k13_wave_fill(M: int, N: int) -> float:
+    """Fraction of K13's last 256-CU tile wave an M x N product fills (1.0
+    from two waves of tiles on: the rule only governs the first two)."""
+    t = -(-M // 256) * -(-N // 256)
+    if t >= 2 * PGEMM_NUM_CUS:
+        return 1.0
+    return t / (PGEMM_NUM_CUS * -(-t // PGEMM_NUM_CUS))
 
 
 def large_gemm_backend(M: int, N: int, K: int, act: int = 0, bias: bool = False) -> str:
@@ -992,6 +1007,8 @@ def large_gemm_backend(M: int, N: int, K: int, act: int = 0, bias: bool = False)
     mode = os.environ.get("LMX_LARGE_GEMM", "auto")
     if mode in ("k13", "lib"):
         return mode
+    if k13_wave_fill(M, N) < PGEMM_MIN_FILL:
+        return "lib"
     e = _enc_table().get((N, K))
     if e is None:
         return "k13"

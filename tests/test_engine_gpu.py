@@ -270,8 +270,9 @@ def test_llama3_8b_shapes_k13_prefill_and_sk_lm_head(graphs):
 @pytest.mark.parametrize("M", [300, 512, 640])
 def test_rows_split_products_match_dense(M):
     """257-1024-row products on the narrow Llama-3-8B projections (QKV, O,
-    down; fewer than 128 K13 tiles) run as equal <= 256-row pieces on the
-    decode kernels (ops.rows_split): same values as the fp32 product."""
+    down; fewer than 128 K13 tiles): a row-major weight takes the library
+    (K13's tile wave would be mostly empty), a packed-only one equal <= 256-row
+    pieces on K14 (ops.rows_split); both give the fp32 product."""
     ops.native()
     torch.manual_seed(M)
     for N, K in ((6144, 4096), (4096, 4096), (4096, 14336)):
@@ -279,18 +280,26 @@ def test_rows_split_products_match_dense(M):
         x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
         w = (torch.randn(N, K, device="cuda") * K ** -0.5).to(torch.bfloat16)
         ops.rs_prepare(w)
+        assert not ops.rows_split(M, N, K, 0, w)
         want = x.float() @ w.float().t()
-        torch.testing.assert_close(ops.linear(x, w).float(), want, atol=3e-2, rtol=3e-2)
-        d = ops.linear(x, w, defer=True)
-        d = d.sum() if isinstance(d, ops.Partials) else d
-        torch.testing.assert_close(d.float(), want, atol=3e-2, rtol=3e-2)
+        forms = [w]
+        if ops.rs_single_ok(w):
+            wp = ops.rs_pack_only(w.clone())
+            assert ops.rows_split(M, N, K, 0, wp)
+            forms.append(wp)
+        for ww in forms:
+            torch.testing.assert_close(ops.linear(x, ww).float(), want, atol=3e-2, rtol=3e-2)
+            d = ops.linear(x, ww, defer=True)
+            d = d.sum() if isinstance(d, ops.Partials) else d
+            torch.testing.assert_close(d.float(), want, atol=3e-2, rtol=3e-2)
 
 
 def test_llama3_8b_400_stream_decode_in_row_pieces():
     """Two layers of Llama-3-8B with 400 streams: the decode steps (graph
-    bucket above 256 rows) run QKV / O / down as 256-row-or-smaller pieces on the
-    decode kernels instead of a CU-starved K13 product; greedy tokens stay
-    (near-)argmax of the dense fp32 forward."""
+    bucket above 256 rows) run QKV / O / down off K13, whose tile waves would
+    be mostly empty (library for row-major weights, <= 256-row K14 pieces for
+    packed-only ones), in captured graphs; greedy tokens stay (near-)argmax of
+    the dense fp32 forward."""
     import dataclasses
 
     from llm_mcp_amd.models import config as mc

@@ -152,10 +152,12 @@ def test_rs_prepare_all_packs_whole_shapes_or_none(monkeypatch):
     assert ops._RS_PACKED_BYTES[0] == 4 * mib
 
 
-def test_rows_split_for_cu_starved_decode_batches():
+def test_rows_split_for_cu_starved_decode_batches(monkeypatch):
     """256 < M <= 1024 rows on a narrow projection (fewer than 128 K13 tiles)
-    runs as equal <= 256-row pieces on the decode kernels; wide products (gate/
-    up, LM head) and prefill-sized batches stay one product."""
+    of a packed-only weight runs as equal <= 256-row pieces on K14; wide
+    products (gate/up, LM head) and prefill-sized batches stay one product.
+    A row-major weight there takes the library: K13's tile waves would be
+    mostly empty (k13_wave_fill)."""
     import torch
     assert ops.rows_split(256, 4096) == 0                 # the decode kernels' own range
     assert ops.rows_split(512, 4096) == 256
@@ -164,10 +166,24 @@ def test_rows_split_for_cu_starved_decode_batches():
     assert ops.rows_split(512, 28672) == 0                # 224 tiles: K13 fills the chip
     assert ops.rows_split(1024, 8192) == 0                # 128 tiles
     assert ops.rows_split(1100, 4096) == 0                # prefill-sized
-    # given K: only where the pieces have a measured decode kernel
-    assert ops.rows_split(512, 4096, 14336) == 256        # Llama-3-8B down
-    assert ops.rows_split(1000, 768, 768) == 0            # encoder projection: no table entry
+    # given K: only for a packed-only weight (a row-major one takes the library)
+    assert ops.rows_split(512, 4096, 14336) == 0
+    assert ops.rows_split(512, 4096, 14336, 0, torch.empty(0)) == 0
     x = torch.randn(300, 64)
     w = torch.randn(32, 64)
     y = ops._by_rows(x, ops.rows_split(300, 4096), 32, lambda xs, o: torch.mm(xs, w.t(), out=o))
     torch.testing.assert_close(y, x @ w.t())
+    assert ops.k13_wave_fill(512, 4096) == 32 / 256
+    assert ops.k13_wave_fill(512, 28672) == 224 / 256
+    assert ops.k13_wave_fill(768, 28672) == 336 / 512
+    assert ops.k13_wave_fill(36864, 4096) == 1.0
+    monkeypatch.delenv("LMX_LARGE_GEMM", raising=False)
+    monkeypatch.setattr(ops, "_ENC_TABLE", {})
+    assert ops.large_gemm_backend(512, 4096, 14336) == "lib"       # 32 tiles
+    assert ops.large_gemm_backend(1536, 6144, 4096) == "lib"       # 144 of 256
+    assert ops.large_gemm_backend(2304, 6144, 4096) == "k13"       # 216 of 256
+    assert ops.large_gemm_backend(512, 28672, 4096, ops.ACT_SWIGLU) == "k13"
+    assert ops.large_gemm_backend(36864, 4096, 14336) == "k13"
+    monkeypatch.setenv("LMX_LARGE_GEMM", "k13")
+    assert ops.large_gemm_backend(512, 4096, 14336) == "k13"
+

@@ -64,7 +64,8 @@ def test_row_scaled_products(M, packed):
 
 
 def test_llama_prefill_folded_norm_matches_norm_pass(monkeypatch):
-    """A 2-layer Llama-3-8B prefill step of 1,100 tokens: the folded path
+    """A 2-layer Llama-3-8B prefill step of 2,400 tokens (every projection
+    fills >= 60 % of K13's tile wave, so all four run on K13): the folded path
     (no norm pass) against the same weights run with the norm kernels."""
     from llm_mcp_amd.models import config as mc
     from llm_mcp_amd.models.llama import LlamaModel
@@ -73,7 +74,7 @@ def test_llama_prefill_folded_norm_matches_norm_pass(monkeypatch):
     cfg = dataclasses.replace(mc.resolve("llama-3-8b"), num_layers=2)
     m = LlamaModel(cfg, DEV, seed=1)
     assert m.norm_folded
-    lens = [600, 300, 200]
+    lens = [1400, 700, 300]
     inp, kc, vc = _prefill_inputs(cfg, lens)
     to = lambda t: t.to(DEV) if isinstance(t, torch.Tensor) else t  # noqa: E731
     inp = dataclasses.replace(inp, **{f.name: to(getattr(inp, f.name))

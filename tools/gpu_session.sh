@@ -232,10 +232,13 @@ for step in "$@"; do
     down_norm)
       run down_norm 180 python -u tools/down_norm_probe.py || exit $?
       run down_norm_o 180 python -u tools/down_norm_probe.py --k 4096 || exit $? ;;
+    rows_split_probe)
+      run rows_split_probe 300 python -u tools/rows_split_probe.py || exit $? ;;
     conc512_ab)
-      # 512 streams, same box: one K13 product (LMX_ROWS_SPLIT_MAX=0) vs decode-kernel row pieces
+      # 512 streams, same box: K13 on every >= 512-row product (the old rule) vs the default
+      # (hipBLASLt below 60 % K13 wave fill, K14 row pieces for packed-only weights)
       for i in 1 2; do
-        LMX_ROWS_SPLIT_MAX=0 run conc512_off_$i 600 python bench.py --steps 2 --warmup 1 --concurrency 512 || exit $?
+        LMX_K13_MIN_FILL=0 LMX_ROWS_SPLIT_MAX=0 run conc512_off_$i 600 python bench.py --steps 2 --warmup 1 --concurrency 512 || exit $?
         run conc512_on_$i 600 python bench.py --steps 2 --warmup 1 --concurrency 512 || exit $?
       done ;;
     closed64)
