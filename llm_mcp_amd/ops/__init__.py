@@ -977,7 +977,10 @@ PGEMM_LIB_MARGIN = 0.05    # "auto": hipBLASLt only where measured > 5 % faster 
 # narrow Llama-3-8B projections ran 1.1-2.6x slower on K13 than on hipBLASLt
 # (QKV / O flat at ~72 / ~67 us from 512 to 1536 rows; tools/rows_split_probe.py,
 # profiles/r6_lab/rows_split_probe.log).  Below this fraction of its last
-# tile wave filled (first two waves only) the product goes to the library.
+# tile wave filled (first two waves only) a decode-sized product (<=
+# ROWS_SPLIT_MAX rows, the captured decode-graph buckets) goes to the library;
+# eager prefill / mixed steps of arbitrary row counts keep K13 (no per-shape
+# library heuristics on the step path).
 PGEMM_NUM_CUS = 256
 PGEMM_MIN_FILL = float(os.environ.get("LMX_K13_MIN_FILL", "0.6"))
 
@@ -1007,8 +1010,8 @@ def large_gemm_backend(M: int, N: int, K: int, act: int = 0, bias: bool = False)
     mode = os.environ.get("LMX_LARGE_GEMM", "auto")
     if mode in ("k13", "lib"):
         return mode
-    if k13_wave_fill(M, N) < PGEMM_MIN_FILL:
-        return "lib"
+    if M <= ROWS_SPLIT_MAX and k13_wave_fill(M, N) < PGEMM_MIN_FILL:
+        return "lib"          # decode-sized batches only: prefill / mixed steps keep K13
     e = _enc_table().get((N, K))
     if e is None:
         return "k13"

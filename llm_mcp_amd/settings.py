@@ -119,7 +119,7 @@ VARS: list[Var] = [
     Var("LMX_RESIDUAL_EPILOGUE", int, 1, "prefill O / down projections on K13 add into the residual stream in their epilogue (0: separate residual-add pass in the norm)"),
     Var("LMX_NORM_FOLD", str, "1", "TP = 1: fold the RMSNorm gains into QKV / gate-up at load; prefill steps on K13 then run no norm pass (row scales from the residual epilogue's sums of squares); 0 keeps the norm kernels"),
     Var("LMX_RS_SINGLE", str, "auto", "one copy of the MLP weights: gate/up and down stored only in K14's packed layout (K14 decode, K13 prefill with packed W) when the table runs them packed; auto = only when the weights take > 25 % of the GPU's memory (a small model keeps its row-major copy for K11 below 129 rows), 1 always, 0 never"),
-    Var("LMX_K13_MIN_FILL", float, 0.6, "large-M projections: below this fraction of K13's last 256-CU tile wave filled (first two waves) the product runs on hipBLASLt (0: K13 whenever the encoder table allows)"),
+    Var("LMX_K13_MIN_FILL", float, 0.6, "decode-sized projections (512..LMX_ROWS_SPLIT_MAX rows): below this fraction of K13's last 256-CU tile wave filled the product runs on hipBLASLt (0: K13 whenever the encoder table allows)"),
     Var("LMX_ROWS_SPLIT_MAX", int, 1024, "decode batches of 257..N rows: a projection with fewer than 128 K13 tiles runs as <= 256-row pieces on the decode kernels (0 disables: one K13 / library product)"),
     Var("LMX_RS_PACK_GB", float, 24.0, "budget for K14's packed copies of decode weights that are not stored packed-only (beside the row-major weights prefill reads)"),
     Var("LMX_RS", str, "1", "0 disables the K14 (register-streamed weights, csrc/kernels/rsgemm.hip) entries of the decode GEMM table"),

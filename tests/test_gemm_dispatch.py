@@ -180,7 +180,8 @@ def test_rows_split_for_cu_starved_decode_batches(monkeypatch):
     monkeypatch.delenv("LMX_LARGE_GEMM", raising=False)
     monkeypatch.setattr(ops, "_ENC_TABLE", {})
     assert ops.large_gemm_backend(512, 4096, 14336) == "lib"       # 32 tiles
-    assert ops.large_gemm_backend(1536, 6144, 4096) == "lib"       # 144 of 256
+    assert ops.large_gemm_backend(1024, 6144, 4096) == "lib"       # 96 of 256
+    assert ops.large_gemm_backend(1536, 6144, 4096) == "k13"       # above ROWS_SPLIT_MAX
     assert ops.large_gemm_backend(2304, 6144, 4096) == "k13"       # 216 of 256
     assert ops.large_gemm_backend(512, 28672, 4096, ops.ACT_SWIGLU) == "k13"
     assert ops.large_gemm_backend(36864, 4096, 14336) == "k13"

@@ -234,6 +234,12 @@ for step in "$@"; do
       run down_norm_o 180 python -u tools/down_norm_probe.py --k 4096 || exit $? ;;
     rows_split_probe)
       run rows_split_probe 300 python -u tools/rows_split_probe.py || exit $? ;;
+    fill_ab)
+      # the headline load, same box: the old K13 rule vs the wave-fill rule (default)
+      for i in 1 2; do
+        LMX_K13_MIN_FILL=0 LMX_ROWS_SPLIT_MAX=0 run fill_off_$i 600 python bench.py --steps 6 --warmup 2 || exit $?
+        run fill_on_$i 600 python bench.py --steps 6 --warmup 2 || exit $?
+      done ;;
     conc512_ab)
       # 512 streams, same box: K13 on every >= 512-row product (the old rule) vs the default
       # (hipBLASLt below 60 % K13 wave fill, K14 row pieces for packed-only weights)
